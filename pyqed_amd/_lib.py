@@ -1,0 +1,102 @@
+"""ctypes binding of libqdyn.so (the C-ABI declared in include/qdyn.h).
+
+The product path has exactly one compute backend: the HIP kernels in this
+library.  There is no CPU fallback — if the library is missing or a call fails,
+a RuntimeError/ValueError is raised.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("QDYN_LIB", os.path.join(_HERE, "libqdyn.so"))
+
+QD_OK = 0
+QD_EINVAL = -1
+QD_EHIP = -2
+QD_ERCCL = -3
+QD_ENOMEM = -4
+
+c_int = ctypes.c_int
+c_double = ctypes.c_double
+c_size_t = ctypes.c_size_t
+c_void_p = ctypes.c_void_p
+c_char_p = ctypes.c_char_p
+
+# name -> (restype, argtypes); must list every symbol of include/qdyn.h
+SIGNATURES = {
+    "qd_version": (c_int, []),
+    "qd_last_error": (c_char_p, []),
+    "qd_init": (c_int, [c_int]),
+    "qd_device_count": (c_int, [ctypes.POINTER(c_int)]),
+    "qd_shutdown": (c_int, []),
+    "qd_synchronize": (c_int, [c_void_p]),
+    "qd_lindblad_rk4": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_double, c_int,
+                                c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
+}
+
+_lib = None
+_lock = threading.Lock()
+_inited_devices: set[int] = set()
+
+
+def load() -> ctypes.CDLL:
+    """Load libqdyn.so (idempotent).  Raises RuntimeError if it is absent."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"libqdyn.so not found at {LIB_PATH}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (make -C pyqed_amd/csrc)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def last_error() -> str:
+    msg = load().qd_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, what: str) -> None:
+    if rc == QD_OK:
+        return
+    msg = last_error()
+    if rc == QD_EINVAL:
+        raise ValueError(f"{what}: {msg}")
+    raise RuntimeError(f"{what} failed (code {rc}): {msg}")
+
+
+def ensure_device(device: torch.device) -> None:
+    """qd_init once per device (checks the gfx950 target)."""
+    if device.type != "cuda":
+        raise RuntimeError(f"pyqed_amd computes on the GPU only; got device {device}")
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx in _inited_devices:
+        return
+    lib = load()
+    with torch.cuda.device(idx):
+        check(lib.qd_init(idx), "qd_init")
+    _inited_devices.add(idx)
+
+
+def stream_ptr(device: torch.device | None = None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    if t is None:
+        return None
+    if not t.is_contiguous():
+        raise ValueError("pyqed_amd: tensor must be contiguous")
+    return t.data_ptr()

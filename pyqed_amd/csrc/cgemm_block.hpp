@@ -1,0 +1,167 @@
+// cgemm_block.hpp — workgroup-level complex-fp64 GEMM engine on
+// v_mfma_f64_16x16x4_f64 (gfx950), used by the density-matrix kernels.
+//
+// One 512-thread workgroup (8 waves, 2 per SIMD) computes a BT x BT complex
+// output block as a sum of "segments"  sum_s A_s[BT x K] * B_s[K x BT],
+// with A_s, B_s row-major complex128 in global memory (L2/MALL resident).
+//
+// Data path per K-tile of 16 complex columns:
+//   global --(16-B coalesced loads, register prefetch of tile t+1)--> LDS
+//   (A tile row stride 18 complex: conflict-free ds_write_b128 staging and
+//    ds_read_b128 fragment reads; B tile stride BT: natural and conflict-free)
+//   LDS --(one complex = one ds_read_b128 per lane)--> MFMA fragments.
+// A complex 16x16x4 MAC is 4 real f64 MFMAs:
+//   Cr += Ar*Br ; Cr += (-Ai)*Bi ; Ci += Ar*Bi ; Ci += Ai*Br
+// f64 MFMA operand / result maps (cdna_hip_programming.md §3):
+//   A: lane l holds A[l&15][k=l>>4];  B: lane l holds B[k=l>>4][l&15]
+//   D: 4 regs/lane, reg r = D[row=(l>>4)+4r][col=l&15]
+#pragma once
+
+#include "qd_common.hpp"
+
+namespace qd {
+
+constexpr int CG_WG = 512;       // threads per workgroup
+constexpr int CG_KT = 16;        // complex K per LDS stage
+constexpr int CG_SA = CG_KT + 2; // padded A-tile row stride (complex)
+
+template <int BT> struct CgCfg;
+// BT x BT block; wave grid WR x WC; each wave owns MW x NW MFMA tiles (16x16).
+template <> struct CgCfg<128> { static constexpr int MW = 2, NW = 4, WR = 4, WC = 2; };
+template <> struct CgCfg<64>  { static constexpr int MW = 1, NW = 2, WR = 4, WC = 2; };
+template <> struct CgCfg<32>  { static constexpr int MW = 1, NW = 1, WR = 2, WC = 2; };
+
+struct CgSeg {
+  const c128* A;  // points at A[block_row0][0], leading dim lda
+  const c128* B;  // points at B[0][block_col0], leading dim ldb
+};
+
+template <int BT>
+struct CgLds {
+  c128 a[2][BT * CG_SA];
+  c128 b[2][CG_KT * BT];
+};
+
+template <int BT>
+struct CgAcc {
+  static constexpr int MW = CgCfg<BT>::MW, NW = CgCfg<BT>::NW;
+  d4 re[MW][NW];
+  d4 im[MW][NW];
+};
+
+// Number of complex elements per thread for one A (or B) tile.
+template <int BT> constexpr int cg_nld() { return (BT * CG_KT) / CG_WG; }
+
+template <int BT>
+__device__ __forceinline__ void cg_load_tile(const CgSeg& s, int lda, int ldb, int k0, c128 (&ra)[cg_nld<BT>()],
+                                             c128 (&rb)[cg_nld<BT>()]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < cg_nld<BT>(); ++q) {
+    const int e = tid + CG_WG * q;
+    const int ar = e >> 4, ac = e & 15;                 // A tile: BT rows x 16
+    ra[q] = s.A[(size_t)ar * lda + k0 + ac];
+    const int br = e / BT, bc = e % BT;                 // B tile: 16 rows x BT
+    rb[q] = s.B[(size_t)(k0 + br) * ldb + bc];
+  }
+}
+
+template <int BT>
+__device__ __forceinline__ void cg_store_tile(CgLds<BT>& L, int buf, const c128 (&ra)[cg_nld<BT>()],
+                                              const c128 (&rb)[cg_nld<BT>()]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < cg_nld<BT>(); ++q) {
+    const int e = tid + CG_WG * q;
+    L.a[buf][(e >> 4) * CG_SA + (e & 15)] = ra[q];
+    L.b[buf][e] = rb[q];  // row (e / BT), col (e % BT), stride BT
+  }
+}
+
+template <int BT>
+__device__ __forceinline__ void cg_compute_tile(const CgLds<BT>& L, int buf, CgAcc<BT>& acc, int wr0, int wc0) {
+  constexpr int MW = CgCfg<BT>::MW, NW = CgCfg<BT>::NW;
+  const int lane = threadIdx.x & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int kk = 0; kk < CG_KT; kk += 4) {
+    c128 a[MW], b[NW];
+#pragma unroll
+    for (int mi = 0; mi < MW; ++mi) a[mi] = L.a[buf][(wr0 + mi * 16 + lr) * CG_SA + kk + lk];
+#pragma unroll
+    for (int nj = 0; nj < NW; ++nj) b[nj] = L.b[buf][(kk + lk) * BT + wc0 + nj * 16 + lr];
+#pragma unroll
+    for (int mi = 0; mi < MW; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < NW; ++nj) {
+        acc.re[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi].re, b[nj].re, acc.re[mi][nj], 0, 0, 0);
+        acc.im[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi].re, b[nj].im, acc.im[mi][nj], 0, 0, 0);
+      }
+#pragma unroll
+    for (int mi = 0; mi < MW; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < NW; ++nj) {
+        acc.re[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(-a[mi].im, b[nj].im, acc.re[mi][nj], 0, 0, 0);
+        acc.im[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi].im, b[nj].re, acc.im[mi][nj], 0, 0, 0);
+      }
+  }
+}
+
+// Accumulate sum_s A_s * B_s over nseg segments of depth K (K % 16 == 0) into
+// a zero-initialised accumulator.  All threads of the workgroup must call it.
+// Ends with a workgroup barrier, so LDS may be reused immediately after.
+template <int BT>
+__device__ __forceinline__ void cg_block_gemm(const CgSeg* segs, int nseg, int K, int lda, int ldb, CgLds<BT>& L,
+                                              CgAcc<BT>& acc) {
+  constexpr int MW = CgCfg<BT>::MW, NW = CgCfg<BT>::NW, WC = CgCfg<BT>::WC, WR = CgCfg<BT>::WR;
+  const int wave = threadIdx.x >> 6;
+  const bool active = wave < WR * WC;
+  const int wr0 = (wave / WC) * (MW * 16);
+  const int wc0 = (wave % WC) * (NW * 16);
+#pragma unroll
+  for (int mi = 0; mi < MW; ++mi)
+#pragma unroll
+    for (int nj = 0; nj < NW; ++nj) {
+      acc.re[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
+      acc.im[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
+    }
+  const int tiles_per_seg = K / CG_KT;
+  const int T = nseg * tiles_per_seg;
+  c128 ra[cg_nld<BT>()], rb[cg_nld<BT>()];
+  cg_load_tile<BT>(segs[0], lda, ldb, 0, ra, rb);
+  cg_store_tile<BT>(L, 0, ra, rb);
+  __syncthreads();
+  for (int t = 0; t < T; ++t) {
+    const bool more = (t + 1) < T;
+    if (more) {
+      const int tn = t + 1;
+      cg_load_tile<BT>(segs[tn / tiles_per_seg], lda, ldb, (tn % tiles_per_seg) * CG_KT, ra, rb);
+    }
+    if (active) cg_compute_tile<BT>(L, t & 1, acc, wr0, wc0);
+    if (more) cg_store_tile<BT>(L, (t + 1) & 1, ra, rb);
+    __syncthreads();
+  }
+}
+
+// Visit every accumulator element: f(row, col, value) with row/col inside the block.
+template <int BT, typename F>
+__device__ __forceinline__ void cg_epilogue(const CgAcc<BT>& acc, F&& f) {
+  constexpr int MW = CgCfg<BT>::MW, NW = CgCfg<BT>::NW, WC = CgCfg<BT>::WC, WR = CgCfg<BT>::WR;
+  const int wave = threadIdx.x >> 6;
+  if (wave >= WR * WC) return;
+  const int lane = threadIdx.x & 63;
+  const int wr0 = (wave / WC) * (MW * 16);
+  const int wc0 = (wave % WC) * (NW * 16);
+#pragma unroll
+  for (int mi = 0; mi < MW; ++mi)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int nj = 0; nj < NW; ++nj) {
+        const int row = wr0 + mi * 16 + (lane >> 4) + 4 * r;
+        const int col = wc0 + nj * 16 + (lane & 15);
+        f(row, col, cmk(acc.re[mi][nj][r], acc.im[mi][nj][r]));
+      }
+}
+
+}  // namespace qd

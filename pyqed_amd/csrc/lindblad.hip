@@ -1,0 +1,316 @@
+// lindblad.hip — batched RK4 Lindblad propagation (qd_lindblad_rk4).
+//
+// Replaces the hot loop of pyqed/oqs.py:1682-1690 (_lindblad), whose RHS is
+// oqs.liouvillian + oqs.lindbladian (oqs.py:697-714) and whose integrator is
+// phys.rk4 (phys.py:1051-1064).
+//
+// Formulation (mathematically identical to the reference RHS):
+//   K    = H - (i/2) sum_c C_c^+ C_c
+//   L[r] = (-iK) r + r (iK^+) + sum_c (C_c r) C_c^+
+//        = -i(H r - r H) + sum_c ( C_c r C_c^+ - 1/2 {C_c^+ C_c, r} )
+// so one RHS costs 2 + 2*nc complex N^3 GEMMs (the reference spends 2 + 4*nc).
+//
+// Kernel layout: one 512-thread workgroup owns one density matrix for the
+// whole run (persistent over nsteps RK4 steps; only workgroup barriers, no
+// inter-workgroup communication).  Per RK4 stage:
+//   phase 1: Y_c = C_c * rs                       (block GEMM, K = N)
+//   phase 2: k   = (-iK) rs + rs (iK^+) + sum_c Y_c C_c^+   (one accumulator,
+//            2+nc segments), fused epilogue does the RK4 bookkeeping
+//            (acc += w k ; rs' = rho + c k ; rho update at stage 4).
+// rs (two ping-pong buffers), acc and Y_c live in a per-workgroup scratch
+// slab in HBM (L2/MALL resident in practice).  Matrices are zero-padded to
+// Np = 32, 64 or a multiple of 128 so every GEMM tile is full; the padding
+// stays exactly zero through the propagation.
+#include "cgemm_block.hpp"
+
+namespace qd {
+namespace {
+
+constexpr int MAX_NC = 8;
+constexpr int MAX_NE = 16;
+
+struct LindbladParams {
+  const c128* Cop;  // [nc][Np][Np]  C_c
+  const c128* mK;   // [Np][Np]      -iK
+  const c128* iKd;  // [Np][Np]      iK^+
+  const c128* Cd;   // [nc][Np][Np]  C_c^+
+  const c128* eT;   // [ne][Np][Np]  E_m^T
+  c128* rho;        // [B][Np][Np]   state (in/out)
+  c128* ws;         // [B][3+nc][Np][Np] scratch
+  c128* obs;        // [B][nsteps+1][ne]
+  c128* snap;       // [B][nsave][N][N]
+  int N, Np, nc, ne, nsteps, save_every, nsave;
+  double dt;
+};
+
+// Tr(E_m rho) = sum_ij rho_ij E_m[j][i] = sum_ij rho_ij eT_m[i][j]; fixed
+// reduction order (per-thread strided partials, wave butterfly, 8-wave sum).
+__device__ void wg_observables(const c128* rho, const c128* eT, int ne, size_t NN, c128* out, c128* sred) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int m = 0; m < ne; ++m) {
+    const c128* e = eT + (size_t)m * NN;
+    double sr = 0.0, si = 0.0;
+    for (size_t i = tid; i < NN; i += CG_WG) {
+      c128 r = rho[i], x = e[i];
+      sr += r.re * x.re - r.im * x.im;
+      si += r.re * x.im + r.im * x.re;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      sr += __shfl_xor(sr, off, 64);
+      si += __shfl_xor(si, off, 64);
+    }
+    if (lane == 0) sred[wave] = cmk(sr, si);
+    __syncthreads();
+    if (tid == 0) {
+      c128 s = sred[0];
+      for (int w = 1; w < CG_WG / 64; ++w) s = cadd(s, sred[w]);
+      out[m] = s;
+    }
+    __syncthreads();
+  }
+}
+
+template <int BT>
+__global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
+  __shared__ CgLds<BT> L;
+  __shared__ c128 sred[CG_WG / 64];
+
+  const int b = blockIdx.x;
+  const int Np = p.Np, nc = p.nc;
+  const size_t NN = (size_t)Np * Np;
+  c128* rho = p.rho + (size_t)b * NN;
+  c128* ws = p.ws + (size_t)b * (3 + nc) * NN;
+  c128* rs[2] = {ws, ws + NN};
+  c128* acc = ws + 2 * NN;
+  c128* Y = ws + 3 * NN;
+  c128* obs = p.obs ? p.obs + (size_t)b * (p.nsteps + 1) * p.ne : nullptr;
+
+  for (size_t i = threadIdx.x; i < NN; i += CG_WG) rs[0][i] = rho[i];
+  if (p.ne > 0) wg_observables(rho, p.eT, p.ne, NN, obs, sred);
+  __syncthreads();
+
+  const int nb = Np / BT;
+  const double dt = p.dt, dt2 = p.dt / 2.0;
+  int cur = 0;
+  CgAcc<BT> A;
+  CgSeg segs[2 + MAX_NC];
+
+  for (int step = 0; step < p.nsteps; ++step) {
+    for (int stage = 0; stage < 4; ++stage) {
+      const c128* r = rs[cur];
+      c128* rn = rs[cur ^ 1];
+      // ---- phase 1: Y_c = C_c r
+      for (int c = 0; c < nc; ++c) {
+        for (int bm = 0; bm < nb; ++bm)
+          for (int bn = 0; bn < nb; ++bn) {
+            segs[0].A = p.Cop + (size_t)c * NN + (size_t)bm * BT * Np;
+            segs[0].B = r + bn * BT;
+            cg_block_gemm<BT>(segs, 1, Np, Np, Np, L, A);
+            c128* Yc = Y + (size_t)c * NN;
+            cg_epilogue<BT>(A, [&](int row, int col, c128 v) {
+              Yc[(size_t)(bm * BT + row) * Np + bn * BT + col] = v;
+            });
+          }
+      }
+      __syncthreads();
+      // ---- phase 2: k = (-iK) r + r (iK^+) + sum_c Y_c C_c^+ ; RK4 epilogue
+      for (int bm = 0; bm < nb; ++bm)
+        for (int bn = 0; bn < nb; ++bn) {
+          segs[0].A = p.mK + (size_t)bm * BT * Np;
+          segs[0].B = r + bn * BT;
+          segs[1].A = r + (size_t)bm * BT * Np;
+          segs[1].B = p.iKd + bn * BT;
+          for (int c = 0; c < nc; ++c) {
+            segs[2 + c].A = Y + (size_t)c * NN + (size_t)bm * BT * Np;
+            segs[2 + c].B = p.Cd + (size_t)c * NN + bn * BT;
+          }
+          cg_block_gemm<BT>(segs, 2 + nc, Np, Np, Np, L, A);
+          cg_epilogue<BT>(A, [&](int row, int col, c128 k) {
+            const size_t idx = (size_t)(bm * BT + row) * Np + bn * BT + col;
+            const c128 r0 = rho[idx];
+            if (stage == 0) {
+              acc[idx] = k;
+              rn[idx] = cadd(r0, cscale(k, dt2));
+            } else if (stage == 1) {
+              acc[idx] = cadd(acc[idx], cscale(k, 2.0));
+              rn[idx] = cadd(r0, cscale(k, dt2));
+            } else if (stage == 2) {
+              acc[idx] = cadd(acc[idx], cscale(k, 2.0));
+              rn[idx] = cadd(r0, cscale(k, dt));
+            } else {
+              const c128 a = cadd(acc[idx], k);
+              const c128 r1 = cadd(r0, cscale(cscale(a, 1.0 / 6.0), dt));
+              rho[idx] = r1;
+              rn[idx] = r1;
+            }
+          });
+        }
+      __syncthreads();
+      cur ^= 1;
+    }
+    if (p.ne > 0) wg_observables(rho, p.eT, p.ne, NN, obs + (size_t)(step + 1) * p.ne, sred);
+    if (p.snap && p.save_every > 0 && ((step + 1) % p.save_every) == 0) {
+      const int s = (step + 1) / p.save_every - 1;
+      if (s < p.nsave) {
+        const int N = p.N;
+        c128* out = p.snap + ((size_t)b * p.nsave + s) * N * N;
+        for (size_t i = threadIdx.x; i < (size_t)N * N; i += CG_WG) {
+          const int ii = (int)(i / N), jj = (int)(i % N);
+          out[i] = rho[(size_t)ii * Np + jj];
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- operator prep
+// K = H - (i/2) sum_c C_c^+ C_c ; writes -iK, iK^+ (transposed), padded C, C^+, E^T.
+__global__ void lindblad_prep_kernel(const c128* H, const c128* C, int nc, const c128* E, int ne, int N, int Np,
+                                     c128* Cop, c128* mK, c128* iKd, c128* Cd, c128* eT) {
+  const size_t NN = (size_t)Np * Np;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < NN; e += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(e / Np), j = (int)(e % Np);
+    const bool in = (i < N) && (j < N);
+    c128 K = cmk(0, 0);
+    if (in) {
+      K = H[(size_t)i * N + j];
+      c128 s = cmk(0, 0);
+      for (int c = 0; c < nc; ++c) {
+        const c128* Cc = C + (size_t)c * N * N;
+        for (int k = 0; k < N; ++k) s = cadd(s, cmul(cconj(Cc[(size_t)k * N + i]), Cc[(size_t)k * N + j]));
+      }
+      K = csub(K, cmuli(cscale(s, 0.5)));  // K - (i/2) s
+    }
+    mK[e] = cmulmi(K);                             // (-iK)[i][j]
+    iKd[(size_t)j * Np + i] = cmuli(cconj(K));     // (iK^+)[j][i] = i conj(K[i][j])
+    for (int c = 0; c < nc; ++c) {
+      const c128 v = in ? C[(size_t)c * N * N + (size_t)i * N + j] : cmk(0, 0);
+      Cop[c * NN + e] = v;
+      Cd[c * NN + (size_t)j * Np + i] = cconj(v);
+    }
+    for (int m = 0; m < ne; ++m) {
+      const c128 v = in ? E[(size_t)m * N * N + (size_t)j * N + i] : cmk(0, 0);
+      eT[m * NN + e] = v;  // eT[i][j] = E[j][i]
+    }
+  }
+}
+
+__global__ void pad_kernel(const c128* src, c128* dst, int B, int N, int Np) {
+  const size_t tot = (size_t)B * Np * Np;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    const size_t b = e / ((size_t)Np * Np);
+    const int r = (int)((e / Np) % Np), c = (int)(e % Np);
+    dst[e] = (r < N && c < N) ? src[(b * N + r) * N + c] : cmk(0, 0);
+  }
+}
+
+__global__ void unpad_kernel(const c128* src, c128* dst, int B, int N, int Np) {
+  const size_t tot = (size_t)B * N * N;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    const size_t b = e / ((size_t)N * N);
+    const int r = (int)((e / N) % N), c = (int)(e % N);
+    dst[e] = src[(b * Np + r) * Np + c];
+  }
+}
+
+int padded_dim(int N) {
+  if (N <= 32) return 32;
+  if (N <= 64) return 64;
+  return ((N + 127) / 128) * 128;
+}
+
+}  // namespace
+}  // namespace qd
+
+using namespace qd;
+
+extern "C" int qd_lindblad_rk4(const qd_c128* H_, const qd_c128* C_, int nc, qd_c128* rho_, int B, int N, double dt,
+                               int nsteps, const qd_c128* E_, int ne, qd_c128* obs_, qd_c128* snap_, int save_every,
+                               void* stream_) {
+  QD_CHECK_ARG(H_ && rho_, "qd_lindblad_rk4: H and rho must be non-null");
+  QD_CHECK_ARG(N >= 1 && N <= 1024, "qd_lindblad_rk4: N=%d outside [1, 1024]", N);
+  QD_CHECK_ARG(B >= 1, "qd_lindblad_rk4: B=%d must be >= 1", B);
+  QD_CHECK_ARG(nc >= 0 && nc <= MAX_NC, "qd_lindblad_rk4: nc=%d outside [0, %d]", nc, MAX_NC);
+  QD_CHECK_ARG(nc == 0 || C_, "qd_lindblad_rk4: C is null but nc=%d", nc);
+  QD_CHECK_ARG(ne >= 0 && ne <= MAX_NE, "qd_lindblad_rk4: ne=%d outside [0, %d]", ne, MAX_NE);
+  QD_CHECK_ARG(ne == 0 || (E_ && obs_), "qd_lindblad_rk4: E/obs null but ne=%d", ne);
+  QD_CHECK_ARG(nsteps >= 0, "qd_lindblad_rk4: nsteps=%d < 0", nsteps);
+  hipStream_t st = (hipStream_t)stream_;
+  const c128* H = reinterpret_cast<const c128*>(H_);
+  const c128* C = reinterpret_cast<const c128*>(C_);
+  const c128* E = reinterpret_cast<const c128*>(E_);
+  c128* rho = reinterpret_cast<c128*>(rho_);
+
+  const int Np = padded_dim(N);
+  const size_t NN = (size_t)Np * Np;
+  // operator workspace: Cop, mK, iKd, Cd, eT
+  const size_t ops_elems = (size_t)(2 + 2 * nc + ne) * NN;
+  void* wops = nullptr;
+  int rc = workspace(WS_LINDBLAD_OPS, ops_elems * sizeof(c128), &wops);
+  if (rc) return rc;
+  c128* Cop = (c128*)wops;
+  c128* mK = Cop + (size_t)nc * NN;
+  c128* iKd = mK + NN;
+  c128* Cd = iKd + NN;
+  c128* eT = Cd + (size_t)nc * NN;
+  // state workspace: per-matrix scratch (+ padded rho when N != Np)
+  const bool pad = (Np != N);
+  const size_t st_elems = (size_t)B * (3 + nc) * NN + (pad ? (size_t)B * NN : 0);
+  void* wst = nullptr;
+  rc = workspace(WS_LINDBLAD, st_elems * sizeof(c128), &wst);
+  if (rc) return rc;
+  c128* scratch = (c128*)wst;
+  c128* rho_p = pad ? scratch + (size_t)B * (3 + nc) * NN : rho;
+
+  {
+    const int threads = 256;
+    const int blocks = (int)std::min<size_t>((NN + threads - 1) / threads, 4096);
+    hipLaunchKernelGGL(lindblad_prep_kernel, dim3(blocks), dim3(threads), 0, st, H, C, nc, E, ne, N, Np, Cop, mK, iKd,
+                       Cd, eT);
+    QD_HIP(hipGetLastError());
+    if (pad) {
+      const size_t tot = (size_t)B * NN;
+      const int pb = (int)std::min<size_t>((tot + threads - 1) / threads, 65535);
+      hipLaunchKernelGGL(pad_kernel, dim3(pb), dim3(threads), 0, st, rho, rho_p, B, N, Np);
+      QD_HIP(hipGetLastError());
+    }
+  }
+
+  LindbladParams p;
+  p.Cop = Cop;
+  p.mK = mK;
+  p.iKd = iKd;
+  p.Cd = Cd;
+  p.eT = eT;
+  p.rho = rho_p;
+  p.ws = scratch;
+  p.obs = reinterpret_cast<c128*>(obs_);
+  p.snap = (save_every > 0) ? reinterpret_cast<c128*>(snap_) : nullptr;
+  p.N = N;
+  p.Np = Np;
+  p.nc = nc;
+  p.ne = ne;
+  p.nsteps = nsteps;
+  p.save_every = save_every;
+  p.nsave = (save_every > 0) ? nsteps / save_every : 0;
+  p.dt = dt;
+
+  if (Np == 32)
+    hipLaunchKernelGGL(lindblad_rk4_kernel<32>, dim3(B), dim3(CG_WG), 0, st, p);
+  else if (Np == 64)
+    hipLaunchKernelGGL(lindblad_rk4_kernel<64>, dim3(B), dim3(CG_WG), 0, st, p);
+  else
+    hipLaunchKernelGGL(lindblad_rk4_kernel<128>, dim3(B), dim3(CG_WG), 0, st, p);
+  QD_HIP(hipGetLastError());
+
+  if (pad) {
+    const int threads = 256;
+    const size_t tot = (size_t)B * N * N;
+    const int pb = (int)std::min<size_t>((tot + threads - 1) / threads, 65535);
+    hipLaunchKernelGGL(unpad_kernel, dim3(pb), dim3(threads), 0, st, rho_p, rho, B, N, Np);
+    QD_HIP(hipGetLastError());
+  }
+  return QD_OK;
+}

@@ -1,0 +1,69 @@
+// qd_common.hpp — shared device/host helpers for libqdyn (gfx950 only).
+//
+// Complex numbers are interleaved fp64 pairs (re, im), byte-compatible with
+// torch.complex128 / numpy.complex128.  Every entry point in include/qdyn.h
+// returns 0 on success and a negative QD_E* code otherwise; the message is
+// kept in a thread-local buffer readable through qd_last_error().
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+#include <cstdio>
+#include <cstdarg>
+#include <cstring>
+#include <algorithm>
+
+#include "../../include/qdyn.h"
+
+namespace qd {
+
+// ---------------------------------------------------------------- errors
+void set_error(const char* fmt, ...);
+
+#define QD_CHECK_ARG(cond, ...)                         \
+  do {                                                  \
+    if (!(cond)) {                                      \
+      ::qd::set_error(__VA_ARGS__);                     \
+      return QD_EINVAL;                                 \
+    }                                                   \
+  } while (0)
+
+#define QD_HIP(call)                                                        \
+  do {                                                                      \
+    hipError_t _e = (call);                                                 \
+    if (_e != hipSuccess) {                                                 \
+      ::qd::set_error("HIP error %s at %s:%d (%s)", hipGetErrorString(_e),  \
+                      __FILE__, __LINE__, #call);                           \
+      return QD_EHIP;                                                       \
+    }                                                                       \
+  } while (0)
+
+// Per-device growable workspace, owned by the library (freed by qd_shutdown).
+// Never handed to the caller.  Slot ids keep independent users apart.
+enum WsSlot { WS_LINDBLAD = 0, WS_LINDBLAD_OPS = 1, WS_SPO = 2, WS_DEOM = 3,
+              WS_SUPEROP = 4, WS_2DES = 5, WS_MISC = 6, WS_NSLOTS = 8 };
+int workspace(WsSlot slot, size_t bytes, void** ptr);
+void free_workspaces();
+
+// ---------------------------------------------------------------- complex
+struct alignas(16) c128 {
+  double re, im;
+};
+
+__host__ __device__ inline c128 cmk(double r, double i) { c128 z; z.re = r; z.im = i; return z; }
+__host__ __device__ inline c128 cadd(c128 a, c128 b) { return cmk(a.re + b.re, a.im + b.im); }
+__host__ __device__ inline c128 csub(c128 a, c128 b) { return cmk(a.re - b.re, a.im - b.im); }
+__host__ __device__ inline c128 cmul(c128 a, c128 b) {
+  return cmk(a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re);
+}
+__host__ __device__ inline c128 cscale(c128 a, double s) { return cmk(a.re * s, a.im * s); }
+__host__ __device__ inline c128 cconj(c128 a) { return cmk(a.re, -a.im); }
+__host__ __device__ inline c128 cmuli(c128 a) { return cmk(-a.im, a.re); }     // i*a
+__host__ __device__ inline c128 cmulmi(c128 a) { return cmk(a.im, -a.re); }    // -i*a
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace qd
