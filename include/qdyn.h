@@ -64,12 +64,71 @@ int qd_synchronize(void* stream);     /* hipStreamSynchronize                 */
  *                         oqs.py:1680), NULL when ne == 0
  *   snap  [B][nsteps/save_every][N][N]  rho after steps save_every, 2*save_every, ...
  *                         (NULL or save_every <= 0: no snapshots)
- * Constraints: 1 <= N <= 1024, 0 <= nc <= 8, 0 <= ne <= 16, B >= 1.
+ * Constraints: 1 <= N <= 1024, 0 <= nc <= 16, 0 <= ne <= 16, B >= 1.
  */
 int qd_lindblad_rk4(const qd_c128* H, const qd_c128* C, int nc, qd_c128* rho,
                     int B, int N, double dt, int nsteps, const qd_c128* E,
                     int ne, qd_c128* obs, qd_c128* snap, int save_every,
                     void* stream);
+
+/*
+ * Batched RK4 for any equation of motion of "generalised Lindblad form"
+ *     d rho/dt = P rho + rho Q + sum_c L_c rho R_c        (c < npairs)
+ * P, Q [N][N]; L, R [npairs][N][N]; other arguments as qd_lindblad_rk4.
+ * Used for Redfield dynamics in the H eigenbasis: replaces the csr R.vec(rho)
+ * RK4 loop of pyqed/oqs.py:436-459 (_redfield) + rhs (oqs.py:462-463); the
+ * pyqed_amd host builds P, Q, L_c, R_c from redfield_tensor's ingredients
+ * (oqs.py:519-570).  Constraints: 0 <= npairs <= 16.
+ */
+int qd_glf_rk4(const qd_c128* P, const qd_c128* Q, const qd_c128* L,
+               const qd_c128* R, int npairs, qd_c128* rho, int B, int N,
+               double dt, int nsteps, const qd_c128* E, int ne, qd_c128* obs,
+               qd_c128* snap, int save_every, void* stream);
+
+/*
+ * Batched basis transform of B matrices [B][N][N] in place:
+ *   mode 0: A <- V^+ A V   (pyqed/phys.py:1121-1137 transform(A, V))
+ *   mode 1: A <- V A V^+   (transform(A, dag(V)), back-transform in oqs.py:450)
+ */
+int qd_basis_transform(const qd_c128* V, qd_c128* A, int B, int N, int mode,
+                       void* stream);
+
+/* ------------------------------------------------------------ response --- */
+/*
+ * SOS Liouville-space propagator U[a][b][k] = sum_j U1[a][j] e^{lam_j t_k} U2[j][b]
+ * (U2 = U1^-1; layout (nL, nL, nt) as RedfieldSolver.U).  Replaces the
+ * contraction of pyqed/oqs.py:196-212 (propagator, method='SOS').
+ */
+int qd_sos_propagator(const qd_c128* U1, const qd_c128* U2, const qd_c128* lam,
+                      int nL, const double* t, int nt, qd_c128* U,
+                      void* stream);
+
+/*
+ * Full third-order response cube in eigen form
+ *   out[i][j][k] = (-i)^3 sum_pqr alpha_p e^{lam_p t3_i} B[p][q] e^{lam_q t2_j}
+ *                                  C[q][r] e^{lam_r t1_k} beta_r
+ * (alpha = I^T a U1, B = U1^-1 b U1, C = U1^-1 c U1, beta = U1^-1 d vec(rho0)).
+ * Replaces the tensordot chain of pyqed/oqs.py:327-357 (correlation_4op_3t);
+ * out layout [n3][n2][n1] = the reference's corr[i, j, k].
+ */
+int qd_response_cube(const qd_c128* alpha, const qd_c128* B, const qd_c128* C,
+                     const qd_c128* beta, const qd_c128* lam, int nL,
+                     const double* t3, int n3, const double* t2, int n2,
+                     const double* t1, int n1, qd_c128* out, void* stream);
+
+/*
+ * Disorder-ensemble 2D response at fixed t2 (2DES (t3, t1) grid):
+ *   out[i][k] (+)= (-i)^3 sum_m sum_pq alpha[m][p] e^{lam[m][p] t3_i}
+ *                                      Mt[m][p][q] beta[m][q] e^{lam[m][q] t1_k}
+ * with Mt_m = B_m diag(e^{lam_m t2}) C_m.  For M = 1 this is the slice
+ * correlation_4op_3t(...)[:, j, :] (oqs.py:268-357).
+ * accumulate != 0 adds into out.  Shards over ranks by members; the
+ * partial grids are summed with one RCCL reduce by the caller.
+ */
+int qd_response2d_ensemble(const qd_c128* alpha, const qd_c128* Mt,
+                           const qd_c128* beta, const qd_c128* lam, int M,
+                           int nL, const double* t3, int n3, const double* t1,
+                           int n1, qd_c128* out, int accumulate, void* stream);
 
 #ifdef __cplusplus
 }

@@ -37,6 +37,14 @@ SIGNATURES = {
     "qd_synchronize": (c_int, [c_void_p]),
     "qd_lindblad_rk4": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_double, c_int,
                                 c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
+    "qd_glf_rk4": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_double,
+                           c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
+    "qd_basis_transform": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "qd_sos_propagator": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]),
+    "qd_response_cube": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
+                                 c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]),
+    "qd_response2d_ensemble": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int,
+                                       c_void_p, c_int, c_void_p, c_int, c_void_p]),
 }
 
 _lib = None

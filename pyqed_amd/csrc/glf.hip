@@ -1,20 +1,24 @@
-// lindblad.hip — batched RK4 Lindblad propagation (qd_lindblad_rk4).
+// glf.hip — batched RK4 propagation of density matrices whose equation of
+// motion has the "generalised Lindblad form" (GLF)
+//     d rho/dt = P rho + rho Q + sum_c L_c rho R_c .
+// Entry points: qd_glf_rk4 (caller supplies P, Q, L_c, R_c) and
+// qd_lindblad_rk4 (builds P, Q, R_c from H and the collapse operators).
 //
-// Replaces the hot loop of pyqed/oqs.py:1682-1690 (_lindblad), whose RHS is
-// oqs.liouvillian + oqs.lindbladian (oqs.py:697-714) and whose integrator is
-// phys.rk4 (phys.py:1051-1064).
-//
-// Formulation (mathematically identical to the reference RHS):
-//   K    = H - (i/2) sum_c C_c^+ C_c
-//   L[r] = (-iK) r + r (iK^+) + sum_c (C_c r) C_c^+
-//        = -i(H r - r H) + sum_c ( C_c r C_c^+ - 1/2 {C_c^+ C_c, r} )
+// Lindblad (replaces pyqed/oqs.py:1682-1690 _lindblad, RHS oqs.py:697-714,
+// integrator phys.rk4 phys.py:1051-1064), mathematically identical to the
+// reference RHS:
+//   K    = H - (i/2) sum_c C_c^+ C_c ,  P = -iK , Q = iK^+ , L_c = C_c , R_c = C_c^+
+//   L[r] = -i(H r - r H) + sum_c ( C_c r C_c^+ - 1/2 {C_c^+ C_c, r} )
 // so one RHS costs 2 + 2*nc complex N^3 GEMMs (the reference spends 2 + 4*nc).
+// Redfield in the H eigenbasis (oqs.py:519-570, R vec(rho) of oqs.py:462) is
+// also GLF: P = -iE - sum_k A_k Lam_k, Q = iE - sum_k Lam_k^+ A_k, pairs
+// (A_k, Lam_k^+) and (Lam_k, A_k) — see pyqed_amd/oqs.py.
 //
 // Kernel layout: one 512-thread workgroup owns one density matrix for the
 // whole run (persistent over nsteps RK4 steps; only workgroup barriers, no
 // inter-workgroup communication).  Per RK4 stage:
-//   phase 1: Y_c = C_c * rs                       (block GEMM, K = N)
-//   phase 2: k   = (-iK) rs + rs (iK^+) + sum_c Y_c C_c^+   (one accumulator,
+//   phase 1: Y_c = L_c * rs                       (block GEMM, K = N)
+//   phase 2: k   = P rs + rs Q + sum_c Y_c R_c    (one accumulator,
 //            2+nc segments), fused epilogue does the RK4 bookkeeping
 //            (acc += w k ; rs' = rho + c k ; rho update at stage 4).
 // rs (two ping-pong buffers), acc and Y_c live in a per-workgroup scratch
@@ -26,14 +30,14 @@
 namespace qd {
 namespace {
 
-constexpr int MAX_NC = 8;
+constexpr int MAX_NC = 16;
 constexpr int MAX_NE = 16;
 
 struct LindbladParams {
-  const c128* Cop;  // [nc][Np][Np]  C_c
-  const c128* mK;   // [Np][Np]      -iK
-  const c128* iKd;  // [Np][Np]      iK^+
-  const c128* Cd;   // [nc][Np][Np]  C_c^+
+  const c128* Cop;  // [nc][Np][Np]  L_c   (Lindblad: C_c)
+  const c128* mK;   // [Np][Np]      P     (Lindblad: -iK)
+  const c128* iKd;  // [Np][Np]      Q     (Lindblad: iK^+)
+  const c128* Cd;   // [nc][Np][Np]  R_c   (Lindblad: C_c^+)
   const c128* eT;   // [ne][Np][Np]  E_m^T
   c128* rho;        // [B][Np][Np]   state (in/out)
   c128* ws;         // [B][3+nc][Np][Np] scratch
@@ -197,6 +201,26 @@ __global__ void lindblad_prep_kernel(const c128* H, const c128* C, int nc, const
   }
 }
 
+// GLF operators supplied by the caller: pad/copy P, Q, L_c, R_c and E^T into
+// the kernel's operator workspace.
+__global__ void glf_prep_kernel(const c128* P, const c128* Q, const c128* Lop, const c128* Rop, int nc,
+                                const c128* E, int ne, int N, int Np, c128* Cop, c128* mK, c128* iKd, c128* Cd,
+                                c128* eT) {
+  const size_t NN = (size_t)Np * Np;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < NN; e += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(e / Np), j = (int)(e % Np);
+    const bool in = (i < N) && (j < N);
+    const size_t src = (size_t)i * N + j;
+    mK[e] = in ? P[src] : cmk(0, 0);
+    iKd[e] = in ? Q[src] : cmk(0, 0);
+    for (int c = 0; c < nc; ++c) {
+      Cop[c * NN + e] = in ? Lop[(size_t)c * N * N + src] : cmk(0, 0);
+      Cd[c * NN + e] = in ? Rop[(size_t)c * N * N + src] : cmk(0, 0);
+    }
+    for (int m = 0; m < ne; ++m) eT[m * NN + e] = in ? E[(size_t)m * N * N + (size_t)j * N + i] : cmk(0, 0);
+  }
+}
+
 __global__ void pad_kernel(const c128* src, c128* dst, int B, int N, int Np) {
   const size_t tot = (size_t)B * Np * Np;
   for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
@@ -215,6 +239,49 @@ __global__ void unpad_kernel(const c128* src, c128* dst, int B, int N, int Np) {
   }
 }
 
+// Batched basis transform, one workgroup per matrix:
+//   mode 0: A <- V^+ A V   (phys.transform(A, V), pyqed/phys.py:1121-1137)
+//   mode 1: A <- V A V^+   (transform(A, dag(V)), the back-transform of oqs.py:450)
+template <int BT>
+__global__ __launch_bounds__(CG_WG) void basis_transform_kernel(const c128* Vl, const c128* Vr, c128* A, c128* T,
+                                                                int Np) {
+  __shared__ CgLds<BT> L;
+  const size_t NN = (size_t)Np * Np;
+  c128* Ab = A + (size_t)blockIdx.x * NN;
+  c128* Tb = T + (size_t)blockIdx.x * NN;
+  const int nb = Np / BT;
+  CgAcc<BT> acc;
+  CgSeg seg;
+  for (int bm = 0; bm < nb; ++bm)
+    for (int bn = 0; bn < nb; ++bn) {  // T = Vl * A
+      seg.A = Vl + (size_t)bm * BT * Np;
+      seg.B = Ab + bn * BT;
+      cg_block_gemm<BT>(&seg, 1, Np, Np, Np, L, acc);
+      cg_epilogue<BT>(acc, [&](int r, int c, c128 v) { Tb[(size_t)(bm * BT + r) * Np + bn * BT + c] = v; });
+    }
+  __syncthreads();
+  for (int bm = 0; bm < nb; ++bm)
+    for (int bn = 0; bn < nb; ++bn) {  // A = T * Vr
+      seg.A = Tb + (size_t)bm * BT * Np;
+      seg.B = Vr + bn * BT;
+      cg_block_gemm<BT>(&seg, 1, Np, Np, Np, L, acc);
+      cg_epilogue<BT>(acc, [&](int r, int c, c128 v) { Ab[(size_t)(bm * BT + r) * Np + bn * BT + c] = v; });
+    }
+}
+
+// Vl, Vr (padded) from V: mode 0 -> Vl = V^+, Vr = V ; mode 1 -> Vl = V, Vr = V^+
+__global__ void transform_prep_kernel(const c128* V, int N, int Np, int mode, c128* Vl, c128* Vr) {
+  const size_t NN = (size_t)Np * Np;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < NN; e += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(e / Np), j = (int)(e % Np);
+    const bool in = i < N && j < N;
+    const c128 v = in ? V[(size_t)i * N + j] : cmk(0, 0);          // V[i][j]
+    const c128 vd = in ? cconj(V[(size_t)j * N + i]) : cmk(0, 0);  // V^+[i][j]
+    Vl[e] = mode == 0 ? vd : v;
+    Vr[e] = mode == 0 ? v : vd;
+  }
+}
+
 int padded_dim(int N) {
   if (N <= 32) return 32;
   if (N <= 64) return 64;
@@ -226,26 +293,17 @@ int padded_dim(int N) {
 
 using namespace qd;
 
-extern "C" int qd_lindblad_rk4(const qd_c128* H_, const qd_c128* C_, int nc, qd_c128* rho_, int B, int N, double dt,
-                               int nsteps, const qd_c128* E_, int ne, qd_c128* obs_, qd_c128* snap_, int save_every,
-                               void* stream_) {
-  QD_CHECK_ARG(H_ && rho_, "qd_lindblad_rk4: H and rho must be non-null");
-  QD_CHECK_ARG(N >= 1 && N <= 1024, "qd_lindblad_rk4: N=%d outside [1, 1024]", N);
-  QD_CHECK_ARG(B >= 1, "qd_lindblad_rk4: B=%d must be >= 1", B);
-  QD_CHECK_ARG(nc >= 0 && nc <= MAX_NC, "qd_lindblad_rk4: nc=%d outside [0, %d]", nc, MAX_NC);
-  QD_CHECK_ARG(nc == 0 || C_, "qd_lindblad_rk4: C is null but nc=%d", nc);
-  QD_CHECK_ARG(ne >= 0 && ne <= MAX_NE, "qd_lindblad_rk4: ne=%d outside [0, %d]", ne, MAX_NE);
-  QD_CHECK_ARG(ne == 0 || (E_ && obs_), "qd_lindblad_rk4: E/obs null but ne=%d", ne);
-  QD_CHECK_ARG(nsteps >= 0, "qd_lindblad_rk4: nsteps=%d < 0", nsteps);
-  hipStream_t st = (hipStream_t)stream_;
-  const c128* H = reinterpret_cast<const c128*>(H_);
-  const c128* C = reinterpret_cast<const c128*>(C_);
-  const c128* E = reinterpret_cast<const c128*>(E_);
-  c128* rho = reinterpret_cast<c128*>(rho_);
+namespace {
 
+enum GlfSource { GLF_FROM_LINDBLAD = 0, GLF_FROM_OPERATORS = 1 };
+
+// Shared driver of qd_lindblad_rk4 / qd_glf_rk4.
+int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c128* Q, const c128* Lop,
+            const c128* Rop, int nc, c128* rho, int B, int N, double dt, int nsteps, const c128* E, int ne,
+            c128* obs, c128* snap, int save_every, hipStream_t st) {
   const int Np = padded_dim(N);
   const size_t NN = (size_t)Np * Np;
-  // operator workspace: Cop, mK, iKd, Cd, eT
+  // operator workspace: Cop(L), mK(P), iKd(Q), Cd(R), eT
   const size_t ops_elems = (size_t)(2 + 2 * nc + ne) * NN;
   void* wops = nullptr;
   int rc = workspace(WS_LINDBLAD_OPS, ops_elems * sizeof(c128), &wops);
@@ -264,18 +322,20 @@ extern "C" int qd_lindblad_rk4(const qd_c128* H_, const qd_c128* C_, int nc, qd_
   c128* scratch = (c128*)wst;
   c128* rho_p = pad ? scratch + (size_t)B * (3 + nc) * NN : rho;
 
-  {
-    const int threads = 256;
-    const int blocks = (int)std::min<size_t>((NN + threads - 1) / threads, 4096);
-    hipLaunchKernelGGL(lindblad_prep_kernel, dim3(blocks), dim3(threads), 0, st, H, C, nc, E, ne, N, Np, Cop, mK, iKd,
-                       Cd, eT);
+  const int threads = 256;
+  const int blocks = (int)std::min<size_t>((NN + threads - 1) / threads, 4096);
+  if (src == GLF_FROM_LINDBLAD)
+    hipLaunchKernelGGL(lindblad_prep_kernel, dim3(blocks), dim3(threads), 0, st, H, C, nc, E, ne, N, Np, Cop, mK,
+                       iKd, Cd, eT);
+  else
+    hipLaunchKernelGGL(glf_prep_kernel, dim3(blocks), dim3(threads), 0, st, P, Q, Lop, Rop, nc, E, ne, N, Np, Cop,
+                       mK, iKd, Cd, eT);
+  QD_HIP(hipGetLastError());
+  if (pad) {
+    const size_t tot = (size_t)B * NN;
+    const int pb = (int)std::min<size_t>((tot + threads - 1) / threads, 65535);
+    hipLaunchKernelGGL(pad_kernel, dim3(pb), dim3(threads), 0, st, rho, rho_p, B, N, Np);
     QD_HIP(hipGetLastError());
-    if (pad) {
-      const size_t tot = (size_t)B * NN;
-      const int pb = (int)std::min<size_t>((tot + threads - 1) / threads, 65535);
-      hipLaunchKernelGGL(pad_kernel, dim3(pb), dim3(threads), 0, st, rho, rho_p, B, N, Np);
-      QD_HIP(hipGetLastError());
-    }
   }
 
   LindbladParams p;
@@ -286,8 +346,8 @@ extern "C" int qd_lindblad_rk4(const qd_c128* H_, const qd_c128* C_, int nc, qd_
   p.eT = eT;
   p.rho = rho_p;
   p.ws = scratch;
-  p.obs = reinterpret_cast<c128*>(obs_);
-  p.snap = (save_every > 0) ? reinterpret_cast<c128*>(snap_) : nullptr;
+  p.obs = obs;
+  p.snap = (save_every > 0) ? snap : nullptr;
   p.N = N;
   p.Np = Np;
   p.nc = nc;
@@ -306,10 +366,87 @@ extern "C" int qd_lindblad_rk4(const qd_c128* H_, const qd_c128* C_, int nc, qd_
   QD_HIP(hipGetLastError());
 
   if (pad) {
-    const int threads = 256;
     const size_t tot = (size_t)B * N * N;
     const int pb = (int)std::min<size_t>((tot + threads - 1) / threads, 65535);
     hipLaunchKernelGGL(unpad_kernel, dim3(pb), dim3(threads), 0, st, rho_p, rho, B, N, Np);
+    QD_HIP(hipGetLastError());
+  }
+  return QD_OK;
+}
+
+int check_common(const char* fn, const void* rho, int B, int N, int nc, int ne, const void* E, const void* obs,
+                 int nsteps) {
+  QD_CHECK_ARG(rho, "%s: rho must be non-null", fn);
+  QD_CHECK_ARG(N >= 1 && N <= 1024, "%s: N=%d outside [1, 1024]", fn, N);
+  QD_CHECK_ARG(B >= 1, "%s: B=%d must be >= 1", fn, B);
+  QD_CHECK_ARG(nc >= 0 && nc <= MAX_NC, "%s: nc=%d outside [0, %d]", fn, nc, MAX_NC);
+  QD_CHECK_ARG(ne >= 0 && ne <= MAX_NE, "%s: ne=%d outside [0, %d]", fn, ne, MAX_NE);
+  QD_CHECK_ARG(ne == 0 || (E && obs), "%s: E/obs null but ne=%d", fn, ne);
+  QD_CHECK_ARG(nsteps >= 0, "%s: nsteps=%d < 0", fn, nsteps);
+  return QD_OK;
+}
+
+}  // namespace
+
+extern "C" int qd_lindblad_rk4(const qd_c128* H, const qd_c128* C, int nc, qd_c128* rho, int B, int N, double dt,
+                               int nsteps, const qd_c128* E, int ne, qd_c128* obs, qd_c128* snap, int save_every,
+                               void* stream) {
+  QD_CHECK_ARG(H && rho, "qd_lindblad_rk4: H and rho must be non-null");
+  int rc = check_common("qd_lindblad_rk4", rho, B, N, nc, ne, E, obs, nsteps);
+  if (rc) return rc;
+  QD_CHECK_ARG(nc == 0 || C, "qd_lindblad_rk4: C is null but nc=%d", nc);
+  return glf_run(GLF_FROM_LINDBLAD, (const c128*)H, (const c128*)C, nullptr, nullptr, nullptr, nullptr, nc,
+                 (c128*)rho, B, N, dt, nsteps, (const c128*)E, ne, (c128*)obs, (c128*)snap, save_every,
+                 (hipStream_t)stream);
+}
+
+extern "C" int qd_glf_rk4(const qd_c128* P, const qd_c128* Q, const qd_c128* L, const qd_c128* R, int npairs,
+                          qd_c128* rho, int B, int N, double dt, int nsteps, const qd_c128* E, int ne, qd_c128* obs,
+                          qd_c128* snap, int save_every, void* stream) {
+  QD_CHECK_ARG(P && Q && rho, "qd_glf_rk4: P, Q and rho must be non-null");
+  int rc = check_common("qd_glf_rk4", rho, B, N, npairs, ne, E, obs, nsteps);
+  if (rc) return rc;
+  QD_CHECK_ARG(npairs == 0 || (L && R), "qd_glf_rk4: L/R null but npairs=%d", npairs);
+  return glf_run(GLF_FROM_OPERATORS, nullptr, nullptr, (const c128*)P, (const c128*)Q, (const c128*)L,
+                 (const c128*)R, npairs, (c128*)rho, B, N, dt, nsteps, (const c128*)E, ne, (c128*)obs, (c128*)snap,
+                 save_every, (hipStream_t)stream);
+}
+
+extern "C" int qd_basis_transform(const qd_c128* V, qd_c128* A_, int B, int N, int mode, void* stream) {
+  QD_CHECK_ARG(V && A_, "qd_basis_transform: null pointer");
+  QD_CHECK_ARG(N >= 1 && N <= 1024 && B >= 1, "qd_basis_transform: bad sizes N=%d B=%d", N, B);
+  QD_CHECK_ARG(mode == 0 || mode == 1, "qd_basis_transform: mode must be 0 or 1");
+  hipStream_t st = (hipStream_t)stream;
+  const int Np = padded_dim(N);
+  const size_t NN = (size_t)Np * Np;
+  const bool pad = Np != N;
+  void* w = nullptr;
+  int rc = workspace(WS_MISC, (2 * NN + (size_t)B * NN * (pad ? 2 : 1)) * sizeof(c128), &w);
+  if (rc) return rc;
+  c128* Vl = (c128*)w;
+  c128* Vr = Vl + NN;
+  c128* T = Vr + NN;
+  c128* A = (c128*)A_;
+  c128* Ap = pad ? T + (size_t)B * NN : A;
+  const int threads = 256;
+  hipLaunchKernelGGL(transform_prep_kernel, dim3((int)std::min<size_t>((NN + 255) / 256, 4096)), dim3(threads), 0, st,
+                     (const c128*)V, N, Np, mode, Vl, Vr);
+  QD_HIP(hipGetLastError());
+  if (pad) {
+    hipLaunchKernelGGL(pad_kernel, dim3((int)std::min<size_t>((B * NN + 255) / 256, 65535)), dim3(threads), 0, st, A,
+                       Ap, B, N, Np);
+    QD_HIP(hipGetLastError());
+  }
+  if (Np == 32)
+    hipLaunchKernelGGL(basis_transform_kernel<32>, dim3(B), dim3(CG_WG), 0, st, Vl, Vr, Ap, T, Np);
+  else if (Np == 64)
+    hipLaunchKernelGGL(basis_transform_kernel<64>, dim3(B), dim3(CG_WG), 0, st, Vl, Vr, Ap, T, Np);
+  else
+    hipLaunchKernelGGL(basis_transform_kernel<128>, dim3(B), dim3(CG_WG), 0, st, Vl, Vr, Ap, T, Np);
+  QD_HIP(hipGetLastError());
+  if (pad) {
+    hipLaunchKernelGGL(unpad_kernel, dim3((int)std::min<size_t>(((size_t)B * N * N + 255) / 256, 65535)),
+                       dim3(threads), 0, st, Ap, A, B, N, Np);
     QD_HIP(hipGetLastError());
   }
   return QD_OK;

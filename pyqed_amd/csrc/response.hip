@@ -1,0 +1,240 @@
+// response.hip — Liouville-space response functions on the (t1, t2, t3) grid.
+//
+// Eigen (sum-over-states) form of the reference's SOS propagator
+// (pyqed/oqs.py:160-214: eig(R), U = U1 diag(e^{lam t}) U1^-1, G = -iU) and of
+// correlation_4op_3t (oqs.py:268-357):
+//   S[i,j,k] = <<I| a G(tau_i) b G(tau_j) c G(tau_k) d |rho0>>
+//            = (-i)^3 sum_pqr alpha_p e^{lam_p tau_i} B_pq e^{lam_q tau_j} C_qr e^{lam_r tau_k} beta_r
+// with alpha = I^T a U1, B = U1^-1 b U1, C = U1^-1 c U1, beta = U1^-1 d rho0
+// (host-side setup, like the reference's eig).  Kernels:
+//   qd_sos_propagator     U[a][b][k]                  (oqs.py:210 contraction)
+//   qd_response_cube      S[i][j][k], full n^3 cube   (oqs.py:339-357 tensordots)
+//   qd_response2d_ensemble  sum over M disorder members of the (t3, t1) slice at
+//                         fixed t2 — one complex GEMM
+//                           S = X [n3 x K] * Z [K x n1],  K = M * nL,
+//                           X[i][m*nL+p] = i * alpha_mp e^{lam_mp t3_i}
+//                           Z[m*nL+p][k] = sum_q Mt_mpq beta_mq e^{lam_mq t1_k},
+//                           Mt_m = B_m diag(e^{lam_m t2}) C_m  (host)
+//                         run split-K over workgroups on the MFMA block engine
+//                         with a deterministic slab reduction.
+#include "cgemm_block.hpp"
+
+namespace qd {
+namespace {
+
+__device__ __forceinline__ c128 cexp_t(c128 lam, double t) {
+  // exp(lam * t) for real t, numpy's formula exp(re)*(cos im, sin im)
+  const double er = exp(lam.re * t);
+  double s, c;
+  sincos(lam.im * t, &s, &c);
+  return cmk(er * c, er * s);
+}
+
+__global__ void sos_propagator_kernel(const c128* U1, const c128* U2, const c128* lam, int nL, const double* t, int nt,
+                                      c128* U) {
+  const size_t tot = (size_t)nL * nL * nt;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    const int k = (int)(e % nt);
+    const int b = (int)((e / nt) % nL);
+    const int a = (int)(e / ((size_t)nt * nL));
+    const double tk = t[k];
+    c128 s = cmk(0, 0);
+    for (int j = 0; j < nL; ++j) s = cadd(s, cmul(cmul(U1[(size_t)a * nL + j], cexp_t(lam[j], tk)), U2[(size_t)j * nL + b]));
+    U[e] = s;
+  }
+}
+
+// Y[k][q] = sum_r C[q][r] e^{lam_r t1_k} beta_r
+__global__ void cube_y_kernel(const c128* C, const c128* beta, const c128* lam, int nL, const double* t1, int n1,
+                              c128* Y) {
+  const size_t tot = (size_t)n1 * nL;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    const int q = (int)(e % nL), k = (int)(e / nL);
+    c128 s = cmk(0, 0);
+    for (int r = 0; r < nL; ++r) s = cadd(s, cmul(C[(size_t)q * nL + r], cmul(cexp_t(lam[r], t1[k]), beta[r])));
+    Y[e] = s;
+  }
+}
+
+// W[j][p][k] = sum_q B[p][q] e^{lam_q t2_j} Y[k][q]
+__global__ void cube_w_kernel(const c128* B, const c128* Y, const c128* lam, int nL, const double* t2, int n2, int n1,
+                              c128* W) {
+  const size_t tot = (size_t)n2 * nL * n1;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    const int k = (int)(e % n1);
+    const int p = (int)((e / n1) % nL);
+    const int j = (int)(e / ((size_t)n1 * nL));
+    c128 s = cmk(0, 0);
+    for (int q = 0; q < nL; ++q)
+      s = cadd(s, cmul(cmul(B[(size_t)p * nL + q], cexp_t(lam[q], t2[j])), Y[(size_t)k * nL + q]));
+    W[e] = s;
+  }
+}
+
+// out[i][j][k] = i * sum_p alpha_p e^{lam_p t3_i} W[j][p][k]      ((-i)^3 = i)
+// One block per (i, j) row; the p-loop coefficients are staged in LDS.
+__global__ void cube_out_kernel(const c128* alpha, const c128* lam, const c128* W, int nL, const double* t3, int n3,
+                                int n2, int n1, c128* out) {
+  extern __shared__ c128 xs[];
+  const int ij = blockIdx.x;
+  const int i = ij / n2, j = ij % n2;
+  for (int p = threadIdx.x; p < nL; p += blockDim.x) xs[p] = cmuli(cmul(alpha[p], cexp_t(lam[p], t3[i])));
+  __syncthreads();
+  const c128* Wj = W + (size_t)j * nL * n1;
+  c128* o = out + ((size_t)i * n2 + j) * n1;
+  for (int k = threadIdx.x; k < n1; k += blockDim.x) {
+    c128 s = cmk(0, 0);
+    for (int p = 0; p < nL; ++p) s = cadd(s, cmul(xs[p], Wj[(size_t)p * n1 + k]));
+    o[k] = s;
+  }
+}
+
+// ---------------------------------------------------------------- ensemble 2D slice
+// X [n3p][Kp]: X[i][m*nL+p] = i * alpha_mp e^{lam_mp t3_i}  (zero in the padding)
+__global__ void ens_x_kernel(const c128* alpha, const c128* lam, int M, int nL, const double* t3, int n3, int n3p,
+                             int Kp, c128* X) {
+  const size_t tot = (size_t)n3p * Kp;
+  const int K = M * nL;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    const int kk = (int)(e % Kp), i = (int)(e / Kp);
+    c128 v = cmk(0, 0);
+    if (i < n3 && kk < K) v = cmuli(cmul(alpha[kk], cexp_t(lam[kk], t3[i])));
+    X[e] = v;
+  }
+}
+
+// Z [Kp][n1p]: Z[m*nL+p][k] = sum_q Mt[m][p][q] beta[m][q] e^{lam_mq t1_k}
+__global__ void ens_z_kernel(const c128* Mt, const c128* beta, const c128* lam, int M, int nL, const double* t1,
+                             int n1, int n1p, int Kp, c128* Z) {
+  const size_t tot = (size_t)Kp * n1p;
+  const int K = M * nL;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    const int k = (int)(e % n1p), row = (int)(e / n1p);
+    c128 v = cmk(0, 0);
+    if (row < K && k < n1) {
+      const int m = row / nL, p = row % nL;
+      const c128* Mr = Mt + ((size_t)m * nL + p) * nL;
+      const c128* bm = beta + (size_t)m * nL;
+      const c128* lm = lam + (size_t)m * nL;
+      const double tk = t1[k];
+      for (int q = 0; q < nL; ++q) v = cadd(v, cmul(Mr[q], cmul(bm[q], cexp_t(lm[q], tk))));
+    }
+    Z[e] = v;
+  }
+}
+
+constexpr int ENS_BT = 128;
+
+// grid: (n1p/BT) x (n3p/BT) x S ; each workgroup accumulates K-tiles [t0, t1) of its block
+__global__ __launch_bounds__(CG_WG) void ens_gemm_kernel(const c128* X, const c128* Z, int Kp, int n1p, int tiles,
+                                                         int S, c128* slabs, int n3p) {
+  __shared__ CgLds<ENS_BT> L;
+  const int bn = blockIdx.x, bm = blockIdx.y, s = blockIdx.z;
+  const int t0 = (int)((long)tiles * s / S), t1 = (int)((long)tiles * (s + 1) / S);
+  CgAcc<ENS_BT> A;
+  CgSeg seg;
+  seg.A = X + (size_t)bm * ENS_BT * Kp + (size_t)t0 * CG_KT;
+  seg.B = Z + (size_t)t0 * CG_KT * n1p + (size_t)bn * ENS_BT;
+  c128* slab = slabs + (size_t)s * n3p * n1p;
+  if (t1 > t0) {
+    cg_block_gemm<ENS_BT>(&seg, 1, (t1 - t0) * CG_KT, Kp, n1p, L, A);
+    cg_epilogue<ENS_BT>(A, [&](int row, int col, c128 v) {
+      slab[(size_t)(bm * ENS_BT + row) * n1p + bn * ENS_BT + col] = v;
+    });
+  } else {
+    for (int e = threadIdx.x; e < ENS_BT * ENS_BT; e += CG_WG)
+      slab[(size_t)(bm * ENS_BT + e / ENS_BT) * n1p + bn * ENS_BT + e % ENS_BT] = cmk(0, 0);
+  }
+}
+
+// out[i][k] (+)= sum_s slab[s][i][k], fixed order -> deterministic
+__global__ void ens_reduce_kernel(const c128* slabs, int S, int n3, int n1, int n3p, int n1p, c128* out,
+                                  int accumulate) {
+  const size_t tot = (size_t)n3 * n1;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(e / n1), k = (int)(e % n1);
+    c128 v = accumulate ? out[e] : cmk(0, 0);
+    for (int s = 0; s < S; ++s) v = cadd(v, slabs[((size_t)s * n3p + i) * n1p + k]);
+    out[e] = v;
+  }
+}
+
+int grid_for(size_t n, int threads) { return (int)std::min<size_t>((n + threads - 1) / threads, 16384); }
+
+}  // namespace
+}  // namespace qd
+
+using namespace qd;
+
+extern "C" int qd_sos_propagator(const qd_c128* U1, const qd_c128* U2, const qd_c128* lam, int nL, const double* t,
+                                 int nt, qd_c128* U, void* stream) {
+  QD_CHECK_ARG(U1 && U2 && lam && t && U, "qd_sos_propagator: null pointer");
+  QD_CHECK_ARG(nL >= 1 && nt >= 1, "qd_sos_propagator: nL=%d nt=%d must be >= 1", nL, nt);
+  const size_t tot = (size_t)nL * nL * nt;
+  hipLaunchKernelGGL(sos_propagator_kernel, dim3(grid_for(tot, 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const c128*)U1, (const c128*)U2, (const c128*)lam, nL, t, nt, (c128*)U);
+  QD_HIP(hipGetLastError());
+  return QD_OK;
+}
+
+extern "C" int qd_response_cube(const qd_c128* alpha, const qd_c128* B, const qd_c128* C, const qd_c128* beta,
+                                const qd_c128* lam, int nL, const double* t3, int n3, const double* t2, int n2,
+                                const double* t1, int n1, qd_c128* out, void* stream) {
+  QD_CHECK_ARG(alpha && B && C && beta && lam && t3 && t2 && t1 && out, "qd_response_cube: null pointer");
+  QD_CHECK_ARG(nL >= 1 && nL <= 4096 && n3 >= 1 && n2 >= 1 && n1 >= 1, "qd_response_cube: bad sizes");
+  hipStream_t st = (hipStream_t)stream;
+  void* w = nullptr;
+  const size_t ny = (size_t)n1 * nL, nw = (size_t)n2 * nL * n1;
+  int rc = workspace(WS_2DES, (ny + nw) * sizeof(c128), &w);
+  if (rc) return rc;
+  c128* Y = (c128*)w;
+  c128* W = Y + ny;
+  hipLaunchKernelGGL(cube_y_kernel, dim3(grid_for(ny, 256)), dim3(256), 0, st, (const c128*)C, (const c128*)beta,
+                     (const c128*)lam, nL, t1, n1, Y);
+  QD_HIP(hipGetLastError());
+  hipLaunchKernelGGL(cube_w_kernel, dim3(grid_for(nw, 256)), dim3(256), 0, st, (const c128*)B, Y, (const c128*)lam,
+                     nL, t2, n2, n1, W);
+  QD_HIP(hipGetLastError());
+  QD_CHECK_ARG((size_t)n3 * n2 < (1u << 31), "qd_response_cube: n3*n2 too large");
+  hipLaunchKernelGGL(cube_out_kernel, dim3(n3 * n2), dim3(256), nL * sizeof(c128), st, (const c128*)alpha,
+                     (const c128*)lam, W, nL, t3, n3, n2, n1, (c128*)out);
+  QD_HIP(hipGetLastError());
+  return QD_OK;
+}
+
+extern "C" int qd_response2d_ensemble(const qd_c128* alpha, const qd_c128* Mt, const qd_c128* beta,
+                                      const qd_c128* lam, int M, int nL, const double* t3, int n3, const double* t1,
+                                      int n1, qd_c128* out, int accumulate, void* stream) {
+  QD_CHECK_ARG(alpha && Mt && beta && lam && t3 && t1 && out, "qd_response2d_ensemble: null pointer");
+  QD_CHECK_ARG(M >= 1 && nL >= 1 && n3 >= 1 && n1 >= 1, "qd_response2d_ensemble: bad sizes");
+  QD_CHECK_ARG((long)M * nL < (1L << 30), "qd_response2d_ensemble: M*nL too large");
+  hipStream_t st = (hipStream_t)stream;
+  const int BT = ENS_BT;
+  const int n3p = ceil_div(n3, BT) * BT, n1p = ceil_div(n1, BT) * BT;
+  const int K = M * nL;
+  const int tiles = ceil_div(K, CG_KT);
+  const int Kp = tiles * CG_KT;
+  const int blocks2d = (n3p / BT) * (n1p / BT);
+  // split K so that the grid covers >= 256 CUs, with >= 4 K-tiles per workgroup
+  int S = std::max(1, std::min(ceil_div(512, blocks2d), std::max(1, tiles / 4)));
+  const size_t nx = (size_t)n3p * Kp, nz = (size_t)Kp * n1p, nsl = (size_t)S * n3p * n1p;
+  void* w = nullptr;
+  int rc = workspace(WS_2DES, (nx + nz + nsl) * sizeof(c128), &w);
+  if (rc) return rc;
+  c128* X = (c128*)w;
+  c128* Z = X + nx;
+  c128* slabs = Z + nz;
+  hipLaunchKernelGGL(ens_x_kernel, dim3(grid_for(nx, 256)), dim3(256), 0, st, (const c128*)alpha, (const c128*)lam, M,
+                     nL, t3, n3, n3p, Kp, X);
+  QD_HIP(hipGetLastError());
+  hipLaunchKernelGGL(ens_z_kernel, dim3(grid_for(nz, 256)), dim3(256), 0, st, (const c128*)Mt, (const c128*)beta,
+                     (const c128*)lam, M, nL, t1, n1, n1p, Kp, Z);
+  QD_HIP(hipGetLastError());
+  hipLaunchKernelGGL(ens_gemm_kernel, dim3(n1p / BT, n3p / BT, S), dim3(CG_WG), 0, st, X, Z, Kp, n1p, tiles, S, slabs,
+                     n3p);
+  QD_HIP(hipGetLastError());
+  hipLaunchKernelGGL(ens_reduce_kernel, dim3(grid_for((size_t)n3 * n1, 256)), dim3(256), 0, st, slabs, S, n3, n1, n3p,
+                     n1p, (c128*)out, accumulate);
+  QD_HIP(hipGetLastError());
+  return QD_OK;
+}

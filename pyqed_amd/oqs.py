@@ -113,7 +113,7 @@ def _lindblad(H, rho0, c_ops, e_ops=None, Nt=1, t0=0, dt=0.005, return_result=Tr
     Hd = torch.from_numpy(np.ascontiguousarray(Hn)).to(dev)
     Cd = stack_ops(c_ops, N, dev)
     Ed = stack_ops(e_ops, N, dev)
-    rho = to_device(rho0, dev).reshape(1, N, N).contiguous()
+    rho = to_device(rho0, dev).reshape(1, N, N).clone()
     obs, snap = lindblad_rk4(Hd, Cd, rho, dt, Nt, Ed, save_every=1 if return_states else 0)
     torch.cuda.synchronize(dev)
 
@@ -129,3 +129,190 @@ def _lindblad(H, rho0, c_ops, e_ops=None, Nt=1, t0=0, dt=0.005, return_result=Tr
         result.rholist = []
     result.rho = rho[0].cpu().numpy()
     return result
+
+
+# --------------------------------------------------------------------------- GLF
+def glf_rk4(P, Q, L, R, rho, dt, nsteps, e_ops=None, save_every=0, stream=None):
+    """d rho/dt = P rho + rho Q + sum_c L_c rho R_c, batched RK4 on the GPU (qd_glf_rk4).
+
+    P, Q [N,N]; L, R [npairs,N,N] or None; rho [B,N,N] in place; e_ops [ne,N,N] or None."""
+    B, N = rho.shape[0], rho.shape[-1]
+    dev = rho.device
+    _lib.ensure_device(dev)
+    for name, t in (("P", P), ("Q", Q), ("rho", rho), ("L", L), ("R", R), ("e_ops", e_ops)):
+        if t is not None and (t.dtype != torch.complex128 or t.device != dev or not t.is_contiguous()):
+            raise ValueError(f"{name} must be a contiguous complex128 tensor on {dev}")
+    if rho.dim() != 3 or rho.shape[1] != N:
+        raise ValueError(f"rho must be [B,N,N], got {tuple(rho.shape)}")
+    npairs = 0 if L is None else L.shape[0]
+    ne = 0 if e_ops is None else e_ops.shape[0]
+    obs = torch.empty((B, nsteps + 1, ne), dtype=torch.complex128, device=dev) if ne else None
+    nsave = nsteps // save_every if save_every > 0 else 0
+    snap = torch.empty((B, nsave, N, N), dtype=torch.complex128, device=dev) if nsave else None
+    st = stream if stream is not None else _lib.stream_ptr(dev)
+    with torch.cuda.device(dev):
+        rc = _lib.load().qd_glf_rk4(_lib.ptr(P), _lib.ptr(Q), _lib.ptr(L), _lib.ptr(R), npairs, _lib.ptr(rho), B, N,
+                                    float(dt), int(nsteps), _lib.ptr(e_ops), ne, _lib.ptr(obs), _lib.ptr(snap),
+                                    int(save_every if nsave else 0), st)
+    _lib.check(rc, "qd_glf_rk4")
+    return obs, snap
+
+
+def basis_transform(V: torch.Tensor, A: torch.Tensor, inverse=False):
+    """In place: A <- V^+ A V (inverse=False, phys.transform) or V A V^+ (inverse=True). A [B,N,N]."""
+    dev = A.device
+    _lib.ensure_device(dev)
+    B, N = A.shape[0], A.shape[-1]
+    with torch.cuda.device(dev):
+        rc = _lib.load().qd_basis_transform(_lib.ptr(V), _lib.ptr(A), B, N, int(bool(inverse)), _lib.stream_ptr(dev))
+    _lib.check(rc, "qd_basis_transform")
+    return A
+
+
+def _isherm(a):
+    return np.allclose(a, a.conj().T)
+
+
+class RedfieldSolver:
+    """Drop-in for pyqed.oqs.RedfieldSolver (oqs.py:30-357).
+
+    redfield_tensor() returns the reference's csr R (built on the host, as the
+    reference does); evolve() propagates in the H eigenbasis on the GPU with the
+    commutator ("GLF") form of the same generator instead of R.vec(rho)."""
+
+    def __init__(self, H, c_ops=None, spectra=None, e_ops=None):
+        self.H = H
+        self.c_ops = c_ops
+        self.R = None
+        self.spectra = spectra
+        self.evecs = None
+        self.dim = H.shape[0]
+        self.U = None
+        self.G = None
+        self.e_ops = e_ops
+        self._glf = None
+        self._sos = None
+
+    def idm(self, sp=True):
+        from scipy.sparse import identity
+        from .superoperator import dm2vec
+        if sp:
+            return dm2vec(identity(self.dim))
+        return dm2vec(identity(self.dim).toarray())
+
+    def configure(self, H, c_ops, e_ops):
+        self.c_ops = c_ops
+        self.e_ops = e_ops
+        self.H = H
+
+    # ---- setup (host): eigenbasis, spectra, Lambda operators (oqs.py:519-560)
+    def _prepare(self):
+        if self._glf is not None:
+            return self._glf
+        if self.spectra is None:
+            raise TypeError('Specify the bath spectral function.')
+        a_ops = self.c_ops or []
+        for a in a_ops:
+            if not _isherm(to_numpy(a)):
+                raise TypeError("Operators in a_ops must be Hermitian.")
+        from scipy.linalg import eigh
+        evals, evecs = eigh(to_numpy(self.H))
+        W = np.real(evals[:, None] - evals[None, :])
+        N = len(evals)
+        A, Lam = [], []
+        for k, a in enumerate(a_ops):
+            c = np.zeros((N, N))
+            for n in range(N):
+                for m in range(N):
+                    c[n, m] = self.spectra[k](-W[n, m])
+            Ak = evecs.conj().T @ to_numpy(a, np.complex128) @ evecs
+            A.append(Ak)
+            Lam.append(c * Ak)
+        self._glf = (evals, evecs, A, Lam)
+        self.evecs = evecs
+        return self._glf
+
+    def redfield_tensor(self, secular=False):
+        """(R csr (N^2, N^2) with -i included, evecs) as oqs.py:519-570."""
+        from scipy.sparse import csr_matrix as _csr
+        from .superoperator import left, op2sop, right
+        evals, evecs, A, Lam = self._prepare()
+        R = 0
+        for a, l in zip(A, Lam):
+            R = R + op2sop(a).dot(left(l) - right(l.conj().T))
+        R = _csr(-1j * op2sop(np.diag(evals)) - R)
+        self.R = R
+        self.evecs = evecs
+        return R, evecs
+
+    def glf_terms(self):
+        """(P, Q, L[], R[]) of d rho~/dt = P rho~ + rho~ Q + sum L rho~ R in the eigenbasis."""
+        evals, evecs, A, Lam = self._prepare()
+        E = np.diag(evals).astype(complex)
+        P = -1j * E
+        Q = 1j * E
+        Ls, Rs = [], []
+        for a, l in zip(A, Lam):
+            ld = l.conj().T
+            P = P - a @ l
+            Q = Q - ld @ a
+            Ls += [a, l]
+            Rs += [ld, a]
+        return P, Q, Ls, Rs
+
+    def evolve(self, rho0, dt, Nt, evecs=None, e_ops=[], store_states=False, t0=0, nout=1):
+        """oqs.py:57-81 -> _redfield (oqs.py:364-459): observables (Nt, n_e) EXCLUDING t0,
+        rholist (Nt) back-transformed to the original basis."""
+        self._prepare()
+        dev = default_device()
+        P, Q, Ls, Rs = self.glf_terms()
+        N = self.dim
+        evecs_t = torch.from_numpy(np.ascontiguousarray(self.evecs.astype(complex))).to(dev)
+        rho = to_device(rho0, dev).reshape(1, N, N).clone()
+        basis_transform(evecs_t, rho, inverse=False)
+        e_ops = e_ops or []
+        Ed = stack_ops(e_ops, N, dev)
+        if Ed is not None:
+            basis_transform(evecs_t, Ed, inverse=False)
+        Pd, Qd = (torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (P, Q))
+        Ld = stack_ops(Ls, N, dev)
+        Rd = stack_ops(Rs, N, dev)
+        rho0_eb = rho[0].cpu().numpy()
+        obs, snap = glf_rk4(Pd, Qd, Ld, Rd, rho, dt, Nt, Ed, save_every=1)
+        result = Result(dt=dt, Nt=Nt, rho0=rho0_eb)
+        result.observables = obs[0, 1:].cpu().numpy() if obs is not None else np.zeros((Nt, 0), complex)
+        if snap is not None:
+            back = snap[0].contiguous()
+            basis_transform(evecs_t, back, inverse=True)
+            host = back.cpu().numpy()
+            result.rholist = [host[k] for k in range(Nt)]
+        else:
+            result.rholist = []
+        torch.cuda.synchronize(dev)
+        return result
+
+    # ---- Liouville-space Green's functions (eigen / SOS form)
+    def propagator(self, t, method='SOS'):
+        """oqs.py:160-214 (SOS): U (nL, nL, nt) on the GPU; G = -1j U."""
+        if self.R is None:
+            raise TypeError('Redfield tensor is not computed. Please call redfield_tensor()')
+        if method not in ['eseries', 'SOS']:
+            raise NotImplementedError(f"propagator method {method!r}: only 'SOS'/'eseries' run on the GPU")
+        from .response import sos_eig, sos_propagator
+        lam, U1, U2 = sos_eig(self.R)
+        t = np.asarray(t, dtype=float)
+        self._sos = (lam, U1, U2, t)
+        self.U = sos_propagator(lam, U1, U2, t).cpu().numpy()
+        self.G = -1j * self.U
+        return self.U
+
+    def correlation_4op_3t(self, rho0, oplist, signature, tau):
+        """<<I|A G(tau3) B G(tau2) C G(tau1) D|rho0>> cube [i=tau3, j=tau2, k=tau1] (oqs.py:268-357)."""
+        if len(oplist) != 4:
+            raise ValueError('Number of operators is not 4.')
+        if self.G is None:
+            self.propagator(tau)
+        from .response import eigen_factors, response_cube
+        lam, U1, U2, tG = self._sos
+        alpha, B, C, beta = eigen_factors(lam, U1, U2, oplist, signature, rho0)
+        return response_cube(lam, alpha, B, C, beta, tG, tG, tG).cpu().numpy()

@@ -1,0 +1,126 @@
+"""Third-order response / 2DES on the GPU (eigen form of the reference's
+RedfieldSolver.propagator + correlation_4op_3t, pyqed/oqs.py:160-357).
+
+Setup (host, like the reference): eig of the Liouvillian/Redfield tensor and
+the O(nL^3) basis changes of the four superoperators.  Grid evaluation (the
+O(n^2 nL) / O(n^3 nL) part) runs in libqdyn.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+from scipy.linalg import eig, inv
+
+from . import _lib
+from ._util import default_device
+from .superoperator import operator_to_superoperator
+
+
+def _t(a, dev, dtype=torch.complex128):
+    return torch.from_numpy(np.ascontiguousarray(np.asarray(a))).to(device=dev, dtype=dtype)
+
+
+def sos_eig(R):
+    """eig of the (dense) generator and its inverse eigenvector matrix (oqs.py:196-200)."""
+    R = R.toarray() if hasattr(R, "toarray") else np.asarray(R)
+    lam, U1 = eig(R)
+    return lam, U1, inv(U1)
+
+
+def sos_propagator(lam, U1, U2, t, device=None):
+    """U[a, b, k] = sum_j U1[a,j] e^{lam_j t_k} U2[j,b] on the GPU (oqs.py:205-210)."""
+    dev = device or default_device()
+    _lib.ensure_device(dev)
+    nL = len(lam)
+    t = np.asarray(t, dtype=float)
+    U = torch.empty((nL, nL, len(t)), dtype=torch.complex128, device=dev)
+    lamt, U1t, U2t = _t(lam, dev), _t(U1, dev), _t(U2, dev)
+    tt = _t(t, dev, torch.float64)
+    with torch.cuda.device(dev):
+        rc = _lib.load().qd_sos_propagator(U1t.data_ptr(), U2t.data_ptr(), lamt.data_ptr(), nL, tt.data_ptr(),
+                                           len(t), U.data_ptr(), _lib.stream_ptr(dev))
+    _lib.check(rc, "qd_sos_propagator")
+    return U
+
+
+def eigen_factors(lam, U1, U2, oplist, signature, rho0):
+    """alpha = I^T a U1, B = U2 b U1, C = U2 c U1, beta = U2 d vec(rho0)."""
+    a, b, c, d = [operator_to_superoperator(op, s).toarray() for op, s in zip(oplist, signature)]
+    rho0 = rho0.toarray() if hasattr(rho0, "toarray") else np.asarray(rho0)
+    N = rho0.shape[0]
+    idm = np.identity(N).flatten()
+    alpha = (idm @ a) @ U1
+    B = U2 @ b @ U1
+    C = U2 @ c @ U1
+    beta = U2 @ (d @ rho0.flatten())
+    return alpha, B, C, beta
+
+
+def response_cube(lam, alpha, B, C, beta, t3, t2, t1, device=None):
+    """S[i, j, k] over (t3_i, t2_j, t1_k) on the GPU (oqs.py:327-357)."""
+    dev = device or default_device()
+    _lib.ensure_device(dev)
+    nL = len(lam)
+    t3, t2, t1 = (np.asarray(x, dtype=float) for x in (t3, t2, t1))
+    out = torch.empty((len(t3), len(t2), len(t1)), dtype=torch.complex128, device=dev)
+    args = [_t(x, dev) for x in (alpha, B, C, beta, lam)]
+    ts = [_t(x, dev, torch.float64) for x in (t3, t2, t1)]
+    with torch.cuda.device(dev):
+        rc = _lib.load().qd_response_cube(*(x.data_ptr() for x in args), nL, ts[0].data_ptr(), len(t3),
+                                          ts[1].data_ptr(), len(t2), ts[2].data_ptr(), len(t1), out.data_ptr(),
+                                          _lib.stream_ptr(dev))
+    _lib.check(rc, "qd_response_cube")
+    return out
+
+
+def ensemble_factors(lam, U1, U2, supops, rho0v, t2):
+    """Batched eigen factors for M members: lam/U1/U2 [M, nL(, nL)], supops (a, b, c, d) [M, nL, nL]
+    or shared [nL, nL]; returns alpha [M,nL], Mt [M,nL,nL] = B diag(e^{lam t2}) C, beta [M,nL]."""
+    a, b, c, d = [np.broadcast_to(x, U1.shape) for x in supops]
+    nL = U1.shape[-1]
+    N = int(round(np.sqrt(nL)))
+    idm = np.identity(N).flatten()
+    alpha = np.einsum("a,mab,mbp->mp", idm, a, U1)
+    Bm = U2 @ b @ U1
+    Cm = U2 @ c @ U1
+    Mt = Bm @ (np.exp(lam * t2)[:, :, None] * Cm)
+    beta = np.einsum("mpa,mab,b->mp", U2, d, rho0v)
+    return alpha, Mt, beta
+
+
+def response2d_ensemble(lam, alpha, Mt, beta, t3, t1, out=None, accumulate=False, device=None):
+    """out[i, k] (+)= sum_m (t3_i, t1_k) slice of member m at fixed t2 (GPU, split-K MFMA GEMM).
+
+    lam, alpha, beta [M, nL], Mt [M, nL, nL] (numpy or device tensors)."""
+    dev = device or (out.device if out is not None else default_device())
+    _lib.ensure_device(dev)
+    lam_t, alpha_t, Mt_t, beta_t = (x if isinstance(x, torch.Tensor) else _t(x, dev) for x in (lam, alpha, Mt, beta))
+    M, nL = alpha_t.shape
+    t3t = t3 if isinstance(t3, torch.Tensor) else _t(np.asarray(t3, float), dev, torch.float64)
+    t1t = t1 if isinstance(t1, torch.Tensor) else _t(np.asarray(t1, float), dev, torch.float64)
+    if out is None:
+        out = torch.empty((t3t.numel(), t1t.numel()), dtype=torch.complex128, device=dev)
+        accumulate = False
+    with torch.cuda.device(dev):
+        rc = _lib.load().qd_response2d_ensemble(alpha_t.data_ptr(), Mt_t.data_ptr(), beta_t.data_ptr(),
+                                                lam_t.data_ptr(), M, nL, t3t.data_ptr(), t3t.numel(),
+                                                t1t.data_ptr(), t1t.numel(), out.data_ptr(), int(bool(accumulate)),
+                                                _lib.stream_ptr(dev))
+    _lib.check(rc, "qd_response2d_ensemble")
+    return out
+
+
+def redfield_superop_batch(E, a_op, spec_vals):
+    """Vectorised redfield_tensor (oqs.py:519-570) for M diagonal Hamiltonians E [M, N] sharing one
+    Hermitian a_op already in the (shared, identity) eigenbasis; spec_vals [M, N, N] = S(-W).
+    Returns R [M, N^2, N^2].  Used to build disorder ensembles (setup)."""
+    M, N = E.shape
+    I = np.identity(N)
+    A = np.asarray(a_op, complex)
+    R = np.empty((M, N * N, N * N), dtype=complex)
+    opA = np.kron(A, I) - np.kron(I, A.T)
+    for m in range(M):
+        Lm = spec_vals[m] * A
+        R[m] = -1j * (np.kron(np.diag(E[m]), I) - np.kron(I, np.diag(E[m]))) \
+            - opA @ (np.kron(Lm, I) - np.kron(I, Lm.conj()))
+    return R

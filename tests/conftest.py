@@ -30,3 +30,10 @@ def relerr(a, b):
     b = np.asarray(b)
     den = max(np.linalg.norm(b.ravel()), 1e-300)
     return np.linalg.norm((a - b).ravel()) / den
+
+
+# spectral functions used by the Redfield golden vectors (tests/golden/make_golden.py SPECTRA)
+SPECTRA = {
+    "flat005": lambda w: 0.05,
+    "tanh": lambda w: 0.02 * (1.0 + np.tanh(2.0 * w)),
+}

@@ -88,6 +88,99 @@ def lindblad_n128():
     _lindblad_case("lindblad_n128", N=128, nc=1, ne=1, Nt=3, dt=1e-3, seed=14, keep_all=False)
 
 
+# ----------------------------------------------------------------- Redfield / 2DES
+# Spectral functions by name (tests/conftest.py SPECTRA holds the same definitions).
+SPECTRA = {
+    "flat005": lambda w: 0.05,
+    "tanh": lambda w: 0.02 * (1.0 + np.tanh(2.0 * w)),
+}
+
+
+def _redfield_case(name, N, nk, Nt, dt, seed, spectrum):
+    import pyqed.oqs as oqs
+    rng = np.random.default_rng(seed)
+    H = _herm(rng, N)
+    a_ops = [_herm(rng, N, 0.5) for _ in range(nk)]
+    E = np.array([_herm(rng, N) for _ in range(2)])
+    psi = rng.standard_normal(N) + 1j * rng.standard_normal(N)
+    psi /= np.linalg.norm(psi)
+    rho0 = np.outer(psi, psi.conj())
+    sol = oqs.RedfieldSolver(H, c_ops=a_ops, spectra=[SPECTRA[spectrum]] * nk)
+    R, evecs = sol.redfield_tensor()
+    r = sol.evolve(rho0, dt=dt, Nt=Nt, e_ops=list(E))
+    save(name, H=H, a_ops=np.array(a_ops), E=E, rho0=rho0, dt=dt, Nt=Nt, spectrum=spectrum,
+         R=R.toarray(), evecs=evecs, observables=r.observables, rholist=np.array(r.rholist))
+
+
+@golden
+def redfield_n4():
+    _redfield_case("redfield_n4", N=4, nk=1, Nt=10, dt=0.05, seed=21, spectrum="tanh")
+
+
+@golden
+def redfield_n6_k2():
+    _redfield_case("redfield_n6_k2", N=6, nk=2, Nt=8, dt=0.02, seed=22, spectrum="flat005")
+
+
+def _three_level(E=(0.0, 1.0, 1.5)):
+    N = 3
+    H = np.diag(np.asarray(E, float))
+    dip = np.zeros((N, N))
+    dip[0, 1] = dip[1, 0] = 1.0
+    dip[1, 2] = dip[2, 1] = 1.0
+    a = np.diag([0.0, 1.0, 2.0])
+    rho0 = np.zeros((N, N), dtype=complex)
+    rho0[0, 0] = 1.0
+    return H, dip, a, rho0
+
+
+@golden
+def corr4_3level():
+    """correlation_4op_3t cubes (3-level ladder, Redfield flat 0.05) for three signatures,
+    plus 2D slices S[:, j, :] of a 64-point cube."""
+    import pyqed.oqs as oqs
+    H, dip, a, rho0 = _three_level()
+    out = dict(H=H, dip=dip, a_op=a, rho0=rho0, spectrum="flat005")
+    tau16 = 0.5 * np.arange(16)
+    for sig in ["lccc", "llll", "lrlr"]:
+        sol = oqs.RedfieldSolver(H, c_ops=[a], spectra=[SPECTRA["flat005"]])
+        sol.redfield_tensor()
+        sol.propagator(tau16)
+        out["cube_" + sig] = sol.correlation_4op_3t(rho0, [dip, dip, dip, dip], sig, tau16)
+    out["tau16"] = tau16
+    out["R"] = sol.R.toarray()
+    tau64 = 0.5 * np.arange(64)
+    sol = oqs.RedfieldSolver(H, c_ops=[a], spectra=[SPECTRA["flat005"]])
+    sol.redfield_tensor()
+    sol.propagator(tau64)
+    cube = sol.correlation_4op_3t(rho0, [dip, dip, dip, dip], "lccc", tau64)
+    out["tau64"] = tau64
+    out["slice64_j0"] = cube[:, 0, :]
+    out["slice64_j5"] = cube[:, 5, :]
+    out["U64_k7"] = sol.U[:, :, 7]
+    save("corr4_3level", **out)
+
+
+@golden
+def corr4_ensemble():
+    """Static-disorder ensemble (3 members): 'lccc' slices at tau2 index 3, n_tau = 32."""
+    import pyqed.oqs as oqs
+    rng = np.random.default_rng(3)
+    tau = 0.5 * np.arange(32)
+    Es, slices = [], []
+    for m in range(3):
+        E = np.array([0.0, 1.0, 1.5]) + np.array([0.0, 0.05, 0.08]) * rng.standard_normal(3)
+        H, dip, a, rho0 = _three_level(E)
+        sol = oqs.RedfieldSolver(H, c_ops=[a], spectra=[SPECTRA["flat005"]])
+        sol.redfield_tensor()
+        sol.propagator(tau)
+        cube = sol.correlation_4op_3t(rho0, [dip, dip, dip, dip], "lccc", tau)
+        Es.append(E)
+        slices.append(cube[:, 3, :])
+    save("corr4_ensemble", E=np.array(Es), tau=tau, j=3, slices=np.array(slices),
+         ens_sum=np.sum(slices, axis=0))
+
+
 if __name__ == "__main__":
     names = sys.argv[1:] or list(GENERATORS)
     for n in names:

@@ -21,3 +21,57 @@ def test_lindblad_oracle_matches_reference(name):
     else:
         assert relerr(rho, g["rho_final"]) < TOL
     assert np.allclose(g["times"], np.arange(Nt + 1) * float(g["dt"]))
+
+
+@pytest.mark.parametrize("name", ["redfield_n4", "redfield_n6_k2"])
+def test_redfield_oracle_matches_reference(name):
+    from conftest import SPECTRA
+    from oracle import redfield as orf
+    g = load_golden(name)
+    spec = SPECTRA[str(g["spectrum"])]
+    R, evecs = orf.redfield_tensor(g["H"], list(g["a_ops"]), [spec] * len(g["a_ops"]))
+    assert relerr(R, g["R"]) < TOL
+    assert relerr(evecs, g["evecs"]) < TOL
+    obs, rholist = orf.redfield_evolve(R, g["rho0"], evecs, int(g["Nt"]), float(g["dt"]), list(g["E"]))
+    assert obs.shape == g["observables"].shape          # (Nt, ne): t0 excluded
+    assert relerr(obs, g["observables"]) < TOL
+    assert relerr(np.array(rholist), g["rholist"]) < TOL
+
+
+def test_correlation_4op_3t_oracle_matches_reference():
+    from conftest import SPECTRA
+    from oracle import redfield as orf
+    g = load_golden("corr4_3level")
+    R, _ = orf.redfield_tensor(g["H"], [g["a_op"]], [SPECTRA["flat005"]])
+    assert relerr(R, g["R"]) < TOL
+    dip = g["dip"]
+    for sig in ["lccc", "llll", "lrlr"]:
+        cube = orf.correlation_4op_3t(R, g["rho0"], [dip] * 4, sig, g["tau16"])
+        assert relerr(cube, g["cube_" + sig]) < 1e-11, sig
+    # closed-form slice at fixed tau2 (the 2DES grid evaluator's formula)
+    from scipy.linalg import eig, inv
+    lam, U1 = eig(R)
+    U2 = inv(U1)
+    a = b = c = d = None
+    ops = [orf.op2sop(dip, s) for s in "lccc"]
+    idm = np.identity(3).flatten()
+    t = g["tau64"]
+    for j, key in [(0, "slice64_j0"), (5, "slice64_j5")]:
+        S = orf.response_slice_eig(lam, U1, U2, *ops, g["rho0"].flatten(), idm, t, t[j], t)
+        assert relerr(S, g[key]) < 1e-11
+
+
+def test_corr4_ensemble_oracle():
+    from conftest import SPECTRA
+    from oracle import redfield as orf
+    g = load_golden("corr4_ensemble")
+    dip = np.zeros((3, 3)); dip[0, 1] = dip[1, 0] = dip[1, 2] = dip[2, 1] = 1.0
+    a = np.diag([0.0, 1.0, 2.0])
+    rho0 = np.zeros((3, 3), complex); rho0[0, 0] = 1
+    tot = 0
+    for m, E in enumerate(g["E"]):
+        R, _ = orf.redfield_tensor(np.diag(E), [a], [SPECTRA["flat005"]])
+        cube = orf.correlation_4op_3t(R, rho0, [dip] * 4, "lccc", g["tau"])
+        assert relerr(cube[:, int(g["j"]), :], g["slices"][m]) < 1e-11
+        tot = tot + cube[:, int(g["j"]), :]
+    assert relerr(tot, g["ens_sum"]) < 1e-11

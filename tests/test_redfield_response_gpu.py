@@ -1,0 +1,117 @@
+"""Redfield propagation (GLF kernel), basis transforms and 2DES response kernels vs golden/oracle."""
+import numpy as np
+import pytest
+
+from conftest import SPECTRA, load_golden, relerr
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-10
+
+
+@pytest.mark.parametrize("name", ["redfield_n4", "redfield_n6_k2"])
+def test_redfield_evolve_matches_reference(name):
+    from pyqed_amd import RedfieldSolver
+    g = load_golden(name)
+    nk = len(g["a_ops"])
+    sol = RedfieldSolver(g["H"], c_ops=list(g["a_ops"]), spectra=[SPECTRA[str(g["spectrum"])]] * nk)
+    R, evecs = sol.redfield_tensor()
+    assert relerr(R.toarray(), g["R"]) < 1e-12
+    r = sol.evolve(g["rho0"], dt=float(g["dt"]), Nt=int(g["Nt"]), e_ops=list(g["E"]))
+    assert r.observables.shape == g["observables"].shape
+    assert relerr(r.observables, g["observables"]) < TOL
+    assert relerr(np.array(r.rholist), g["rholist"]) < TOL
+
+
+def test_basis_transform_batched():
+    import torch
+    from pyqed_amd.oqs import basis_transform
+    rng = np.random.default_rng(5)
+    for N, B in [(5, 3), (40, 2), (130, 2)]:
+        V = np.linalg.qr(rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N)))[0]
+        A = rng.standard_normal((B, N, N)) + 1j * rng.standard_normal((B, N, N))
+        dev = torch.device("cuda", 0)
+        At = torch.from_numpy(A.copy()).to(dev)
+        Vt = torch.from_numpy(V).to(dev)
+        basis_transform(Vt, At, inverse=False)
+        ref = np.einsum("ji,bjk,kl->bil", V.conj(), A, V)
+        assert relerr(At.cpu().numpy(), ref) < 1e-13
+        basis_transform(Vt, At, inverse=True)
+        assert relerr(At.cpu().numpy(), A) < 1e-13
+
+
+def test_propagator_and_cube_match_reference():
+    from pyqed_amd import RedfieldSolver
+    g = load_golden("corr4_3level")
+    dip = g["dip"]
+    for sig in ["lccc", "llll", "lrlr"]:
+        sol = RedfieldSolver(g["H"], c_ops=[g["a_op"]], spectra=[SPECTRA["flat005"]])
+        sol.redfield_tensor()
+        sol.propagator(g["tau16"])
+        cube = sol.correlation_4op_3t(g["rho0"], [dip] * 4, sig, g["tau16"])
+        assert cube.shape == (16, 16, 16)
+        assert relerr(cube, g["cube_" + sig]) < TOL, sig
+    sol = RedfieldSolver(g["H"], c_ops=[g["a_op"]], spectra=[SPECTRA["flat005"]])
+    sol.redfield_tensor()
+    U = sol.propagator(g["tau64"])
+    assert relerr(U[:, :, 7], g["U64_k7"]) < TOL
+    cube = sol.correlation_4op_3t(g["rho0"], [dip] * 4, "lccc", g["tau64"])
+    assert relerr(cube[:, 0, :], g["slice64_j0"]) < TOL
+    assert relerr(cube[:, 5, :], g["slice64_j5"]) < TOL
+
+
+def _ensemble_inputs(E_list, t2):
+    from pyqed_amd.response import ensemble_factors, redfield_superop_batch, sos_eig
+    from pyqed_amd.superoperator import operator_to_superoperator
+    N = 3
+    dip = np.zeros((3, 3)); dip[0, 1] = dip[1, 0] = dip[1, 2] = dip[2, 1] = 1.0
+    a = np.diag([0.0, 1.0, 2.0])
+    rho0 = np.zeros((3, 3), complex); rho0[0, 0] = 1
+    E = np.asarray(E_list)
+    spec = np.full((len(E), N, N), 0.05)
+    R = redfield_superop_batch(E, a, spec)
+    lam, U1 = np.linalg.eig(R)
+    U2 = np.linalg.inv(U1)
+    ops = [operator_to_superoperator(dip, s).toarray() for s in "lccc"]
+    return lam, ensemble_factors(lam, U1, U2, ops, rho0.flatten(), t2)
+
+
+def test_ensemble_slice_matches_reference():
+    from pyqed_amd.response import response2d_ensemble
+    g = load_golden("corr4_ensemble")
+    tau = g["tau"]
+    j = int(g["j"])
+    lam, (alpha, Mt, beta) = _ensemble_inputs(g["E"], tau[j])
+    # member by member
+    for m in range(len(g["E"])):
+        S = response2d_ensemble(lam[m:m + 1], alpha[m:m + 1], Mt[m:m + 1], beta[m:m + 1], tau, tau)
+        assert relerr(S.cpu().numpy(), g["slices"][m]) < TOL
+    S = response2d_ensemble(lam, alpha, Mt, beta, tau, tau)
+    assert relerr(S.cpu().numpy(), g["ens_sum"]) < TOL
+
+
+def test_ensemble_large_linearity_and_shards():
+    """Size-independent properties at bench scale: sum of shard results == full result,
+    and a doubled ensemble gives twice the signal (linearity)."""
+    import torch
+    from pyqed_amd.response import response2d_ensemble
+    rng = np.random.default_rng(7)
+    M = 512
+    E = np.array([0.0, 1.0, 1.5]) + np.array([0.0, 0.05, 0.08]) * rng.standard_normal((M, 3))
+    t = 0.5 * np.arange(256)
+    lam, (alpha, Mt, beta) = _ensemble_inputs(E, 0.0)
+    full = response2d_ensemble(lam, alpha, Mt, beta, t, t)
+    part = None
+    for sl in [slice(0, 100), slice(100, 333), slice(333, M)]:
+        part = response2d_ensemble(lam[sl], alpha[sl], Mt[sl], beta[sl], t, t, out=part, accumulate=part is not None)
+    assert relerr(part.cpu().numpy(), full.cpu().numpy()) < 1e-13
+    dbl = response2d_ensemble(np.concatenate([lam, lam]), np.concatenate([alpha, alpha]),
+                              np.concatenate([Mt, Mt]), np.concatenate([beta, beta]), t, t)
+    assert relerr(dbl.cpu().numpy(), 2 * full.cpu().numpy()) < 1e-13
+    # spot-check a few members' exact slice against the closed form
+    from oracle import redfield as orf
+    m = 17
+    X = alpha[m][None, :] * np.exp(np.outer(t, lam[m]))
+    Y = beta[m][None, :] * np.exp(np.outer(t, lam[m]))
+    ref = (-1j) ** 3 * X @ Mt[m] @ Y.T
+    one = response2d_ensemble(lam[m:m + 1], alpha[m:m + 1], Mt[m:m + 1], beta[m:m + 1], t, t)
+    assert relerr(one.cpu().numpy(), ref) < TOL
