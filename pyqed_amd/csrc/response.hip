@@ -103,9 +103,42 @@ __global__ void ens_x_kernel(const c128* alpha, const c128* lam, int M, int nL, 
   }
 }
 
-// Z [Kp][n1p]: Z[m*nL+p][k] = sum_q Mt[m][p][q] beta[m][q] e^{lam_mq t1_k}
-__global__ void ens_z_kernel(const c128* Mt, const c128* beta, const c128* lam, int M, int nL, const double* t1,
-                             int n1, int n1p, int Kp, c128* Z) {
+// Z [Kp][n1p]: Z[m*nL+p][k] = sum_q Mt[m][p][q] y_q(k),  y_q(k) = beta[m][q] e^{lam_mq t1_k}
+// grid (ceil(n1p/256), M): one thread per t1 point computes the nL exponentials once
+// (registers, nL <= ZMAX) and emits the nL outputs of its column; Mt_m staged in LDS.
+constexpr int ZMAX = 16;
+__global__ __launch_bounds__(256) void ens_z_kernel(const c128* Mt, const c128* beta, const c128* lam, int M, int nL,
+                                                    const double* t1, int n1, int n1p, int Kp, c128* Z) {
+  __shared__ c128 sM[ZMAX * ZMAX];
+  const int m = blockIdx.y;
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  for (int e = threadIdx.x; e < nL * nL; e += 256) sM[e] = Mt[(size_t)m * nL * nL + e];
+  __syncthreads();
+  if (k >= n1p) return;
+  c128 y[ZMAX];
+  const double tk = k < n1 ? t1[k] : 0.0;
+#pragma unroll
+  for (int q = 0; q < ZMAX; ++q)
+    y[q] = (q < nL && k < n1) ? cmul(beta[(size_t)m * nL + q], cexp_t(lam[(size_t)m * nL + q], tk)) : cmk(0, 0);
+  for (int p = 0; p < nL; ++p) {
+    c128 v = cmk(0, 0);
+#pragma unroll
+    for (int q = 0; q < ZMAX; ++q)
+      if (q < nL) v = cadd(v, cmul(sM[p * nL + q], y[q]));
+    Z[((size_t)m * nL + p) * n1p + k] = v;
+  }
+}
+
+// rows K..Kp-1 of Z are padding
+__global__ void ens_z_pad_kernel(int K, int Kp, int n1p, c128* Z) {
+  const size_t tot = (size_t)(Kp - K) * n1p;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x)
+    Z[(size_t)K * n1p + e] = cmk(0, 0);
+}
+
+// Generic fallback for nL > ZMAX (one thread per output element).
+__global__ void ens_z_generic_kernel(const c128* Mt, const c128* beta, const c128* lam, int M, int nL,
+                                     const double* t1, int n1, int n1p, int Kp, c128* Z) {
   const size_t tot = (size_t)Kp * n1p;
   const int K = M * nL;
   for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
@@ -114,10 +147,8 @@ __global__ void ens_z_kernel(const c128* Mt, const c128* beta, const c128* lam, 
     if (row < K && k < n1) {
       const int m = row / nL, p = row % nL;
       const c128* Mr = Mt + ((size_t)m * nL + p) * nL;
-      const c128* bm = beta + (size_t)m * nL;
-      const c128* lm = lam + (size_t)m * nL;
-      const double tk = t1[k];
-      for (int q = 0; q < nL; ++q) v = cadd(v, cmul(Mr[q], cmul(bm[q], cexp_t(lm[q], tk))));
+      for (int q = 0; q < nL; ++q)
+        v = cadd(v, cmul(Mr[q], cmul(beta[(size_t)m * nL + q], cexp_t(lam[(size_t)m * nL + q], t1[k]))));
     }
     Z[e] = v;
   }
@@ -207,7 +238,7 @@ extern "C" int qd_response2d_ensemble(const qd_c128* alpha, const qd_c128* Mt, c
                                       int n1, qd_c128* out, int accumulate, void* stream) {
   QD_CHECK_ARG(alpha && Mt && beta && lam && t3 && t1 && out, "qd_response2d_ensemble: null pointer");
   QD_CHECK_ARG(M >= 1 && nL >= 1 && n3 >= 1 && n1 >= 1, "qd_response2d_ensemble: bad sizes");
-  QD_CHECK_ARG((long)M * nL < (1L << 30), "qd_response2d_ensemble: M*nL too large");
+  QD_CHECK_ARG((long)M * nL < (1L << 30) && M < 65536 * 1024, "qd_response2d_ensemble: M*nL too large");
   hipStream_t st = (hipStream_t)stream;
   const int BT = ENS_BT;
   const int n3p = ceil_div(n3, BT) * BT, n1p = ceil_div(n1, BT) * BT;
@@ -227,9 +258,19 @@ extern "C" int qd_response2d_ensemble(const qd_c128* alpha, const qd_c128* Mt, c
   hipLaunchKernelGGL(ens_x_kernel, dim3(grid_for(nx, 256)), dim3(256), 0, st, (const c128*)alpha, (const c128*)lam, M,
                      nL, t3, n3, n3p, Kp, X);
   QD_HIP(hipGetLastError());
-  hipLaunchKernelGGL(ens_z_kernel, dim3(grid_for(nz, 256)), dim3(256), 0, st, (const c128*)Mt, (const c128*)beta,
-                     (const c128*)lam, M, nL, t1, n1, n1p, Kp, Z);
-  QD_HIP(hipGetLastError());
+  if (nL <= ZMAX) {
+    hipLaunchKernelGGL(ens_z_kernel, dim3(n1p / 256 + (n1p % 256 != 0), M), dim3(256), 0, st, (const c128*)Mt,
+                       (const c128*)beta, (const c128*)lam, M, nL, t1, n1, n1p, Kp, Z);
+    QD_HIP(hipGetLastError());
+    if (Kp > K) {
+      hipLaunchKernelGGL(ens_z_pad_kernel, dim3(64), dim3(256), 0, st, K, Kp, n1p, Z);
+      QD_HIP(hipGetLastError());
+    }
+  } else {
+    hipLaunchKernelGGL(ens_z_generic_kernel, dim3(grid_for(nz, 256)), dim3(256), 0, st, (const c128*)Mt,
+                       (const c128*)beta, (const c128*)lam, M, nL, t1, n1, n1p, Kp, Z);
+    QD_HIP(hipGetLastError());
+  }
   hipLaunchKernelGGL(ens_gemm_kernel, dim3(n1p / BT, n3p / BT, S), dim3(CG_WG), 0, st, X, Z, Kp, n1p, tiles, S, slabs,
                      n3p);
   QD_HIP(hipGetLastError());
