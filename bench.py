@@ -160,6 +160,78 @@ def cpu_baseline_2des(lam, alpha, Mt, beta, n=256, budget_s=5.0):
             "sample": f"{m} ensemble members x {n}x{n} grid, NumPy eigen-form slice in {el:.2f}s"}
 
 
+def bench_spo2(dev, steps, n=256, dt=0.05):
+    """BASELINE config d2: 2D vibronic SPO, 256x256 grid x 2 diabatic states, Strang steps."""
+    import torch
+    from pyqed_amd import _lib
+    from pyqed_amd.wpd import SPO2
+    x = np.linspace(-6, 6, n)
+    X, Y = np.meshgrid(x, x, indexing="ij")
+    sol = SPO2(x, x, mass=[1.0, 1.0], nstates=2)
+    sol.set_DPES([0.5 * ((X + 1) ** 2 + Y ** 2), 0.5 * ((X - 1) ** 2 + Y ** 2) + 0.1], [[[0, 1], 0.2 * X]])
+    sol.build(dt)
+    psi0 = np.zeros((n, n, 2), complex)
+    psi0[:, :, 0] = np.exp(-((X + 1.5) ** 2 + Y ** 2) / 2 + 0.5j * X) / np.sqrt(np.pi)
+    psi = torch.from_numpy(psi0).to(dev)
+    eVh = torch.from_numpy(sol.exp_V_half).to(dev)
+    eK = torch.from_numpy(sol.exp_K).to(dev)
+    lib = _lib.load()
+    st = _lib.stream_ptr(dev)
+
+    def run(k):
+        _lib.check(lib.qd_spo2_run(psi.data_ptr(), eVh.data_ptr(), eK.data_ptr(), n, n, 2, k, k, None, st),
+                   "qd_spo2_run")
+
+    run(10)
+    torch.cuda.synchronize(dev)
+    stream = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    run(steps)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    ev = e0.elapsed_time(e1) / 1e3
+    bytes_per_step = (4 * n * n * 2 + n * n * 4 + n * n) * 16  # psi r/w x2 kernels, exp_V_half, exp_K
+    norm = float((psi.abs() ** 2).sum().item() / (np.abs(psi0) ** 2).sum())
+    return {
+        "value": round(steps / wall, 1), "unit": "SPO steps/s",
+        "config": {"workload": "spo2_256x256x2 (BASELINE.json configs[2])", "grid": [n, n], "nstates": 2,
+                   "dt": dt},
+        "roofline": {"bound": "hbm", "achieved": round(bytes_per_step * steps / ev / 1e9, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(bytes_per_step * steps / ev / 1e9 / HBM_PEAK_GBS, 4),
+                     "bytes_per_step": bytes_per_step,
+                     "note": "working set (7 MiB) is MALL-resident; launch-gap bound at this size"},
+        "us_per_step": round(wall / steps * 1e6, 2), "norm_ratio": norm,
+    }
+
+
+def cpu_baseline_spo2(n=256, dt=0.05, budget_s=5.0):
+    from oracle import spo as ospo
+    x = np.linspace(-6, 6, n)
+    X, Y = np.meshgrid(x, x, indexing="ij")
+    v = np.zeros((n, n, 2, 2))
+    v[:, :, 0, 0] = 0.5 * ((X + 1) ** 2 + Y ** 2)
+    v[:, :, 1, 1] = 0.5 * ((X - 1) ** 2 + Y ** 2) + 0.1
+    v[:, :, 0, 1] = v[:, :, 1, 0] = 0.2 * X
+    w, u = np.linalg.eigh(v)
+    eVh = (u * np.exp(-1j * w * dt / 2)[..., None, :]) @ np.conj(np.swapaxes(u, -1, -2))
+    kx = 2 * np.pi * np.fft.fftfreq(n, x[1] - x[0])
+    KX, KY = np.meshgrid(kx, kx, indexing="ij")
+    eK = np.exp(-1j * (KX ** 2 + KY ** 2) / 2 * dt)
+    psi = np.zeros((n, n, 2), complex)
+    psi[:, :, 0] = np.exp(-((X + 1.5) ** 2 + Y ** 2) / 2)
+    t0 = time.perf_counter()
+    k = 0
+    while time.perf_counter() - t0 < budget_s:
+        psi = ospo.spo2_run(eVh, eK, psi, 5, 5)[-1]
+        k += 5
+    el = time.perf_counter() - t0
+    return {"value": round(k / el, 2), "unit": "SPO steps/s", "cores": 1, "kind": "port",
+            "sample": f"{k} Strang steps of the scipy.fftpack restatement of SPO2.run at {n}x{n}x2 in {el:.1f}s"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -173,6 +245,8 @@ def main():
     ap.add_argument("--ens", type=int, default=4096, help="2DES disorder-ensemble members (total)")
     ap.add_argument("--ens-reps", type=int, default=20)
     ap.add_argument("--no-2des", action="store_true")
+    ap.add_argument("--spo-steps", type=int, default=1000)
+    ap.add_argument("--no-spo", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -241,6 +315,10 @@ def main():
         if rank == 0:
             twodes["signal_abs_max"] = float(sig.abs().max().item())
 
+    spo = None
+    if not args.no_spo:
+        spo = bench_spo2(dev, args.spo_steps)
+
     if rank == 0:
         total_dm_steps = B * args.steps * world
         value = total_dm_steps / wall_max
@@ -283,7 +361,11 @@ def main():
         if twodes is not None:
             if world == 1 and not args.no_cpu:
                 twodes["cpu_baseline"] = cpu_baseline_2des(*ens_in)
-            out["secondary"] = {"2des": twodes}
+            out.setdefault("secondary", {})["2des"] = twodes
+        if spo is not None:
+            if world == 1 and not args.no_cpu:
+                spo["cpu_baseline"] = cpu_baseline_spo2()
+            out.setdefault("secondary", {})["spo2"] = spo
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

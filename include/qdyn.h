@@ -93,6 +93,30 @@ int qd_glf_rk4(const qd_c128* P, const qd_c128* Q, const qd_c128* L,
 int qd_basis_transform(const qd_c128* V, qd_c128* A, int B, int N, int mode,
                        void* stream);
 
+/* ------------------------------------------------------------ split-operator */
+/*
+ * 2D multi-state split-operator propagation, nsteps Strang steps
+ *     psi <- V/2 . IFFT2( exp_K * FFT2( V/2 . psi ) )
+ * exactly as pyqed/wpd.py:723-732 (SPO2.run, return_states=True, linear KEO
+ * _KEO_linear wpd.py:837-848).  psi [nx][ny][ns] in/out (state index fastest),
+ * expVh [nx][ny][ns][ns] = U e^{-i w dt/2} U^+ per grid point, expK [nx][ny].
+ * snap [nsteps/nout][nx][ny][ns]: psi after steps nout, 2*nout, ... (NULL: none).
+ * nx, ny powers of two in [16, 1024]; 1 <= ns <= 8; ns*ny/4 and ns*nx/4 <= 256.
+ */
+int qd_spo2_run(qd_c128* psi, const qd_c128* expVh, const qd_c128* expK, int nx,
+                int ny, int ns, int nsteps, int nout, qd_c128* snap,
+                void* stream);
+
+/*
+ * 1D single-surface split-operator with the step structure of pyqed/wpd.py:225-273
+ * (SPO.run): V/2 ; (nt//nout - 1)*nout x [K, V] (snapshot after each block) ; K, V/2.
+ * psi [B][nx] in/out (B independent wavepackets, one workgroup each, all steps in
+ * LDS), expV/expVh/expK [nx]; snap [B][nt//nout - 1][nx] or NULL.
+ */
+int qd_spo1d_run(qd_c128* psi, const qd_c128* expV, const qd_c128* expVh,
+                 const qd_c128* expK, int nx, int B, int nt, int nout,
+                 qd_c128* snap, void* stream);
+
 /* ------------------------------------------------------------ response --- */
 /*
  * SOS Liouville-space propagator U[a][b][k] = sum_j U1[a][j] e^{lam_j t_k} U2[j][b]

@@ -1,0 +1,62 @@
+"""NumPy restatement of the split-operator propagators (test infrastructure only).
+
+Follows:
+  pyqed/wpd.py:191-273   SPO (1D): build (exp_V, exp_V_half, exp_K), run with the
+                         reference's step structure V/2 ; (nt//nout-1)*nout x [K, V] ; K, V/2
+  pyqed/wpd.py:496-625   SPO2.build (per-point eigh, sorted, U e^{-iw dt} U^+)
+  pyqed/wpd.py:692-758   SPO2.run (return_states=True): nt//nout*nout Strang steps
+                         V/2 . IFFT2 . exp_K . FFT2 . V/2, psilist incl. psi0
+  pyqed/wpd.py:837-848   _KEO_linear (scipy.fftpack fft2/ifft2 over axes (0, 1))
+"""
+import numpy as np
+import scipy.linalg
+from scipy.fftpack import fft, fft2, fftfreq, ifft, ifft2
+
+
+def spo1d_ops(x, V, mass, dt):
+    dx = x[1] - x[0]
+    k = 2.0 * np.pi * fftfreq(len(x), dx)
+    return np.exp(-1j * V * dt), np.exp(-1j * V * dt / 2.0), np.exp(-0.5j / mass * (k * k) * dt)
+
+
+def spo1d_run(x, V, psi0, dt, nt, nout=1, mass=1.0):
+    expV, expVh, expK = spo1d_ops(x, V, mass, dt)
+    psi = expVh * psi0.copy()
+    psilist = []
+    for i in range(1, nt // nout):
+        for _ in range(nout):
+            psi = ifft(fft(psi) * expK)
+            psi = expV * psi
+        psilist.append(psi.copy())
+    psi = ifft(fft(psi) * expK)
+    psi = expVh * psi
+    return psilist, psi
+
+
+def spo2_build(x, y, v, masses, dt):
+    nx, ny, ns = v.shape[0], v.shape[1], v.shape[2]
+    kx = 2.0 * np.pi * fftfreq(nx, x[1] - x[0])
+    ky = 2.0 * np.pi * fftfreq(ny, y[1] - y[0])
+    Kx, Ky = np.meshgrid(kx, ky, indexing="ij")
+    mx, my = masses
+    exp_K = np.exp(-1j * (Kx ** 2 / 2. / mx + Ky ** 2 / 2. / my) * dt)
+    exp_V_half = np.zeros(v.shape, dtype=complex)
+    for i in range(nx):
+        for j in range(ny):
+            w, u = scipy.linalg.eigh(v[i, j])
+            idx = np.argsort(w)
+            w, u = w[idx], u[:, idx]
+            exp_V_half[i, j] = u @ np.diag(np.exp(-1j * w * dt / 2)) @ u.conj().T
+    return exp_V_half, exp_K
+
+
+def spo2_run(exp_V_half, exp_K, psi0, nt, nout=1):
+    psi = psi0.copy()
+    psilist = [psi0]
+    for _ in range(nt // nout):
+        for _ in range(nout):
+            psi = np.einsum("ijab,ijb->ija", exp_V_half, psi)
+            psi = ifft2(np.einsum("ij,ija->ija", exp_K, fft2(psi, axes=(0, 1))), axes=(0, 1))
+            psi = np.einsum("ijab,ijb->ija", exp_V_half, psi)
+        psilist.append(psi.copy())
+    return psilist

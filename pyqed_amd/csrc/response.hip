@@ -258,7 +258,7 @@ extern "C" int qd_response2d_ensemble(const qd_c128* alpha, const qd_c128* Mt, c
   hipLaunchKernelGGL(ens_x_kernel, dim3(grid_for(nx, 256)), dim3(256), 0, st, (const c128*)alpha, (const c128*)lam, M,
                      nL, t3, n3, n3p, Kp, X);
   QD_HIP(hipGetLastError());
-  if (nL <= ZMAX) {
+  if (nL <= ZMAX && M <= 65535) {
     hipLaunchKernelGGL(ens_z_kernel, dim3(n1p / 256 + (n1p % 256 != 0), M), dim3(256), 0, st, (const c128*)Mt,
                        (const c128*)beta, (const c128*)lam, M, nL, t1, n1, n1p, Kp, Z);
     QD_HIP(hipGetLastError());

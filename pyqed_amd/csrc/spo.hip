@@ -1,0 +1,360 @@
+// spo.hip — split-operator wavepacket propagation (1D and 2D, multi-state).
+//
+// Replaces the Strang loops of pyqed/wpd.py:
+//   SPO.run   (wpd.py:225-273, 1D single surface)   -> qd_spo1d_run
+//   SPO2.run  (wpd.py:692-758, 2D diabatic, return_states=True, _KEO_linear
+//              wpd.py:837-848)                       -> qd_spo2_run
+//
+// FFT: hand-written Stockham autosort (radix-4 stages + one radix-2 stage when
+// log2 L is odd) on LDS, fp64 twiddles exp(-2 pi i k/L) from sincospi, L a power
+// of two in [16, 1024].  Natural-order output, no bit reversal pass.
+//
+// 2D step layout (psi [nx][ny][ns], state index fastest, as the reference):
+//   row kernel    (one row i per workgroup; contiguous 16-B loads):
+//                   [IFFT_y] -> V/2 -> [snapshot] -> [V/2] -> [FFT_y]
+//   column kernel (C columns per workgroup):
+//                   FFT_x -> * exp_K / (nx ny) -> IFFT_x
+// A run of n Strang steps V/2 K V/2 is: row(V/2, FFT_y), then n x {col, row},
+// the last row kernel without the trailing V/2 + FFT_y.  Both V/2 are applied
+// separately (no V/2 V/2 -> V merge) so every step is the reference's
+// return_states=True arithmetic.  psi is read and written once per kernel;
+// exp_V_half (ns^2 per point) once per row pass, exp_K once per column pass.
+#include "qd_common.hpp"
+
+namespace qd {
+namespace {
+
+constexpr int SPO_MAX_NS = 8;
+
+__global__ void twiddle_kernel(int L, c128* tw) {
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < L; k += gridDim.x * blockDim.x) {
+    double s, c;
+    sincospi(-2.0 * (double)k / (double)L, &s, &c);
+    tw[k] = cmk(c, s);
+  }
+}
+
+// Stockham FFT of length L on LDS buffers a/b (one transform), T = L/4 threads,
+// thread index t in [0, T).  All threads of the workgroup must call it (barriers).
+// Returns the buffer holding the result.  INV: conjugated twiddles, no scaling.
+template <int L, bool INV>
+__device__ __forceinline__ c128* fft_lds(c128* a, c128* b, const c128* tw, int t, bool active) {
+#pragma unroll
+  for (int Ns = 1; Ns * 4 <= L; Ns *= 4) {
+    if (active) {
+      const int j = t;
+      const int k = j % Ns;
+      const int base = k * (L / (4 * Ns));
+      c128 w1 = tw[base], w2 = tw[2 * base], w3 = tw[3 * base];
+      if (INV) {
+        w1 = cconj(w1);
+        w2 = cconj(w2);
+        w3 = cconj(w3);
+      }
+      const c128 v0 = a[j];
+      const c128 v1 = cmul(a[j + L / 4], w1);
+      const c128 v2 = cmul(a[j + L / 2], w2);
+      const c128 v3 = cmul(a[j + 3 * L / 4], w3);
+      const c128 a0 = cadd(v0, v2), a1 = csub(v0, v2), b0 = cadd(v1, v3), b1 = csub(v1, v3);
+      const c128 ib1 = INV ? cmuli(b1) : cmulmi(b1);  // (+i or -i) * b1
+      const int d = (j / Ns) * Ns * 4 + k;
+      b[d] = cadd(a0, b0);
+      b[d + Ns] = cadd(a1, ib1);
+      b[d + 2 * Ns] = csub(a0, b0);
+      b[d + 3 * Ns] = csub(a1, ib1);
+    }
+    __syncthreads();
+    c128* tmp = a;
+    a = b;
+    b = tmp;
+  }
+  constexpr int lg = __builtin_ctz(L);
+  if (lg & 1) {  // final radix-2 stage, Ns = L/2
+    if (active) {
+      constexpr int Ns = L / 2;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int j = t + h * (L / 4);
+        const int k = j % Ns;
+        c128 w = tw[k];
+        if (INV) w = cconj(w);
+        const c128 v0 = a[j], v1 = cmul(a[j + L / 2], w);
+        const int d = (j / Ns) * Ns * 2 + k;
+        b[d] = cadd(v0, v1);
+        b[d + Ns] = csub(v0, v1);
+      }
+    }
+    __syncthreads();
+    c128* tmp = a;
+    a = b;
+    b = tmp;
+  }
+  return a;
+}
+
+// psi_point <- U psi_point for each grid point of one row held in LDS (buf[a][j]).
+__device__ __forceinline__ void apply_point_op(c128* buf, int stride, const c128* U /*[n][ns][ns]*/, int n, int ns) {
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    c128 in[SPO_MAX_NS];
+    for (int a = 0; a < ns; ++a) in[a] = buf[a * stride + j];
+    const c128* u = U + (size_t)j * ns * ns;
+    for (int a = 0; a < ns; ++a) {
+      c128 s = cmk(0, 0);
+      for (int b = 0; b < ns; ++b) s = cadd(s, cmul(u[a * ns + b], in[b]));
+      buf[a * stride + j] = s;
+    }
+  }
+}
+
+enum RowFlags { ROW_INV = 1, ROW_VH1 = 2, ROW_SNAP = 4, ROW_VH2 = 8, ROW_FWD = 16 };
+
+// One row i of psi [nx][ny][ns]; FFTs along y (length L = ny) for each state.
+template <int L>
+__global__ __launch_bounds__(256) void spo2_row_kernel(c128* psi, const c128* expVh, const c128* twy, int ny, int ns,
+                                                       int flags, c128* snap) {
+  extern __shared__ c128 sm[];
+  c128* tw = sm;            // L
+  c128* A = sm + L;         // ns * L
+  c128* Bf = A + ns * L;    // ns * L
+  const int i = blockIdx.x;
+  const size_t rowoff = (size_t)i * L * ns;
+  for (int k = threadIdx.x; k < L; k += blockDim.x) tw[k] = twy[k];
+  for (int e = threadIdx.x; e < L * ns; e += blockDim.x) A[(e % ns) * L + e / ns] = psi[rowoff + e];
+  __syncthreads();
+  const int T = L / 4;
+  const int f = threadIdx.x / T, t = threadIdx.x % T;
+  const bool active = f < ns;
+  c128* cur = A;
+  c128* oth = Bf;
+  if (flags & ROW_INV) {
+    c128* r = fft_lds<L, true>(A + (active ? f : 0) * L, Bf + (active ? f : 0) * L, tw, t, active);
+    const bool inA = (r == A + (active ? f : 0) * L);
+    cur = inA ? A : Bf;
+    oth = inA ? Bf : A;
+  }
+  const c128* Ui = expVh + (size_t)i * L * ns * ns;
+  if (flags & ROW_VH1) {
+    apply_point_op(cur, L, Ui, L, ns);
+    __syncthreads();
+  }
+  if (flags & ROW_SNAP) {
+    for (int e = threadIdx.x; e < L * ns; e += blockDim.x) snap[rowoff + e] = cur[(e % ns) * L + e / ns];
+    __syncthreads();
+  }
+  if (flags & ROW_VH2) {
+    apply_point_op(cur, L, Ui, L, ns);
+    __syncthreads();
+  }
+  if (flags & ROW_FWD) {
+    c128* r = fft_lds<L, false>(cur + (active ? f : 0) * L, oth + (active ? f : 0) * L, tw, t, active);
+    cur = (r == cur + (active ? f : 0) * L) ? cur : oth;
+  }
+  for (int e = threadIdx.x; e < L * ns; e += blockDim.x) psi[rowoff + e] = cur[(e % ns) * L + e / ns];
+}
+
+// C columns j0..j0+C-1 of psi [nx][ny][ns]; FFT along x (length L = nx), multiply
+// by expKT[j][i] (exp_K transposed and pre-scaled by 1/(nx ny)), inverse FFT.
+template <int L, int C>
+__global__ __launch_bounds__(256) void spo2_col_kernel(c128* psi, const c128* expKT, const c128* twx, int ny, int ns) {
+  extern __shared__ c128 sm[];
+  c128* tw = sm;                 // L
+  c128* A = sm + L;              // C * ns * L   (layout [c][a][i])
+  c128* Bf = A + C * ns * L;
+  const int j0 = blockIdx.x * C;
+  const int W = C * ns;  // transforms in this workgroup
+  for (int k = threadIdx.x; k < L; k += blockDim.x) tw[k] = twx[k];
+  for (int e = threadIdx.x; e < L * W; e += blockDim.x) {
+    const int ca = e % W, i = e / W;
+    A[ca * L + i] = psi[((size_t)i * ny + j0) * ns + ca];  // (j0 + c) * ns + a == j0*ns + ca
+  }
+  __syncthreads();
+  const int T = L / 4;
+  const int f = threadIdx.x / T, t = threadIdx.x % T;
+  const bool active = f < W;
+  const int fo = (active ? f : 0) * L;
+  c128* r = fft_lds<L, false>(A + fo, Bf + fo, tw, t, active);
+  c128* cur = (r == A + fo) ? A : Bf;
+  c128* oth = (cur == A) ? Bf : A;
+  for (int e = threadIdx.x; e < L * W; e += blockDim.x) {
+    const int ca = e / L, i = e % L;
+    const int c = ca / ns;
+    cur[ca * L + i] = cmul(cur[ca * L + i], expKT[(size_t)(j0 + c) * L + i]);
+  }
+  __syncthreads();
+  r = fft_lds<L, true>(cur + fo, oth + fo, tw, t, active);
+  cur = (r == cur + fo) ? cur : oth;
+  for (int e = threadIdx.x; e < L * W; e += blockDim.x) {
+    const int ca = e % W, i = e / W;
+    psi[((size_t)i * ny + j0) * ns + ca] = cur[ca * L + i];
+  }
+}
+
+// expKT[j][i] = expK[i][j] * scale
+__global__ void transpose_scale_kernel(const c128* expK, int nx, int ny, double scale, c128* expKT) {
+  const size_t tot = (size_t)nx * ny;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(e / ny), j = (int)(e % ny);
+    expKT[(size_t)j * nx + i] = cscale(expK[e], scale);
+  }
+}
+
+// ---------------------------------------------------------------- 1D persistent SPO
+// SPO.run structure (wpd.py:250-270): V/2 ; for i in 1..nt//nout-1: nout x [K, V], snapshot ;
+// then K, V/2.  One workgroup per wavepacket, all steps in LDS.
+template <int L>
+__global__ __launch_bounds__(256) void spo1d_kernel(c128* psi, const c128* expV, const c128* expVh, const c128* expK,
+                                                    const c128* twg, int nt, int nout, c128* snap) {
+  __shared__ c128 tw[L], A[L], Bf[L], eV[L], eK[L];
+  const int b = blockIdx.x;
+  c128* p = psi + (size_t)b * L;
+  for (int k = threadIdx.x; k < L; k += blockDim.x) {
+    tw[k] = twg[k];
+    eV[k] = expV[k];
+    eK[k] = cscale(expK[k], 1.0 / L);
+    A[k] = cmul(expVh[k], p[k]);
+  }
+  __syncthreads();
+  const int T = L / 4;
+  const int t = threadIdx.x;
+  const bool active = t < T;
+  c128* cur = A;
+  c128* oth = Bf;
+  const int nblk = nt / nout;
+  const int nsnap = nblk > 0 ? nblk - 1 : 0;
+  auto kstep = [&]() {
+    c128* r = fft_lds<L, false>(cur, oth, tw, t, active);
+    if (r != cur) { oth = cur; cur = r; }
+    for (int k = threadIdx.x; k < L; k += blockDim.x) cur[k] = cmul(cur[k], eK[k]);
+    __syncthreads();
+    r = fft_lds<L, true>(cur, oth, tw, t, active);
+    if (r != cur) { oth = cur; cur = r; }
+  };
+  for (int blk = 1; blk < nblk; ++blk) {
+    for (int s = 0; s < nout; ++s) {
+      kstep();
+      for (int k = threadIdx.x; k < L; k += blockDim.x) cur[k] = cmul(eV[k], cur[k]);
+      __syncthreads();
+    }
+    if (snap)
+      for (int k = threadIdx.x; k < L; k += blockDim.x) snap[((size_t)b * nsnap + (blk - 1)) * L + k] = cur[k];
+  }
+  kstep();
+  for (int k = threadIdx.x; k < L; k += blockDim.x) p[k] = cmul(expVh[k], cur[k]);
+}
+
+bool pow2_in_range(int n) { return n >= 16 && n <= 1024 && (n & (n - 1)) == 0; }
+
+// L dispatch helpers
+#define QD_FFT_DISPATCH(L, CALL) \
+  switch (L) {                   \
+    case 16: CALL(16); break;    \
+    case 32: CALL(32); break;    \
+    case 64: CALL(64); break;    \
+    case 128: CALL(128); break;  \
+    case 256: CALL(256); break;  \
+    case 512: CALL(512); break;  \
+    case 1024: CALL(1024); break;\
+    default: break;              \
+  }
+
+int twiddles(int L, hipStream_t st, c128* tw) {
+  hipLaunchKernelGGL(twiddle_kernel, dim3((L + 255) / 256), dim3(256), 0, st, L, tw);
+  QD_HIP(hipGetLastError());
+  return QD_OK;
+}
+
+}  // namespace
+}  // namespace qd
+
+using namespace qd;
+
+extern "C" int qd_spo2_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* expK_, int nx, int ny, int ns,
+                           int nsteps, int nout, qd_c128* snap_, void* stream) {
+  QD_CHECK_ARG(psi_ && expVh_ && expK_, "qd_spo2_run: null pointer");
+  QD_CHECK_ARG(pow2_in_range(nx) && pow2_in_range(ny), "qd_spo2_run: nx=%d, ny=%d must be powers of 2 in [16, 1024]",
+               nx, ny);
+  QD_CHECK_ARG(ns >= 1 && ns <= SPO_MAX_NS, "qd_spo2_run: ns=%d outside [1, %d]", ns, SPO_MAX_NS);
+  QD_CHECK_ARG(nsteps >= 0 && nout >= 1, "qd_spo2_run: nsteps=%d nout=%d", nsteps, nout);
+  QD_CHECK_ARG(ns * (ny / 4) <= 256, "qd_spo2_run: ns*ny/4 = %d > 256 threads", ns * (ny / 4));
+  if (nsteps == 0) return QD_OK;
+  hipStream_t st = (hipStream_t)stream;
+  c128* psi = (c128*)psi_;
+  const c128* expVh = (const c128*)expVh_;
+  c128* snap = (c128*)snap_;
+  void* w = nullptr;
+  const size_t nkt = (size_t)nx * ny;
+  int rc = workspace(WS_SPO, (nkt + nx + ny) * sizeof(c128), &w);
+  if (rc) return rc;
+  c128* expKT = (c128*)w;
+  c128* twx = expKT + nkt;
+  c128* twy = twx + nx;
+  if ((rc = twiddles(nx, st, twx))) return rc;
+  if ((rc = twiddles(ny, st, twy))) return rc;
+  hipLaunchKernelGGL(transpose_scale_kernel, dim3((int)std::min<size_t>((nkt + 255) / 256, 4096)), dim3(256), 0, st,
+                     (const c128*)expK_, nx, ny, 1.0 / ((double)nx * ny), expKT);
+  QD_HIP(hipGetLastError());
+
+  // column tiling: C columns per workgroup so that C*ns transforms of nx/4 threads fit 256 threads
+  int C = std::max(1, 256 / (ns * (nx / 4)));
+  while (C > 1 && ny % C) C >>= 1;
+  C = std::min(C, 2);  // keep >= ny/2 workgroups in flight
+  QD_CHECK_ARG(ns * (nx / 4) <= 256, "qd_spo2_run: ns*nx/4 = %d > 256 threads", ns * (nx / 4));
+  const int row_threads = std::max(64, ((ns * (ny / 4) + 63) / 64) * 64);
+  const size_t row_lds = (size_t)(ny + 2 * ns * ny) * sizeof(c128);
+  const int col_threads = std::max(64, ((C * ns * (nx / 4) + 63) / 64) * 64);
+  const size_t col_lds = (size_t)(nx + 2 * C * ns * nx) * sizeof(c128);
+  QD_CHECK_ARG(row_lds <= 160 * 1024 && col_lds <= 160 * 1024, "qd_spo2_run: LDS footprint too large");
+
+  auto row = [&](int flags, c128* sp) -> int {
+#define ROWCALL(L) \
+  hipLaunchKernelGGL(spo2_row_kernel<L>, dim3(nx), dim3(row_threads), row_lds, st, psi, expVh, twy, ny, ns, flags, sp)
+    QD_FFT_DISPATCH(ny, ROWCALL)
+#undef ROWCALL
+    QD_HIP(hipGetLastError());
+    return QD_OK;
+  };
+  auto col = [&]() -> int {
+#define COLCALL(L)                                                                                                   \
+  if (C == 2)                                                                                                        \
+    hipLaunchKernelGGL((spo2_col_kernel<L, 2>), dim3(ny / 2), dim3(col_threads), col_lds, st, psi, expKT, twx, ny,   \
+                       ns);                                                                                          \
+  else                                                                                                               \
+    hipLaunchKernelGGL((spo2_col_kernel<L, 1>), dim3(ny), dim3(col_threads), col_lds, st, psi, expKT, twx, ny, ns)
+    QD_FFT_DISPATCH(nx, COLCALL)
+#undef COLCALL
+    QD_HIP(hipGetLastError());
+    return QD_OK;
+  };
+  const size_t grid_elems = (size_t)nx * ny * ns;
+  if ((rc = row(ROW_VH1 | ROW_FWD, nullptr))) return rc;
+  for (int s = 1; s <= nsteps; ++s) {
+    if ((rc = col())) return rc;
+    const bool take = snap && (s % nout == 0);
+    c128* sp = take ? snap + (size_t)(s / nout - 1) * grid_elems : nullptr;
+    int flags = ROW_INV | ROW_VH1 | (take ? ROW_SNAP : 0);
+    if (s < nsteps) flags |= ROW_VH2 | ROW_FWD;
+    if ((rc = row(flags, sp))) return rc;
+  }
+  return QD_OK;
+}
+
+extern "C" int qd_spo1d_run(qd_c128* psi_, const qd_c128* expV_, const qd_c128* expVh_, const qd_c128* expK_, int nx,
+                            int B, int nt, int nout, qd_c128* snap_, void* stream) {
+  QD_CHECK_ARG(psi_ && expV_ && expVh_ && expK_, "qd_spo1d_run: null pointer");
+  QD_CHECK_ARG(pow2_in_range(nx), "qd_spo1d_run: nx=%d must be a power of 2 in [16, 1024]", nx);
+  QD_CHECK_ARG(B >= 1 && nt >= 0 && nout >= 1, "qd_spo1d_run: B=%d nt=%d nout=%d", B, nt, nout);
+  hipStream_t st = (hipStream_t)stream;
+  void* w = nullptr;
+  int rc = workspace(WS_MISC, nx * sizeof(c128), &w);
+  if (rc) return rc;
+  c128* tw = (c128*)w;
+  if ((rc = twiddles(nx, st, tw))) return rc;
+  const int threads = std::max(64, nx / 4);
+#define CALL1D(L)                                                                                                   \
+  hipLaunchKernelGGL(spo1d_kernel<L>, dim3(B), dim3(threads), 0, st, (c128*)psi_, (const c128*)expV_,               \
+                     (const c128*)expVh_, (const c128*)expK_, (const c128*)tw, nt, nout, (c128*)snap_)
+  QD_FFT_DISPATCH(nx, CALL1D)
+#undef CALL1D
+  QD_HIP(hipGetLastError());
+  return QD_OK;
+}

@@ -181,6 +181,73 @@ def corr4_ensemble():
          ens_sum=np.sum(slices, axis=0))
 
 
+# ----------------------------------------------------------------- split-operator
+def spo2_model(n, L=6.0, complex_coupling=False):
+    """BASELINE config d2 model: surfaces 1/2((X+-1)^2+Y^2) (+0.1 offset), coupling 0.2*X."""
+    x = np.linspace(-L, L, n)
+    y = np.linspace(-L, L, n)
+    X, Y = np.meshgrid(x, y, indexing="ij")
+    v0 = 0.5 * ((X + 1) ** 2 + Y ** 2)
+    v1 = 0.5 * ((X - 1) ** 2 + Y ** 2) + 0.1
+    c = 0.2 * X + (0.1j * Y if complex_coupling else 0)
+    psi0 = np.zeros((n, n, 2), dtype=complex)
+    psi0[:, :, 0] = np.exp(-((X + 1.5) ** 2 + Y ** 2) / 2 + 0.5j * X) / np.sqrt(np.pi)
+    return x, y, v0, v1, c, psi0
+
+
+def _spo2_case(name, n, nt, nout, dt, complex_coupling=False, masses=(1.0, 1.0), keep_ops=True):
+    from pyqed.wpd import SPO2
+    x, y, v0, v1, c, psi0 = spo2_model(n, complex_coupling=complex_coupling)
+    sol = SPO2(x, y, mass=list(masses), nstates=2)
+    if complex_coupling:
+        # set_DPES builds a real array (wpd.py:466) and drops Im; set_dpes keeps a complex
+        # Hermitian potential -> exercises the complex branch of build (wpd.py:583-600)
+        v = np.zeros((n, n, 2, 2), dtype=complex)
+        v[:, :, 0, 0], v[:, :, 1, 1], v[:, :, 0, 1], v[:, :, 1, 0] = v0, v1, c, np.conj(c)
+        sol.set_dpes(v)
+    else:
+        sol.set_DPES([v0, v1], [[[0, 1], c]])
+    r = sol.run(psi0, dt=dt, nt=nt, nout=nout)
+    out = dict(x=x, y=y, v0=v0, v1=v1, coupling=np.asarray(c), psi0=psi0, dt=dt, nt=nt, nout=nout,
+               masses=np.array(masses), psilist=np.array(r.psilist), times=r.times,
+               apes=sol.apes if sol.apes is not None else np.zeros(0))
+    if keep_ops:
+        out.update(exp_V_half=sol.exp_V_half, exp_K=sol.exp_K)
+    save(name, **out)
+
+
+@golden
+def spo2_32():
+    _spo2_case("spo2_32", n=32, nt=6, nout=2, dt=0.05)
+
+
+@golden
+def spo2_64_complex():
+    _spo2_case("spo2_64_complex", n=64, nt=3, nout=1, dt=0.05, complex_coupling=True, masses=(1.0, 2.0),
+               keep_ops=False)
+
+
+def _spo1d_case(name, n, nt, nout, dt):
+    from pyqed.wpd import SPO
+    x = np.linspace(-8, 8, n)
+    psi0 = (np.exp(-(x + 2) ** 2 / 2 + 1j * 0.5 * x) / np.pi ** 0.25).astype(complex)
+    sol = SPO(x, mass=1.0)
+    sol.set_potential(lambda x: x ** 2 / 2)
+    r = sol.run(psi0, dt=dt, nt=nt, nout=nout)
+    save(name, x=x, psi0=psi0, dt=dt, nt=nt, nout=nout, psilist=np.array(r.psilist).reshape(-1, n), psi=r.psi,
+         times=r.times)
+
+
+@golden
+def spo1d_256():
+    _spo1d_case("spo1d_256", n=256, nt=20, nout=1, dt=0.01)
+
+
+@golden
+def spo1d_256_nout3():
+    _spo1d_case("spo1d_256_nout3", n=256, nt=20, nout=3, dt=0.01)
+
+
 if __name__ == "__main__":
     names = sys.argv[1:] or list(GENERATORS)
     for n in names:

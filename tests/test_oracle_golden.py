@@ -75,3 +75,30 @@ def test_corr4_ensemble_oracle():
         assert relerr(cube[:, int(g["j"]), :], g["slices"][m]) < 1e-11
         tot = tot + cube[:, int(g["j"]), :]
     assert relerr(tot, g["ens_sum"]) < 1e-11
+
+
+@pytest.mark.parametrize("name", ["spo1d_256", "spo1d_256_nout3"])
+def test_spo1d_oracle_matches_reference(name):
+    from oracle import spo
+    g = load_golden(name)
+    psilist, psi = spo.spo1d_run(g["x"], g["x"] ** 2 / 2, g["psi0"], float(g["dt"]), int(g["nt"]), int(g["nout"]))
+    assert len(psilist) == int(g["nt"]) // int(g["nout"]) - 1
+    assert relerr(np.array(psilist).reshape(g["psilist"].shape), g["psilist"]) < TOL
+    assert relerr(psi, g["psi"]) < TOL
+
+
+@pytest.mark.parametrize("name", ["spo2_32", "spo2_64_complex"])
+def test_spo2_oracle_matches_reference(name):
+    from oracle import spo
+    g = load_golden(name)
+    n = len(g["x"])
+    v = np.zeros((n, n, 2, 2), dtype=complex if np.iscomplexobj(g["coupling"]) else float)
+    v[:, :, 0, 0], v[:, :, 1, 1] = g["v0"], g["v1"]
+    v[:, :, 0, 1], v[:, :, 1, 0] = g["coupling"], np.conj(g["coupling"])
+    eVh, eK = spo.spo2_build(g["x"], g["y"], v, g["masses"], float(g["dt"]))
+    if "exp_V_half" in g:
+        assert relerr(eVh, g["exp_V_half"]) < TOL
+        assert relerr(eK, g["exp_K"]) < TOL
+    psilist = spo.spo2_run(eVh, eK, g["psi0"], int(g["nt"]), int(g["nout"]))
+    assert len(psilist) == int(g["nt"]) // int(g["nout"]) + 1
+    assert relerr(np.array(psilist), g["psilist"]) < TOL
