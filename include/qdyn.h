@@ -117,6 +117,32 @@ int qd_spo1d_run(qd_c128* psi, const qd_c128* expV, const qd_c128* expVh,
                  const qd_c128* expK, int nx, int B, int nt, int nout,
                  qd_c128* snap, void* stream);
 
+/* ------------------------------------------------------------ DEOM / HEOM -- */
+/*
+ * RK4 propagation of B independent DEOM hierarchies (dissipaton equation of
+ * motion) sharing one bath, one H and the same coupling operators.
+ * Replaces DEOMSolver.run (pyqed/heom/deom.py:1072-1114) -> rk4 (:725-766) ->
+ * rem_cal / generate_dot_element (:641-673) with generate_time (:676-688).
+ *   ados   [B][nmax][ns][ns]  ADOs, in/out (ADO 0 = system density matrix)
+ *   minus, plus [nmax][K]     int32 neighbour tables: index of key -/+ e_k, -1 if absent
+ *   coef   [nmax][K][3]       cL, cR, cP prefactors (see deom.hip)
+ *   damp   [nmax]             -sum_k key_k expn_k
+ *   mode   [K]                int32 coupling-operator index of each dissipaton
+ *   H, Hdip [ns][ns]; Q, Qdip [nmod][ns][ns]  (Hdip / Qdip may be NULL)
+ *   fsys, fcoup  HOST arrays [nsteps][3]: pulse values at t, t+dt/2, t+dt of
+ *                each step (NULL when the dipole is NULL)
+ *   rho_sys [B][nsteps+1][ns][ns]  ADO 0 after every step (row 0 = initial), or NULL
+ *   p1 [ns][ns], trace [B][nsteps+1]  Tr(p1 rho_0) per step (deom.py:1100,1113), or NULL
+ * Constraints: ns <= 16, nmod <= 8.
+ */
+int qd_deom_rk4(qd_c128* ados, int B, int nmax, int K, int ns,
+                const int32_t* minus, const int32_t* plus, const qd_c128* coef,
+                const qd_c128* damp, const int32_t* mode, int nmod,
+                const qd_c128* H, const qd_c128* Hdip, const qd_c128* Q,
+                const qd_c128* Qdip, const qd_c128* fsys, const qd_c128* fcoup,
+                double dt, int nsteps, qd_c128* rho_sys, const qd_c128* p1,
+                qd_c128* trace, void* stream);
+
 /* ------------------------------------------------------------ response --- */
 /*
  * SOS Liouville-space propagator U[a][b][k] = sum_j U1[a][j] e^{lam_j t_k} U2[j][b]

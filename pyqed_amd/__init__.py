@@ -2,8 +2,10 @@
 
 Hot path (HIP, libqdyn.so): Lindblad RK4, ....
 """
+from .deom import Bath, DEOMSolver
 from .mol import Result, load_result
+from .wpd import SPO, SPO2
 from .oqs import LindbladSolver, RedfieldSolver, glf_rk4, lindblad_rk4
 
-__all__ = ["Result", "load_result", "LindbladSolver", "RedfieldSolver", "glf_rk4", "lindblad_rk4"]
+__all__ = ["Bath", "DEOMSolver", "SPO", "SPO2", "Result", "load_result", "LindbladSolver", "RedfieldSolver", "glf_rk4", "lindblad_rk4"]
 __version__ = "0.1.0"

@@ -1,0 +1,224 @@
+// deom.hip — DEOM / HEOM auxiliary-density-operator (ADO) hierarchy, RK4.
+//
+// Replaces DEOMSolver.run's loop (pyqed/heom/deom.py:1107-1113) over rk4
+// (deom.py:725-766) whose RHS is rem_cal / generate_dot_element
+// (deom.py:641-673) with the time-dependent H(t), Q(t) of generate_time
+// (deom.py:676-688).  Per ADO n with index vector key_n:
+//   d rho_n = damp_n rho_n - i[H(t), rho_n]
+//           + sum_{k: n_k>0} ( cL_nk Q_m rho_{n-e_k} + cR_nk rho_{n-e_k} Q_m )
+//           + sum_{k: tier<L} cP_nk [Q_m, rho_{n+e_k}]
+// with damp_n = -sum_k n_k expn_k, cL = -i sqrt(n_k)/sqrt(etaa_k) etal_k,
+// cR = +i sqrt(n_k)/sqrt(etaa_k) etar_k, cP = -i sqrt(n_k+1) sqrt(etaa_k),
+// m = mode[k].  The host builds the bit-exact neighbour tables minus/plus
+// (hash of key -/+ e_k, -1 when absent) and the coefficient tables once.
+//
+// One launch per RK4 stage (the stage needs every ADO of the previous stage);
+// one thread per matrix element (b, n, i, j); H(t)/Q(t) are assembled in LDS
+// per workgroup from H + f_sys(t) Hdip, Q + f_coup(t) Qdip.  The fused
+// epilogue does the RK4 bookkeeping (acc, next-stage state, final update) and
+// records rho_0 (the system density matrix) after every step.
+#include "qd_common.hpp"
+
+namespace qd {
+namespace {
+
+constexpr int DEOM_MAX_NS = 16;
+constexpr int DEOM_MAX_NMOD = 8;
+constexpr int DEOM_TPB = 256;
+
+struct DeomParams {
+  const c128* rho;     // [B][nmax][ns][ns]   state at step start (stage 0 input)
+  c128* rho_out;       // same buffer as rho (written at stage 3 only)
+  const c128* xin;     // stage input (stage 0: rho)
+  c128* xout;          // next-stage input
+  c128* acc;           // RK4 accumulator
+  const int* minus;    // [nmax][K]
+  const int* plus;     // [nmax][K]
+  const c128* coef;    // [nmax][K][3] : cL, cR, cP
+  const c128* damp;    // [nmax]
+  const int* mode;     // [K]
+  const c128* H;       // [ns][ns]
+  const c128* Hdip;    // [ns][ns] or null
+  const c128* Q;       // [nmod][ns][ns]
+  const c128* Qdip;    // [nmod][ns][ns] or null
+  c128 fs, fc;         // pulse values at this stage's time
+  c128* snap;          // [B][nsteps+1][ns][ns] (rho_0 after each step) or null
+  int B, nmax, K, ns, nmod, stage, step, nsteps;
+  double dt;
+};
+
+__global__ __launch_bounds__(DEOM_TPB) void deom_stage_kernel(DeomParams p) {
+  __shared__ c128 sH[DEOM_MAX_NS * DEOM_MAX_NS];
+  __shared__ c128 sQ[DEOM_MAX_NMOD * DEOM_MAX_NS * DEOM_MAX_NS];
+  const int ns = p.ns, ns2 = ns * ns;
+  for (int e = threadIdx.x; e < ns2; e += blockDim.x)
+    sH[e] = p.Hdip ? cadd(p.H[e], cmul(p.Hdip[e], p.fs)) : p.H[e];
+  for (int e = threadIdx.x; e < p.nmod * ns2; e += blockDim.x)
+    sQ[e] = p.Qdip ? cadd(p.Q[e], cmul(p.Qdip[e], p.fc)) : p.Q[e];
+  __syncthreads();
+
+  const size_t tot = (size_t)p.B * p.nmax * ns2;
+  const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (e >= tot) return;
+  const int j = (int)(e % ns), i = (int)((e / ns) % ns);
+  const size_t bn = e / ns2;                  // b * nmax + n
+  const int n = (int)(bn % p.nmax);
+  const size_t bbase = (bn - n) * ns2;        // start of batch member b
+  const c128* X = p.xin + bbase;
+  const c128* xn = X + (size_t)n * ns2;
+
+  // damping + coherent part: damp_n x - i (H x - x H)
+  c128 d = cmul(p.damp[n], xn[i * ns + j]);
+  c128 comm = cmk(0, 0);
+  for (int l = 0; l < ns; ++l)
+    comm = cadd(comm, csub(cmul(sH[i * ns + l], xn[l * ns + j]), cmul(xn[i * ns + l], sH[l * ns + j])));
+  d = cadd(d, cmulmi(comm));
+
+  const int* mi = p.minus + (size_t)n * p.K;
+  const int* pl = p.plus + (size_t)n * p.K;
+  const c128* cf = p.coef + (size_t)n * p.K * 3;
+  for (int k = 0; k < p.K; ++k) {
+    const c128* Qm = sQ + p.mode[k] * ns2;
+    const int nm = mi[k];
+    if (nm >= 0) {
+      const c128* y = X + (size_t)nm * ns2;
+      c128 qy = cmk(0, 0), yq = cmk(0, 0);
+      for (int l = 0; l < ns; ++l) {
+        qy = cadd(qy, cmul(Qm[i * ns + l], y[l * ns + j]));
+        yq = cadd(yq, cmul(y[i * ns + l], Qm[l * ns + j]));
+      }
+      d = cadd(d, cadd(cmul(cf[3 * k + 0], qy), cmul(cf[3 * k + 1], yq)));
+    }
+    const int np = pl[k];
+    if (np >= 0) {
+      const c128* y = X + (size_t)np * ns2;
+      c128 c = cmk(0, 0);
+      for (int l = 0; l < ns; ++l)
+        c = cadd(c, csub(cmul(Qm[i * ns + l], y[l * ns + j]), cmul(y[i * ns + l], Qm[l * ns + j])));
+      d = cadd(d, cmul(cf[3 * k + 2], c));
+    }
+  }
+
+  // RK4 bookkeeping (deom.py:735-766 order: ddos1 = k1; ddos1 += 2 k2; += 2 k3; += k4; ddos += ddos1*dt/6)
+  const double dt = p.dt;
+  const c128 r0 = p.rho[e];
+  if (p.stage == 0) {
+    p.acc[e] = d;
+    p.xout[e] = cadd(r0, cscale(d, dt / 2));
+  } else if (p.stage == 1) {
+    p.acc[e] = cadd(p.acc[e], cscale(d, 2.0));
+    p.xout[e] = cadd(r0, cscale(d, dt / 2));
+  } else if (p.stage == 2) {
+    p.acc[e] = cadd(p.acc[e], cscale(d, 2.0));
+    p.xout[e] = cadd(r0, cscale(d, dt));
+  } else {
+    const c128 a = cadd(p.acc[e], d);
+    const c128 r1 = cadd(r0, cscale(cscale(a, dt), 1.0 / 6.0));
+    p.rho_out[e] = r1;
+    if (p.snap && n == 0) {
+      const size_t b = bn / p.nmax;
+      p.snap[(b * (p.nsteps + 1) + p.step + 1) * ns2 + i * ns + j] = r1;
+    }
+  }
+}
+
+__global__ void deom_snap0_kernel(const c128* rho, c128* snap, int B, int nmax, int ns, int nsteps) {
+  const int ns2 = ns * ns;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < B * ns2; e += gridDim.x * blockDim.x) {
+    const int b = e / ns2, ij = e % ns2;
+    snap[(size_t)b * (nsteps + 1) * ns2 + ij] = rho[(size_t)b * nmax * ns2 + ij];
+  }
+}
+
+// trace[b][s] = Tr(p1 rho_0(s)) = sum_ij p1[j][i] rho[i][j]   (deom.py:1100,1113)
+__global__ void deom_trace_kernel(const c128* snap, const c128* p1, int B, int ns, int nsteps, c128* trace) {
+  const int ns2 = ns * ns;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < B * (nsteps + 1); e += gridDim.x * blockDim.x) {
+    const c128* r = snap + (size_t)e * ns2;
+    c128 s = cmk(0, 0);
+    for (int i = 0; i < ns; ++i)
+      for (int j = 0; j < ns; ++j) s = cadd(s, cmul(p1[j * ns + i], r[i * ns + j]));
+    trace[e] = s;
+  }
+}
+
+}  // namespace
+}  // namespace qd
+
+using namespace qd;
+
+extern "C" int qd_deom_rk4(qd_c128* ados, int B, int nmax, int K, int ns, const int32_t* minus, const int32_t* plus,
+                           const qd_c128* coef, const qd_c128* damp, const int32_t* mode, int nmod, const qd_c128* H,
+                           const qd_c128* Hdip, const qd_c128* Q, const qd_c128* Qdip, const qd_c128* fsys,
+                           const qd_c128* fcoup, double dt, int nsteps, qd_c128* rho_sys, const qd_c128* p1,
+                           qd_c128* trace, void* stream) {
+  QD_CHECK_ARG(ados && minus && plus && coef && damp && mode && H && Q, "qd_deom_rk4: null pointer");
+  QD_CHECK_ARG(B >= 1 && nmax >= 1 && K >= 1 && nsteps >= 0, "qd_deom_rk4: bad sizes B=%d nmax=%d K=%d", B, nmax, K);
+  QD_CHECK_ARG(ns >= 1 && ns <= DEOM_MAX_NS, "qd_deom_rk4: ns=%d outside [1, %d]", ns, DEOM_MAX_NS);
+  QD_CHECK_ARG(nmod >= 1 && nmod <= DEOM_MAX_NMOD, "qd_deom_rk4: nmod=%d outside [1, %d]", nmod, DEOM_MAX_NMOD);
+  QD_CHECK_ARG(!Hdip || fsys, "qd_deom_rk4: Hdip given without fsys");
+  QD_CHECK_ARG(!Qdip || fcoup, "qd_deom_rk4: Qdip given without fcoup");
+  QD_CHECK_ARG(!trace || p1, "qd_deom_rk4: trace requested without p1");
+  hipStream_t st = (hipStream_t)stream;
+  const size_t ns2 = (size_t)ns * ns;
+  const size_t tot = (size_t)B * nmax * ns2;
+  const bool need_snap = rho_sys || trace;
+  const size_t snap_elems = need_snap && !rho_sys ? (size_t)B * (nsteps + 1) * ns2 : 0;
+  void* w = nullptr;
+  int rc = workspace(WS_DEOM, (3 * tot + snap_elems) * sizeof(c128), &w);
+  if (rc) return rc;
+  c128* acc = (c128*)w;
+  c128* xs[2] = {acc + tot, acc + 2 * tot};
+  c128* snap = rho_sys ? (c128*)rho_sys : (need_snap ? acc + 3 * tot : nullptr);
+  // fsys/fcoup are host arrays [nsteps][3] (values at t, t+dt/2, t+dt): kernel args per stage
+  const qd_c128* fs_h = fsys;
+  const qd_c128* fc_h = fcoup;
+  if (snap) {
+    hipLaunchKernelGGL(deom_snap0_kernel, dim3(std::max(1, std::min(1024, (int)((B * ns2 + 255) / 256)))), dim3(256),
+                       0, st, (const c128*)ados, snap, B, nmax, ns, nsteps);
+    QD_HIP(hipGetLastError());
+  }
+  DeomParams p;
+  p.rho = (const c128*)ados;
+  p.rho_out = (c128*)ados;
+  p.acc = acc;
+  p.minus = minus;
+  p.plus = plus;
+  p.coef = (const c128*)coef;
+  p.damp = (const c128*)damp;
+  p.mode = mode;
+  p.H = (const c128*)H;
+  p.Hdip = (const c128*)Hdip;
+  p.Q = (const c128*)Q;
+  p.Qdip = (const c128*)Qdip;
+  p.snap = snap;
+  p.B = B;
+  p.nmax = nmax;
+  p.K = K;
+  p.ns = ns;
+  p.nmod = nmod;
+  p.nsteps = nsteps;
+  p.dt = dt;
+  const int grid = (int)((tot + DEOM_TPB - 1) / DEOM_TPB);
+  static const int stage_time[4] = {0, 1, 1, 2};
+  for (int s = 0; s < nsteps; ++s) {
+    p.step = s;
+    for (int stage = 0; stage < 4; ++stage) {
+      p.stage = stage;
+      p.xin = stage == 0 ? (const c128*)ados : xs[(stage - 1) & 1];
+      p.xout = xs[stage & 1];
+      const int ti = s * 3 + stage_time[stage];
+      p.fs = fs_h ? cmk(fs_h[ti].re, fs_h[ti].im) : cmk(0, 0);
+      p.fc = fc_h ? cmk(fc_h[ti].re, fc_h[ti].im) : cmk(0, 0);
+      hipLaunchKernelGGL(deom_stage_kernel, dim3(grid), dim3(DEOM_TPB), 0, st, p);
+      QD_HIP(hipGetLastError());
+    }
+  }
+  if (trace) {
+    const int n = B * (nsteps + 1);
+    hipLaunchKernelGGL(deom_trace_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0, st,
+                       (const c128*)snap, (const c128*)p1, B, ns, nsteps, (c128*)trace);
+    QD_HIP(hipGetLastError());
+  }
+  return QD_OK;
+}

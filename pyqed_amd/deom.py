@@ -1,0 +1,331 @@
+"""DEOM / HEOM hierarchy on MI355X (drop-in for pyqed/heom/deom.py Bath, DEOMSolver).
+
+Host (setup, as the reference): Pade decomposition of the bath correlation
+function (sympy), the graded ADO index and its neighbour tables.  Propagation:
+libqdyn qd_deom_rk4 (one kernel launch per RK4 stage).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._util import default_device, to_numpy
+
+
+# --------------------------------------------------------------------------- bath
+def _tridiag_eigs_desc(offdiag, size):
+    m = np.diag(offdiag, -1) + np.diag(offdiag, 1) if size > 1 else np.zeros((1, 1))
+    return np.sort(np.linalg.eigvalsh(m))[::-1]
+
+
+def matsubara_approximation_distribution(N, BoseFermi=1):
+    """Matsubara poles/residues (heom/deom.py:84-101)."""
+    if BoseFermi == 1:
+        return np.array([2 * (i + 1) * np.pi for i in range(N)]), np.ones(N)
+    return np.array([(2 * i + 1) * np.pi for i in range(N)]), np.ones(N)
+
+
+def pade_approximation_distribution(N, BoseFermi=1, pade=1):
+    """[N-1/N] (pade=1) or [N/N] (pade=2) Pade spectrum decomposition of the Bose/Fermi
+    function (Hu, Xu, Yan, JCP 133, 101106 (2010)); same poles/residues as heom/deom.py:104-206.
+
+    Poles xi_j = 2/eps_j from the N largest eigenvalues of the tridiagonal matrix with
+    off-diagonals 1/sqrt((a+2i)(a+2i+2)), a = 3 (Bose) or 1 (Fermi); zeta from the second
+    matrix (a+2); residue_j = (s/2) prod_k (zeta_k^2 - xi_j^2) / prod_{k != j} (xi_k^2 - xi_j^2).
+    """
+    if N < 0 or BoseFermi not in (1, 2) or pade not in (0, 1, 2, 3):
+        raise ValueError("N or BoseFermi or pade has wrong value!")
+    if pade == 0:
+        return matsubara_approximation_distribution(N, BoseFermi)
+    if pade == 3:
+        raise NotImplementedError("pade=3 (extended PSD) is not implemented in pyqed_amd")
+    if N == 0:
+        return [], []
+    M = 2 * N + pade // 2
+    a = 3.0 if BoseFermi == 1 else 1.0
+    off = np.array([1.0 / math.sqrt((a + 2.0 * i) * (a + 2.0 * i + 2.0)) for i in range(M - 1)])
+    xi = 2.0 / _tridiag_eigs_desc(off, M)[:N]
+    xi2 = xi * xi
+    M2 = M - 1
+    a2 = a + 2.0
+    off2 = np.array([1.0 / math.sqrt((a2 + 2.0 * i) * (a2 + 2.0 * i + 2.0)) for i in range(M2 - 1)])
+    nz = M2 // 2
+    zeta2 = (2.0 / _tridiag_eigs_desc(off2, M2)[:nz]) ** 2
+    if BoseFermi == 1:
+        s = N * (2.0 * N + 3.0) if pade == 1 else 1.0 / (4.0 * (N + 1.0) * (2.0 * N + 3.0))
+    else:
+        s = N * (2.0 * N + 1.0) if pade == 1 else 1.0 / (4.0 * (N + 1.0) * (2.0 * N + 1.0))
+    resi = np.zeros(N)
+    for j in range(N):
+        num = np.prod([zeta2[k] - xi2[j] for k in range(nz)]) if nz else 1.0
+        den = np.prod([xi2[k] - xi2[j] for k in range(N) if k != j]) if N > 1 else 1.0
+        resi[j] = 0.5 * s * num / den
+    return xi, resi
+
+
+def function_bose(x, pole, resi):
+    """Pade-approximated Bose function x n(x) / ... (heom/deom.py:67-72)."""
+    return 1 / x + 0.5 + sum(2.0 * resi[i] * x / (x ** 2 + pole[i] ** 2) for i in range(len(pole)))
+
+
+def decompose_spectrum_pade(spe, w_sp, beta, npsd, pade=1, bose_fermi=1):
+    """Bath correlation as a sum of exponentials (heom/deom.py:226-307): (etal, etar, etaa, expn).
+
+    Poles of the spectral density in the lower half plane give the 'physical' exponents
+    expn = i*pole (sorted by |Im| descending; complex pairs first, then real ones), each
+    weighted by its residue times the Pade Bose function; the npsd Pade poles of the Bose
+    function give the remaining exponents pole*T."""
+    import sympy as sp
+    re_part, im_part = sp.cancel(spe).as_real_imag()
+    part = re_part if im_part == 0 else im_part
+    numer, denom = sp.cancel(sp.factor(part)).as_numer_denom()
+    roots = np.array([complex(z) for z in sp.nroots(denom)])
+    expn = np.array([1j * z for z in roots if z.imag < 0])
+    order = np.argsort(np.abs(np.imag(expn)))[::-1]
+    mag = np.sort(np.abs(np.imag(expn)))[::-1]
+    cc = expn[order[mag != 0]]
+    real = expn[order[mag == 0]]
+    expn_all = list(expn[order])
+    pole, resi = pade_approximation_distribution(npsd, bose_fermi, pade)
+    T = 1.0 / beta
+    num_f = sp.lambdify(w_sp, numer, "numpy")
+
+    def residue_weight(x):
+        w = -1j * x
+        others = roots[np.abs(roots + 1j * x) > 1e-14]
+        val = -2j * complex(num_f(w)) / np.prod(w - others)
+        return complex(val * function_bose(-1j * x / T, pole, resi))
+
+    etal, etar, etaa = [], [], []
+    for ii in range(0, len(cc), 2):
+        e0, e1 = residue_weight(cc[ii]), residue_weight(cc[ii + 1])
+        etal += [e0, e1]
+        etar += [np.conj(e1), np.conj(e0)]
+        etaa += [np.sqrt(abs(e0) * abs(np.conj(e1))), np.sqrt(abs(e1) * abs(np.conj(e0)))]
+    for x in real:
+        e = residue_weight(x)
+        etal.append(e)
+        etar.append(np.conj(e))
+        etaa.append(np.sqrt(abs(e) * abs(np.conj(e))))
+    for j in range(len(pole)):
+        z = -1j * pole[j] * T
+        fz = complex(num_f(z)) / np.prod(z - roots)
+        expn_all.append(pole[j] * T)
+        e = -2j * resi[j] * T * fz
+        etal.append(e)
+        etar.append(np.conj(e))
+        etaa.append(abs(e))
+    return np.array(etal), np.array(etar), np.array(etaa), np.array(expn_all)
+
+
+class Bath:
+    """Drop-in for pyqed.heom.deom.Bath (heom/deom.py:895-942), list form:
+    Bath([spe_1, ...], w_sp, [beta_1, ...], [npsd_1, ...], mode, function)."""
+
+    def __init__(self, spectrum_sp=None, w_sp=None, beta=None, npsd=None, mode=None, function=None):
+        self.bath = spectrum_sp
+        self.w_sp = w_sp
+        self.beta = beta
+        self.npsd = npsd
+        self.mode = mode
+        if isinstance(self.bath, list) and isinstance(self.beta, list) and isinstance(self.npsd, list):
+            if function is None:
+                function = [decompose_spectrum_pade] * len(self.bath)
+            parts = [function[i](self.bath[i], self.w_sp, self.beta[i], self.npsd[i]) for i in range(len(self.bath))]
+            self.etal, self.etar, self.etaa, self.expn = (
+                np.concatenate([np.asarray(p[c], dtype=np.complex128) for p in parts]) for c in range(4))
+            if self.mode is None:
+                raise ValueError("mode is not set!")
+            if len(self.mode) != len(self.expn):
+                raise ValueError("the length of mode is not equal to the number of dissipatons!")
+            self.mode = np.asarray(self.mode, dtype=np.int64)
+        else:
+            self.etal, self.etar, self.etaa, self.expn = decompose_spectrum_pade(self.bath, self.w_sp, self.beta,
+                                                                                 self.npsd)
+            self.mode = np.zeros_like(self.expn, dtype=np.int64)
+
+
+# --------------------------------------------------------------------------- ADO index
+def comb_table(L, K):
+    n = K + L + 1
+    c = np.zeros((n, n), dtype=np.int64)
+    c[:, 0] = 1
+    for i in range(1, n):
+        c[i, 1:] = c[i - 1, 1:] + c[i - 1, :-1]
+    return c
+
+
+def ado_hash(keys, comb):
+    """heom/deom.py:555-566 vectorised: h = sum_i comb[S_i + i, i + 1], S = cumsum(key)."""
+    keys = np.atleast_2d(keys)
+    S = np.cumsum(keys, axis=1)
+    idx = np.arange(keys.shape[1])
+    return comb[S + idx, idx + 1].sum(axis=1)
+
+
+def ado_tables(L, K):
+    """(keys [nmax, K] int64 bit-identical to gen_keys, minus/plus [nmax, K] int32, comb)."""
+    comb = comb_table(L, K)
+    nmax = int(comb[L + K, L])
+    tier = np.zeros((1, K), dtype=np.int64)
+    keys = np.zeros((nmax, K), dtype=np.int64)
+    for _ in range(L):
+        keys[ado_hash(tier, comb)] = tier
+        tier = np.unique((tier[:, None, :] + np.eye(K, dtype=np.int64)[None]).reshape(-1, K), axis=0)
+    keys[ado_hash(tier, comb)] = tier
+    tiers = keys.sum(axis=1)
+    eye = np.eye(K, dtype=np.int64)
+    minus = np.full((nmax, K), -1, dtype=np.int32)
+    plus = np.full((nmax, K), -1, dtype=np.int32)
+    for k in range(K):
+        has = keys[:, k] > 0
+        minus[has, k] = ado_hash(keys[has] - eye[k], comb)
+        up = tiers < L
+        plus[up, k] = ado_hash(keys[up] + eye[k], comb)
+    return keys, minus, plus, comb
+
+
+def ado_coefficients(keys, etal, etar, etaa, expn, L):
+    """Per-(ADO, dissipaton) prefactors of generate_dot_element (heom/deom.py:641-664)."""
+    n = keys.astype(float)
+    sq_e = np.sqrt(np.asarray(etaa, dtype=complex))
+    cm = 1j * np.sqrt(n) / sq_e[None, :]
+    coef = np.empty(keys.shape + (3,), dtype=complex)
+    coef[..., 0] = -cm * etal[None, :]
+    coef[..., 1] = cm * etar[None, :]
+    coef[..., 2] = -1j * np.sqrt(n + 1) * sq_e[None, :]
+    damp = -np.sum(keys * np.asarray(expn)[None, :], axis=1)
+    return coef, damp
+
+
+# --------------------------------------------------------------------------- solver
+class DEOMSolver:
+    """Drop-in for pyqed.heom.deom.DEOMSolver (heom/deom.py:953-1125)."""
+
+    def __init__(self, system=None, system_dipole=None, bath=None, coupling=None, coupling_dipole=None,
+                 pulse_system_func=None, pulse_coupling_func=None, lmax=None):
+        self.system = system
+        self.system_dipole = system_dipole
+        self.coupling = coupling
+        self.coupling_dipole = coupling_dipole
+        self.pulse_system_func = pulse_system_func
+        self.pulse_coupling_func = pulse_coupling_func
+        self.lmax = lmax
+        self.nsys = 0
+        self.nmax = 1
+        self.nind = 0
+        self.nmod = 0
+        self.bath = bath
+        self.comb_list = []
+        self.keys = None
+        self.ddos = None
+
+    def set_hierarchy(self, lmax):
+        self.lmax = lmax
+
+    def set_system(self, system):
+        self.system = np.array(system, dtype=np.complex128)
+
+    def set_system_dipole(self, system_dipole):
+        self.system_dipole = np.array(system_dipole, dtype=np.complex128)
+
+    def set_coupling(self, coupling):
+        self.coupling = np.array(coupling, dtype=np.complex128)
+
+    def set_coupling_dipole(self, coupling_dipole):
+        self.coupling_dipole = np.array(coupling_dipole, dtype=np.complex128)
+
+    def set_pulse_system_func(self, f):
+        self.pulse_system_func = f
+
+    def set_pulse_coupling_func(self, f):
+        self.pulse_coupling_func = f
+
+    def check_(self):
+        if self.system is None:
+            raise ValueError('System Hamiltonian is not set.')
+        if self.coupling is None:
+            raise ValueError('system bath interaction operator is not set.')
+        self.nsys = np.shape(self.system)[0]
+        self.nind = len(self.bath.expn)
+        self.nmod = int(np.max(self.bath.mode)) + 1
+
+    def init_(self):
+        keys, minus, plus, comb = ado_tables(self.lmax, self.nind)
+        self.keys, self._minus, self._plus, self.comb_list = keys, minus, plus, comb
+        self.nmax = len(keys)
+
+    @staticmethod
+    def _dip_values(dip, func, nt, dt, shape):
+        if dip is None or func is None or not np.any(np.asarray(dip)):
+            return None, None
+        f = np.empty((nt, 3), dtype=complex)
+        for s in range(nt):
+            t = s * dt
+            f[s] = [func(t), func(t + dt / 2), func(t + dt)]
+        return np.asarray(dip, dtype=complex).reshape(shape), f
+
+    def run(self, rho0, dt, nt, p1=None):
+        """heom/deom.py:1072-1114: returns (t_save (nt+1,), ddos_save) with ddos_save the
+        Tr(p1 rho_0) values (p1 given) or the list of rho_0 copies.  As in the reference,
+        a complex ndarray rho0 is overwritten with the final system density matrix."""
+        self.check_()
+        self.init_()
+        out = self.run_batch(np.asarray(rho0)[None], dt, nt, p1)
+        t_save, saved = out
+        saved = saved[0]
+        if isinstance(rho0, np.ndarray) and np.iscomplexobj(rho0) and rho0.flags.writeable:
+            rho0[...] = self.ddos[0][0]
+        self.ddos = self.ddos[0]
+        if p1 is None:
+            return t_save, [saved[k] for k in range(nt + 1)]
+        return t_save, saved
+
+    def run_batch(self, rho0, dt, nt, p1=None):
+        """Extension: B independent hierarchies (rho0 [B, ns, ns]) in one launch sequence."""
+        if self.keys is None:
+            self.check_()
+            self.init_()
+        dev = default_device()
+        _lib.ensure_device(dev)
+        ns, K, nmax = self.nsys, self.nind, self.nmax
+        rho0 = np.asarray(rho0, dtype=complex)
+        B = rho0.shape[0]
+        b = self.bath
+        coef, damp = ado_coefficients(self.keys, np.asarray(b.etal), np.asarray(b.etar), np.asarray(b.etaa),
+                                      np.asarray(b.expn), self.lmax)
+        c128 = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=complex))).to(dev)
+        i32 = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=np.int32))).to(dev)
+        ados = torch.zeros((B, nmax, ns, ns), dtype=torch.complex128, device=dev)
+        ados[:, 0] = c128(rho0)
+        H = c128(self.system)
+        Q = c128(np.asarray(self.coupling, dtype=complex).reshape(-1, ns, ns))
+        nmod = Q.shape[0]
+        Hdip, fs = self._dip_values(self.system_dipole, self.pulse_system_func, nt, dt, (ns, ns))
+        Qdip, fc = self._dip_values(self.coupling_dipole, self.pulse_coupling_func, nt, dt, (nmod, ns, ns))
+        Hdip_t = c128(Hdip) if Hdip is not None else None
+        Qdip_t = c128(Qdip) if Qdip is not None else None
+        fs = np.ascontiguousarray(fs) if fs is not None else None
+        fc = np.ascontiguousarray(fc) if fc is not None else None
+        rho_sys = torch.empty((B, nt + 1, ns, ns), dtype=torch.complex128, device=dev)
+        p1_t = c128(p1) if p1 is not None else None
+        trace = torch.empty((B, nt + 1), dtype=torch.complex128, device=dev) if p1 is not None else None
+        tabs = (i32(self._minus), i32(self._plus), c128(coef), c128(damp), i32(b.mode))
+        with torch.cuda.device(dev):
+            rc = _lib.load().qd_deom_rk4(
+                ados.data_ptr(), B, nmax, K, ns, tabs[0].data_ptr(), tabs[1].data_ptr(), tabs[2].data_ptr(),
+                tabs[3].data_ptr(), tabs[4].data_ptr(), nmod, H.data_ptr(), _lib.ptr(Hdip_t), Q.data_ptr(),
+                _lib.ptr(Qdip_t), fs.ctypes.data if fs is not None else None,
+                fc.ctypes.data if fc is not None else None, float(dt), int(nt), rho_sys.data_ptr(),
+                _lib.ptr(p1_t), _lib.ptr(trace), _lib.stream_ptr(dev))
+        _lib.check(rc, "qd_deom_rk4")
+        torch.cuda.synchronize(dev)
+        self.ddos = ados.cpu().numpy()
+        t_save = np.arange(nt + 1) * dt
+        t_save[0] = 0
+        if p1 is not None:
+            return t_save, trace.cpu().numpy()
+        return t_save, rho_sys.cpu().numpy()

@@ -248,6 +248,100 @@ def spo1d_256_nout3():
     _spo1d_case("spo1d_256_nout3", n=256, nt=20, nout=3, dt=0.01)
 
 
+# ----------------------------------------------------------------- DEOM / HEOM
+def _drude_bath(lam, gam, beta, npsd):
+    import sympy as sp
+    from pyqed.heom.deom import Bath
+    w_sp = sp.symbols(r"\omega", real=True)
+    spe = 2 * lam * gam * w_sp / (gam ** 2 + w_sp ** 2)
+    # list form (the scalar form of Bath.__init__ fails at heom/deom.py:917: len() of a sympy expr)
+    return Bath([spe], w_sp, [beta], [npsd], [0] * (1 + npsd))
+
+
+@golden
+def deom_bath():
+    """Pade decomposition of a Drude bath (decompose_spectrum_pade, heom/deom.py:226-307)."""
+    out = {}
+    for lam, gam, tag in [(0.5, 1.0, "d4"), (1.0, 1.0, "ll"), (0.2, 2.0, "g2")]:
+        for npsd in [1, 2, 3, 4]:
+            b = _drude_bath(lam, gam, 1.0, npsd)
+            for k in ["etal", "etar", "etaa", "expn"]:
+                out[f"{tag}_n{npsd}_{k}"] = np.asarray(getattr(b, k), dtype=complex)
+    from pyqed.heom.deom import pade_approximation_distribution
+    for N in [1, 2, 3, 4, 6]:
+        pole, resi = pade_approximation_distribution(N, 1, 1)
+        out[f"pade_pole_{N}"] = np.asarray(pole)
+        out[f"pade_resi_{N}"] = np.asarray(resi)
+    save("deom_bath", **out)
+
+
+@golden
+def deom_keys():
+    """Graded ADO index (init_/gen_keys, heom/deom.py:1048-1064, 555-638)."""
+    from pyqed.heom.deom import gen_keys
+    out = {}
+    for L, K in [(3, 2), (10, 3), (4, 3), (12, 5)]:
+        combmax = K + L + 1
+        comb = np.zeros((combmax, combmax), dtype=np.int64)
+        comb[0, 0] = 1
+        for i in range(1, combmax):
+            for j in range(1, combmax):
+                comb[i, j] = comb[i - 1, j] + comb[i - 1, j - 1]
+            comb[i, 0] = 1
+        nmax = comb[L + K, L]
+        keys = np.zeros((nmax, K), dtype=np.int64)
+        gen_keys(keys, L, K, comb)
+        out[f"keys_L{L}_K{K}"] = keys
+    save("deom_keys", **out)
+
+
+def _deom_case(lmax, npsd, nt, dt, pulses=False, p1=True, lam=0.5, gam=1.0, beta=1.0):
+    from pyqed.heom.deom import DEOMSolver
+    s0 = np.eye(2, dtype=complex)
+    sx = np.array([[0, 1], [1, 0]], dtype=complex)
+    sz = np.array([[1, 0], [0, -1]], dtype=complex)
+    H = sz + sx
+    bath = _drude_bath(lam, gam, beta, npsd)
+    rho0 = np.zeros((2, 2), dtype=complex)
+    rho0[0, 0] = 1
+    if pulses:
+        fs, fc = (lambda t: 0.3 * np.sin(2 * t)), (lambda t: 0.1 * np.cos(t))
+        sdip, cdip = sx.copy(), np.array([sz])
+    else:
+        fs, fc = (lambda t: 0), (lambda t: 0)
+        sdip, cdip = np.zeros((2, 2), complex), np.zeros((1, 2, 2), complex)
+    solver = DEOMSolver(H, sdip, bath, np.array([sx]), cdip, fs, fc, lmax)
+    P1 = np.array([[1, 0], [0, 0]], dtype=complex)
+    t_save, ddos_save = solver.run(rho0.copy(), dt, nt, P1 if p1 else None)
+    out = dict(H=H, Q=np.array([sx]), sdip=sdip, cdip=cdip, lmax=lmax, npsd=npsd, dt=dt, nt=nt, lam=lam,
+               gam=gam, beta=beta, pulses=pulses, t_save=t_save, nmax=solver.nmax,
+               etal=bath.etal, etar=bath.etar, etaa=bath.etaa, expn=bath.expn)
+    if p1:
+        out["trace_p1"] = np.asarray(ddos_save)
+    else:
+        out["rho_sys"] = np.array([np.asarray(x) for x in ddos_save])
+    out["ado_final"] = np.array([np.asarray(x.toarray() if hasattr(x, "toarray") else x) for x in solver.ddos])
+    return out
+
+
+@golden
+def deom_run_small():
+    save("deom_run_small", **_deom_case(lmax=4, npsd=2, nt=20, dt=0.01))
+
+
+@golden
+def deom_run_pulsed():
+    save("deom_run_pulsed", **_deom_case(lmax=3, npsd=1, nt=15, dt=0.02, pulses=True, p1=False))
+
+
+@golden
+def deom_run_bench():
+    """BASELINE config d4 (L=12, npsd=4 -> K=5, 6188 ADOs), 3 steps (reference ~0.3 steps/s)."""
+    out = _deom_case(lmax=12, npsd=4, nt=3, dt=0.01)
+    out.pop("ado_final")
+    save("deom_run_bench", **out)
+
+
 if __name__ == "__main__":
     names = sys.argv[1:] or list(GENERATORS)
     for n in names:

@@ -1,0 +1,57 @@
+"""Host-side DEOM setup (no GPU): Pade bath decomposition and the bit-exact ADO index."""
+import numpy as np
+import pytest
+import sympy as sp
+
+from conftest import load_golden, relerr
+
+
+def _bath(lam, gam, beta, npsd):
+    from pyqed_amd.deom import Bath
+    w = sp.symbols(r"\omega", real=True)
+    return Bath([2 * lam * gam * w / (gam ** 2 + w ** 2)], w, [beta], [npsd], [0] * (1 + npsd))
+
+
+def test_pade_poles_residues_match_reference():
+    from pyqed_amd.deom import pade_approximation_distribution
+    g = load_golden("deom_bath")
+    for N in [1, 2, 3, 4, 6]:
+        pole, resi = pade_approximation_distribution(N, 1, 1)
+        assert relerr(pole, g[f"pade_pole_{N}"]) < 1e-13
+        assert relerr(resi, g[f"pade_resi_{N}"]) < 1e-12
+
+
+@pytest.mark.parametrize("tag,lam,gam", [("d4", 0.5, 1.0), ("ll", 1.0, 1.0), ("g2", 0.2, 2.0)])
+def test_bath_decomposition_matches_reference(tag, lam, gam):
+    g = load_golden("deom_bath")
+    for npsd in [1, 2, 3, 4]:
+        b = _bath(lam, gam, 1.0, npsd)
+        for k in ["etal", "etar", "etaa", "expn"]:
+            assert relerr(getattr(b, k), g[f"{tag}_n{npsd}_{k}"]) < 1e-12, (npsd, k)
+
+
+@pytest.mark.parametrize("L,K", [(3, 2), (10, 3), (4, 3), (12, 5)])
+def test_ado_keys_bit_exact(L, K):
+    from pyqed_amd.deom import ado_hash, ado_tables
+    g = load_golden("deom_keys")
+    keys, minus, plus, comb = ado_tables(L, K)
+    assert keys.dtype == np.int64
+    assert np.array_equal(keys, g[f"keys_L{L}_K{K}"])
+    assert np.array_equal(ado_hash(keys, comb), np.arange(len(keys)))
+    # neighbour tables: key -/+ e_k exactly where defined
+    for k in range(K):
+        has = minus[:, k] >= 0
+        assert np.array_equal(has, keys[:, k] > 0)
+        e = np.eye(K, dtype=np.int64)[k]
+        assert np.array_equal(keys[minus[has, k]], keys[has] - e)
+        up = plus[:, k] >= 0
+        assert np.array_equal(up, keys.sum(1) < L)
+        assert np.array_equal(keys[plus[up, k]], keys[up] + e)
+
+
+def test_tier_sizes_bench_config():
+    from pyqed_amd.deom import ado_tables
+    keys, *_ = ado_tables(12, 5)
+    assert len(keys) == 6188
+    sizes = np.bincount(keys.sum(1))
+    assert list(sizes) == [1, 5, 15, 35, 70, 126, 210, 330, 495, 715, 1001, 1365, 1820]
