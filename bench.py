@@ -232,6 +232,57 @@ def cpu_baseline_spo2(n=256, dt=0.05, budget_s=5.0):
             "sample": f"{k} Strang steps of the scipy.fftpack restatement of SPO2.run at {n}x{n}x2 in {el:.1f}s"}
 
 
+def bench_deom(dev, steps, batch):
+    """BASELINE config d4: spin-boson H = sz + sx, Q = sx, Drude lambda=0.5 gamma=1 beta=1, Pade npsd=4
+    (K=5), L=12 -> 6188 ADOs, dt=0.01.  Single hierarchy and a batch of independent hierarchies."""
+    import sympy as sp
+    import torch
+    from pyqed_amd.deom import Bath, DEOMSolver
+    w = sp.symbols(r"\omega", real=True)
+    bath = Bath([2 * 0.5 * 1.0 * w / (1.0 + w ** 2)], w, [1.0], [4], [0] * 5)
+    sx = np.array([[0, 1], [1, 0]], complex)
+    sz = np.diag([1.0, -1.0]).astype(complex)
+    sol = DEOMSolver(sz + sx, None, bath, np.array([sx]), None, None, None, 12)
+    rho0 = np.zeros((2, 2), complex)
+    rho0[0, 0] = 1
+    sol.run_batch(rho0[None], 0.01, 5)
+    res = {}
+    for B in (1, batch):
+        r = np.repeat(rho0[None], B, axis=0)
+        t0 = time.perf_counter()
+        sol.run_batch(r, 0.01, steps)
+        el = time.perf_counter() - t0
+        res[B] = el
+    nmax = sol.nmax
+    return {
+        "value": round(steps / res[1], 1), "unit": "RK4 steps/s (one hierarchy)",
+        "ado_steps_per_s_single": round(steps * nmax / res[1], 1),
+        "batched": {"hierarchies": batch, "ado_steps_per_s": round(steps * nmax * batch / res[batch], 1),
+                    "steps_per_s": round(steps / res[batch], 1)},
+        "config": {"workload": "deom_spin_boson_drude_L12_K5 (BASELINE.json configs[3])", "nmax": nmax, "K": 5,
+                   "L": 12, "dt": 0.01, "steps": steps},
+        "note": "wall time incl. host setup of tables and per-call transfers",
+    }
+
+
+def cpu_baseline_deom(budget_s=8.0):
+    import sympy as sp
+    from oracle import deom as od
+    from pyqed_amd.deom import Bath
+    w = sp.symbols(r"\omega", real=True)
+    bath = Bath([2 * 0.5 * 1.0 * w / (1.0 + w ** 2)], w, [1.0], [4], [0] * 5)
+    sx = np.array([[0, 1], [1, 0]], complex)
+    sz = np.diag([1.0, -1.0]).astype(complex)
+    rho0 = np.zeros((2, 2), complex)
+    rho0[0, 0] = 1
+    t0 = time.perf_counter()
+    od.run(sz + sx, np.zeros((2, 2)), lambda t: 0, np.array([sx]), np.zeros((1, 2, 2)), lambda t: 0,
+           (bath.etal, bath.etar, bath.etaa, bath.expn), 12, rho0, 0.01, 1)
+    el = time.perf_counter() - t0
+    return {"value": round(1 / el, 4), "unit": "RK4 steps/s", "cores": 1, "kind": "port",
+            "sample": f"1 RK4 step of the NumPy restatement of DEOMSolver.run at L=12, K=5 in {el:.1f}s"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -247,6 +298,9 @@ def main():
     ap.add_argument("--no-2des", action="store_true")
     ap.add_argument("--spo-steps", type=int, default=1000)
     ap.add_argument("--no-spo", action="store_true")
+    ap.add_argument("--deom-steps", type=int, default=200)
+    ap.add_argument("--deom-batch", type=int, default=64)
+    ap.add_argument("--no-deom", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -319,6 +373,10 @@ def main():
     if not args.no_spo:
         spo = bench_spo2(dev, args.spo_steps)
 
+    deom = None
+    if not args.no_deom:
+        deom = bench_deom(dev, args.deom_steps, args.deom_batch)
+
     if rank == 0:
         total_dm_steps = B * args.steps * world
         value = total_dm_steps / wall_max
@@ -366,6 +424,10 @@ def main():
             if world == 1 and not args.no_cpu:
                 spo["cpu_baseline"] = cpu_baseline_spo2()
             out.setdefault("secondary", {})["spo2"] = spo
+        if deom is not None:
+            if world == 1 and not args.no_cpu:
+                deom["cpu_baseline"] = cpu_baseline_deom()
+            out.setdefault("secondary", {})["deom"] = deom
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
