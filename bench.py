@@ -234,7 +234,8 @@ def cpu_baseline_spo2(n=256, dt=0.05, budget_s=5.0):
 
 def bench_deom(dev, steps, batch):
     """BASELINE config d4: spin-boson H = sz + sx, Q = sx, Drude lambda=0.5 gamma=1 beta=1, Pade npsd=4
-    (K=5), L=12 -> 6188 ADOs, dt=0.01.  Single hierarchy and a batch of independent hierarchies."""
+    (K=5), L=12 -> 6188 ADOs.  dt=0.002 (RK4 stability: dt*L*max Re expn < 2.8; the SURVEY value 0.01
+    diverges).  Single hierarchy and a batch of independent hierarchies."""
     import sympy as sp
     import torch
     from pyqed_amd.deom import Bath, DEOMSolver
@@ -250,7 +251,7 @@ def bench_deom(dev, steps, batch):
     for B in (1, batch):
         r = np.repeat(rho0[None], B, axis=0)
         t0 = time.perf_counter()
-        sol.run_batch(r, 0.01, steps)
+        sol.run_batch(r, 0.002, steps)
         el = time.perf_counter() - t0
         res[B] = el
     nmax = sol.nmax
@@ -260,7 +261,7 @@ def bench_deom(dev, steps, batch):
         "batched": {"hierarchies": batch, "ado_steps_per_s": round(steps * nmax * batch / res[batch], 1),
                     "steps_per_s": round(steps / res[batch], 1)},
         "config": {"workload": "deom_spin_boson_drude_L12_K5 (BASELINE.json configs[3])", "nmax": nmax, "K": 5,
-                   "L": 12, "dt": 0.01, "steps": steps},
+                   "L": 12, "dt": 0.002, "steps": steps},
         "note": "wall time incl. host setup of tables and per-call transfers",
     }
 

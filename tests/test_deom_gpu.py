@@ -62,7 +62,9 @@ def test_deom_batch_vs_oracle_and_trace():
 
 
 def test_deom_bench_size_properties():
-    """L=12, K=5 (6188 ADOs): trace of rho_0 conserved, hermiticity kept, 300 steps."""
+    """L=12, K=5 (6188 ADOs): trace of rho_0 conserved, hermiticity kept, 300 steps.
+    dt = 0.002: explicit RK4 needs dt * L * max Re(expn) = dt * 12 * 57.8 < 2.8 (dt = 0.01 diverges,
+    in the reference arithmetic as well)."""
     from pyqed_amd.deom import Bath, DEOMSolver
     w = sp.symbols(r"\omega", real=True)
     bath = Bath([2 * 0.5 * w / (1.0 + w ** 2)], w, [1.0], [4], [0] * 5)
@@ -71,7 +73,7 @@ def test_deom_bench_size_properties():
     sol = DEOMSolver(sz + sx, None, bath, np.array([sx]), None, None, None, 12)
     rho0 = np.zeros((2, 2), complex)
     rho0[0, 0] = 1
-    t, saved = sol.run(rho0, 0.01, 300)
+    t, saved = sol.run(rho0, 0.002, 300)
     saved = np.array(saved)
     assert sol.nmax == 6188
     assert np.max(np.abs(np.trace(saved, axis1=1, axis2=2) - 1)) < 1e-12
