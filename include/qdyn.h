@@ -93,6 +93,14 @@ int qd_glf_rk4(const qd_c128* P, const qd_c128* Q, const qd_c128* L,
 int qd_basis_transform(const qd_c128* V, qd_c128* A, int B, int N, int mode,
                        void* stream);
 
+/*
+ * Batched two-sided product A[b] <- L A[b] R (in place), [B][N][N].  Builds the
+ * quantum-regression initial states C rho(t) A of oqs.py:1291-1292 and
+ * oqs.py:1240 (correlation_3op_1t/_2t) for a whole batch of restarts.
+ */
+int qd_sandwich(const qd_c128* L, const qd_c128* R, qd_c128* A, int B, int N,
+                void* stream);
+
 /* ------------------------------------------------------------ split-operator */
 /*
  * 2D multi-state split-operator propagation, nsteps Strang steps

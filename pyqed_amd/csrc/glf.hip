@@ -282,6 +282,17 @@ __global__ void transform_prep_kernel(const c128* V, int N, int Np, int mode, c1
   }
 }
 
+// Vl = L, Vr = R (padded), for the general two-sided product A <- L A R
+__global__ void sandwich_prep_kernel(const c128* Lm, const c128* Rm, int N, int Np, c128* Vl, c128* Vr) {
+  const size_t NN = (size_t)Np * Np;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < NN; e += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(e / Np), j = (int)(e % Np);
+    const bool in = i < N && j < N;
+    Vl[e] = in ? Lm[(size_t)i * N + j] : cmk(0, 0);
+    Vr[e] = in ? Rm[(size_t)i * N + j] : cmk(0, 0);
+  }
+}
+
 int padded_dim(int N) {
   if (N <= 32) return 32;
   if (N <= 64) return 64;
@@ -412,11 +423,9 @@ extern "C" int qd_glf_rk4(const qd_c128* P, const qd_c128* Q, const qd_c128* L, 
                  save_every, (hipStream_t)stream);
 }
 
-extern "C" int qd_basis_transform(const qd_c128* V, qd_c128* A_, int B, int N, int mode, void* stream) {
-  QD_CHECK_ARG(V && A_, "qd_basis_transform: null pointer");
-  QD_CHECK_ARG(N >= 1 && N <= 1024 && B >= 1, "qd_basis_transform: bad sizes N=%d B=%d", N, B);
-  QD_CHECK_ARG(mode == 0 || mode == 1, "qd_basis_transform: mode must be 0 or 1");
-  hipStream_t st = (hipStream_t)stream;
+namespace {
+// shared driver: A[b] <- Vl A[b] Vr for b < B; mode 0/1 = V^+ . V / V . V^+, mode 2 = L . R
+int sandwich_run(const c128* V, const c128* Lm, const c128* Rm, c128* A, int B, int N, int mode, hipStream_t st) {
   const int Np = padded_dim(N);
   const size_t NN = (size_t)Np * Np;
   const bool pad = Np != N;
@@ -426,11 +435,13 @@ extern "C" int qd_basis_transform(const qd_c128* V, qd_c128* A_, int B, int N, i
   c128* Vl = (c128*)w;
   c128* Vr = Vl + NN;
   c128* T = Vr + NN;
-  c128* A = (c128*)A_;
   c128* Ap = pad ? T + (size_t)B * NN : A;
   const int threads = 256;
-  hipLaunchKernelGGL(transform_prep_kernel, dim3((int)std::min<size_t>((NN + 255) / 256, 4096)), dim3(threads), 0, st,
-                     (const c128*)V, N, Np, mode, Vl, Vr);
+  const int pb = (int)std::min<size_t>((NN + 255) / 256, 4096);
+  if (mode == 2)
+    hipLaunchKernelGGL(sandwich_prep_kernel, dim3(pb), dim3(threads), 0, st, Lm, Rm, N, Np, Vl, Vr);
+  else
+    hipLaunchKernelGGL(transform_prep_kernel, dim3(pb), dim3(threads), 0, st, V, N, Np, mode, Vl, Vr);
   QD_HIP(hipGetLastError());
   if (pad) {
     hipLaunchKernelGGL(pad_kernel, dim3((int)std::min<size_t>((B * NN + 255) / 256, 65535)), dim3(threads), 0, st, A,
@@ -450,4 +461,18 @@ extern "C" int qd_basis_transform(const qd_c128* V, qd_c128* A_, int B, int N, i
     QD_HIP(hipGetLastError());
   }
   return QD_OK;
+}
+}  // namespace
+
+extern "C" int qd_basis_transform(const qd_c128* V, qd_c128* A, int B, int N, int mode, void* stream) {
+  QD_CHECK_ARG(V && A, "qd_basis_transform: null pointer");
+  QD_CHECK_ARG(N >= 1 && N <= 1024 && B >= 1, "qd_basis_transform: bad sizes N=%d B=%d", N, B);
+  QD_CHECK_ARG(mode == 0 || mode == 1, "qd_basis_transform: mode must be 0 or 1");
+  return sandwich_run((const c128*)V, nullptr, nullptr, (c128*)A, B, N, mode, (hipStream_t)stream);
+}
+
+extern "C" int qd_sandwich(const qd_c128* Lm, const qd_c128* Rm, qd_c128* A, int B, int N, void* stream) {
+  QD_CHECK_ARG(Lm && Rm && A, "qd_sandwich: null pointer");
+  QD_CHECK_ARG(N >= 1 && N <= 1024 && B >= 1, "qd_sandwich: bad sizes N=%d B=%d", N, B);
+  return sandwich_run(nullptr, (const c128*)Lm, (const c128*)Rm, (c128*)A, B, N, 2, (hipStream_t)stream);
 }

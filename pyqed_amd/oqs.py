@@ -100,6 +100,75 @@ class LindbladSolver:
         return _lindblad(self.H, rho0, c_ops=self.c_ops, e_ops=e_ops, Nt=Nt, dt=dt,
                          return_states=return_states)
 
+    # ---- quantum-regression correlation functions (oqs.py:1193-1329)
+    def correlation_2op_1t(self, rho0, a_op, b_op, dt, Nt, output='cor.dat'):
+        """<A(t)B> (oqs.py:1193-1222 -> _correlation_2p_1t oqs.py:717-791): rho <- B rho0,
+        Nt RK4 steps, cor[k] = Tr(A rho_k) AFTER each step (t0 excluded); writes `output`."""
+        return _correlation_2p_1t(self.H, rho0, [a_op, b_op], self.c_ops, dt, Nt, output=output)
+
+    def correlation_3op_1t(self, rho0, oplist, dt=0.005, Nt=1):
+        """<A B(t) C> (oqs.py:1224-1243): Tr(B rho(t)) from rho(0) = C rho0 A, Nt+1 values incl. t0."""
+        a_op, b_op, c_op = oplist
+        r0 = _dense(c_op) @ _dense(rho0) @ _dense(a_op)
+        return _lindblad(self.H, r0, c_ops=self.c_ops, e_ops=[b_op], dt=dt, Nt=Nt,
+                         return_states=False).observables[:, 0]
+
+    def correlation_3op_2t(self, rho0, ops, dt, Nt, Ntau):
+        """<A(t) B(t+tau) C(t)> (oqs.py:1264-1296).  All Nt restarts C rho(t_k) A are propagated
+        together as ONE batch on the GPU.  The reference fills an (Nt, Ntau) array with Ntau+1
+        observables and raises; this returns corr[t_k, tau_j] for tau_j = j*dt, j < Ntau."""
+        a_op, b_op, c_op = (_dense(x) for x in ops)
+        dev = default_device()
+        H = _dense(self.H)
+        N = H.shape[0]
+        Hd = torch.from_numpy(H).to(dev)
+        Cd = stack_ops(self.c_ops or [], N, dev)
+        rho = torch.from_numpy(_dense(rho0).reshape(1, N, N).copy()).to(dev)
+        _, snap = lindblad_rk4(Hd, Cd, rho, dt, Nt, None, save_every=1)   # rho_t, t = dt..Nt dt
+        at = torch.from_numpy(a_op).to(dev)
+        ct = torch.from_numpy(c_op).to(dev)
+        r = snap[0].contiguous()                                           # [Nt, N, N]
+        sandwich(ct, at, r)                                                # C rho(t_k) A, batched
+
+        Ed = torch.from_numpy(b_op.reshape(1, N, N).copy()).to(dev)
+        obs, _ = lindblad_rk4(Hd, Cd, r, dt, Ntau, Ed)
+        return obs[:, :Ntau, 0].cpu().numpy()
+
+    def correlation_4op_1t(self, rho0, ops, dt, nt):
+        """<A B(t) C(t) D> (oqs.py:1298-1313, the definition that wins): 3op_1t with [a, b@c, d]."""
+        if len(ops) != 4:
+            raise ValueError('Number of operators is not 4.')
+        a, b, c, d = ops
+        return self.correlation_3op_1t(rho0, [a, _dense(b) @ _dense(c), d], dt, nt)
+
+    def correlation_4op_2t(self, rho0, ops, dt, nt, ntau):
+        """<A(t) B(t+tau) C(t+tau) D(t)> (oqs.py:1315-1329): 3op_2t with [a, b@c, d]."""
+        if len(ops) != 4:
+            raise ValueError('Number of operators is not 4.')
+        a, b, c, d = ops
+        return self.correlation_3op_2t(rho0, [a, _dense(b) @ _dense(c), d], dt, nt, ntau)
+
+
+def _dense(a):
+    return np.ascontiguousarray(to_numpy(a, np.complex128))
+
+
+def _correlation_2p_1t(H, rho0, ops, c_ops, dt, Nt, method='lindblad', output='cor.dat'):
+    """oqs.py:717-791 on the GPU."""
+    if method != 'lindblad':
+        raise NotImplementedError(f'The method {method} has not been implemented yet! Please try lindblad.')
+    A, B = ops
+    r0 = _dense(B) @ _dense(rho0)
+    res = _lindblad(H, r0, c_ops=c_ops or [], e_ops=[A], Nt=Nt, dt=dt, return_states=False)
+    cor = res.observables[1:, 0].copy()
+    if output is not None:
+        with open(output, 'w') as f:
+            t = 0.0
+            for k in range(Nt):
+                t += dt
+                f.write('{} {} \n'.format(t, cor[k]))
+    return cor
+
 
 def _lindblad(H, rho0, c_ops, e_ops=None, Nt=1, t0=0, dt=0.005, return_result=True, return_states=True):
     """GPU restatement of oqs._lindblad (oqs.py:1596-1696)."""
@@ -166,6 +235,17 @@ def basis_transform(V: torch.Tensor, A: torch.Tensor, inverse=False):
     with torch.cuda.device(dev):
         rc = _lib.load().qd_basis_transform(_lib.ptr(V), _lib.ptr(A), B, N, int(bool(inverse)), _lib.stream_ptr(dev))
     _lib.check(rc, "qd_basis_transform")
+    return A
+
+
+def sandwich(L: torch.Tensor, R: torch.Tensor, A: torch.Tensor):
+    """In place A[b] <- L A[b] R on the GPU (qd_sandwich).  A [B,N,N]."""
+    dev = A.device
+    _lib.ensure_device(dev)
+    B, N = A.shape[0], A.shape[-1]
+    with torch.cuda.device(dev):
+        rc = _lib.load().qd_sandwich(_lib.ptr(L), _lib.ptr(R), _lib.ptr(A), B, N, _lib.stream_ptr(dev))
+    _lib.check(rc, "qd_sandwich")
     return A
 
 

@@ -88,6 +88,43 @@ def lindblad_n128():
     _lindblad_case("lindblad_n128", N=128, nc=1, ne=1, Nt=3, dt=1e-3, seed=14, keep_all=False)
 
 
+@golden
+def lindblad_corr():
+    """LindbladSolver correlation functions (oqs.py:1193-1329, _correlation_2p_1t oqs.py:717-791)."""
+    import tempfile
+    import pyqed.oqs as oqs
+    rng = np.random.default_rng(15)
+    N = 5
+    H = _herm(rng, N, 1 / np.sqrt(N))
+    C = _ginibre(rng, N, 0.3 / np.sqrt(N))
+    A, B, Cop, D = (_ginibre(rng, N) for _ in range(4))
+    psi = rng.standard_normal(N) + 1j * rng.standard_normal(N)
+    psi /= np.linalg.norm(psi)
+    rho0 = np.outer(psi, psi.conj())
+    sol = oqs.LindbladSolver(csr_matrix(H), [csr_matrix(C)])
+    dt, Nt = 0.02, 12
+    with tempfile.TemporaryDirectory() as d:
+        cwd = os.getcwd()
+        os.chdir(d)
+        try:
+            c2 = sol.correlation_2op_1t(rho0, csr_matrix(A), csr_matrix(B), dt, Nt)
+            cordat = open("cor.dat").read()
+        finally:
+            os.chdir(cwd)
+    c3 = sol.correlation_3op_1t(rho0, [csr_matrix(A), csr_matrix(B), csr_matrix(Cop)], dt=dt, Nt=Nt)
+    c4 = sol.correlation_4op_1t(rho0, [csr_matrix(A), csr_matrix(B), csr_matrix(Cop), csr_matrix(D)], dt, Nt)
+    # correlation_3op_2t is broken at oqs.py:1292 (Nt+1 vs Ntau); build its intended matrix
+    # from the reference's own _lindblad exactly as the method does
+    Ntau = 7
+    rho_t = oqs._lindblad(csr_matrix(H), rho0, [csr_matrix(C)], dt=dt, Nt=Nt).rholist
+    c32 = np.zeros((Nt, Ntau), dtype=complex)
+    for k, r in enumerate(rho_t):
+        c32[k] = oqs._lindblad(csr_matrix(H), rho0=csr_matrix(Cop) @ r @ csr_matrix(A), dt=dt, Nt=Ntau,
+                               c_ops=[csr_matrix(C)], e_ops=[csr_matrix(B)]).observables[:Ntau, 0]
+    save("lindblad_corr", H=H, C=C, A=A, B=B, Cop=Cop, D=D, rho0=rho0, dt=dt, Nt=Nt, Ntau=Ntau, c2=c2, c3=c3,
+         c4=c4, c32=c32, cordat=np.array(cordat))
+
+
 # ----------------------------------------------------------------- Redfield / 2DES
 # Spectral functions by name (tests/conftest.py SPECTRA holds the same definitions).
 SPECTRA = {
