@@ -188,6 +188,13 @@ int qd_response2d_ensemble(const qd_c128* alpha, const qd_c128* Mt,
                            int nL, const double* t3, int n3, const double* t1,
                            int n1, qd_c128* out, int accumulate, void* stream);
 
+/*
+ * Frequency-domain pole sum out[i] = sum_n -coeff_n / (lam_n + i w_i)
+ * (Lindblad_solver.correlation_2op_1w / 3op_1w, pyqed/superoperator.py:603-700).
+ */
+int qd_resolvent_sum(const qd_c128* coeff, const qd_c128* lam, int n,
+                     const double* w, int nw, qd_c128* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -52,6 +52,7 @@ SIGNATURES = {
                                  c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]),
     "qd_response2d_ensemble": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int,
                                        c_void_p, c_int, c_void_p, c_int, c_void_p]),
+    "qd_resolvent_sum": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]),
 }
 
 _lib = None

@@ -190,6 +190,20 @@ __global__ void ens_reduce_kernel(const c128* slabs, int S, int n3, int n1, int 
   }
 }
 
+// out[i] = sum_n -c_n / (lam_n + i w_i)   (Lindblad_solver.correlation_*_1w, superoperator.py:603-700)
+__global__ void resolvent_sum_kernel(const c128* c, const c128* lam, int n, const double* w, int nw, c128* out) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += gridDim.x * blockDim.x) {
+    c128 s = cmk(0, 0);
+    for (int k = 0; k < n; ++k) {
+      const c128 den = cmk(lam[k].re, lam[k].im + w[i]);
+      const double d2 = den.re * den.re + den.im * den.im;
+      const c128 inv = cmk(den.re / d2, -den.im / d2);
+      s = csub(s, cmul(c[k], inv));
+    }
+    out[i] = s;
+  }
+}
+
 int grid_for(size_t n, int threads) { return (int)std::min<size_t>((n + threads - 1) / threads, 16384); }
 
 }  // namespace
@@ -276,6 +290,16 @@ extern "C" int qd_response2d_ensemble(const qd_c128* alpha, const qd_c128* Mt, c
   QD_HIP(hipGetLastError());
   hipLaunchKernelGGL(ens_reduce_kernel, dim3(grid_for((size_t)n3 * n1, 256)), dim3(256), 0, st, slabs, S, n3, n1, n3p,
                      n1p, (c128*)out, accumulate);
+  QD_HIP(hipGetLastError());
+  return QD_OK;
+}
+
+extern "C" int qd_resolvent_sum(const qd_c128* coeff, const qd_c128* lam, int n, const double* w, int nw,
+                                qd_c128* out, void* stream) {
+  QD_CHECK_ARG(coeff && lam && w && out, "qd_resolvent_sum: null pointer");
+  QD_CHECK_ARG(n >= 1 && nw >= 1, "qd_resolvent_sum: bad sizes");
+  hipLaunchKernelGGL(resolvent_sum_kernel, dim3(grid_for(nw, 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const c128*)coeff, (const c128*)lam, n, w, nw, (c128*)out);
   QD_HIP(hipGetLastError());
   return QD_OK;
 }

@@ -125,6 +125,33 @@ def lindblad_corr():
          c4=c4, c32=c32, cordat=np.array(cordat))
 
 
+@golden
+def lindblad_eig():
+    """superoperator.Lindblad_solver eigen path (superoperator.py:455-772), N=3 ladder."""
+    import pyqed.superoperator as so
+    N = 3
+    H = np.diag([0.0, 1.0, 1.6]).astype(complex)
+    H[0, 1] = H[1, 0] = 0.1
+    c1 = np.zeros((N, N), complex); c1[0, 1] = np.sqrt(0.1)
+    c2 = np.zeros((N, N), complex); c2[1, 2] = np.sqrt(0.05)
+    dip = np.zeros((N, N), complex); dip[0, 1] = dip[1, 0] = 1.0; dip[1, 2] = dip[2, 1] = 0.7
+    rho0 = np.zeros((N, N), complex); rho0[0, 0] = 1
+    sol = so.Lindblad_solver(H, [c1, c2])
+    L = sol.liouvillian()
+    w, vr, vl = sol.eigenstates()
+    t = 0.3 * np.arange(40)
+    tau = 0.25 * np.arange(11)
+    freq = np.linspace(-3, 3, 33)
+    out = dict(H=H, c1=c1, c2=c2, dip=dip, rho0=rho0, L=L.toarray(), eigvals=w, norm=sol.norm, t=t, tau=tau, w=freq)
+    out["c2t"] = sol.correlation_2op_1t(rho0, [dip, dip], t)
+    out["c2w"] = sol.correlation_2op_1w(rho0, [dip, dip], freq)
+    out["c3t"] = sol.correlation_3op_1t(rho0, [dip, dip, dip], t)
+    out["c3w"] = sol.correlation_3op_1w(rho0, [dip, dip, dip], freq)
+    out["c32"] = sol.correlation_3op_2t(rho0, [dip, dip, dip], t[:9], tau)
+    out["c42"] = sol.correlation_4op_2t(rho0, [dip, dip, dip, dip], t[:9], tau)
+    save("lindblad_eig", **out)
+
+
 # ----------------------------------------------------------------- Redfield / 2DES
 # Spectral functions by name (tests/conftest.py SPECTRA holds the same definitions).
 SPECTRA = {
