@@ -167,10 +167,14 @@ class Lindblad_solver:
 
     def evolve(self, rho0, tlist, e_ops):
         """Intended semantics of superoperator.py:524-563 (the reference crashes building
-        Result(times=...)): observables[i, m] = obs(U1 (coeff e^{lam t_i}), e_m)."""
+        Result(times=...)): observables[i, m] = obs(U1 (coeff e^{lam t_i}), e_m).
+        Uses the complex biorthogonal norm l_n^+ r_n: the reference's `self.norm` keeps only
+        its real part (superoperator.py:514), which the correlation_* methods mirror for parity
+        but which is wrong whenever l_n^+ r_n has a phase."""
         from .mol import Result
         self._ensure()
-        evals, U1, U2, norm = self.eigvals, self.right_eigvecs, self.left_eigvecs, self.norm
+        evals, U1, U2 = self.eigvals, self.right_eigvecs, self.left_eigvecs
+        norm = np.diagonal(cdot(U2, U1))
         r0 = operator_to_vector(to_dense(rho0))
         coeff = (U2.conj().T @ r0) / norm
         tlist = np.asarray(tlist, float)
