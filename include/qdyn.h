@@ -140,7 +140,10 @@ int qd_spo1d_run(qd_c128* psi, const qd_c128* expV, const qd_c128* expVh,
  *   fsys, fcoup  HOST arrays [nsteps][3]: pulse values at t, t+dt/2, t+dt of
  *                each step (NULL when the dipole is NULL)
  *   rho_sys [B][nsteps+1][ns][ns]  ADO 0 after every step (row 0 = initial), or NULL
- *   p1 [ns][ns], trace [B][nsteps+1]  Tr(p1 rho_0) per step (deom.py:1100,1113), or NULL
+ *   E [ne][ns][ns], trace [B][nsteps+1][ne]  Tr(E_m rho_0) per step (p1 of
+ *                deom.py:1100,1113; e_ops of HEOM/heom.py:339-343), or NULL
+ * Also runs the single-exponential HEOM chain of pyqed/HEOM/heom.py:275-347
+ * (_heom, RK4) with chain tables (K = 1) built by the host.
  * Constraints: ns <= 16, nmod <= 8.
  */
 int qd_deom_rk4(qd_c128* ados, int B, int nmax, int K, int ns,
@@ -148,8 +151,20 @@ int qd_deom_rk4(qd_c128* ados, int B, int nmax, int K, int ns,
                 const qd_c128* damp, const int32_t* mode, int nmod,
                 const qd_c128* H, const qd_c128* Hdip, const qd_c128* Q,
                 const qd_c128* Qdip, const qd_c128* fsys, const qd_c128* fcoup,
-                double dt, int nsteps, qd_c128* rho_sys, const qd_c128* p1,
-                qd_c128* trace, void* stream);
+                double dt, int nsteps, qd_c128* rho_sys, const qd_c128* E,
+                int ne, qd_c128* trace, void* stream);
+
+/*
+ * Single-exponential (high-T Drude) HEOM chain of pyqed/oqs.py:1808-1875
+ * (oqs._heom): explicit in-place sweep per step, ADO n updated from the NEW
+ * n-1 and the old n, n+1; ADO nado-1 never updated.  ados [B][nado][ns][ns]
+ * in/out; D0 = D0_re + i D0_im; rho_sys [B][nsteps+1][ns][ns] or NULL;
+ * obs [B][nsteps+1][ne] = Tr(E_m ado_0) or NULL.  ns <= 16, nado >= 2.
+ */
+int qd_heom_chain_euler(qd_c128* ados, int B, int nado, int ns, const qd_c128* H,
+                        const qd_c128* Q, double gamma, double D0_re,
+                        double D0_im, double dt, int nsteps, qd_c128* rho_sys,
+                        const qd_c128* E, int ne, qd_c128* obs, void* stream);
 
 /* ------------------------------------------------------------ response --- */
 /*

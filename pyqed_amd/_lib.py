@@ -45,7 +45,9 @@ SIGNATURES = {
                              c_void_p]),
     "qd_deom_rk4": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_double, c_int,
-                            c_void_p, c_void_p, c_void_p, c_void_p]),
+                            c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "qd_heom_chain_euler": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_double, c_double, c_double,
+                                    c_double, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "qd_sandwich": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "qd_sos_propagator": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]),
     "qd_response_cube": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,

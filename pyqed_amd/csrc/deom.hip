@@ -130,15 +130,66 @@ __global__ void deom_snap0_kernel(const c128* rho, c128* snap, int B, int nmax, 
   }
 }
 
-// trace[b][s] = Tr(p1 rho_0(s)) = sum_ij p1[j][i] rho[i][j]   (deom.py:1100,1113)
-__global__ void deom_trace_kernel(const c128* snap, const c128* p1, int B, int ns, int nsteps, c128* trace) {
+// obs[b][s][m] = Tr(E_m rho_0(s)) = sum_ij E_m[j][i] rho[i][j]   (deom.py:1100,1113)
+__global__ void deom_trace_kernel(const c128* snap, const c128* E, int ne, int B, int ns, int nsnap, c128* obs) {
   const int ns2 = ns * ns;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < B * (nsteps + 1); e += gridDim.x * blockDim.x) {
-    const c128* r = snap + (size_t)e * ns2;
+  const int tot = B * nsnap * ne;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += gridDim.x * blockDim.x) {
+    const int m = e % ne, bs = e / ne;
+    const c128* r = snap + (size_t)bs * ns2;
+    const c128* Em = E + (size_t)m * ns2;
     c128 s = cmk(0, 0);
     for (int i = 0; i < ns; ++i)
-      for (int j = 0; j < ns; ++j) s = cadd(s, cmul(p1[j * ns + i], r[i * ns + j]));
-    trace[e] = s;
+      for (int j = 0; j < ns; ++j) s = cadd(s, cmul(Em[j * ns + i], r[i * ns + j]));
+    obs[e] = s;
+  }
+}
+
+// oqs._heom (pyqed/oqs.py:1808-1875): single-exponential chain, explicit in-place sweep per
+// step (ADO n uses the already-updated n-1, the old n and n+1; ADO nado-1 is never updated).
+// One workgroup per hierarchy, one thread per matrix element, ADOs in global memory.
+__global__ __launch_bounds__(256) void heom_chain_sweep_kernel(c128* ados, int nado, int ns, const c128* H,
+                                                               const c128* Q, double gamma, c128 D0, double dt,
+                                                               int nsteps, c128* snap) {
+  const int ns2 = ns * ns;
+  c128* A = ados + (size_t)blockIdx.x * nado * ns2;
+  const int t = threadIdx.x;
+  const bool act = t < ns2;
+  const int i = act ? t / ns : 0, j = act ? t % ns : 0;
+  auto comm = [&](const c128* X, const c128* Y, int ii, int jj) {  // (X Y - Y X)[ii][jj]
+    c128 s = cmk(0, 0);
+    for (int l = 0; l < ns; ++l) s = cadd(s, csub(cmul(X[ii * ns + l], Y[l * ns + jj]), cmul(Y[ii * ns + l], X[l * ns + jj])));
+    return s;
+  };
+  auto acomm = [&](const c128* X, const c128* Y, int ii, int jj) {
+    c128 s = cmk(0, 0);
+    for (int l = 0; l < ns; ++l) s = cadd(s, cadd(cmul(X[ii * ns + l], Y[l * ns + jj]), cmul(Y[ii * ns + l], X[l * ns + jj])));
+    return s;
+  };
+  if (snap && act) snap[(size_t)blockIdx.x * (nsteps + 1) * ns2 + t] = A[t];
+  for (int s = 0; s < nsteps; ++s) {
+    for (int n = 0; n < nado - 1; ++n) {
+      c128 v = cmk(0, 0);
+      if (act) {
+        const c128* xn = A + (size_t)n * ns2;
+        const c128* xp = A + (size_t)(n + 1) * ns2;
+        const c128 x = xn[t];
+        if (n == 0) {
+          v = csub(csub(x, cscale(cmuli(comm(H, xn, i, j)), dt)), cscale(comm(Q, xp, i, j), dt));
+        } else {
+          const c128* xm = A + (size_t)(n - 1) * ns2;
+          const c128 coh = cscale(cmulmi(comm(H, xn, i, j)), dt);
+          c128 inner = csub(cscale(comm(Q, xp, i, j), -1.0), cscale(x, n * gamma));
+          const c128 mix = cadd(cscale(comm(Q, xm, i, j), D0.re), cmuli(cscale(acomm(Q, xm, i, j), D0.im)));
+          inner = cadd(inner, cscale(mix, (double)n));
+          v = cadd(x, cadd(coh, cscale(inner, dt)));
+        }
+      }
+      __syncthreads();
+      if (act) A[(size_t)n * ns2 + t] = v;
+      __syncthreads();
+    }
+    if (snap && act) snap[((size_t)blockIdx.x * (nsteps + 1) + s + 1) * ns2 + t] = A[t];
   }
 }
 
@@ -150,7 +201,7 @@ using namespace qd;
 extern "C" int qd_deom_rk4(qd_c128* ados, int B, int nmax, int K, int ns, const int32_t* minus, const int32_t* plus,
                            const qd_c128* coef, const qd_c128* damp, const int32_t* mode, int nmod, const qd_c128* H,
                            const qd_c128* Hdip, const qd_c128* Q, const qd_c128* Qdip, const qd_c128* fsys,
-                           const qd_c128* fcoup, double dt, int nsteps, qd_c128* rho_sys, const qd_c128* p1,
+                           const qd_c128* fcoup, double dt, int nsteps, qd_c128* rho_sys, const qd_c128* E, int ne,
                            qd_c128* trace, void* stream) {
   QD_CHECK_ARG(ados && minus && plus && coef && damp && mode && H && Q, "qd_deom_rk4: null pointer");
   QD_CHECK_ARG(B >= 1 && nmax >= 1 && K >= 1 && nsteps >= 0, "qd_deom_rk4: bad sizes B=%d nmax=%d K=%d", B, nmax, K);
@@ -158,7 +209,7 @@ extern "C" int qd_deom_rk4(qd_c128* ados, int B, int nmax, int K, int ns, const 
   QD_CHECK_ARG(nmod >= 1 && nmod <= DEOM_MAX_NMOD, "qd_deom_rk4: nmod=%d outside [1, %d]", nmod, DEOM_MAX_NMOD);
   QD_CHECK_ARG(!Hdip || fsys, "qd_deom_rk4: Hdip given without fsys");
   QD_CHECK_ARG(!Qdip || fcoup, "qd_deom_rk4: Qdip given without fcoup");
-  QD_CHECK_ARG(!trace || p1, "qd_deom_rk4: trace requested without p1");
+  QD_CHECK_ARG(!trace || (E && ne >= 1), "qd_deom_rk4: trace requested without observables");
   hipStream_t st = (hipStream_t)stream;
   const size_t ns2 = (size_t)ns * ns;
   const size_t tot = (size_t)B * nmax * ns2;
@@ -215,9 +266,37 @@ extern "C" int qd_deom_rk4(qd_c128* ados, int B, int nmax, int K, int ns, const 
     }
   }
   if (trace) {
-    const int n = B * (nsteps + 1);
+    const int n = B * (nsteps + 1) * ne;
     hipLaunchKernelGGL(deom_trace_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0, st,
-                       (const c128*)snap, (const c128*)p1, B, ns, nsteps, (c128*)trace);
+                       (const c128*)snap, (const c128*)E, ne, B, ns, nsteps + 1, (c128*)trace);
+    QD_HIP(hipGetLastError());
+  }
+  return QD_OK;
+}
+
+extern "C" int qd_heom_chain_euler(qd_c128* ados, int B, int nado, int ns, const qd_c128* H, const qd_c128* Q,
+                                   double gamma, double D0_re, double D0_im, double dt, int nsteps, qd_c128* rho_sys,
+                                   const qd_c128* E, int ne, qd_c128* obs, void* stream) {
+  QD_CHECK_ARG(ados && H && Q, "qd_heom_chain_euler: null pointer");
+  QD_CHECK_ARG(B >= 1 && nado >= 2 && nsteps >= 0, "qd_heom_chain_euler: bad sizes B=%d nado=%d", B, nado);
+  QD_CHECK_ARG(ns >= 1 && ns <= 16, "qd_heom_chain_euler: ns=%d outside [1, 16]", ns);
+  QD_CHECK_ARG(!obs || (E && ne >= 1), "qd_heom_chain_euler: obs requested without observables");
+  hipStream_t st = (hipStream_t)stream;
+  const size_t ns2 = (size_t)ns * ns;
+  c128* snap = (c128*)rho_sys;
+  if (!snap && obs) {
+    void* w = nullptr;
+    int rc = workspace(WS_DEOM, (size_t)B * (nsteps + 1) * ns2 * sizeof(c128), &w);
+    if (rc) return rc;
+    snap = (c128*)w;
+  }
+  hipLaunchKernelGGL(heom_chain_sweep_kernel, dim3(B), dim3(256), 0, st, (c128*)ados, nado, ns, (const c128*)H,
+                     (const c128*)Q, gamma, cmk(D0_re, D0_im), dt, nsteps, snap);
+  QD_HIP(hipGetLastError());
+  if (obs) {
+    const int n = B * (nsteps + 1) * ne;
+    hipLaunchKernelGGL(deom_trace_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0, st,
+                       (const c128*)snap, (const c128*)E, ne, B, ns, nsteps + 1, (c128*)obs);
     QD_HIP(hipGetLastError());
   }
   return QD_OK;

@@ -311,8 +311,8 @@ class DEOMSolver:
         fs = np.ascontiguousarray(fs) if fs is not None else None
         fc = np.ascontiguousarray(fc) if fc is not None else None
         rho_sys = torch.empty((B, nt + 1, ns, ns), dtype=torch.complex128, device=dev)
-        p1_t = c128(p1) if p1 is not None else None
-        trace = torch.empty((B, nt + 1), dtype=torch.complex128, device=dev) if p1 is not None else None
+        p1_t = c128(np.asarray(p1, dtype=complex).reshape(1, ns, ns)) if p1 is not None else None
+        trace = torch.empty((B, nt + 1, 1), dtype=torch.complex128, device=dev) if p1 is not None else None
         tabs = (i32(self._minus), i32(self._plus), c128(coef), c128(damp), i32(b.mode))
         with torch.cuda.device(dev):
             rc = _lib.load().qd_deom_rk4(
@@ -320,12 +320,12 @@ class DEOMSolver:
                 tabs[3].data_ptr(), tabs[4].data_ptr(), nmod, H.data_ptr(), _lib.ptr(Hdip_t), Q.data_ptr(),
                 _lib.ptr(Qdip_t), fs.ctypes.data if fs is not None else None,
                 fc.ctypes.data if fc is not None else None, float(dt), int(nt), rho_sys.data_ptr(),
-                _lib.ptr(p1_t), _lib.ptr(trace), _lib.stream_ptr(dev))
+                _lib.ptr(p1_t), 1 if p1 is not None else 0, _lib.ptr(trace), _lib.stream_ptr(dev))
         _lib.check(rc, "qd_deom_rk4")
         torch.cuda.synchronize(dev)
         self.ddos = ados.cpu().numpy()
         t_save = np.arange(nt + 1) * dt
         t_save[0] = 0
         if p1 is not None:
-            return t_save, trace.cpu().numpy()
+            return t_save, trace[..., 0].cpu().numpy()
         return t_save, rho_sys.cpu().numpy()

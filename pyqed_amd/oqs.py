@@ -396,3 +396,60 @@ class RedfieldSolver:
         lam, U1, U2, tG = self._sos
         alpha, B, C, beta = eigen_factors(lam, U1, U2, oplist, signature, rho0)
         return response_cube(lam, alpha, B, C, beta, tG, tG, tG).cpu().numpy()
+
+
+class HEOMSolver:
+    """Drop-in for pyqed.oqs.HEOMSolver (oqs.py:1332-1403): single-exponential chain with the
+    reference's explicit in-place sweep (oqs._heom, oqs.py:1808-1875) on the GPU."""
+
+    def __init__(self, H=None, c_ops=None, e_ops=None):
+        self.c_ops = c_ops
+        self.e_ops = e_ops
+        self.H = H
+
+    def set_c_ops(self, c_ops):
+        self.c_ops = c_ops
+
+    def set_e_ops(self, e_ops):
+        self.e_ops = e_ops
+
+    def setH(self, H):
+        self.H = H
+
+    def configure(self, c_ops, e_ops):
+        self.c_ops = c_ops
+        self.e_ops = e_ops
+
+    def run(self, rho0, dt, nt, temperature, cutoff, reorganization, nado):
+        return _heom(self.H, rho0, self.c_ops, self.e_ops, temperature, cutoff, reorganization, nado, dt, nt)
+
+    def correlation_2op_1t(self, rho0, a_op, b_op, dt, Nt, output='cor.dat'):
+        """oqs.py:1374-1403: as the reference, computed with the Lindblad RHS."""
+        return _correlation_2p_1t(self.H, rho0, [a_op, b_op], self.c_ops, dt, Nt, output=output)
+
+
+def _heom(H, rho0, c_ops, e_ops, temperature, cutoff, reorganization, nado, dt, nt, fname=None,
+          return_result=True):
+    """oqs.py:1808-1875: observables (len(e_ops), nt) after every sweep step."""
+    gamma, T, reorg = cutoff, temperature, reorganization
+    D0 = reorg * gamma * (1.0 / np.tanh(gamma / (2. * T)) - 1j)
+    dev = default_device()
+    _lib.ensure_device(dev)
+    Hn = _dense(H)
+    ns = Hn.shape[0]
+    e_ops = list(e_ops or [])
+    ados = torch.zeros((1, nado, ns, ns), dtype=torch.complex128, device=dev)
+    ados[0, 0] = torch.from_numpy(_dense(rho0)).to(dev)
+    Hd = torch.from_numpy(Hn).to(dev)
+    Qd = torch.from_numpy(_dense(c_ops[0])).to(dev)
+    ne = len(e_ops)
+    Ed = stack_ops(e_ops, ns, dev)
+    obs = torch.empty((1, nt + 1, ne), dtype=torch.complex128, device=dev) if ne else None
+    with torch.cuda.device(dev):
+        rc = _lib.load().qd_heom_chain_euler(ados.data_ptr(), 1, int(nado), ns, Hd.data_ptr(), Qd.data_ptr(),
+                                             float(gamma), float(D0.real), float(D0.imag), float(dt), int(nt),
+                                             None, _lib.ptr(Ed), ne, _lib.ptr(obs), _lib.stream_ptr(dev))
+    _lib.check(rc, "qd_heom_chain_euler")
+    if not ne:
+        return np.zeros((0, nt), dtype=complex)
+    return obs[0, 1:].T.cpu().numpy()

@@ -389,6 +389,31 @@ def _deom_case(lmax, npsd, nt, dt, pulses=False, p1=True, lam=0.5, gam=1.0, beta
 
 
 @golden
+def heom_chain():
+    """Single-exponential HEOM chains: HEOM/heom.py _heom (RK4, :275-347) and oqs._heom
+    (in-place explicit sweep, oqs.py:1808-1875), examples/heom.py:79-97 model."""
+    import pyqed.HEOM.heom as hh
+    import pyqed.oqs as oqs
+    sx = np.array([[0, 1], [1, 0]], complex)
+    sz = np.array([[1, 0], [0, -1]], complex)
+    H = -1 / 2.0 * sx - 1.0 / 2.0 * sz
+    rho0 = np.zeros((2, 2), complex)
+    rho0[1, 1] = 1
+    out = dict(H=H, Q=sz, rho0=rho0)
+    cases = {"ex": dict(temperature=600, cutoff=5, reorganization=0.2, nado=5, dt=0.02, nt=100),
+             "mild": dict(temperature=1.0, cutoff=0.5, reorganization=0.2, nado=6, dt=0.02, nt=80)}
+    for tag, c in cases.items():
+        for mod, name in [(hh, "rk4"), (oqs, "euler")]:
+            sol = mod.HEOMSolver(H, c_ops=[sz], e_ops=[sz, sx])
+            obs = sol.run(rho0=rho0.copy(), dt=c["dt"], nt=c["nt"], temperature=c["temperature"],
+                          cutoff=c["cutoff"], reorganization=c["reorganization"], nado=c["nado"])
+            out[f"{tag}_{name}"] = np.asarray(obs)
+        for k, v in c.items():
+            out[f"{tag}_{k}"] = v
+    save("heom_chain", **out)
+
+
+@golden
 def deom_run_small():
     save("deom_run_small", **_deom_case(lmax=4, npsd=2, nt=20, dt=0.01))
 
