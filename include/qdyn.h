@@ -166,6 +166,19 @@ int qd_heom_chain_euler(qd_c128* ados, int B, int nado, int ns, const qd_c128* H
                         double D0_im, double dt, int nsteps, qd_c128* rho_sys,
                         const qd_c128* E, int ne, qd_c128* obs, void* stream);
 
+/* ------------------------------------------------------------ TDSE ------- */
+/*
+ * Batched RK4 for dpsi/dt = -i H psi (pyqed/mol.py:1603-1691 _quantum_dynamics,
+ * reached from SESolver.run mol.py:1392 / Mol.run mol.py:628; tdse phys.py:1322).
+ *   psi  [B][N] in/out; nsteps RK4 steps
+ *   snap [B][nsteps/save_every][N]  psi after steps save_every, 2 save_every, ... or NULL
+ *   E [ne][N][N], obs [B][nsteps/save_every + 1][ne] = <psi|E_m|psi> at t0 and at
+ *   every snapshot (phys.obs, phys.py:1266-1283), or NULL.   N <= 2048.
+ */
+int qd_tdse_rk4(const qd_c128* H, qd_c128* psi, int B, int N, double dt,
+                int nsteps, int save_every, qd_c128* snap, const qd_c128* E,
+                int ne, qd_c128* obs, void* stream);
+
 /* ------------------------------------------------------------ response --- */
 /*
  * SOS Liouville-space propagator U[a][b][k] = sum_j U1[a][j] e^{lam_j t_k} U2[j][b]

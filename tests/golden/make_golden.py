@@ -152,6 +152,26 @@ def lindblad_eig():
     save("lindblad_eig", **out)
 
 
+@golden
+def sesolver():
+    """SESolver.run / Mol.run -> _quantum_dynamics (mol.py:1392-1459, 628-674, 1603-1691)."""
+    from pyqed.mol import Mol, SESolver
+    rng = np.random.default_rng(31)
+    out = {}
+    for tag, N, Nt, nout, dt in [("a", 8, 10, 2, 0.05), ("b", 37, 31, 4, 0.02)]:
+        H = _herm(rng, N, 1 / np.sqrt(N))
+        E = [_herm(rng, N) for _ in range(2)]
+        psi0 = rng.standard_normal(N) + 1j * rng.standard_normal(N)
+        psi0 /= np.linalg.norm(psi0)
+        r = SESolver(H).run(psi0=psi0, dt=dt, Nt=Nt, e_ops=E, nout=nout)
+        r2 = Mol(H).run(psi0=psi0, dt=dt, e_ops=E, nt=Nt, nout=nout)
+        assert np.allclose(r.observables, r2.observables)
+        out.update({f"{tag}_H": H, f"{tag}_E": np.array(E), f"{tag}_psi0": psi0, f"{tag}_Nt": Nt,
+                    f"{tag}_nout": nout, f"{tag}_dt": dt, f"{tag}_obs": r.observables,
+                    f"{tag}_psilist": np.array(r.psilist), f"{tag}_times": r.times})
+    save("sesolver", **out)
+
+
 # ----------------------------------------------------------------- Redfield / 2DES
 # Spectral functions by name (tests/conftest.py SPECTRA holds the same definitions).
 SPECTRA = {
