@@ -223,6 +223,20 @@ int qd_response2d_ensemble(const qd_c128* alpha, const qd_c128* Mt,
 int qd_resolvent_sum(const qd_c128* coeff, const qd_c128* lam, int n,
                      const double* w, int nw, qd_c128* out, void* stream);
 
+/*
+ * Sum-over-states 2D photon-echo spectrum (GSB + SE + ESA) of pyqed/signal/sos.py:
+ * photon_echo (:962-1052) -> _photon_echo (:845-879) -> GSB (:624), SE (:731),
+ * ESA (:498).  E [N] eigenvalues (complex allowed), dip [N][N], gamma [N];
+ * g/e/f index lists (int32); omega1 = -pump.  S [n3][n1]: row = probe
+ * (omega3), column = pump (the reference's meshgrid layout; the reference
+ * itself only works for n1 == n3).
+ */
+int qd_photon_echo(const qd_c128* E, const qd_c128* dip, const double* gamma,
+                   int N, const int32_t* g_idx, int ng, const int32_t* e_idx,
+                   int ne, const int32_t* f_idx, int nf, const double* pump,
+                   int n1, const double* probe, int n3, double t2, qd_c128* S,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -161,3 +161,15 @@ class Mol:
         if pulse is not None:
             raise NotImplementedError("laser-driven dynamics (pulse=...) is not on the GPU path yet")
         return _quantum_dynamics(self.H, psi0, dt=dt, Nt=nt, e_ops=e_ops, nout=nout, t0=t0)
+
+    def eigvals(self):
+        """mol.py:459-463."""
+        H = np.asarray(self.H.toarray() if hasattr(self.H, "toarray") else self.H)
+        if np.count_nonzero(H - np.diag(np.diagonal(H))) == 0:
+            return np.diagonal(H)
+        return np.linalg.eigvals(H)
+
+    def photon_echo(self, pump, probe, t2=0.0, **kwargs):
+        """mol.py:804-829 -> sos.photon_echo (GPU)."""
+        from . import sos
+        return sos.photon_echo(self, pump=pump, probe=probe, t2=t2, **kwargs)

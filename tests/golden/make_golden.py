@@ -172,6 +172,40 @@ def sesolver():
     save("sesolver", **out)
 
 
+@golden
+def photon_echo():
+    """sos.photon_echo (signal/sos.py:962-1052) via Mol.photon_echo (mol.py:804-829)."""
+    import tempfile
+    from pyqed.mol import Mol
+    import pyqed.signal.sos as sos
+    out = {}
+    H3 = np.diag([0.0, 1.0, 1.5])
+    dip3 = np.zeros((3, 3)); dip3[0, 1] = dip3[1, 0] = 1.0; dip3[1, 2] = dip3[2, 1] = 1.0
+    rng = np.random.default_rng(41)
+    H4 = np.diag([0.0, 0.9, 1.1, 2.05])
+    d4 = rng.standard_normal((4, 4)); d4 = d4 + d4.T
+    cases = {"l3_t0": (H3, dip3, np.array([0, 0.1, 0.1]), 32, 0.0),
+             "l3_t2": (H3, dip3, np.array([0, 0.1, 0.05]), 32, 1.5),
+             "r4": (H4, d4, np.array([0.0, 0.05, 0.08, 0.1]), 48, 0.7)}
+    for tag, (H, dip, gam, n, t2) in cases.items():
+        mol = Mol(H, dip)
+        mol.edip_rms = dip
+        mol.gamma = gam
+        pump = np.linspace(0.5, 2.0, n)
+        probe = np.linspace(0.4, 2.2, n)
+        with tempfile.TemporaryDirectory() as d:
+            cwd = os.getcwd(); os.chdir(d)
+            try:
+                S = mol.photon_echo(pump=pump, probe=probe, t2=t2)
+                saved = np.load("signal.npz")
+                assert np.array_equal(saved["arr_2"], S)
+            finally:
+                os.chdir(cwd)
+        out.update({f"{tag}_H": H, f"{tag}_dip": dip, f"{tag}_gamma": gam, f"{tag}_pump": pump,
+                    f"{tag}_probe": probe, f"{tag}_t2": t2, f"{tag}_S": S})
+    save("photon_echo", **out)
+
+
 # ----------------------------------------------------------------- Redfield / 2DES
 # Spectral functions by name (tests/conftest.py SPECTRA holds the same definitions).
 SPECTRA = {
