@@ -237,6 +237,26 @@ int qd_photon_echo(const qd_c128* E, const qd_c128* dip, const double* gamma,
                    int n1, const double* probe, int n3, double t2, qd_c128* S,
                    void* stream);
 
+/* ------------------------------------------------------------ FFT -------- */
+/*
+ * In-place FFT (inverse != 0: unnormalised inverse) along the middle axis of a
+ * contiguous array [outer][n][inner], fused with fftshift (shift != 0), a scale
+ * and, when freq != NULL, the phase exp(-/+ i freq[k] x0) (forward/inverse).
+ * Implements pyqed/fft.py fft (:11-68), ifft (:70-102) and fft2 (:104-126).
+ * Powers of two in [16, 1024]: Stockham LDS FFT; other n <= 3200: direct DFT.
+ */
+int qd_fft_axis(qd_c128* data, int outer, int n, int inner, int inverse,
+                int shift, double scale, const double* freq, double x0,
+                void* stream);
+
+/*
+ * out[i][j] = weight * sum_{a,b} f[a][b] exp(-i (kx_i x_b + ky_j y_a)),
+ * f [ny][nx]: pyqed/fft.py dft (ny = 1, y = 0) and dft2 (:128-160).
+ */
+int qd_dft2(const double* x, int nx, const double* y, int ny, const qd_c128* f,
+            const double* kx, int nkx, const double* ky, int nky,
+            double weight, qd_c128* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

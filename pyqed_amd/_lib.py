@@ -59,6 +59,9 @@ SIGNATURES = {
                             c_void_p, c_void_p]),
     "qd_photon_echo": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p,
                                c_int, c_void_p, c_int, c_void_p, c_int, c_double, c_void_p, c_void_p]),
+    "qd_fft_axis": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_double, c_void_p, c_double, c_void_p]),
+    "qd_dft2": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_double,
+                        c_void_p, c_void_p]),
 }
 
 _lib = None

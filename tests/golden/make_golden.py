@@ -206,6 +206,34 @@ def photon_echo():
     save("photon_echo", **out)
 
 
+@golden
+def fft_phys():
+    """pyqed.fft fft / ifft / fft2 / dft2 (fft.py:11-160)."""
+    import importlib
+    pf = importlib.import_module("pyqed.fft")   # `pyqed.fft` the attribute is a function (phys *)
+    x = np.linspace(-10, 10, 256)
+    a = np.exp(-x ** 2 / 2) * (1 + 0.3j * x)
+    out = dict(x=x, a=a)
+    out["fft_g"], out["fft_w"] = pf.fft(a, x)
+    out["ifft_g"], out["ifft_w"] = pf.ifft(a, x)
+    x2 = np.linspace(-5, 7, 100)                       # non power of two
+    b = np.exp(-(x2 - 1) ** 2) * np.exp(0.5j * x2)
+    out["x2"], out["b"] = x2, b
+    out["fft100_g"], out["fft100_w"] = pf.fft(b, x2)
+    rng = np.random.default_rng(51)
+    M = rng.standard_normal((32, 48)) + 1j * rng.standard_normal((32, 48))
+    out["M"] = M
+    out["fftax0_g"], out["fftax0_w"] = pf.fft(M, x=np.linspace(0, 3.1, 32), axis=0)
+    out["ifftax0_g"], _ = pf.ifft(M, x=np.linspace(0, 3.1, 32), axis=0)
+    fx, fy, g2 = pf.fft2(M[:, :32], dx=0.1, dy=0.2)
+    out["fft2_fx"], out["fft2_fy"], out["fft2_g"] = fx, fy, g2
+    xs, ys = np.linspace(0, 1, 9), np.linspace(-1, 1, 7)
+    F = rng.standard_normal((7, 9)) + 0j
+    kx, ky = np.linspace(-3, 3, 5), np.linspace(-2, 2, 4)
+    out.update(xs=xs, ys=ys, F=F, kx=kx, ky=ky, dft2=pf.dft2(xs, ys, F, kx, ky))
+    save("fft_phys", **out)
+
+
 # ----------------------------------------------------------------- Redfield / 2DES
 # Spectral functions by name (tests/conftest.py SPECTRA holds the same definitions).
 SPECTRA = {
