@@ -179,6 +179,16 @@ int qd_tdse_rk4(const qd_c128* H, qd_c128* psi, int B, int N, double dt,
                 int nsteps, int save_every, qd_c128* snap, const qd_c128* E,
                 int ne, qd_c128* obs, void* stream);
 
+/*
+ * 3D multi-state split operator (pyqed/wpd.py:1349-1411 SPO3.run, linear KEO
+ * _KEO_linear wpd.py:1419-1432 = fftn over axes (0,1,2)).  psi [nx][ny][nz][ns],
+ * expVh [nx][ny][nz][ns][ns], expK [nx][ny][nz]; snap [nsteps/nout][...].
+ * nx, ny, nz powers of two in [16, 256].
+ */
+int qd_spo3_run(qd_c128* psi, const qd_c128* expVh, const qd_c128* expK, int nx,
+                int ny, int nz, int ns, int nsteps, int nout, qd_c128* snap,
+                void* stream);
+
 /* ------------------------------------------------------------ response --- */
 /*
  * SOS Liouville-space propagator U[a][b][k] = sum_j U1[a][j] e^{lam_j t_k} U2[j][b]

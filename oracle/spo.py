@@ -60,3 +60,16 @@ def spo2_run(exp_V_half, exp_K, psi0, nt, nout=1):
             psi = np.einsum("ijab,ijb->ija", exp_V_half, psi)
         psilist.append(psi.copy())
     return psilist
+
+
+def spo3_run(exp_V_half, exp_K, psi0, nt, nout=1):
+    """wpd.py:1349-1411 (return_states=True): psilist WITHOUT psi0, numpy fftn over axes (0,1,2)."""
+    psi = psi0.copy()
+    psilist = []
+    for _ in range(nt // nout):
+        for _ in range(nout):
+            psi = np.einsum("ijkab,ijkb->ijka", exp_V_half, psi)
+            psi = np.fft.ifftn(np.einsum("ijk,ijka->ijka", exp_K, np.fft.fftn(psi, axes=(0, 1, 2))), axes=(0, 1, 2))
+            psi = np.einsum("ijkab,ijkb->ijka", exp_V_half, psi)
+        psilist.append(psi.copy())
+    return psilist, psi

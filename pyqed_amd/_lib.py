@@ -62,6 +62,8 @@ SIGNATURES = {
     "qd_fft_axis": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_double, c_void_p, c_double, c_void_p]),
     "qd_dft2": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_double,
                         c_void_p, c_void_p]),
+    "qd_spo3_run": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                            c_void_p]),
 }
 
 _lib = None

@@ -189,6 +189,34 @@ __global__ __launch_bounds__(256) void spo2_col_kernel(c128* psi, const c128* ex
   }
 }
 
+// Middle-axis pass of a 3D grid psi [nx][ny][nz][ns] viewed as [outer][L][inner]
+// (inner = nz*ns): each workgroup transforms C consecutive inner indices of one
+// outer index i along the L axis (chunks of C*16 B per row: coalesced).
+template <int L, bool INV>
+__global__ __launch_bounds__(256) void spo_mid_kernel(c128* psi, const c128* tw_g, int inner, int C) {
+  __shared__ c128 tw[L];
+  __shared__ c128 A[1024], Bf[1024];  // layout [c][j], C * L <= 1024
+  const int chunks = inner / C;
+  const int i = blockIdx.x / chunks, c0 = (blockIdx.x % chunks) * C;
+  c128* base = psi + (size_t)i * L * inner + c0;
+  for (int k = threadIdx.x; k < L; k += blockDim.x) tw[k] = tw_g[k];
+  for (int e = threadIdx.x; e < L * C; e += blockDim.x) {
+    const int c = e % C, j = e / C;
+    A[c * L + j] = base[(size_t)j * inner + c];
+  }
+  __syncthreads();
+  const int T = L / 4;
+  const int f = threadIdx.x / T, t = threadIdx.x % T;
+  const bool active = f < C;
+  const int fo = (active ? f : 0) * L;
+  c128* r = fft_lds<L, INV>(A + fo, Bf + fo, tw, t, active);
+  c128* cur = (r == A + fo) ? A : Bf;
+  for (int e = threadIdx.x; e < L * C; e += blockDim.x) {
+    const int c = e % C, j = e / C;
+    base[(size_t)j * inner + c] = cur[c * L + j];
+  }
+}
+
 // expKT[j][i] = expK[i][j] * scale
 __global__ void transpose_scale_kernel(const c128* expK, int nx, int ny, double scale, c128* expKT) {
   const size_t tot = (size_t)nx * ny;
@@ -356,5 +384,91 @@ extern "C" int qd_spo1d_run(qd_c128* psi_, const qd_c128* expV_, const qd_c128* 
   QD_FFT_DISPATCH(nx, CALL1D)
 #undef CALL1D
   QD_HIP(hipGetLastError());
+  return QD_OK;
+}
+
+extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* expK_, int nx, int ny, int nz, int ns,
+                           int nsteps, int nout, qd_c128* snap_, void* stream) {
+  QD_CHECK_ARG(psi_ && expVh_ && expK_, "qd_spo3_run: null pointer");
+  QD_CHECK_ARG(pow2_in_range(nx) && pow2_in_range(ny) && pow2_in_range(nz) && nx <= 256 && ny <= 256 && nz <= 256,
+               "qd_spo3_run: nx, ny, nz must be powers of 2 in [16, 256]");
+  QD_CHECK_ARG(ns >= 1 && ns <= SPO_MAX_NS && ns * (nz / 4) <= 256 && ns * (nx / 4) <= 256,
+               "qd_spo3_run: ns=%d too large for the grid", ns);
+  QD_CHECK_ARG(nsteps >= 0 && nout >= 1, "qd_spo3_run: nsteps=%d nout=%d", nsteps, nout);
+  if (nsteps == 0) return QD_OK;
+  hipStream_t st = (hipStream_t)stream;
+  c128* psi = (c128*)psi_;
+  const c128* expVh = (const c128*)expVh_;
+  c128* snap = (c128*)snap_;
+  const int nyz = ny * nz;
+  const size_t nk = (size_t)nx * nyz;
+  void* w = nullptr;
+  int rc = workspace(WS_SPO, (nk + nx + ny + nz) * sizeof(c128), &w);
+  if (rc) return rc;
+  c128* expKT = (c128*)w;
+  c128* twx = expKT + nk;
+  c128* twy = twx + nx;
+  c128* twz = twy + ny;
+  if ((rc = twiddles(nx, st, twx))) return rc;
+  if ((rc = twiddles(ny, st, twy))) return rc;
+  if ((rc = twiddles(nz, st, twz))) return rc;
+  hipLaunchKernelGGL(transpose_scale_kernel, dim3((int)std::min<size_t>((nk + 255) / 256, 4096)), dim3(256), 0, st,
+                     (const c128*)expK_, nx, nyz, 1.0 / ((double)nx * ny * nz), expKT);
+  QD_HIP(hipGetLastError());
+  // z pass: rows = nx*ny, length nz (contiguous, fused V/2); x pass: columns = ny*nz
+  const int row_threads = std::max(64, ((ns * (nz / 4) + 63) / 64) * 64);
+  const size_t row_lds = (size_t)(nz + 2 * ns * nz) * sizeof(c128);
+  const int col_threads = std::max(64, ((2 * ns * (nx / 4) + 63) / 64) * 64);
+  const size_t col_lds = (size_t)(nx + 2 * 2 * ns * nx) * sizeof(c128);
+  const int inner = nz * ns;
+  auto row = [&](int flags, c128* sp) -> int {
+#define ROWCALL3(L) \
+  hipLaunchKernelGGL(spo2_row_kernel<L>, dim3(nx * ny), dim3(row_threads), row_lds, st, psi, expVh, twz, nz, ns, flags, sp)
+    QD_FFT_DISPATCH(nz, ROWCALL3)
+#undef ROWCALL3
+    QD_HIP(hipGetLastError());
+    return QD_OK;
+  };
+  auto col = [&]() -> int {
+#define COLCALL3(L) \
+  hipLaunchKernelGGL((spo2_col_kernel<L, 2>), dim3(nyz / 2), dim3(col_threads), col_lds, st, psi, expKT, twx, nyz, ns)
+    QD_FFT_DISPATCH(nx, COLCALL3)
+#undef COLCALL3
+    QD_HIP(hipGetLastError());
+    return QD_OK;
+  };
+  auto mid = [&](bool inv) -> int {
+    // C = 1024 / ny transforms of ny/4 threads = 256 threads; needs inner % C == 0
+    int C = 1024 / ny;  // transforms per workgroup (C * ny/4 = 256 threads)
+    while (C > 1 && inner % C) C >>= 1;
+    const int grid = nx * (inner / C);
+    const int threads = std::max(64, C * (ny / 4));
+#define MIDCALL(L)                                                                                              \
+  if (inv) hipLaunchKernelGGL((spo_mid_kernel<L, true>), dim3(grid), dim3(threads), 0, st, psi, twy, inner, C); \
+  else hipLaunchKernelGGL((spo_mid_kernel<L, false>), dim3(grid), dim3(threads), 0, st, psi, twy, inner, C)
+    switch (ny) {
+      case 16: MIDCALL(16); break;
+      case 32: MIDCALL(32); break;
+      case 64: MIDCALL(64); break;
+      case 128: MIDCALL(128); break;
+      case 256: MIDCALL(256); break;
+    }
+#undef MIDCALL
+    QD_HIP(hipGetLastError());
+    return QD_OK;
+  };
+  const size_t grid_elems = nk * ns;
+  if ((rc = row(ROW_VH1 | ROW_FWD, nullptr))) return rc;
+  if ((rc = mid(false))) return rc;
+  for (int s = 1; s <= nsteps; ++s) {
+    if ((rc = col())) return rc;
+    if ((rc = mid(true))) return rc;
+    const bool take = snap && (s % nout == 0);
+    c128* sp = take ? snap + (size_t)(s / nout - 1) * grid_elems : nullptr;
+    int flags = ROW_INV | ROW_VH1 | (take ? ROW_SNAP : 0);
+    if (s < nsteps) flags |= ROW_VH2 | ROW_FWD;
+    if ((rc = row(flags, sp))) return rc;
+    if (s < nsteps && (rc = mid(false))) return rc;
+  }
   return QD_OK;
 }

@@ -229,3 +229,84 @@ class SPO2:
         r.psilist = psilist
         r.psi = psi.cpu().numpy()
         return r
+
+
+class SPO3:
+    """Drop-in for pyqed.wpd.SPO3 (wpd.py:1105-1432), linear coordinates."""
+
+    def __init__(self, x, y, z, masses, nstates=2, coords='linear', G=None, abc=False):
+        self.x, self.y, self.z = x, y, z
+        self.X, self.Y, self.Z = meshgrid(x, y, z)
+        self.nx, self.ny, self.nz = len(x), len(y), len(z)
+        self.dx, self.dy, self.dz = interval(x), interval(y), interval(z)
+        self.masses = masses
+        self.kx = self.ky = self.kz = None
+        self.dim = 3
+        self.exp_V = self.exp_V_half = self.exp_K = None
+        self.V = None
+        self.G = G
+        self.nstates = nstates
+        self.coords = coords
+        self.abc = abc
+
+    def set_grid(self, x, y, z):
+        self.x, self.y, self.z = x, y, z
+
+    def set_masses(self, masses):
+        self.masses = masses
+
+    def setG(self, G):
+        self.G = G
+
+    def set_DPES(self, surfaces, diabatic_couplings, eta=None):
+        """wpd.py:1163-1200 (real array; couplings written symmetrically)."""
+        ns = self.nstates
+        v = np.zeros([self.nx, self.ny, self.nz, ns, ns])
+        for a in range(ns):
+            v[:, :, :, a, a] = surfaces[a]
+        for dc in diabatic_couplings:
+            a, b = dc[0][:]
+            v[:, :, :, a, b] = v[:, :, :, b, a] = np.real(dc[1])
+        self.V = v
+        return v
+
+    def build(self, dt, inertia=None):
+        """wpd.py:1210-1340 (linear): exp_K on the 'ij' grid, exp(-i V dt/2) per point."""
+        if self.coords != 'linear':
+            raise NotImplementedError("only linear coordinates run on the GPU path")
+        self.kx = 2. * np.pi * fftfreq(self.nx, self.dx)
+        self.ky = 2. * np.pi * fftfreq(self.ny, self.dy)
+        self.kz = 2. * np.pi * fftfreq(self.nz, self.dz)
+        mx, my, mz = self.masses
+        Kx, Ky, Kz = meshgrid(self.kx, self.ky, self.kz)
+        self.exp_K = np.exp(-1j * (Kx ** 2 / 2. / mx + Ky ** 2 / 2. / my + Kz ** 2 / 2. / mz) * dt)
+        if self.V is None:
+            raise ValueError('The diabatic PES is not specified.')
+        w, u = np.linalg.eigh(self.V)
+        ud = np.conj(np.swapaxes(u, -1, -2))
+        self.exp_V = (u * np.exp(-1j * w * dt)[..., None, :]) @ ud
+        self.exp_V_half = (u * np.exp(-1j * w * dt / 2)[..., None, :]) @ ud
+
+    def run(self, psi0, e_ops=[], dt=0.01, nt=1, t0=0., nout=1, return_states=True):
+        """wpd.py:1349-1411: nt//nout*nout Strang steps; psilist = state after every nout steps
+        (psi0 NOT included, as the reference); r.psi the final state."""
+        self.build(dt=dt)
+        dev = default_device()
+        _lib.ensure_device(dev)
+        nsteps = (nt // nout) * nout
+        nsnap = nt // nout
+        psi = _dev_c128(psi0, dev)
+        shape = (self.nx, self.ny, self.nz, self.nstates)
+        snap = torch.empty((nsnap,) + shape, dtype=torch.complex128, device=dev) if nsnap else None
+        eVh = _dev_c128(self.exp_V_half, dev)
+        eK = _dev_c128(self.exp_K, dev)
+        with torch.cuda.device(dev):
+            rc = _lib.load().qd_spo3_run(psi.data_ptr(), eVh.data_ptr(), eK.data_ptr(), self.nx, self.ny, self.nz,
+                                         self.nstates, int(nsteps), int(nout), _lib.ptr(snap), _lib.stream_ptr(dev))
+        _lib.check(rc, "qd_spo3_run")
+        r = Result(dt=dt, psi0=psi0, Nt=nt, t0=t0, nout=nout)
+        if snap is not None:
+            host = snap.cpu().numpy()
+            r.psilist = [host[k] for k in range(nsnap)]
+        r.psi = psi.cpu().numpy()
+        return r

@@ -373,6 +373,23 @@ def spo2_64_complex():
                keep_ops=False)
 
 
+@golden
+def spo3_16():
+    """SPO3 (wpd.py:1105-1432) on a 16^3 x 2 grid, examples/spo.py model (64^3 x 2 there)."""
+    from pyqed.wpd import SPO3
+    n = 16
+    x = np.linspace(-6, 6, n)
+    X, Y, Z = np.meshgrid(x, x, x, indexing="ij")
+    sol = SPO3(x, x, x, masses=[1.0, 1.0, 1.0], nstates=2)
+    sol.set_DPES([0.5 * ((X + 1) ** 2 + Y ** 2 + Z ** 2), 0.5 * ((X - 1) ** 2 + Y ** 2 + Z ** 2)],
+                 [[[0, 1], 0.2 * X]])
+    psi0 = np.zeros((n, n, n, 2), dtype=complex)
+    psi0[..., 1] = np.exp(-((X + 1) ** 2 + Y ** 2 + Z ** 2) / 2) / np.pi ** 0.75
+    r = sol.run(psi0=psi0, dt=0.25, nt=4, nout=2)
+    save("spo3_16", x=x, psi0_norm=np.vdot(psi0, psi0).real, dt=0.25, nt=4, nout=2,
+         psilist=np.array(r.psilist), psi=r.psi)
+
+
 def _spo1d_case(name, n, nt, nout, dt):
     from pyqed.wpd import SPO
     x = np.linspace(-8, 8, n)
