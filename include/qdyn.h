@@ -189,6 +189,18 @@ int qd_spo3_run(qd_c128* psi, const qd_c128* expVh, const qd_c128* expK, int nx,
                 int ny, int nz, int ns, int nsteps, int nout, qd_c128* snap,
                 void* stream);
 
+/*
+ * RK4 with a dense Liouville-space generator, d v/dt = L v (B vectors).
+ * Replaces the csr GEMV loop of pyqed/oqs.py:436-463 (_redfield + rhs) for any
+ * dense superoperator.  L [N2][N2], v [B][N2] in/out (row-major vec(rho)),
+ * W [ne][N2]: obs[b][k][m] = sum_j W[m][j] v_k[b][j] for k = 0..nsteps
+ * (W = vec(E^T) gives Tr(E rho)), snap [B][nsteps/save_every][N2] or NULL.
+ * HBM-bound: 16 N2^2 bytes per stage per group of 4 vectors.
+ */
+int qd_superop_rk4(const qd_c128* L, qd_c128* v, int B, int N2, double dt,
+                   int nsteps, const qd_c128* W, int ne, qd_c128* obs,
+                   qd_c128* snap, int save_every, void* stream);
+
 /* ------------------------------------------------------------ response --- */
 /*
  * SOS Liouville-space propagator U[a][b][k] = sum_j U1[a][j] e^{lam_j t_k} U2[j][b]

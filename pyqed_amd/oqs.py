@@ -227,6 +227,61 @@ def glf_rk4(P, Q, L, R, rho, dt, nsteps, e_ops=None, save_every=0, stream=None):
     return obs, snap
 
 
+def superop_rk4(L: torch.Tensor, v: torch.Tensor, dt, nsteps, W: torch.Tensor | None = None, save_every=0):
+    """d v/dt = L v, batched RK4 with a dense superoperator (qd_superop_rk4).  L [N2,N2], v [B,N2] in place,
+    W [ne,N2] observable weights.  Returns (obs [B,nsteps+1,ne] | None, snap [B,nsave,N2] | None)."""
+    dev = v.device
+    _lib.ensure_device(dev)
+    B, N2 = v.shape
+    ne = 0 if W is None else W.shape[0]
+    obs = torch.empty((B, nsteps + 1, ne), dtype=torch.complex128, device=dev) if ne else None
+    nsave = nsteps // save_every if save_every > 0 else 0
+    snap = torch.empty((B, nsave, N2), dtype=torch.complex128, device=dev) if nsave else None
+    with torch.cuda.device(dev):
+        rc = _lib.load().qd_superop_rk4(_lib.ptr(L), _lib.ptr(v), B, N2, float(dt), int(nsteps), _lib.ptr(W), ne,
+                                        _lib.ptr(obs), _lib.ptr(snap), int(save_every if nsave else 0),
+                                        _lib.stream_ptr(dev))
+    _lib.check(rc, "qd_superop_rk4")
+    return obs, snap
+
+
+def _redfield(R, rho0, evecs=None, Nt=1, dt=0.005, t0=0, e_ops=[], return_result=True):
+    """oqs.py:364-459 with an explicit (dense or csr) R: RK4 on vec(rho~) on the GPU, observables
+    (Nt, n_e) EXCLUDING t0, rholist back-transformed with dag(evecs)."""
+    N = np.asarray(rho0.toarray() if hasattr(rho0, "toarray") else rho0).shape[0]
+    dev = default_device()
+    if e_ops is None:
+        e_ops = []
+    Rd = torch.from_numpy(np.ascontiguousarray(_dense(R))).to(dev)
+    rho = to_device(rho0, dev).reshape(1, N, N).clone()
+    Ed = stack_ops(e_ops, N, dev)
+    if evecs is not None:
+        ev = torch.from_numpy(np.ascontiguousarray(np.asarray(evecs, dtype=complex))).to(dev)
+        basis_transform(ev, rho, inverse=False)
+        if Ed is not None:
+            basis_transform(ev, Ed, inverse=False)
+    W = Ed.transpose(1, 2).reshape(len(e_ops), N * N).contiguous() if Ed is not None else None  # vec(E^T)
+    v = rho.reshape(1, N * N).contiguous()
+    rho0_eb = rho[0].cpu().numpy()
+    obs, snap = superop_rk4(Rd, v, dt, Nt, W, save_every=1)
+    result = Result(dt=dt, Nt=Nt, rho0=rho0_eb)
+    result.observables = obs[0, 1:].cpu().numpy() if obs is not None else np.zeros((Nt, 0), complex)
+    if snap is not None:
+        back = snap[0].reshape(Nt, N, N).contiguous()
+        if evecs is not None:
+            basis_transform(ev, back, inverse=True)
+        host = back.cpu().numpy()
+        result.rholist = [host[k] for k in range(Nt)]
+    else:
+        result.rholist = []
+    return result
+
+
+def rhs(psi, H):
+    """oqs.py:462-463 (host helper of the reference's RK4 RHS)."""
+    return H.dot(psi)
+
+
 def basis_transform(V: torch.Tensor, A: torch.Tensor, inverse=False):
     """In place: A <- V^+ A V (inverse=False, phys.transform) or V A V^+ (inverse=True). A [B,N,N]."""
     dev = A.device
@@ -342,7 +397,10 @@ class RedfieldSolver:
 
     def evolve(self, rho0, dt, Nt, evecs=None, e_ops=[], store_states=False, t0=0, nout=1):
         """oqs.py:57-81 -> _redfield (oqs.py:364-459): observables (Nt, n_e) EXCLUDING t0,
-        rholist (Nt) back-transformed to the original basis."""
+        rholist (Nt) back-transformed to the original basis.  With an R set by the caller (no
+        spectra), the dense-superoperator kernel propagates R.vec(rho) as the reference does."""
+        if self.spectra is None and self.R is not None:
+            return _redfield(self.R, rho0, evecs=self.evecs, Nt=Nt, dt=dt, t0=t0, e_ops=e_ops)
         self._prepare()
         dev = default_device()
         P, Q, Ls, Rs = self.glf_terms()

@@ -115,3 +115,32 @@ def test_ensemble_large_linearity_and_shards():
     ref = (-1j) ** 3 * X @ Mt[m] @ Y.T
     one = response2d_ensemble(lam[m:m + 1], alpha[m:m + 1], Mt[m:m + 1], beta[m:m + 1], t, t)
     assert relerr(one.cpu().numpy(), ref) < TOL
+
+
+@pytest.mark.parametrize("name", ["redfield_n4", "redfield_n6_k2"])
+def test_redfield_dense_superop_path(name):
+    """Module-level _redfield(R, ...) (oqs.py:364-459) on the HBM-bound dense-superoperator kernel."""
+    from pyqed_amd.oqs import _redfield
+    g = load_golden(name)
+    r = _redfield(g["R"], g["rho0"], evecs=g["evecs"], Nt=int(g["Nt"]), dt=float(g["dt"]), e_ops=list(g["E"]))
+    assert relerr(r.observables, g["observables"]) < TOL
+    assert relerr(np.array(r.rholist), g["rholist"]) < TOL
+
+
+def test_superop_batch_vs_glf():
+    """Dense L.vec(rho) (Lindblad superoperator, N=24, B=6 -> two groups of <=4) vs the GLF kernel."""
+    import torch
+    from oracle import lindblad as olb
+    from pyqed_amd import lindblad_rk4
+    from pyqed_amd.oqs import superop_rk4
+    from pyqed_amd.superoperator import liouvillian
+    N, B = 24, 6
+    H, cs = olb.synthetic_lindblad(N)
+    L = liouvillian(H, cs).toarray()
+    rho0 = olb.random_pure_states(B, N)
+    dev = torch.device("cuda", 0)
+    v = torch.from_numpy(rho0.reshape(B, N * N).copy()).to(dev)
+    superop_rk4(torch.from_numpy(L).to(dev), v, 0.01, 20)
+    rho = torch.from_numpy(rho0.copy()).to(dev)
+    lindblad_rk4(torch.from_numpy(H).to(dev), torch.from_numpy(np.array(cs)).to(dev), rho, 0.01, 20)
+    assert relerr(v.cpu().numpy().reshape(B, N, N), rho.cpu().numpy()) < 1e-12
