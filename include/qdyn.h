@@ -72,6 +72,18 @@ int qd_lindblad_rk4(const qd_c128* H, const qd_c128* C, int nc, qd_c128* rho,
                     void* stream);
 
 /*
+ * Driven Lindblad RK4 (pyqed/oqs.py:1699-1806 _lindblad_driven):
+ *   H(t_k) = H0 - sum_d f_d(t_k) Hd_d, constant within step k, t_k = t0 + (k+1) dt
+ * fvals is a HOST array [nsteps][nd] of the drive values (complex).  Other
+ * arguments as qd_lindblad_rk4 (obs row 0 = t0).  1 <= nd <= 16.
+ */
+int qd_lindblad_driven_rk4(const qd_c128* H0, const qd_c128* Hd, int nd,
+                           const qd_c128* fvals, const qd_c128* C, int nc,
+                           qd_c128* rho, int B, int N, double dt, int nsteps,
+                           const qd_c128* E, int ne, qd_c128* obs, qd_c128* snap,
+                           int save_every, void* stream);
+
+/*
  * Batched RK4 for any equation of motion of "generalised Lindblad form"
  *     d rho/dt = P rho + rho Q + sum_c L_c rho R_c        (c < npairs)
  * P, Q [N][N]; L, R [npairs][N][N]; other arguments as qd_lindblad_rk4.

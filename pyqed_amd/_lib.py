@@ -66,6 +66,8 @@ SIGNATURES = {
                             c_void_p]),
     "qd_superop_rk4": (c_int, [c_void_p, c_void_p, c_int, c_int, c_double, c_int, c_void_p, c_int, c_void_p,
                                c_void_p, c_int, c_void_p]),
+    "qd_lindblad_driven_rk4": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int,
+                                       c_double, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
 }
 
 _lib = None

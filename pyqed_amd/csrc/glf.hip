@@ -44,6 +44,7 @@ struct LindbladParams {
   c128* obs;        // [B][nsteps+1][ne]
   c128* snap;       // [B][nsave][N][N]
   int N, Np, nc, ne, nsteps, save_every, nsave;
+  int step0, total_steps;  // this launch runs global steps step0 .. step0+nsteps-1 of total_steps
   double dt;
 };
 
@@ -88,10 +89,10 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
   c128* rs[2] = {ws, ws + NN};
   c128* acc = ws + 2 * NN;
   c128* Y = ws + 3 * NN;
-  c128* obs = p.obs ? p.obs + (size_t)b * (p.nsteps + 1) * p.ne : nullptr;
+  c128* obs = p.obs ? p.obs + (size_t)b * (p.total_steps + 1) * p.ne : nullptr;
 
   for (size_t i = threadIdx.x; i < NN; i += CG_WG) rs[0][i] = rho[i];
-  if (p.ne > 0) wg_observables(rho, p.eT, p.ne, NN, obs, sred);
+  if (p.ne > 0 && p.step0 == 0) wg_observables(rho, p.eT, p.ne, NN, obs, sred);
   __syncthreads();
 
   const int nb = Np / BT;
@@ -153,9 +154,10 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
       __syncthreads();
       cur ^= 1;
     }
-    if (p.ne > 0) wg_observables(rho, p.eT, p.ne, NN, obs + (size_t)(step + 1) * p.ne, sred);
-    if (p.snap && p.save_every > 0 && ((step + 1) % p.save_every) == 0) {
-      const int s = (step + 1) / p.save_every - 1;
+    const int gs = p.step0 + step + 1;  // global step count after this step
+    if (p.ne > 0) wg_observables(rho, p.eT, p.ne, NN, obs + (size_t)gs * p.ne, sred);
+    if (p.snap && p.save_every > 0 && (gs % p.save_every) == 0) {
+      const int s = gs / p.save_every - 1;
       if (s < p.nsave) {
         const int N = p.N;
         c128* out = p.snap + ((size_t)b * p.nsave + s) * N * N;
@@ -309,13 +311,34 @@ namespace {
 enum GlfSource { GLF_FROM_LINDBLAD = 0, GLF_FROM_OPERATORS = 1 };
 
 // Shared driver of qd_lindblad_rk4 / qd_glf_rk4.
+// K(t) = K0 - sum_d f_d Hd_d ; mK = -iK ; iKd = iK^+   (time-dependent Hamiltonian of
+// _lindblad_driven, oqs.py:1725-1732: H(t) = H0 - sum_i f_i(t) H_i, constant within a step)
+__global__ void driven_update_kernel(const c128* K0, const c128* Hd, int nd, const c128* f, int N, int Np, c128* mK,
+                                     c128* iKd) {
+  const size_t NN = (size_t)Np * Np;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < NN; e += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(e / Np), j = (int)(e % Np);
+    c128 K = K0[e];
+    if (i < N && j < N)
+      for (int d = 0; d < nd; ++d) K = csub(K, cmul(f[d], Hd[(size_t)d * N * N + (size_t)i * N + j]));
+    mK[e] = cmulmi(K);
+    iKd[(size_t)j * Np + i] = cmuli(cconj(K));
+  }
+}
+
+__global__ void save_k0_kernel(const c128* mK, size_t NN, c128* K0) {
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < NN; e += (size_t)gridDim.x * blockDim.x)
+    K0[e] = cmuli(mK[e]);  // K = i * (-iK)
+}
+
 int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c128* Q, const c128* Lop,
             const c128* Rop, int nc, c128* rho, int B, int N, double dt, int nsteps, const c128* E, int ne,
-            c128* obs, c128* snap, int save_every, hipStream_t st) {
+            c128* obs, c128* snap, int save_every, hipStream_t st, const c128* Hd = nullptr, int nd = 0,
+            const qd_c128* fvals = nullptr) {
   const int Np = padded_dim(N);
   const size_t NN = (size_t)Np * Np;
-  // operator workspace: Cop(L), mK(P), iKd(Q), Cd(R), eT
-  const size_t ops_elems = (size_t)(2 + 2 * nc + ne) * NN;
+  // operator workspace: Cop(L), mK(P), iKd(Q), Cd(R), eT, [K0, f scratch for driven runs]
+  const size_t ops_elems = (size_t)(2 + 2 * nc + ne + (nd ? 1 : 0)) * NN + (size_t)nd * nsteps;
   void* wops = nullptr;
   int rc = workspace(WS_LINDBLAD_OPS, ops_elems * sizeof(c128), &wops);
   if (rc) return rc;
@@ -324,6 +347,8 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   c128* iKd = mK + NN;
   c128* Cd = iKd + NN;
   c128* eT = Cd + (size_t)nc * NN;
+  c128* K0 = eT + (size_t)ne * NN;
+  c128* fdev = K0 + (nd ? NN : 0);
   // state workspace: per-matrix scratch (+ padded rho when N != Np)
   const bool pad = (Np != N);
   const size_t st_elems = (size_t)B * (3 + nc) * NN + (pad ? (size_t)B * NN : 0);
@@ -342,6 +367,12 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
     hipLaunchKernelGGL(glf_prep_kernel, dim3(blocks), dim3(threads), 0, st, P, Q, Lop, Rop, nc, E, ne, N, Np, Cop,
                        mK, iKd, Cd, eT);
   QD_HIP(hipGetLastError());
+  if (nd) {
+    hipLaunchKernelGGL(save_k0_kernel, dim3(blocks), dim3(threads), 0, st, (const c128*)mK, NN, K0);
+    QD_HIP(hipGetLastError());
+    if (nsteps > 0)
+      QD_HIP(hipMemcpyAsync(fdev, fvals, (size_t)nd * nsteps * sizeof(c128), hipMemcpyHostToDevice, st));
+  }
   if (pad) {
     const size_t tot = (size_t)B * NN;
     const int pb = (int)std::min<size_t>((tot + threads - 1) / threads, 65535);
@@ -367,14 +398,32 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   p.save_every = save_every;
   p.nsave = (save_every > 0) ? nsteps / save_every : 0;
   p.dt = dt;
+  p.step0 = 0;
+  p.total_steps = nsteps;
 
-  if (Np == 32)
-    hipLaunchKernelGGL(lindblad_rk4_kernel<32>, dim3(B), dim3(CG_WG), 0, st, p);
-  else if (Np == 64)
-    hipLaunchKernelGGL(lindblad_rk4_kernel<64>, dim3(B), dim3(CG_WG), 0, st, p);
-  else
-    hipLaunchKernelGGL(lindblad_rk4_kernel<128>, dim3(B), dim3(CG_WG), 0, st, p);
-  QD_HIP(hipGetLastError());
+  auto launch = [&]() -> int {
+    if (Np == 32)
+      hipLaunchKernelGGL(lindblad_rk4_kernel<32>, dim3(B), dim3(CG_WG), 0, st, p);
+    else if (Np == 64)
+      hipLaunchKernelGGL(lindblad_rk4_kernel<64>, dim3(B), dim3(CG_WG), 0, st, p);
+    else
+      hipLaunchKernelGGL(lindblad_rk4_kernel<128>, dim3(B), dim3(CG_WG), 0, st, p);
+    QD_HIP(hipGetLastError());
+    return QD_OK;
+  };
+  if (!nd) {
+    if ((rc = launch())) return rc;
+  } else {
+    // one launch per step: H(t_k) is constant within a step (oqs.py:1780-1786 evaluates it once per step)
+    p.nsteps = 1;
+    for (int k = 0; k < nsteps; ++k) {
+      hipLaunchKernelGGL(driven_update_kernel, dim3(blocks), dim3(threads), 0, st, (const c128*)K0, Hd, nd,
+                         (const c128*)fdev + (size_t)k * nd, N, Np, mK, iKd);
+      QD_HIP(hipGetLastError());
+      p.step0 = k;
+      if ((rc = launch())) return rc;
+    }
+  }
 
   if (pad) {
     const size_t tot = (size_t)B * N * N;
@@ -475,4 +524,18 @@ extern "C" int qd_sandwich(const qd_c128* Lm, const qd_c128* Rm, qd_c128* A, int
   QD_CHECK_ARG(Lm && Rm && A, "qd_sandwich: null pointer");
   QD_CHECK_ARG(N >= 1 && N <= 1024 && B >= 1, "qd_sandwich: bad sizes N=%d B=%d", N, B);
   return sandwich_run(nullptr, (const c128*)Lm, (const c128*)Rm, (c128*)A, B, N, 2, (hipStream_t)stream);
+}
+
+extern "C" int qd_lindblad_driven_rk4(const qd_c128* H0, const qd_c128* Hd, int nd, const qd_c128* fvals,
+                                      const qd_c128* C, int nc, qd_c128* rho, int B, int N, double dt, int nsteps,
+                                      const qd_c128* E, int ne, qd_c128* obs, qd_c128* snap, int save_every,
+                                      void* stream) {
+  QD_CHECK_ARG(H0 && rho, "qd_lindblad_driven_rk4: H0 and rho must be non-null");
+  int rc = check_common("qd_lindblad_driven_rk4", rho, B, N, nc, ne, E, obs, nsteps);
+  if (rc) return rc;
+  QD_CHECK_ARG(nc == 0 || C, "qd_lindblad_driven_rk4: C is null but nc=%d", nc);
+  QD_CHECK_ARG(nd >= 1 && nd <= 16 && Hd && fvals, "qd_lindblad_driven_rk4: need 1 <= nd <= 16 drive terms");
+  return glf_run(GLF_FROM_LINDBLAD, (const c128*)H0, (const c128*)C, nullptr, nullptr, nullptr, nullptr, nc,
+                 (c128*)rho, B, N, dt, nsteps, (const c128*)E, ne, (c128*)obs, (c128*)snap, save_every,
+                 (hipStream_t)stream, (const c128*)Hd, nd, fvals);
 }

@@ -96,7 +96,8 @@ class LindbladSolver:
         `return_states=False` (extension) skips the per-step snapshots.
         """
         if isinstance(self.H, list):
-            raise NotImplementedError("time-dependent H ([H0, [f, H1]]) is not on the GPU path yet")
+            return _lindblad_driven(self.H, rho0=rho0, c_ops=self.c_ops, e_ops=e_ops, Nt=Nt, dt=dt, t0=t0,
+                                    return_states=return_states)
         return _lindblad(self.H, rho0, c_ops=self.c_ops, e_ops=e_ops, Nt=Nt, dt=dt,
                          return_states=return_states)
 
@@ -147,6 +148,53 @@ class LindbladSolver:
             raise ValueError('Number of operators is not 4.')
         a, b, c, d = ops
         return self.correlation_3op_2t(rho0, [a, _dense(b) @ _dense(c), d], dt, nt, ntau)
+
+
+def _lindblad_driven(H, rho0, c_ops=None, e_ops=None, Nt=1, dt=0.005, t0=0., return_result=True,
+                     return_states=True):
+    """oqs.py:1699-1806: H = [H0, [H1, f1], ...], H(t) = H0 - sum f_i(t) H_i evaluated once per step at
+    t_k = t0 + (k+1) dt.  observables (Nt, n_e) EXCLUDE t0; rholist has Nt csr matrices.
+    (With the csr H0 the reference requires, `Ht += ...` rebinds instead of mutating H0, so no
+    drive accumulates; a dense H0 fails in the reference's RHS.)"""
+    if c_ops is None:
+        c_ops = []
+    if e_ops is None:
+        e_ops = []
+    dev = default_device()
+    H0 = _dense(H[0])
+    N = H0.shape[0]
+    drives = H[1:]
+    nd = len(drives)
+    Hd = torch.from_numpy(np.ascontiguousarray(np.array([_dense(h[0]) for h in drives]).reshape(nd, N, N))).to(dev)
+    f = np.zeros((Nt, nd), dtype=complex)
+    t = t0
+    for k in range(Nt):
+        t += dt
+        f[k] = [h[1](t) for h in drives]
+    f = np.ascontiguousarray(f)
+    Cd = stack_ops(c_ops, N, dev)
+    Ed = stack_ops(e_ops, N, dev)
+    rho = to_device(rho0, dev).reshape(1, N, N).clone()
+    ne = len(e_ops)
+    obs = torch.empty((1, Nt + 1, ne), dtype=torch.complex128, device=dev) if ne else None
+    snap = torch.empty((1, Nt, N, N), dtype=torch.complex128, device=dev) if (return_states and Nt) else None
+    H0d = torch.from_numpy(H0).to(dev)
+    _lib.ensure_device(dev)
+    with torch.cuda.device(dev):
+        rc = _lib.load().qd_lindblad_driven_rk4(H0d.data_ptr(), Hd.data_ptr(), nd, f.ctypes.data, _lib.ptr(Cd),
+                                                0 if Cd is None else Cd.shape[0], rho.data_ptr(), 1, N, float(dt),
+                                                int(Nt), _lib.ptr(Ed), ne, _lib.ptr(obs), _lib.ptr(snap),
+                                                1 if snap is not None else 0, _lib.stream_ptr(dev))
+    _lib.check(rc, "qd_lindblad_driven_rk4")
+    result = Result(dt=dt, Nt=Nt, rho0=rho0)
+    result.observables = obs[0, 1:].cpu().numpy() if obs is not None else np.zeros((Nt, 0), complex)
+    if snap is not None:
+        host = snap[0].cpu().numpy()
+        result.rholist = [csr_matrix(host[k]) for k in range(Nt)]
+    else:
+        result.rholist = []
+    result.rho = rho[0].cpu().numpy()
+    return result
 
 
 def _dense(a):

@@ -89,6 +89,31 @@ def lindblad_n128():
 
 
 @golden
+def lindblad_driven():
+    """LindbladSolver.run with H = [H0, [H1, f]] -> _lindblad_driven (oqs.py:1699-1806)."""
+    import pyqed.oqs as oqs
+    rng = np.random.default_rng(16)
+    N = 6
+    H0 = _herm(rng, N, 1 / np.sqrt(N))
+    H1 = _herm(rng, N, 0.3)
+    H2 = _herm(rng, N, 0.2)
+    C = _ginibre(rng, N, 0.2 / np.sqrt(N))
+    E = _herm(rng, N)
+    psi = rng.standard_normal(N) + 1j * rng.standard_normal(N)
+    psi /= np.linalg.norm(psi)
+    rho0 = np.outer(psi, psi.conj())
+    f1 = lambda t: np.cos(2.0 * t) * np.exp(-(t - 0.3) ** 2)
+    f2 = lambda t: 0.5 * np.sin(t)
+    H0c = csr_matrix(H0)
+    H0_before = H0c.toarray().copy()
+    sol = oqs.LindbladSolver([H0c, [csr_matrix(H1), f1], [csr_matrix(H2), f2]], [csr_matrix(C)])
+    r = sol.run(rho0, dt=0.02, Nt=25, t0=0.1, e_ops=[csr_matrix(E)])
+    h0_mutated = not np.array_equal(H0c.toarray(), H0_before)
+    save("lindblad_driven", H0=H0, H1=H1, H2=H2, C=C, E=E, rho0=rho0, dt=0.02, Nt=25, t0=0.1,
+         observables=r.observables, rholist=np.array([x.toarray() for x in r.rholist]), h0_mutated=h0_mutated)
+
+
+@golden
 def lindblad_corr():
     """LindbladSolver correlation functions (oqs.py:1193-1329, _correlation_2p_1t oqs.py:717-791)."""
     import tempfile

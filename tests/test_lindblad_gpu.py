@@ -149,3 +149,19 @@ def test_sandwich_batched():
         At = torch.from_numpy(A.copy()).to(dev)
         sandwich(torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev), At)
         assert relerr(At.cpu().numpy(), L @ A @ R) < 1e-13
+
+
+def test_lindblad_driven_matches_reference():
+    from scipy.sparse import csr_matrix
+    from pyqed_amd import LindbladSolver
+    g = load_golden("lindblad_driven")
+    assert not bool(g["h0_mutated"])
+    f1 = lambda t: np.cos(2.0 * t) * np.exp(-(t - 0.3) ** 2)
+    f2 = lambda t: 0.5 * np.sin(t)
+    H0 = csr_matrix(g["H0"])
+    sol = LindbladSolver([H0, [csr_matrix(g["H1"]), f1], [csr_matrix(g["H2"]), f2]], [csr_matrix(g["C"])])
+    r = sol.run(g["rho0"], dt=float(g["dt"]), Nt=int(g["Nt"]), t0=float(g["t0"]), e_ops=[csr_matrix(g["E"])])
+    assert r.observables.shape == g["observables"].shape
+    assert relerr(r.observables, g["observables"]) < TOL
+    assert relerr(np.array([x.toarray() for x in r.rholist]), g["rholist"]) < TOL
+    assert np.array_equal(H0.toarray(), g["H0"])
