@@ -94,8 +94,9 @@ def bench_2des(dev, world, rank, M_total, reps, n=256):
     """Ensemble 2DES (t3, t1) grid at fixed t2: members sharded over ranks, one RCCL reduce."""
     import torch
     import torch.distributed as dist
+    from pyqed_amd.distributed import shard_range, sharded_sum
     from pyqed_amd.response import response2d_ensemble
-    lo, hi = M_total * rank // world, M_total * (rank + 1) // world
+    lo, hi = shard_range(M_total, rank, world)
     lam, alpha, Mt, beta = twodes_inputs(M_total)
     sl = slice(lo, hi)
     to = lambda x: torch.from_numpy(np.ascontiguousarray(x[sl])).to(dev)
@@ -103,12 +104,14 @@ def bench_2des(dev, world, rank, M_total, reps, n=256):
     t = torch.from_numpy(0.5 * np.arange(n)).to(dev)
     out = torch.empty((n, n), dtype=torch.complex128, device=dev)
 
-    def once():
-        response2d_ensemble(lam_t, alpha_t, Mt_t, beta_t, t, t, out=out, accumulate=False)
-        if world > 1:
-            dist.reduce(out, dst=0, op=dist.ReduceOp.SUM)
+    def local(a, b):
+        # this rank's members are already resident on its GPU (inputs in HBM before timing)
+        return response2d_ensemble(lam_t, alpha_t, Mt_t, beta_t, t, t, out=out, accumulate=False)
 
-    once()
+    def once():
+        return sharded_sum(local, M_total, dst=0)   # one RCCL reduce(sum) of the 1 MiB grid when world > 1
+
+    out = once()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

@@ -1,0 +1,92 @@
+"""Multi-process path on CPU with gloo (world_size 2): sharding + the single reduce reproduce the
+single-process result.  The per-rank compute is the oracle's closed-form 2DES slice (CPU)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _inputs(M=37, n=24):
+    rng = np.random.default_rng(5)
+    lam = -0.1 * rng.random((M, 9)) + 1j * rng.standard_normal((M, 9))
+    alpha = rng.standard_normal((M, 9)) + 1j * rng.standard_normal((M, 9))
+    beta = rng.standard_normal((M, 9)) + 1j * rng.standard_normal((M, 9))
+    Mt = rng.standard_normal((M, 9, 9)) + 1j * rng.standard_normal((M, 9, 9))
+    t = 0.5 * np.arange(n)
+    return lam, alpha, Mt, beta, t
+
+
+def _slice_sum(lam, alpha, Mt, beta, t, lo, hi):
+    out = np.zeros((len(t), len(t)), complex)
+    for m in range(lo, hi):
+        X = alpha[m][None, :] * np.exp(np.outer(t, lam[m]))
+        Y = beta[m][None, :] * np.exp(np.outer(t, lam[m]))
+        out += (-1j) ** 3 * X @ Mt[m] @ Y.T
+    return out
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pyqed_amd.distributed import sharded_sum, world as w
+    assert w() == (rank, world)
+    lam, alpha, Mt, beta, t = _inputs()
+
+    def local(lo, hi):
+        return torch.from_numpy(_slice_sum(lam, alpha, Mt, beta, t, lo, hi))
+
+    out = sharded_sum(local, len(lam), dst=0)
+    allr = sharded_sum(local, len(lam), dst=None)
+    if rank == 0:
+        q.put((out.numpy(), allr.numpy()))
+    else:
+        q.put((None, allr.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_2des_reduce_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    lam, alpha, Mt, beta, t = _inputs()
+    full = _slice_sum(lam, alpha, Mt, beta, t, 0, len(lam))
+    reduced = [r[0] for r in res if r[0] is not None]
+    assert len(reduced) == 1
+    assert np.allclose(reduced[0], full, rtol=1e-12, atol=1e-12 * np.abs(full).max())
+    for _, a in res:
+        assert np.allclose(a, full, rtol=1e-12, atol=1e-12 * np.abs(full).max())
+
+
+def test_shard_range_partition():
+    from pyqed_amd.distributed import shard_range
+    for n in [0, 1, 7, 4096, 4097]:
+        for ws in [1, 2, 3, 8]:
+            parts = [shard_range(n, r, ws) for r in range(ws)]
+            assert parts[0][0] == 0 and parts[-1][1] == n
+            assert all(parts[i][1] == parts[i + 1][0] for i in range(ws - 1))
+            sizes = [h - l for l, h in parts]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        shard_range(4, 2, 2)
