@@ -52,31 +52,16 @@ struct CgAcc {
 // Number of complex elements per thread for one A (or B) tile.
 template <int BT> constexpr int cg_nld() { return (BT * CG_KT) / CG_WG; }
 
-template <int BT>
-__device__ __forceinline__ void cg_load_tile(const CgSeg& s, int lda, int ldb, int k0, c128 (&ra)[cg_nld<BT>()],
-                                             c128 (&rb)[cg_nld<BT>()]) {
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int q = 0; q < cg_nld<BT>(); ++q) {
-    const int e = tid + CG_WG * q;
-    const int ar = e >> 4, ac = e & 15;                 // A tile: BT rows x 16
-    ra[q] = s.A[(size_t)ar * lda + k0 + ac];
-    const int br = e / BT, bc = e % BT;                 // B tile: 16 rows x BT
-    rb[q] = s.B[(size_t)(k0 + br) * ldb + bc];
-  }
-}
+// Staging registers are plain 16-B vectors and the loads go through an explicit
+// global (address space 1) pointer: global_load_dwordx4 that stay in flight
+// across the MFMA work of the current tile (no flat loads, no scratch round trip).
+typedef double cg_v2 __attribute__((ext_vector_type(2)));
+typedef const __attribute__((address_space(1))) cg_v2 cg_gv2;
 
-template <int BT>
-__device__ __forceinline__ void cg_store_tile(CgLds<BT>& L, int buf, const c128 (&ra)[cg_nld<BT>()],
-                                              const c128 (&rb)[cg_nld<BT>()]) {
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int q = 0; q < cg_nld<BT>(); ++q) {
-    const int e = tid + CG_WG * q;
-    L.a[buf][(e >> 4) * CG_SA + (e & 15)] = ra[q];
-    L.b[buf][e] = rb[q];  // row (e / BT), col (e % BT), stride BT
-  }
+__device__ __forceinline__ cg_v2 cg_ld(const c128* p) {
+  return *(cg_gv2*)(p);  // generic -> global address-space cast (the pointer is a global buffer)
 }
+__device__ __forceinline__ void cg_st_lds(c128* p, cg_v2 v) { *reinterpret_cast<cg_v2*>(p) = v; }
 
 template <int BT>
 __device__ __forceinline__ void cg_compute_tile(const CgLds<BT>& L, int buf, CgAcc<BT>& acc, int wr0, int wc0) {
@@ -109,6 +94,8 @@ __device__ __forceinline__ void cg_compute_tile(const CgLds<BT>& L, int buf, CgA
 
 // Accumulate sum_s A_s * B_s over nseg segments of depth K (K % 16 == 0) into
 // a zero-initialised accumulator.  All threads of the workgroup must call it.
+// `segs` should live in LDS (or be uniform): it is indexed at run time, and a
+// private array indexed at run time would be placed in scratch memory.
 // Ends with a workgroup barrier, so LDS may be reused immediately after.
 template <int BT>
 __device__ __forceinline__ void cg_block_gemm(const CgSeg* segs, int nseg, int K, int lda, int ldb, CgLds<BT>& L,
@@ -125,20 +112,38 @@ __device__ __forceinline__ void cg_block_gemm(const CgSeg* segs, int nseg, int K
       acc.re[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
       acc.im[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
     }
+  constexpr int NLD = cg_nld<BT>();
   const int tiles_per_seg = K / CG_KT;
   const int T = nseg * tiles_per_seg;
-  c128 ra[cg_nld<BT>()], rb[cg_nld<BT>()];
-  cg_load_tile<BT>(segs[0], lda, ldb, 0, ra, rb);
-  cg_store_tile<BT>(L, 0, ra, rb);
+  const int tid = threadIdx.x;
+  // per-thread element offsets inside a tile (A: BT rows x 16, B: 16 rows x BT)
+  cg_v2 ra[NLD], rb[NLD];
+  auto load = [&](int t) {
+    const CgSeg sg = segs[t / tiles_per_seg];
+    const int k0 = (t % tiles_per_seg) * CG_KT;
+#pragma unroll
+    for (int q = 0; q < NLD; ++q) {
+      const int e = tid + CG_WG * q;
+      ra[q] = cg_ld(sg.A + (size_t)(e >> 4) * lda + k0 + (e & 15));
+      rb[q] = cg_ld(sg.B + (size_t)(k0 + e / BT) * ldb + (e % BT));
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < NLD; ++q) {
+      const int e = tid + CG_WG * q;
+      cg_st_lds(&L.a[buf][(e >> 4) * CG_SA + (e & 15)], ra[q]);
+      cg_st_lds(&L.b[buf][e], rb[q]);
+    }
+  };
+  load(0);
+  store(0);
   __syncthreads();
   for (int t = 0; t < T; ++t) {
     const bool more = (t + 1) < T;
-    if (more) {
-      const int tn = t + 1;
-      cg_load_tile<BT>(segs[tn / tiles_per_seg], lda, ldb, (tn % tiles_per_seg) * CG_KT, ra, rb);
-    }
+    if (more) load(t + 1);
     if (active) cg_compute_tile<BT>(L, t & 1, acc, wr0, wc0);
-    if (more) cg_store_tile<BT>(L, (t + 1) & 1, ra, rb);
+    if (more) store((t + 1) & 1);
     __syncthreads();
   }
 }

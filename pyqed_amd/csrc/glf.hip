@@ -80,6 +80,7 @@ template <int BT>
 __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
   __shared__ CgLds<BT> L;
   __shared__ c128 sred[CG_WG / 64];
+  __shared__ CgSeg segs[2 + MAX_NC];   // segment table in LDS (no scratch)
 
   const int b = blockIdx.x;
   const int Np = p.Np, nc = p.nc;
@@ -99,7 +100,6 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
   const double dt = p.dt, dt2 = p.dt / 2.0;
   int cur = 0;
   CgAcc<BT> A;
-  CgSeg segs[2 + MAX_NC];
 
   for (int step = 0; step < p.nsteps; ++step) {
     for (int stage = 0; stage < 4; ++stage) {
@@ -109,8 +109,11 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
       for (int c = 0; c < nc; ++c) {
         for (int bm = 0; bm < nb; ++bm)
           for (int bn = 0; bn < nb; ++bn) {
-            segs[0].A = p.Cop + (size_t)c * NN + (size_t)bm * BT * Np;
-            segs[0].B = r + bn * BT;
+            if (threadIdx.x == 0) {
+              segs[0].A = p.Cop + (size_t)c * NN + (size_t)bm * BT * Np;
+              segs[0].B = r + bn * BT;
+            }
+            __syncthreads();
             cg_block_gemm<BT>(segs, 1, Np, Np, Np, L, A);
             c128* Yc = Y + (size_t)c * NN;
             cg_epilogue<BT>(A, [&](int row, int col, c128 v) {
@@ -122,14 +125,17 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
       // ---- phase 2: k = (-iK) r + r (iK^+) + sum_c Y_c C_c^+ ; RK4 epilogue
       for (int bm = 0; bm < nb; ++bm)
         for (int bn = 0; bn < nb; ++bn) {
-          segs[0].A = p.mK + (size_t)bm * BT * Np;
-          segs[0].B = r + bn * BT;
-          segs[1].A = r + (size_t)bm * BT * Np;
-          segs[1].B = p.iKd + bn * BT;
-          for (int c = 0; c < nc; ++c) {
-            segs[2 + c].A = Y + (size_t)c * NN + (size_t)bm * BT * Np;
-            segs[2 + c].B = p.Cd + (size_t)c * NN + bn * BT;
+          if (threadIdx.x == 0) {
+            segs[0].A = p.mK + (size_t)bm * BT * Np;
+            segs[0].B = r + bn * BT;
+            segs[1].A = r + (size_t)bm * BT * Np;
+            segs[1].B = p.iKd + bn * BT;
+            for (int c = 0; c < nc; ++c) {
+              segs[2 + c].A = Y + (size_t)c * NN + (size_t)bm * BT * Np;
+              segs[2 + c].B = p.Cd + (size_t)c * NN + bn * BT;
+            }
           }
+          __syncthreads();
           cg_block_gemm<BT>(segs, 2 + nc, Np, Np, Np, L, A);
           cg_epilogue<BT>(A, [&](int row, int col, c128 k) {
             const size_t idx = (size_t)(bm * BT + row) * Np + bn * BT + col;
@@ -253,20 +259,26 @@ __global__ __launch_bounds__(CG_WG) void basis_transform_kernel(const c128* Vl, 
   c128* Tb = T + (size_t)blockIdx.x * NN;
   const int nb = Np / BT;
   CgAcc<BT> acc;
-  CgSeg seg;
+  __shared__ CgSeg seg[1];
   for (int bm = 0; bm < nb; ++bm)
     for (int bn = 0; bn < nb; ++bn) {  // T = Vl * A
-      seg.A = Vl + (size_t)bm * BT * Np;
-      seg.B = Ab + bn * BT;
-      cg_block_gemm<BT>(&seg, 1, Np, Np, Np, L, acc);
+      if (threadIdx.x == 0) {
+        seg[0].A = Vl + (size_t)bm * BT * Np;
+        seg[0].B = Ab + bn * BT;
+      }
+      __syncthreads();
+      cg_block_gemm<BT>(seg, 1, Np, Np, Np, L, acc);
       cg_epilogue<BT>(acc, [&](int r, int c, c128 v) { Tb[(size_t)(bm * BT + r) * Np + bn * BT + c] = v; });
     }
   __syncthreads();
   for (int bm = 0; bm < nb; ++bm)
     for (int bn = 0; bn < nb; ++bn) {  // A = T * Vr
-      seg.A = Tb + (size_t)bm * BT * Np;
-      seg.B = Vr + bn * BT;
-      cg_block_gemm<BT>(&seg, 1, Np, Np, Np, L, acc);
+      if (threadIdx.x == 0) {
+        seg[0].A = Tb + (size_t)bm * BT * Np;
+        seg[0].B = Vr + bn * BT;
+      }
+      __syncthreads();
+      cg_block_gemm<BT>(seg, 1, Np, Np, Np, L, acc);
       cg_epilogue<BT>(acc, [&](int r, int c, c128 v) { Ab[(size_t)(bm * BT + r) * Np + bn * BT + c] = v; });
     }
 }

@@ -163,12 +163,15 @@ __global__ __launch_bounds__(CG_WG) void ens_gemm_kernel(const c128* X, const c1
   const int bn = blockIdx.x, bm = blockIdx.y, s = blockIdx.z;
   const int t0 = (int)((long)tiles * s / S), t1 = (int)((long)tiles * (s + 1) / S);
   CgAcc<ENS_BT> A;
-  CgSeg seg;
-  seg.A = X + (size_t)bm * ENS_BT * Kp + (size_t)t0 * CG_KT;
-  seg.B = Z + (size_t)t0 * CG_KT * n1p + (size_t)bn * ENS_BT;
+  __shared__ CgSeg seg[1];
+  if (threadIdx.x == 0) {
+    seg[0].A = X + (size_t)bm * ENS_BT * Kp + (size_t)t0 * CG_KT;
+    seg[0].B = Z + (size_t)t0 * CG_KT * n1p + (size_t)bn * ENS_BT;
+  }
+  __syncthreads();
   c128* slab = slabs + (size_t)s * n3p * n1p;
   if (t1 > t0) {
-    cg_block_gemm<ENS_BT>(&seg, 1, (t1 - t0) * CG_KT, Kp, n1p, L, A);
+    cg_block_gemm<ENS_BT>(seg, 1, (t1 - t0) * CG_KT, Kp, n1p, L, A);
     cg_epilogue<ENS_BT>(A, [&](int row, int col, c128 v) {
       slab[(size_t)(bm * ENS_BT + row) * n1p + bn * ENS_BT + col] = v;
     });
