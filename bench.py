@@ -32,6 +32,15 @@ FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense FP64 matrix peak (spec; SURVEY.md 
 HBM_PEAK_GBS = 8000.0
 
 
+def measured_traffic(kernel: str, units: float):
+    """HBM bytes per launch from the committed PMC measurement (profiles/pmc_traffic.json), or None."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))[kernel]
+    except Exception:
+        return None
+    return (d["read_bytes_per_unit"] + d["write_bytes_per_unit"]) * units
+
+
 def lindblad_flops_per_step(N: int, nc: int) -> float:
     # 4 RK4 stages x (2 + 2*nc) complex N^3 GEMMs x 8 real flop per complex MAC
     return 4.0 * (2 + 2 * nc) * 8.0 * N ** 3
@@ -411,7 +420,9 @@ def main():
                 "peak": FP64_MFMA_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": round(achieved / FP64_MFMA_PEAK_TFLOPS, 4),
-                "traffic": None,
+                "traffic": measured_traffic("lindblad_rk4_kernel<128>", B * args.steps)
+                if (N, nc) == (128, 1) else None,
+                "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE+WRITE_SIZE, calibrated; profiles/pmc_traffic.json)",
                 "flop_per_dm_step": lindblad_flops_per_step(N, nc),
                 "launch_ms": round(kern_s * 1e3, 3),
             },
