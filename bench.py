@@ -41,9 +41,11 @@ def measured_traffic(kernel: str, units: float):
     return (d["read_bytes_per_unit"] + d["write_bytes_per_unit"]) * units
 
 
-def lindblad_flops_per_step(N: int, nc: int) -> float:
-    # 4 RK4 stages x (2 + 2*nc) complex N^3 GEMMs x 8 real flop per complex MAC
-    return 4.0 * (2 + 2 * nc) * 8.0 * N ** 3
+def lindblad_flops_per_step(N: int, nc: int, hermitian: bool = False) -> float:
+    # 4 RK4 stages x (complex N^3 GEMMs per RHS) x 8 real flop per complex MAC.
+    # general GLF kernel: (-iK)r, r(iK^+), C r, (C r)C^+      -> 2 + 2*nc GEMMs
+    # Hermitian kernel:   X = (-iK)r + 1/2 (C r)C^+, L = X + X^+ -> 1 + 2*nc GEMMs
+    return 4.0 * ((1 if hermitian else 2) + 2 * nc) * 8.0 * N ** 3
 
 
 def cpu_baseline(N, nc, dt, budget_s=10.0):
@@ -306,6 +308,8 @@ def main():
     ap.add_argument("--nc", type=int, default=1)
     ap.add_argument("--dt", type=float, default=1e-3)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--general", action="store_true",
+                    help="force the general (non-Hermitian) GLF kernel instead of the Hermitian one")
     ap.add_argument("--ens", type=int, default=4096, help="2DES disorder-ensemble members (total)")
     ap.add_argument("--ens-reps", type=int, default=20)
     ap.add_argument("--no-2des", action="store_true")
@@ -338,8 +342,11 @@ def main():
     Ct = torch.from_numpy(np.array(cs)).to(dev) if nc else None
     rho = torch.from_numpy(rho0).to(dev)
 
+    herm = not args.general and N <= 128  # pure states are exactly Hermitian
+    kname = f"lindblad_rk4_kernel<{min(128, N)},{'herm' if herm else 'general'}>"
+
     # warm-up
-    lindblad_rk4(Ht, Ct, rho, args.dt, args.warmup)
+    lindblad_rk4(Ht, Ct, rho, args.dt, args.warmup, hermitian=herm)
     torch.cuda.synchronize(dev)
 
     stream = torch.cuda.current_stream(dev)
@@ -349,7 +356,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     ev0.record(stream)
-    lindblad_rk4(Ht, Ct, rho, args.dt, args.steps)
+    lindblad_rk4(Ht, Ct, rho, args.dt, args.steps, hermitian=herm)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
@@ -368,11 +375,11 @@ def main():
 
     # single-trajectory latency (B=1), informational
     r1 = rho[:1].clone()
-    lindblad_rk4(Ht, Ct, r1, args.dt, 2)
+    lindblad_rk4(Ht, Ct, r1, args.dt, 2, hermitian=herm)
     torch.cuda.synchronize(dev)
     s1 = 20
     ta = time.perf_counter()
-    lindblad_rk4(Ht, Ct, r1, args.dt, s1)
+    lindblad_rk4(Ht, Ct, r1, args.dt, s1, hermitian=herm)
     torch.cuda.synchronize(dev)
     single_rate = s1 / (time.perf_counter() - ta)
 
@@ -393,7 +400,7 @@ def main():
     if rank == 0:
         total_dm_steps = B * args.steps * world
         value = total_dm_steps / wall_max
-        flops = lindblad_flops_per_step(N, nc) * B * args.steps
+        flops = lindblad_flops_per_step(N, nc, herm) * B * args.steps
         achieved = flops / kern_s / 1e12
         out = {
             "metric": "density-matrix steps/sec (N=128 Lindblad) + 2DES grid-points/sec at 1/2/4/8 GPU",
@@ -415,15 +422,16 @@ def main():
             },
             "roofline": {
                 "bound": "mfma",
-                "kernel": "lindblad_rk4_kernel<128>",
+                "kernel": kname,
                 "achieved": round(achieved, 3),
                 "peak": FP64_MFMA_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": round(achieved / FP64_MFMA_PEAK_TFLOPS, 4),
-                "traffic": measured_traffic("lindblad_rk4_kernel<128>", B * args.steps)
+                "traffic": measured_traffic(kname, B * args.steps)
                 if (N, nc) == (128, 1) else None,
                 "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE+WRITE_SIZE, calibrated; profiles/pmc_traffic.json)",
-                "flop_per_dm_step": lindblad_flops_per_step(N, nc),
+                "flop_per_dm_step": lindblad_flops_per_step(N, nc, herm),
+                "general_path_equiv_tflops": round(lindblad_flops_per_step(N, nc) * B * args.steps / kern_s / 1e12, 3),
                 "launch_ms": round(kern_s * 1e3, 3),
             },
             "single_trajectory_steps_per_s": round(single_rate, 2),

@@ -72,6 +72,18 @@ int qd_lindblad_rk4(const qd_c128* H, const qd_c128* C, int nc, qd_c128* rho,
                     void* stream);
 
 /*
+ * Same as qd_lindblad_rk4 for density matrices that are EXACTLY Hermitian
+ * (rho == rho^+ bit for bit; the caller checks).  Uses L[rho] = X + X^+ with
+ * X = -iK rho + 1/2 sum_c (C_c rho) C_c^+ : 1 + 2 nc complex GEMMs per RHS
+ * instead of 2 + 2 nc, and keeps every RK4 stage exactly Hermitian.  N <= 128
+ * (larger N falls back to the general path inside the library).
+ */
+int qd_lindblad_rk4_herm(const qd_c128* H, const qd_c128* C, int nc,
+                         qd_c128* rho, int B, int N, double dt, int nsteps,
+                         const qd_c128* E, int ne, qd_c128* obs, qd_c128* snap,
+                         int save_every, void* stream);
+
+/*
  * Driven Lindblad RK4 (pyqed/oqs.py:1699-1806 _lindblad_driven):
  *   H(t_k) = H0 - sum_d f_d(t_k) Hd_d, constant within step k, t_k = t0 + (k+1) dt
  * fvals is a HOST array [nsteps][nd] of the drive values (complex).  Other

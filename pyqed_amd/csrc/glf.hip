@@ -45,6 +45,7 @@ struct LindbladParams {
   c128* snap;       // [B][nsave][N][N]
   int N, Np, nc, ne, nsteps, save_every, nsave;
   int step0, total_steps;  // this launch runs global steps step0 .. step0+nsteps-1 of total_steps
+  int herm;                // Hermitian fast path (Lindblad, rho exactly Hermitian, single block)
   double dt;
 };
 
@@ -76,7 +77,7 @@ __device__ void wg_observables(const c128* rho, const c128* eT, int ne, size_t N
   }
 }
 
-template <int BT>
+template <int BT, bool HERM>
 __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
   __shared__ CgLds<BT> L;
   __shared__ c128 sred[CG_WG / 64];
@@ -86,13 +87,13 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
   const int Np = p.Np, nc = p.nc;
   const size_t NN = (size_t)Np * Np;
   c128* rho = p.rho + (size_t)b * NN;
-  c128* ws = p.ws + (size_t)b * (3 + nc) * NN;
-  c128* rs[2] = {ws, ws + NN};
+  c128* ws = p.ws + (size_t)b * (3 + nc + (HERM ? 1 : 0)) * NN;
   c128* acc = ws + 2 * NN;
   c128* Y = ws + 3 * NN;
+  c128* X = Y + (size_t)nc * NN;  // Hermitian path only
   c128* obs = p.obs ? p.obs + (size_t)b * (p.total_steps + 1) * p.ne : nullptr;
 
-  for (size_t i = threadIdx.x; i < NN; i += CG_WG) rs[0][i] = rho[i];
+  for (size_t i = threadIdx.x; i < NN; i += CG_WG) ws[i] = rho[i];
   if (p.ne > 0 && p.step0 == 0) wg_observables(rho, p.eT, p.ne, NN, obs, sred);
   __syncthreads();
 
@@ -103,8 +104,88 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
 
   for (int step = 0; step < p.nsteps; ++step) {
     for (int stage = 0; stage < 4; ++stage) {
-      const c128* r = rs[cur];
-      c128* rn = rs[cur ^ 1];
+      const c128* r = cur ? ws + NN : ws;
+      c128* rn = cur ? ws : ws + NN;
+      auto rk4_update = [&](size_t idx, c128 k) {
+        const c128 r0 = rho[idx];
+        if (stage == 0) {
+          acc[idx] = k;
+          rn[idx] = cadd(r0, cscale(k, dt2));
+        } else if (stage == 1) {
+          acc[idx] = cadd(acc[idx], cscale(k, 2.0));
+          rn[idx] = cadd(r0, cscale(k, dt2));
+        } else if (stage == 2) {
+          acc[idx] = cadd(acc[idx], cscale(k, 2.0));
+          rn[idx] = cadd(r0, cscale(k, dt));
+        } else {
+          const c128 a = cadd(acc[idx], k);
+          const c128 r1 = cadd(r0, cscale(cscale(a, 1.0 / 6.0), dt));
+          rho[idx] = r1;
+          rn[idx] = r1;
+        }
+      };
+      if constexpr (HERM) {
+        // Hermitian rho: L[rho] = X + X^+,  X = (-iK) rho + 1/2 sum_c (C_c rho) C_c^+   (single block, nb == 1)
+        // phase 1: X <- (-iK) r ; Y_c <- C_c r
+        if (threadIdx.x == 0) {
+          segs[0].A = p.mK;
+          segs[0].B = r;
+        }
+        __syncthreads();
+        cg_block_gemm<BT>(segs, 1, Np, Np, Np, L, A);
+        cg_epilogue<BT>(A, [&](int row, int col, c128 v) { X[(size_t)row * Np + col] = v; });
+        for (int c = 0; c < nc; ++c) {
+          if (threadIdx.x == 0) {
+            segs[0].A = p.Cop + (size_t)c * NN;
+            segs[0].B = r;
+          }
+          __syncthreads();
+          cg_block_gemm<BT>(segs, 1, Np, Np, Np, L, A);
+          c128* Yc = Y + (size_t)c * NN;
+          cg_epilogue<BT>(A, [&](int row, int col, c128 v) { Yc[(size_t)row * Np + col] = v; });
+        }
+        __syncthreads();
+        if (nc > 0) {  // phase 2: X += 1/2 sum_c Y_c C_c^+
+          if (threadIdx.x == 0)
+            for (int c = 0; c < nc; ++c) {
+              segs[c].A = Y + (size_t)c * NN;
+              segs[c].B = p.Cd + (size_t)c * NN;
+            }
+          __syncthreads();
+          cg_block_gemm<BT>(segs, nc, Np, Np, Np, L, A);
+          cg_epilogue<BT>(A, [&](int row, int col, c128 v) {
+            const size_t idx = (size_t)row * Np + col;
+            X[idx] = cadd(X[idx], cscale(v, 0.5));
+          });
+          __syncthreads();
+        }
+        // phase 3: k = X + X^+, exactly Hermitian; RK4 bookkeeping on every element.
+        // 32x32 tiles: the mirror tile X[tj][ti] is read row-wise (coalesced) into LDS
+        // (stride 33, the GEMM staging buffer is free here) and transposed there.
+        {
+          c128* T = L.a[0];
+          const int nt = Np / 32;
+          const int tr = threadIdx.x >> 5, tc = threadIdx.x & 31;  // 16 rows x 32 cols per pass
+          for (int t = 0; t < nt * nt; ++t) {
+            const int ti = t / nt, tj = t % nt;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int rr = tr + 16 * h;
+              T[rr * 33 + tc] = X[(size_t)(tj * 32 + rr) * Np + ti * 32 + tc];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int rr = tr + 16 * h;
+              const size_t e = (size_t)(ti * 32 + rr) * Np + tj * 32 + tc;
+              rk4_update(e, cadd(X[e], cconj(T[tc * 33 + rr])));
+            }
+            __syncthreads();
+          }
+        }
+        cur ^= 1;
+        continue;
+      } else {
       // ---- phase 1: Y_c = C_c r
       for (int c = 0; c < nc; ++c) {
         for (int bm = 0; bm < nb; ++bm)
@@ -138,27 +219,12 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
           __syncthreads();
           cg_block_gemm<BT>(segs, 2 + nc, Np, Np, Np, L, A);
           cg_epilogue<BT>(A, [&](int row, int col, c128 k) {
-            const size_t idx = (size_t)(bm * BT + row) * Np + bn * BT + col;
-            const c128 r0 = rho[idx];
-            if (stage == 0) {
-              acc[idx] = k;
-              rn[idx] = cadd(r0, cscale(k, dt2));
-            } else if (stage == 1) {
-              acc[idx] = cadd(acc[idx], cscale(k, 2.0));
-              rn[idx] = cadd(r0, cscale(k, dt2));
-            } else if (stage == 2) {
-              acc[idx] = cadd(acc[idx], cscale(k, 2.0));
-              rn[idx] = cadd(r0, cscale(k, dt));
-            } else {
-              const c128 a = cadd(acc[idx], k);
-              const c128 r1 = cadd(r0, cscale(cscale(a, 1.0 / 6.0), dt));
-              rho[idx] = r1;
-              rn[idx] = r1;
-            }
+            rk4_update((size_t)(bm * BT + row) * Np + bn * BT + col, k);
           });
         }
       __syncthreads();
       cur ^= 1;
+      }
     }
     const int gs = p.step0 + step + 1;  // global step count after this step
     if (p.ne > 0) wg_observables(rho, p.eT, p.ne, NN, obs + (size_t)gs * p.ne, sred);
@@ -346,7 +412,7 @@ __global__ void save_k0_kernel(const c128* mK, size_t NN, c128* K0) {
 int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c128* Q, const c128* Lop,
             const c128* Rop, int nc, c128* rho, int B, int N, double dt, int nsteps, const c128* E, int ne,
             c128* obs, c128* snap, int save_every, hipStream_t st, const c128* Hd = nullptr, int nd = 0,
-            const qd_c128* fvals = nullptr) {
+            const qd_c128* fvals = nullptr, int herm = 0) {
   const int Np = padded_dim(N);
   const size_t NN = (size_t)Np * Np;
   // operator workspace: Cop(L), mK(P), iKd(Q), Cd(R), eT, [K0, f scratch for driven runs]
@@ -363,12 +429,14 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   c128* fdev = K0 + (nd ? NN : 0);
   // state workspace: per-matrix scratch (+ padded rho when N != Np)
   const bool pad = (Np != N);
-  const size_t st_elems = (size_t)B * (3 + nc) * NN + (pad ? (size_t)B * NN : 0);
+  if (Np > 128) herm = 0;  // the Hermitian path is single-block
+  const size_t per = (size_t)(3 + nc + herm) * NN;
+  const size_t st_elems = (size_t)B * per + (pad ? (size_t)B * NN : 0);
   void* wst = nullptr;
   rc = workspace(WS_LINDBLAD, st_elems * sizeof(c128), &wst);
   if (rc) return rc;
   c128* scratch = (c128*)wst;
-  c128* rho_p = pad ? scratch + (size_t)B * (3 + nc) * NN : rho;
+  c128* rho_p = pad ? scratch + (size_t)B * per : rho;
 
   const int threads = 256;
   const int blocks = (int)std::min<size_t>((NN + threads - 1) / threads, 4096);
@@ -412,14 +480,19 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   p.dt = dt;
   p.step0 = 0;
   p.total_steps = nsteps;
+  p.herm = herm;
 
   auto launch = [&]() -> int {
-    if (Np == 32)
-      hipLaunchKernelGGL(lindblad_rk4_kernel<32>, dim3(B), dim3(CG_WG), 0, st, p);
-    else if (Np == 64)
-      hipLaunchKernelGGL(lindblad_rk4_kernel<64>, dim3(B), dim3(CG_WG), 0, st, p);
-    else
-      hipLaunchKernelGGL(lindblad_rk4_kernel<128>, dim3(B), dim3(CG_WG), 0, st, p);
+    if (Np == 32) {
+      if (herm) hipLaunchKernelGGL((lindblad_rk4_kernel<32, true>), dim3(B), dim3(CG_WG), 0, st, p);
+      else hipLaunchKernelGGL((lindblad_rk4_kernel<32, false>), dim3(B), dim3(CG_WG), 0, st, p);
+    } else if (Np == 64) {
+      if (herm) hipLaunchKernelGGL((lindblad_rk4_kernel<64, true>), dim3(B), dim3(CG_WG), 0, st, p);
+      else hipLaunchKernelGGL((lindblad_rk4_kernel<64, false>), dim3(B), dim3(CG_WG), 0, st, p);
+    } else {
+      if (herm) hipLaunchKernelGGL((lindblad_rk4_kernel<128, true>), dim3(B), dim3(CG_WG), 0, st, p);
+      else hipLaunchKernelGGL((lindblad_rk4_kernel<128, false>), dim3(B), dim3(CG_WG), 0, st, p);
+    }
     QD_HIP(hipGetLastError());
     return QD_OK;
   };
@@ -470,6 +543,18 @@ extern "C" int qd_lindblad_rk4(const qd_c128* H, const qd_c128* C, int nc, qd_c1
   return glf_run(GLF_FROM_LINDBLAD, (const c128*)H, (const c128*)C, nullptr, nullptr, nullptr, nullptr, nc,
                  (c128*)rho, B, N, dt, nsteps, (const c128*)E, ne, (c128*)obs, (c128*)snap, save_every,
                  (hipStream_t)stream);
+}
+
+extern "C" int qd_lindblad_rk4_herm(const qd_c128* H, const qd_c128* C, int nc, qd_c128* rho, int B, int N,
+                                    double dt, int nsteps, const qd_c128* E, int ne, qd_c128* obs, qd_c128* snap,
+                                    int save_every, void* stream) {
+  QD_CHECK_ARG(H && rho, "qd_lindblad_rk4_herm: H and rho must be non-null");
+  int rc = check_common("qd_lindblad_rk4_herm", rho, B, N, nc, ne, E, obs, nsteps);
+  if (rc) return rc;
+  QD_CHECK_ARG(nc == 0 || C, "qd_lindblad_rk4_herm: C is null but nc=%d", nc);
+  return glf_run(GLF_FROM_LINDBLAD, (const c128*)H, (const c128*)C, nullptr, nullptr, nullptr, nullptr, nc,
+                 (c128*)rho, B, N, dt, nsteps, (const c128*)E, ne, (c128*)obs, (c128*)snap, save_every,
+                 (hipStream_t)stream, nullptr, 0, nullptr, 1);
 }
 
 extern "C" int qd_glf_rk4(const qd_c128* P, const qd_c128* Q, const qd_c128* L, const qd_c128* R, int npairs,

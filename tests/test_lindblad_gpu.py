@@ -165,3 +165,50 @@ def test_lindblad_driven_matches_reference():
     assert relerr(r.observables, g["observables"]) < TOL
     assert relerr(np.array([x.toarray() for x in r.rholist]), g["rholist"]) < TOL
     assert np.array_equal(H0.toarray(), g["H0"])
+
+
+@pytest.mark.parametrize("N,nc,B", [(16, 1, 3), (40, 2, 2), (128, 1, 4), (128, 0, 2)])
+def test_lindblad_hermitian_kernel_matches_general(N, nc, B):
+    """qd_lindblad_rk4_herm (L = X + X^+) vs the general GLF kernel and the oracle; the
+    Hermitian kernel keeps rho exactly Hermitian at every step."""
+    import torch
+    from oracle import lindblad as olb
+    from pyqed_amd import lindblad_rk4
+    H, cs = olb.synthetic_lindblad(N, nc=max(nc, 1))
+    cs = cs[:nc]
+    rho0 = olb.random_pure_states(B, N)
+    steps, dt = 8, 1e-2
+    ref = olb.lindblad_batch(H, cs, rho0, dt, steps)
+    dev = torch.device("cuda", 0)
+    Ht = torch.from_numpy(H).to(dev)
+    Ct = torch.from_numpy(np.array(cs)).to(dev) if nc else None
+    E = torch.eye(N, dtype=torch.complex128, device=dev).unsqueeze(0)
+    out = {}
+    for herm in (True, False):
+        rho = torch.from_numpy(rho0.copy()).to(dev)
+        obs, snap = lindblad_rk4(Ht, Ct, rho, dt, steps, e_ops=E, save_every=4, hermitian=herm)
+        torch.cuda.synchronize()
+        out[herm] = (rho.cpu().numpy(), obs.cpu().numpy(), snap.cpu().numpy())
+    r = out[True][0]
+    assert relerr(r, ref) < TOL
+    assert np.array_equal(r, np.conj(np.swapaxes(r, 1, 2)))
+    for a, b in zip(out[True], out[False]):
+        assert relerr(a, b) < TOL
+
+
+def test_lindblad_auto_dispatch_non_hermitian_state():
+    """A non-Hermitian initial operator (e.g. A rho, as in the correlation functions) must take
+    the general kernel under hermitian=None."""
+    import torch
+    from oracle import lindblad as olb
+    from pyqed_amd import lindblad_rk4
+    N, B = 24, 2
+    H, cs = olb.synthetic_lindblad(N)
+    rng = np.random.default_rng(7)
+    rho0 = rng.standard_normal((B, N, N)) + 1j * rng.standard_normal((B, N, N))
+    ref = olb.lindblad_batch(H, cs, rho0, 1e-2, 5)
+    dev = torch.device("cuda", 0)
+    rho = torch.from_numpy(rho0.copy()).to(dev)
+    lindblad_rk4(torch.from_numpy(H).to(dev), torch.from_numpy(np.array(cs)).to(dev), rho, 1e-2, 5)
+    torch.cuda.synchronize()
+    assert relerr(rho.cpu().numpy(), ref) < TOL
