@@ -122,6 +122,114 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_kernel(DeomParams p) {
   }
 }
 
+// Group kernel: G = next pow2 >= ns^2 lanes per ADO, one lane per matrix element, so every
+// neighbour ADO is read once per group as one coalesced ns^2 x 16-B row (not once per row/column
+// it touches).  All 2K neighbour indices, coefficients and neighbour elements are loaded up front
+// (one dependent-load round trip instead of one per k), and the ns x ns products exchange
+// elements inside the group with lane shuffles.  Every lane of a group follows the same branches
+// (they share the ADO), so the shuffles never read an inactive lane.
+template <int G, int KMAX>
+__global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) {
+  __shared__ c128 sH[DEOM_MAX_NS * DEOM_MAX_NS];
+  __shared__ c128 sQ[DEOM_MAX_NMOD * DEOM_MAX_NS * DEOM_MAX_NS];
+  const int ns = p.ns, ns2 = ns * ns, K = p.K;
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  const size_t ngrp = (size_t)p.B * p.nmax;
+  const size_t grp = t / G;                 // b * nmax + n
+  const int e = (int)(t % G);
+  const bool live = grp < ngrp;             // uniform within a group
+  const bool valid = live && e < ns2;
+  const int n = live ? (int)(grp % p.nmax) : 0;
+  const int ee = e < ns2 ? e : 0;           // padding lanes shadow element 0
+  const c128* X = p.xin + (live ? (grp - n) * ns2 : 0);
+
+  // round trip 1: indices, coefficients, own element, H/Q into LDS
+  int im[KMAX], ip[KMAX];
+  c128 cf[KMAX][3];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    im[k] = -1;
+    ip[k] = -1;
+    cf[k][0] = cf[k][1] = cf[k][2] = cmk(0, 0);
+    if (live && k < K) {
+      im[k] = p.minus[(size_t)n * K + k];
+      ip[k] = p.plus[(size_t)n * K + k];
+      const c128* c = p.coef + ((size_t)n * K + k) * 3;
+      cf[k][0] = c[0];
+      cf[k][1] = c[1];
+      cf[k][2] = c[2];
+    }
+  }
+  const c128 own = live ? X[(size_t)n * ns2 + ee] : cmk(0, 0);
+  const c128 dmp = live ? p.damp[n] : cmk(0, 0);
+  for (int q = threadIdx.x; q < ns2; q += blockDim.x)
+    sH[q] = p.Hdip ? cadd(p.H[q], cmul(p.Hdip[q], p.fs)) : p.H[q];
+  for (int q = threadIdx.x; q < p.nmod * ns2; q += blockDim.x)
+    sQ[q] = p.Qdip ? cadd(p.Q[q], cmul(p.Qdip[q], p.fc)) : p.Q[q];
+  __syncthreads();
+
+  // round trip 2: every neighbour element this lane owns
+  c128 ym[KMAX], yp[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    ym[k] = im[k] >= 0 ? X[(size_t)im[k] * ns2 + ee] : cmk(0, 0);
+    yp[k] = ip[k] >= 0 ? X[(size_t)ip[k] * ns2 + ee] : cmk(0, 0);
+  }
+
+  const int i = ee / ns, j = ee % ns;
+  const int base = (int)(threadIdx.x & 63) & ~(G - 1);
+  auto shfl = [&](c128 v, int src) { return cmk(__shfl(v.re, base + src, 64), __shfl(v.im, base + src, 64)); };
+
+  // damping + coherent part: damp_n x - i (H x - x H)
+  c128 d = cmul(dmp, own);
+  c128 comm = cmk(0, 0);
+  for (int l = 0; l < ns; ++l)
+    comm = cadd(comm, csub(cmul(sH[i * ns + l], shfl(own, l * ns + j)), cmul(shfl(own, i * ns + l), sH[l * ns + j])));
+  d = cadd(d, cmulmi(comm));
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    if (k >= K) break;
+    const c128* Qm = sQ + p.mode[k] * ns2;
+    if (im[k] >= 0) {
+      c128 qy = cmk(0, 0), yq = cmk(0, 0);
+      for (int l = 0; l < ns; ++l) {
+        qy = cadd(qy, cmul(Qm[i * ns + l], shfl(ym[k], l * ns + j)));
+        yq = cadd(yq, cmul(shfl(ym[k], i * ns + l), Qm[l * ns + j]));
+      }
+      d = cadd(d, cadd(cmul(cf[k][0], qy), cmul(cf[k][1], yq)));
+    }
+    if (ip[k] >= 0) {
+      c128 c = cmk(0, 0);
+      for (int l = 0; l < ns; ++l)
+        c = cadd(c, csub(cmul(Qm[i * ns + l], shfl(yp[k], l * ns + j)), cmul(shfl(yp[k], i * ns + l), Qm[l * ns + j])));
+      d = cadd(d, cmul(cf[k][2], c));
+    }
+  }
+  if (!valid) return;
+
+  const size_t idx = grp * ns2 + e;
+  const double dt = p.dt;
+  const c128 r0 = p.rho[idx];
+  if (p.stage == 0) {
+    p.acc[idx] = d;
+    p.xout[idx] = cadd(r0, cscale(d, dt / 2));
+  } else if (p.stage == 1) {
+    p.acc[idx] = cadd(p.acc[idx], cscale(d, 2.0));
+    p.xout[idx] = cadd(r0, cscale(d, dt / 2));
+  } else if (p.stage == 2) {
+    p.acc[idx] = cadd(p.acc[idx], cscale(d, 2.0));
+    p.xout[idx] = cadd(r0, cscale(d, dt));
+  } else {
+    const c128 a = cadd(p.acc[idx], d);
+    const c128 r1 = cadd(r0, cscale(cscale(a, dt), 1.0 / 6.0));
+    p.rho_out[idx] = r1;
+    if (p.snap && n == 0) {
+      const size_t b = grp / p.nmax;
+      p.snap[(b * (p.nsteps + 1) + p.step + 1) * ns2 + e] = r1;
+    }
+  }
+}
+
 __global__ void deom_snap0_kernel(const c128* rho, c128* snap, int B, int nmax, int ns, int nsteps) {
   const int ns2 = ns * ns;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < B * ns2; e += gridDim.x * blockDim.x) {
@@ -250,7 +358,25 @@ extern "C" int qd_deom_rk4(qd_c128* ados, int B, int nmax, int K, int ns, const 
   p.nmod = nmod;
   p.nsteps = nsteps;
   p.dt = dt;
-  const int grid = (int)((tot + DEOM_TPB - 1) / DEOM_TPB);
+  // group kernel when ns^2 <= 64 lanes and K <= 8; else the element kernel
+  int G = 1;
+  while (G < (int)ns2) G *= 2;
+  const bool grp = G <= 64 && K <= 8;
+  const size_t nthreads = grp ? (size_t)B * nmax * G : tot;
+  const int grid = (int)((nthreads + DEOM_TPB - 1) / DEOM_TPB);
+  auto launch_stage = [&]() {
+    if (!grp) {
+      hipLaunchKernelGGL(deom_stage_kernel, dim3(grid), dim3(DEOM_TPB), 0, st, p);
+      return;
+    }
+    switch (G) {
+      case 1: hipLaunchKernelGGL((deom_stage_grp_kernel<1, 8>), dim3(grid), dim3(DEOM_TPB), 0, st, p); break;
+      case 4: hipLaunchKernelGGL((deom_stage_grp_kernel<4, 8>), dim3(grid), dim3(DEOM_TPB), 0, st, p); break;
+      case 16: hipLaunchKernelGGL((deom_stage_grp_kernel<16, 8>), dim3(grid), dim3(DEOM_TPB), 0, st, p); break;
+      case 32: hipLaunchKernelGGL((deom_stage_grp_kernel<32, 8>), dim3(grid), dim3(DEOM_TPB), 0, st, p); break;
+      default: hipLaunchKernelGGL((deom_stage_grp_kernel<64, 8>), dim3(grid), dim3(DEOM_TPB), 0, st, p); break;
+    }
+  };
   static const int stage_time[4] = {0, 1, 1, 2};
   for (int s = 0; s < nsteps; ++s) {
     p.step = s;
@@ -261,7 +387,7 @@ extern "C" int qd_deom_rk4(qd_c128* ados, int B, int nmax, int K, int ns, const 
       const int ti = s * 3 + stage_time[stage];
       p.fs = fs_h ? cmk(fs_h[ti].re, fs_h[ti].im) : cmk(0, 0);
       p.fc = fc_h ? cmk(fc_h[ti].re, fc_h[ti].im) : cmk(0, 0);
-      hipLaunchKernelGGL(deom_stage_kernel, dim3(grid), dim3(DEOM_TPB), 0, st, p);
+      launch_stage();
       QD_HIP(hipGetLastError());
     }
   }

@@ -27,6 +27,10 @@
 // stays exactly zero through the propagation.
 #include "cgemm_block.hpp"
 
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
 namespace qd {
 namespace {
 
@@ -47,7 +51,35 @@ struct LindbladParams {
   int step0, total_steps;  // this launch runs global steps step0 .. step0+nsteps-1 of total_steps
   int herm;                // Hermitian fast path (Lindblad, rho exactly Hermitian, single block)
   double dt;
+  unsigned long long* tbuf;  // [B][8] per-phase wall-clock ticks (QD_PHASE_TIMING diagnostics) or null
 };
+
+// Per-matrix scratch slots of Np x Np: stage buffer(s), RK4 accumulator, Y_c.
+__host__ __device__ inline int glf_slots(int Np, int nc, int herm) {
+  (void)herm;
+  return (Np <= 128 ? 1 : 2) + 1 + nc;
+}
+
+#ifdef QD_PHASE_TIMING
+// Diagnostics only (p.tbuf != null): barrier, then thread 0 charges the ticks since the last mark to `slot`.
+#define QD_TMARK(slot)                                   \
+  if (p.tbuf) {                                          \
+    __syncthreads();                                     \
+    if (threadIdx.x == 0) {                              \
+      const unsigned long long now_ = wall_clock64();    \
+      tacc[slot] += now_ - tlast;                        \
+      tlast = now_;                                      \
+    }                                                    \
+  }
+#define QD_TIMING_DECL unsigned long long tacc[5] = {0, 0, 0, 0, 0}, tlast = p.tbuf ? wall_clock64() : 0;
+#define QD_TIMING_FLUSH \
+  if (p.tbuf && threadIdx.x == 0)                                  \
+    for (int q = 0; q < 5; ++q) p.tbuf[(size_t)b * 8 + q] += tacc[q];
+#else
+#define QD_TMARK(slot)
+#define QD_TIMING_DECL
+#define QD_TIMING_FLUSH
+#endif
 
 // Tr(E_m rho) = sum_ij rho_ij E_m[j][i] = sum_ij rho_ij eT_m[i][j]; fixed
 // reduction order (per-thread strided partials, wave butterfly, 8-wave sum).
@@ -87,10 +119,13 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
   const int Np = p.Np, nc = p.nc;
   const size_t NN = (size_t)Np * Np;
   c128* rho = p.rho + (size_t)b * NN;
-  c128* ws = p.ws + (size_t)b * (3 + nc + (HERM ? 1 : 0)) * NN;
-  c128* acc = ws + 2 * NN;
-  c128* Y = ws + 3 * NN;
-  c128* X = Y + (size_t)nc * NN;  // Hermitian path only
+  // single block (Np <= 128): every stage input is fully consumed by the GEMMs before the epilogue
+  // overwrites it, so one stage buffer is updated in place; else two alternate.
+  const bool single = (Np / BT) == 1;
+  c128* ws = p.ws + (size_t)b * glf_slots(Np, nc, HERM) * NN;
+  c128* rbuf1 = single ? ws : ws + NN;
+  c128* acc = single ? ws + NN : ws + 2 * NN;
+  c128* Y = acc + NN;
   c128* obs = p.obs ? p.obs + (size_t)b * (p.total_steps + 1) * p.ne : nullptr;
 
   for (size_t i = threadIdx.x; i < NN; i += CG_WG) ws[i] = rho[i];
@@ -101,11 +136,12 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
   const double dt = p.dt, dt2 = p.dt / 2.0;
   int cur = 0;
   CgAcc<BT> A;
+  QD_TIMING_DECL
 
   for (int step = 0; step < p.nsteps; ++step) {
     for (int stage = 0; stage < 4; ++stage) {
-      const c128* r = cur ? ws + NN : ws;
-      c128* rn = cur ? ws : ws + NN;
+      const c128* r = cur ? rbuf1 : ws;
+      c128* rn = cur ? ws : rbuf1;
       auto rk4_update = [&](size_t idx, c128 k) {
         const c128 r0 = rho[idx];
         if (stage == 0) {
@@ -125,15 +161,8 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
         }
       };
       if constexpr (HERM) {
-        // Hermitian rho: L[rho] = X + X^+,  X = (-iK) rho + 1/2 sum_c (C_c rho) C_c^+   (single block, nb == 1)
-        // phase 1: X <- (-iK) r ; Y_c <- C_c r
-        if (threadIdx.x == 0) {
-          segs[0].A = p.mK;
-          segs[0].B = r;
-        }
-        __syncthreads();
-        cg_block_gemm<BT>(segs, 1, Np, Np, Np, L, A);
-        cg_epilogue<BT>(A, [&](int row, int col, c128 v) { X[(size_t)row * Np + col] = v; });
+        // Hermitian rho: L[rho] = X + X^+ with X = (-iK) r + sum_c (C_c r)(C_c^+ / 2)   (single block, nb == 1;
+        // p.Cd holds C_c^+ / 2 on this path).  phase 1: Y_c = C_c r
         for (int c = 0; c < nc; ++c) {
           if (threadIdx.x == 0) {
             segs[0].A = p.Cop + (size_t)c * NN;
@@ -141,48 +170,47 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
           }
           __syncthreads();
           cg_block_gemm<BT>(segs, 1, Np, Np, Np, L, A);
+          QD_TMARK(0);
           c128* Yc = Y + (size_t)c * NN;
           cg_epilogue<BT>(A, [&](int row, int col, c128 v) { Yc[(size_t)row * Np + col] = v; });
+          QD_TMARK(1);
         }
         __syncthreads();
-        if (nc > 0) {  // phase 2: X += 1/2 sum_c Y_c C_c^+
-          if (threadIdx.x == 0)
-            for (int c = 0; c < nc; ++c) {
-              segs[c].A = Y + (size_t)c * NN;
-              segs[c].B = p.Cd + (size_t)c * NN;
-            }
-          __syncthreads();
-          cg_block_gemm<BT>(segs, nc, Np, Np, Np, L, A);
-          cg_epilogue<BT>(A, [&](int row, int col, c128 v) {
-            const size_t idx = (size_t)row * Np + col;
-            X[idx] = cadd(X[idx], cscale(v, 0.5));
-          });
-          __syncthreads();
+        // phase 2: X in registers (one accumulator over 1 + nc segments); k_ij = X_ij + conj(X_ji) is
+        // formed from the accumulator and an LDS transpose: exactly Hermitian, fused RK4 epilogue
+        if (threadIdx.x == 0) {
+          segs[0].A = p.mK;
+          segs[0].B = r;
+          for (int c = 0; c < nc; ++c) {
+            segs[1 + c].A = Y + (size_t)c * NN;
+            segs[1 + c].B = p.Cd + (size_t)c * NN;
+          }
         }
-        // phase 3: k = X + X^+, exactly Hermitian; RK4 bookkeeping on every element.
-        // 32x32 tiles: the mirror tile X[tj][ti] is read row-wise (coalesced) into LDS
-        // (stride 33, the GEMM staging buffer is free here) and transposed there.
+        __syncthreads();
+        cg_block_gemm<BT>(segs, 1 + nc, Np, Np, Np, L, A);
+        QD_TMARK(2);
+        // k = X + X^+ through LDS in two column halves (the staging buffers are free now): pass h publishes
+        // X[:, h*BT/2 .. +BT/2) transposed (T[c][row], stride BT+1), then finalises rows h*BT/2 .. +BT/2,
+        // each element from its own accumulator value plus conj(T[row][col]).  Wave-uniform predicates.
         {
-          c128* T = L.a[0];
-          const int nt = Np / 32;
-          const int tr = threadIdx.x >> 5, tc = threadIdx.x & 31;  // 16 rows x 32 cols per pass
-          for (int t = 0; t < nt * nt; ++t) {
-            const int ti = t / nt, tj = t % nt;
+          constexpr int HB = BT / 2;
+          static_assert(sizeof(CgLds<BT>) >= (size_t)HB * (BT + 1) * sizeof(c128), "LDS transpose buffer");
+          c128* T = reinterpret_cast<c128*>(&L);
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              const int rr = tr + 16 * h;
-              T[rr * 33 + tc] = X[(size_t)(tj * 32 + rr) * Np + ti * 32 + tc];
-            }
+          for (int h = 0; h < 2; ++h) {
+            cg_epilogue<BT>(A, [&](int row, int col, c128 v) {
+              const int c = col - h * HB;
+              if (c >= 0 && c < HB) T[c * (BT + 1) + row] = v;
+            });
             __syncthreads();
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              const int rr = tr + 16 * h;
-              const size_t e = (size_t)(ti * 32 + rr) * Np + tj * 32 + tc;
-              rk4_update(e, cadd(X[e], cconj(T[tc * 33 + rr])));
-            }
+            cg_epilogue<BT>(A, [&](int row, int col, c128 v) {
+              const int rr = row - h * HB;
+              if (rr >= 0 && rr < HB) rk4_update((size_t)row * Np + col, cadd(v, cconj(T[rr * (BT + 1) + col])));
+            });
             __syncthreads();
           }
         }
+        QD_TMARK(3);
         cur ^= 1;
         continue;
       } else {
@@ -196,10 +224,12 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
             }
             __syncthreads();
             cg_block_gemm<BT>(segs, 1, Np, Np, Np, L, A);
+            QD_TMARK(0);
             c128* Yc = Y + (size_t)c * NN;
             cg_epilogue<BT>(A, [&](int row, int col, c128 v) {
               Yc[(size_t)(bm * BT + row) * Np + bn * BT + col] = v;
             });
+            QD_TMARK(1);
           }
       }
       __syncthreads();
@@ -218,9 +248,11 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
           }
           __syncthreads();
           cg_block_gemm<BT>(segs, 2 + nc, Np, Np, Np, L, A);
+          QD_TMARK(2);
           cg_epilogue<BT>(A, [&](int row, int col, c128 k) {
             rk4_update((size_t)(bm * BT + row) * Np + bn * BT + col, k);
           });
+          QD_TMARK(3);
         }
       __syncthreads();
       cur ^= 1;
@@ -240,7 +272,9 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
       }
     }
     __syncthreads();
+    QD_TMARK(4);
   }
+  QD_TIMING_FLUSH
 }
 
 // ---------------------------------------------------------------- operator prep
@@ -409,6 +443,11 @@ __global__ void save_k0_kernel(const c128* mK, size_t NN, c128* K0) {
     K0[e] = cmuli(mK[e]);  // K = i * (-iK)
 }
 
+__global__ void scale_kernel(c128* a, size_t n, double s) {
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x)
+    a[e] = cscale(a[e], s);
+}
+
 int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c128* Q, const c128* Lop,
             const c128* Rop, int nc, c128* rho, int B, int N, double dt, int nsteps, const c128* E, int ne,
             c128* obs, c128* snap, int save_every, hipStream_t st, const c128* Hd = nullptr, int nd = 0,
@@ -430,7 +469,7 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   // state workspace: per-matrix scratch (+ padded rho when N != Np)
   const bool pad = (Np != N);
   if (Np > 128) herm = 0;  // the Hermitian path is single-block
-  const size_t per = (size_t)(3 + nc + herm) * NN;
+  const size_t per = (size_t)glf_slots(Np, nc, herm) * NN;
   const size_t st_elems = (size_t)B * per + (pad ? (size_t)B * NN : 0);
   void* wst = nullptr;
   rc = workspace(WS_LINDBLAD, st_elems * sizeof(c128), &wst);
@@ -447,6 +486,10 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
     hipLaunchKernelGGL(glf_prep_kernel, dim3(blocks), dim3(threads), 0, st, P, Q, Lop, Rop, nc, E, ne, N, Np, Cop,
                        mK, iKd, Cd, eT);
   QD_HIP(hipGetLastError());
+  if (herm && nc > 0) {  // the Hermitian kernel consumes C_c^+ / 2
+    hipLaunchKernelGGL(scale_kernel, dim3(blocks), dim3(threads), 0, st, Cd, (size_t)nc * NN, 0.5);
+    QD_HIP(hipGetLastError());
+  }
   if (nd) {
     hipLaunchKernelGGL(save_k0_kernel, dim3(blocks), dim3(threads), 0, st, (const c128*)mK, NN, K0);
     QD_HIP(hipGetLastError());
@@ -481,6 +524,16 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   p.step0 = 0;
   p.total_steps = nsteps;
   p.herm = herm;
+  p.tbuf = nullptr;
+#ifdef QD_PHASE_TIMING
+  const bool timing = true;  // diagnostics build: per-phase clocks to stderr
+#else
+  const bool timing = false;
+#endif
+  if (timing) {
+    QD_HIP(hipMalloc(&p.tbuf, (size_t)B * 8 * sizeof(unsigned long long)));
+    QD_HIP(hipMemsetAsync(p.tbuf, 0, (size_t)B * 8 * sizeof(unsigned long long), st));
+  }
 
   auto launch = [&]() -> int {
     if (Np == 32) {
@@ -515,6 +568,24 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
     const int pb = (int)std::min<size_t>((tot + threads - 1) / threads, 65535);
     hipLaunchKernelGGL(unpad_kernel, dim3(pb), dim3(threads), 0, st, rho_p, rho, B, N, Np);
     QD_HIP(hipGetLastError());
+  }
+  if (timing) {
+    std::vector<unsigned long long> t((size_t)B * 8);
+    QD_HIP(hipStreamSynchronize(st));
+    QD_HIP(hipMemcpy(t.data(), p.tbuf, t.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    (void)hipFree(p.tbuf);
+    int dev = 0, khz = 100000;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+    const char* names[5] = {"gemm1", "epi1", "gemm2", "epi2", "obs/snap"};
+    std::fprintf(stderr, "[qd phase timing] N=%d B=%d herm=%d nsteps=%d, us per step (mean over workgroups):", N, B,
+                 herm, nsteps);
+    for (int q = 0; q < 5; ++q) {
+      double s = 0;
+      for (int b = 0; b < B; ++b) s += (double)t[(size_t)b * 8 + q];
+      std::fprintf(stderr, " %s %.2f", names[q], s / B / (khz * 1e-3) / std::max(1, nsteps));
+    }
+    std::fprintf(stderr, "\n");
   }
   return QD_OK;
 }

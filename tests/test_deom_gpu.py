@@ -78,3 +78,26 @@ def test_deom_bench_size_properties():
     assert sol.nmax == 6188
     assert np.max(np.abs(np.trace(saved, axis1=1, axis2=2) - 1)) < 1e-12
     assert np.max(np.abs(saved - np.conj(np.swapaxes(saved, 1, 2)))) < 1e-12
+
+
+@pytest.mark.parametrize("ns,npsd,L", [(3, 3, 4), (5, 1, 3), (2, 8, 2)])
+def test_deom_layouts_vs_oracle(ns, npsd, L):
+    """ns = 3 / 5 exercise the lane-group kernel with padding lanes (groups of 16 / 32 lanes);
+    npsd = 8 (K = 9 > 8) exercises the element-per-thread kernel."""
+    from oracle import deom as od
+    from pyqed_amd.deom import Bath, DEOMSolver
+    w = sp.symbols(r"\omega", real=True)
+    bath = Bath([2 * 0.4 * 1.0 * w / (1.0 + w ** 2)], w, [1.0], [npsd], [0] * (1 + npsd))
+    rng = np.random.default_rng(ns)
+    A = rng.standard_normal((ns, ns)) + 1j * rng.standard_normal((ns, ns))
+    H = (A + A.conj().T) / 4
+    Q = np.diag(np.arange(ns, dtype=float)).astype(complex) + 0.2 * (np.eye(ns, k=1) + np.eye(ns, k=-1))
+    psi = rng.standard_normal(ns) + 1j * rng.standard_normal(ns)
+    psi /= np.linalg.norm(psi)
+    rho0 = np.outer(psi, psi.conj())
+    sol = DEOMSolver(H, None, bath, np.array([Q]), None, None, None, L)
+    dt, nt = 0.005, 12
+    t, saved = sol.run_batch(rho0[None], dt, nt)
+    tt, ref, _ = od.run(H, np.zeros((ns, ns)), lambda t: 0, np.array([Q]), np.zeros((1, ns, ns)), lambda t: 0,
+                        (bath.etal, bath.etar, bath.etaa, bath.expn), L, rho0, dt, nt)
+    assert relerr(saved[0], ref) < TOL
