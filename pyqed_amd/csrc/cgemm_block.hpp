@@ -115,7 +115,8 @@ __device__ __forceinline__ void cg_block_gemm(const CgSeg* segs, int nseg, int K
   constexpr int NLD = cg_nld<BT>();
   const int tiles_per_seg = K / CG_KT;
   const int T = nseg * tiles_per_seg;
-  const int tid = threadIdx.x;
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));  // staging address math stays per call (see cg_epilogue)
   // per-thread element offsets inside a tile (A: BT rows x 16, B: 16 rows x BT)
   cg_v2 ra[NLD], rb[NLD];
   auto load = [&](int t) {
@@ -152,9 +153,13 @@ __device__ __forceinline__ void cg_block_gemm(const CgSeg* segs, int nseg, int K
 template <int BT, typename F>
 __device__ __forceinline__ void cg_epilogue(const CgAcc<BT>& acc, F&& f) {
   constexpr int MW = CgCfg<BT>::MW, NW = CgCfg<BT>::NW, WC = CgCfg<BT>::WC, WR = CgCfg<BT>::WR;
-  const int wave = threadIdx.x >> 6;
+  // The thread index goes through an empty asm so the compiler cannot hoist the per-element
+  // address math of an epilogue out of a persistent kernel's step loop (it would spill it).
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const int wave = tid >> 6;
   if (wave >= WR * WC) return;
-  const int lane = threadIdx.x & 63;
+  const int lane = tid & 63;
   const int wr0 = (wave / WC) * (MW * 16);
   const int wc0 = (wave % WC) * (NW * 16);
 #pragma unroll

@@ -71,10 +71,15 @@ __host__ __device__ inline int glf_slots(int Np, int nc, int herm) {
       tlast = now_;                                      \
     }                                                    \
   }
-#define QD_TIMING_DECL unsigned long long tacc[5] = {0, 0, 0, 0, 0}, tlast = p.tbuf ? wall_clock64() : 0;
-#define QD_TIMING_FLUSH \
-  if (p.tbuf && threadIdx.x == 0)                                  \
-    for (int q = 0; q < 5; ++q) p.tbuf[(size_t)b * 8 + q] += tacc[q];
+#define QD_TIMING_DECL                                                                \
+  unsigned long long tacc[5] = {0, 0, 0, 0, 0}, tlast = p.tbuf ? wall_clock64() : 0; \
+  const unsigned long long t0w_ = tlast, t0c_ = clock64();
+#define QD_TIMING_FLUSH                                                     \
+  if (p.tbuf && threadIdx.x == 0) {                                         \
+    for (int q = 0; q < 5; ++q) p.tbuf[(size_t)b * 8 + q] += tacc[q];      \
+    p.tbuf[(size_t)b * 8 + 5] += clock64() - t0c_;                          \
+    p.tbuf[(size_t)b * 8 + 6] += wall_clock64() - t0w_;                     \
+  }
 #else
 #define QD_TMARK(slot)
 #define QD_TIMING_DECL
@@ -189,26 +194,70 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
         __syncthreads();
         cg_block_gemm<BT>(segs, 1 + nc, Np, Np, Np, L, A);
         QD_TMARK(2);
-        // k = X + X^+ through LDS in two column halves (the staging buffers are free now): pass h publishes
-        // X[:, h*BT/2 .. +BT/2) transposed (T[c][row], stride BT+1), then finalises rows h*BT/2 .. +BT/2,
-        // each element from its own accumulator value plus conj(T[row][col]).  Wave-uniform predicates.
+        // k = X + X^+ through LDS, two rounds of two TS x TS tiles (TS = BT/2; the GEMM staging buffers
+        // are free).  The accumulator fragments of the off-diagonal pair X(0,1), X(1,0) go to LDS and those
+        // of the diagonal tiles to Y_0's slot (Y is dead once the GEMM has returned), so no accumulator stays
+        // live past one epilogue.  Round 0 finalises the off-diagonal pair from LDS; round 1 reloads the
+        // diagonal tiles (coalesced rows) into LDS and finalises them.  Each element reads its own value
+        // and its mirror from LDS; the loads of a chunk of elements are issued together.
         {
-          constexpr int HB = BT / 2;
-          static_assert(sizeof(CgLds<BT>) >= (size_t)HB * (BT + 1) * sizeof(c128), "LDS transpose buffer");
-          c128* T = reinterpret_cast<c128*>(&L);
+          constexpr int TS = BT / 2, LD = TS + 1;
+          static_assert(2 * TS * LD * sizeof(c128) <= sizeof(CgLds<BT>), "LDS transpose buffer");
+          constexpr int PER = BT * BT / 2 / CG_WG;  // elements per thread per round
+          constexpr int CH = PER < 4 ? PER : 4;
+          c128* T0 = reinterpret_cast<c128*>(&L);
+          c128* T1 = T0 + TS * LD;
+          c128* Xd = Y;
+          int tid = threadIdx.x;
+          asm volatile("" : "+v"(tid));  // keep the per-element index math inside the stage loop (no LICM + spill)
+          cg_epilogue<BT>(A, [&](int row, int col, c128 v) {
+            const int ti = row / TS, tj = col / TS;
+            if (ti != tj) (ti == 0 ? T0 : T1)[(row - ti * TS) * LD + (col - tj * TS)] = v;
+            else Xd[(size_t)row * Np + col] = v;
+          });
+          __syncthreads();
+          for (int rd = 0; rd < 2; ++rd) {
+            if (rd == 1) {  // diagonal tiles: global -> LDS
+              __syncthreads();
+              for (int q = 0; q < PER; ++q) {
+                const int e = tid + CG_WG * q;
+                const int ts = e / (TS * TS), rem = e % (TS * TS), ra = rem / TS, cc = rem % TS;
+                (ts == 0 ? T0 : T1)[ra * LD + cc] = Xd[(size_t)(ts * TS + ra) * Np + ts * TS + cc];
+              }
+              __syncthreads();
+            }
+            for (int q0 = 0; q0 < PER; q0 += CH) {
+              size_t idx[CH];
+              c128 k[CH], r0[CH], a0[CH];
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            cg_epilogue<BT>(A, [&](int row, int col, c128 v) {
-              const int c = col - h * HB;
-              if (c >= 0 && c < HB) T[c * (BT + 1) + row] = v;
-            });
-            __syncthreads();
-            cg_epilogue<BT>(A, [&](int row, int col, c128 v) {
-              const int rr = row - h * HB;
-              if (rr >= 0 && rr < HB) rk4_update((size_t)row * Np + col, cadd(v, cconj(T[rr * (BT + 1) + col])));
-            });
-            __syncthreads();
+              for (int q = 0; q < CH; ++q) {
+                const int e = tid + CG_WG * (q0 + q);
+                const int ts = e / (TS * TS), rem = e % (TS * TS), ra = rem / TS, cc = rem % TS;
+                const c128* own = ts == 0 ? T0 : T1;
+                const c128* mir = rd == 0 ? (ts == 0 ? T1 : T0) : own;
+                const int gc = (rd == 0 ? 1 - ts : ts) * TS + cc;  // off-diagonal: column block 1 - ts
+                idx[q] = (size_t)(ts * TS + ra) * Np + gc;
+                k[q] = cadd(own[ra * LD + cc], cconj(mir[cc * LD + ra]));
+                r0[q] = rho[idx[q]];
+                a0[q] = stage == 0 ? cmk(0, 0) : acc[idx[q]];
+              }
+#pragma unroll
+              for (int q = 0; q < CH; ++q) {
+                if (stage == 0) {
+                  acc[idx[q]] = k[q];
+                  rn[idx[q]] = cadd(r0[q], cscale(k[q], dt2));
+                } else if (stage < 3) {
+                  acc[idx[q]] = cadd(a0[q], cscale(k[q], 2.0));
+                  rn[idx[q]] = cadd(r0[q], cscale(k[q], stage == 1 ? dt2 : dt));
+                } else {
+                  const c128 r1 = cadd(r0[q], cscale(cscale(cadd(a0[q], k[q]), 1.0 / 6.0), dt));
+                  rho[idx[q]] = r1;
+                  rn[idx[q]] = r1;
+                }
+              }
+            }
           }
+          __syncthreads();
         }
         QD_TMARK(3);
         cur ^= 1;
@@ -585,7 +634,12 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
       for (int b = 0; b < B; ++b) s += (double)t[(size_t)b * 8 + q];
       std::fprintf(stderr, " %s %.2f", names[q], s / B / (khz * 1e-3) / std::max(1, nsteps));
     }
-    std::fprintf(stderr, "\n");
+    double cyc = 0, wt = 0;
+    for (int b = 0; b < B; ++b) {
+      cyc += (double)t[(size_t)b * 8 + 5];
+      wt += (double)t[(size_t)b * 8 + 6];
+    }
+    std::fprintf(stderr, " | shader clock %.0f MHz\n", wt > 0 ? cyc / (wt / (khz * 1e3)) / 1e6 : 0.0);
   }
   return QD_OK;
 }

@@ -93,15 +93,17 @@ __device__ __forceinline__ c128* fft_lds(c128* a, c128* b, const c128* tw, int t
 }
 
 // psi_point <- U psi_point for each grid point of one row held in LDS (buf[a][j]).
-__device__ __forceinline__ void apply_point_op(c128* buf, int stride, const c128* U /*[n][ns][ns]*/, int n, int ns) {
+// out[a][j] = sum_b U[j][a][b] in[b][j] for the n points j of a row ([state][point] LDS layout, row
+// stride `stride`).  Reads one LDS buffer and writes the other (no per-thread state arrays, which
+// would be indexed at run time and land in scratch).
+__device__ __forceinline__ void apply_point_op(const c128* in, c128* out, int stride, const c128* U /*[n][ns][ns]*/,
+                                               int n, int ns) {
   for (int j = threadIdx.x; j < n; j += blockDim.x) {
-    c128 in[SPO_MAX_NS];
-    for (int a = 0; a < ns; ++a) in[a] = buf[a * stride + j];
     const c128* u = U + (size_t)j * ns * ns;
     for (int a = 0; a < ns; ++a) {
       c128 s = cmk(0, 0);
-      for (int b = 0; b < ns; ++b) s = cadd(s, cmul(u[a * ns + b], in[b]));
-      buf[a * stride + j] = s;
+      for (int b = 0; b < ns; ++b) s = cadd(s, cmul(u[a * ns + b], in[b * stride + j]));
+      out[a * stride + j] = s;
     }
   }
 }
@@ -134,7 +136,10 @@ __global__ __launch_bounds__(256) void spo2_row_kernel(c128* psi, const c128* ex
   }
   const c128* Ui = expVh + (size_t)i * L * ns * ns;
   if (flags & ROW_VH1) {
-    apply_point_op(cur, L, Ui, L, ns);
+    apply_point_op(cur, oth, L, Ui, L, ns);
+    c128* tmp = cur;
+    cur = oth;
+    oth = tmp;
     __syncthreads();
   }
   if (flags & ROW_SNAP) {
@@ -142,7 +147,10 @@ __global__ __launch_bounds__(256) void spo2_row_kernel(c128* psi, const c128* ex
     __syncthreads();
   }
   if (flags & ROW_VH2) {
-    apply_point_op(cur, L, Ui, L, ns);
+    apply_point_op(cur, oth, L, Ui, L, ns);
+    c128* tmp = cur;
+    cur = oth;
+    oth = tmp;
     __syncthreads();
   }
   if (flags & ROW_FWD) {

@@ -75,16 +75,21 @@ __global__ __launch_bounds__(TD_TPB) void tdse_rk4_kernel(const c128* mHT, c128*
   for (int s = 0; s < nsteps; ++s) {
     for (int stage = 0; stage < 4; ++stage) {
       // k = (-iH) xs ; each thread owns rows r
-      c128 kreg[TD_MAXN / TD_TPB];
-      int q = 0;
-      for (int r = threadIdx.x; r < N; r += TD_TPB, ++q) {
+      constexpr int QMAX = TD_MAXN / TD_TPB;  // rows per thread; fully unrolled -> registers, not scratch
+      c128 kreg[QMAX];
+#pragma unroll
+      for (int q = 0; q < QMAX; ++q) {
+        const int r = threadIdx.x + q * TD_TPB;
         c128 k = cmk(0, 0);
-        for (int j = 0; j < N; ++j) k = cadd(k, cmul(mHT[(size_t)j * N + r], xs[j]));
+        if (r < N)
+          for (int j = 0; j < N; ++j) k = cadd(k, cmul(mHT[(size_t)j * N + r], xs[j]));
         kreg[q] = k;
       }
       __syncthreads();  // all reads of xs done
-      q = 0;
-      for (int r = threadIdx.x; r < N; r += TD_TPB, ++q) {
+#pragma unroll
+      for (int q = 0; q < QMAX; ++q) {
+        const int r = threadIdx.x + q * TD_TPB;
+        if (r >= N) break;
         const c128 k = kreg[q];
         if (stage == 0) {
           acc[r] = k;
