@@ -204,6 +204,21 @@ int qd_tdse_rk4(const qd_c128* H, qd_c128* psi, int B, int N, double dt,
                 int ne, qd_c128* obs, void* stream);
 
 /*
+ * Laser-driven TDSE (pyqed/mol.py:1862-1958 driven_dynamics, reached from
+ * Mol.run / SESolver.run with a pulse, mol.py:660-675 / 1430-1456):
+ *   H_k = H0 - sum_d f_d(t_k) Hd_d,  t_k = t0 + k nout dt,
+ * constant over block k of nout RK4 steps (calcH is evaluated with the block's
+ * start time).  fvals is a HOST array [nblocks][nd] (f_d(t_k), complex).
+ *   psi  [B][N] in/out; snap [B][nblocks][N] psi after each block, or NULL;
+ *   E [ne][N][N], obs [B][nblocks+1][ne] = <psi|E_m|psi> at t0 and after
+ *   each block, or NULL.   N <= 2048, 0 <= nd <= 16, nout >= 1.
+ */
+int qd_tdse_driven_rk4(const qd_c128* H0, const qd_c128* Hd, int nd,
+                       const qd_c128* fvals, qd_c128* psi, int B, int N,
+                       double dt, int nblocks, int nout, qd_c128* snap,
+                       const qd_c128* E, int ne, qd_c128* obs, void* stream);
+
+/*
  * 3D multi-state split operator (pyqed/wpd.py:1349-1411 SPO3.run, linear KEO
  * _KEO_linear wpd.py:1419-1432 = fftn over axes (0,1,2)).  psi [nx][ny][nz][ns],
  * expVh [nx][ny][nz][ns][ns], expK [nx][ny][nz]; snap [nsteps/nout][...].

@@ -59,6 +59,8 @@ SIGNATURES = {
     "qd_resolvent_sum": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]),
     "qd_tdse_rk4": (c_int, [c_void_p, c_void_p, c_int, c_int, c_double, c_int, c_int, c_void_p, c_void_p, c_int,
                             c_void_p, c_void_p]),
+    "qd_tdse_driven_rk4": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_double, c_int,
+                                   c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "qd_photon_echo": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p,
                                c_int, c_void_p, c_int, c_void_p, c_int, c_double, c_void_p, c_void_p]),
     "qd_fft_axis": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_double, c_void_p, c_double, c_void_p]),

@@ -63,6 +63,84 @@ def tdse_rk4(H, psi, dt, nsteps, save_every=0, e_ops=None):
     return snap, obs
 
 
+def tdse_driven_rk4(H0, Hd, fvals, psi, dt, nout, e_ops=None):
+    """Laser-driven batched RK4 on the GPU (qd_tdse_driven_rk4): block k of `nout` steps uses
+    H0 - sum_d fvals[k, d] Hd[d].  H0 [N,N], Hd [nd,N,N] | None, fvals host complex [nblocks, nd],
+    psi [B,N] (in place), e_ops [ne,N,N] | None.  Returns (snap [B,nblocks,N], obs [B,nblocks+1,ne] | None)."""
+    import torch
+    from . import _lib
+    dev = psi.device
+    _lib.ensure_device(dev)
+    B, N = psi.shape
+    fv = np.ascontiguousarray(np.asarray(fvals, dtype=np.complex128))
+    nblocks = fv.shape[0]
+    nd = 0 if Hd is None else Hd.shape[0]
+    ne = 0 if e_ops is None else e_ops.shape[0]
+    snap = torch.empty((B, nblocks, N), dtype=torch.complex128, device=dev) if nblocks else None
+    obs = torch.empty((B, nblocks + 1, ne), dtype=torch.complex128, device=dev) if ne else None
+    with torch.cuda.device(dev):
+        rc = _lib.load().qd_tdse_driven_rk4(_lib.ptr(H0), _lib.ptr(Hd), nd, fv.ctypes.data if fv.size else None,
+                                            _lib.ptr(psi), B, N, float(dt), nblocks, int(nout), _lib.ptr(snap),
+                                            _lib.ptr(e_ops), ne, _lib.ptr(obs), _lib.stream_ptr(dev))
+        torch.cuda.current_stream(dev).synchronize()  # fvals is a host buffer read asynchronously
+    _lib.check(rc, "qd_tdse_driven_rk4")
+    return snap, obs
+
+
+def driven_dynamics(H, psi0, dt=0.01, Nt=1, e_ops=None, nout=1, t0=0.0, return_result=True, use_sparse=True):
+    """mol.py:1862-1958.  H = [H0, [Hd_1, f_1], [Hd_2, f_2], ...] with H(t) = H0 - sum_d f_d(t) Hd_d,
+    evaluated once per block of nout steps at the block's start time (calcH(t), t advanced by
+    dt*nout after each block).  return_result=True: Nt//nout - 1 blocks; psilist = [psi0] + the
+    state after each block (csr columns when use_sparse, as the reference's sparse psi);
+    observables (Nt//nout, n_e) including t0; result.psi = psit [nstates, Nt//nout].
+    return_result=False: int(Nt/nout) blocks written to psi.dat / obs.dat (t after the block,
+    then the values; dense formatting)."""
+    import torch
+    from scipy.sparse import csr_matrix
+    from ._util import default_device, stack_ops, to_numpy
+    if e_ops is None:
+        e_ops = []
+    dev = default_device()
+    H0 = to_numpy(H[0], np.complex128)
+    N = H0.shape[0]
+    drives = H[1:]
+    Hd = [to_numpy(h[0], np.complex128) for h in drives]
+    p0 = to_numpy(psi0, np.complex128).reshape(N)
+    nblocks = max(Nt // nout - 1, 0) if return_result else int(Nt / nout)
+    fvals = np.array([[complex(f(t0 + k * dt * nout)) for (_, f) in drives] for k in range(nblocks)],
+                     dtype=np.complex128).reshape(nblocks, len(drives))
+    psi = torch.from_numpy(p0.copy()).to(dev).reshape(1, N)
+    Hdt = torch.from_numpy(np.ascontiguousarray(np.array(Hd))).to(dev) if Hd else None
+    Ed = stack_ops(e_ops, N, dev)
+    snap, obs = tdse_driven_rk4(torch.from_numpy(np.ascontiguousarray(H0)).to(dev), Hdt, fvals, psi, dt, nout,
+                                e_ops=Ed)
+    states = snap[0].cpu().numpy() if snap is not None else np.zeros((0, N), complex)
+    o = obs[0].cpu().numpy() if obs is not None else np.zeros((nblocks + 1, 0), complex)
+    if not return_result:
+        with open("psi.dat", "w") as f_dm, open("obs.dat", "w") as f_obs:
+            fmt = "{} " * (len(e_ops) + 1) + "\n"
+            fmt_dm = "{} " * (N + 1) + "\n"
+            for k in range(nblocks):
+                t = t0 + (k + 1) * dt * nout
+                f_dm.write(fmt_dm.format(t, *states[k]))
+                f_obs.write(fmt.format(t, *o[k + 1]))
+        return None
+    result = Result(dt=dt, Nt=Nt, psi0=psi0, t0=t0, nout=nout)
+    nrec = Nt // nout
+    observables = np.zeros((nrec, len(e_ops)), dtype=complex)
+    observables[:nblocks + 1] = o[:nrec]
+    psit = np.zeros((N, nrec), dtype=complex)
+    psit[:, 0] = p0
+    psilist = [np.array(psi0, copy=True)]
+    for k in range(nblocks):
+        psit[:, k + 1] = states[k]
+        psilist.append(csr_matrix(states[k].reshape(N, 1)) if use_sparse else states[k].copy())
+    result.psilist = psilist
+    result.psi = psit
+    result.observables = observables
+    return result
+
+
 def _quantum_dynamics(H, psi0, dt=0.001, Nt=1, e_ops=[], t0=0.0, nout=1, store_states=True, output='obs.dat'):
     """mol.py:1603-1691 (store_states=True): (Nt//nout - 1)*nout RK4 steps; psilist = [psi0] + the
     state after every nout steps; observables (Nt//nout, n_e) at those states."""
@@ -102,11 +180,21 @@ class SESolver:
         self.groundstate = None
 
     def run(self, psi0=None, dt=0.01, Nt=1, e_ops=None, nout=1, t0=0.0, edip=None, pulse=None, use_sparse=True):
+        """mol.py:1392-1459: time-independent H -> _quantum_dynamics; with a pulse (or a list of
+        pulses with a list of dipoles) -> driven_dynamics, H(t) = H - sum_i f_i(t) edip_i."""
         if psi0 is None:
             psi0 = self.groundstate
-        if pulse is not None:
-            raise NotImplementedError("laser-driven TDSE (pulse=...) is not on the GPU path yet")
-        return _quantum_dynamics(self.H, psi0, dt=dt, Nt=Nt, e_ops=e_ops, nout=nout, t0=t0)
+        if pulse is None:
+            return _quantum_dynamics(self.H, psi0, dt=dt, Nt=Nt, e_ops=e_ops, nout=nout, t0=t0)
+        if edip is None:
+            raise ValueError('Electric dipole must be provided for laser-driven dynamics.')
+        if isinstance(pulse, list):
+            H = [self.H] + [[edip[i], pulse[i].efield] for i in range(len(pulse))]
+            return driven_dynamics(H=H, psi0=psi0, dt=dt, Nt=Nt, e_ops=e_ops, nout=nout, t0=t0)
+        if np.ndim(edip) == 2:
+            return driven_dynamics(H=[self.H, [edip, pulse.efield]], psi0=psi0, dt=dt, Nt=Nt, e_ops=e_ops,
+                                   nout=nout, t0=t0, use_sparse=use_sparse)
+        raise NotImplementedError("full 3D dipole with a vector pulse (mol._driven_dynamics) is not on the GPU path")
 
 
 class Mol:
@@ -155,12 +243,18 @@ class Mol:
         self._edip_rms = edip
 
     def run(self, psi0=None, dt=0.01, e_ops=None, nt=1, nout=1, t0=0.0, edip=None, pulse=None):
-        """mol.py:628-674 (time-independent H) -> _quantum_dynamics."""
+        """mol.py:628-674: _quantum_dynamics, or driven_dynamics with H(t) = H - f(t) edip for a pulse
+        (self.edip is used, as in the reference; a list of pulses pairs with a list of dipoles)."""
         if psi0 is None:
             raise ValueError("Please specify initial wavefunction psi0.")
-        if pulse is not None:
-            raise NotImplementedError("laser-driven dynamics (pulse=...) is not on the GPU path yet")
-        return _quantum_dynamics(self.H, psi0, dt=dt, Nt=nt, e_ops=e_ops, nout=nout, t0=t0)
+        if pulse is None:
+            return _quantum_dynamics(self.H, psi0, dt=dt, Nt=nt, e_ops=e_ops, nout=nout, t0=t0)
+        edip = self.edip
+        if isinstance(pulse, list):
+            H = [self.H] + [[edip[i], pulse[i].efield] for i in range(len(pulse))]
+        else:
+            H = [self.H, [edip, pulse.efield]]
+        return driven_dynamics(H, psi0, dt=dt, Nt=nt, e_ops=e_ops, nout=nout, t0=t0)
 
     def eigvals(self):
         """mol.py:459-463."""

@@ -198,6 +198,45 @@ def sesolver():
 
 
 @golden
+def tdse_driven():
+    """Laser-driven TDSE: SESolver.run / Mol.run with pulses -> driven_dynamics (mol.py:1392-1456,
+    628-675, 1862-1958) and optics.Pulse.efield (optics.py:229-318)."""
+    from pyqed.mol import Mol, SESolver
+    from pyqed.optics import Pulse
+    rng = np.random.default_rng(37)
+    out = {}
+    # a: single pulse, SESolver, 2D dipole, csr psi (use_sparse=True)
+    N = 6
+    H = np.diag(np.linspace(0.0, 1.5, N)).astype(complex) + 0.05 * _herm(rng, N)
+    d = _herm(rng, N, 0.5)
+    E = [_herm(rng, N) for _ in range(2)]
+    psi0 = np.zeros(N, complex); psi0[0] = 1.0
+    p = dict(omegac=0.8, tau=2.0, tc=3.0, amplitude=0.3)
+    r = SESolver(H).run(psi0=psi0, dt=0.05, Nt=60, e_ops=[csr_matrix(e) for e in E], nout=3, edip=d,
+                        pulse=Pulse(**p))
+    out.update({"a_H": H, "a_d": d, "a_E": np.array(E), "a_psi0": psi0, "a_dt": 0.05, "a_Nt": 60, "a_nout": 3,
+                "a_t0": 0.0, "a_pulse": np.array([p["omegac"], p["tau"], p["tc"], p["amplitude"]]),
+                "a_obs": r.observables, "a_psit": r.psi,
+                "a_psilist": np.array([np.asarray(x.toarray() if hasattr(x, "toarray") else x).reshape(N)
+                                       for x in r.psilist])})
+    # b: two pulses, Mol.run (self.edip list), t0 != 0, nout = 1
+    N = 9
+    H = np.diag(np.linspace(0.0, 2.0, N)).astype(complex) + 0.1 * _herm(rng, N)
+    ds = [_herm(rng, N, 0.3), _herm(rng, N, 0.2)]
+    E = [_herm(rng, N)]
+    psi0 = rng.standard_normal(N) + 1j * rng.standard_normal(N); psi0 /= np.linalg.norm(psi0)
+    ps = [dict(omegac=1.1, tau=1.5, tc=1.0, amplitude=0.2), dict(omegac=0.6, tau=3.0, tc=2.5, amplitude=0.1)]
+    r = Mol(H, edip=ds).run(psi0=psi0, dt=0.04, e_ops=[csr_matrix(e) for e in E], nt=50, nout=1, t0=0.3, pulse=[Pulse(**q) for q in ps])
+    out.update({"b_H": H, "b_d": np.array(ds), "b_E": np.array(E), "b_psi0": psi0, "b_dt": 0.04, "b_Nt": 50,
+                "b_nout": 1, "b_t0": 0.3,
+                "b_pulse": np.array([[q["omegac"], q["tau"], q["tc"], q["amplitude"]] for q in ps]),
+                "b_obs": r.observables, "b_psit": r.psi,
+                "b_psilist": np.array([np.asarray(x.toarray() if hasattr(x, "toarray") else x).reshape(N)
+                                       for x in r.psilist])})
+    save("tdse_driven", **out)
+
+
+@golden
 def photon_echo():
     """sos.photon_echo (signal/sos.py:962-1052) via Mol.photon_echo (mol.py:804-829)."""
     import tempfile

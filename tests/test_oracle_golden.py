@@ -132,3 +132,29 @@ def test_deom_run_oracle_matches_reference(name):
     ref = g["trace_p1"] if p1 is not None else g["rho_sys"]
     assert relerr(saved, ref) < TOL
     assert relerr(ddos, g["ado_final"]) < 1e-12
+
+
+@pytest.mark.parametrize("tag", ["a", "b"])
+def test_tdse_oracle_matches_reference(tag):
+    from oracle import tdse as ot
+    g = load_golden("sesolver")
+    obs, psil = ot.quantum_dynamics(g[f"{tag}_H"], g[f"{tag}_psi0"], float(g[f"{tag}_dt"]), int(g[f"{tag}_Nt"]),
+                                    list(g[f"{tag}_E"]), int(g[f"{tag}_nout"]))
+    assert relerr(obs, g[f"{tag}_obs"]) < 1e-12
+    assert relerr(psil, g[f"{tag}_psilist"]) < 1e-12
+
+
+@pytest.mark.parametrize("tag", ["a", "b"])
+def test_tdse_driven_oracle_matches_reference(tag):
+    from oracle import tdse as ot
+    g = load_golden("tdse_driven")
+    d = g[f"{tag}_d"]
+    pulses = np.atleast_2d(g[f"{tag}_pulse"])
+    dips = [d] if d.ndim == 2 else list(d)
+    drives = [(dp, ot.gaussian_efield(*p)) for dp, p in zip(dips, pulses)]
+    obs, psit, psil = ot.driven_dynamics(g[f"{tag}_H"], drives, g[f"{tag}_psi0"], float(g[f"{tag}_dt"]),
+                                         int(g[f"{tag}_Nt"]), list(g[f"{tag}_E"]), int(g[f"{tag}_nout"]),
+                                         float(g[f"{tag}_t0"]))
+    assert relerr(obs, g[f"{tag}_obs"]) < 1e-12
+    assert relerr(psit, g[f"{tag}_psit"]) < 1e-12
+    assert relerr(psil, g[f"{tag}_psilist"]) < 1e-12
