@@ -140,6 +140,20 @@ int qd_spo2_run(qd_c128* psi, const qd_c128* expVh, const qd_c128* expK, int nx,
                 void* stream);
 
 /*
+ * qd_spo2_run with the two other SPO2 step structures of pyqed/wpd.py:
+ *   expKy != NULL: Jacobi KEO (_KEO_jacobi, wpd.py:850-887): FFT_y, * expKy[i][ky]
+ *                  (row i's factor exp(-i ky^2/(2 I(x_i)) dt)), FFT_x, * expK, IFFT2;
+ *                  expK is then exp_Kx[kx] broadcast over ky ([nx][ny]).
+ *   expV != NULL:  merged potential (run(return_states=False), wpd.py:736-755 and
+ *                  SPO2NH.run wpd.py:1054-1077): V/2, nsteps x [K, V] with a snapshot
+ *                  after every nout steps (state after V), then K, V/2.
+ * expVh / expV may be non-unitary (SPO2NH's U e^{-i w dt} U^-1 of a complex potential).
+ */
+int qd_spo2_run_ex(qd_c128* psi, const qd_c128* expVh, const qd_c128* expV,
+                   const qd_c128* expK, const qd_c128* expKy, int nx, int ny,
+                   int ns, int nsteps, int nout, qd_c128* snap, void* stream);
+
+/*
  * 1D single-surface split-operator with the step structure of pyqed/wpd.py:225-273
  * (SPO.run): V/2 ; (nt//nout - 1)*nout x [K, V] (snapshot after each block) ; K, V/2.
  * psi [B][nx] in/out (B independent wavepackets, one workgroup each, all steps in

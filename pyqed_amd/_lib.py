@@ -42,6 +42,8 @@ SIGNATURES = {
     "qd_glf_rk4": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_double,
                            c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "qd_basis_transform": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "qd_spo2_run_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                               c_void_p, c_void_p]),
     "qd_spo2_run": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "qd_spo1d_run": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                              c_void_p]),

@@ -108,12 +108,14 @@ __device__ __forceinline__ void apply_point_op(const c128* in, c128* out, int st
   }
 }
 
-enum RowFlags { ROW_INV = 1, ROW_VH1 = 2, ROW_SNAP = 4, ROW_VH2 = 8, ROW_FWD = 16 };
+enum RowFlags { ROW_INV = 1, ROW_VH1 = 2, ROW_SNAP = 4, ROW_VH2 = 8, ROW_FWD = 16, ROW_KY = 32 };
 
 // One row i of psi [nx][ny][ns]; FFTs along y (length L = ny) for each state.
+// ROW_KY (Jacobi KEO, wpd.py:850-887): after FFT_y multiply by expKy[i][ky] (row i's k_y factor).
+// `expVh` is the point operator of this pass (exp_V_half, or exp_V on merged passes).
 template <int L>
 __global__ __launch_bounds__(256) void spo2_row_kernel(c128* psi, const c128* expVh, const c128* twy, int ny, int ns,
-                                                       int flags, c128* snap) {
+                                                       int flags, c128* snap, const c128* expKy) {
   extern __shared__ c128 sm[];
   c128* tw = sm;            // L
   c128* A = sm + L;         // ns * L
@@ -156,6 +158,11 @@ __global__ __launch_bounds__(256) void spo2_row_kernel(c128* psi, const c128* ex
   if (flags & ROW_FWD) {
     c128* r = fft_lds<L, false>(cur + (active ? f : 0) * L, oth + (active ? f : 0) * L, tw, t, active);
     cur = (r == cur + (active ? f : 0) * L) ? cur : oth;
+  }
+  if (flags & ROW_KY) {
+    const c128* ky = expKy + (size_t)i * L;
+    for (int e = threadIdx.x; e < L * ns; e += blockDim.x) cur[e] = cmul(ky[e % L], cur[e]);
+    __syncthreads();
   }
   for (int e = threadIdx.x; e < L * ns; e += blockDim.x) psi[rowoff + e] = cur[(e % ns) * L + e / ns];
 }
@@ -304,15 +311,16 @@ int twiddles(int L, hipStream_t st, c128* tw) {
 
 using namespace qd;
 
-extern "C" int qd_spo2_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* expK_, int nx, int ny, int ns,
-                           int nsteps, int nout, qd_c128* snap_, void* stream) {
-  QD_CHECK_ARG(psi_ && expVh_ && expK_, "qd_spo2_run: null pointer");
-  QD_CHECK_ARG(pow2_in_range(nx) && pow2_in_range(ny), "qd_spo2_run: nx=%d, ny=%d must be powers of 2 in [16, 1024]",
+extern "C" int qd_spo2_run_ex(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* expV_, const qd_c128* expK_,
+                              const qd_c128* expKy_, int nx, int ny, int ns, int nsteps, int nout, qd_c128* snap_,
+                              void* stream) {
+  QD_CHECK_ARG(psi_ && expVh_ && expK_, "qd_spo2_run_ex: null pointer");
+  QD_CHECK_ARG(pow2_in_range(nx) && pow2_in_range(ny), "qd_spo2_run_ex: nx=%d, ny=%d must be powers of 2 in [16, 1024]",
                nx, ny);
-  QD_CHECK_ARG(ns >= 1 && ns <= SPO_MAX_NS, "qd_spo2_run: ns=%d outside [1, %d]", ns, SPO_MAX_NS);
-  QD_CHECK_ARG(nsteps >= 0 && nout >= 1, "qd_spo2_run: nsteps=%d nout=%d", nsteps, nout);
-  QD_CHECK_ARG(ns * (ny / 4) <= 256, "qd_spo2_run: ns*ny/4 = %d > 256 threads", ns * (ny / 4));
-  if (nsteps == 0) return QD_OK;
+  QD_CHECK_ARG(ns >= 1 && ns <= SPO_MAX_NS, "qd_spo2_run_ex: ns=%d outside [1, %d]", ns, SPO_MAX_NS);
+  QD_CHECK_ARG(nsteps >= 0 && nout >= 1, "qd_spo2_run_ex: nsteps=%d nout=%d", nsteps, nout);
+  QD_CHECK_ARG(ns * (ny / 4) <= 256, "qd_spo2_run_ex: ns*ny/4 = %d > 256 threads", ns * (ny / 4));
+  if (nsteps == 0 && !expV_) return QD_OK;
   hipStream_t st = (hipStream_t)stream;
   c128* psi = (c128*)psi_;
   const c128* expVh = (const c128*)expVh_;
@@ -334,16 +342,20 @@ extern "C" int qd_spo2_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
   int C = std::max(1, 256 / (ns * (nx / 4)));
   while (C > 1 && ny % C) C >>= 1;
   C = std::min(C, 2);  // keep >= ny/2 workgroups in flight
-  QD_CHECK_ARG(ns * (nx / 4) <= 256, "qd_spo2_run: ns*nx/4 = %d > 256 threads", ns * (nx / 4));
+  QD_CHECK_ARG(ns * (nx / 4) <= 256, "qd_spo2_run_ex: ns*nx/4 = %d > 256 threads", ns * (nx / 4));
   const int row_threads = std::max(64, ((ns * (ny / 4) + 63) / 64) * 64);
   const size_t row_lds = (size_t)(ny + 2 * ns * ny) * sizeof(c128);
   const int col_threads = std::max(64, ((C * ns * (nx / 4) + 63) / 64) * 64);
   const size_t col_lds = (size_t)(nx + 2 * C * ns * nx) * sizeof(c128);
-  QD_CHECK_ARG(row_lds <= 160 * 1024 && col_lds <= 160 * 1024, "qd_spo2_run: LDS footprint too large");
+  QD_CHECK_ARG(row_lds <= 160 * 1024 && col_lds <= 160 * 1024, "qd_spo2_run_ex: LDS footprint too large");
 
-  auto row = [&](int flags, c128* sp) -> int {
+  const c128* expV = (const c128*)expV_;
+  const c128* expKy = (const c128*)expKy_;
+  const int ky = expKy ? ROW_KY : 0;
+  auto row = [&](int flags, c128* sp, const c128* U) -> int {
 #define ROWCALL(L) \
-  hipLaunchKernelGGL(spo2_row_kernel<L>, dim3(nx), dim3(row_threads), row_lds, st, psi, expVh, twy, ny, ns, flags, sp)
+  hipLaunchKernelGGL(spo2_row_kernel<L>, dim3(nx), dim3(row_threads), row_lds, st, psi, U, twy, ny, ns, flags, sp, \
+                     expKy)
     QD_FFT_DISPATCH(ny, ROWCALL)
 #undef ROWCALL
     QD_HIP(hipGetLastError());
@@ -362,16 +374,29 @@ extern "C" int qd_spo2_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
     return QD_OK;
   };
   const size_t grid_elems = (size_t)nx * ny * ns;
-  if ((rc = row(ROW_VH1 | ROW_FWD, nullptr))) return rc;
+  if ((rc = row(ROW_VH1 | ROW_FWD | ky, nullptr, expVh))) return rc;
   for (int s = 1; s <= nsteps; ++s) {
     if ((rc = col())) return rc;
     const bool take = snap && (s % nout == 0);
     c128* sp = take ? snap + (size_t)(s / nout - 1) * grid_elems : nullptr;
     int flags = ROW_INV | ROW_VH1 | (take ? ROW_SNAP : 0);
-    if (s < nsteps) flags |= ROW_VH2 | ROW_FWD;
-    if ((rc = row(flags, sp))) return rc;
+    if (expV) {  // merged: IFFT_y -> V -> [snapshot] -> FFT_y
+      flags |= ROW_FWD | ky;
+    } else if (s < nsteps) {  // Strang: IFFT_y -> V/2 -> [snapshot] -> V/2 -> FFT_y
+      flags |= ROW_VH2 | ROW_FWD | ky;
+    }
+    if ((rc = row(flags, sp, expV ? expV : expVh))) return rc;
+  }
+  if (expV) {  // merged tail (wpd.py:752-755): K, then V/2
+    if ((rc = col())) return rc;
+    if ((rc = row(ROW_INV | ROW_VH1, nullptr, expVh))) return rc;
   }
   return QD_OK;
+}
+
+extern "C" int qd_spo2_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* expK_, int nx, int ny, int ns,
+                           int nsteps, int nout, qd_c128* snap_, void* stream) {
+  return qd_spo2_run_ex(psi_, expVh_, nullptr, expK_, nullptr, nx, ny, ns, nsteps, nout, snap_, stream);
 }
 
 extern "C" int qd_spo1d_run(qd_c128* psi_, const qd_c128* expV_, const qd_c128* expVh_, const qd_c128* expK_, int nx,
@@ -431,7 +456,8 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
   const int inner = nz * ns;
   auto row = [&](int flags, c128* sp) -> int {
 #define ROWCALL3(L) \
-  hipLaunchKernelGGL(spo2_row_kernel<L>, dim3(nx * ny), dim3(row_threads), row_lds, st, psi, expVh, twz, nz, ns, flags, sp)
+  hipLaunchKernelGGL(spo2_row_kernel<L>, dim3(nx * ny), dim3(row_threads), row_lds, st, psi, expVh, twz, nz, ns, flags, sp, \
+                     (const c128*)nullptr)
     QD_FFT_DISPATCH(nz, ROWCALL3)
 #undef ROWCALL3
     QD_HIP(hipGetLastError());

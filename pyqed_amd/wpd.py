@@ -120,7 +120,7 @@ class SPO:
 
 
 class SPO2:
-    """Drop-in for pyqed.wpd.SPO2 (wpd.py:379-887), linear coordinates."""
+    """Drop-in for pyqed.wpd.SPO2 (wpd.py:379-887), linear and Jacobi coordinates."""
 
     def __init__(self, x, y, mass=None, nstates=2, coords='linear', G=None, abc=False):
         self.x = x
@@ -181,16 +181,13 @@ class SPO2:
         return self
 
     def build(self, dt, inertia=None):
-        """wpd.py:496-625: exp_K on the 'ij' k-grid and per-point U e^{-i w dt/2} U^+
-        (vectorised eigh over the grid instead of the reference's Python loop)."""
-        if self.coords != 'linear':
-            raise NotImplementedError("only linear coordinates run on the GPU path")
+        """wpd.py:496-625: the kinetic propagator (linear: exp_K on the 'ij' k-grid; jacobi:
+        exp_Kx and exp_Ky[i, ky] = exp(-i ky^2 / (2 I(x_i)) dt) with I = masses[1]) and per-point
+        U e^{-i w dt/2} U^+ (vectorised eigh over the grid instead of the reference's Python loop)."""
         nx, ny = self.nx, self.ny
         self.kx = 2. * np.pi * fftfreq(nx, interval(self.x))
         self.ky = 2. * np.pi * fftfreq(ny, interval(self.y))
-        mx, my = self.masses
-        Kx, Ky = meshgrid(self.kx, self.ky)
-        self.exp_K = np.exp(-1j * (Kx ** 2 / 2. / mx + Ky ** 2 / 2. / my) * dt)
+        self._build_keo(dt)
         if self.v is None:
             raise ValueError('The diabatic PES is not specified.')
         v = self.v
@@ -202,32 +199,107 @@ class SPO2:
         if not np.iscomplexobj(v):
             self.apes = w
 
-    def run(self, psi0, e_ops=[], dt=0.01, nt=1, t0=0., nout=1, return_states=True):
-        """wpd.py:692-758 with return_states=True semantics: psilist = [psi0] + the state after
-        every nout Strang steps (nt//nout*nout steps in total); r.psi is the final state."""
-        self.build(dt=dt)
+    def _build_keo(self, dt):
+        if self.coords == 'linear':
+            mx, my = self.masses
+            Kx, Ky = meshgrid(self.kx, self.ky)
+            self.exp_K = np.exp(-1j * (Kx ** 2 / 2. / mx + Ky ** 2 / 2. / my) * dt)
+        elif self.coords == 'jacobi':
+            mx = self.masses[0]
+            self.exp_Kx = np.exp(-1j * self.kx ** 2 / 2. / mx * dt)
+            Iinv = 1. / self.masses[1](self.x)  # y is the angle
+            self.exp_Ky = np.exp(-1j * np.outer(Iinv, self.ky ** 2 / 2.) * dt)
+        else:
+            raise ValueError(f"unknown coordinates {self.coords!r}")
+
+    def _propagate(self, psi0, dt, nt, nout, merged):
+        """GPU run (qd_spo2_run_ex): Strang steps V/2 K V/2 with a snapshot after every nout
+        steps (merged=False), or the merged V/2, [K V]..., K, V/2 structure (merged=True).
+        Returns (final psi, list of snapshots)."""
         dev = default_device()
         _lib.ensure_device(dev)
         nsteps = (nt // nout) * nout
         psi = _dev_c128(psi0, dev)
         nsnap = nt // nout
-        snap = torch.empty((nsnap, self.nx, self.ny, self.ns), dtype=torch.complex128, device=dev) \
-            if (nsnap and return_states) else None
+        snap = torch.empty((nsnap, self.nx, self.ny, self.ns), dtype=torch.complex128, device=dev) if nsnap else None
         eVh = _dev_c128(self.exp_V_half, dev)
-        eK = _dev_c128(self.exp_K, dev)
+        eV = _dev_c128(self.exp_V, dev) if merged else None
+        if self.coords == 'jacobi':
+            eK = _dev_c128(np.broadcast_to(self.exp_Kx[:, None], (self.nx, self.ny)), dev)
+            eKy = _dev_c128(self.exp_Ky, dev)
+        else:
+            eK = _dev_c128(self.exp_K, dev)
+            eKy = None
         with torch.cuda.device(dev):
-            rc = _lib.load().qd_spo2_run(psi.data_ptr(), eVh.data_ptr(), eK.data_ptr(), self.nx, self.ny, self.ns,
-                                         int(nsteps), int(nout), _lib.ptr(snap), _lib.stream_ptr(dev))
-        _lib.check(rc, "qd_spo2_run")
+            rc = _lib.load().qd_spo2_run_ex(psi.data_ptr(), eVh.data_ptr(), _lib.ptr(eV), eK.data_ptr(), _lib.ptr(eKy),
+                                            self.nx, self.ny, self.ns, int(nsteps), int(nout), _lib.ptr(snap),
+                                            _lib.stream_ptr(dev))
+        _lib.check(rc, "qd_spo2_run_ex")
+        states = []
+        if snap is not None:
+            host = snap.cpu().numpy()
+            states = [host[k] for k in range(nsnap)]
+        return psi.cpu().numpy(), states
+
+    def run(self, psi0, e_ops=[], dt=0.01, nt=1, t0=0., nout=1, return_states=True):
+        """wpd.py:692-758.  return_states=True: psilist = [psi0] + the state after every nout
+        Strang steps (nt//nout*nout steps).  return_states=False: the merged-V arithmetic runs
+        but, as in the reference, psilist is only [psi0].  r.psi is the final state (the
+        reference leaves it unset)."""
+        self.build(dt=dt)
+        psi, states = self._propagate(psi0, dt, nt, nout, merged=not return_states)
         r = ResultSPO2(dt=dt, psi0=psi0, Nt=nt, t0=t0, nout=nout)
         r.x = self.x
         r.y = self.y
-        psilist = [psi0]
-        if snap is not None:
-            host = snap.cpu().numpy()
-            psilist += [host[k] for k in range(nsnap)]
-        r.psilist = psilist
-        r.psi = psi.cpu().numpy()
+        r.psilist = [psi0] + (states if return_states else [])
+        r.psi = psi
+        return r
+
+
+class SPO2NH(SPO2):
+    """Drop-in for pyqed.wpd.SPO2NH (wpd.py:921-1081): complex (non-Hermitian) diabatic
+    potential; exp_V = U_R e^{-i w dt} U_R^-1 from the right eigenvectors (nonherm.eig,
+    nonherm.py:26-76, eigenvalues sorted by np.argsort)."""
+
+    def __init__(self, x, y, *args, **kwargs):
+        self.right_eigenstates = None
+        super().__init__(x, y, *args, **kwargs)
+
+    def build(self, dt):
+        nx, ny = self.nx, self.ny
+        self.kx = 2. * np.pi * fftfreq(nx, interval(self.x))
+        self.ky = 2. * np.pi * fftfreq(ny, interval(self.y))
+        self._build_keo(dt)
+        v = np.asarray(self.v, dtype=complex)
+        w, ur = np.linalg.eig(v)
+        idx = np.argsort(w, axis=-1)
+        w = np.take_along_axis(w, idx, axis=-1)
+        ur = np.take_along_axis(ur, idx[..., None, :], axis=-1)
+        ul = np.linalg.inv(ur)
+        self.right_eigenstates = ur
+        self.ovlp_rr = np.conj(np.swapaxes(ur, -1, -2)) @ ur
+        self.exp_V = (ur * np.exp(-1j * w * dt)[..., None, :]) @ ul
+        self.exp_V_half = (ur * np.exp(-1j * w * dt / 2)[..., None, :]) @ ul
+
+    def position(self, psilist):
+        """wpd.py:997-1017 (no plot, no xAve.npz file)."""
+        dx, dy = interval(self.x), interval(self.y)
+        S = self.ovlp_rr
+        xAve = [np.einsum('ijm, i, ijmn, ijn ->', psi.conj(), self.x, S, psi) * dx * dy for psi in psilist]
+        yAve = [np.einsum('ijn, j, ijmn, ijn ->', psi.conj(), self.y, S, psi) * dx * dy for psi in psilist]
+        self.xAve = [xAve, yAve]
+        return xAve, yAve
+
+    def run(self, psi0, e_ops=[], dt=0.01, nt=1, t0=0., nout=1, return_states=True):
+        """wpd.py:1019-1077: Strang steps (return_states=True) or the merged structure
+        (False); psilist = [psi0] + the state after every nout steps in both cases; r.psi set."""
+        self.build(dt=dt)
+        psi, states = self._propagate(psi0, dt, nt, nout, merged=not return_states)
+        r = ResultSPO2(dt=dt, psi0=psi0, Nt=nt, t0=t0, nout=nout)
+        r.x = self.x
+        r.y = self.y
+        r.psilist = [psi0] + states
+        r.psi = psi
         return r
 
 

@@ -438,6 +438,43 @@ def spo2_64_complex():
 
 
 @golden
+def spo2nh_32():
+    """SPO2NH (wpd.py:921-1077): complex potential (absorbing wall -i eta (x-3)^2 on both surfaces),
+    Strang (return_states=True) and merged (return_states=False) runs."""
+    from pyqed.wpd import SPO2NH
+    n = 32
+    x, y, v0, v1, c, psi0 = spo2_model(n)
+    X, Y = np.meshgrid(x, y, indexing="ij")
+    v = np.zeros((n, n, 2, 2), dtype=complex)
+    absorb = -1j * 0.02 * np.clip(X - 3.0, 0, None) ** 2
+    v[:, :, 0, 0], v[:, :, 1, 1] = v0 + absorb, v1 + absorb
+    v[:, :, 0, 1] = v[:, :, 1, 0] = c
+    out = dict(x=x, y=y, v=v, psi0=psi0, dt=0.1, nt=6, nout=2)
+    for tag, rs in (("strang", True), ("merged", False)):
+        sol = SPO2NH(x, y, mass=[1.0, 1.0], nstates=2)
+        sol.set_dpes(v)
+        r = sol.run(psi0, dt=0.1, nt=6, nout=2, return_states=rs)
+        out[f"{tag}_psilist"] = np.array(r.psilist)
+        out[f"{tag}_psi"] = r.psi
+    out["exp_V_half"] = sol.exp_V_half
+    out["exp_V"] = sol.exp_V
+    save("spo2nh_32", **out)
+
+
+@golden
+def spo2_jacobi_32():
+    """SPO2 coords='jacobi' (build wpd.py:540-553, _KEO_jacobi wpd.py:850-887), I(x) = 1.5 + 0.2 x^2."""
+    from pyqed.wpd import SPO2
+    n = 32
+    x, y, v0, v1, c, psi0 = spo2_model(n)
+    sol = SPO2(x, y, mass=[1.0, lambda r: 1.5 + 0.2 * r ** 2], nstates=2, coords='jacobi')
+    sol.set_DPES([v0, v1], [[[0, 1], c]])
+    r = sol.run(psi0, dt=0.05, nt=6, nout=3)
+    save("spo2_jacobi_32", x=x, y=y, v0=v0, v1=v1, coupling=np.asarray(c), psi0=psi0, dt=0.05, nt=6, nout=3,
+         inertia=np.array([1.5, 0.2]), psilist=np.array(r.psilist), exp_Kx=sol.exp_Kx, exp_Ky=sol.exp_Ky)
+
+
+@golden
 def spo3_16():
     """SPO3 (wpd.py:1105-1432) on a 16^3 x 2 grid, examples/spo.py model (64^3 x 2 there)."""
     from pyqed.wpd import SPO3

@@ -158,3 +158,41 @@ def test_tdse_driven_oracle_matches_reference(tag):
     assert relerr(obs, g[f"{tag}_obs"]) < 1e-12
     assert relerr(psit, g[f"{tag}_psit"]) < 1e-12
     assert relerr(psil, g[f"{tag}_psilist"]) < 1e-12
+
+
+def test_spo2nh_oracle_matches_reference():
+    from oracle import spo
+    g = load_golden("spo2nh_32")
+    eV, eVh = spo.spo2nh_build(g["v"], float(g["dt"]))
+    assert relerr(eV, g["exp_V"]) < TOL
+    assert relerr(eVh, g["exp_V_half"]) < TOL
+    x, y = g["x"], g["y"]
+    X, Y = np.meshgrid(x, y, indexing="ij")
+    n = len(x)
+    kx = 2 * np.pi * np.fft.fftfreq(n, x[1] - x[0])
+    ky = 2 * np.pi * np.fft.fftfreq(n, y[1] - y[0])
+    Kx, Ky = np.meshgrid(kx, ky, indexing="ij")
+    keo = spo.keo_linear(np.exp(-1j * (Kx ** 2 / 2 + Ky ** 2 / 2) * float(g["dt"])))
+    nt, nout = int(g["nt"]), int(g["nout"])
+    pl, psi = spo.spo2_strang_run(eVh, keo, g["psi0"], nt, nout)
+    assert relerr(np.array(pl), g["strang_psilist"]) < TOL
+    assert relerr(psi, g["strang_psi"]) < TOL
+    pl, psi = spo.spo2_merged_run(eV, eVh, keo, g["psi0"], nt, nout)
+    assert relerr(np.array(pl), g["merged_psilist"]) < TOL
+    assert relerr(psi, g["merged_psi"]) < TOL
+
+
+def test_spo2_jacobi_oracle_matches_reference():
+    from oracle import spo
+    g = load_golden("spo2_jacobi_32")
+    a, b = g["inertia"]
+    eKx, eKy = spo.jacobi_ops(g["x"], g["y"], 1.0, lambda r: a + b * r ** 2, float(g["dt"]))
+    assert relerr(eKx, g["exp_Kx"]) < TOL
+    assert relerr(eKy, g["exp_Ky"]) < TOL
+    n = len(g["x"])
+    v = np.zeros((n, n, 2, 2))
+    v[:, :, 0, 0], v[:, :, 1, 1] = g["v0"], g["v1"]
+    v[:, :, 0, 1] = v[:, :, 1, 0] = g["coupling"]
+    eVh, _ = spo.spo2_build(g["x"], g["y"], v, [1.0, 1.0], float(g["dt"]))
+    pl, _ = spo.spo2_strang_run(eVh, spo.keo_jacobi(eKx, eKy), g["psi0"], int(g["nt"]), int(g["nout"]))
+    assert relerr(np.array(pl), g["psilist"]) < TOL

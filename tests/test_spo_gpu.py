@@ -135,3 +135,43 @@ def test_spo3_example_size_vs_oracle():
     ref, psi = ospo.spo3_run(sol.exp_V_half, sol.exp_K, psi0, 4, 2)
     assert relerr(np.array(r.psilist), np.array(ref)) < TOL
     assert abs(np.vdot(r.psi, r.psi).real / np.vdot(psi0, psi0).real - 1) < 1e-12
+
+
+@pytest.mark.parametrize("return_states", [True, False])
+def test_spo2nh_matches_reference(return_states):
+    """SPO2NH (complex potential): Strang and merged step structures (qd_spo2_run_ex)."""
+    from pyqed_amd import SPO2NH
+    g = load_golden("spo2nh_32")
+    tag = "strang" if return_states else "merged"
+    sol = SPO2NH(g["x"], g["y"], mass=[1.0, 1.0], nstates=2)
+    sol.set_dpes(g["v"])
+    r = sol.run(g["psi0"], dt=float(g["dt"]), nt=int(g["nt"]), nout=int(g["nout"]), return_states=return_states)
+    assert relerr(sol.exp_V_half, g["exp_V_half"]) < 1e-12
+    assert relerr(np.array(r.psilist), g[f"{tag}_psilist"]) < 1e-11
+    assert relerr(r.psi, g[f"{tag}_psi"]) < 1e-11
+
+
+def test_spo2_jacobi_matches_reference():
+    """SPO2 coords='jacobi': row-dependent k_y factor after FFT_y (qd_spo2_run_ex, expKy)."""
+    from pyqed_amd import SPO2
+    g = load_golden("spo2_jacobi_32")
+    a, b = g["inertia"]
+    sol = SPO2(g["x"], g["y"], mass=[1.0, lambda r: a + b * r ** 2], nstates=2, coords='jacobi')
+    sol.set_DPES([g["v0"], g["v1"]], [[[0, 1], g["coupling"]]])
+    r = sol.run(g["psi0"], dt=float(g["dt"]), nt=int(g["nt"]), nout=int(g["nout"]))
+    assert relerr(sol.exp_Ky, g["exp_Ky"]) < 1e-12
+    assert relerr(np.array(r.psilist), g["psilist"]) < 1e-11
+
+
+def test_spo2_merged_equals_strang_unitary():
+    """For a Hermitian potential the merged structure equals Strang up to rounding (V/2 V/2 = V)."""
+    from pyqed_amd import SPO2
+    g = load_golden("spo2_32")
+    n = len(g["x"])
+    out = {}
+    for rs in (True, False):
+        sol = SPO2(g["x"], g["y"], mass=list(g["masses"]), nstates=2)
+        sol.set_DPES([g["v0"], g["v1"]], [[[0, 1], g["coupling"]]])
+        out[rs] = sol.run(g["psi0"], dt=float(g["dt"]), nt=8, nout=4, return_states=rs).psi
+    assert out[True].shape == (n, n, 2)
+    assert relerr(out[False], out[True]) < 1e-12
