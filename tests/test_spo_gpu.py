@@ -164,14 +164,15 @@ def test_spo2_jacobi_matches_reference():
 
 
 def test_spo2_merged_equals_strang_unitary():
-    """For a Hermitian potential the merged structure equals Strang up to rounding (V/2 V/2 = V)."""
+    """For a Hermitian potential the merged structure V/2 (K V)^n K V/2 equals n + 1 Strang steps up to
+    rounding (V/2 V/2 = V)."""
     from pyqed_amd import SPO2
     g = load_golden("spo2_32")
     n = len(g["x"])
     out = {}
-    for rs in (True, False):
+    for rs, nt, nout in ((True, 9, 1), (False, 8, 4)):
         sol = SPO2(g["x"], g["y"], mass=list(g["masses"]), nstates=2)
         sol.set_DPES([g["v0"], g["v1"]], [[[0, 1], g["coupling"]]])
-        out[rs] = sol.run(g["psi0"], dt=float(g["dt"]), nt=8, nout=4, return_states=rs).psi
+        out[rs] = sol.run(g["psi0"], dt=float(g["dt"]), nt=nt, nout=nout, return_states=rs).psi
     assert out[True].shape == (n, n, 2)
     assert relerr(out[False], out[True]) < 1e-12
