@@ -92,14 +92,14 @@ __device__ __forceinline__ void cg_compute_tile(const CgLds<BT>& L, int buf, CgA
   }
 }
 
-// Accumulate sum_s A_s * B_s over nseg segments of depth K (K % 16 == 0) into
-// a zero-initialised accumulator.  All threads of the workgroup must call it.
-// `segs` should live in LDS (or be uniform): it is indexed at run time, and a
-// private array indexed at run time would be placed in scratch memory.
-// Ends with a workgroup barrier, so LDS may be reused immediately after.
-template <int BT>
-__device__ __forceinline__ void cg_block_gemm(const CgSeg* segs, int nseg, int K, int lda, int ldb, CgLds<BT>& L,
-                                              CgAcc<BT>& acc) {
+// Generic engine: T K-tiles; the operand tiles come from two policies with
+//   Raw fetch(int t, int e, int q)           issued one tile ahead (global loads in flight during MFMA)
+//   cg_v2 finish(const Raw&, int t, int e, int q)  run just before the LDS store (after the MFMA work)
+// where e = tid + CG_WG*q is the element of the tile this thread stages (A: row e>>4, col e&15;
+// B: row e/BT, col e%BT) and q < cg_nld<BT>() its compile-time slot.  A policy may fetch inputs and compute the operand in finish (generated operands).
+// All threads of the workgroup must call it.  Ends with a workgroup barrier.
+template <int BT, typename APol, typename BPol>
+__device__ __forceinline__ void cg_block_gemm_gen(int T, APol& pa, BPol& pb, CgLds<BT>& L, CgAcc<BT>& acc) {
   constexpr int MW = CgCfg<BT>::MW, NW = CgCfg<BT>::NW, WC = CgCfg<BT>::WC, WR = CgCfg<BT>::WR;
   const int wave = threadIdx.x >> 6;
   const bool active = wave < WR * WC;
@@ -113,40 +113,74 @@ __device__ __forceinline__ void cg_block_gemm(const CgSeg* segs, int nseg, int K
       acc.im[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
     }
   constexpr int NLD = cg_nld<BT>();
-  const int tiles_per_seg = K / CG_KT;
-  const int T = nseg * tiles_per_seg;
   int tid = threadIdx.x;
   asm volatile("" : "+v"(tid));  // staging address math stays per call (see cg_epilogue)
-  // per-thread element offsets inside a tile (A: BT rows x 16, B: 16 rows x BT)
-  cg_v2 ra[NLD], rb[NLD];
+  typename APol::Raw ra[NLD];
+  typename BPol::Raw rb[NLD];
   auto load = [&](int t) {
-    const CgSeg sg = segs[t / tiles_per_seg];
-    const int k0 = (t % tiles_per_seg) * CG_KT;
 #pragma unroll
     for (int q = 0; q < NLD; ++q) {
       const int e = tid + CG_WG * q;
-      ra[q] = cg_ld(sg.A + (size_t)(e >> 4) * lda + k0 + (e & 15));
-      rb[q] = cg_ld(sg.B + (size_t)(k0 + e / BT) * ldb + (e % BT));
+      ra[q] = pa.fetch(t, e, q);
+      rb[q] = pb.fetch(t, e, q);
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int t, int buf) {
 #pragma unroll
     for (int q = 0; q < NLD; ++q) {
       const int e = tid + CG_WG * q;
-      cg_st_lds(&L.a[buf][(e >> 4) * CG_SA + (e & 15)], ra[q]);
-      cg_st_lds(&L.b[buf][e], rb[q]);
+      cg_st_lds(&L.a[buf][(e >> 4) * CG_SA + (e & 15)], pa.finish(ra[q], t, e, q));
+      cg_st_lds(&L.b[buf][e], pb.finish(rb[q], t, e, q));
     }
   };
   load(0);
-  store(0);
+  store(0, 0);
   __syncthreads();
   for (int t = 0; t < T; ++t) {
     const bool more = (t + 1) < T;
     if (more) load(t + 1);
     if (active) cg_compute_tile<BT>(L, t & 1, acc, wr0, wc0);
-    if (more) store((t + 1) & 1);
+    if (more) store(t + 1, (t + 1) & 1);
     __syncthreads();
   }
+}
+
+// Policies that read row-major complex tiles from memory through segment tables in LDS.
+template <int BT>
+struct CgSegA {
+  using Raw = cg_v2;
+  const CgSeg* segs;
+  int tps, lda;
+  __device__ __forceinline__ Raw fetch(int t, int e, int) const {
+    const CgSeg sg = segs[t / tps];
+    return cg_ld(sg.A + (size_t)(e >> 4) * lda + (t % tps) * CG_KT + (e & 15));
+  }
+  __device__ __forceinline__ cg_v2 finish(const Raw& r, int, int, int) const { return r; }
+};
+template <int BT>
+struct CgSegB {
+  using Raw = cg_v2;
+  const CgSeg* segs;
+  int tps, ldb;
+  __device__ __forceinline__ Raw fetch(int t, int e, int) const {
+    const CgSeg sg = segs[t / tps];
+    return cg_ld(sg.B + (size_t)((t % tps) * CG_KT + e / BT) * ldb + (e % BT));
+  }
+  __device__ __forceinline__ cg_v2 finish(const Raw& r, int, int, int) const { return r; }
+};
+
+// Accumulate sum_s A_s * B_s over nseg segments of depth K (K % 16 == 0) into
+// a zero-initialised accumulator.  All threads of the workgroup must call it.
+// `segs` should live in LDS (or be uniform): it is indexed at run time, and a
+// private array indexed at run time would be placed in scratch memory.
+// Ends with a workgroup barrier, so LDS may be reused immediately after.
+template <int BT>
+__device__ __forceinline__ void cg_block_gemm(const CgSeg* segs, int nseg, int K, int lda, int ldb, CgLds<BT>& L,
+                                              CgAcc<BT>& acc) {
+  const int tps = K / CG_KT;
+  CgSegA<BT> pa{segs, tps, lda};
+  CgSegB<BT> pb{segs, tps, ldb};
+  cg_block_gemm_gen<BT>(nseg * tps, pa, pb, L, acc);
 }
 
 // Visit every accumulator element: f(row, col, value) with row/col inside the block.

@@ -143,17 +143,20 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) 
   const int ee = e < ns2 ? e : 0;           // padding lanes shadow element 0
   const c128* X = p.xin + (live ? (grp - n) * ns2 : 0);
 
-  // round trip 1: indices, coefficients, own element, H/Q into LDS
-  int im[KMAX], ip[KMAX];
+  // round trip 1: indices, coefficients, modes, own element, the RK4 state of this element,
+  // and H/Q into LDS -- all independent loads, issued together
+  int im[KMAX], ip[KMAX], md[KMAX];
   c128 cf[KMAX][3];
 #pragma unroll
   for (int k = 0; k < KMAX; ++k) {
     im[k] = -1;
     ip[k] = -1;
+    md[k] = 0;
     cf[k][0] = cf[k][1] = cf[k][2] = cmk(0, 0);
     if (live && k < K) {
       im[k] = p.minus[(size_t)n * K + k];
       ip[k] = p.plus[(size_t)n * K + k];
+      md[k] = p.mode[k];
       const c128* c = p.coef + ((size_t)n * K + k) * 3;
       cf[k][0] = c[0];
       cf[k][1] = c[1];
@@ -162,6 +165,9 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) 
   }
   const c128 own = live ? X[(size_t)n * ns2 + ee] : cmk(0, 0);
   const c128 dmp = live ? p.damp[n] : cmk(0, 0);
+  const size_t idx = grp * ns2 + e;
+  const c128 r0 = valid ? p.rho[idx] : cmk(0, 0);
+  const c128 a0 = (valid && p.stage > 0) ? p.acc[idx] : cmk(0, 0);
   for (int q = threadIdx.x; q < ns2; q += blockDim.x)
     sH[q] = p.Hdip ? cadd(p.H[q], cmul(p.Hdip[q], p.fs)) : p.H[q];
   for (int q = threadIdx.x; q < p.nmod * ns2; q += blockDim.x)
@@ -189,7 +195,7 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) 
 #pragma unroll
   for (int k = 0; k < KMAX; ++k) {
     if (k >= K) break;
-    const c128* Qm = sQ + p.mode[k] * ns2;
+    const c128* Qm = sQ + md[k] * ns2;
     if (im[k] >= 0) {
       c128 qy = cmk(0, 0), yq = cmk(0, 0);
       for (int l = 0; l < ns; ++l) {
@@ -207,20 +213,18 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) 
   }
   if (!valid) return;
 
-  const size_t idx = grp * ns2 + e;
   const double dt = p.dt;
-  const c128 r0 = p.rho[idx];
   if (p.stage == 0) {
     p.acc[idx] = d;
     p.xout[idx] = cadd(r0, cscale(d, dt / 2));
   } else if (p.stage == 1) {
-    p.acc[idx] = cadd(p.acc[idx], cscale(d, 2.0));
+    p.acc[idx] = cadd(a0, cscale(d, 2.0));
     p.xout[idx] = cadd(r0, cscale(d, dt / 2));
   } else if (p.stage == 2) {
-    p.acc[idx] = cadd(p.acc[idx], cscale(d, 2.0));
+    p.acc[idx] = cadd(a0, cscale(d, 2.0));
     p.xout[idx] = cadd(r0, cscale(d, dt));
   } else {
-    const c128 a = cadd(p.acc[idx], d);
+    const c128 a = cadd(a0, d);
     const c128 r1 = cadd(r0, cscale(cscale(a, dt), 1.0 / 6.0));
     p.rho_out[idx] = r1;
     if (p.snap && n == 0) {

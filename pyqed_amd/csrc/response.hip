@@ -90,26 +90,31 @@ __global__ void cube_out_kernel(const c128* alpha, const c128* lam, const c128* 
 }
 
 // ---------------------------------------------------------------- ensemble 2D slice
-// X [n3p][Kp]: X[i][m*nL+p] = i * alpha_mp e^{lam_mp t3_i}  (zero in the padding)
-__global__ void ens_x_kernel(const c128* alpha, const c128* lam, int M, int nL, const double* t3, int n3, int n3p,
-                             int Kp, c128* X) {
-  const size_t tot = (size_t)n3p * Kp;
-  const int K = M * nL;
-  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
-    const int kk = (int)(e % Kp), i = (int)(e / Kp);
-    c128 v = cmk(0, 0);
-    if (i < n3 && kk < K) v = cmuli(cmul(alpha[kk], cexp_t(lam[kk], t3[i])));
-    X[e] = v;
-  }
-}
-
+// One launch builds both GEMM operands (two bandwidth-bound writes of n x K c128 overlap):
+//   blockIdx.y <  M : Z rows of member m (below)
+//   blockIdx.y >= M : X [n3p][Kp], X[i][m*nL+p] = i * alpha_mp e^{lam_mp t3_i} (zero in the padding),
+//                     grid-strided over the (blockIdx.y - M, blockIdx.x) blocks
 // Z [Kp][n1p]: Z[m*nL+p][k] = sum_q Mt[m][p][q] y_q(k),  y_q(k) = beta[m][q] e^{lam_mq t1_k}
-// grid (ceil(n1p/256), M): one thread per t1 point computes the nL exponentials once
-// (registers, nL <= ZMAX) and emits the nL outputs of its column; Mt_m staged in LDS.
+// one thread per t1 point computes the nL exponentials once (registers, nL <= ZMAX) and emits the
+// nL outputs of its column; Mt_m staged in LDS.
 constexpr int ZMAX = 16;
-__global__ __launch_bounds__(256) void ens_z_kernel(const c128* Mt, const c128* beta, const c128* lam, int M, int nL,
-                                                    const double* t1, int n1, int n1p, int Kp, c128* Z) {
+__global__ __launch_bounds__(256) void ens_xz_kernel(const c128* Mt, const c128* beta, const c128* lam, int M, int nL,
+                                                     const double* t1, int n1, int n1p, int Kp, c128* Z,
+                                                     const c128* alpha, const double* t3, int n3, int n3p, int xrows,
+                                                     int K, c128* X) {
   __shared__ c128 sM[ZMAX * ZMAX];
+  if ((int)blockIdx.y >= M) {
+    const size_t tot = (size_t)n3p * Kp;
+    const size_t nthr = (size_t)xrows * gridDim.x * blockDim.x;
+    for (size_t e = ((size_t)(blockIdx.y - M) * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x; e < tot;
+         e += nthr) {
+      const int kk = (int)(e % Kp), i = (int)(e / Kp);
+      c128 v = cmk(0, 0);
+      if (i < n3 && kk < K) v = cmuli(cmul(alpha[kk], cexp_t(lam[kk], t3[i])));
+      X[e] = v;
+    }
+    return;
+  }
   const int m = blockIdx.y;
   const int k = blockIdx.x * 256 + threadIdx.x;
   for (int e = threadIdx.x; e < nL * nL; e += 256) sM[e] = Mt[(size_t)m * nL * nL + e];
@@ -156,22 +161,39 @@ __global__ void ens_z_generic_kernel(const c128* Mt, const c128* beta, const c12
 
 constexpr int ENS_BT = 128;
 
+// A operand X [n3p][Kp] (materialised by ens_xz_kernel), streamed one tile ahead.
+struct EnsXA {
+  using Raw = cg_v2;
+  const c128* X;
+  int Kp, row0, k0;
+  __device__ __forceinline__ Raw fetch(int t, int e, int) const {
+    return cg_ld(X + (size_t)(row0 + (e >> 4)) * Kp + k0 + t * CG_KT + (e & 15));
+  }
+  __device__ __forceinline__ cg_v2 finish(const Raw& r, int, int, int) const { return r; }
+};
+
+struct EnsZB {
+  using Raw = cg_v2;
+  const c128* Z;
+  int n1p, col0, k0;
+  __device__ __forceinline__ Raw fetch(int t, int e, int) const {
+    return cg_ld(Z + (size_t)(k0 + t * CG_KT + e / ENS_BT) * n1p + col0 + (e % ENS_BT));
+  }
+  __device__ __forceinline__ cg_v2 finish(const Raw& r, int, int, int) const { return r; }
+};
+
 // grid: (n1p/BT) x (n3p/BT) x S ; each workgroup accumulates K-tiles [t0, t1) of its block
-__global__ __launch_bounds__(CG_WG) void ens_gemm_kernel(const c128* X, const c128* Z, int Kp, int n1p, int tiles,
+__global__ __launch_bounds__(CG_WG) void ens_gemm_kernel(const c128* X, int Kp, const c128* Z, int n1p, int tiles,
                                                          int S, c128* slabs, int n3p) {
   __shared__ CgLds<ENS_BT> L;
   const int bn = blockIdx.x, bm = blockIdx.y, s = blockIdx.z;
   const int t0 = (int)((long)tiles * s / S), t1 = (int)((long)tiles * (s + 1) / S);
   CgAcc<ENS_BT> A;
-  __shared__ CgSeg seg[1];
-  if (threadIdx.x == 0) {
-    seg[0].A = X + (size_t)bm * ENS_BT * Kp + (size_t)t0 * CG_KT;
-    seg[0].B = Z + (size_t)t0 * CG_KT * n1p + (size_t)bn * ENS_BT;
-  }
-  __syncthreads();
   c128* slab = slabs + (size_t)s * n3p * n1p;
   if (t1 > t0) {
-    cg_block_gemm<ENS_BT>(seg, 1, (t1 - t0) * CG_KT, Kp, n1p, L, A);
+    EnsXA pa{X, Kp, bm * ENS_BT, t0 * CG_KT};
+    EnsZB pb{Z, n1p, bn * ENS_BT, t0 * CG_KT};
+    cg_block_gemm_gen<ENS_BT>(t1 - t0, pa, pb, L, A);
     cg_epilogue<ENS_BT>(A, [&](int row, int col, c128 v) {
       slab[(size_t)(bm * ENS_BT + row) * n1p + bn * ENS_BT + col] = v;
     });
@@ -263,8 +285,9 @@ extern "C" int qd_response2d_ensemble(const qd_c128* alpha, const qd_c128* Mt, c
   const int tiles = ceil_div(K, CG_KT);
   const int Kp = tiles * CG_KT;
   const int blocks2d = (n3p / BT) * (n1p / BT);
-  // split K so that the grid covers >= 256 CUs, with >= 4 K-tiles per workgroup
-  int S = std::max(1, std::min(ceil_div(512, blocks2d), std::max(1, tiles / 4)));
+  // split K so that the grid covers the 256 CUs once (one 512-thread workgroup per CU), with
+  // >= 4 K-tiles per workgroup; fewer splits = fewer partial slabs to write and reduce
+  int S = std::max(1, std::min(ceil_div(256, blocks2d), std::max(1, tiles / 4)));
   const size_t nx = (size_t)n3p * Kp, nz = (size_t)Kp * n1p, nsl = (size_t)S * n3p * n1p;
   void* w = nullptr;
   int rc = workspace(WS_2DES, (nx + nz + nsl) * sizeof(c128), &w);
@@ -272,24 +295,27 @@ extern "C" int qd_response2d_ensemble(const qd_c128* alpha, const qd_c128* Mt, c
   c128* X = (c128*)w;
   c128* Z = X + nx;
   c128* slabs = Z + nz;
-  hipLaunchKernelGGL(ens_x_kernel, dim3(grid_for(nx, 256)), dim3(256), 0, st, (const c128*)alpha, (const c128*)lam, M,
-                     nL, t3, n3, n3p, Kp, X);
-  QD_HIP(hipGetLastError());
-  if (nL <= ZMAX && M <= 65535) {
-    hipLaunchKernelGGL(ens_z_kernel, dim3(n1p / 256 + (n1p % 256 != 0), M), dim3(256), 0, st, (const c128*)Mt,
-                       (const c128*)beta, (const c128*)lam, M, nL, t1, n1, n1p, Kp, Z);
+  const int zbx = n1p / 256 + (n1p % 256 != 0);
+  if (nL <= ZMAX && M <= 65535 - 4096) {
+    // X gets as many block rows as Z has (capped), so both halves of the launch move similar bytes
+    const int xrows = std::max(1, std::min(M, 4096));
+    hipLaunchKernelGGL(ens_xz_kernel, dim3(zbx, M + xrows), dim3(256), 0, st, (const c128*)Mt, (const c128*)beta,
+                       (const c128*)lam, M, nL, t1, n1, n1p, Kp, Z, (const c128*)alpha, t3, n3, n3p, xrows, K, X);
     QD_HIP(hipGetLastError());
     if (Kp > K) {
       hipLaunchKernelGGL(ens_z_pad_kernel, dim3(64), dim3(256), 0, st, K, Kp, n1p, Z);
       QD_HIP(hipGetLastError());
     }
   } else {
+    hipLaunchKernelGGL(ens_xz_kernel, dim3(zbx, 4096), dim3(256), 0, st, (const c128*)Mt, (const c128*)beta,
+                       (const c128*)lam, 0, nL, t1, n1, n1p, Kp, Z, (const c128*)alpha, t3, n3, n3p, 4096, K, X);
+    QD_HIP(hipGetLastError());
     hipLaunchKernelGGL(ens_z_generic_kernel, dim3(grid_for(nz, 256)), dim3(256), 0, st, (const c128*)Mt,
                        (const c128*)beta, (const c128*)lam, M, nL, t1, n1, n1p, Kp, Z);
     QD_HIP(hipGetLastError());
   }
-  hipLaunchKernelGGL(ens_gemm_kernel, dim3(n1p / BT, n3p / BT, S), dim3(CG_WG), 0, st, X, Z, Kp, n1p, tiles, S, slabs,
-                     n3p);
+  hipLaunchKernelGGL(ens_gemm_kernel, dim3(n1p / BT, n3p / BT, S), dim3(CG_WG), 0, st, X, Kp, Z, n1p, tiles, S,
+                     slabs, n3p);
   QD_HIP(hipGetLastError());
   hipLaunchKernelGGL(ens_reduce_kernel, dim3(grid_for((size_t)n3 * n1, 256)), dim3(256), 0, st, slabs, S, n3, n1, n3p,
                      n1p, (c128*)out, accumulate);

@@ -144,3 +144,25 @@ def test_superop_batch_vs_glf():
     rho = torch.from_numpy(rho0.copy()).to(dev)
     lindblad_rk4(torch.from_numpy(H).to(dev), torch.from_numpy(np.array(cs)).to(dev), rho, 0.01, 20)
     assert relerr(v.cpu().numpy().reshape(B, N, N), rho.cpu().numpy()) < 1e-12
+
+
+@pytest.mark.parametrize("M,nL,n3,n1", [(3, 20, 70, 40), (5, 9, 130, 257)])
+def test_ensemble_slice_formula_generic_sizes(M, nL, n3, n1):
+    """Direct evaluation of S[i,k] = (-i)^3 sum_m sum_pq alpha_mp e^{lam_mp t3_i} Mt_mpq beta_mq e^{lam_mq t1_k}:
+    nL > 16 takes the generic Z path; ragged n3/n1 exercise the block padding."""
+    from pyqed_amd.response import response2d_ensemble
+    rng = np.random.default_rng(nL)
+    lam = -rng.uniform(0.01, 0.2, (M, nL)) + 1j * rng.uniform(-2, 2, (M, nL))
+    alpha = rng.standard_normal((M, nL)) + 1j * rng.standard_normal((M, nL))
+    beta = rng.standard_normal((M, nL)) + 1j * rng.standard_normal((M, nL))
+    Mt = rng.standard_normal((M, nL, nL)) + 1j * rng.standard_normal((M, nL, nL))
+    t3 = 0.3 * np.arange(n3)
+    t1 = 0.25 * np.arange(n1)
+    ref = np.zeros((n3, n1), complex)
+    for m in range(M):
+        X = alpha[m][None, :] * np.exp(np.outer(t3, lam[m]))
+        Z = (Mt[m] * beta[m][None, :]) @ np.exp(np.outer(lam[m], t1))
+        ref += X @ Z
+    ref *= (-1j) ** 3
+    S = response2d_ensemble(lam, alpha, Mt, beta, t3, t1).cpu().numpy()
+    assert relerr(S, ref) < 1e-12
