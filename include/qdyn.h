@@ -292,6 +292,18 @@ int qd_response2d_ensemble(const qd_c128* alpha, const qd_c128* Mt,
                            int n1, qd_c128* out, int accumulate, void* stream);
 
 /*
+ * qd_response2d_ensemble on uniform grids t3_i = t3_0 + i dt3, t1_k = t1_0 + k dt1 (the
+ * 2DES case, e.g. 0.5*arange(256)): the exponentials come from two-level tables
+ * (a few transcendentals per 16-64 outputs), relative error ~1e-14 against direct
+ * exponentials.  nL <= 16, n1 <= 1024.
+ */
+int qd_response2d_ensemble_uniform(const qd_c128* alpha, const qd_c128* Mt,
+                                   const qd_c128* beta, const qd_c128* lam, int M,
+                                   int nL, double t3_0, double dt3, int n3,
+                                   double t1_0, double dt1, int n1, qd_c128* out,
+                                   int accumulate, void* stream);
+
+/*
  * Frequency-domain pole sum out[i] = sum_n -coeff_n / (lam_n + i w_i)
  * (Lindblad_solver.correlation_2op_1w / 3op_1w, pyqed/superoperator.py:603-700).
  */

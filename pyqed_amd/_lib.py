@@ -56,6 +56,9 @@ SIGNATURES = {
     "qd_sos_propagator": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]),
     "qd_response_cube": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
                                  c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]),
+    "qd_response2d_ensemble_uniform": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double,
+                                               c_double, c_int, c_double, c_double, c_int, c_void_p, c_int,
+                                               c_void_p]),
     "qd_response2d_ensemble": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int,
                                        c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "qd_resolvent_sum": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]),

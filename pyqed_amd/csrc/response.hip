@@ -134,6 +134,76 @@ __global__ __launch_bounds__(256) void ens_xz_kernel(const c128* Mt, const c128*
   }
 }
 
+// ---- uniform time grids (t = t0 + j dt): exponentials from two-level tables,
+// e^{lam (t0 + (16 l + j) dt)} = e^{lam (t0 + 16 l dt)} * e^{lam j dt}; the coarse factor is a direct
+// exponential, the fine table a product chain of e^{lam dt} (<= 15 products).  A handful of
+// transcendentals per 16-64 outputs instead of one per output; relative error ~1e-14.
+constexpr int UNI_ROWS = 64;  // X rows per block
+__device__ __forceinline__ void ens_x_uniform_block(int bx, int by, const c128* alpha, const c128* lam, int K, int Kp,
+                                                    double t0, double dt, int n3, int n3p, c128* X) {
+  const int kk = bx * 256 + threadIdx.x;
+  const int i0 = by * UNI_ROWS;
+  if (kk >= Kp) return;
+  const bool col = kk < K;
+  const c128 l = col ? lam[kk] : cmk(0, 0);
+  const c128 a = col ? cmuli(alpha[kk]) : cmk(0, 0);
+  c128 T1[16];
+  T1[0] = cmk(1, 0);
+  const c128 st = cexp_t(l, dt);
+#pragma unroll
+  for (int j = 1; j < 16; ++j) T1[j] = cmul(T1[j - 1], st);
+  for (int g = 0; g < UNI_ROWS / 16; ++g) {
+    const int ib = i0 + 16 * g;
+    const c128 base = cmul(a, cexp_t(l, t0 + (double)ib * dt));
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int i = ib + j;
+      if (i >= n3p) break;
+      X[(size_t)i * Kp + kk] = (col && i < n3) ? cmul(base, T1[j]) : cmk(0, 0);
+    }
+  }
+}
+
+// Z rows of member m = blockIdx.y, uniform t1: tables of e^{lam_q t} in LDS (nL x (16 + n1p/16)).
+constexpr int UNI_MAXC = 1024 / 16;
+// One launch, both operands: blockIdx.y < M -> Z rows of member blockIdx.y (blockIdx.x = column
+// block); blockIdx.y >= M -> X block (blockIdx.y - M) in a (Kp/256) x (n3p/UNI_ROWS) tiling.
+__global__ __launch_bounds__(256) void ens_xz_uniform_kernel(const c128* Mt, const c128* beta, const c128* lam, int M,
+                                                             int nL, double t0, double dt, int n1, int n1p, int Kp,
+                                                             c128* Z, const c128* alpha, int K, double t3_0,
+                                                             double dt3, int n3, int n3p, int xbx, c128* X) {
+  __shared__ c128 sM[ZMAX * ZMAX];
+  __shared__ c128 sF[ZMAX * 16];        // e^{lam_q j dt}
+  __shared__ c128 sC[ZMAX * UNI_MAXC];  // beta_q e^{lam_q (t0 + 16 l dt)}
+  if ((int)blockIdx.y >= M) {
+    if (blockIdx.x != 0) return;
+    const int xb = blockIdx.y - M;
+    ens_x_uniform_block(xb % xbx, xb / xbx, alpha, lam, K, Kp, t3_0, dt3, n3, n3p, X);
+    return;
+  }
+  const int m = blockIdx.y;
+  const int nC = n1p / 16;
+  const c128* lm = lam + (size_t)m * nL;
+  for (int e = threadIdx.x; e < nL * nL; e += 256) sM[e] = Mt[(size_t)m * nL * nL + e];
+  for (int e = threadIdx.x; e < nL * 16; e += 256) sF[e] = cexp_t(lm[e / 16], (double)(e % 16) * dt);
+  for (int e = threadIdx.x; e < nL * nC; e += 256)
+    sC[e] = cmul(beta[(size_t)m * nL + e / nC], cexp_t(lm[e / nC], t0 + 16.0 * (double)(e % nC) * dt));
+  __syncthreads();
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= n1p) return;
+  c128 y[ZMAX];
+#pragma unroll
+  for (int q = 0; q < ZMAX; ++q)
+    y[q] = (q < nL && k < n1) ? cmul(sC[q * nC + (k >> 4)], sF[q * 16 + (k & 15)]) : cmk(0, 0);
+  for (int p = 0; p < nL; ++p) {
+    c128 v = cmk(0, 0);
+#pragma unroll
+    for (int q = 0; q < ZMAX; ++q)
+      if (q < nL) v = cadd(v, cmul(sM[p * nL + q], y[q]));
+    Z[((size_t)m * nL + p) * n1p + k] = v;
+  }
+}
+
 // rows K..Kp-1 of Z are padding
 __global__ void ens_z_pad_kernel(int K, int Kp, int n1p, c128* Z) {
   const size_t tot = (size_t)(Kp - K) * n1p;
@@ -272,12 +342,15 @@ extern "C" int qd_response_cube(const qd_c128* alpha, const qd_c128* B, const qd
   return QD_OK;
 }
 
-extern "C" int qd_response2d_ensemble(const qd_c128* alpha, const qd_c128* Mt, const qd_c128* beta,
-                                      const qd_c128* lam, int M, int nL, const double* t3, int n3, const double* t1,
-                                      int n1, qd_c128* out, int accumulate, void* stream) {
-  QD_CHECK_ARG(alpha && Mt && beta && lam && t3 && t1 && out, "qd_response2d_ensemble: null pointer");
-  QD_CHECK_ARG(M >= 1 && nL >= 1 && n3 >= 1 && n1 >= 1, "qd_response2d_ensemble: bad sizes");
-  QD_CHECK_ARG((long)M * nL < (1L << 30) && M < 65536 * 1024, "qd_response2d_ensemble: M*nL too large");
+namespace {
+// Shared driver.  Time grids are either device arrays (t3 / t1) or uniform (t0 + j dt, when the
+// array pointer is null): the uniform form builds the GEMM operands from exponential tables.
+int ens_run(const char* fn, const qd_c128* alpha, const qd_c128* Mt, const qd_c128* beta, const qd_c128* lam, int M,
+            int nL, const double* t3, double t3_0, double dt3, int n3, const double* t1, double t1_0, double dt1,
+            int n1, qd_c128* out, int accumulate, void* stream) {
+  QD_CHECK_ARG(alpha && Mt && beta && lam && out, "%s: null pointer", fn);
+  QD_CHECK_ARG(M >= 1 && nL >= 1 && n3 >= 1 && n1 >= 1, "%s: bad sizes", fn);
+  QD_CHECK_ARG((long)M * nL < (1L << 30) && M < 65536 * 1024, "%s: M*nL too large", fn);
   hipStream_t st = (hipStream_t)stream;
   const int BT = ENS_BT;
   const int n3p = ceil_div(n3, BT) * BT, n1p = ceil_div(n1, BT) * BT;
@@ -296,23 +369,59 @@ extern "C" int qd_response2d_ensemble(const qd_c128* alpha, const qd_c128* Mt, c
   c128* Z = X + nx;
   c128* slabs = Z + nz;
   const int zbx = n1p / 256 + (n1p % 256 != 0);
-  if (nL <= ZMAX && M <= 65535 - 4096) {
-    // X gets as many block rows as Z has (capped), so both halves of the launch move similar bytes
-    const int xrows = std::max(1, std::min(M, 4096));
-    hipLaunchKernelGGL(ens_xz_kernel, dim3(zbx, M + xrows), dim3(256), 0, st, (const c128*)Mt, (const c128*)beta,
-                       (const c128*)lam, M, nL, t1, n1, n1p, Kp, Z, (const c128*)alpha, t3, n3, n3p, xrows, K, X);
+  const bool zfast = nL <= ZMAX && M <= 65535 - 4096;
+  const int xbx = ceil_div(Kp, 256), xblocks = xbx * (n3p / UNI_ROWS);
+  if (!t1 && zfast && n1p <= 16 * UNI_MAXC) {
+    // Z (uniform t1) and, when t3 is uniform too, X in the same launch (separately if the grid
+    // would exceed 65535 block rows)
+    const bool xin = !t3 && (long)M + xblocks <= 65535;
+    hipLaunchKernelGGL(ens_xz_uniform_kernel, dim3(zbx, M + (xin ? xblocks : 0)), dim3(256), 0, st, (const c128*)Mt,
+                       (const c128*)beta, (const c128*)lam, M, nL, t1_0, dt1, n1, n1p, Kp, Z, (const c128*)alpha, K,
+                       t3_0, dt3, n3, n3p, xbx, X);
     QD_HIP(hipGetLastError());
+    if (!t3 && !xin) {
+      hipLaunchKernelGGL(ens_xz_uniform_kernel, dim3(1, xblocks), dim3(256), 0, st, (const c128*)Mt,
+                         (const c128*)beta, (const c128*)lam, 0, nL, 0.0, 0.0, n1, n1p, Kp, Z, (const c128*)alpha, K,
+                         t3_0, dt3, n3, n3p, xbx, X);
+      QD_HIP(hipGetLastError());
+    }
     if (Kp > K) {
       hipLaunchKernelGGL(ens_z_pad_kernel, dim3(64), dim3(256), 0, st, K, Kp, n1p, Z);
       QD_HIP(hipGetLastError());
     }
+    if (t3) {  // X from the array (X part of the combined kernel only)
+      hipLaunchKernelGGL(ens_xz_kernel, dim3(zbx, 4096), dim3(256), 0, st, (const c128*)Mt, (const c128*)beta,
+                         (const c128*)lam, 0, nL, t1, n1, n1p, Kp, Z, (const c128*)alpha, t3, n3, n3p, 4096, K, X);
+      QD_HIP(hipGetLastError());
+    }
   } else {
-    hipLaunchKernelGGL(ens_xz_kernel, dim3(zbx, 4096), dim3(256), 0, st, (const c128*)Mt, (const c128*)beta,
-                       (const c128*)lam, 0, nL, t1, n1, n1p, Kp, Z, (const c128*)alpha, t3, n3, n3p, 4096, K, X);
-    QD_HIP(hipGetLastError());
-    hipLaunchKernelGGL(ens_z_generic_kernel, dim3(grid_for(nz, 256)), dim3(256), 0, st, (const c128*)Mt,
-                       (const c128*)beta, (const c128*)lam, M, nL, t1, n1, n1p, Kp, Z);
-    QD_HIP(hipGetLastError());
+    QD_CHECK_ARG(t1, "%s: uniform t1 needs nL <= %d and n1 <= %d", fn, ZMAX, 16 * UNI_MAXC);
+    if (!t3) {  // uniform t3 with an array t1: X blocks only
+      hipLaunchKernelGGL(ens_xz_uniform_kernel, dim3(1, xblocks), dim3(256), 0, st, (const c128*)Mt,
+                         (const c128*)beta, (const c128*)lam, 0, nL, 0.0, 0.0, n1, n1p, Kp, Z, (const c128*)alpha, K,
+                         t3_0, dt3, n3, n3p, xbx, X);
+      QD_HIP(hipGetLastError());
+    }
+    if (zfast) {
+      // X (when from an array) gets as many block rows as Z has (capped): one launch, both writes
+      const int xrows = t3 ? std::max(1, std::min(M, 4096)) : 0;
+      hipLaunchKernelGGL(ens_xz_kernel, dim3(zbx, M + xrows), dim3(256), 0, st, (const c128*)Mt, (const c128*)beta,
+                         (const c128*)lam, M, nL, t1, n1, n1p, Kp, Z, (const c128*)alpha, t3, n3, n3p, xrows, K, X);
+      QD_HIP(hipGetLastError());
+      if (Kp > K) {
+        hipLaunchKernelGGL(ens_z_pad_kernel, dim3(64), dim3(256), 0, st, K, Kp, n1p, Z);
+        QD_HIP(hipGetLastError());
+      }
+    } else {
+      if (t3) {
+        hipLaunchKernelGGL(ens_xz_kernel, dim3(zbx, 4096), dim3(256), 0, st, (const c128*)Mt, (const c128*)beta,
+                           (const c128*)lam, 0, nL, t1, n1, n1p, Kp, Z, (const c128*)alpha, t3, n3, n3p, 4096, K, X);
+        QD_HIP(hipGetLastError());
+      }
+      hipLaunchKernelGGL(ens_z_generic_kernel, dim3(grid_for(nz, 256)), dim3(256), 0, st, (const c128*)Mt,
+                         (const c128*)beta, (const c128*)lam, M, nL, t1, n1, n1p, Kp, Z);
+      QD_HIP(hipGetLastError());
+    }
   }
   hipLaunchKernelGGL(ens_gemm_kernel, dim3(n1p / BT, n3p / BT, S), dim3(CG_WG), 0, st, X, Kp, Z, n1p, tiles, S,
                      slabs, n3p);
@@ -321,6 +430,25 @@ extern "C" int qd_response2d_ensemble(const qd_c128* alpha, const qd_c128* Mt, c
                      n1p, (c128*)out, accumulate);
   QD_HIP(hipGetLastError());
   return QD_OK;
+}
+}  // namespace
+
+extern "C" int qd_response2d_ensemble(const qd_c128* alpha, const qd_c128* Mt, const qd_c128* beta,
+                                      const qd_c128* lam, int M, int nL, const double* t3, int n3, const double* t1,
+                                      int n1, qd_c128* out, int accumulate, void* stream) {
+  QD_CHECK_ARG(t3 && t1, "qd_response2d_ensemble: null time grid");
+  return ens_run("qd_response2d_ensemble", alpha, Mt, beta, lam, M, nL, t3, 0, 0, n3, t1, 0, 0, n1, out, accumulate,
+                 stream);
+}
+
+extern "C" int qd_response2d_ensemble_uniform(const qd_c128* alpha, const qd_c128* Mt, const qd_c128* beta,
+                                              const qd_c128* lam, int M, int nL, double t3_0, double dt3, int n3,
+                                              double t1_0, double dt1, int n1, qd_c128* out, int accumulate,
+                                              void* stream) {
+  QD_CHECK_ARG(nL <= ZMAX && n1 <= 16 * UNI_MAXC, "qd_response2d_ensemble_uniform: nL=%d (<= %d), n1=%d (<= %d)", nL,
+               ZMAX, n1, 16 * UNI_MAXC);
+  return ens_run("qd_response2d_ensemble_uniform", alpha, Mt, beta, lam, M, nL, nullptr, t3_0, dt3, n3, nullptr, t1_0,
+                 dt1, n1, out, accumulate, stream);
 }
 
 extern "C" int qd_resolvent_sum(const qd_c128* coeff, const qd_c128* lam, int n, const double* w, int nw,

@@ -88,19 +88,43 @@ def ensemble_factors(lam, U1, U2, supops, rho0v, t2):
     return alpha, Mt, beta
 
 
+def _uniform(t):
+    """(t0, dt) when the host grid t is uniform to 1e-13 relative (np.arange / linspace grids), else None."""
+    if isinstance(t, torch.Tensor):
+        return None
+    t = np.asarray(t, float).ravel()
+    if t.size == 1:
+        return float(t[0]), 0.0
+    dt = (t[-1] - t[0]) / (t.size - 1)
+    dev = np.max(np.abs(t - (t[0] + dt * np.arange(t.size))))
+    return (float(t[0]), float(dt)) if dev <= 1e-13 * max(np.max(np.abs(t)), 1.0) else None
+
+
 def response2d_ensemble(lam, alpha, Mt, beta, t3, t1, out=None, accumulate=False, device=None):
     """out[i, k] (+)= sum_m (t3_i, t1_k) slice of member m at fixed t2 (GPU, split-K MFMA GEMM).
 
-    lam, alpha, beta [M, nL], Mt [M, nL, nL] (numpy or device tensors)."""
+    lam, alpha, beta [M, nL], Mt [M, nL, nL] (numpy or device tensors).  Uniform host grids (the
+    2DES case) take qd_response2d_ensemble_uniform (exponential tables); others the array path."""
     dev = device or (out.device if out is not None else default_device())
     _lib.ensure_device(dev)
     lam_t, alpha_t, Mt_t, beta_t = (x if isinstance(x, torch.Tensor) else _t(x, dev) for x in (lam, alpha, Mt, beta))
     M, nL = alpha_t.shape
+    u3, u1 = _uniform(t3), _uniform(t1)
+    n3 = t3.numel() if isinstance(t3, torch.Tensor) else np.asarray(t3).size
+    n1 = t1.numel() if isinstance(t1, torch.Tensor) else np.asarray(t1).size
+    if out is None:
+        out = torch.empty((n3, n1), dtype=torch.complex128, device=dev)
+        accumulate = False
+    if u3 is not None and u1 is not None and nL <= 16 and n1 <= 1024:
+        with torch.cuda.device(dev):
+            rc = _lib.load().qd_response2d_ensemble_uniform(alpha_t.data_ptr(), Mt_t.data_ptr(), beta_t.data_ptr(),
+                                                            lam_t.data_ptr(), M, nL, u3[0], u3[1], n3, u1[0], u1[1],
+                                                            n1, out.data_ptr(), int(bool(accumulate)),
+                                                            _lib.stream_ptr(dev))
+        _lib.check(rc, "qd_response2d_ensemble_uniform")
+        return out
     t3t = t3 if isinstance(t3, torch.Tensor) else _t(np.asarray(t3, float), dev, torch.float64)
     t1t = t1 if isinstance(t1, torch.Tensor) else _t(np.asarray(t1, float), dev, torch.float64)
-    if out is None:
-        out = torch.empty((t3t.numel(), t1t.numel()), dtype=torch.complex128, device=dev)
-        accumulate = False
     with torch.cuda.device(dev):
         rc = _lib.load().qd_response2d_ensemble(alpha_t.data_ptr(), Mt_t.data_ptr(), beta_t.data_ptr(),
                                                 lam_t.data_ptr(), M, nL, t3t.data_ptr(), t3t.numel(),

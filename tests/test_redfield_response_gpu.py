@@ -166,3 +166,28 @@ def test_ensemble_slice_formula_generic_sizes(M, nL, n3, n1):
     ref *= (-1j) ** 3
     S = response2d_ensemble(lam, alpha, Mt, beta, t3, t1).cpu().numpy()
     assert relerr(S, ref) < 1e-12
+
+
+def test_ensemble_uniform_tables_vs_array_path():
+    """Uniform host grids take the exponential-table operand build; device-tensor grids take the direct
+    exponentials.  Same result to ~1e-14; a non-uniform grid stays on the array path."""
+    import torch
+    from pyqed_amd.response import _uniform, response2d_ensemble
+    rng = np.random.default_rng(11)
+    M, nL = 64, 9
+    lam = -rng.uniform(0.01, 0.2, (M, nL)) + 1j * rng.uniform(-2, 2, (M, nL))
+    alpha = rng.standard_normal((M, nL)) + 1j * rng.standard_normal((M, nL))
+    beta = rng.standard_normal((M, nL)) + 1j * rng.standard_normal((M, nL))
+    Mt = rng.standard_normal((M, nL, nL)) + 1j * rng.standard_normal((M, nL, nL))
+    t = 0.5 * np.arange(200)
+    assert _uniform(t) == (0.0, 0.5)
+    dev = torch.device("cuda", 0)
+    uni = response2d_ensemble(lam, alpha, Mt, beta, t, t).cpu().numpy()
+    arr = response2d_ensemble(lam, alpha, Mt, beta, torch.from_numpy(t).to(dev), torch.from_numpy(t).to(dev))
+    assert relerr(uni, arr.cpu().numpy()) < 1e-13
+    tn = np.sort(rng.uniform(0, 60, 150))
+    assert _uniform(tn) is None
+    S = response2d_ensemble(lam[:3], alpha[:3], Mt[:3], beta[:3], tn, t).cpu().numpy()
+    ref = sum((alpha[m][None, :] * np.exp(np.outer(tn, lam[m]))) @
+              ((Mt[m] * beta[m][None, :]) @ np.exp(np.outer(lam[m], t))) for m in range(3)) * (-1j) ** 3
+    assert relerr(S, ref) < 1e-12
