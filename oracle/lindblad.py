@@ -132,3 +132,24 @@ def lindblad_csr(H, rho0, c_ops, e_ops, Nt, dt):
         rho = rk4(rho, rhs, dt, H, c_ops)
         obs[k + 1, :] = [(e @ rho).diagonal().sum() for e in e_ops]
     return obs, rho
+
+
+def correlation_3p_1t(H, rho0, ops, c_ops, tlist):
+    """correlation.correlation_3p_1t (pyqed/correlation.py:17-70) with dyn = oqs.liouvillian.
+
+    rho <- C rho0 A (:41), then len(tlist) RK4 steps of dt = tlist[1]-tlist[0] (:50-57); after each
+    step t += dt and cor = Tr(B rho) (:59).  Returns (t [Nt], cor [Nt], rho_k [Nt,N,N]) -- the values
+    the reference writes to cor.dat / dm.dat (it returns None)."""
+    A, B, C = (np.asarray(o, complex) for o in ops)
+    H = np.asarray(H, complex)
+    c_ops = [np.asarray(c, complex) for c in c_ops]
+    rho = C @ (np.asarray(rho0, complex) @ A)
+    dt = tlist[1] - tlist[0]
+    t, ts, cor, rhos = 0.0, [], [], []
+    for _ in range(len(tlist)):
+        t += dt
+        rho = rk4(rho, liouvillian, dt, H, c_ops)
+        ts.append(t)
+        cor.append((B @ rho).diagonal().sum())
+        rhos.append(rho.copy())
+    return np.array(ts), np.array(cor), np.array(rhos)

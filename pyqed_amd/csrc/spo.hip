@@ -204,6 +204,139 @@ __global__ __launch_bounds__(256) void spo2_col_kernel(c128* psi, const c128* ex
   }
 }
 
+// ---------------------------------------------------------------- latency-shaped 2D passes (ns <= 2)
+// At 256 x 256 x 2 a pass moves 8-16 KB per workgroup, so its time is the chain of dependent
+// memory round trips, not bandwidth.  These variants issue EVERY global load of the pass (psi,
+// the point operator, exp_Ky / exp_K, twiddles) before the first wait, keep the point-local work
+// (V/2, snapshot, V/2, k_y phase) in registers, and touch LDS only for the FFT exchanges: one
+// load round trip + one store drain per pass.  Same arithmetic, same order as the generic kernels.
+
+// Row pass, thread j owns grid point j of row i (blockDim = max(L, 64)).
+template <int L, int NS>
+__global__ __launch_bounds__(L < 64 ? 64 : L) void spo2_row_fast_kernel(c128* psi, const c128* U, const c128* twy,
+                                                                        int flags, c128* snap, const c128* expKy) {
+  extern __shared__ c128 sm[];
+  c128* tw = sm;          // L
+  c128* A = sm + L;       // NS * L   ([state][point])
+  c128* Bf = A + NS * L;  // NS * L
+  const int i = blockIdx.x, j = threadIdx.x;
+  const bool own = j < L;
+  const size_t pt = (size_t)i * L + j;
+  c128 p[NS], u[NS * NS], ky = cmk(1, 0);
+  if (own) {
+#pragma unroll
+    for (int a = 0; a < NS; ++a) p[a] = psi[pt * NS + a];
+    if (flags & (ROW_VH1 | ROW_VH2)) {
+#pragma unroll
+      for (int e = 0; e < NS * NS; ++e) u[e] = U[pt * NS * NS + e];
+    }
+    if (flags & ROW_KY) ky = expKy[pt];
+    tw[j] = twy[j];
+  }
+  constexpr int T = L / 4;
+  const int f = j / T, t = j % T;
+  const bool active = f < NS;
+  auto fft = [&](auto inv_tag) {
+    constexpr bool INV = decltype(inv_tag)::value;
+    if (own) {
+#pragma unroll
+      for (int a = 0; a < NS; ++a) A[a * L + j] = p[a];
+    }
+    __syncthreads();
+    c128* r = fft_lds<L, INV>(A + (active ? f : 0) * L, Bf + (active ? f : 0) * L, tw, t, active);
+    // fft_lds ends on a barrier; the result buffer is the same for every transform
+    c128* res = (r == A + (active ? f : 0) * L) ? A : Bf;
+    if (own) {
+#pragma unroll
+      for (int a = 0; a < NS; ++a) p[a] = res[a * L + j];
+    }
+    __syncthreads();  // the next FFT overwrites A
+  };
+  auto point_op = [&]() {
+    c128 q[NS];
+#pragma unroll
+    for (int a = 0; a < NS; ++a) {
+      c128 s = cmk(0, 0);
+#pragma unroll
+      for (int b = 0; b < NS; ++b) s = cadd(s, cmul(u[a * NS + b], p[b]));
+      q[a] = s;
+    }
+#pragma unroll
+    for (int a = 0; a < NS; ++a) p[a] = q[a];
+  };
+  if (flags & ROW_INV) fft(std::true_type{});  // (fft's first barrier also publishes tw)
+  if (flags & ROW_VH1) point_op();
+  if ((flags & ROW_SNAP) && own) {
+#pragma unroll
+    for (int a = 0; a < NS; ++a) snap[pt * NS + a] = p[a];
+  }
+  if (flags & ROW_VH2) point_op();
+  if (flags & ROW_FWD) fft(std::false_type{});
+  if (flags & ROW_KY) {
+#pragma unroll
+    for (int a = 0; a < NS; ++a) p[a] = cmul(ky, p[a]);
+  }
+  if (own) {
+#pragma unroll
+    for (int a = 0; a < NS; ++a) psi[pt * NS + a] = p[a];
+  }
+}
+
+// Column pass over C columns j0..j0+C-1 (W = C*NS transforms, blockDim = W*L/4): exp_K for the
+// pass is loaded with psi, before the forward FFT.
+template <int L, int C, int NS>
+__global__ __launch_bounds__(C * NS * L / 4 < 64 ? 64 : C * NS * L / 4) void spo2_col_fast_kernel(
+    c128* psi, const c128* expKT, const c128* twx, int ny) {
+  constexpr int W = C * NS;
+  constexpr int BD = W * L / 4 < 64 ? 64 : W * L / 4;
+  constexpr int IT = (L * W + BD - 1) / BD;
+  extern __shared__ c128 sm[];
+  c128* tw = sm;           // L
+  c128* A = sm + L;        // W * L  ([c][a][i])
+  c128* Bf = A + W * L;
+  const int j0 = blockIdx.x * C;
+  const int tid = threadIdx.x;
+  constexpr bool FULL = (L * W) % BD == 0;
+  c128 v[IT], kf[IT];
+#pragma unroll
+  for (int n = 0; n < IT; ++n) {
+    const int e = tid + n * BD;  // load order: row i = e / W, transform ca = e % W (coalesced);
+    v[n] = cmk(0, 0);            // multiply order: transform ca = e / L, row i = e % L
+    kf[n] = cmk(0, 0);
+    if (FULL || e < L * W) {
+      v[n] = psi[((size_t)(e / W) * ny + j0) * NS + e % W];
+      kf[n] = expKT[(size_t)(j0 + (e / L) / NS) * L + e % L];
+    }
+  }
+  for (int k = tid; k < L; k += BD) tw[k] = twx[k];
+#pragma unroll
+  for (int n = 0; n < IT; ++n) {
+    const int e = tid + n * BD;
+    if (FULL || e < L * W) A[(e % W) * L + e / W] = v[n];
+  }
+  __syncthreads();
+  constexpr int T = L / 4;
+  const int f = tid / T, t = tid % T;
+  const bool active = f < W;
+  const int fo = (active ? f : 0) * L;
+  c128* r = fft_lds<L, false>(A + fo, Bf + fo, tw, t, active);
+  c128* cur = (r == A + fo) ? A : Bf;
+  c128* oth = (cur == A) ? Bf : A;
+#pragma unroll
+  for (int n = 0; n < IT; ++n) {
+    const int e = tid + n * BD;
+    if (FULL || e < L * W) cur[e] = cmul(cur[e], kf[n]);
+  }
+  __syncthreads();
+  r = fft_lds<L, true>(cur + fo, oth + fo, tw, t, active);
+  cur = (r == cur + fo) ? cur : oth;
+#pragma unroll
+  for (int n = 0; n < IT; ++n) {
+    const int e = tid + n * BD;
+    if (FULL || e < L * W) psi[((size_t)(e / W) * ny + j0) * NS + e % W] = cur[(e % W) * L + e / W];
+  }
+}
+
 // Middle-axis pass of a 3D grid psi [nx][ny][nz][ns] viewed as [outer][L][inner]
 // (inner = nz*ns): each workgroup transforms C consecutive inner indices of one
 // outer index i along the L axis (chunks of C*16 B per row: coalesced).
@@ -306,6 +439,40 @@ int twiddles(int L, hipStream_t st, c128* tw) {
   return QD_OK;
 }
 
+// Launch the latency-shaped row pass (ns <= 2): `rows` rows of length L.
+int row_fast(int L, int ns, int rows, int flags, c128* psi, const c128* U, const c128* tw, c128* snap,
+             const c128* expKy, hipStream_t st) {
+  const int bd = std::max(64, L);
+  const size_t lds = (size_t)(L + 2 * ns * L) * sizeof(c128);
+#define RF(LL)                                                                                                      \
+  if (ns == 1) hipLaunchKernelGGL((spo2_row_fast_kernel<LL, 1>), dim3(rows), dim3(bd), lds, st, psi, U, tw, flags, \
+                                  snap, expKy);                                                                     \
+  else hipLaunchKernelGGL((spo2_row_fast_kernel<LL, 2>), dim3(rows), dim3(bd), lds, st, psi, U, tw, flags, snap,   \
+                          expKy)
+  QD_FFT_DISPATCH(L, RF)
+#undef RF
+  QD_HIP(hipGetLastError());
+  return QD_OK;
+}
+
+// Latency-shaped column pass (ns <= 2, two columns per workgroup) over `cols` columns of length L;
+// `pitch` = points per row of psi.
+int col_fast(int L, int ns, int cols, c128* psi, const c128* expKT, const c128* tw, hipStream_t st, int pitch = -1) {
+  if (pitch < 0) pitch = cols;
+  const int W = 2 * ns;
+  const int bd = std::max(64, W * L / 4);
+  const size_t lds = (size_t)(L + 2 * W * L) * sizeof(c128);
+#define CF(LL)                                                                                                   \
+  if (ns == 1) hipLaunchKernelGGL((spo2_col_fast_kernel<LL, 2, 1>), dim3(cols / 2), dim3(bd), lds, st, psi,     \
+                                  expKT, tw, pitch);                                                             \
+  else hipLaunchKernelGGL((spo2_col_fast_kernel<LL, 2, 2>), dim3(cols / 2), dim3(bd), lds, st, psi, expKT, tw,  \
+                          pitch)
+  QD_FFT_DISPATCH(L, CF)
+#undef CF
+  QD_HIP(hipGetLastError());
+  return QD_OK;
+}
+
 }  // namespace
 }  // namespace qd
 
@@ -352,7 +519,9 @@ extern "C" int qd_spo2_run_ex(qd_c128* psi_, const qd_c128* expVh_, const qd_c12
   const c128* expV = (const c128*)expV_;
   const c128* expKy = (const c128*)expKy_;
   const int ky = expKy ? ROW_KY : 0;
+  const bool fast = ns <= 2 && C == 2;
   auto row = [&](int flags, c128* sp, const c128* U) -> int {
+    if (fast) return row_fast(ny, ns, nx, flags, psi, U, twy, sp, expKy, st);
 #define ROWCALL(L) \
   hipLaunchKernelGGL(spo2_row_kernel<L>, dim3(nx), dim3(row_threads), row_lds, st, psi, U, twy, ny, ns, flags, sp, \
                      expKy)
@@ -362,6 +531,7 @@ extern "C" int qd_spo2_run_ex(qd_c128* psi_, const qd_c128* expVh_, const qd_c12
     return QD_OK;
   };
   auto col = [&]() -> int {
+    if (fast) return col_fast(nx, ns, ny, psi, expKT, twx, st);
 #define COLCALL(L)                                                                                                   \
   if (C == 2)                                                                                                        \
     hipLaunchKernelGGL((spo2_col_kernel<L, 2>), dim3(ny / 2), dim3(col_threads), col_lds, st, psi, expKT, twx, ny,   \
@@ -454,7 +624,9 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
   const int col_threads = std::max(64, ((2 * ns * (nx / 4) + 63) / 64) * 64);
   const size_t col_lds = (size_t)(nx + 2 * 2 * ns * nx) * sizeof(c128);
   const int inner = nz * ns;
+  const bool fast = ns <= 2;
   auto row = [&](int flags, c128* sp) -> int {
+    if (fast) return row_fast(nz, ns, nx * ny, flags, psi, expVh, twz, sp, nullptr, st);
 #define ROWCALL3(L) \
   hipLaunchKernelGGL(spo2_row_kernel<L>, dim3(nx * ny), dim3(row_threads), row_lds, st, psi, expVh, twz, nz, ns, flags, sp, \
                      (const c128*)nullptr)
@@ -464,6 +636,7 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
     return QD_OK;
   };
   auto col = [&]() -> int {
+    if (fast) return col_fast(nx, ns, nyz, psi, expKT, twx, st);
 #define COLCALL3(L) \
   hipLaunchKernelGGL((spo2_col_kernel<L, 2>), dim3(nyz / 2), dim3(col_threads), col_lds, st, psi, expKT, twx, nyz, ns)
     QD_FFT_DISPATCH(nx, COLCALL3)

@@ -151,6 +151,35 @@ def lindblad_corr():
 
 
 @golden
+def corr3p_1t():
+    """correlation.correlation_3p_1t (pyqed/correlation.py:17-70) with dyn = oqs.liouvillian:
+    returns None, writes cor.dat (t, <A B(t) C>) and dm.dat (t, ravel rho) in the CWD."""
+    import tempfile
+    import pyqed.oqs as oqs
+    from pyqed.correlation import correlation_3p_1t
+    rng = np.random.default_rng(17)
+    N = 4
+    H = _herm(rng, N, 1 / np.sqrt(N))
+    C = _ginibre(rng, N, 0.2 / np.sqrt(N))
+    A, B, Cop = (_ginibre(rng, N) for _ in range(3))
+    psi = rng.standard_normal(N) + 1j * rng.standard_normal(N)
+    psi /= np.linalg.norm(psi)
+    rho0 = np.outer(psi, psi.conj())
+    tlist = np.linspace(0, 0.3, 16)
+    with tempfile.TemporaryDirectory() as d:
+        cwd = os.getcwd()
+        os.chdir(d)
+        try:
+            ret = correlation_3p_1t(csr_matrix(H), csr_matrix(rho0), [csr_matrix(A), csr_matrix(B), csr_matrix(Cop)],
+                                    [csr_matrix(C)], tlist, oqs.liouvillian)
+            cordat, dmdat = open("cor.dat").read(), open("dm.dat").read()
+        finally:
+            os.chdir(cwd)
+    save("corr3p_1t", H=H, C=C, A=A, B=B, Cop=Cop, rho0=rho0, tlist=tlist, returned_none=ret is None,
+         cordat=np.array(cordat), dmdat=np.array(dmdat))
+
+
+@golden
 def lindblad_eig():
     """superoperator.Lindblad_solver eigen path (superoperator.py:455-772), N=3 ladder."""
     import pyqed.superoperator as so

@@ -212,3 +212,25 @@ def test_lindblad_auto_dispatch_non_hermitian_state():
     lindblad_rk4(torch.from_numpy(H).to(dev), torch.from_numpy(np.array(cs)).to(dev), rho, 1e-2, 5)
     torch.cuda.synchronize()
     assert relerr(rho.cpu().numpy(), ref) < TOL
+
+
+@pytest.mark.gpu
+def test_correlation_3p_1t_matches_reference(tmp_path, monkeypatch):
+    """pyqed.correlation.correlation_3p_1t drop-in: returns None, cor.dat / dm.dat as the reference."""
+    from scipy.sparse import csr_matrix
+    from pyqed_amd.correlation import correlation_3p_1t
+    from test_oracle_golden import _parse_dat
+    g = load_golden("corr3p_1t")
+    monkeypatch.chdir(tmp_path)
+    ops = [csr_matrix(g[k]) for k in ("A", "B", "Cop")]
+    ret = correlation_3p_1t(csr_matrix(g["H"]), csr_matrix(g["rho0"]), ops, [csr_matrix(g["C"])], g["tlist"],
+                            "lindblad")
+    assert ret is None
+    t, cor = _parse_dat(open(tmp_path / "cor.dat").read())
+    tr, cr = _parse_dat(g["cordat"])
+    assert np.array_equal(t, tr) and relerr(cor, cr) < TOL
+    td, dm = _parse_dat(open(tmp_path / "dm.dat").read())
+    _, dmr = _parse_dat(g["dmdat"])
+    assert np.array_equal(td, tr) and relerr(dm, dmr) < TOL
+    with pytest.raises(NotImplementedError):
+        correlation_3p_1t(g["H"], g["rho0"], ops, [], g["tlist"], lambda r, H, c: r)

@@ -196,3 +196,19 @@ def test_spo2_jacobi_oracle_matches_reference():
     eVh, _ = spo.spo2_build(g["x"], g["y"], v, [1.0, 1.0], float(g["dt"]))
     pl, _ = spo.spo2_strang_run(eVh, spo.keo_jacobi(eKx, eKy), g["psi0"], int(g["nt"]), int(g["nout"]))
     assert relerr(np.array(pl), g["psilist"]) < TOL
+
+
+def _parse_dat(text):
+    rows = [ln.split() for ln in str(text).splitlines()]
+    return np.array([float(r[0]) for r in rows]), np.array([[complex(v) for v in r[1:]] for r in rows])
+
+
+def test_correlation_3p_1t_oracle_matches_reference():
+    g = load_golden("corr3p_1t")
+    assert bool(g["returned_none"])
+    t, cor, rhos = olb.correlation_3p_1t(g["H"], g["rho0"], [g["A"], g["B"], g["Cop"]], [g["C"]], g["tlist"])
+    tr, cr = _parse_dat(g["cordat"])
+    assert np.array_equal(t, tr)                         # same float accumulation t += dt
+    assert relerr(cor, cr[:, 0]) < TOL
+    td, dm = _parse_dat(g["dmdat"])
+    assert np.array_equal(td, tr) and relerr(rhos.reshape(len(t), -1), dm) < TOL
