@@ -159,6 +159,87 @@ def bench_2des(dev, world, rank, M_total, reps, n=256):
     return res, out, (lam, alpha, Mt, beta)
 
 
+def bench_2des_t2scan(dev, world, rank, M_total, n2, reps, n=256):
+    """2DES waiting-time scan: n2 (t3, t1) grids at t2 = 2.5*j of the M_total-member ensemble.  Members
+    shard over ranks; each rank runs ONE qd_response2d_t2scan launch sequence per rep (t3 operand built
+    once, every t2 in one split-K MFMA GEMM), then ONE RCCL reduce(sum) of the [n2, n, n] stack."""
+    import torch
+    import torch.distributed as dist
+    from pyqed_amd.distributed import shard_range
+    from pyqed_amd.response import ensemble_factors_bc, redfield_superop_batch
+    from pyqed_amd.superoperator import operator_to_superoperator
+    lo, hi = shard_range(M_total, rank, world)
+    rng = np.random.default_rng(3)
+    E = np.array([0.0, 1.0, 1.5]) + np.array([0.0, 0.05, 0.08]) * rng.standard_normal((M_total, 3))
+    E = E[lo:hi]
+    dip = np.zeros((3, 3)); dip[0, 1] = dip[1, 0] = dip[1, 2] = dip[2, 1] = 1.0
+    R = redfield_superop_batch(E, np.diag([0.0, 1.0, 2.0]), np.full((len(E), 3, 3), 0.05))
+    lam, U1 = np.linalg.eig(R)
+    U2 = np.linalg.inv(U1)
+    rho0v = np.zeros(9, complex); rho0v[0] = 1
+    ops = [operator_to_superoperator(dip, s).toarray() for s in "lccc"]
+    alpha, B, C, beta = ensemble_factors_bc(lam, U1, U2, ops, rho0v)
+    to = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+    lam_t, alpha_t, B_t, C_t, beta_t = to(lam), to(alpha), to(B), to(C), to(beta)
+    t = 0.5 * np.arange(n)
+    t2 = to(2.5 * np.arange(n2))
+    out = torch.empty((n2, n, n), dtype=torch.complex128, device=dev)
+    from pyqed_amd.response import response2d_t2scan
+
+    from pyqed_amd.distributed import sharded_sum_buckets
+    bucket = max(1, min(n2, 4))           # 4 waiting times = 4 MiB per RCCL reduce
+    buckets = [slice(b, min(n2, b + bucket)) for b in range(0, n2, bucket)]
+
+    def local(lo_, hi_, b):               # this rank's members are resident; t2 bucket b of the scan
+        response2d_t2scan(lam_t, alpha_t, B_t, C_t, beta_t, t, t2[b], t, out=out[b])
+
+    def once():
+        sharded_sum_buckets(local, M_total, out, buckets, dst=0)
+
+    once()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    stream = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(reps):
+        once()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    tt = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    wall = float(tt.item())
+    # compute-only time of this rank's launch sequence (no collective), for the scaling breakdown
+    torch.cuda.synchronize(dev)
+    c0 = time.perf_counter()
+    for _ in range(reps):
+        for b in buckets:
+            local(lo, hi, b)
+    torch.cuda.synchronize(dev)
+    comp = (time.perf_counter() - c0) / reps
+    Kp = ((hi - lo) * 9 + 15) // 16 * 16
+    gemm_flop = 8.0 * n * n * n2 * Kp
+    return {
+        "value": round(n * n * n2 * M_total * reps / wall, 1),
+        "unit": "grid-points/s ((t3,t1,t2) points x ensemble members)",
+        "config": {"workload": "2des_3level_256x256_redfield_ensemble_t2scan (BASELINE.json configs[4] x waiting times)",
+                   "grid": [n, n], "n_t2": n2, "ensemble_members": M_total, "members_per_rank": hi - lo,
+                   "signature": "lccc", "scaling": "strong",
+                   "collective": f"RCCL reduce(sum) of the [{n2},{n},{n}] c128 stack in {len(buckets)} buckets of "
+                   f"{bucket} waiting times, each overlapped with the next bucket's GEMM" if world > 1 else "none"},
+        "ms_per_scan": round(wall / reps * 1e3, 4),
+        "compute_ms_per_scan": round(comp * 1e3, 4),
+        "gemm_tflops": round(gemm_flop / comp / 1e12, 2),
+    }
+
+
 def cpu_baseline_2des(lam, alpha, Mt, beta, n=256, budget_s=5.0):
     """Closed-form slice per member with NumPy (oracle formula of correlation_4op_3t[:, j, :])."""
     t = 0.5 * np.arange(n)
@@ -325,6 +406,8 @@ def main():
     ap.add_argument("--ens", type=int, default=4096, help="2DES disorder-ensemble members (total)")
     ap.add_argument("--ens-reps", type=int, default=20)
     ap.add_argument("--no-2des", action="store_true")
+    ap.add_argument("--t2", type=int, default=16, help="2DES waiting times per scan (0 = skip the scan leg)")
+    ap.add_argument("--t2-reps", type=int, default=3)
     ap.add_argument("--spo-steps", type=int, default=1000)
     ap.add_argument("--no-spo", action="store_true")
     ap.add_argument("--deom-steps", type=int, default=200)
@@ -400,6 +483,8 @@ def main():
         twodes, sig, ens_in = bench_2des(dev, world, rank, args.ens, args.ens_reps)
         if rank == 0:
             twodes["signal_abs_max"] = float(sig.abs().max().item())
+        if args.t2 > 0:
+            twodes["t2scan"] = bench_2des_t2scan(dev, world, rank, args.ens, args.t2, args.t2_reps)
 
     spo = None
     if not args.no_spo:

@@ -304,6 +304,22 @@ int qd_response2d_ensemble_uniform(const qd_c128* alpha, const qd_c128* Mt,
                                    int accumulate, void* stream);
 
 /*
+ * Waiting-time scan of the disorder-ensemble 2D response (uniform t3 / t1 grids, t2 a device array of
+ * n2 waiting times):
+ *   out[j][i][k] (+)= (-i)^3 sum_m sum_pq alpha[m][p] e^{lam[m][p] t3_i}
+ *                       (B_m diag(e^{lam_m t2_j}) C_m)[p][q] beta[m][q] e^{lam[m][q] t1_k}
+ * i.e. qd_response2d_ensemble_uniform for every t2_j with Mt formed on the device from
+ * B = U1^-1 b U1, C = U1^-1 c U1 [M][nL][nL].  The t3 operand is built once and all waiting times
+ * share one split-K MFMA GEMM (N = n2 * n1).  Per rank: one member shard; the caller sums the
+ * [n2][n3][n1] stack over ranks with ONE RCCL reduce.  nL <= 16, n1 <= 1024.
+ */
+int qd_response2d_t2scan(const qd_c128* alpha, const qd_c128* B, const qd_c128* C,
+                         const qd_c128* beta, const qd_c128* lam, int M, int nL,
+                         double t3_0, double dt3, int n3, const double* t2, int n2,
+                         double t1_0, double dt1, int n1, qd_c128* out, int accumulate,
+                         void* stream);
+
+/*
  * Frequency-domain pole sum out[i] = sum_n -coeff_n / (lam_n + i w_i)
  * (Lindblad_solver.correlation_2op_1w / 3op_1w, pyqed/superoperator.py:603-700).
  */

@@ -285,6 +285,71 @@ __global__ void ens_reduce_kernel(const c128* slabs, int S, int n3, int n1, int 
   }
 }
 
+// ---- t2 scan: Z_all [Kp][n2 * n1p], column block j = waiting time t2_j (uniform t1 tables as above).
+// Member m = blockIdx.y, waiting time j = blockIdx.z: Mt_mj = B_m diag(e^{lam_m t2_j}) C_m is formed in
+// LDS (nL^3 complex MACs, r ascending like the host's B @ (e * C)), then the Z rows as ens_xz_uniform.
+__global__ __launch_bounds__(256) void ens_z_t2_kernel(const c128* Bm, const c128* Cm, const c128* beta,
+                                                       const c128* lam, const double* t2, int nL, double t0, double dt,
+                                                       int n1, int n1p, int ldz, c128* Z) {
+  __shared__ c128 sB[ZMAX * ZMAX], sCm[ZMAX * ZMAX], sM[ZMAX * ZMAX], sE[ZMAX];
+  __shared__ c128 sF[ZMAX * 16];
+  __shared__ c128 sC[ZMAX * UNI_MAXC];
+  const int m = blockIdx.y, j = blockIdx.z;
+  const int nC = n1p / 16;
+  const c128* lm = lam + (size_t)m * nL;
+  for (int e = threadIdx.x; e < nL * nL; e += 256) {
+    sB[e] = Bm[(size_t)m * nL * nL + e];
+    sCm[e] = Cm[(size_t)m * nL * nL + e];
+  }
+  for (int e = threadIdx.x; e < nL; e += 256) sE[e] = cexp_t(lm[e], t2[j]);
+  for (int e = threadIdx.x; e < nL * 16; e += 256) sF[e] = cexp_t(lm[e / 16], (double)(e % 16) * dt);
+  for (int e = threadIdx.x; e < nL * nC; e += 256)
+    sC[e] = cmul(beta[(size_t)m * nL + e / nC], cexp_t(lm[e / nC], t0 + 16.0 * (double)(e % nC) * dt));
+  __syncthreads();
+  for (int e = threadIdx.x; e < nL * nL; e += 256) {
+    const int p = e / nL, q = e % nL;
+    c128 v = cmk(0, 0);
+    for (int r = 0; r < nL; ++r) v = cadd(v, cmul(sB[p * nL + r], cmul(sE[r], sCm[r * nL + q])));
+    sM[e] = v;
+  }
+  __syncthreads();
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= n1p) return;
+  c128 y[ZMAX];
+#pragma unroll
+  for (int q = 0; q < ZMAX; ++q)
+    y[q] = (q < nL && k < n1) ? cmul(sC[q * nC + (k >> 4)], sF[q * 16 + (k & 15)]) : cmk(0, 0);
+  for (int p = 0; p < nL; ++p) {
+    c128 v = cmk(0, 0);
+#pragma unroll
+    for (int q = 0; q < ZMAX; ++q)
+      if (q < nL) v = cadd(v, cmul(sM[p * nL + q], y[q]));
+    Z[((size_t)m * nL + p) * ldz + (size_t)j * n1p + k] = v;
+  }
+}
+
+// rows K..Kp-1 of a Z with leading dimension ldz are padding
+__global__ void ens_z_pad_ld_kernel(int K, int Kp, int ldz, c128* Z) {
+  const size_t tot = (size_t)(Kp - K) * ldz;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x)
+    Z[(size_t)K * ldz + e] = cmk(0, 0);
+}
+
+// out[j][i][k] (+)= sum_s slab[s][i][j*n1p + k]   (slab leading dimension ldz = n2*n1p), fixed order
+__global__ void ens_reduce_t2_kernel(const c128* slabs, int S, int n2, int n3, int n1, int n3p, int n1p, c128* out,
+                                     int accumulate) {
+  const size_t tot = (size_t)n2 * n3 * n1;
+  const size_t ldz = (size_t)n2 * n1p;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    const int k = (int)(e % n1);
+    const int i = (int)((e / n1) % n3);
+    const int j = (int)(e / ((size_t)n1 * n3));
+    c128 v = accumulate ? out[e] : cmk(0, 0);
+    for (int s = 0; s < S; ++s) v = cadd(v, slabs[((size_t)s * n3p + i) * ldz + (size_t)j * n1p + k]);
+    out[e] = v;
+  }
+}
+
 // out[i] = sum_n -c_n / (lam_n + i w_i)   (Lindblad_solver.correlation_*_1w, superoperator.py:603-700)
 __global__ void resolvent_sum_kernel(const c128* c, const c128* lam, int n, const double* w, int nw, c128* out) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += gridDim.x * blockDim.x) {
@@ -449,6 +514,55 @@ extern "C" int qd_response2d_ensemble_uniform(const qd_c128* alpha, const qd_c12
                ZMAX, n1, 16 * UNI_MAXC);
   return ens_run("qd_response2d_ensemble_uniform", alpha, Mt, beta, lam, M, nL, nullptr, t3_0, dt3, n3, nullptr, t1_0,
                  dt1, n1, out, accumulate, stream);
+}
+
+extern "C" int qd_response2d_t2scan(const qd_c128* alpha, const qd_c128* Bm, const qd_c128* Cm, const qd_c128* beta,
+                                    const qd_c128* lam, int M, int nL, double t3_0, double dt3, int n3,
+                                    const double* t2, int n2, double t1_0, double dt1, int n1, qd_c128* out,
+                                    int accumulate, void* stream) {
+  const char* fn = "qd_response2d_t2scan";
+  QD_CHECK_ARG(alpha && Bm && Cm && beta && lam && t2 && out, "%s: null pointer", fn);
+  QD_CHECK_ARG(M >= 1 && nL >= 1 && n3 >= 1 && n1 >= 1 && n2 >= 1, "%s: bad sizes", fn);
+  QD_CHECK_ARG(nL <= ZMAX && n1 <= 16 * UNI_MAXC, "%s: nL=%d (<= %d), n1=%d (<= %d)", fn, nL, ZMAX, n1, 16 * UNI_MAXC);
+  QD_CHECK_ARG(M <= 65535 && n2 <= 65535 && (long)M * nL < (1L << 30), "%s: M=%d n2=%d too large", fn, M, n2);
+  hipStream_t st = (hipStream_t)stream;
+  const int BT = ENS_BT;
+  const int n3p = ceil_div(n3, BT) * BT, n1p = ceil_div(n1, BT) * BT;
+  const long ldz = (long)n2 * n1p;
+  QD_CHECK_ARG(ldz / BT <= 65535, "%s: n2*n1 too large", fn);
+  const int K = M * nL;
+  const int tiles = ceil_div(K, CG_KT);
+  const int Kp = tiles * CG_KT;
+  const int blocks2d = (int)((n3p / BT) * (ldz / BT));
+  // all waiting times share one GEMM (N = n2 * n1p): more output blocks, less split-K
+  int S = std::max(1, std::min(ceil_div(256, blocks2d), std::max(1, tiles / 4)));
+  const size_t nx = (size_t)n3p * Kp, nz = (size_t)Kp * ldz, nsl = (size_t)S * n3p * ldz;
+  void* w = nullptr;
+  int rc = workspace(WS_2DES, (nx + nz + nsl) * sizeof(c128), &w);
+  if (rc) return rc;
+  c128* X = (c128*)w;
+  c128* Z = X + nx;
+  c128* slabs = Z + nz;
+  const int xbx = ceil_div(Kp, 256), xblocks = xbx * (n3p / UNI_ROWS);
+  hipLaunchKernelGGL(ens_xz_uniform_kernel, dim3(1, xblocks), dim3(256), 0, st, (const c128*)nullptr,
+                     (const c128*)nullptr, (const c128*)lam, 0, nL, 0.0, 0.0, n1, n1p, Kp, (c128*)nullptr,
+                     (const c128*)alpha, K, t3_0, dt3, n3, n3p, xbx, X);
+  QD_HIP(hipGetLastError());
+  const int zbx = ceil_div(n1p, 256);
+  hipLaunchKernelGGL(ens_z_t2_kernel, dim3(zbx, M, n2), dim3(256), 0, st, (const c128*)Bm, (const c128*)Cm,
+                     (const c128*)beta, (const c128*)lam, t2, nL, t1_0, dt1, n1, n1p, (int)ldz, Z);
+  QD_HIP(hipGetLastError());
+  if (Kp > K) {
+    hipLaunchKernelGGL(ens_z_pad_ld_kernel, dim3(64), dim3(256), 0, st, K, Kp, (int)ldz, Z);
+    QD_HIP(hipGetLastError());
+  }
+  hipLaunchKernelGGL(ens_gemm_kernel, dim3((int)(ldz / BT), n3p / BT, S), dim3(CG_WG), 0, st, X, Kp, Z, (int)ldz,
+                     tiles, S, slabs, n3p);
+  QD_HIP(hipGetLastError());
+  hipLaunchKernelGGL(ens_reduce_t2_kernel, dim3(grid_for((size_t)n2 * n3 * n1, 256)), dim3(256), 0, st, slabs, S, n2,
+                     n3, n1, n3p, n1p, (c128*)out, accumulate);
+  QD_HIP(hipGetLastError());
+  return QD_OK;
 }
 
 extern "C" int qd_resolvent_sum(const qd_c128* coeff, const qd_c128* lam, int n, const double* w, int nw,

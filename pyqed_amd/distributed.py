@@ -3,6 +3,8 @@
 The hot path shards only where units are independent:
   * 2DES disorder ensemble: members split into contiguous ranges, each rank evaluates its
     partial (t3, t1) grid, ONE reduce(sum) of the 1 MiB grid to rank 0 (strong scaling);
+    a waiting-time scan reduces its [n2, n3, n1] stack in buckets, each bucket's reduce overlapped
+    with the next bucket's compute (sharded_sum_buckets);
   * Lindblad / DEOM / SPO batches: independent replicas per rank, no collective.
 """
 from __future__ import annotations
@@ -36,6 +38,26 @@ def sharded_sum(local_fn, n_units: int, dst: int | None = 0, group=None) -> torc
             dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
         else:
             dist.reduce(out, dst=dst, op=dist.ReduceOp.SUM, group=group)
+    return out
+
+
+def sharded_sum_buckets(local_fn, n_units: int, out: torch.Tensor, buckets, dst: int = 0, group=None):
+    """Bucketed, overlapped variant of sharded_sum for a stacked output (e.g. a 2DES waiting-time scan).
+
+    For each bucket (a slice along axis 0 of `out`): local_fn(lo, hi, bucket) fills out[bucket] with this
+    rank's member-shard partial sum, then the bucket is reduced to `dst` asynchronously, so the reduce of
+    bucket b overlaps the compute of bucket b+1 (the collective runs on RCCL's own stream).  All reduces
+    are waited for before returning.  Single process: local_fn(0, n_units, bucket) per bucket.
+    """
+    rank, ws = world()
+    lo, hi = shard_range(n_units, rank, ws)
+    works = []
+    for b in buckets:
+        local_fn(lo, hi, b)
+        if ws > 1:
+            works.append(dist.reduce(out[b], dst=dst, op=dist.ReduceOp.SUM, group=group, async_op=True))
+    for w in works:
+        w.wait()
     return out
 
 

@@ -88,6 +88,18 @@ def ensemble_factors(lam, U1, U2, supops, rho0v, t2):
     return alpha, Mt, beta
 
 
+def ensemble_factors_bc(lam, U1, U2, supops, rho0v):
+    """t2-independent factors for a waiting-time scan: alpha [M,nL], B = U2 b U1, C = U2 c U1
+    [M,nL,nL], beta [M,nL] (ensemble_factors without the e^{lam t2} contraction)."""
+    a, b, c, d = [np.broadcast_to(x, U1.shape) for x in supops]
+    nL = U1.shape[-1]
+    N = int(round(np.sqrt(nL)))
+    idm = np.identity(N).flatten()
+    alpha = np.einsum("a,mab,mbp->mp", idm, a, U1)
+    beta = np.einsum("mpa,mab,b->mp", U2, d, rho0v)
+    return alpha, U2 @ b @ U1, U2 @ c @ U1, beta
+
+
 def _uniform(t):
     """(t0, dt) when the host grid t is uniform to 1e-13 relative (np.arange / linspace grids), else None."""
     if isinstance(t, torch.Tensor):
@@ -148,3 +160,33 @@ def redfield_superop_batch(E, a_op, spec_vals):
         R[m] = -1j * (np.kron(np.diag(E[m]), I) - np.kron(I, np.diag(E[m]))) \
             - opA @ (np.kron(Lm, I) - np.kron(I, Lm.conj()))
     return R
+
+
+def response2d_t2scan(lam, alpha, B, C, beta, t3, t2, t1, out=None, accumulate=False, device=None):
+    """out[j, i, k] (+)= sum_m (t3_i, t1_k) slice of member m at waiting time t2_j (GPU).
+
+    Mt_mj = B_m diag(e^{lam_m t2_j}) C_m is formed on the device; every t2 shares one split-K MFMA
+    GEMM (qd_response2d_t2scan).  t3 and t1 must be uniform host grids (np.arange / linspace);
+    t2 any host array or device float64 tensor.  Returns [n2, n3, n1] complex128."""
+    dev = device or (out.device if out is not None else default_device())
+    _lib.ensure_device(dev)
+    lam_t, alpha_t, B_t, C_t, beta_t = (x if isinstance(x, torch.Tensor) else _t(x, dev)
+                                        for x in (lam, alpha, B, C, beta))
+    M, nL = alpha_t.shape
+    u3, u1 = _uniform(t3), _uniform(t1)
+    if u3 is None or u1 is None:
+        raise ValueError("response2d_t2scan: t3 and t1 must be uniform host grids")
+    n3, n1 = np.asarray(t3).size, np.asarray(t1).size
+    t2t = t2 if isinstance(t2, torch.Tensor) else _t(np.atleast_1d(np.asarray(t2, float)), dev, torch.float64)
+    n2 = t2t.numel()
+    if out is None:
+        out = torch.empty((n2, n3, n1), dtype=torch.complex128, device=dev)
+        accumulate = False
+    if tuple(out.shape) != (n2, n3, n1) or not out.is_contiguous() or out.dtype != torch.complex128:
+        raise ValueError(f"out must be a contiguous complex128 [{n2}, {n3}, {n1}] tensor")
+    with torch.cuda.device(dev):
+        rc = _lib.load().qd_response2d_t2scan(alpha_t.data_ptr(), B_t.data_ptr(), C_t.data_ptr(), beta_t.data_ptr(),
+                                              lam_t.data_ptr(), M, nL, u3[0], u3[1], n3, t2t.data_ptr(), n2, u1[0],
+                                              u1[1], n1, out.data_ptr(), int(bool(accumulate)), _lib.stream_ptr(dev))
+    _lib.check(rc, "qd_response2d_t2scan")
+    return out

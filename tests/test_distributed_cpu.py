@@ -79,6 +79,54 @@ def test_sharded_2des_reduce_gloo(world):
         assert np.allclose(a, full, rtol=1e-12, atol=1e-12 * np.abs(full).max())
 
 
+def _worker_buckets(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pyqed_amd.distributed import sharded_sum_buckets
+    lam, alpha, Mt, beta, t = _inputs()
+    n2 = 5
+    out = torch.zeros((n2, len(t), len(t)), dtype=torch.complex128)
+    calls = []
+
+    def local(lo, hi, b):
+        calls.append((lo, hi, b.start, b.stop))
+        for j in range(b.start, b.stop):   # waiting time j scales member m's slice by (j + 1 + m % 3)
+            acc = np.zeros((len(t), len(t)), complex)
+            for m in range(lo, hi):
+                acc += (j + 1 + m % 3) * _slice_sum(lam, alpha, Mt, beta, t, m, m + 1)
+            out[j] = torch.from_numpy(acc)
+
+    sharded_sum_buckets(local, len(lam), out, [slice(0, 2), slice(2, 4), slice(4, 5)], dst=0)
+    q.put((rank, out.numpy() if rank == 0 else None, calls))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bucketed_overlapped_reduce_gloo():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_buckets, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    lam, alpha, Mt, beta, t = _inputs()
+    M = len(lam)
+    full = np.array([sum((j + 1 + m % 3) * _slice_sum(lam, alpha, Mt, beta, t, m, m + 1) for m in range(M))
+                     for j in range(5)])
+    got = res[0][1]
+    assert np.allclose(got, full, rtol=1e-12, atol=1e-12 * np.abs(full).max())
+    # each rank computed its own member shard for every bucket, in order
+    assert [c[:2] for c in res[0][2]] == [(0, M // 2)] * 3
+    assert [c[:2] for c in res[1][2]] == [(M // 2, M)] * 3
+    assert [c[2:] for c in res[1][2]] == [(0, 2), (2, 4), (4, 5)]
+
+
 def test_shard_range_partition():
     from pyqed_amd.distributed import shard_range
     for n in [0, 1, 7, 4096, 4097]:

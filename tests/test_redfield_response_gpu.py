@@ -191,3 +191,49 @@ def test_ensemble_uniform_tables_vs_array_path():
     ref = sum((alpha[m][None, :] * np.exp(np.outer(tn, lam[m]))) @
               ((Mt[m] * beta[m][None, :]) @ np.exp(np.outer(lam[m], t))) for m in range(3)) * (-1j) ** 3
     assert relerr(S, ref) < 1e-12
+
+
+def test_t2scan_matches_reference_cube():
+    """Waiting-time scan, one member: out[j, i, k] == correlation_4op_3t cube[i, j, k] of the reference."""
+    from pyqed_amd.response import eigen_factors, response2d_t2scan, sos_eig
+    g = load_golden("corr4_3level")
+    lam, U1, U2 = sos_eig(g["R"])
+    tau = g["tau16"]
+    for sig in ["lccc", "llll", "lrlr"]:
+        alpha, B, C, beta = eigen_factors(lam, U1, U2, [g["dip"]] * 4, sig, g["rho0"])
+        S = response2d_t2scan(lam[None], alpha[None], B[None], C[None], beta[None], tau, tau, tau).cpu().numpy()
+        assert S.shape == (16, 16, 16)
+        assert relerr(S.transpose(1, 0, 2), g["cube_" + sig]) < TOL, sig
+
+
+@pytest.mark.parametrize("M,n3,n1", [(300, 200, 256), (7, 130, 40)])
+def test_t2scan_equals_per_t2_ensemble(M, n3, n1):
+    """Every waiting time of the scan equals the fixed-t2 ensemble slice (Mt built on the host); shard
+    accumulation over members equals the full scan."""
+    import torch
+    from pyqed_amd.response import (ensemble_factors, ensemble_factors_bc, redfield_superop_batch,
+                                    response2d_ensemble, response2d_t2scan)
+    from pyqed_amd.superoperator import operator_to_superoperator
+    rng = np.random.default_rng(M)
+    E = np.array([0.0, 1.0, 1.5]) + np.array([0.0, 0.05, 0.08]) * rng.standard_normal((M, 3))
+    R = redfield_superop_batch(E, np.diag([0.0, 1.0, 2.0]), np.full((M, 3, 3), 0.05))
+    lam, U1 = np.linalg.eig(R)
+    U2 = np.linalg.inv(U1)
+    dip = np.zeros((3, 3)); dip[0, 1] = dip[1, 0] = dip[1, 2] = dip[2, 1] = 1.0
+    ops = [operator_to_superoperator(dip, s).toarray() for s in "lccc"]
+    rho0v = np.zeros(9, complex); rho0v[0] = 1
+    alpha, B, C, beta = ensemble_factors_bc(lam, U1, U2, ops, rho0v)
+    t3, t1 = 0.5 * np.arange(n3), 0.4 * np.arange(n1)
+    t2 = np.array([0.0, 1.3, 4.0, 25.0])
+    scan = response2d_t2scan(lam, alpha, B, C, beta, t3, t2, t1).cpu().numpy()
+    for j, tj in enumerate(t2):
+        a2, Mt, b2 = ensemble_factors(lam, U1, U2, ops, rho0v, tj)
+        ref = response2d_ensemble(lam, a2, Mt, b2, t3, t1).cpu().numpy()
+        assert relerr(scan[j], ref) < 1e-12, j
+    dev = torch.device("cuda", 0)
+    part = torch.zeros((len(t2), n3, n1), dtype=torch.complex128, device=dev)
+    cut = [0, M // 3, M]
+    for lo, hi in zip(cut[:-1], cut[1:]):
+        response2d_t2scan(lam[lo:hi], alpha[lo:hi], B[lo:hi], C[lo:hi], beta[lo:hi], t3, t2, t1, out=part,
+                          accumulate=True)
+    assert relerr(part.cpu().numpy(), scan) < 1e-13
