@@ -154,6 +154,16 @@ int qd_spo2_run_ex(qd_c128* psi, const qd_c128* expVh, const qd_c128* expV,
                    int ns, int nsteps, int nout, qd_c128* snap, void* stream);
 
 /*
+ * Device build of the SPO point propagators (replaces the per-point eigh loop of
+ * SPO2.build / SPO3.build, pyqed/wpd.py:585-623 and :1290-1330): for every grid point
+ *   expV  = U e^{-i w dt} U^+,  expVh = U e^{-i w dt/2} U^+,  (w, U) = eigh(V_point)
+ * with LAPACK's conventions (lower triangle, real diagonal).  v is [npts][ns][ns] float64
+ * (v_complex = 0) or complex128 (v_complex = 1); ns in {1, 2}; expV may be null.
+ */
+int qd_spo_expv(const void* v, int v_complex, long npts, int ns, double dt,
+                qd_c128* expV, qd_c128* expVh, void* stream);
+
+/*
  * 1D single-surface split-operator with the step structure of pyqed/wpd.py:225-273
  * (SPO.run): V/2 ; (nt//nout - 1)*nout x [K, V] (snapshot after each block) ; K, V/2.
  * psi [B][nx] in/out (B independent wavepackets, one workgroup each, all steps in

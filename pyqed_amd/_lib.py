@@ -23,6 +23,7 @@ QD_ENOMEM = -4
 
 c_int = ctypes.c_int
 c_double = ctypes.c_double
+c_long = ctypes.c_long
 c_size_t = ctypes.c_size_t
 c_void_p = ctypes.c_void_p
 c_char_p = ctypes.c_char_p
@@ -45,6 +46,7 @@ SIGNATURES = {
     "qd_spo2_run_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                                c_void_p, c_void_p]),
     "qd_spo2_run": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "qd_spo_expv": (c_int, [c_void_p, c_int, c_long, c_int, c_double, c_void_p, c_void_p, c_void_p]),
     "qd_spo1d_run": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                              c_void_p]),
     "qd_deom_rk4": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -418,6 +418,64 @@ __global__ __launch_bounds__(256) void spo1d_kernel(c128* psi, const c128* expV,
   for (int k = threadIdx.x; k < L; k += blockDim.x) p[k] = cmul(expVh[k], cur[k]);
 }
 
+// ---------------------------------------------------------------- point propagators (SPO build)
+// exp(-i V tau) per grid point for tau = dt and dt/2 (wpd.py:585-623: eigh -> U e^{-i w tau} U^+).
+// LAPACK's eigh reads the lower triangle and ignores Im of the diagonal; so does this: a = Re V00,
+// d = Re V11, b = conj(V10).  For ns = 2 the exponential is closed form,
+//   exp(-i H tau) = e^{-i m tau} [cos(r tau) I - i (sin(r tau)/r) (H - m I)],
+//   m = (a + d)/2, delta = (a - d)/2, r = sqrt(delta^2 + |b|^2)   (sin(r tau)/r -> tau at r = 0),
+// identical to the eigen form in exact arithmetic and independent of the eigenvector phases.
+__device__ __forceinline__ void expv2(double a, double d, c128 b, double tau, c128* E) {
+  const double m = 0.5 * (a + d), de = 0.5 * (a - d);
+  const double r = sqrt(de * de + b.re * b.re + b.im * b.im);
+  double sn, cs, ph_s, ph_c;
+  sincos(r * tau, &sn, &cs);
+  const double sr = r > 0.0 ? sn / r : tau;
+  sincos(-m * tau, &ph_s, &ph_c);
+  const c128 ph = cmk(ph_c, ph_s);
+  E[0] = cmul(ph, cmk(cs, -sr * de));                 // c - i s delta
+  E[3] = cmul(ph, cmk(cs, sr * de));                  // c + i s delta
+  E[1] = cmul(ph, cmulmi(cscale(b, sr)));             // -i s b
+  E[2] = cmul(ph, cmulmi(cscale(cconj(b), sr)));      // -i s b*
+}
+
+template <bool CPLX>
+__global__ void spo_expv_kernel(const void* v_, long npts, int ns, double dt, c128* expV, c128* expVh) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < npts; e += (long)gridDim.x * blockDim.x) {
+    if (ns == 1) {
+      const double a = CPLX ? ((const c128*)v_)[e].re : ((const double*)v_)[e];
+      double sn, cs;
+      sincos(-a * dt, &sn, &cs);
+      if (expV) expV[e] = cmk(cs, sn);
+      sincos(-a * 0.5 * dt, &sn, &cs);
+      expVh[e] = cmk(cs, sn);
+      continue;
+    }
+    double a, d;
+    c128 b;
+    if (CPLX) {
+      const c128* v = (const c128*)v_ + e * 4;
+      a = v[0].re;
+      d = v[3].re;
+      b = cconj(v[2]);
+    } else {
+      const double* v = (const double*)v_ + e * 4;
+      a = v[0];
+      d = v[3];
+      b = cmk(v[2], 0.0);
+    }
+    c128 E[4];
+    if (expV) {
+      expv2(a, d, b, dt, E);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) expV[e * 4 + q] = E[q];
+    }
+    expv2(a, d, b, 0.5 * dt, E);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) expVh[e * 4 + q] = E[q];
+  }
+}
+
 bool pow2_in_range(int n) { return n >= 16 && n <= 1024 && (n & (n - 1)) == 0; }
 
 // L dispatch helpers
@@ -677,5 +735,22 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
     if ((rc = row(flags, sp))) return rc;
     if (s < nsteps && (rc = mid(false))) return rc;
   }
+  return QD_OK;
+}
+
+extern "C" int qd_spo_expv(const void* v, int v_complex, long npts, int ns, double dt, qd_c128* expV_,
+                           qd_c128* expVh_, void* stream) {
+  QD_CHECK_ARG(v && expVh_, "qd_spo_expv: null pointer");
+  QD_CHECK_ARG(ns == 1 || ns == 2, "qd_spo_expv: ns=%d (the device build covers ns <= 2)", ns);
+  QD_CHECK_ARG(npts >= 0, "qd_spo_expv: npts=%ld", npts);
+  if (npts == 0) return QD_OK;
+  const int grid = (int)std::min<long>((npts + 255) / 256, 8192);
+  if (v_complex)
+    hipLaunchKernelGGL(spo_expv_kernel<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, v, npts, ns, dt,
+                       (c128*)expV_, (c128*)expVh_);
+  else
+    hipLaunchKernelGGL(spo_expv_kernel<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, v, npts, ns, dt,
+                       (c128*)expV_, (c128*)expVh_);
+  QD_HIP(hipGetLastError());
   return QD_OK;
 }

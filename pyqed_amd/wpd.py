@@ -1,8 +1,8 @@
 """Split-operator wavepacket dynamics on MI355X (drop-in for pyqed/wpd.py SPO, SPO2).
 
-Setup (grids, exp_K, per-point exp(-i V dt/2)) is host-side like the reference's
-build (wpd.py:217-223, 496-625), vectorised; every propagation step runs in
-libqdyn (qd_spo1d_run / qd_spo2_run).
+Setup: grids and exp_K on the host like the reference's build (wpd.py:217-223, 496-625);
+the per-point propagators exp(-i V dt), exp(-i V dt/2) on the device (qd_spo_expv, ns <= 2).
+Every propagation step runs in libqdyn (qd_spo1d_run / qd_spo2_run_ex / qd_spo3_run).
 """
 from __future__ import annotations
 
@@ -119,7 +119,102 @@ class SPO:
         return r
 
 
-class SPO2:
+class _PointPropagators:
+    """exp_V / exp_V_half of a Hermitian diabatic potential, built on the device.
+
+    The reference's build (wpd.py:585-623, SPO3 :1290-1330) loops over grid points calling eigh and
+    forming U e^{-i w tau} U^+.  For ns <= 2 qd_spo_expv evaluates the same point propagators in
+    closed form on the GPU (LAPACK conventions: lower triangle, real diagonal); they stay on the
+    device for the run and are copied to the host only when exp_V / exp_V_half are read.  The
+    eigen data (d2a = U, apes = w) are host eigh results computed on first access.  ns > 2 builds
+    on the host with a vectorised eigh (setup, like the reference).
+    """
+    _eV_dev = _eVh_dev = None
+    _exp_V_host = _exp_V_half_host = None
+    _d2a = _apes = None
+    _eig_pending = False
+
+    @property
+    def exp_V(self):
+        if self._exp_V_host is None and self._eV_dev is not None:
+            self._exp_V_host = self._eV_dev.cpu().numpy()
+        return self._exp_V_host
+
+    @exp_V.setter
+    def exp_V(self, a):
+        self._exp_V_host, self._eV_dev = a, None
+
+    @property
+    def exp_V_half(self):
+        if self._exp_V_half_host is None and self._eVh_dev is not None:
+            self._exp_V_half_host = self._eVh_dev.cpu().numpy()
+        return self._exp_V_half_host
+
+    @exp_V_half.setter
+    def exp_V_half(self, a):
+        self._exp_V_half_host, self._eVh_dev = a, None
+
+    def _host_eig(self):
+        v = self._pot()
+        w, u = np.linalg.eigh(v)          # ascending eigenvalues per point (phys.sort order)
+        self._d2a = u
+        self._apes = None if np.iscomplexobj(v) else w
+        self._eig_pending = False
+        return w, u
+
+    @property
+    def d2a(self):
+        if self._eig_pending:
+            self._host_eig()
+        return self._d2a
+
+    @d2a.setter
+    def d2a(self, u):
+        self._d2a = u
+
+    @property
+    def apes(self):
+        if self._eig_pending:
+            self._host_eig()
+        return self._apes
+
+    @apes.setter
+    def apes(self, w):
+        self._apes = w
+
+    def _build_point_ops(self, dt):
+        v = self._pot()
+        ns = v.shape[-1]
+        if ns > 2:
+            w, u = self._host_eig()
+            ud = np.conj(np.swapaxes(u, -1, -2))
+            self.exp_V = (u * np.exp(-1j * w * dt)[..., None, :]) @ ud
+            self.exp_V_half = (u * np.exp(-1j * w * dt / 2)[..., None, :]) @ ud
+            return
+        dev = default_device()
+        _lib.ensure_device(dev)
+        cplx = np.iscomplexobj(v)
+        vd = torch.from_numpy(np.ascontiguousarray(v, dtype=complex if cplx else float)).to(dev)
+        eV = torch.empty(v.shape, dtype=torch.complex128, device=dev)
+        eVh = torch.empty_like(eV)
+        with torch.cuda.device(dev):
+            rc = _lib.load().qd_spo_expv(vd.data_ptr(), int(cplx), int(v.size // (ns * ns)), ns, float(dt),
+                                         eV.data_ptr(), eVh.data_ptr(), _lib.stream_ptr(dev))
+        _lib.check(rc, "qd_spo_expv")
+        self.exp_V, self.exp_V_half = None, None
+        self._eV_dev, self._eVh_dev = eV, eVh
+        self._d2a = self._apes = None
+        self._eig_pending = True
+
+    def _point_ops_dev(self, dev, need_full=False):
+        eVh = self._eVh_dev if self._eVh_dev is not None else _dev_c128(self.exp_V_half, dev)
+        eV = None
+        if need_full:
+            eV = self._eV_dev if self._eV_dev is not None else _dev_c128(self.exp_V, dev)
+        return eV, eVh
+
+
+class SPO2(_PointPropagators):
     """Drop-in for pyqed.wpd.SPO2 (wpd.py:379-887), linear and Jacobi coordinates."""
 
     def __init__(self, x, y, mass=None, nstates=2, coords='linear', G=None, abc=False):
@@ -180,24 +275,20 @@ class SPO2:
         self.V = self.v = v
         return self
 
+    def _pot(self):
+        return self.v
+
     def build(self, dt, inertia=None):
         """wpd.py:496-625: the kinetic propagator (linear: exp_K on the 'ij' k-grid; jacobi:
-        exp_Kx and exp_Ky[i, ky] = exp(-i ky^2 / (2 I(x_i)) dt) with I = masses[1]) and per-point
-        U e^{-i w dt/2} U^+ (vectorised eigh over the grid instead of the reference's Python loop)."""
+        exp_Kx and exp_Ky[i, ky] = exp(-i ky^2 / (2 I(x_i)) dt) with I = masses[1]) and the per-point
+        U e^{-i w tau} U^+ (device build, _PointPropagators)."""
         nx, ny = self.nx, self.ny
         self.kx = 2. * np.pi * fftfreq(nx, interval(self.x))
         self.ky = 2. * np.pi * fftfreq(ny, interval(self.y))
         self._build_keo(dt)
         if self.v is None:
             raise ValueError('The diabatic PES is not specified.')
-        v = self.v
-        w, u = np.linalg.eigh(v)  # ascending eigenvalues per point (phys.sort order)
-        ud = np.conj(np.swapaxes(u, -1, -2))
-        self.exp_V = (u * np.exp(-1j * w * dt)[..., None, :]) @ ud
-        self.exp_V_half = (u * np.exp(-1j * w * dt / 2)[..., None, :]) @ ud
-        self.d2a = u
-        if not np.iscomplexobj(v):
-            self.apes = w
+        self._build_point_ops(dt)
 
     def _build_keo(self, dt):
         if self.coords == 'linear':
@@ -222,8 +313,7 @@ class SPO2:
         psi = _dev_c128(psi0, dev)
         nsnap = nt // nout
         snap = torch.empty((nsnap, self.nx, self.ny, self.ns), dtype=torch.complex128, device=dev) if nsnap else None
-        eVh = _dev_c128(self.exp_V_half, dev)
-        eV = _dev_c128(self.exp_V, dev) if merged else None
+        eV, eVh = self._point_ops_dev(dev, need_full=merged)
         if self.coords == 'jacobi':
             eK = _dev_c128(np.broadcast_to(self.exp_Kx[:, None], (self.nx, self.ny)), dev)
             eKy = _dev_c128(self.exp_Ky, dev)
@@ -303,7 +393,7 @@ class SPO2NH(SPO2):
         return r
 
 
-class SPO3:
+class SPO3(_PointPropagators):
     """Drop-in for pyqed.wpd.SPO3 (wpd.py:1105-1432), linear coordinates."""
 
     def __init__(self, x, y, z, masses, nstates=2, coords='linear', G=None, abc=False):
@@ -354,10 +444,10 @@ class SPO3:
         self.exp_K = np.exp(-1j * (Kx ** 2 / 2. / mx + Ky ** 2 / 2. / my + Kz ** 2 / 2. / mz) * dt)
         if self.V is None:
             raise ValueError('The diabatic PES is not specified.')
-        w, u = np.linalg.eigh(self.V)
-        ud = np.conj(np.swapaxes(u, -1, -2))
-        self.exp_V = (u * np.exp(-1j * w * dt)[..., None, :]) @ ud
-        self.exp_V_half = (u * np.exp(-1j * w * dt / 2)[..., None, :]) @ ud
+        self._build_point_ops(dt)
+
+    def _pot(self):
+        return self.V
 
     def run(self, psi0, e_ops=[], dt=0.01, nt=1, t0=0., nout=1, return_states=True):
         """wpd.py:1349-1411: nt//nout*nout Strang steps; psilist = state after every nout steps
@@ -370,7 +460,7 @@ class SPO3:
         psi = _dev_c128(psi0, dev)
         shape = (self.nx, self.ny, self.nz, self.nstates)
         snap = torch.empty((nsnap,) + shape, dtype=torch.complex128, device=dev) if nsnap else None
-        eVh = _dev_c128(self.exp_V_half, dev)
+        _, eVh = self._point_ops_dev(dev)
         eK = _dev_c128(self.exp_K, dev)
         with torch.cuda.device(dev):
             rc = _lib.load().qd_spo3_run(psi.data_ptr(), eVh.data_ptr(), eK.data_ptr(), self.nx, self.ny, self.nz,

@@ -176,3 +176,34 @@ def test_spo2_merged_equals_strang_unitary():
         out[rs] = sol.run(g["psi0"], dt=float(g["dt"]), nt=nt, nout=nout, return_states=rs).psi
     assert out[True].shape == (n, n, 2)
     assert relerr(out[False], out[True]) < 1e-12
+
+
+@pytest.mark.parametrize("ns,cplx", [(2, False), (2, True), (1, False)])
+def test_device_point_propagators_match_eigh(ns, cplx):
+    """qd_spo_expv (closed form) == U e^{-i w tau} U^+ from eigh (wpd.py:585-623), with LAPACK's
+    conventions: lower triangle and real diagonal are what eigh reads.  Includes degenerate points."""
+    from pyqed_amd.wpd import SPO2
+    rng = np.random.default_rng(3 + ns + cplx)
+    n = 32
+    x = np.linspace(-4, 4, n)
+    v = rng.standard_normal((n, n, ns, ns))
+    if cplx:
+        v = v + 1j * rng.standard_normal((n, n, ns, ns))   # not Hermitian: upper triangle / Im diag ignored
+    else:
+        v = 0.5 * (v + np.swapaxes(v, -1, -2))
+    if ns == 2:
+        v[0, 0] = [[0.3, 0.0], [0.0, 0.3]]                   # r = 0
+        v[0, 1] = [[-1.0, 0.0], [0.0, 2.0]]                  # diagonal
+    sol = SPO2(x, x, mass=[1.0, 1.0], nstates=ns)
+    sol.set_dpes(v)
+    dt = 0.07
+    sol.build(dt)
+    vl = np.tril(v) + np.conj(np.swapaxes(np.tril(v, -1), -1, -2))
+    w, u = np.linalg.eigh(vl)
+    ud = np.conj(np.swapaxes(u, -1, -2))
+    for tau, got in [(dt, sol.exp_V), (dt / 2, sol.exp_V_half)]:
+        ref = (u * np.exp(-1j * w * tau)[..., None, :]) @ ud
+        assert relerr(got, ref) < 1e-14
+    w2, u2 = np.linalg.eigh(v)                              # lazy host eigen data
+    assert np.array_equal(sol.d2a, u2)
+    assert (sol.apes is None) if cplx else np.array_equal(sol.apes, w2)
