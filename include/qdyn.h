@@ -330,6 +330,17 @@ int qd_response2d_t2scan(const qd_c128* alpha, const qd_c128* B, const qd_c128* 
                          void* stream);
 
 /*
+ * Frequency-domain 2D signal of an eigen-decomposed generator (DEOMSolver.correlation_4op_3t,
+ * pyqed/heom/deom.py:1127-1209, whose per-(w_x, w_y) trace this evaluates in closed form):
+ *   out[i][j] = sum_pq a_p / (-lam_p - i wx_i) * M_pq * v_q / (-lam_q - i wy_j)
+ * a, v, lam [n]; M [n][n] row-major; wx [nx], wy [ny] device float64; out [nx][ny].
+ * Two split-K MFMA GEMMs (W = M Z, out = X W) on generated resolvent operands.
+ */
+int qd_resolvent_grid2d(const qd_c128* a, const qd_c128* M, const qd_c128* v,
+                        const qd_c128* lam, int n, const double* wx, int nx,
+                        const double* wy, int ny, qd_c128* out, void* stream);
+
+/*
  * Frequency-domain pole sum out[i] = sum_n -coeff_n / (lam_n + i w_i)
  * (Lindblad_solver.correlation_2op_1w / 3op_1w, pyqed/superoperator.py:603-700).
  */

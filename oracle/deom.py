@@ -8,6 +8,8 @@ Follows pyqed/heom/deom.py:
   :676-688    generate_time (H(t) = H + Hdip f(t), Q(t) = Q + Qdip g(t))
   :725-766    rk4 (stages at t, t+dt/2, t+dt/2, t+dt)
   :1072-1114  DEOMSolver.run (t_save, Tr(p1 rho_0) or rho_0 per step)
+  :769-893    generate_propgator / generate_actions (dense ADO Liouvillian, element by element)
+  :1127-1209  DEOMSolver.correlation_4op_3t (eig + pinv, trace per (w_x, w_y) point)
 """
 import numpy as np
 
@@ -105,3 +107,89 @@ def run(H, Hdip, fs, Q, Qdip, fc, bath, L, rho0, dt, nt, p1=None, mode=None):
         t_save[i + 1] = (i + 1) * dt
         saved.append(np.trace(p1 @ ddos[0]) if p1 is not None else ddos[0].copy())
     return t_save, np.array(saved), ddos
+
+
+def _idx(iado, i, j, ns):
+    return iado * ns * ns + i * ns + j                       # gen_index2 (:769-771)
+
+
+def propagator(keys, comb, L, expn, etal, etar, etaa, mode, H, Q):
+    """generate_propgator (:856-882): dense P with P vec(ddos) = rem_cal, element by element."""
+    nmax, K = keys.shape
+    ns = H.shape[0]
+    P = np.zeros((nmax * ns * ns, nmax * ns * ns), dtype=complex)
+    for a in range(nmax):
+        key = keys[a]
+        for i in range(ns):
+            for j in range(ns):
+                P[_idx(a, i, j, ns), _idx(a, i, j, ns)] -= np.sum(key * expn)
+        for i in range(ns):
+            for j in range(ns):
+                if np.abs(H[i, j]) > 1e-10:                       # allcator_H (:774-782)
+                    for k in range(ns):
+                        P[_idx(a, i, k, ns), _idx(a, j, k, ns)] -= 1j * H[i, j]
+                        P[_idx(a, k, j, ns), _idx(a, k, i, ns)] += 1j * H[i, j]
+        for mp in range(K):
+            n, q = key[mp], Q[mode[mp]]
+            if n > 0:                                             # allcator_Q_m (:799-810)
+                km = key.copy(); km[mp] -= 1
+                pos = gen_hash_value(km, comb)
+                for i in range(ns):
+                    for j in range(ns):
+                        for k in range(ns):
+                            P[_idx(a, i, k, ns), _idx(pos, j, k, ns)] -= \
+                                1j * np.sqrt(n) / np.sqrt(etaa[mp]) * etal[mp] * q[i, j]
+                            P[_idx(a, k, j, ns), _idx(pos, k, i, ns)] += \
+                                1j * np.sqrt(n) / np.sqrt(etaa[mp]) * etar[mp] * q[i, j]
+            if key.sum() < L:                                     # allcator_Q_p (:813-823)
+                kp = key.copy(); kp[mp] += 1
+                pos = gen_hash_value(kp, comb)
+                for i in range(ns):
+                    for j in range(ns):
+                        for k in range(ns):
+                            P[_idx(a, i, k, ns), _idx(pos, j, k, ns)] -= 1j * np.sqrt(n + 1) * np.sqrt(etaa[mp]) * q[i, j]
+                            P[_idx(a, k, j, ns), _idx(pos, k, i, ns)] += 1j * np.sqrt(n + 1) * np.sqrt(etaa[mp]) * q[i, j]
+    return P
+
+
+def actions(A, nmax, lcr):
+    """generate_actions (:885-892) / actions_element (:826-838)."""
+    ns = A.shape[0]
+    X = np.zeros((nmax * ns * ns, nmax * ns * ns), dtype=complex)
+    for a in range(nmax):
+        for i in range(ns):
+            for j in range(ns):
+                if np.abs(A[i, j]) > 1e-10:
+                    for k in range(ns):
+                        if lcr in ('l', 'c'):
+                            X[_idx(a, i, k, ns), _idx(a, j, k, ns)] += A[i, j]
+                        if lcr in ('r', 'c'):
+                            X[_idx(a, k, j, ns), _idx(a, k, i, ns)] += A[i, j]
+    return X
+
+
+def correlation_4op_3t(P, nmax, ns, ops, rho0, T, w_x, w_y, if_full=True, cut_off_min=0.5, cut_off_max=1.1,
+                       lcr='llll'):
+    """DEOMSolver.correlation_4op_3t (:1127-1209) with ops = (a, b, c, d), evaluated as the reference does:
+    one trace per (w_x, w_y) point."""
+    import scipy.linalg as la
+    lam, V = la.eig(P)
+    Vi = la.pinv(V)
+    a, b, c, d = ops
+    A1, A2, A3, A4 = actions(d, nmax, lcr[3]), actions(c, nmax, lcr[2]), actions(b, nmax, lcr[1]), \
+        actions(a, nmax, lcr[0])
+    rho = np.zeros((nmax * ns * ns, 1), dtype=complex)
+    rho[:ns * ns, 0] = np.asarray(rho0).flatten()
+    if not if_full:
+        lo, hi = np.min(np.real(lam)) * cut_off_min, np.max(np.real(lam)) * cut_off_max
+        sel = (np.real(lam) > lo) & (np.real(lam) < hi)
+        V, Vi, lam = V[:, sel], Vi[sel, :], lam[sel]
+    A1V = A1 @ V
+    G = (Vi @ A2 @ V) @ (np.diag(np.exp(lam * T)) @ (Vi @ A3 @ V))
+    VA4 = Vi @ (A4 @ rho)
+    cw = np.zeros((len(w_x), len(w_y)), dtype=complex)
+    for i in range(len(w_x)):
+        for j in range(len(w_y)):
+            y = A1V @ ((1 / (-lam - 1j * w_x[i])).reshape(-1, 1) * (G @ ((1 / (-lam - 1j * w_y[j])).reshape(-1, 1) * VA4)))
+            cw[i, j] = np.trace(y[:ns * ns, 0].reshape(ns, ns))
+    return cw

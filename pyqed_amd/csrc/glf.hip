@@ -52,6 +52,7 @@ struct LindbladParams {
   int herm;                // Hermitian fast path (Lindblad, rho exactly Hermitian, single block)
   double dt;
   unsigned long long* tbuf;  // [B][8] per-phase wall-clock ticks (QD_PHASE_TIMING diagnostics) or null
+  unsigned long long stagger;  // start offset (wall-clock ticks) of the odd workgroup group of each XCD
 };
 
 // Per-matrix scratch slots of Np x Np: stage buffer(s), RK4 accumulator, Y_c.
@@ -141,6 +142,13 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
   const double dt = p.dt, dt2 = p.dt / 2.0;
   int cur = 0;
   CgAcc<BT> A;
+  // Phase offset: the workgroups run identical schedules, so without an offset every CU reaches its
+  // memory-bound RK4 epilogue at the same moment.  Delaying every other workgroup of each XCD
+  // (blocks b, b + 8 share an XCD) interleaves one group's epilogue with the other's MFMA phase.
+  if (p.stagger && ((b >> 3) & 1)) {
+    const unsigned long long t0s = wall_clock64();
+    while (wall_clock64() - t0s < p.stagger) __builtin_amdgcn_s_sleep(32);
+  }
   QD_TIMING_DECL
 
   for (int step = 0; step < p.nsteps; ++step) {
@@ -204,7 +212,10 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
           constexpr int TS = BT / 2, LD = TS + 1;
           static_assert(2 * TS * LD * sizeof(c128) <= sizeof(CgLds<BT>), "LDS transpose buffer");
           constexpr int PER = BT * BT / 2 / CG_WG;  // elements per thread per round
-          constexpr int CH = PER < 4 ? PER : 4;
+          #ifndef QD_EPI_CH
+#define QD_EPI_CH 4
+#endif
+          constexpr int CH = PER < QD_EPI_CH ? PER : QD_EPI_CH;
           c128* T0 = reinterpret_cast<c128*>(&L);
           c128* T1 = T0 + TS * LD;
           c128* Xd = Y;
@@ -226,31 +237,35 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
               }
               __syncthreads();
             }
+            // global loads of a chunk are issued together; k (from LDS) is formed only at its use, so
+            // a chunk holds 2 c128 + 1 index per element while its loads are in flight
             for (int q0 = 0; q0 < PER; q0 += CH) {
-              size_t idx[CH];
-              c128 k[CH], r0[CH], a0[CH];
+              int idx[CH];
+              c128 r0[CH], a0[CH];
+#pragma unroll
+              for (int q = 0; q < CH; ++q) {
+                const int e = tid + CG_WG * (q0 + q);
+                const int ts = e / (TS * TS), rem = e % (TS * TS), ra = rem / TS, cc = rem % TS;
+                const int gc = (rd == 0 ? 1 - ts : ts) * TS + cc;  // off-diagonal: column block 1 - ts
+                idx[q] = (ts * TS + ra) * Np + gc;
+                r0[q] = rho[idx[q]];
+                a0[q] = stage == 0 ? cmk(0, 0) : acc[idx[q]];
+              }
 #pragma unroll
               for (int q = 0; q < CH; ++q) {
                 const int e = tid + CG_WG * (q0 + q);
                 const int ts = e / (TS * TS), rem = e % (TS * TS), ra = rem / TS, cc = rem % TS;
                 const c128* own = ts == 0 ? T0 : T1;
                 const c128* mir = rd == 0 ? (ts == 0 ? T1 : T0) : own;
-                const int gc = (rd == 0 ? 1 - ts : ts) * TS + cc;  // off-diagonal: column block 1 - ts
-                idx[q] = (size_t)(ts * TS + ra) * Np + gc;
-                k[q] = cadd(own[ra * LD + cc], cconj(mir[cc * LD + ra]));
-                r0[q] = rho[idx[q]];
-                a0[q] = stage == 0 ? cmk(0, 0) : acc[idx[q]];
-              }
-#pragma unroll
-              for (int q = 0; q < CH; ++q) {
+                const c128 k = cadd(own[ra * LD + cc], cconj(mir[cc * LD + ra]));
                 if (stage == 0) {
-                  acc[idx[q]] = k[q];
-                  rn[idx[q]] = cadd(r0[q], cscale(k[q], dt2));
+                  acc[idx[q]] = k;
+                  rn[idx[q]] = cadd(r0[q], cscale(k, dt2));
                 } else if (stage < 3) {
-                  acc[idx[q]] = cadd(a0[q], cscale(k[q], 2.0));
-                  rn[idx[q]] = cadd(r0[q], cscale(k[q], stage == 1 ? dt2 : dt));
+                  acc[idx[q]] = cadd(a0[q], cscale(k, 2.0));
+                  rn[idx[q]] = cadd(r0[q], cscale(k, stage == 1 ? dt2 : dt));
                 } else {
-                  const c128 r1 = cadd(r0[q], cscale(cscale(cadd(a0[q], k[q]), 1.0 / 6.0), dt));
+                  const c128 r1 = cadd(r0[q], cscale(cscale(cadd(a0[q], k), 1.0 / 6.0), dt));
                   rho[idx[q]] = r1;
                   rn[idx[q]] = r1;
                 }
@@ -574,6 +589,8 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   p.total_steps = nsteps;
   p.herm = herm;
   p.tbuf = nullptr;
+  p.stagger = 0;
+  if (const char* e = std::getenv("QD_STAGGER_US")) p.stagger = (unsigned long long)(std::atof(e) * 100.0);  // 100 MHz
 #ifdef QD_PHASE_TIMING
   const bool timing = true;  // diagnostics build: per-phase clocks to stderr
 #else

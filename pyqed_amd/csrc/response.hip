@@ -350,6 +350,42 @@ __global__ void ens_reduce_t2_kernel(const c128* slabs, int S, int n2, int n3, i
   }
 }
 
+// ---- frequency-domain bilinear grids (DEOMSolver.correlation_4op_3t, heom/deom.py:1127-1209):
+//   out[i][j] = sum_pq x_p(wx_i) M_pq z_q(wy_j),  x_p(w) = a_p / (-lam_p - i w),  z_q(w) = v_q / (-lam_q - i w)
+// as two split-K MFMA GEMMs: W = M Z (n x n x ny), out = X W (nx x n x ny).
+__device__ __forceinline__ c128 cdiv(c128 a, c128 b) {
+  // Smith's algorithm (scaled, as numpy's complex division)
+  if (fabs(b.re) >= fabs(b.im)) {
+    const double r = b.im / b.re, d = b.re + b.im * r;
+    return cmk((a.re + a.im * r) / d, (a.im - a.re * r) / d);
+  }
+  const double r = b.re / b.im, d = b.im + b.re * r;
+  return cmk((a.re * r + a.im) / d, (a.im * r - a.re) / d);
+}
+
+// rows_w = 1: out[i][p] (ld = Kp) = coef_p / (-lam_p - i w_i) for i < nw, p < n, zero padding up to [rows][Kp]
+// rows_w = 0: out[q][j] (ld = nwp) = coef_q / (-lam_q - i w_j), [Kp][nwp]
+__global__ void resolvent_operand_kernel(const c128* coef, const c128* lam, int n, const double* w, int nw, int rows_w,
+                                         int R, int C, c128* out) {
+  const size_t tot = (size_t)R * C;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    const int r = (int)(e / C), c = (int)(e % C);
+    const int iw = rows_w ? r : c, p = rows_w ? c : r;
+    c128 v = cmk(0, 0);
+    if (iw < nw && p < n) v = cdiv(coef[p], cmk(-lam[p].re, -lam[p].im - w[iw]));
+    out[e] = v;
+  }
+}
+
+// dst [R][C] = src [n][n] zero-padded
+__global__ void pad_square_kernel(const c128* src, int n, int R, int C, c128* dst) {
+  const size_t tot = (size_t)R * C;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    const int r = (int)(e / C), c = (int)(e % C);
+    dst[e] = (r < n && c < n) ? src[(size_t)r * n + c] : cmk(0, 0);
+  }
+}
+
 // out[i] = sum_n -c_n / (lam_n + i w_i)   (Lindblad_solver.correlation_*_1w, superoperator.py:603-700)
 __global__ void resolvent_sum_kernel(const c128* c, const c128* lam, int n, const double* w, int nw, c128* out) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += gridDim.x * blockDim.x) {
@@ -563,6 +599,57 @@ extern "C" int qd_response2d_t2scan(const qd_c128* alpha, const qd_c128* Bm, con
                      n3, n1, n3p, n1p, (c128*)out, accumulate);
   QD_HIP(hipGetLastError());
   return QD_OK;
+}
+
+namespace {
+// C[m][k] (m < Mo, k < No, leading dimension No) = A [Mp][Kp] * B [Kp][Np]; padded operands, split-K MFMA GEMM
+int splitk_gemm(const c128* A, const c128* B, int Mp, int Kp, int Np, int Mo, int No, c128* C, c128* slabs, int S,
+                hipStream_t st) {
+  const int tiles = Kp / CG_KT;
+  hipLaunchKernelGGL(ens_gemm_kernel, dim3(Np / ENS_BT, Mp / ENS_BT, S), dim3(CG_WG), 0, st, A, Kp, B, Np, tiles, S,
+                     slabs, Mp);
+  QD_HIP(hipGetLastError());
+  hipLaunchKernelGGL(ens_reduce_kernel, dim3(grid_for((size_t)Mo * No, 256)), dim3(256), 0, st, slabs, S, Mo, No, Mp,
+                     Np, C, 0);
+  QD_HIP(hipGetLastError());
+  return QD_OK;
+}
+int splits_for(int Mp, int Np, int Kp) {
+  const int blocks = (Mp / ENS_BT) * (Np / ENS_BT), tiles = Kp / CG_KT;
+  return std::max(1, std::min(ceil_div(256, blocks), std::max(1, tiles / 4)));
+}
+}  // namespace
+
+extern "C" int qd_resolvent_grid2d(const qd_c128* a, const qd_c128* M, const qd_c128* v, const qd_c128* lam, int n,
+                                   const double* wx, int nx, const double* wy, int ny, qd_c128* out, void* stream) {
+  const char* fn = "qd_resolvent_grid2d";
+  QD_CHECK_ARG(a && M && v && lam && wx && wy && out, "%s: null pointer", fn);
+  QD_CHECK_ARG(n >= 1 && nx >= 1 && ny >= 1 && n <= 65536 && nx <= 65536 && ny <= 65536, "%s: bad sizes", fn);
+  hipStream_t st = (hipStream_t)stream;
+  const int BT = ENS_BT;
+  const int np_ = ceil_div(n, BT) * BT;  // n as a row / column block dimension and as K (multiple of 16 too)
+  const int nxp = ceil_div(nx, BT) * BT, nyp = ceil_div(ny, BT) * BT;
+  const int S1 = splits_for(np_, nyp, np_), S2 = splits_for(nxp, nyp, np_);
+  const size_t nM = (size_t)np_ * np_, nZ = (size_t)np_ * nyp, nW = (size_t)np_ * nyp, nX = (size_t)nxp * np_;
+  const size_t nsl = std::max((size_t)S1 * np_ * nyp, (size_t)S2 * nxp * nyp);
+  void* w = nullptr;
+  int rc = workspace(WS_2DES, (nM + nZ + nW + nX + nsl) * sizeof(c128), &w);
+  if (rc) return rc;
+  c128* Mp = (c128*)w;
+  c128* Z = Mp + nM;
+  c128* W = Z + nZ;
+  c128* X = W + nW;
+  c128* slabs = X + nX;
+  hipLaunchKernelGGL(pad_square_kernel, dim3(grid_for(nM, 256)), dim3(256), 0, st, (const c128*)M, n, np_, np_, Mp);
+  QD_HIP(hipGetLastError());
+  hipLaunchKernelGGL(resolvent_operand_kernel, dim3(grid_for(nZ, 256)), dim3(256), 0, st, (const c128*)v,
+                     (const c128*)lam, n, wy, ny, 0, np_, nyp, Z);
+  QD_HIP(hipGetLastError());
+  hipLaunchKernelGGL(resolvent_operand_kernel, dim3(grid_for(nX, 256)), dim3(256), 0, st, (const c128*)a,
+                     (const c128*)lam, n, wx, nx, 1, nxp, np_, X);
+  QD_HIP(hipGetLastError());
+  if ((rc = splitk_gemm(Mp, Z, np_, np_, nyp, np_, nyp, W, slabs, S1, st))) return rc;      // W = M Z (padded)
+  return splitk_gemm(X, W, nxp, np_, nyp, nx, ny, (c128*)out, slabs, S2, st);              // out = X W
 }
 
 extern "C" int qd_resolvent_sum(const qd_c128* coeff, const qd_c128* lam, int n, const double* w, int nw,

@@ -618,6 +618,38 @@ def _deom_case(lmax, npsd, nt, dt, pulses=False, p1=True, lam=0.5, gam=1.0, beta
 
 
 @golden
+def deom_corr4():
+    """DEOMSolver.correlation_4op_3t (heom/deom.py:1127-1209): dense ADO Liouvillian (generate_propgator,
+    :769-893), eig + pinv, frequency-domain (w_x, w_y) signal; full and eigenvalue-cut variants."""
+    import contextlib
+    import io
+    from pyqed.heom.deom import DEOMSolver
+    s0 = np.eye(2, dtype=complex)
+    sx = np.array([[0, 1], [1, 0]], dtype=complex)
+    sz = np.array([[1, 0], [0, -1]], dtype=complex)
+    H = sz + sx
+    lmax, npsd = 4, 2
+    bath = _drude_bath(0.5, 1.0, 1.0, npsd)
+    solver = DEOMSolver(H, np.zeros((2, 2), complex), bath, np.array([sx]), np.zeros((1, 2, 2), complex),
+                        lambda t: 0, lambda t: 0, lmax)
+    rho0 = np.zeros((2, 2), dtype=complex)
+    rho0[0, 0] = 1
+    wx = np.linspace(-4, 4, 24)
+    wy = np.linspace(-3, 5, 20)
+    T = 0.5
+    out = dict(H=H, Q=np.array([sx]), lmax=lmax, npsd=npsd, rho0=rho0, wx=wx, wy=wy, T=T,
+               etal=bath.etal, etar=bath.etar, etaa=bath.etaa, expn=bath.expn)
+    with contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
+        for lcr in ["llll", "lrlr", "lccc"]:
+            out["cw_" + lcr] = solver.correlation_4op_3t(sx, sx, sx, sx, rho0, T, wx, wy, lcr=lcr)
+        out["cw_cut_llll"] = solver.correlation_4op_3t(sz, sx, sx, sz, rho0, T, wx, wy, if_full=False,
+                                                        cut_off_min=0.5, cut_off_max=1.1, lcr="llll")
+    out["propagator"] = solver.propgator
+    out["nmax"] = solver.nmax
+    save("deom_corr4", **out)
+
+
+@golden
 def heom_chain():
     """Single-exponential HEOM chains: HEOM/heom.py _heom (RK4, :275-347) and oqs._heom
     (in-place explicit sweep, oqs.py:1808-1875), examples/heom.py:79-97 model."""

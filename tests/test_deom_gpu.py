@@ -101,3 +101,59 @@ def test_deom_layouts_vs_oracle(ns, npsd, L):
     tt, ref, _ = od.run(H, np.zeros((ns, ns)), lambda t: 0, np.array([Q]), np.zeros((1, ns, ns)), lambda t: 0,
                         (bath.etal, bath.etar, bath.etaa, bath.expn), L, rho0, dt, nt)
     assert relerr(saved[0], ref) < TOL
+
+
+def test_deom_correlation_4op_3t_matches_reference(tmp_path, monkeypatch):
+    """DEOMSolver.correlation_4op_3t (heom/deom.py:1127-1209): host P / eig, GPU (w_x, w_y) grid."""
+    from pyqed_amd.deom import Bath, DEOMSolver
+    g = load_golden("deom_corr4")
+    sx = g["Q"][0]
+    sz = np.diag([1.0, -1.0]).astype(complex)
+    bath = Bath.__new__(Bath)
+    bath.etal, bath.etar, bath.etaa, bath.expn = g["etal"], g["etar"], g["etaa"], g["expn"]
+    bath.mode = np.zeros(len(g["expn"]), dtype=np.int64)
+    sol = DEOMSolver(g["H"], np.zeros((2, 2), complex), bath, g["Q"], np.zeros((1, 2, 2), complex),
+                     lambda t: 0, lambda t: 0, int(g["lmax"]))
+    T, wx, wy = float(g["T"]), g["wx"], g["wy"]
+    for lcr in ["llll", "lrlr", "lccc"]:
+        cw = sol.correlation_4op_3t(sx, sx, sx, sx, g["rho0"], T, wx, wy, lcr=lcr)
+        assert cw.shape == (len(wx), len(wy))
+        assert relerr(cw, g["cw_" + lcr]) < 1e-10, lcr
+    assert relerr(sol.propgator, g["propagator"]) < 1e-14
+    monkeypatch.chdir(tmp_path)
+    cw = sol.correlation_4op_3t(sz, sx, sx, sz, g["rho0"], T, wx, wy, if_full=False, lcr="llll", if_save=True)
+    # The eigenvalue cut keeps V[:, sel] and pinv(V)[sel, :] of a non-normal P: the result inherits the
+    # conditioning of LAPACK's eig (another host's OpenBLAS kernels move it by ~1e-8 relative, the
+    # reference's own output included).  Against the oracle on THIS host's eig the GPU grid is exact.
+    assert relerr(cw, g["cw_cut_llll"]) < 1e-7
+    from oracle import deom as od
+    ref_here = od.correlation_4op_3t(sol.propgator, sol.nmax, 2, [sz, sx, sx, sz], g["rho0"], T, wx, wy,
+                                     if_full=False)
+    assert relerr(cw, ref_here) < 1e-10
+    sol2 = DEOMSolver(g["H"], None, bath, g["Q"], None, None, None, int(g["lmax"]))
+    cw2 = sol2.correlation_4op_3t(sz, sx, sx, sz, g["rho0"], T, wx, wy, if_full=False, if_load=True)
+    assert relerr(cw2, cw) < 1e-12
+
+
+def test_resolvent_grid2d_ragged_sizes():
+    """qd_resolvent_grid2d against its closed form at sizes that exercise every padding path."""
+    import torch
+    from pyqed_amd import _lib
+    rng = np.random.default_rng(4)
+    dev = torch.device("cuda", 0)
+    for n, nx, ny in [(7, 5, 3), (140, 129, 300), (300, 64, 130)]:
+        lam = -rng.uniform(0.05, 2, n) + 1j * rng.uniform(-5, 5, n)
+        a, v = (rng.standard_normal(n) + 1j * rng.standard_normal(n) for _ in range(2))
+        M = rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))
+        wx, wy = np.linspace(-4, 4, nx), np.linspace(-3, 6, ny)
+        X = a[None, :] / (-lam[None, :] - 1j * wx[:, None])
+        Z = v[:, None] / (-lam[:, None] - 1j * wy[None, :])
+        ref = X @ M @ Z
+        t = lambda x, dt=torch.complex128: torch.from_numpy(np.ascontiguousarray(x)).to(device=dev, dtype=dt)
+        out = torch.empty((nx, ny), dtype=torch.complex128, device=dev)
+        args = [t(a), t(M), t(v), t(lam)]
+        wxt, wyt = t(wx, torch.float64), t(wy, torch.float64)
+        rc = _lib.load().qd_resolvent_grid2d(*(x.data_ptr() for x in args), n, wxt.data_ptr(), nx, wyt.data_ptr(),
+                                             ny, out.data_ptr(), _lib.stream_ptr(dev))
+        _lib.check(rc, "qd_resolvent_grid2d")
+        assert relerr(out.cpu().numpy(), ref) < 1e-12, (n, nx, ny)

@@ -55,3 +55,15 @@ def test_tier_sizes_bench_config():
     assert len(keys) == 6188
     sizes = np.bincount(keys.sum(1))
     assert list(sizes) == [1, 5, 15, 35, 70, 126, 210, 330, 495, 715, 1001, 1365, 1820]
+
+
+def test_ado_liouvillian_matches_reference_propagator():
+    """Dense ADO Liouvillian (generate_propgator, heom/deom.py:769-893) vs the reference's matrix."""
+    from pyqed_amd.deom import ado_coefficients, ado_liouvillian, ado_tables
+    g = load_golden("deom_corr4")
+    K = len(g["expn"])
+    keys, minus, plus, comb = ado_tables(int(g["lmax"]), K)
+    coef, damp = ado_coefficients(keys, g["etal"], g["etar"], g["etaa"], g["expn"], int(g["lmax"]))
+    P = ado_liouvillian(keys, minus, plus, coef, damp, g["H"], g["Q"], np.zeros(K, dtype=np.int64))
+    assert P.shape == g["propagator"].shape
+    assert relerr(P, g["propagator"]) < 1e-14

@@ -212,3 +212,21 @@ def test_correlation_3p_1t_oracle_matches_reference():
     assert relerr(cor, cr[:, 0]) < TOL
     td, dm = _parse_dat(g["dmdat"])
     assert np.array_equal(td, tr) and relerr(rhos.reshape(len(t), -1), dm) < TOL
+
+
+def test_deom_corr4_oracle_matches_reference():
+    from oracle import deom as od
+    g = load_golden("deom_corr4")
+    K = len(g["expn"])
+    keys, comb = od.gen_keys(int(g["lmax"]), K)
+    P = od.propagator(keys, comb, int(g["lmax"]), g["expn"], g["etal"], g["etar"], g["etaa"], np.zeros(K, int),
+                      g["H"], g["Q"])
+    assert relerr(P, g["propagator"]) < 1e-14
+    sx = g["Q"][0]
+    sz = np.diag([1.0, -1.0]).astype(complex)
+    args = (int(g["nmax"]), 2)
+    for lcr in ["llll", "lrlr", "lccc"]:
+        cw = od.correlation_4op_3t(P, *args, [sx] * 4, g["rho0"], float(g["T"]), g["wx"], g["wy"], lcr=lcr)
+        assert relerr(cw, g["cw_" + lcr]) < 1e-12, lcr
+    cw = od.correlation_4op_3t(P, *args, [sz, sx, sx, sz], g["rho0"], float(g["T"]), g["wx"], g["wy"], if_full=False)
+    assert relerr(cw, g["cw_cut_llll"]) < 1e-12
