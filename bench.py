@@ -184,16 +184,20 @@ def bench_2des_t2scan(dev, world, rank, M_total, n2, reps, n=256):
     t = 0.5 * np.arange(n)
     t2 = to(2.5 * np.arange(n2))
     out = torch.empty((n2, n, n), dtype=torch.complex128, device=dev)
-    from pyqed_amd.response import response2d_t2scan
+    from pyqed_amd.response import T2Scan
 
     from pyqed_amd.distributed import sharded_sum_buckets
     bucket = max(1, min(n2, 4))           # 4 waiting times = 4 MiB per RCCL reduce
     buckets = [slice(b, min(n2, b + bucket)) for b in range(0, n2, bucket)]
 
+    scan = [None]
+
     def local(lo_, hi_, b):               # this rank's members are resident; t2 bucket b of the scan
-        response2d_t2scan(lam_t, alpha_t, B_t, C_t, beta_t, t, t2[b], t, out=out[b])
+        scan[0].apply(t2[b], out=out[b])
 
     def once():
+        # P = X B and Q = C Y on the (t3, t1) grids, once per scan; then the buckets of waiting times
+        scan[0] = T2Scan(lam_t, alpha_t, B_t, C_t, beta_t, t, t)
         sharded_sum_buckets(local, M_total, out, buckets, dst=0)
 
     once()
@@ -220,6 +224,7 @@ def bench_2des_t2scan(dev, world, rank, M_total, n2, reps, n=256):
     torch.cuda.synchronize(dev)
     c0 = time.perf_counter()
     for _ in range(reps):
+        scan[0] = T2Scan(lam_t, alpha_t, B_t, C_t, beta_t, t, t)
         for b in buckets:
             local(lo, hi, b)
     torch.cuda.synchronize(dev)

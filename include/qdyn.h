@@ -318,16 +318,32 @@ int qd_response2d_ensemble_uniform(const qd_c128* alpha, const qd_c128* Mt,
  * n2 waiting times):
  *   out[j][i][k] (+)= (-i)^3 sum_m sum_pq alpha[m][p] e^{lam[m][p] t3_i}
  *                       (B_m diag(e^{lam_m t2_j}) C_m)[p][q] beta[m][q] e^{lam[m][q] t1_k}
- * i.e. qd_response2d_ensemble_uniform for every t2_j with Mt formed on the device from
- * B = U1^-1 b U1, C = U1^-1 c U1 [M][nL][nL].  The t3 operand is built once and all waiting times
- * share one split-K MFMA GEMM (N = n2 * n1).  Per rank: one member shard; the caller sums the
- * [n2][n3][n1] stack over ranks with ONE RCCL reduce.  nL <= 16, n1 <= 1024.
+ * i.e. qd_response2d_ensemble_uniform for every t2_j with Mt_j = B diag(e^{lam t2_j}) C, where
+ * B = U1^-1 b U1, C = U1^-1 c U1 [M][nL][nL].  Evaluated as S_j = P diag(E_j) Q with
+ * P = X B (t3 side) and Q = C Y (t1 side) built once and E_j = e^{lam t2_j} applied to Q's rows while the
+ * GEMM stages them: every waiting time shares P and Q, and all of them run in one split-K MFMA GEMM
+ * (N = n2 * n1).  Per rank: one member shard; the caller sums the [n2][n3][n1] stack over ranks
+ * (RCCL reduce).  nL <= 16, n1 <= 1024.
  */
 int qd_response2d_t2scan(const qd_c128* alpha, const qd_c128* B, const qd_c128* C,
                          const qd_c128* beta, const qd_c128* lam, int M, int nL,
                          double t3_0, double dt3, int n3, const double* t2, int n2,
                          double t1_0, double dt1, int n1, qd_c128* out, int accumulate,
                          void* stream);
+
+/* Padded operand sizes of the scan: P is [n3p][Kp], Q is [Kp][n1p] complex128. */
+int qd_response2d_t2_dims(int M, int nL, int n3, int n1, int* n3p, int* n1p, int* Kp);
+
+/* Build the scan operands P, Q into caller-owned device buffers (once per ensemble / grid). */
+int qd_response2d_t2_operands(const qd_c128* alpha, const qd_c128* B, const qd_c128* C,
+                              const qd_c128* beta, const qd_c128* lam, int M, int nL,
+                              double t3_0, double dt3, int n3, double t1_0, double dt1,
+                              int n1, qd_c128* P, qd_c128* Q, void* stream);
+
+/* out [n2][n3][n1] (+)= the scan for waiting times t2 (device array) from prepared P, Q. */
+int qd_response2d_t2_apply(const qd_c128* P, const qd_c128* Q, const qd_c128* lam, int M,
+                           int nL, int n3, int n1, const double* t2, int n2, qd_c128* out,
+                           int accumulate, void* stream);
 
 /*
  * Frequency-domain 2D signal of an eigen-decomposed generator (DEOMSolver.correlation_4op_3t,

@@ -66,6 +66,11 @@ SIGNATURES = {
     "qd_response2d_t2scan": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double,
                                      c_double, c_int, c_void_p, c_int, c_double, c_double, c_int, c_void_p, c_int,
                                      c_void_p]),
+    "qd_response2d_t2_dims": (c_int, [c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "qd_response2d_t2_operands": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double,
+                                          c_double, c_int, c_double, c_double, c_int, c_void_p, c_void_p, c_void_p]),
+    "qd_response2d_t2_apply": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                                       c_void_p, c_int, c_void_p]),
     "qd_resolvent_grid2d": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int,
                                     c_void_p, c_void_p]),
     "qd_resolvent_sum": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]),

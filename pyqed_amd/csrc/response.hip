@@ -285,56 +285,6 @@ __global__ void ens_reduce_kernel(const c128* slabs, int S, int n3, int n1, int 
   }
 }
 
-// ---- t2 scan: Z_all [Kp][n2 * n1p], column block j = waiting time t2_j (uniform t1 tables as above).
-// Member m = blockIdx.y, waiting time j = blockIdx.z: Mt_mj = B_m diag(e^{lam_m t2_j}) C_m is formed in
-// LDS (nL^3 complex MACs, r ascending like the host's B @ (e * C)), then the Z rows as ens_xz_uniform.
-__global__ __launch_bounds__(256) void ens_z_t2_kernel(const c128* Bm, const c128* Cm, const c128* beta,
-                                                       const c128* lam, const double* t2, int nL, double t0, double dt,
-                                                       int n1, int n1p, int ldz, c128* Z) {
-  __shared__ c128 sB[ZMAX * ZMAX], sCm[ZMAX * ZMAX], sM[ZMAX * ZMAX], sE[ZMAX];
-  __shared__ c128 sF[ZMAX * 16];
-  __shared__ c128 sC[ZMAX * UNI_MAXC];
-  const int m = blockIdx.y, j = blockIdx.z;
-  const int nC = n1p / 16;
-  const c128* lm = lam + (size_t)m * nL;
-  for (int e = threadIdx.x; e < nL * nL; e += 256) {
-    sB[e] = Bm[(size_t)m * nL * nL + e];
-    sCm[e] = Cm[(size_t)m * nL * nL + e];
-  }
-  for (int e = threadIdx.x; e < nL; e += 256) sE[e] = cexp_t(lm[e], t2[j]);
-  for (int e = threadIdx.x; e < nL * 16; e += 256) sF[e] = cexp_t(lm[e / 16], (double)(e % 16) * dt);
-  for (int e = threadIdx.x; e < nL * nC; e += 256)
-    sC[e] = cmul(beta[(size_t)m * nL + e / nC], cexp_t(lm[e / nC], t0 + 16.0 * (double)(e % nC) * dt));
-  __syncthreads();
-  for (int e = threadIdx.x; e < nL * nL; e += 256) {
-    const int p = e / nL, q = e % nL;
-    c128 v = cmk(0, 0);
-    for (int r = 0; r < nL; ++r) v = cadd(v, cmul(sB[p * nL + r], cmul(sE[r], sCm[r * nL + q])));
-    sM[e] = v;
-  }
-  __syncthreads();
-  const int k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= n1p) return;
-  c128 y[ZMAX];
-#pragma unroll
-  for (int q = 0; q < ZMAX; ++q)
-    y[q] = (q < nL && k < n1) ? cmul(sC[q * nC + (k >> 4)], sF[q * 16 + (k & 15)]) : cmk(0, 0);
-  for (int p = 0; p < nL; ++p) {
-    c128 v = cmk(0, 0);
-#pragma unroll
-    for (int q = 0; q < ZMAX; ++q)
-      if (q < nL) v = cadd(v, cmul(sM[p * nL + q], y[q]));
-    Z[((size_t)m * nL + p) * ldz + (size_t)j * n1p + k] = v;
-  }
-}
-
-// rows K..Kp-1 of a Z with leading dimension ldz are padding
-__global__ void ens_z_pad_ld_kernel(int K, int Kp, int ldz, c128* Z) {
-  const size_t tot = (size_t)(Kp - K) * ldz;
-  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x)
-    Z[(size_t)K * ldz + e] = cmk(0, 0);
-}
-
 // out[j][i][k] (+)= sum_s slab[s][i][j*n1p + k]   (slab leading dimension ldz = n2*n1p), fixed order
 __global__ void ens_reduce_t2_kernel(const c128* slabs, int S, int n2, int n3, int n1, int n3p, int n1p, c128* out,
                                      int accumulate) {
@@ -347,6 +297,112 @@ __global__ void ens_reduce_t2_kernel(const c128* slabs, int S, int n2, int n3, i
     c128 v = accumulate ? out[e] : cmk(0, 0);
     for (int s = 0; s < S; ++s) v = cadd(v, slabs[((size_t)s * n3p + i) * ldz + (size_t)j * n1p + k]);
     out[e] = v;
+  }
+}
+
+// ---- t2 scan without a per-t2 operand: with P_m = X_m B_m and Q_m = C_m Y_m,
+//   S_j = sum_m P_m diag(e^{lam_m t2_j}) Q_m = P * diag(E_j) * Q,   E_j[(m,r)] = e^{lam_mr t2_j},
+// so P [n3p][Kp] and Q [Kp][n1p] are built once per scan and the GEMM's B operand for waiting time j is
+// Q with its rows scaled by E_j, formed in the staging step (one complex multiply per staged element).
+// P block: MB = floor(256 / nL) members (MB nL columns), UNI_ROWS rows; the X values of a 16-row group go
+// through LDS and every column thread contracts them with its B_m[:, r] (registers).
+__global__ __launch_bounds__(256) void ens_p_uniform_kernel(const c128* alpha, const c128* Bm, const c128* lam, int M,
+                                                            int nL, double t0, double dt, int n3, int n3p, int Kp,
+                                                            c128* P) {
+  __shared__ c128 sX[16 * 256];
+  const int MB = 256 / nL, W = MB * nL;
+  const int m0 = blockIdx.x * MB;
+  const int c = threadIdx.x;                 // column of this block: member m0 + c / nL, index c % nL
+  const int m = m0 + c / nL, r = c % nL;
+  const bool col = c < W && m < M;
+  const int kk = m * nL + r;
+  const int i0 = blockIdx.y * UNI_ROWS;
+  // X part: this thread's x_{m r}(t) = i alpha_mr e^{lam_mr t} (the column it also owns in sX)
+  const c128 l = col ? lam[kk] : cmk(0, 0);
+  const c128 a = col ? cmuli(alpha[kk]) : cmk(0, 0);
+  c128 T1[16];
+  T1[0] = cmk(1, 0);
+  const c128 st = cexp_t(l, dt);
+#pragma unroll
+  for (int j = 1; j < 16; ++j) T1[j] = cmul(T1[j - 1], st);
+  c128 b[ZMAX];
+#pragma unroll
+  for (int p = 0; p < ZMAX; ++p) b[p] = (col && p < nL) ? Bm[((size_t)m * nL + p) * nL + r] : cmk(0, 0);
+  const int mc0 = (c / nL) * nL;             // first column of this thread's member in the block
+  for (int g = 0; g < UNI_ROWS / 16; ++g) {
+    const int ib = i0 + 16 * g;
+    const c128 base = cmul(a, cexp_t(l, t0 + (double)ib * dt));
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 16; ++j) sX[j * 256 + c] = cmul(base, T1[j]);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int i = ib + j;
+      if (i >= n3p) break;
+      c128 v = cmk(0, 0);
+      if (col && i < n3) {
+#pragma unroll
+        for (int p = 0; p < ZMAX; ++p)
+          if (p < nL) v = cadd(v, cmul(sX[j * 256 + mc0 + p], b[p]));
+      }
+      if (c < W && kk < Kp) P[(size_t)i * Kp + kk] = v;
+    }
+  }
+}
+
+// columns K..Kp-1 of P are padding (the member blocks cover columns < K only)
+__global__ void ens_p_pad_kernel(int K, int Kp, int n3p, c128* P) {
+  const int w = Kp - K;
+  const size_t tot = (size_t)n3p * w;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x)
+    P[(e / w) * Kp + K + e % w] = cmk(0, 0);
+}
+
+// E [n2][Kp]: e^{lam_kk t2_j}, zero in the padding
+__global__ void ens_e_kernel(const c128* lam, int K, int Kp, const double* t2, int n2, c128* E) {
+  const size_t tot = (size_t)n2 * Kp;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    const int kk = (int)(e % Kp), j = (int)(e / Kp);
+    E[e] = kk < K ? cexp_t(lam[kk], t2[j]) : cmk(0, 0);
+  }
+}
+
+struct EnsQEB {
+  struct Raw { cg_v2 q, e; };
+  const c128* Q;
+  const c128* Ej;   // E row of this column block's waiting time
+  int n1p, col0, k0;
+  __device__ __forceinline__ Raw fetch(int t, int e, int) const {
+    const int row = k0 + t * CG_KT + e / ENS_BT;
+    return Raw{cg_ld(Q + (size_t)row * n1p + col0 + (e % ENS_BT)), cg_ld(Ej + row)};
+  }
+  __device__ __forceinline__ cg_v2 finish(const Raw& r, int, int, int) const {
+    const c128 v = cmul(cmk(r.e.x, r.e.y), cmk(r.q.x, r.q.y));
+    return cg_v2{v.re, v.im};
+  }
+};
+
+// grid: (n2 * n1p / BT) x (n3p / BT) x S; column block bn is waiting time (bn * BT) / n1p
+__global__ __launch_bounds__(CG_WG) void ens_t2_gemm_kernel(const c128* P, int Kp, const c128* Q, int n1p,
+                                                            const c128* E, int tiles, int S, c128* slabs, int n3p,
+                                                            int ldz) {
+  __shared__ CgLds<ENS_BT> L;
+  const int bn = blockIdx.x, bm = blockIdx.y, s = blockIdx.z;
+  const int t0 = (int)((long)tiles * s / S), t1 = (int)((long)tiles * (s + 1) / S);
+  const int j = (bn * ENS_BT) / n1p, colq = (bn * ENS_BT) % n1p;
+  CgAcc<ENS_BT> A;
+  c128* slab = slabs + (size_t)s * n3p * ldz;
+  if (t1 > t0) {
+    EnsXA pa{P, Kp, bm * ENS_BT, t0 * CG_KT};
+    EnsQEB pb{Q, E + (size_t)j * Kp, n1p, colq, t0 * CG_KT};
+    cg_block_gemm_gen<ENS_BT>(t1 - t0, pa, pb, L, A);
+    cg_epilogue<ENS_BT>(A, [&](int row, int col, c128 v) {
+      slab[(size_t)(bm * ENS_BT + row) * ldz + bn * ENS_BT + col] = v;
+    });
+  } else {
+    for (int e = threadIdx.x; e < ENS_BT * ENS_BT; e += CG_WG)
+      slab[(size_t)(bm * ENS_BT + e / ENS_BT) * ldz + bn * ENS_BT + e % ENS_BT] = cmk(0, 0);
   }
 }
 
@@ -552,6 +608,92 @@ extern "C" int qd_response2d_ensemble_uniform(const qd_c128* alpha, const qd_c12
                  dt1, n1, out, accumulate, stream);
 }
 
+namespace {
+struct T2Dims {
+  int n3p, n1p, K, Kp, tiles;
+};
+T2Dims t2_dims(int M, int nL, int n3, int n1) {
+  T2Dims d;
+  d.n3p = ceil_div(n3, ENS_BT) * ENS_BT;
+  d.n1p = ceil_div(n1, ENS_BT) * ENS_BT;
+  d.K = M * nL;
+  d.tiles = ceil_div(d.K, CG_KT);
+  d.Kp = d.tiles * CG_KT;
+  return d;
+}
+}  // namespace
+
+extern "C" int qd_response2d_t2_dims(int M, int nL, int n3, int n1, int* n3p, int* n1p, int* Kp) {
+  QD_CHECK_ARG(n3p && n1p && Kp, "qd_response2d_t2_dims: null pointer");
+  QD_CHECK_ARG(M >= 1 && nL >= 1 && n3 >= 1 && n1 >= 1, "qd_response2d_t2_dims: bad sizes");
+  const T2Dims d = t2_dims(M, nL, n3, n1);
+  *n3p = d.n3p;
+  *n1p = d.n1p;
+  *Kp = d.Kp;
+  return QD_OK;
+}
+
+extern "C" int qd_response2d_t2_operands(const qd_c128* alpha, const qd_c128* Bm, const qd_c128* Cm,
+                                         const qd_c128* beta, const qd_c128* lam, int M, int nL, double t3_0,
+                                         double dt3, int n3, double t1_0, double dt1, int n1, qd_c128* P_,
+                                         qd_c128* Q_, void* stream) {
+  const char* fn = "qd_response2d_t2_operands";
+  QD_CHECK_ARG(alpha && Bm && Cm && beta && lam && P_ && Q_, "%s: null pointer", fn);
+  QD_CHECK_ARG(M >= 1 && nL >= 1 && n3 >= 1 && n1 >= 1, "%s: bad sizes", fn);
+  QD_CHECK_ARG(nL <= ZMAX && n1 <= 16 * UNI_MAXC, "%s: nL=%d (<= %d), n1=%d (<= %d)", fn, nL, ZMAX, n1, 16 * UNI_MAXC);
+  QD_CHECK_ARG(M <= 65535 && (long)M * nL < (1L << 30), "%s: M=%d too large", fn, M);
+  hipStream_t st = (hipStream_t)stream;
+  const T2Dims d = t2_dims(M, nL, n3, n1);
+  c128* P = (c128*)P_;
+  c128* Q = (c128*)Q_;
+  const int MB = 256 / nL;
+  hipLaunchKernelGGL(ens_p_uniform_kernel, dim3(ceil_div(M, MB), d.n3p / UNI_ROWS), dim3(256), 0, st,
+                     (const c128*)alpha, (const c128*)Bm, (const c128*)lam, M, nL, t3_0, dt3, n3, d.n3p, d.Kp, P);
+  QD_HIP(hipGetLastError());
+  if (d.Kp > d.K) {
+    hipLaunchKernelGGL(ens_p_pad_kernel, dim3(64), dim3(256), 0, st, d.K, d.Kp, d.n3p, P);
+    QD_HIP(hipGetLastError());
+  }
+  // Q = C_m Y_m: the uniform Z build with Mt := C (Z rows only)
+  hipLaunchKernelGGL(ens_xz_uniform_kernel, dim3(ceil_div(d.n1p, 256), M), dim3(256), 0, st, (const c128*)Cm,
+                     (const c128*)beta, (const c128*)lam, M, nL, t1_0, dt1, n1, d.n1p, d.Kp, Q, (const c128*)nullptr,
+                     d.K, 0.0, 0.0, n3, d.n3p, 1, (c128*)nullptr);
+  QD_HIP(hipGetLastError());
+  if (d.Kp > d.K) {
+    hipLaunchKernelGGL(ens_z_pad_kernel, dim3(64), dim3(256), 0, st, d.K, d.Kp, d.n1p, Q);
+    QD_HIP(hipGetLastError());
+  }
+  return QD_OK;
+}
+
+extern "C" int qd_response2d_t2_apply(const qd_c128* P, const qd_c128* Q, const qd_c128* lam, int M, int nL, int n3,
+                                      int n1, const double* t2, int n2, qd_c128* out, int accumulate, void* stream) {
+  const char* fn = "qd_response2d_t2_apply";
+  QD_CHECK_ARG(P && Q && lam && t2 && out, "%s: null pointer", fn);
+  QD_CHECK_ARG(M >= 1 && nL >= 1 && n3 >= 1 && n1 >= 1 && n2 >= 1 && n2 <= 65535, "%s: bad sizes", fn);
+  hipStream_t st = (hipStream_t)stream;
+  const T2Dims d = t2_dims(M, nL, n3, n1);
+  const long ldz = (long)n2 * d.n1p;
+  QD_CHECK_ARG(ldz / ENS_BT <= 65535, "%s: n2*n1 too large", fn);
+  const int blocks2d = (int)((d.n3p / ENS_BT) * (ldz / ENS_BT));
+  const int S = std::max(1, std::min(ceil_div(256, blocks2d), std::max(1, d.tiles / 4)));
+  const size_t nE = (size_t)n2 * d.Kp, nsl = (size_t)S * d.n3p * ldz;
+  void* w = nullptr;
+  int rc = workspace(WS_2DES, (nE + nsl) * sizeof(c128), &w);
+  if (rc) return rc;
+  c128* E = (c128*)w;
+  c128* slabs = E + nE;
+  hipLaunchKernelGGL(ens_e_kernel, dim3(grid_for(nE, 256)), dim3(256), 0, st, (const c128*)lam, d.K, d.Kp, t2, n2, E);
+  QD_HIP(hipGetLastError());
+  hipLaunchKernelGGL(ens_t2_gemm_kernel, dim3((int)(ldz / ENS_BT), d.n3p / ENS_BT, S), dim3(CG_WG), 0, st,
+                     (const c128*)P, d.Kp, (const c128*)Q, d.n1p, (const c128*)E, d.tiles, S, slabs, d.n3p, (int)ldz);
+  QD_HIP(hipGetLastError());
+  hipLaunchKernelGGL(ens_reduce_t2_kernel, dim3(grid_for((size_t)n2 * n3 * n1, 256)), dim3(256), 0, st, slabs, S, n2,
+                     n3, n1, d.n3p, d.n1p, (c128*)out, accumulate);
+  QD_HIP(hipGetLastError());
+  return QD_OK;
+}
+
 extern "C" int qd_response2d_t2scan(const qd_c128* alpha, const qd_c128* Bm, const qd_c128* Cm, const qd_c128* beta,
                                     const qd_c128* lam, int M, int nL, double t3_0, double dt3, int n3,
                                     const double* t2, int n2, double t1_0, double dt1, int n1, qd_c128* out,
@@ -559,46 +701,15 @@ extern "C" int qd_response2d_t2scan(const qd_c128* alpha, const qd_c128* Bm, con
   const char* fn = "qd_response2d_t2scan";
   QD_CHECK_ARG(alpha && Bm && Cm && beta && lam && t2 && out, "%s: null pointer", fn);
   QD_CHECK_ARG(M >= 1 && nL >= 1 && n3 >= 1 && n1 >= 1 && n2 >= 1, "%s: bad sizes", fn);
-  QD_CHECK_ARG(nL <= ZMAX && n1 <= 16 * UNI_MAXC, "%s: nL=%d (<= %d), n1=%d (<= %d)", fn, nL, ZMAX, n1, 16 * UNI_MAXC);
-  QD_CHECK_ARG(M <= 65535 && n2 <= 65535 && (long)M * nL < (1L << 30), "%s: M=%d n2=%d too large", fn, M, n2);
-  hipStream_t st = (hipStream_t)stream;
-  const int BT = ENS_BT;
-  const int n3p = ceil_div(n3, BT) * BT, n1p = ceil_div(n1, BT) * BT;
-  const long ldz = (long)n2 * n1p;
-  QD_CHECK_ARG(ldz / BT <= 65535, "%s: n2*n1 too large", fn);
-  const int K = M * nL;
-  const int tiles = ceil_div(K, CG_KT);
-  const int Kp = tiles * CG_KT;
-  const int blocks2d = (int)((n3p / BT) * (ldz / BT));
-  // all waiting times share one GEMM (N = n2 * n1p): more output blocks, less split-K
-  int S = std::max(1, std::min(ceil_div(256, blocks2d), std::max(1, tiles / 4)));
-  const size_t nx = (size_t)n3p * Kp, nz = (size_t)Kp * ldz, nsl = (size_t)S * n3p * ldz;
+  const T2Dims d = t2_dims(M, nL, n3, n1);
   void* w = nullptr;
-  int rc = workspace(WS_2DES, (nx + nz + nsl) * sizeof(c128), &w);
+  int rc = workspace(WS_2DES_OPS, ((size_t)d.n3p * d.Kp + (size_t)d.Kp * d.n1p) * sizeof(c128), &w);
   if (rc) return rc;
-  c128* X = (c128*)w;
-  c128* Z = X + nx;
-  c128* slabs = Z + nz;
-  const int xbx = ceil_div(Kp, 256), xblocks = xbx * (n3p / UNI_ROWS);
-  hipLaunchKernelGGL(ens_xz_uniform_kernel, dim3(1, xblocks), dim3(256), 0, st, (const c128*)nullptr,
-                     (const c128*)nullptr, (const c128*)lam, 0, nL, 0.0, 0.0, n1, n1p, Kp, (c128*)nullptr,
-                     (const c128*)alpha, K, t3_0, dt3, n3, n3p, xbx, X);
-  QD_HIP(hipGetLastError());
-  const int zbx = ceil_div(n1p, 256);
-  hipLaunchKernelGGL(ens_z_t2_kernel, dim3(zbx, M, n2), dim3(256), 0, st, (const c128*)Bm, (const c128*)Cm,
-                     (const c128*)beta, (const c128*)lam, t2, nL, t1_0, dt1, n1, n1p, (int)ldz, Z);
-  QD_HIP(hipGetLastError());
-  if (Kp > K) {
-    hipLaunchKernelGGL(ens_z_pad_ld_kernel, dim3(64), dim3(256), 0, st, K, Kp, (int)ldz, Z);
-    QD_HIP(hipGetLastError());
-  }
-  hipLaunchKernelGGL(ens_gemm_kernel, dim3((int)(ldz / BT), n3p / BT, S), dim3(CG_WG), 0, st, X, Kp, Z, (int)ldz,
-                     tiles, S, slabs, n3p);
-  QD_HIP(hipGetLastError());
-  hipLaunchKernelGGL(ens_reduce_t2_kernel, dim3(grid_for((size_t)n2 * n3 * n1, 256)), dim3(256), 0, st, slabs, S, n2,
-                     n3, n1, n3p, n1p, (c128*)out, accumulate);
-  QD_HIP(hipGetLastError());
-  return QD_OK;
+  qd_c128* P = (qd_c128*)w;
+  qd_c128* Q = P + (size_t)d.n3p * d.Kp;
+  if ((rc = qd_response2d_t2_operands(alpha, Bm, Cm, beta, lam, M, nL, t3_0, dt3, n3, t1_0, dt1, n1, P, Q, stream)))
+    return rc;
+  return qd_response2d_t2_apply(P, Q, lam, M, nL, n3, n1, t2, n2, out, accumulate, stream);
 }
 
 namespace {

@@ -190,3 +190,50 @@ def response2d_t2scan(lam, alpha, B, C, beta, t3, t2, t1, out=None, accumulate=F
                                               u1[1], n1, out.data_ptr(), int(bool(accumulate)), _lib.stream_ptr(dev))
     _lib.check(rc, "qd_response2d_t2scan")
     return out
+
+
+class T2Scan:
+    """Waiting-time scan with operands prepared once (qd_response2d_t2_operands): P = X B on the t3 grid and
+    Q = C Y on the t1 grid live in caller-owned device tensors; apply(t2, out) evaluates any subset of
+    waiting times (e.g. one bucket of a bucketed, overlapped reduce) without rebuilding them."""
+
+    def __init__(self, lam, alpha, B, C, beta, t3, t1, device=None):
+        import ctypes
+        dev = device or default_device()
+        _lib.ensure_device(dev)
+        self.dev = dev
+        self.lam, alpha, B, C, beta = (x if isinstance(x, torch.Tensor) else _t(x, dev)
+                                       for x in (lam, alpha, B, C, beta))
+        self.M, self.nL = alpha.shape
+        u3, u1 = _uniform(t3), _uniform(t1)
+        if u3 is None or u1 is None:
+            raise ValueError("T2Scan: t3 and t1 must be uniform host grids")
+        self.n3, self.n1 = np.asarray(t3).size, np.asarray(t1).size
+        dims = [ctypes.c_int() for _ in range(3)]
+        lib = _lib.load()
+        _lib.check(lib.qd_response2d_t2_dims(self.M, self.nL, self.n3, self.n1, *(ctypes.byref(d) for d in dims)),
+                   "qd_response2d_t2_dims")
+        n3p, n1p, Kp = (d.value for d in dims)
+        self.P = torch.empty((n3p, Kp), dtype=torch.complex128, device=dev)
+        self.Q = torch.empty((Kp, n1p), dtype=torch.complex128, device=dev)
+        with torch.cuda.device(dev):
+            rc = lib.qd_response2d_t2_operands(alpha.data_ptr(), B.data_ptr(), C.data_ptr(), beta.data_ptr(),
+                                               self.lam.data_ptr(), self.M, self.nL, u3[0], u3[1], self.n3, u1[0],
+                                               u1[1], self.n1, self.P.data_ptr(), self.Q.data_ptr(),
+                                               _lib.stream_ptr(dev))
+        _lib.check(rc, "qd_response2d_t2_operands")
+
+    def apply(self, t2, out=None, accumulate=False):
+        t2t = t2 if isinstance(t2, torch.Tensor) else _t(np.atleast_1d(np.asarray(t2, float)), self.dev, torch.float64)
+        n2 = t2t.numel()
+        if out is None:
+            out = torch.empty((n2, self.n3, self.n1), dtype=torch.complex128, device=self.dev)
+            accumulate = False
+        if tuple(out.shape) != (n2, self.n3, self.n1) or not out.is_contiguous():
+            raise ValueError(f"out must be a contiguous [{n2}, {self.n3}, {self.n1}] tensor")
+        with torch.cuda.device(self.dev):
+            rc = _lib.load().qd_response2d_t2_apply(self.P.data_ptr(), self.Q.data_ptr(), self.lam.data_ptr(), self.M,
+                                                    self.nL, self.n3, self.n1, t2t.data_ptr(), n2, out.data_ptr(),
+                                                    int(bool(accumulate)), _lib.stream_ptr(self.dev))
+        _lib.check(rc, "qd_response2d_t2_apply")
+        return out

@@ -237,3 +237,23 @@ def test_t2scan_equals_per_t2_ensemble(M, n3, n1):
         response2d_t2scan(lam[lo:hi], alpha[lo:hi], B[lo:hi], C[lo:hi], beta[lo:hi], t3, t2, t1, out=part,
                           accumulate=True)
     assert relerr(part.cpu().numpy(), scan) < 1e-13
+
+
+def test_t2scan_prepared_operands_buckets():
+    """T2Scan: operands once, waiting times applied in buckets == the one-shot scan."""
+    from pyqed_amd.response import T2Scan, response2d_t2scan
+    rng = np.random.default_rng(21)
+    M, nL = 50, 9
+    lam = -rng.uniform(0.01, 0.2, (M, nL)) + 1j * rng.uniform(-2, 2, (M, nL))
+    alpha, beta = (rng.standard_normal((M, nL)) + 1j * rng.standard_normal((M, nL)) for _ in range(2))
+    B, C = (rng.standard_normal((M, nL, nL)) + 1j * rng.standard_normal((M, nL, nL)) for _ in range(2))
+    t3, t1, t2 = 0.5 * np.arange(140), 0.3 * np.arange(200), np.array([0.0, 0.7, 3.1, 9.0, 20.0])
+    full = response2d_t2scan(lam, alpha, B, C, beta, t3, t2, t1).cpu().numpy()
+    sc = T2Scan(lam, alpha, B, C, beta, t3, t1)
+    parts = np.concatenate([sc.apply(t2[:2]).cpu().numpy(), sc.apply(t2[2:]).cpu().numpy()])
+    assert relerr(parts, full) < 1e-14
+    # closed form for one waiting time
+    j = 3
+    ref = sum((alpha[m][None, :] * np.exp(np.outer(t3, lam[m]))) @ (B[m] * np.exp(lam[m] * t2[j])[None, :]) @ C[m]
+              @ (beta[m][:, None] * np.exp(np.outer(lam[m], t1))) for m in range(M)) * (-1j) ** 3
+    assert relerr(full[j], ref) < 1e-12
