@@ -34,6 +34,8 @@ extern "C" {
 #define QD_ERCCL -3    /* RCCL error                                           */
 #define QD_ENOMEM -4   /* workspace allocation failed                          */
 
+#define QD_COMM_ID_BYTES 128  /* size of the RCCL unique id qd_comm_unique_id writes */
+
 typedef struct qd_c128 {
   double re;
   double im;
@@ -396,6 +398,17 @@ int qd_fft_axis(qd_c128* data, int outer, int n, int inner, int inverse,
 int qd_dft2(const double* x, int nx, const double* y, int ny, const qd_c128* f,
             const double* kx, int nkx, const double* ky, int nky,
             double weight, qd_c128* out, void* stream);
+
+/*
+ * RCCL (one communicator per process, one process per GPU) for hosts without torch.distributed:
+ * rank 0 calls qd_comm_unique_id and ships the QD_COMM_ID_BYTES bytes (host memory) to every rank,
+ * which calls qd_comm_init.  qd_reduce_sum sums the complex128 buffer of every rank in place into
+ * `root` (the single reduce of a member-sharded 2DES grid / waiting-time stack).
+ */
+int qd_comm_unique_id(void* uid);
+int qd_comm_init(int nranks, int rank, const void* uid);
+int qd_reduce_sum(qd_c128* buf, size_t n, int root, void* stream);
+int qd_comm_destroy(void);
 
 #ifdef __cplusplus
 }

@@ -71,6 +71,10 @@ SIGNATURES = {
                                           c_double, c_int, c_double, c_double, c_int, c_void_p, c_void_p, c_void_p]),
     "qd_response2d_t2_apply": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
                                        c_void_p, c_int, c_void_p]),
+    "qd_comm_unique_id": (c_int, [c_void_p]),
+    "qd_comm_init": (c_int, [c_int, c_int, c_void_p]),
+    "qd_reduce_sum": (c_int, [c_void_p, c_size_t, c_int, c_void_p]),
+    "qd_comm_destroy": (c_int, []),
     "qd_resolvent_grid2d": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int,
                                     c_void_p, c_void_p]),
     "qd_resolvent_sum": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]),

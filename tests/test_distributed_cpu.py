@@ -138,3 +138,26 @@ def test_shard_range_partition():
             assert max(sizes) - min(sizes) <= 1
     with pytest.raises(ValueError):
         shard_range(4, 2, 2)
+
+
+@pytest.mark.gpu
+def test_native_rccl_reduce_single_rank():
+    """The C-ABI's own RCCL path (qd_comm_* / qd_reduce_sum) on a one-rank communicator: the reduce of one
+    contribution is the identity, errors come back as return codes."""
+    import ctypes
+    from pyqed_amd import _lib
+    lib = _lib.load()
+    dev = torch.device("cuda", 0)
+    uid = ctypes.create_string_buffer(128)
+    _lib.check(lib.qd_comm_unique_id(uid), "qd_comm_unique_id")
+    _lib.check(lib.qd_comm_init(1, 0, uid), "qd_comm_init")
+    try:
+        x = torch.randn(1000, dtype=torch.complex128, device=dev)
+        ref = x.clone()
+        _lib.check(lib.qd_reduce_sum(x.data_ptr(), x.numel(), 0, _lib.stream_ptr(dev)), "qd_reduce_sum")
+        torch.cuda.synchronize(dev)
+        assert torch.equal(x, ref)
+        assert lib.qd_reduce_sum(x.data_ptr(), x.numel(), 1, _lib.stream_ptr(dev)) != 0   # bad root
+        assert lib.qd_comm_init(1, 0, uid) != 0                                            # double init
+    finally:
+        _lib.check(lib.qd_comm_destroy(), "qd_comm_destroy")
