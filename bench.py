@@ -220,15 +220,23 @@ def bench_2des_t2scan(dev, world, rank, M_total, n2, reps, n=256):
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     wall = float(tt.item())
-    # compute-only time of this rank's launch sequence (no collective), for the scaling breakdown
+    # compute-only time of this rank's launch sequence (no collective), for the scaling breakdown;
+    # HIP events around the bucket applies (E table + the t2 GEMM + slab reduction) give the
+    # dominant kernel's rate as a lower bound (rocprof's kernel-only average is in profiles/)
     torch.cuda.synchronize(dev)
     c0 = time.perf_counter()
+    ev_apply = 0.0
     for _ in range(reps):
         scan[0] = T2Scan(lam_t, alpha_t, B_t, C_t, beta_t, t, t)
+        a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a0.record(stream)
         for b in buckets:
             local(lo, hi, b)
-    torch.cuda.synchronize(dev)
+        a1.record(stream)
+        torch.cuda.synchronize(dev)
+        ev_apply += a0.elapsed_time(a1) / 1e3
     comp = (time.perf_counter() - c0) / reps
+    ev_apply /= reps
     Kp = ((hi - lo) * 9 + 15) // 16 * 16
     gemm_flop = 8.0 * n * n * n2 * Kp
     return {
@@ -242,6 +250,12 @@ def bench_2des_t2scan(dev, world, rank, M_total, n2, reps, n=256):
         "ms_per_scan": round(wall / reps * 1e3, 4),
         "compute_ms_per_scan": round(comp * 1e3, 4),
         "gemm_tflops": round(gemm_flop / comp / 1e12, 2),
+        "roofline": {"bound": "mfma", "kernel": "ens_t2_gemm_kernel", "achieved": round(gemm_flop / ev_apply / 1e12, 3),
+                     "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(gemm_flop / ev_apply / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
+                     "flop_per_scan": gemm_flop, "traffic": None,
+                     "note": "8 n3 n1 n2 K flop per scan (K = members x nL) / event time of the bucket applies "
+                             "(E table + GEMM + slab reduction): a lower bound on the GEMM kernel's own rate"},
     }
 
 

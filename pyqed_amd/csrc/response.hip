@@ -252,11 +252,26 @@ struct EnsZB {
   __device__ __forceinline__ cg_v2 finish(const Raw& r, int, int, int) const { return r; }
 };
 
+// XCD-aware tile order for the split-K GEMMs (speed only: any placement computes the same tiles).
+// Workgroups are dealt round-robin over the 8 XCDs, so linear id L runs on XCD L % 8.  Tile u (column
+// block fastest, then row block, then K split) is given to L with u = (L % 8) * (T / 8) + L / 8: each
+// XCD owns a contiguous run of tiles, i.e. whole rows of column blocks that share one A (P / X) K-range
+// and neighbouring row blocks that share B (Q / Z) tiles, in its own L2.  Identity when T % 8 != 0.
+__device__ __forceinline__ void ens_tile(int& bn, int& bm, int& s) {
+  const int NX = gridDim.x, NY = gridDim.y, T = NX * NY * gridDim.z;
+  const int L = blockIdx.x + NX * (blockIdx.y + NY * blockIdx.z);
+  const int u = (T % 8 == 0) ? (L % 8) * (T / 8) + L / 8 : L;
+  bn = u % NX;
+  bm = (u / NX) % NY;
+  s = u / (NX * NY);
+}
+
 // grid: (n1p/BT) x (n3p/BT) x S ; each workgroup accumulates K-tiles [t0, t1) of its block
 __global__ __launch_bounds__(CG_WG) void ens_gemm_kernel(const c128* X, int Kp, const c128* Z, int n1p, int tiles,
                                                          int S, c128* slabs, int n3p) {
   __shared__ CgLds<ENS_BT> L;
-  const int bn = blockIdx.x, bm = blockIdx.y, s = blockIdx.z;
+  int bn, bm, s;
+  ens_tile(bn, bm, s);
   const int t0 = (int)((long)tiles * s / S), t1 = (int)((long)tiles * (s + 1) / S);
   CgAcc<ENS_BT> A;
   c128* slab = slabs + (size_t)s * n3p * n1p;
@@ -388,7 +403,8 @@ __global__ __launch_bounds__(CG_WG) void ens_t2_gemm_kernel(const c128* P, int K
                                                             const c128* E, int tiles, int S, c128* slabs, int n3p,
                                                             int ldz) {
   __shared__ CgLds<ENS_BT> L;
-  const int bn = blockIdx.x, bm = blockIdx.y, s = blockIdx.z;
+  int bn, bm, s;
+  ens_tile(bn, bm, s);
   const int t0 = (int)((long)tiles * s / S), t1 = (int)((long)tiles * (s + 1) / S);
   const int j = (bn * ENS_BT) / n1p, colq = (bn * ENS_BT) % n1p;
   CgAcc<ENS_BT> A;
