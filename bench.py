@@ -83,6 +83,82 @@ def cpu_baseline(N, nc, dt, budget_s=10.0):
     }
 
 
+def redfield_inputs(N, seed=5):
+    """Redfield N = 128 (BASELINE.json configs[1]): GUE H / sqrt(N), one Hermitian a_op
+    (0.2 (A + A^+)/2 / sqrt(N)), flat spectrum S = 0.05.  Returns the solver (host setup done)."""
+    from pyqed_amd import RedfieldSolver
+    rng = np.random.default_rng(seed)
+    a = rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N))
+    H = (a + a.conj().T) / 2 / np.sqrt(N)
+    x = rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N))
+    a_op = 0.2 * (x + x.conj().T) / 2 / np.sqrt(N)
+    sol = RedfieldSolver(H, c_ops=[a_op], spectra=[lambda w: 0.05 + 0.0 * w])
+    sol.redfield_tensor()
+    return sol
+
+
+def bench_redfield(dev, steps, B, N=128, dt=1e-3, warmup=3):
+    """Redfield propagation in the H eigenbasis (RedfieldSolver.evolve's kernel, Hermitian-state GLF form:
+    X = P rho + A rho Lam^+, d rho/dt = X + X^+), B independent density matrices."""
+    import torch
+    from oracle import lindblad as olb
+    from pyqed_amd.oqs import glf_rk4
+    sol = redfield_inputs(N)
+    P, Ls, Ws = sol.glf_terms_herm()
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(np.asarray(x, complex))).to(dev)
+    Pd, Ld, Wd = t(P), t(Ls), t(Ws)
+    rho = t(olb.random_pure_states(B, N, seed=7))
+    glf_rk4(Pd, None, Ld, Wd, rho, dt, warmup, hermitian=True)
+    torch.cuda.synchronize(dev)
+    stream = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    glf_rk4(Pd, None, Ld, Wd, rho, dt, steps, hermitian=True)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    kern = e0.elapsed_time(e1) / 1e3
+    flops = lindblad_flops_per_step(N, len(Ls), hermitian=True) * B * steps
+    tr = torch.diagonal(rho, dim1=1, dim2=2).sum(-1)
+    return {
+        "value": round(B * steps / wall, 1), "unit": "density-matrix steps/s",
+        "config": {"workload": "redfield_n128_rk4_fp64 (BASELINE.json configs[1], Redfield half)", "N": N,
+                   "n_a_ops": len(Ls), "batch": B, "dt": dt, "kernel": "qd_glf_rk4_herm"},
+        "roofline": {"bound": "mfma", "kernel": "lindblad_rk4_kernel<128,herm> (GLF operands)",
+                     "achieved": round(flops / kern / 1e12, 3), "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(flops / kern / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
+                     "flop_per_dm_step": lindblad_flops_per_step(N, len(Ls), hermitian=True), "traffic": None},
+        "trace_err": float((tr - 1).abs().max().item()),
+    }, sol
+
+
+def cpu_baseline_redfield(sol, dt=1e-3, budget_s=5.0):
+    """NumPy port of the same RHS (dense GLF form, BLAS threads as set), one density matrix."""
+    from oracle import lindblad as olb
+    P, Q, Ls, Rs = sol.glf_terms()
+    N = P.shape[0]
+    rho = olb.random_pure_states(1, N, seed=7)[0]
+
+    def rhs(r):
+        out = P @ r + r @ Q
+        for L, R in zip(Ls, Rs):
+            out = out + L @ r @ R
+        return out
+
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        rho = olb.rk4(rho, rhs, dt)
+        steps += 1
+    el = time.perf_counter() - t0
+    threads = os.environ.get("OMP_NUM_THREADS") or os.environ.get("OPENBLAS_NUM_THREADS") or str(os.cpu_count())
+    return {"value": round(steps / el, 3), "unit": "density-matrix steps/s", "cores": int(threads) if threads.isdigit()
+            else threads, "kind": "port",
+            "sample": f"1 density matrix, N={N}, {steps} RK4 steps of the dense NumPy GLF form of R vec(rho) "
+                      f"(oqs.py:519-570 in the eigenbasis) in {el:.1f}s; the reference's csr R (N^4 = 2.7e8 "
+                      f"nonzeros) runs ~0.42 steps/s here (SURVEY.md §8(a5))"}
+
+
 def twodes_inputs(M, seed=3):
     """BASELINE config d5: 3-level ladder E=[0,1,1.5] + static disorder (seed 3), Redfield with
     a_op = diag(0,1,2), flat spectrum 0.05, signature 'lccc', t2 = 0, t1 = t3 = 0.5*arange(256)."""
@@ -445,6 +521,7 @@ def main():
     ap.add_argument("--deom-steps", type=int, default=200)
     ap.add_argument("--deom-batch", type=int, default=64)
     ap.add_argument("--no-deom", action="store_true")
+    ap.add_argument("--no-redfield", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -518,6 +595,10 @@ def main():
         if args.t2 > 0:
             twodes["t2scan"] = bench_2des_t2scan(dev, world, rank, args.ens, args.t2, args.t2_reps)
 
+    redfield = None
+    if not args.no_redfield:
+        redfield, rf_sol = bench_redfield(dev, args.steps, B)
+
     spo = None
     if not args.no_spo:
         spo = bench_spo2(dev, args.spo_steps)
@@ -572,6 +653,10 @@ def main():
             if world == 1 and not args.no_cpu:
                 twodes["cpu_baseline"] = cpu_baseline_2des(*ens_in)
             out.setdefault("secondary", {})["2des"] = twodes
+        if redfield is not None:
+            if world == 1 and not args.no_cpu:
+                redfield["cpu_baseline"] = cpu_baseline_redfield(rf_sol)
+            out.setdefault("secondary", {})["redfield"] = redfield
         if spo is not None:
             if world == 1 and not args.no_cpu:
                 spo["cpu_baseline"] = cpu_baseline_spo2()

@@ -112,6 +112,17 @@ int qd_glf_rk4(const qd_c128* P, const qd_c128* Q, const qd_c128* L,
                qd_c128* snap, int save_every, void* stream);
 
 /*
+ * Hermitian-state GLF (RedfieldSolver.evolve's R vec(rho) in the eigenbasis, oqs.py:364-463, and any
+ * generator with Q = P^+ and pairs closed under conjugate transposition):
+ *   d rho/dt = X + X^+,   X = P rho + sum_c L_c rho W_c,
+ * valid for exactly Hermitian rho (every stage stays exactly Hermitian).  Redfield: P = -iE - sum A_k Lam_k,
+ * L_k = A_k, W_k = Lam_k^+.  1 + 2 npairs complex GEMMs per RHS (qd_glf_rk4: 2 + 2 * 2 npairs).  N <= 128.
+ */
+int qd_glf_rk4_herm(const qd_c128* P, const qd_c128* L, const qd_c128* W, int npairs,
+                    qd_c128* rho, int B, int N, double dt, int nsteps, const qd_c128* E,
+                    int ne, qd_c128* obs, qd_c128* snap, int save_every, void* stream);
+
+/*
  * Batched basis transform of B matrices [B][N][N] in place:
  *   mode 0: A <- V^+ A V   (pyqed/phys.py:1121-1137 transform(A, V))
  *   mode 1: A <- V A V^+   (transform(A, dag(V)), back-transform in oqs.py:450)

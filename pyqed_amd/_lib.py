@@ -40,6 +40,8 @@ SIGNATURES = {
                                 c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "qd_lindblad_rk4_herm": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_double, c_int,
                                      c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
+    "qd_glf_rk4_herm": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_double, c_int,
+                                c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "qd_glf_rk4": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_double,
                            c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "qd_basis_transform": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),

@@ -550,7 +550,7 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
     hipLaunchKernelGGL(glf_prep_kernel, dim3(blocks), dim3(threads), 0, st, P, Q, Lop, Rop, nc, E, ne, N, Np, Cop,
                        mK, iKd, Cd, eT);
   QD_HIP(hipGetLastError());
-  if (herm && nc > 0) {  // the Hermitian kernel consumes C_c^+ / 2
+  if (herm && nc > 0 && src == GLF_FROM_LINDBLAD) {  // the Hermitian kernel consumes C_c^+ / 2
     hipLaunchKernelGGL(scale_kernel, dim3(blocks), dim3(threads), 0, st, Cd, (size_t)nc * NN, 0.5);
     QD_HIP(hipGetLastError());
   }
@@ -709,6 +709,20 @@ extern "C" int qd_glf_rk4(const qd_c128* P, const qd_c128* Q, const qd_c128* L, 
   return glf_run(GLF_FROM_OPERATORS, nullptr, nullptr, (const c128*)P, (const c128*)Q, (const c128*)L,
                  (const c128*)R, npairs, (c128*)rho, B, N, dt, nsteps, (const c128*)E, ne, (c128*)obs, (c128*)snap,
                  save_every, (hipStream_t)stream);
+}
+
+extern "C" int qd_glf_rk4_herm(const qd_c128* P, const qd_c128* L, const qd_c128* W, int npairs, qd_c128* rho, int B,
+                               int N, double dt, int nsteps, const qd_c128* E, int ne, qd_c128* obs, qd_c128* snap,
+                               int save_every, void* stream) {
+  QD_CHECK_ARG(P && rho, "qd_glf_rk4_herm: P and rho must be non-null");
+  int rc = check_common("qd_glf_rk4_herm", rho, B, N, npairs, ne, E, obs, nsteps);
+  if (rc) return rc;
+  QD_CHECK_ARG(npairs == 0 || (L && W), "qd_glf_rk4_herm: L/W null but npairs=%d", npairs);
+  QD_CHECK_ARG(N <= 128, "qd_glf_rk4_herm: N=%d > 128 (the Hermitian kernel is single-block)", N);
+  // the Hermitian kernel reads X = P r + sum_c L_c r W_c from the mK / Cop / Cd slots; Q is not used
+  return glf_run(GLF_FROM_OPERATORS, nullptr, nullptr, (const c128*)P, (const c128*)P, (const c128*)L,
+                 (const c128*)W, npairs, (c128*)rho, B, N, dt, nsteps, (const c128*)E, ne, (c128*)obs, (c128*)snap,
+                 save_every, (hipStream_t)stream, nullptr, 0, nullptr, 1);
 }
 
 namespace {

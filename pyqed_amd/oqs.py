@@ -258,10 +258,12 @@ def _lindblad(H, rho0, c_ops, e_ops=None, Nt=1, t0=0, dt=0.005, return_result=Tr
 
 
 # --------------------------------------------------------------------------- GLF
-def glf_rk4(P, Q, L, R, rho, dt, nsteps, e_ops=None, save_every=0, stream=None):
+def glf_rk4(P, Q, L, R, rho, dt, nsteps, e_ops=None, save_every=0, stream=None, hermitian=False):
     """d rho/dt = P rho + rho Q + sum_c L_c rho R_c, batched RK4 on the GPU (qd_glf_rk4).
 
-    P, Q [N,N]; L, R [npairs,N,N] or None; rho [B,N,N] in place; e_ops [ne,N,N] or None."""
+    P, Q [N,N]; L, R [npairs,N,N] or None; rho [B,N,N] in place; e_ops [ne,N,N] or None.
+    hermitian=True: the Hermitian-state form d rho/dt = X + X^+, X = P rho + sum_c L_c rho R_c
+    (qd_glf_rk4_herm; Q is unused and R holds the W_c): rho must be exactly Hermitian, N <= 128."""
     B, N = rho.shape[0], rho.shape[-1]
     dev = rho.device
     _lib.ensure_device(dev)
@@ -277,10 +279,15 @@ def glf_rk4(P, Q, L, R, rho, dt, nsteps, e_ops=None, save_every=0, stream=None):
     snap = torch.empty((B, nsave, N, N), dtype=torch.complex128, device=dev) if nsave else None
     st = stream if stream is not None else _lib.stream_ptr(dev)
     with torch.cuda.device(dev):
-        rc = _lib.load().qd_glf_rk4(_lib.ptr(P), _lib.ptr(Q), _lib.ptr(L), _lib.ptr(R), npairs, _lib.ptr(rho), B, N,
-                                    float(dt), int(nsteps), _lib.ptr(e_ops), ne, _lib.ptr(obs), _lib.ptr(snap),
-                                    int(save_every if nsave else 0), st)
-    _lib.check(rc, "qd_glf_rk4")
+        if hermitian:
+            rc = _lib.load().qd_glf_rk4_herm(_lib.ptr(P), _lib.ptr(L), _lib.ptr(R), npairs, _lib.ptr(rho), B, N,
+                                             float(dt), int(nsteps), _lib.ptr(e_ops), ne, _lib.ptr(obs),
+                                             _lib.ptr(snap), int(save_every if nsave else 0), st)
+        else:
+            rc = _lib.load().qd_glf_rk4(_lib.ptr(P), _lib.ptr(Q), _lib.ptr(L), _lib.ptr(R), npairs, _lib.ptr(rho), B,
+                                        N, float(dt), int(nsteps), _lib.ptr(e_ops), ne, _lib.ptr(obs), _lib.ptr(snap),
+                                        int(save_every if nsave else 0), st)
+    _lib.check(rc, "qd_glf_rk4_herm" if hermitian else "qd_glf_rk4")
     return obs, snap
 
 
@@ -452,6 +459,19 @@ class RedfieldSolver:
             Rs += [ld, a]
         return P, Q, Ls, Rs
 
+    def glf_terms_herm(self):
+        """(P, L[], W[]) of the Hermitian-state form d rho~/dt = X + X^+, X = P rho~ + sum_k A_k rho~ Lam_k^+
+        (the pair (Lam_k, A_k) of glf_terms is the conjugate transpose of (A_k, Lam_k^+) acting on a
+        Hermitian rho~, and Q = P^+)."""
+        evals, evecs, A, Lam = self._prepare()
+        P = -1j * np.diag(evals).astype(complex)
+        Ls, Ws = [], []
+        for a, l in zip(A, Lam):
+            P = P - a @ l
+            Ls.append(a)
+            Ws.append(l.conj().T)
+        return P, Ls, Ws
+
     def evolve(self, rho0, dt, Nt, evecs=None, e_ops=[], store_states=False, t0=0, nout=1):
         """oqs.py:57-81 -> _redfield (oqs.py:364-459): observables (Nt, n_e) EXCLUDING t0,
         rholist (Nt) back-transformed to the original basis.  With an R set by the caller (no
@@ -469,11 +489,18 @@ class RedfieldSolver:
         Ed = stack_ops(e_ops, N, dev)
         if Ed is not None:
             basis_transform(evecs_t, Ed, inverse=False)
+        rho0_eb = rho[0].cpu().numpy()
+        r0 = to_numpy(rho0, np.complex128)
+        herm = N <= 128 and np.array_equal(r0, r0.conj().T)
+        if herm:
+            # Hermitian input: symmetrise the transformed state (rounding of V^+ rho V only) and propagate
+            # with the Hermitian-state kernel (1 + 2 n_a GEMMs per RHS instead of 2 + 4 n_a)
+            rho = (0.5 * (rho + rho.transpose(-1, -2).conj())).contiguous()
+            P, Ls, Rs = self.glf_terms_herm()
         Pd, Qd = (torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (P, Q))
         Ld = stack_ops(Ls, N, dev)
         Rd = stack_ops(Rs, N, dev)
-        rho0_eb = rho[0].cpu().numpy()
-        obs, snap = glf_rk4(Pd, Qd, Ld, Rd, rho, dt, Nt, Ed, save_every=1)
+        obs, snap = glf_rk4(Pd, Qd, Ld, Rd, rho, dt, Nt, Ed, save_every=1, hermitian=herm)
         result = Result(dt=dt, Nt=Nt, rho0=rho0_eb)
         result.observables = obs[0, 1:].cpu().numpy() if obs is not None else np.zeros((Nt, 0), complex)
         if snap is not None:

@@ -257,3 +257,47 @@ def test_t2scan_prepared_operands_buckets():
     ref = sum((alpha[m][None, :] * np.exp(np.outer(t3, lam[m]))) @ (B[m] * np.exp(lam[m] * t2[j])[None, :]) @ C[m]
               @ (beta[m][:, None] * np.exp(np.outer(lam[m], t1))) for m in range(M)) * (-1j) ** 3
     assert relerr(full[j], ref) < 1e-12
+
+
+@pytest.mark.parametrize("N,nk,B", [(40, 1, 3), (128, 2, 4)])
+def test_redfield_hermitian_glf_matches_general(N, nk, B):
+    """qd_glf_rk4_herm (X + X^+, X = P rho + sum A rho Lam^+) == qd_glf_rk4 with the full (P, Q, pairs) form."""
+    import torch
+    from oracle import lindblad as olb
+    from pyqed_amd import RedfieldSolver
+    from pyqed_amd.oqs import glf_rk4
+    rng = np.random.default_rng(N + nk)
+    a = rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N))
+    H = (a + a.conj().T) / 2 / np.sqrt(N)
+    a_ops = []
+    for _ in range(nk):
+        x = rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N))
+        a_ops.append(0.2 * (x + x.conj().T) / 2 / np.sqrt(N))
+    sol = RedfieldSolver(H, c_ops=a_ops, spectra=[SPECTRA["flat005"]] * nk)
+    sol.redfield_tensor()
+    dev = torch.device("cuda", 0)
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(np.asarray(x, complex))).to(dev)
+    P, Q, Ls, Rs = sol.glf_terms()
+    Ph, Lh, Wh = sol.glf_terms_herm()
+    rho0 = olb.random_pure_states(B, N, seed=N)
+    r1, r2 = t(rho0), t(rho0)
+    glf_rk4(t(P), t(Q), t(Ls), t(Rs), r1, 0.02, 30)
+    glf_rk4(t(Ph), None, t(Lh), t(Wh), r2, 0.02, 30, hermitian=True)
+    a1, a2 = r1.cpu().numpy(), r2.cpu().numpy()
+    assert relerr(a2, a1) < 1e-12
+    assert np.array_equal(a2, np.conj(np.swapaxes(a2, -1, -2)))      # exactly Hermitian
+
+
+def test_redfield_evolve_non_hermitian_input_general_path():
+    """A non-Hermitian rho0 (e.g. a coherence C rho0 A of a response function) takes the general GLF kernel."""
+    from oracle import redfield as orf
+    from pyqed_amd import RedfieldSolver
+    g = load_golden("redfield_n4")
+    rng = np.random.default_rng(3)
+    r0 = rng.standard_normal((4, 4)) + 1j * rng.standard_normal((4, 4))
+    sol = RedfieldSolver(g["H"], c_ops=list(g["a_ops"]), spectra=[SPECTRA[str(g["spectrum"])]])
+    R, evecs = sol.redfield_tensor()
+    r = sol.evolve(r0, dt=float(g["dt"]), Nt=int(g["Nt"]), e_ops=list(g["E"]))
+    obs, rholist = orf.redfield_evolve(R.toarray(), r0, evecs, int(g["Nt"]), float(g["dt"]), list(g["E"]))
+    assert relerr(r.observables, obs) < TOL
+    assert relerr(np.array(r.rholist), np.array(rholist)) < TOL
