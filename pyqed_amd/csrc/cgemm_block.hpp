@@ -63,13 +63,42 @@ __device__ __forceinline__ cg_v2 cg_ld(const c128* p) {
 }
 __device__ __forceinline__ void cg_st_lds(c128* p, cg_v2 v) { *reinterpret_cast<cg_v2*>(p) = v; }
 
-template <int BT>
-__device__ __forceinline__ void cg_compute_tile(const CgLds<BT>& L, int buf, CgAcc<BT>& acc, int wr0, int wc0) {
+#ifndef CG_STAGE_AT
+#define CG_STAGE_AT 3  // k-step (of 4) before which the next tile's LDS stores are issued (4 = after compute)
+#endif
+
+#ifndef CG_SCHED_FENCE
+#define CG_SCHED_FENCE 1
+#endif
+__device__ __forceinline__ void cg_sched_fence() {
+#if CG_SCHED_FENCE
+  __builtin_amdgcn_sched_barrier(0);
+#endif
+}
+
+struct CgNoMid {
+  __device__ __forceinline__ void operator()() const {}
+};
+
+// One K-tile of MFMA work from LDS buffer `buf`.  `mid()` runs before k-step CG_STAGE_AT: the caller puts
+// the next tile's LDS stores there, so they issue while this tile's MFMAs are still in the pipe instead
+// of between the last MFMA and the barrier (the double buffer keeps the two tiles apart).
+template <int BT, typename Mid = CgNoMid>
+__device__ __forceinline__ void cg_compute_tile(const CgLds<BT>& L, int buf, CgAcc<BT>& acc, int wr0, int wc0,
+                                                Mid mid = Mid()) {
   constexpr int MW = CgCfg<BT>::MW, NW = CgCfg<BT>::NW;
   const int lane = threadIdx.x & 63;
   const int lr = lane & 15, lk = lane >> 4;
 #pragma unroll
   for (int kk = 0; kk < CG_KT; kk += 4) {
+    if (kk == 4 * CG_STAGE_AT) {
+      // keep the staging stores (and the vmcnt wait for their data) behind the MFMAs already issued:
+      // without the fence the scheduler hoists them above the tile's MFMAs and every tile stalls on
+      // the global-load latency before its first MFMA
+      cg_sched_fence();
+      mid();
+      cg_sched_fence();
+    }
     c128 a[MW], b[NW];
 #pragma unroll
     for (int mi = 0; mi < MW; ++mi) a[mi] = L.a[buf][(wr0 + mi * 16 + lr) * CG_SA + kk + lk];
@@ -89,6 +118,10 @@ __device__ __forceinline__ void cg_compute_tile(const CgLds<BT>& L, int buf, CgA
         acc.re[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(-a[mi].im, b[nj].im, acc.re[mi][nj], 0, 0, 0);
         acc.im[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi].im, b[nj].re, acc.im[mi][nj], 0, 0, 0);
       }
+  }
+  if (CG_STAGE_AT >= CG_KT / 4) {
+    cg_sched_fence();
+    mid();
   }
 }
 
@@ -139,8 +172,14 @@ __device__ __forceinline__ void cg_block_gemm_gen(int T, APol& pa, BPol& pb, CgL
   for (int t = 0; t < T; ++t) {
     const bool more = (t + 1) < T;
     if (more) load(t + 1);
-    if (active) cg_compute_tile<BT>(L, t & 1, acc, wr0, wc0);
-    if (more) store(t + 1, (t + 1) & 1);
+    auto mid = [&]() {
+      if (more) store(t + 1, (t + 1) & 1);
+    };
+    if (active) {
+      cg_compute_tile<BT>(L, t & 1, acc, wr0, wc0, mid);
+    } else {
+      mid();
+    }
     __syncthreads();
   }
 }
