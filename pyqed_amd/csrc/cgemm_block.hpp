@@ -83,43 +83,57 @@ struct CgNoMid {
 // One K-tile of MFMA work from LDS buffer `buf`.  `mid()` runs before k-step CG_STAGE_AT: the caller puts
 // the next tile's LDS stores there, so they issue while this tile's MFMAs are still in the pipe instead
 // of between the last MFMA and the barrier (the double buffer keeps the two tiles apart).
-template <int BT, typename Mid = CgNoMid>
+// PIPE: the fragments of k-step q+1 are read from LDS into a second register set before the MFMAs
+// of k-step q issue, so only the tile's first k-step waits on LDS latency (without it every k-step's
+// first MFMA waits for its ds_read_b128s: the reads reuse the registers the previous MFMAs consume).
+template <int BT, bool PIPE = false, typename Mid = CgNoMid>
 __device__ __forceinline__ void cg_compute_tile(const CgLds<BT>& L, int buf, CgAcc<BT>& acc, int wr0, int wc0,
                                                 Mid mid = Mid()) {
   constexpr int MW = CgCfg<BT>::MW, NW = CgCfg<BT>::NW;
+  constexpr int NQ = CG_KT / 4;
   const int lane = threadIdx.x & 63;
   const int lr = lane & 15, lk = lane >> 4;
+  constexpr int NS = PIPE ? 2 : 1;
+  c128 a[NS][MW], b[NS][NW];
+  auto frag = [&](int q, int slot) {
+    const int kk = 4 * q;
 #pragma unroll
-  for (int kk = 0; kk < CG_KT; kk += 4) {
-    if (kk == 4 * CG_STAGE_AT) {
+    for (int mi = 0; mi < MW; ++mi) a[slot][mi] = L.a[buf][(wr0 + mi * 16 + lr) * CG_SA + kk + lk];
+#pragma unroll
+    for (int nj = 0; nj < NW; ++nj) b[slot][nj] = L.b[buf][(kk + lk) * BT + wc0 + nj * 16 + lr];
+  };
+  if (PIPE) frag(0, 0);
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    if (q == CG_STAGE_AT) {
       // keep the staging stores (and the vmcnt wait for their data) behind the MFMAs already issued:
-      // without the fence the scheduler hoists them above the tile's MFMAs and every tile stalls on
-      // the global-load latency before its first MFMA
+      // without the fence the scheduler hoists them above the tile's MFMAs
       cg_sched_fence();
       mid();
       cg_sched_fence();
     }
-    c128 a[MW], b[NW];
-#pragma unroll
-    for (int mi = 0; mi < MW; ++mi) a[mi] = L.a[buf][(wr0 + mi * 16 + lr) * CG_SA + kk + lk];
-#pragma unroll
-    for (int nj = 0; nj < NW; ++nj) b[nj] = L.b[buf][(kk + lk) * BT + wc0 + nj * 16 + lr];
+    const int cs = PIPE ? (q & 1) : 0;
+    if (PIPE) {
+      if (q + 1 < NQ) frag(q + 1, (q + 1) & 1);
+    } else {
+      frag(q, 0);
+    }
 #pragma unroll
     for (int mi = 0; mi < MW; ++mi)
 #pragma unroll
       for (int nj = 0; nj < NW; ++nj) {
-        acc.re[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi].re, b[nj].re, acc.re[mi][nj], 0, 0, 0);
-        acc.im[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi].re, b[nj].im, acc.im[mi][nj], 0, 0, 0);
+        acc.re[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[cs][mi].re, b[cs][nj].re, acc.re[mi][nj], 0, 0, 0);
+        acc.im[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[cs][mi].re, b[cs][nj].im, acc.im[mi][nj], 0, 0, 0);
       }
 #pragma unroll
     for (int mi = 0; mi < MW; ++mi)
 #pragma unroll
       for (int nj = 0; nj < NW; ++nj) {
-        acc.re[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(-a[mi].im, b[nj].im, acc.re[mi][nj], 0, 0, 0);
-        acc.im[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi].im, b[nj].re, acc.im[mi][nj], 0, 0, 0);
+        acc.re[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(-a[cs][mi].im, b[cs][nj].im, acc.re[mi][nj], 0, 0, 0);
+        acc.im[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[cs][mi].im, b[cs][nj].re, acc.im[mi][nj], 0, 0, 0);
       }
   }
-  if (CG_STAGE_AT >= CG_KT / 4) {
+  if (CG_STAGE_AT >= NQ) {
     cg_sched_fence();
     mid();
   }
@@ -131,7 +145,7 @@ __device__ __forceinline__ void cg_compute_tile(const CgLds<BT>& L, int buf, CgA
 // where e = tid + CG_WG*q is the element of the tile this thread stages (A: row e>>4, col e&15;
 // B: row e/BT, col e%BT) and q < cg_nld<BT>() its compile-time slot.  A policy may fetch inputs and compute the operand in finish (generated operands).
 // All threads of the workgroup must call it.  Ends with a workgroup barrier.
-template <int BT, typename APol, typename BPol>
+template <int BT, bool PIPE = false, typename APol, typename BPol>
 __device__ __forceinline__ void cg_block_gemm_gen(int T, APol& pa, BPol& pb, CgLds<BT>& L, CgAcc<BT>& acc) {
   constexpr int MW = CgCfg<BT>::MW, NW = CgCfg<BT>::NW, WC = CgCfg<BT>::WC, WR = CgCfg<BT>::WR;
   const int wave = threadIdx.x >> 6;
@@ -176,7 +190,7 @@ __device__ __forceinline__ void cg_block_gemm_gen(int T, APol& pa, BPol& pb, CgL
       if (more) store(t + 1, (t + 1) & 1);
     };
     if (active) {
-      cg_compute_tile<BT>(L, t & 1, acc, wr0, wc0, mid);
+      cg_compute_tile<BT, PIPE>(L, t & 1, acc, wr0, wc0, mid);
     } else {
       mid();
     }

@@ -19,6 +19,8 @@
 // records rho_0 (the system density matrix) after every step.
 #include "qd_common.hpp"
 
+#include <cstdlib>
+
 namespace qd {
 namespace {
 
@@ -122,17 +124,35 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_kernel(DeomParams p) {
   }
 }
 
+// Quad-permute DPP move of a double / complex (gfx9 quad_perm: lane q of each group of 4 lanes reads
+// lane (CTRL >> 2q) & 3 of its group); one VALU op per dword, no LDS traffic.
+template <int CTRL>
+__device__ __forceinline__ double dpp_qd(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+template <int CTRL>
+__device__ __forceinline__ c128 dpp_qc(c128 v) { return cmk(dpp_qd<CTRL>(v.re), dpp_qd<CTRL>(v.im)); }
+template <int CTRL>
+__device__ __forceinline__ int dpp_qi(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false); }
+
 // Group kernel: G = next pow2 >= ns^2 lanes per ADO, one lane per matrix element, so every
 // neighbour ADO is read once per group as one coalesced ns^2 x 16-B row (not once per row/column
-// it touches).  All 2K neighbour indices, coefficients and neighbour elements are loaded up front
-// (one dependent-load round trip instead of one per k), and the ns x ns products exchange
-// elements inside the group with lane shuffles.  Every lane of a group follows the same branches
-// (they share the ADO), so the shuffles never read an inactive lane.
-template <int G, int KMAX>
+// it touches).  The ADO's neighbour indices and prefactors are loaded ONCE per group: lane e loads
+// entries e, e + G, ... of the ADO's rows (contiguous across the group) and the group broadcasts them
+// (quad DPP for G = 4, lane shuffles otherwise), so a lane issues ~2K/G + 3K/G of these loads instead
+// of 5K.  All of them are issued together with the lane's own element and RK4 state (round trip 1),
+// then every neighbour element (round trip 2).  NS2: ns = 2 (G = 4) with every exchange of the
+// 2 x 2 products a quad DPP move.  Every lane of a group follows the same branches (they share the
+// ADO), so no exchange reads an inactive lane.  H(t), Q(t) go to dynamic LDS ((1 + nmod) ns^2).
+template <int G, int KMAX, bool NS2>
 __global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) {
-  __shared__ c128 sH[DEOM_MAX_NS * DEOM_MAX_NS];
-  __shared__ c128 sQ[DEOM_MAX_NMOD * DEOM_MAX_NS * DEOM_MAX_NS];
-  const int ns = p.ns, ns2 = ns * ns, K = p.K;
+  extern __shared__ c128 deom_lds[];
+  c128* sH = deom_lds;
+  c128* sQ = deom_lds + p.ns * p.ns;
+  const int ns = NS2 ? 2 : p.ns, ns2 = ns * ns, K = p.K;
   const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   const size_t ngrp = (size_t)p.B * p.nmax;
   const size_t grp = t / G;                 // b * nmax + n
@@ -142,26 +162,49 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) 
   const int n = live ? (int)(grp % p.nmax) : 0;
   const int ee = e < ns2 ? e : 0;           // padding lanes shadow element 0
   const c128* X = p.xin + (live ? (grp - n) * ns2 : 0);
-
-  // round trip 1: indices, coefficients, modes, own element, the RK4 state of this element,
-  // and H/Q into LDS -- all independent loads, issued together
-  int im[KMAX], ip[KMAX], md[KMAX];
-  c128 cf[KMAX][3];
-#pragma unroll
-  for (int k = 0; k < KMAX; ++k) {
-    im[k] = -1;
-    ip[k] = -1;
-    md[k] = 0;
-    cf[k][0] = cf[k][1] = cf[k][2] = cmk(0, 0);
-    if (live && k < K) {
-      im[k] = p.minus[(size_t)n * K + k];
-      ip[k] = p.plus[(size_t)n * K + k];
-      md[k] = p.mode[k];
-      const c128* c = p.coef + ((size_t)n * K + k) * 3;
-      cf[k][0] = c[0];
-      cf[k][1] = c[1];
-      cf[k][2] = c[2];
+  const int base = (int)(threadIdx.x & 63) & ~(G - 1);
+  auto shfl = [&](c128 v, int src) { return cmk(__shfl(v.re, base + src, 64), __shfl(v.im, base + src, 64)); };
+  // value of v held by lane `src` of this group (src is a compile-time constant after unrolling)
+  auto bc = [&](c128 v, int src) -> c128 {
+    if constexpr (G == 4) {
+      switch (src) {
+        case 0: return dpp_qc<0x00>(v);
+        case 1: return dpp_qc<0x55>(v);
+        case 2: return dpp_qc<0xAA>(v);
+        default: return dpp_qc<0xFF>(v);
+      }
+    } else {
+      return shfl(v, src);
     }
+  };
+  auto bci = [&](int v, int src) -> int {
+    if constexpr (G == 4) {
+      switch (src) {
+        case 0: return dpp_qi<0x00>(v);
+        case 1: return dpp_qi<0x55>(v);
+        case 2: return dpp_qi<0xAA>(v);
+        default: return dpp_qi<0xFF>(v);
+      }
+    } else {
+      return __shfl(v, base + src, 64);
+    }
+  };
+
+  // round trip 1: this lane's share of the indices and prefactors, own element, RK4 state, H/Q -> LDS
+  constexpr int NI = (KMAX + G - 1) / G;
+  constexpr int NC = (3 * KMAX + G - 1) / G;
+  int lm[NI], lp[NI];
+  c128 lc[NC];
+#pragma unroll
+  for (int q = 0; q < NI; ++q) {
+    const int k = e + G * q;
+    lm[q] = (live && k < K) ? p.minus[(size_t)n * K + k] : -1;
+    lp[q] = (live && k < K) ? p.plus[(size_t)n * K + k] : -1;
+  }
+#pragma unroll
+  for (int q = 0; q < NC; ++q) {
+    const int c = e + G * q;
+    lc[q] = (live && c < 3 * K) ? p.coef[(size_t)n * K * 3 + c] : cmk(0, 0);
   }
   const c128 own = live ? X[(size_t)n * ns2 + ee] : cmk(0, 0);
   const c128 dmp = live ? p.damp[n] : cmk(0, 0);
@@ -172,43 +215,69 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) 
     sH[q] = p.Hdip ? cadd(p.H[q], cmul(p.Hdip[q], p.fs)) : p.H[q];
   for (int q = threadIdx.x; q < p.nmod * ns2; q += blockDim.x)
     sQ[q] = p.Qdip ? cadd(p.Q[q], cmul(p.Qdip[q], p.fc)) : p.Q[q];
-  __syncthreads();
+  int im[KMAX], ip[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    im[k] = bci(lm[k / G], k % G);
+    ip[k] = bci(lp[k / G], k % G);
+  }
 
   // round trip 2: every neighbour element this lane owns
   c128 ym[KMAX], yp[KMAX];
 #pragma unroll
   for (int k = 0; k < KMAX; ++k) {
-    ym[k] = im[k] >= 0 ? X[(size_t)im[k] * ns2 + ee] : cmk(0, 0);
-    yp[k] = ip[k] >= 0 ? X[(size_t)ip[k] * ns2 + ee] : cmk(0, 0);
+    ym[k] = (k < K && im[k] >= 0) ? X[(size_t)im[k] * ns2 + ee] : cmk(0, 0);
+    yp[k] = (k < K && ip[k] >= 0) ? X[(size_t)ip[k] * ns2 + ee] : cmk(0, 0);
   }
+  __syncthreads();
 
   const int i = ee / ns, j = ee % ns;
-  const int base = (int)(threadIdx.x & 63) & ~(G - 1);
-  auto shfl = [&](c128 v, int src) { return cmk(__shfl(v.re, base + src, 64), __shfl(v.im, base + src, 64)); };
+  // v[l][j] and v[i][l] of this lane's group (v[i][j] held by lane i ns + j)
+  auto colv = [&](c128 v, int l) -> c128 {
+    if constexpr (NS2) return l == 0 ? dpp_qc<0x44>(v) : dpp_qc<0xEE>(v);   // lanes (0,1,0,1) / (2,3,2,3)
+    else return shfl(v, l * ns + j);
+  };
+  auto rowv = [&](c128 v, int l) -> c128 {
+    if constexpr (NS2) return l == 0 ? dpp_qc<0xA0>(v) : dpp_qc<0xF5>(v);   // lanes (0,0,2,2) / (1,1,3,3)
+    else return shfl(v, i * ns + l);
+  };
+  auto for_l = [&](auto&& f) {   // l = 0 .. ns-1 (two literal calls for ns = 2)
+    if constexpr (NS2) {
+      f(0);
+      f(1);
+    } else {
+      for (int l = 0; l < ns; ++l) f(l);
+    }
+  };
 
   // damping + coherent part: damp_n x - i (H x - x H)
   c128 d = cmul(dmp, own);
   c128 comm = cmk(0, 0);
-  for (int l = 0; l < ns; ++l)
-    comm = cadd(comm, csub(cmul(sH[i * ns + l], shfl(own, l * ns + j)), cmul(shfl(own, i * ns + l), sH[l * ns + j])));
+  for_l([&](int l) {
+    comm = cadd(comm, csub(cmul(sH[i * ns + l], colv(own, l)), cmul(rowv(own, l), sH[l * ns + j])));
+  });
   d = cadd(d, cmulmi(comm));
 #pragma unroll
   for (int k = 0; k < KMAX; ++k) {
     if (k >= K) break;
-    const c128* Qm = sQ + md[k] * ns2;
+    const c128* Qm = sQ + p.mode[k] * ns2;
+    const c128 cL = bc(lc[(3 * k) / G], (3 * k) % G);
+    const c128 cR = bc(lc[(3 * k + 1) / G], (3 * k + 1) % G);
+    const c128 cP = bc(lc[(3 * k + 2) / G], (3 * k + 2) % G);
     if (im[k] >= 0) {
       c128 qy = cmk(0, 0), yq = cmk(0, 0);
-      for (int l = 0; l < ns; ++l) {
-        qy = cadd(qy, cmul(Qm[i * ns + l], shfl(ym[k], l * ns + j)));
-        yq = cadd(yq, cmul(shfl(ym[k], i * ns + l), Qm[l * ns + j]));
-      }
-      d = cadd(d, cadd(cmul(cf[k][0], qy), cmul(cf[k][1], yq)));
+      for_l([&](int l) {
+        qy = cadd(qy, cmul(Qm[i * ns + l], colv(ym[k], l)));
+        yq = cadd(yq, cmul(rowv(ym[k], l), Qm[l * ns + j]));
+      });
+      d = cadd(d, cadd(cmul(cL, qy), cmul(cR, yq)));
     }
     if (ip[k] >= 0) {
       c128 c = cmk(0, 0);
-      for (int l = 0; l < ns; ++l)
-        c = cadd(c, csub(cmul(Qm[i * ns + l], shfl(yp[k], l * ns + j)), cmul(shfl(yp[k], i * ns + l), Qm[l * ns + j])));
-      d = cadd(d, cmul(cf[k][2], c));
+      for_l([&](int l) {
+        c = cadd(c, csub(cmul(Qm[i * ns + l], colv(yp[k], l)), cmul(rowv(yp[k], l), Qm[l * ns + j])));
+      });
+      d = cadd(d, cmul(cP, c));
     }
   }
   if (!valid) return;
@@ -367,18 +436,29 @@ extern "C" int qd_deom_rk4(qd_c128* ados, int B, int nmax, int K, int ns, const 
   while (G < (int)ns2) G *= 2;
   const bool grp = G <= 64 && K <= 8;
   const size_t nthreads = grp ? (size_t)B * nmax * G : tot;
-  const int grid = (int)((nthreads + DEOM_TPB - 1) / DEOM_TPB);
+  // A small hierarchy (one at L = 12, K = 5: 24.8k lanes) as 256-thread blocks would occupy ~100 of the
+  // 256 CUs, each CU then issuing the loads of 4 waves; 64-thread blocks spread the same lanes over every
+  // CU.  QD_DEOM_TPB overrides (64 or 256) for A/B runs.
+  int tpb = (nthreads + DEOM_TPB - 1) / DEOM_TPB < 1024 ? 64 : DEOM_TPB;
+  if (const char* s = getenv("QD_DEOM_TPB")) tpb = atoi(s) == 64 ? 64 : DEOM_TPB;
+  if (!grp) tpb = DEOM_TPB;
+  const int grid = (int)((nthreads + tpb - 1) / tpb);
+  const size_t lds = (size_t)(1 + nmod) * ns2 * sizeof(c128);   // H(t), Q(t) of the group kernel
   auto launch_stage = [&]() {
     if (!grp) {
-      hipLaunchKernelGGL(deom_stage_kernel, dim3(grid), dim3(DEOM_TPB), 0, st, p);
+      hipLaunchKernelGGL(deom_stage_kernel, dim3(grid), dim3(tpb), 0, st, p);
       return;
     }
     switch (G) {
-      case 1: hipLaunchKernelGGL((deom_stage_grp_kernel<1, 8>), dim3(grid), dim3(DEOM_TPB), 0, st, p); break;
-      case 4: hipLaunchKernelGGL((deom_stage_grp_kernel<4, 8>), dim3(grid), dim3(DEOM_TPB), 0, st, p); break;
-      case 16: hipLaunchKernelGGL((deom_stage_grp_kernel<16, 8>), dim3(grid), dim3(DEOM_TPB), 0, st, p); break;
-      case 32: hipLaunchKernelGGL((deom_stage_grp_kernel<32, 8>), dim3(grid), dim3(DEOM_TPB), 0, st, p); break;
-      default: hipLaunchKernelGGL((deom_stage_grp_kernel<64, 8>), dim3(grid), dim3(DEOM_TPB), 0, st, p); break;
+      case 1: hipLaunchKernelGGL((deom_stage_grp_kernel<1, 8, false>), dim3(grid), dim3(tpb), lds, st, p); break;
+      case 4:  // ns = 2; registers sized to K (ym/yp/indices scale with KMAX)
+        if (K <= 4) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 4, true>), dim3(grid), dim3(tpb), lds, st, p);
+        else if (K <= 6) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 6, true>), dim3(grid), dim3(tpb), lds, st, p);
+        else hipLaunchKernelGGL((deom_stage_grp_kernel<4, 8, true>), dim3(grid), dim3(tpb), lds, st, p);
+        break;
+      case 16: hipLaunchKernelGGL((deom_stage_grp_kernel<16, 8, false>), dim3(grid), dim3(tpb), lds, st, p); break;
+      case 32: hipLaunchKernelGGL((deom_stage_grp_kernel<32, 8, false>), dim3(grid), dim3(tpb), lds, st, p); break;
+      default: hipLaunchKernelGGL((deom_stage_grp_kernel<64, 8, false>), dim3(grid), dim3(tpb), lds, st, p); break;
     }
   };
   static const int stage_time[4] = {0, 1, 1, 2};

@@ -230,6 +230,9 @@ __global__ void ens_z_generic_kernel(const c128* Mt, const c128* beta, const c12
 }
 
 constexpr int ENS_BT = 128;
+#ifndef ENS_PIPE
+#define ENS_PIPE false  // fragment double-buffering (PIPE) fits (250 VGPRs, no scratch) but measured neutral here
+#endif
 
 // A operand X [n3p][Kp] (materialised by ens_xz_kernel), streamed one tile ahead.
 struct EnsXA {
@@ -278,7 +281,7 @@ __global__ __launch_bounds__(CG_WG) void ens_gemm_kernel(const c128* X, int Kp, 
   if (t1 > t0) {
     EnsXA pa{X, Kp, bm * ENS_BT, t0 * CG_KT};
     EnsZB pb{Z, n1p, bn * ENS_BT, t0 * CG_KT};
-    cg_block_gemm_gen<ENS_BT>(t1 - t0, pa, pb, L, A);
+    cg_block_gemm_gen<ENS_BT, ENS_PIPE>(t1 - t0, pa, pb, L, A);
     cg_epilogue<ENS_BT>(A, [&](int row, int col, c128 v) {
       slab[(size_t)(bm * ENS_BT + row) * n1p + bn * ENS_BT + col] = v;
     });
