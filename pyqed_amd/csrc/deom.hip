@@ -124,20 +124,6 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_kernel(DeomParams p) {
   }
 }
 
-// Quad-permute DPP move of a double / complex (gfx9 quad_perm: lane q of each group of 4 lanes reads
-// lane (CTRL >> 2q) & 3 of its group); one VALU op per dword, no LDS traffic.
-template <int CTRL>
-__device__ __forceinline__ double dpp_qd(double v) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-template <int CTRL>
-__device__ __forceinline__ c128 dpp_qc(c128 v) { return cmk(dpp_qd<CTRL>(v.re), dpp_qd<CTRL>(v.im)); }
-template <int CTRL>
-__device__ __forceinline__ int dpp_qi(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false); }
-
 // Group kernel: G = next pow2 >= ns^2 lanes per ADO, one lane per matrix element, so every
 // neighbour ADO is read once per group as one coalesced ns^2 x 16-B row (not once per row/column
 // it touches).  The ADO's neighbour indices and prefactors are loaded ONCE per group: lane e loads

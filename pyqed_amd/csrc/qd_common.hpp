@@ -64,6 +64,20 @@ __host__ __device__ inline c128 cmulmi(c128 a) { return cmk(a.im, -a.re); }    /
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
+// Quad-permute DPP move of a double / complex (gfx9 quad_perm: lane q of each group of 4 lanes reads
+// lane (CTRL >> 2q) & 3 of its group); one VALU op per dword, no LDS traffic.
+template <int CTRL>
+__device__ __forceinline__ double dpp_qd(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+template <int CTRL>
+__device__ __forceinline__ c128 dpp_qc(c128 v) { return cmk(dpp_qd<CTRL>(v.re), dpp_qd<CTRL>(v.im)); }
+template <int CTRL>
+__device__ __forceinline__ int dpp_qi(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false); }
+
 inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
 }  // namespace qd

@@ -21,6 +21,8 @@
 // exp_V_half (ns^2 per point) once per row pass, exp_K once per column pass.
 #include "qd_common.hpp"
 
+#include <cstdlib>
+
 namespace qd {
 namespace {
 
@@ -476,6 +478,180 @@ __global__ void spo_expv_kernel(const void* v_, long npts, int ns, double dt, c1
   }
 }
 
+// ---------------------------------------------------------------- 256-point passes in registers
+// L = 256 = 16 x 16 (Cooley-Tukey, n = 16 n1 + n2, k = k1 + 16 k2):
+//   X[k1 + 16 k2] = sum_n2 w16^(n2 k2) w256^(n2 k1) sum_n1 x[16 n1 + n2] w16^(n1 k1)
+// ONE wave per transform set.  Lane (g, s) = (lane >> 2, lane & 3) holds the points
+// p_a = 64 a + 16 s + g (a = 0..3) of its line, before and after every transform: an inverse FFT,
+// point-local work and a forward FFT chain with no data movement.  Each 16-point DFT runs inside
+// a quad (4 x 4: DFT4 in registers, three quad-DPP rotations, DFT4); the two 16-point steps
+// exchange through LDS once.  Per pass: one global load round trip, two wave-local LDS
+// transposes per FFT, no workgroup-wide barrier (the Stockham LDS FFT takes 4 barrier stages per
+// transform plus the staging).  w = exp(-2 pi i / L) forward, its conjugate inverse; no scaling.
+template <bool ZPOS>  // y[r] = sum_a x[a] z^(a r), z = +i (ZPOS) or -i
+__device__ __forceinline__ void dft4(c128 (&x)[4]) {
+  const c128 s02 = cadd(x[0], x[2]), d02 = csub(x[0], x[2]);
+  const c128 s13 = cadd(x[1], x[3]), d13 = csub(x[1], x[3]);
+  const c128 zd = ZPOS ? cmuli(d13) : cmulmi(d13);
+  x[0] = cadd(s02, s13);
+  x[1] = cadd(d02, zd);
+  x[2] = csub(s02, s13);
+  x[3] = csub(d02, zd);
+}
+
+struct Q16Tw {
+  c128 a[4];  // w4^(a s)            (pre-rotation of the inputs, also the final w4^(s d))
+  c128 b[4];  // w16^(s ((s - r) & 3))  (inner twiddle of the sent element r)
+  c128 d[4];  // w256^(g (s + 4 d))  (inter-step twiddle of output k1 = s + 4 d)
+};
+
+__device__ __forceinline__ Q16Tw q16_twiddles(const c128* tw, int g, int s) {
+  Q16Tw t;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    t.a[q] = tw[64 * ((q * s) & 3)];
+    t.b[q] = tw[16 * ((s * ((s - q) & 3)) & 15)];
+    t.d[q] = tw[(g * (s + 4 * q)) & 255];
+  }
+  return t;
+}
+
+__device__ __forceinline__ c128 twmul(c128 v, c128 w, bool inv) { return cmul(v, inv ? cconj(w) : w); }
+
+// 16-point DFT of the quad: lane s holds v[a] = x[4 a + s]; on return lane s holds X[s + 4 d] in v[d].
+template <bool INV>
+__device__ __forceinline__ void dft16_quad(c128 (&v)[4], const Q16Tw& t) {
+  // U_s[(s - r) & 3] = sum_a (v[a] w4^(a s)) w4^(-a r): pre-rotate, DFT4 with root w4^-1
+#pragma unroll
+  for (int a = 1; a < 4; ++a) v[a] = twmul(v[a], t.a[a], INV);
+  dft4<!INV>(v);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = twmul(v[r], t.b[r], INV);
+  // lane l receives element r of lane (l + r) & 3: R_r = U_b[l] w16^(b l), b = (l + r) & 3
+  v[1] = dpp_qc<0x39>(v[1]);
+  v[2] = dpp_qc<0x4E>(v[2]);
+  v[3] = dpp_qc<0x93>(v[3]);
+  // X[l + 4 d] = w4^(l d) sum_r w4^(r d) R_r
+  dft4<INV>(v);
+#pragma unroll
+  for (int d = 1; d < 4; ++d) v[d] = twmul(v[d], t.a[d], INV);
+}
+
+// 256-point FFT of NS lines held in the wave's layout; S: NS x 16 x 17 c128 of LDS (this wave's).
+template <bool INV, int NS>
+__device__ __forceinline__ void fft256_wave(c128 (&x)[NS][4], const Q16Tw& t, c128* S, int g, int s) {
+#pragma unroll
+  for (int c = 0; c < NS; ++c) {
+    dft16_quad<INV>(x[c], t);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) S[c * 272 + (s + 4 * d) * 17 + g] = twmul(x[c][d], t.d[d], INV);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int c = 0; c < NS; ++c) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) x[c][a] = S[c * 272 + g * 17 + 4 * a + s];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int c = 0; c < NS; ++c) dft16_quad<INV>(x[c], t);
+}
+
+// Row pass of spo2_row_fast_kernel for L = 256: one workgroup per row, wave c = state c (its 256-point
+// transforms run on 4 values per lane).  The point operators mix the states of a point, whose values
+// sit in the same lane of every wave: they are exchanged through LDS (one workgroup barrier per point
+// operator).  Same flags and arithmetic order of the point work as the LDS kernels:
+// [IFFT_y] -> V/2 -> [snapshot] -> [V/2] -> [FFT_y] -> [k_y phase].
+template <int NS>
+__global__ __launch_bounds__(64 * NS) void spo2_row_q16_kernel(c128* psi, const c128* U, const c128* twy, int flags,
+                                                               c128* snap, const c128* expKy) {
+  __shared__ c128 S[NS * 272];
+  __shared__ c128 Xs[NS * 256];   // point-operator exchange: [state][lane * 4 + a]
+  const int i = blockIdx.x, c = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 2, s = lane & 3;
+  c128 x[1][4], u[4][NS], ky[4];
+  const size_t row = (size_t)i * 256;
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const size_t pt = row + 64 * a + 16 * s + g;
+    x[0][a] = psi[pt * NS + c];
+    if (flags & (ROW_VH1 | ROW_VH2)) {
+#pragma unroll
+      for (int b = 0; b < NS; ++b) u[a][b] = U[(pt * NS + c) * NS + b];   // row c of the point's operator
+    }
+    ky[a] = (flags & ROW_KY) ? expKy[pt] : cmk(1, 0);
+  }
+  const Q16Tw t = q16_twiddles(twy, g, s);
+  c128* Sw = S + c * 272;
+  auto point_op = [&]() {
+    if (NS > 1) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a) Xs[c * 256 + lane * 4 + a] = x[0][a];
+      __syncthreads();
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      c128 acc = cmk(0, 0);
+#pragma unroll
+      for (int b = 0; b < NS; ++b) acc = cadd(acc, cmul(u[a][b], NS > 1 ? Xs[b * 256 + lane * 4 + a] : x[0][a]));
+      x[0][a] = acc;
+    }
+    if (NS > 1) __syncthreads();   // Xs is rewritten by the next operator
+  };
+  if (flags & ROW_INV) fft256_wave<true, 1>(x, t, Sw, g, s);
+  if (flags & ROW_VH1) point_op();
+  if (flags & ROW_SNAP) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) snap[(row + 64 * a + 16 * s + g) * NS + c] = x[0][a];
+  }
+  if (flags & ROW_VH2) point_op();
+  if (flags & ROW_FWD) fft256_wave<false, 1>(x, t, Sw, g, s);
+  if (flags & ROW_KY) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) x[0][a] = cmul(ky[a], x[0][a]);
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) psi[(row + 64 * a + 16 * s + g) * NS + c] = x[0][a];
+}
+
+// Column pass of spo2_col_fast_kernel for L = nx = 256: one 64-lane workgroup per (column j, state c)
+// (no state mixing in this pass): FFT_x -> * exp_K / (nx ny) -> IFFT_x.  Blocks of one XCD (blockIdx.x
+// % 8) take a contiguous run of columns, so the pieces that adjacent columns read from one row share
+// that XCD's L2 lines.
+template <int NS>
+__global__ __launch_bounds__(64) void spo2_col_q16_kernel(c128* psi, const c128* expKT, const c128* twx, int ncols,
+                                                          int pitch) {
+  __shared__ c128 S[272];
+  const int b = blockIdx.x, c = blockIdx.y;
+  const int j = (ncols % 8 == 0) ? (b % 8) * (ncols / 8) + b / 8 : b;
+  const int lane = threadIdx.x, g = lane >> 2, s = lane & 3;
+  c128 x[1][4], kf[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int p = 64 * a + 16 * s + g;
+    x[0][a] = psi[((size_t)p * pitch + j) * NS + c];
+    kf[a] = expKT[(size_t)j * 256 + p];
+  }
+  const Q16Tw t = q16_twiddles(twx, g, s);
+  fft256_wave<false, 1>(x, t, S, g, s);
+#pragma unroll
+  for (int a = 0; a < 4; ++a) x[0][a] = cmul(x[0][a], kf[a]);
+  fft256_wave<true, 1>(x, t, S, g, s);
+#pragma unroll
+  for (int a = 0; a < 4; ++a) psi[((size_t)(64 * a + 16 * s + g) * pitch + j) * NS + c] = x[0][a];
+}
+
+bool q16_enabled() {
+  static const int on = [] {
+    const char* e = getenv("QD_SPO_Q16");
+    return e ? atoi(e) : 1;
+  }();
+  return on != 0;
+}
+
 bool pow2_in_range(int n) { return n >= 16 && n <= 1024 && (n & (n - 1)) == 0; }
 
 // L dispatch helpers
@@ -500,6 +676,12 @@ int twiddles(int L, hipStream_t st, c128* tw) {
 // Launch the latency-shaped row pass (ns <= 2): `rows` rows of length L.
 int row_fast(int L, int ns, int rows, int flags, c128* psi, const c128* U, const c128* tw, c128* snap,
              const c128* expKy, hipStream_t st) {
+  if (L == 256 && q16_enabled()) {
+    if (ns == 1) hipLaunchKernelGGL(spo2_row_q16_kernel<1>, dim3(rows), dim3(64), 0, st, psi, U, tw, flags, snap, expKy);
+    else hipLaunchKernelGGL(spo2_row_q16_kernel<2>, dim3(rows), dim3(128), 0, st, psi, U, tw, flags, snap, expKy);
+    QD_HIP(hipGetLastError());
+    return QD_OK;
+  }
   const int bd = std::max(64, L);
   const size_t lds = (size_t)(L + 2 * ns * L) * sizeof(c128);
 #define RF(LL)                                                                                                      \
@@ -517,6 +699,12 @@ int row_fast(int L, int ns, int rows, int flags, c128* psi, const c128* U, const
 // `pitch` = points per row of psi.
 int col_fast(int L, int ns, int cols, c128* psi, const c128* expKT, const c128* tw, hipStream_t st, int pitch = -1) {
   if (pitch < 0) pitch = cols;
+  if (L == 256 && q16_enabled()) {
+    if (ns == 1) hipLaunchKernelGGL(spo2_col_q16_kernel<1>, dim3(cols, 1), dim3(64), 0, st, psi, expKT, tw, cols, pitch);
+    else hipLaunchKernelGGL(spo2_col_q16_kernel<2>, dim3(cols, 2), dim3(64), 0, st, psi, expKT, tw, cols, pitch);
+    QD_HIP(hipGetLastError());
+    return QD_OK;
+  }
   const int W = 2 * ns;
   const int bd = std::max(64, W * L / 4);
   const size_t lds = (size_t)(L + 2 * W * L) * sizeof(c128);

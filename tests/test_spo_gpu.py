@@ -43,7 +43,8 @@ def test_spo2_matches_reference(name):
     assert relerr(r.psi, g["psilist"][-1]) < TOL
 
 
-@pytest.mark.parametrize("n,ns,masses", [(256, 2, (1.0, 1.0)), (128, 3, (1.0, 2.0)), (512, 1, (2.0, 1.0)),
+@pytest.mark.parametrize("n,ns,masses", [(256, 2, (1.0, 1.0)), (256, 1, (1.0, 2.0)), (128, 3, (1.0, 2.0)),
+                                         (512, 1, (2.0, 1.0)),
                                          (16, 2, (1.0, 1.0))])
 def test_spo2_vs_oracle_bench_size(n, ns, masses):
     """BASELINE config d2 size (256x256x2) and other shapes vs the NumPy restatement."""
