@@ -329,7 +329,10 @@ def bench_2des_t2scan(dev, world, rank, M_total, n2, reps, n=256):
         "roofline": {"bound": "mfma", "kernel": "ens_t2_gemm_kernel", "achieved": round(gemm_flop / ev_apply / 1e12, 3),
                      "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(gemm_flop / ev_apply / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
-                     "flop_per_scan": gemm_flop, "traffic": None,
+                     "flop_per_scan": gemm_flop,
+                     "traffic": measured_traffic("ens_t2_gemm_kernel", 1) if (M_total, n, world) == (4096, 256, 1) else None,
+                     "traffic_unit": "HBM bytes per ens_t2_gemm_kernel launch (4 waiting times; PMC FETCH_SIZE+WRITE_SIZE, "
+                                     "calibrated; profiles/pmc_traffic.json)",
                      "note": "8 n3 n1 n2 K flop per scan (K = members x nL) / event time of the bucket applies "
                              "(E table + GEMM + slab reduction): a lower bound on the GEMM kernel's own rate"},
     }
@@ -402,7 +405,11 @@ def bench_spo2(dev, steps, n=256, dt=0.05):
         "roofline": {"bound": "hbm", "achieved": round(bytes_per_step * steps / ev / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(bytes_per_step * steps / ev / 1e9 / HBM_PEAK_GBS, 4),
                      "bytes_per_step": bytes_per_step,
-                     "note": "working set (7 MiB) is MALL-resident; launch-gap bound at this size"},
+                     "traffic": (measured_traffic("spo2_row_q16_kernel<2>", 1) + measured_traffic("spo2_col_q16_kernel<2>", 1))
+                     if n == 256 and os.environ.get("QD_SPO_Q16", "1") != "0" else None,
+                     "traffic_unit": "HBM bytes per Strang step (row + column pass; PMC FETCH_SIZE+WRITE_SIZE, calibrated; "
+                                     "profiles/pmc_traffic.json)",
+                     "note": "working set (7 MiB) is MALL-resident; two dependent passes per step bound it (latency)"},
         "us_per_step": round(wall / steps * 1e6, 2), "norm_ratio": norm,
         "build_ms": round(build_ms, 3),
         "run_wall_s": round(run_wall, 4),
