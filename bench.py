@@ -585,12 +585,13 @@ def main():
     tr_err = float((tr - 1).abs().max().item())
 
     # single-trajectory latency (B=1), informational
+    # (the auto dispatch of LindbladSolver.run: one matrix runs the general kernel's split path)
     r1 = rho[:1].clone()
-    lindblad_rk4(Ht, Ct, r1, args.dt, 2, hermitian=herm)
+    lindblad_rk4(Ht, Ct, r1, args.dt, 2)
     torch.cuda.synchronize(dev)
-    s1 = 20
+    s1 = 100
     ta = time.perf_counter()
-    lindblad_rk4(Ht, Ct, r1, args.dt, s1, hermitian=herm)
+    lindblad_rk4(Ht, Ct, r1, args.dt, s1)
     torch.cuda.synchronize(dev)
     single_rate = s1 / (time.perf_counter() - ta)
 

@@ -53,6 +53,7 @@ struct LindbladParams {
   double dt;
   unsigned long long* tbuf;  // [B][8] per-phase wall-clock ticks (QD_PHASE_TIMING diagnostics) or null
   unsigned long long stagger;  // start offset (wall-clock ticks) of the odd workgroup group of each XCD
+  int stage, rin, rout;        // split path: RK4 stage; stage input / output buffer (0 = rho, 1/2 = scratch 0/1)
 };
 
 // Per-matrix scratch slots of Np x Np: stage buffer(s), RK4 accumulator, Y_c.
@@ -471,6 +472,108 @@ __global__ void sandwich_prep_kernel(const c128* Lm, const c128* Rm, int N, int 
   }
 }
 
+// ---------------------------------------------------------------- split path (small batches)
+// A persistent workgroup per density matrix leaves most of the chip idle when B is small (one
+// trajectory = one CU).  Here every BT x BT output block of a stage phase is a workgroup of its own,
+// and the phases are kernel launches:
+//   glf_split_y_kernel  grid (nb^2, nc, B):  Y_c[bm, bn] = L_c[bm, :] r[:, bn]
+//   glf_split_k_kernel  grid (nb^2, 1, B):   k[bm, bn] = P r + r Q + sum_c Y_c R_c (2 + nc segments),
+//                                            fused RK4 epilogue of the block (same order as the
+//                                            persistent kernel's rk4_update)
+// Stage buffers: stage 0 reads rho, then scratch 0 / 1 alternate; stage 3 writes rho only, which is the
+// next step's stage-0 input.  Scratch per matrix: [buf0, buf1, acc, Y_0 .. Y_nc-1].
+__device__ __forceinline__ c128* split_buf(const LindbladParams& p, int b, int which) {
+  const size_t NN = (size_t)p.Np * p.Np;
+  if (which == 0) return p.rho + (size_t)b * NN;
+  return p.ws + (size_t)b * (3 + p.nc) * NN + (size_t)(which - 1) * NN;
+}
+
+template <int BT>
+__global__ __launch_bounds__(CG_WG) void glf_split_y_kernel(LindbladParams p) {
+  __shared__ CgLds<BT> L;
+  __shared__ CgSeg segs[1];
+  const int nb = p.Np / BT, bm = blockIdx.x / nb, bn = blockIdx.x % nb, c = blockIdx.y, b = blockIdx.z;
+  const int Np = p.Np;
+  const size_t NN = (size_t)Np * Np;
+  const c128* r = split_buf(p, b, p.rin);
+  c128* Yc = p.ws + (size_t)b * (3 + p.nc) * NN + (size_t)(3 + c) * NN;
+  if (threadIdx.x == 0) {
+    segs[0].A = p.Cop + (size_t)c * NN + (size_t)bm * BT * Np;
+    segs[0].B = r + bn * BT;
+  }
+  __syncthreads();
+  CgAcc<BT> A;
+  cg_block_gemm<BT>(segs, 1, Np, Np, Np, L, A);
+  cg_epilogue<BT>(A, [&](int row, int col, c128 v) { Yc[(size_t)(bm * BT + row) * Np + bn * BT + col] = v; });
+}
+
+template <int BT>
+__global__ __launch_bounds__(CG_WG) void glf_split_k_kernel(LindbladParams p) {
+  __shared__ CgLds<BT> L;
+  __shared__ CgSeg segs[2 + MAX_NC];
+  const int nb = p.Np / BT, bm = blockIdx.x / nb, bn = blockIdx.x % nb, b = blockIdx.y;
+  const int Np = p.Np, nc = p.nc;
+  const size_t NN = (size_t)Np * Np;
+  const c128* r = split_buf(p, b, p.rin);
+  c128* rn = p.rout ? split_buf(p, b, p.rout) : nullptr;
+  c128* rho = p.rho + (size_t)b * NN;
+  c128* ws = p.ws + (size_t)b * (3 + nc) * NN;
+  c128* acc = ws + 2 * NN;
+  const c128* Y = ws + 3 * NN;
+  if (threadIdx.x == 0) {
+    segs[0].A = p.mK + (size_t)bm * BT * Np;
+    segs[0].B = r + bn * BT;
+    segs[1].A = r + (size_t)bm * BT * Np;
+    segs[1].B = p.iKd + bn * BT;
+    for (int c = 0; c < nc; ++c) {
+      segs[2 + c].A = Y + (size_t)c * NN + (size_t)bm * BT * Np;
+      segs[2 + c].B = p.Cd + (size_t)c * NN + bn * BT;
+    }
+  }
+  __syncthreads();
+  CgAcc<BT> A;
+  cg_block_gemm<BT>(segs, 2 + nc, Np, Np, Np, L, A);
+  const int stage = p.stage;
+  const double dt = p.dt, dt2 = p.dt / 2.0;
+  cg_epilogue<BT>(A, [&](int row, int col, c128 k) {
+    const size_t idx = (size_t)(bm * BT + row) * Np + bn * BT + col;
+    const c128 r0 = rho[idx];
+    if (stage == 0) {
+      acc[idx] = k;
+      rn[idx] = cadd(r0, cscale(k, dt2));
+    } else if (stage == 1) {
+      acc[idx] = cadd(acc[idx], cscale(k, 2.0));
+      rn[idx] = cadd(r0, cscale(k, dt2));
+    } else if (stage == 2) {
+      acc[idx] = cadd(acc[idx], cscale(k, 2.0));
+      rn[idx] = cadd(r0, cscale(k, dt));
+    } else {
+      const c128 a = cadd(acc[idx], k);
+      rho[idx] = cadd(r0, cscale(cscale(a, 1.0 / 6.0), dt));
+    }
+  });
+}
+
+// Observables / snapshot of global step gs (after it; gs = 0: the initial state), one workgroup per matrix.
+__global__ __launch_bounds__(CG_WG) void glf_split_obs_kernel(LindbladParams p, int gs) {
+  __shared__ c128 sred[CG_WG / 64];
+  const int b = blockIdx.x;
+  const size_t NN = (size_t)p.Np * p.Np;
+  const c128* rho = p.rho + (size_t)b * NN;
+  if (p.ne > 0) wg_observables(rho, p.eT, p.ne, NN, p.obs + ((size_t)b * (p.total_steps + 1) + gs) * p.ne, sred);
+  if (gs > 0 && p.snap && p.save_every > 0 && (gs % p.save_every) == 0) {
+    const int s = gs / p.save_every - 1;
+    if (s < p.nsave) {
+      const int N = p.N;
+      c128* out = p.snap + ((size_t)b * p.nsave + s) * N * N;
+      for (size_t i = threadIdx.x; i < (size_t)N * N; i += CG_WG) {
+        const int ii = (int)(i / N), jj = (int)(i % N);
+        out[i] = rho[(size_t)ii * p.Np + jj];
+      }
+    }
+  }
+}
+
 int padded_dim(int N) {
   if (N <= 32) return 32;
   if (N <= 64) return 64;
@@ -533,7 +636,29 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   // state workspace: per-matrix scratch (+ padded rho when N != Np)
   const bool pad = (Np != N);
   if (Np > 128) herm = 0;  // the Hermitian path is single-block
-  const size_t per = (size_t)glf_slots(Np, nc, herm) * NN;
+  // Split path (glf_split_*): each output block of a phase is a workgroup, for batches too small to
+  // occupy the chip with one persistent workgroup per matrix.  QD_GLF_SPLIT=0 / 1 forces it off / on.
+  // Measured (tools/glf_split_bench.py, N = 128 / 256, B = 1 .. 256): the split path wins for every batch
+  // below ~192 matrices at Np <= 128 (6.6x at one trajectory) and at every batch size above Np = 128;
+  // the block is the largest BT < Np that still gives >= 512 workgroups, else 32.
+  int split_bt = 0;
+  {
+    int bt = 32;
+    for (int v : {128, 64}) {
+      if (v < Np && Np % v == 0 && (long)B * (Np / v) * (Np / v) >= 512) {
+        bt = v;
+        break;
+      }
+    }
+    if (const char* e = std::getenv("QD_GLF_SPLIT_BT")) {  // A/B override: 32, 64 or 128 (dividing Np)
+      const int v = std::atoi(e);
+      if ((v == 32 || v == 64 || v == 128) && Np % v == 0) bt = v;
+    }
+    bool use = !herm && Np >= 64 && (Np > 128 || B < 192);
+    if (const char* e = std::getenv("QD_GLF_SPLIT")) use = std::atoi(e) != 0 && !herm && Np >= 64;
+    if (use) split_bt = bt;
+  }
+  const size_t per = (size_t)(split_bt ? 3 + nc : glf_slots(Np, nc, herm)) * NN;
   const size_t st_elems = (size_t)B * per + (pad ? (size_t)B * NN : 0);
   void* wst = nullptr;
   rc = workspace(WS_LINDBLAD, st_elems * sizeof(c128), &wst);
@@ -590,6 +715,7 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   p.herm = herm;
   p.tbuf = nullptr;
   p.stagger = 0;
+  p.stage = p.rin = p.rout = 0;
   if (const char* e = std::getenv("QD_STAGGER_US")) p.stagger = (unsigned long long)(std::atof(e) * 100.0);  // 100 MHz
 #ifdef QD_PHASE_TIMING
   const bool timing = true;  // diagnostics build: per-phase clocks to stderr
@@ -601,7 +727,41 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
     QD_HIP(hipMemsetAsync(p.tbuf, 0, (size_t)B * 8 * sizeof(unsigned long long), st));
   }
 
+  auto launch_split = [&]() -> int {
+    const int nb = Np / split_bt;
+    auto obs_at = [&](int gs) -> int {
+      hipLaunchKernelGGL(glf_split_obs_kernel, dim3(B), dim3(CG_WG), 0, st, p, gs);
+      QD_HIP(hipGetLastError());
+      return QD_OK;
+    };
+    int rc2;
+    if (p.ne > 0 && p.step0 == 0 && (rc2 = obs_at(0))) return rc2;
+    for (int s = 0; s < p.nsteps; ++s) {
+      for (int stage = 0; stage < 4; ++stage) {
+        p.stage = stage;
+        p.rin = stage == 0 ? 0 : ((stage - 1) & 1) + 1;
+        p.rout = stage == 3 ? 0 : (stage & 1) + 1;
+#define QD_SPLIT(KERN, GRID)                                                                   \
+  switch (split_bt) {                                                                            \
+    case 32: hipLaunchKernelGGL(KERN<32>, GRID, dim3(CG_WG), 0, st, p); break;                   \
+    case 64: hipLaunchKernelGGL(KERN<64>, GRID, dim3(CG_WG), 0, st, p); break;                   \
+    default: hipLaunchKernelGGL(KERN<128>, GRID, dim3(CG_WG), 0, st, p); break;                  \
+  }
+        if (nc > 0) {
+          QD_SPLIT(glf_split_y_kernel, dim3(nb * nb, nc, B));
+          QD_HIP(hipGetLastError());
+        }
+        QD_SPLIT(glf_split_k_kernel, dim3(nb * nb, B));
+        QD_HIP(hipGetLastError());
+#undef QD_SPLIT
+      }
+      const int gs = p.step0 + s + 1;
+      if ((p.ne > 0 || (p.snap && p.save_every > 0 && gs % p.save_every == 0)) && (rc2 = obs_at(gs))) return rc2;
+    }
+    return QD_OK;
+  };
   auto launch = [&]() -> int {
+    if (split_bt) return launch_split();
     if (Np == 32) {
       if (herm) hipLaunchKernelGGL((lindblad_rk4_kernel<32, true>), dim3(B), dim3(CG_WG), 0, st, p);
       else hipLaunchKernelGGL((lindblad_rk4_kernel<32, false>), dim3(B), dim3(CG_WG), 0, st, p);

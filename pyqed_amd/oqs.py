@@ -23,6 +23,11 @@ except Exception:  # pragma: no cover
 
 
 # --------------------------------------------------------------------------- functional
+# Below this many matrices the general kernel's split path (a workgroup per output block and phase)
+# outruns the persistent Hermitian kernel (one workgroup per matrix): tools/glf_split_bench.py.
+HERM_MIN_BATCH = 192
+
+
 def lindblad_rk4(H: torch.Tensor, c_ops: torch.Tensor | None, rho: torch.Tensor, dt: float, nsteps: int,
                  e_ops: torch.Tensor | None = None, save_every: int = 0, stream=None,
                  hermitian: bool | None = None):
@@ -33,9 +38,12 @@ def lindblad_rk4(H: torch.Tensor, c_ops: torch.Tensor | None, rho: torch.Tensor,
     snap [B,nsteps//save_every,N,N] | None).  Reference RHS: oqs.py:697-714.
 
     hermitian: use the Hermitian-state kernel (qd_lindblad_rk4_herm: L[rho] = X + X^+,
-    1 + 2nc complex GEMMs per RHS instead of 2 + 2nc).  None = auto: on when every rho
-    in the batch equals its conjugate transpose bit for bit and N <= 128.  The Lindblad
-    generator preserves Hermiticity, and the kernel keeps it exact at every stage.
+    1 + 2nc complex GEMMs per RHS instead of 2 + 2nc, one persistent workgroup per matrix).
+    None = auto: on when every rho in the batch equals its conjugate transpose bit for bit,
+    N <= 128 and the batch fills the chip (B >= HERM_MIN_BATCH); smaller batches run the general
+    kernel, whose split path spreads each matrix over many workgroups (qd_lindblad_rk4: 8.3k
+    instead of 1.3k steps/s for one N = 128 trajectory).  The Lindblad generator preserves
+    Hermiticity, and the Hermitian kernel keeps it exact at every stage.
     """
     squeeze = rho.dim() == 2
     if squeeze:
@@ -60,7 +68,7 @@ def lindblad_rk4(H: torch.Tensor, c_ops: torch.Tensor | None, rho: torch.Tensor,
     snap = torch.empty((B, nsave, N, N), dtype=torch.complex128, device=dev) if nsave else None
     st = stream if stream is not None else _lib.stream_ptr(dev)
     if hermitian is None:
-        hermitian = N <= 128 and bool(torch.equal(rho, rho.transpose(-1, -2).conj()))
+        hermitian = N <= 128 and B >= HERM_MIN_BATCH and bool(torch.equal(rho, rho.transpose(-1, -2).conj()))
     fn = "qd_lindblad_rk4_herm" if hermitian else "qd_lindblad_rk4"
     with torch.cuda.device(dev):
         rc = getattr(_lib.load(), fn)(_lib.ptr(H), _lib.ptr(c_ops), nc, _lib.ptr(rho), B, N, float(dt),
@@ -491,7 +499,10 @@ class RedfieldSolver:
             basis_transform(evecs_t, Ed, inverse=False)
         rho0_eb = rho[0].cpu().numpy()
         r0 = to_numpy(rho0, np.complex128)
-        herm = N <= 128 and np.array_equal(r0, r0.conj().T)
+        # one trajectory (B = 1 < HERM_MIN_BATCH): the general GLF kernel's split path outruns the persistent
+        # Hermitian-state kernel, which serves batches of Hermitian states (glf_rk4(..., hermitian=True))
+        B = 1
+        herm = N <= 128 and B >= HERM_MIN_BATCH and np.array_equal(r0, r0.conj().T)
         if herm:
             # Hermitian input: symmetrise the transformed state (rounding of V^+ rho V only) and propagate
             # with the Hermitian-state kernel (1 + 2 n_a GEMMs per RHS instead of 2 + 4 n_a)
