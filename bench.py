@@ -218,7 +218,11 @@ def bench_2des(dev, world, rank, M_total, reps, n=256):
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     wall = float(tt.item())
-    K = (hi - lo) * 9
+    # executed GEMM K: members x the smaller pruned eigen-index set (exact structural zeros dropped,
+    # pyqed_amd.response._prune_fixed_t2), padded to the 16-wide K-tile
+    from pyqed_amd.response import _prune_fixed_t2
+    nk = _prune_fixed_t2(lam_t, alpha_t, Mt_t, beta_t)[1].shape[1]
+    K = (hi - lo) * nk
     Kp = (K + 15) // 16 * 16
     gemm_flop = 8.0 * n * n * Kp
     res = {
@@ -230,6 +234,7 @@ def bench_2des(dev, world, rank, M_total, reps, n=256):
                    if world > 1 else "none"},
         "ms_per_grid": round(wall / reps * 1e3, 4),
         "gemm_flop_per_grid_per_rank": gemm_flop,
+        "gemm_k_per_member": nk,
         "event_ms_per_grid": round(e0.elapsed_time(e1) / reps, 4),
     }
     return res, out, (lam, alpha, Mt, beta)
@@ -313,7 +318,8 @@ def bench_2des_t2scan(dev, world, rank, M_total, n2, reps, n=256):
         ev_apply += a0.elapsed_time(a1) / 1e3
     comp = (time.perf_counter() - c0) / reps
     ev_apply /= reps
-    Kp = ((hi - lo) * 9 + 15) // 16 * 16
+    nr = scan[0].nL                         # executed K per member: the pruned waiting-time index set
+    Kp = ((hi - lo) * nr + 15) // 16 * 16
     gemm_flop = 8.0 * n * n * n2 * Kp
     return {
         "value": round(n * n * n2 * M_total * reps / wall, 1),
@@ -326,11 +332,12 @@ def bench_2des_t2scan(dev, world, rank, M_total, n2, reps, n=256):
         "ms_per_scan": round(wall / reps * 1e3, 4),
         "compute_ms_per_scan": round(comp * 1e3, 4),
         "gemm_tflops": round(gemm_flop / comp / 1e12, 2),
+        "index_set_sizes_p_r_q": list(scan[0].index_sizes),
         "roofline": {"bound": "mfma", "kernel": "ens_t2_gemm_kernel", "achieved": round(gemm_flop / ev_apply / 1e12, 3),
                      "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(gemm_flop / ev_apply / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
                      "flop_per_scan": gemm_flop,
-                     "traffic": measured_traffic("ens_t2_gemm_kernel", 1) if (M_total, n, world) == (4096, 256, 1) else None,
+                     "traffic": measured_traffic("ens_t2_gemm_kernel_pruned", 1) if (M_total, n, world) == (4096, 256, 1) else None,
                      "traffic_unit": "HBM bytes per ens_t2_gemm_kernel launch (4 waiting times; PMC FETCH_SIZE+WRITE_SIZE, "
                                      "calibrated; profiles/pmc_traffic.json)",
                      "note": "8 n3 n1 n2 K flop per scan (K = members x nL) / event time of the bucket applies "

@@ -327,6 +327,22 @@ int qd_response2d_ensemble_uniform(const qd_c128* alpha, const qd_c128* Mt,
                                    int accumulate, void* stream);
 
 /*
+ * Rectangular form of qd_response2d_ensemble(_uniform), used after the host prunes index sets that are
+ * structurally zero (selection rules: alpha[:, p] == 0 or beta[:, q] == 0 for every member, exactly):
+ *   S[i][k] = (-i)^3 sum_m sum_{p < nx} sum_{q < nz} alpha[m][p] e^{lamx[m][p] t3_i}
+ *                                      Mt[m][p][q] beta[m][q] e^{lamz[m][q] t1_k}
+ * with alpha, lamx [M][nx], Mt [M][nx][nz], beta, lamz [M][nz].  GEMM K = M nx.  A null t3 / t1 means
+ * the uniform grid t0 + j dt (exponential tables).  transpose_out != 0 writes out[k][i] = S[i][k]
+ * (out is [n1][n3]): the host's swapped call, which puts the smaller index set on K.
+ */
+int qd_response2d_ensemble_rect(const qd_c128* alpha, const qd_c128* lamx, int nx,
+                                const qd_c128* Mt, const qd_c128* beta, const qd_c128* lamz,
+                                int nz, int M, const double* t3, double t3_0, double dt3,
+                                int n3, const double* t1, double t1_0, double dt1, int n1,
+                                int transpose_out, qd_c128* out, int accumulate,
+                                void* stream);
+
+/*
  * Waiting-time scan of the disorder-ensemble 2D response (uniform t3 / t1 grids, t2 a device array of
  * n2 waiting times):
  *   out[j][i][k] (+)= (-i)^3 sum_m sum_pq alpha[m][p] e^{lam[m][p] t3_i}
@@ -352,6 +368,17 @@ int qd_response2d_t2_operands(const qd_c128* alpha, const qd_c128* B, const qd_c
                               const qd_c128* beta, const qd_c128* lam, int M, int nL,
                               double t3_0, double dt3, int n3, double t1_0, double dt1,
                               int n1, qd_c128* P, qd_c128* Q, void* stream);
+
+/*
+ * Pruned scan operands: alpha, lamp [M][np] (t3 side), B [M][np][nr], lamr [M][nr] (the waiting-time
+ * index r; E_j = e^{lamr t2_j}), C [M][nr][nq], beta, lamq [M][nq] (t1 side).  P is [n3p][Kp] and Q
+ * [Kp][n1p] with Kp from qd_response2d_t2_dims(M, nr, ...); apply with (lamr, nr).
+ */
+int qd_response2d_t2_operands_rect(const qd_c128* alpha, const qd_c128* lamp, int np,
+                                   const qd_c128* B, const qd_c128* lamr, int nr,
+                                   const qd_c128* C, const qd_c128* beta, const qd_c128* lamq,
+                                   int nq, int M, double t3_0, double dt3, int n3, double t1_0,
+                                   double dt1, int n1, qd_c128* P, qd_c128* Q, void* stream);
 
 /* out [n2][n3][n1] (+)= the scan for waiting times t2 (device array) from prepared P, Q. */
 int qd_response2d_t2_apply(const qd_c128* P, const qd_c128* Q, const qd_c128* lam, int M,

@@ -71,6 +71,12 @@ SIGNATURES = {
     "qd_response2d_t2_dims": (c_int, [c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "qd_response2d_t2_operands": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double,
                                           c_double, c_int, c_double, c_double, c_int, c_void_p, c_void_p, c_void_p]),
+    "qd_response2d_ensemble_rect": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                            c_void_p, c_double, c_double, c_int, c_void_p, c_double, c_double, c_int,
+                                            c_int, c_void_p, c_int, c_void_p]),
+    "qd_response2d_t2_operands_rect": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                                               c_void_p, c_void_p, c_int, c_int, c_double, c_double, c_int, c_double,
+                                               c_double, c_int, c_void_p, c_void_p, c_void_p]),
     "qd_response2d_t2_apply": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
                                        c_void_p, c_int, c_void_p]),
     "qd_comm_unique_id": (c_int, [c_void_p]),

@@ -94,14 +94,15 @@ __global__ void cube_out_kernel(const c128* alpha, const c128* lam, const c128* 
 //   blockIdx.y <  M : Z rows of member m (below)
 //   blockIdx.y >= M : X [n3p][Kp], X[i][m*nL+p] = i * alpha_mp e^{lam_mp t3_i} (zero in the padding),
 //                     grid-strided over the (blockIdx.y - M, blockIdx.x) blocks
-// Z [Kp][n1p]: Z[m*nL+p][k] = sum_q Mt[m][p][q] y_q(k),  y_q(k) = beta[m][q] e^{lam_mq t1_k}
-// one thread per t1 point computes the nL exponentials once (registers, nL <= ZMAX) and emits the
-// nL outputs of its column; Mt_m staged in LDS.
+// Z [Kp][n1p]: Z[m*nL+p][k] = sum_q Mt[m][p][q] y_q(k),  y_q(k) = beta[m][q] e^{lamz_mq t1_k}
+// one thread per t1 point computes the nz exponentials once (registers, nz <= ZMAX) and emits the
+// nL outputs of its column; Mt_m (nL x nz, rectangular when structurally zero alpha / beta columns
+// were pruned on the host) staged in LDS.
 constexpr int ZMAX = 16;
 __global__ __launch_bounds__(256) void ens_xz_kernel(const c128* Mt, const c128* beta, const c128* lam, int M, int nL,
                                                      const double* t1, int n1, int n1p, int Kp, c128* Z,
                                                      const c128* alpha, const double* t3, int n3, int n3p, int xrows,
-                                                     int K, c128* X) {
+                                                     int K, c128* X, int nz, const c128* lamz) {
   __shared__ c128 sM[ZMAX * ZMAX];
   if ((int)blockIdx.y >= M) {
     const size_t tot = (size_t)n3p * Kp;
@@ -117,19 +118,19 @@ __global__ __launch_bounds__(256) void ens_xz_kernel(const c128* Mt, const c128*
   }
   const int m = blockIdx.y;
   const int k = blockIdx.x * 256 + threadIdx.x;
-  for (int e = threadIdx.x; e < nL * nL; e += 256) sM[e] = Mt[(size_t)m * nL * nL + e];
+  for (int e = threadIdx.x; e < nL * nz; e += 256) sM[e] = Mt[(size_t)m * nL * nz + e];
   __syncthreads();
   if (k >= n1p) return;
   c128 y[ZMAX];
   const double tk = k < n1 ? t1[k] : 0.0;
 #pragma unroll
   for (int q = 0; q < ZMAX; ++q)
-    y[q] = (q < nL && k < n1) ? cmul(beta[(size_t)m * nL + q], cexp_t(lam[(size_t)m * nL + q], tk)) : cmk(0, 0);
+    y[q] = (q < nz && k < n1) ? cmul(beta[(size_t)m * nz + q], cexp_t(lamz[(size_t)m * nz + q], tk)) : cmk(0, 0);
   for (int p = 0; p < nL; ++p) {
     c128 v = cmk(0, 0);
 #pragma unroll
     for (int q = 0; q < ZMAX; ++q)
-      if (q < nL) v = cadd(v, cmul(sM[p * nL + q], y[q]));
+      if (q < nz) v = cadd(v, cmul(sM[p * nz + q], y[q]));
     Z[((size_t)m * nL + p) * n1p + k] = v;
   }
 }
@@ -171,7 +172,8 @@ constexpr int UNI_MAXC = 1024 / 16;
 __global__ __launch_bounds__(256) void ens_xz_uniform_kernel(const c128* Mt, const c128* beta, const c128* lam, int M,
                                                              int nL, double t0, double dt, int n1, int n1p, int Kp,
                                                              c128* Z, const c128* alpha, int K, double t3_0,
-                                                             double dt3, int n3, int n3p, int xbx, c128* X) {
+                                                             double dt3, int n3, int n3p, int xbx, c128* X, int nz,
+                                                             const c128* lamz) {
   __shared__ c128 sM[ZMAX * ZMAX];
   __shared__ c128 sF[ZMAX * 16];        // e^{lam_q j dt}
   __shared__ c128 sC[ZMAX * UNI_MAXC];  // beta_q e^{lam_q (t0 + 16 l dt)}
@@ -183,23 +185,23 @@ __global__ __launch_bounds__(256) void ens_xz_uniform_kernel(const c128* Mt, con
   }
   const int m = blockIdx.y;
   const int nC = n1p / 16;
-  const c128* lm = lam + (size_t)m * nL;
-  for (int e = threadIdx.x; e < nL * nL; e += 256) sM[e] = Mt[(size_t)m * nL * nL + e];
-  for (int e = threadIdx.x; e < nL * 16; e += 256) sF[e] = cexp_t(lm[e / 16], (double)(e % 16) * dt);
-  for (int e = threadIdx.x; e < nL * nC; e += 256)
-    sC[e] = cmul(beta[(size_t)m * nL + e / nC], cexp_t(lm[e / nC], t0 + 16.0 * (double)(e % nC) * dt));
+  const c128* lm = lamz + (size_t)m * nz;
+  for (int e = threadIdx.x; e < nL * nz; e += 256) sM[e] = Mt[(size_t)m * nL * nz + e];
+  for (int e = threadIdx.x; e < nz * 16; e += 256) sF[e] = cexp_t(lm[e / 16], (double)(e % 16) * dt);
+  for (int e = threadIdx.x; e < nz * nC; e += 256)
+    sC[e] = cmul(beta[(size_t)m * nz + e / nC], cexp_t(lm[e / nC], t0 + 16.0 * (double)(e % nC) * dt));
   __syncthreads();
   const int k = blockIdx.x * 256 + threadIdx.x;
   if (k >= n1p) return;
   c128 y[ZMAX];
 #pragma unroll
   for (int q = 0; q < ZMAX; ++q)
-    y[q] = (q < nL && k < n1) ? cmul(sC[q * nC + (k >> 4)], sF[q * 16 + (k & 15)]) : cmk(0, 0);
+    y[q] = (q < nz && k < n1) ? cmul(sC[q * nC + (k >> 4)], sF[q * 16 + (k & 15)]) : cmk(0, 0);
   for (int p = 0; p < nL; ++p) {
     c128 v = cmk(0, 0);
 #pragma unroll
     for (int q = 0; q < ZMAX; ++q)
-      if (q < nL) v = cadd(v, cmul(sM[p * nL + q], y[q]));
+      if (q < nz) v = cadd(v, cmul(sM[p * nz + q], y[q]));
     Z[((size_t)m * nL + p) * n1p + k] = v;
   }
 }
@@ -213,7 +215,7 @@ __global__ void ens_z_pad_kernel(int K, int Kp, int n1p, c128* Z) {
 
 // Generic fallback for nL > ZMAX (one thread per output element).
 __global__ void ens_z_generic_kernel(const c128* Mt, const c128* beta, const c128* lam, int M, int nL,
-                                     const double* t1, int n1, int n1p, int Kp, c128* Z) {
+                                     const double* t1, int n1, int n1p, int Kp, c128* Z, int nz) {
   const size_t tot = (size_t)Kp * n1p;
   const int K = M * nL;
   for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
@@ -221,9 +223,9 @@ __global__ void ens_z_generic_kernel(const c128* Mt, const c128* beta, const c12
     c128 v = cmk(0, 0);
     if (row < K && k < n1) {
       const int m = row / nL, p = row % nL;
-      const c128* Mr = Mt + ((size_t)m * nL + p) * nL;
-      for (int q = 0; q < nL; ++q)
-        v = cadd(v, cmul(Mr[q], cmul(beta[(size_t)m * nL + q], cexp_t(lam[(size_t)m * nL + q], t1[k]))));
+      const c128* Mr = Mt + ((size_t)m * nL + p) * nz;
+      for (int q = 0; q < nz; ++q)
+        v = cadd(v, cmul(Mr[q], cmul(beta[(size_t)m * nz + q], cexp_t(lam[(size_t)m * nz + q], t1[k]))));
     }
     Z[e] = v;
   }
@@ -245,12 +247,13 @@ struct EnsXA {
   __device__ __forceinline__ cg_v2 finish(const Raw& r, int, int, int) const { return r; }
 };
 
+template <int BT = ENS_BT>
 struct EnsZB {
   using Raw = cg_v2;
   const c128* Z;
   int n1p, col0, k0;
   __device__ __forceinline__ Raw fetch(int t, int e, int) const {
-    return cg_ld(Z + (size_t)(k0 + t * CG_KT + e / ENS_BT) * n1p + col0 + (e % ENS_BT));
+    return cg_ld(Z + (size_t)(k0 + t * CG_KT + e / BT) * n1p + col0 + (e % BT));
   }
   __device__ __forceinline__ cg_v2 finish(const Raw& r, int, int, int) const { return r; }
 };
@@ -269,26 +272,60 @@ __device__ __forceinline__ void ens_tile(int& bn, int& bm, int& s) {
   s = u / (NX * NY);
 }
 
-// grid: (n1p/BT) x (n3p/BT) x S ; each workgroup accumulates K-tiles [t0, t1) of its block
+// grid: (n1p/BT) x (n3p/BT) x S ; each workgroup accumulates K-tiles [t0, t1) of its block.  BT = 64 for
+// problems whose 128-blocks cannot fill the chip with >= 4 K-tiles per workgroup (4x the blocks, 1/4 the
+// split-K slabs to write and reduce).
+template <int BT>
 __global__ __launch_bounds__(CG_WG) void ens_gemm_kernel(const c128* X, int Kp, const c128* Z, int n1p, int tiles,
                                                          int S, c128* slabs, int n3p) {
-  __shared__ CgLds<ENS_BT> L;
+  __shared__ CgLds<BT> L;
   int bn, bm, s;
   ens_tile(bn, bm, s);
   const int t0 = (int)((long)tiles * s / S), t1 = (int)((long)tiles * (s + 1) / S);
-  CgAcc<ENS_BT> A;
+  CgAcc<BT> A;
   c128* slab = slabs + (size_t)s * n3p * n1p;
   if (t1 > t0) {
-    EnsXA pa{X, Kp, bm * ENS_BT, t0 * CG_KT};
-    EnsZB pb{Z, n1p, bn * ENS_BT, t0 * CG_KT};
-    cg_block_gemm_gen<ENS_BT, ENS_PIPE>(t1 - t0, pa, pb, L, A);
-    cg_epilogue<ENS_BT>(A, [&](int row, int col, c128 v) {
-      slab[(size_t)(bm * ENS_BT + row) * n1p + bn * ENS_BT + col] = v;
+    EnsXA pa{X, Kp, bm * BT, t0 * CG_KT};
+    EnsZB<BT> pb{Z, n1p, bn * BT, t0 * CG_KT};
+    cg_block_gemm_gen<BT, ENS_PIPE>(t1 - t0, pa, pb, L, A);
+    cg_epilogue<BT>(A, [&](int row, int col, c128 v) {
+      slab[(size_t)(bm * BT + row) * n1p + bn * BT + col] = v;
     });
   } else {
-    for (int e = threadIdx.x; e < ENS_BT * ENS_BT; e += CG_WG)
-      slab[(size_t)(bm * ENS_BT + e / ENS_BT) * n1p + bn * ENS_BT + e % ENS_BT] = cmk(0, 0);
+    for (int e = threadIdx.x; e < BT * BT; e += CG_WG)
+      slab[(size_t)(bm * BT + e / BT) * n1p + bn * BT + e % BT] = cmk(0, 0);
   }
+}
+
+// (BT, S) for a split-K GEMM of Mp x Np (multiples of 128) over `tiles` K-tiles: 128-blocks with enough
+// splits to cover the 256 CUs once at >= 4 K-tiles per workgroup; 64-blocks when that leaves the chip
+// under-filled or needs more than 16 slabs.  QD_ENS_BT=64/128 forces the block size (A/B runs).
+struct SplitPlan {
+  int bt, S;
+};
+SplitPlan split_plan(int Mp, int Np, int tiles) {
+  static const int force = [] {
+    const char* e = std::getenv("QD_ENS_BT");
+    return e ? std::atoi(e) : 0;
+  }();
+  auto splits = [&](int bt) {
+    const int blocks = (Mp / bt) * (Np / bt);
+    return std::max(1, std::min(ceil_div(256, blocks), std::max(1, tiles / 4)));
+  };
+  const int S128 = splits(128);
+  const bool small = (Mp / 128) * (Np / 128) * S128 < 256 || S128 > 16;
+  const int bt = force == 64 || force == 128 ? force : (small ? 64 : 128);
+  return {bt, splits(bt)};
+}
+
+void launch_ens_gemm(const SplitPlan& pl, const c128* X, int Kp, const c128* Z, int Mp, int Np, int tiles,
+                     c128* slabs, hipStream_t st) {
+  if (pl.bt == 64)
+    hipLaunchKernelGGL(ens_gemm_kernel<64>, dim3(Np / 64, Mp / 64, pl.S), dim3(CG_WG), 0, st, X, Kp, Z, Np, tiles,
+                       pl.S, slabs, Mp);
+  else
+    hipLaunchKernelGGL(ens_gemm_kernel<128>, dim3(Np / 128, Mp / 128, pl.S), dim3(CG_WG), 0, st, X, Kp, Z, Np, tiles,
+                       pl.S, slabs, Mp);
 }
 
 // out[i][k] (+)= sum_s slab[s][i][k], fixed order -> deterministic
@@ -300,6 +337,28 @@ __global__ void ens_reduce_kernel(const c128* slabs, int S, int n3, int n1, int 
     c128 v = accumulate ? out[e] : cmk(0, 0);
     for (int s = 0; s < S; ++s) v = cadd(v, slabs[((size_t)s * n3p + i) * n1p + k]);
     out[e] = v;
+  }
+}
+
+// out[k][i] (+)= sum_s slab[s][i][k] (out is n1 x n3): 16 x 16 tiles through LDS, coalesced on both sides
+__global__ __launch_bounds__(256) void ens_reduce_trans_kernel(const c128* slabs, int S, int n3, int n1, int n3p,
+                                                               int n1p, c128* out, int accumulate) {
+  __shared__ c128 tile[16][17];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int k0 = blockIdx.x * 16, i0 = blockIdx.y * 16;
+  {
+    const int i = i0 + ty, k = k0 + tx;
+    c128 v = cmk(0, 0);
+    if (i < n3 && k < n1)
+      for (int s = 0; s < S; ++s) v = cadd(v, slabs[((size_t)s * n3p + i) * n1p + k]);
+    tile[ty][tx] = v;
+  }
+  __syncthreads();
+  const int k = k0 + ty, i = i0 + tx;
+  if (i < n3 && k < n1) {
+    const size_t e = (size_t)k * n3 + i;
+    const c128 v = tile[tx][ty];
+    out[e] = accumulate ? cadd(out[e], v) : v;
   }
 }
 
@@ -322,22 +381,27 @@ __global__ void ens_reduce_t2_kernel(const c128* slabs, int S, int n2, int n3, i
 //   S_j = sum_m P_m diag(e^{lam_m t2_j}) Q_m = P * diag(E_j) * Q,   E_j[(m,r)] = e^{lam_mr t2_j},
 // so P [n3p][Kp] and Q [Kp][n1p] are built once per scan and the GEMM's B operand for waiting time j is
 // Q with its rows scaled by E_j, formed in the staging step (one complex multiply per staged element).
-// P block: MB = floor(256 / nL) members (MB nL columns), UNI_ROWS rows; the X values of a 16-row group go
-// through LDS and every column thread contracts them with its B_m[:, r] (registers).
-__global__ __launch_bounds__(256) void ens_p_uniform_kernel(const c128* alpha, const c128* Bm, const c128* lam, int M,
-                                                            int nL, double t0, double dt, int n3, int n3p, int Kp,
-                                                            c128* P) {
+// P block: MB = floor(256 / max(np, nr)) members; thread c < MB np computes x_{m p}(t) for (m, p) =
+// (m0 + c / np, c % np), the X values of a 16-row group go through LDS, and output thread c < MB nr,
+// (m, r) = (m0 + c / nr, c % nr), contracts its member's np values with B_m[:, r] (registers).
+// np = nr = nL and lamp = lam in the unpruned form; the host passes the compact index sets otherwise.
+__global__ __launch_bounds__(256) void ens_p_uniform_kernel(const c128* alpha, const c128* Bm, const c128* lamp, int M,
+                                                            int np, int nr, double t0, double dt, int n3, int n3p,
+                                                            int Kp, c128* P) {
   __shared__ c128 sX[16 * 256];
-  const int MB = 256 / nL, W = MB * nL;
+  const int MB = 256 / (np > nr ? np : nr);
   const int m0 = blockIdx.x * MB;
-  const int c = threadIdx.x;                 // column of this block: member m0 + c / nL, index c % nL
-  const int m = m0 + c / nL, r = c % nL;
-  const bool col = c < W && m < M;
-  const int kk = m * nL + r;
-  const int i0 = blockIdx.y * UNI_ROWS;
-  // X part: this thread's x_{m r}(t) = i alpha_mr e^{lam_mr t} (the column it also owns in sX)
-  const c128 l = col ? lam[kk] : cmk(0, 0);
-  const c128 a = col ? cmuli(alpha[kk]) : cmk(0, 0);
+  const int c = threadIdx.x;
+  // X part: x_{m p}(t) = i alpha_mp e^{lamp_mp t} for (m, p) = (m0 + c / np, c % np)
+  const int mx = m0 + c / np, px = c % np;
+  const bool xcol = c < MB * np && mx < M;
+  const int kx = mx * np + px;
+  const c128 l = xcol ? lamp[kx] : cmk(0, 0);
+  const c128 a = xcol ? cmuli(alpha[kx]) : cmk(0, 0);
+  // output column (m, r) = (m0 + c / nr, c % nr), P column kk = m nr + r
+  const int m = m0 + c / nr, r = c % nr;
+  const bool col = c < MB * nr && m < M;
+  const int kk = m * nr + r;
   c128 T1[16];
   T1[0] = cmk(1, 0);
   const c128 st = cexp_t(l, dt);
@@ -345,10 +409,10 @@ __global__ __launch_bounds__(256) void ens_p_uniform_kernel(const c128* alpha, c
   for (int j = 1; j < 16; ++j) T1[j] = cmul(T1[j - 1], st);
   c128 b[ZMAX];
 #pragma unroll
-  for (int p = 0; p < ZMAX; ++p) b[p] = (col && p < nL) ? Bm[((size_t)m * nL + p) * nL + r] : cmk(0, 0);
-  const int mc0 = (c / nL) * nL;             // first column of this thread's member in the block
+  for (int p = 0; p < ZMAX; ++p) b[p] = (col && p < np) ? Bm[((size_t)m * np + p) * nr + r] : cmk(0, 0);
+  const int mc0 = (c / nr) * np;             // first sX column of this output thread's member
   for (int g = 0; g < UNI_ROWS / 16; ++g) {
-    const int ib = i0 + 16 * g;
+    const int ib = (int)blockIdx.y * UNI_ROWS + 16 * g;
     const c128 base = cmul(a, cexp_t(l, t0 + (double)ib * dt));
     __syncthreads();
 #pragma unroll
@@ -362,9 +426,9 @@ __global__ __launch_bounds__(256) void ens_p_uniform_kernel(const c128* alpha, c
       if (col && i < n3) {
 #pragma unroll
         for (int p = 0; p < ZMAX; ++p)
-          if (p < nL) v = cadd(v, cmul(sX[j * 256 + mc0 + p], b[p]));
+          if (p < np) v = cadd(v, cmul(sX[j * 256 + mc0 + p], b[p]));
       }
-      if (c < W && kk < Kp) P[(size_t)i * Kp + kk] = v;
+      if (col && kk < Kp) P[(size_t)i * Kp + kk] = v;
     }
   }
 }
@@ -521,11 +585,16 @@ extern "C" int qd_response_cube(const qd_c128* alpha, const qd_c128* B, const qd
 namespace {
 // Shared driver.  Time grids are either device arrays (t3 / t1) or uniform (t0 + j dt, when the
 // array pointer is null): the uniform form builds the GEMM operands from exponential tables.
+// nL / lam: the t3 (X, GEMM K) side; nz / lamz: the t1 side (Mt is [M][nL][nz]).  trans != 0 writes
+// out[k][i] = S[i][k] (the host's swapped form, which puts the smaller pruned index set on K).
 int ens_run(const char* fn, const qd_c128* alpha, const qd_c128* Mt, const qd_c128* beta, const qd_c128* lam, int M,
             int nL, const double* t3, double t3_0, double dt3, int n3, const double* t1, double t1_0, double dt1,
-            int n1, qd_c128* out, int accumulate, void* stream) {
+            int n1, qd_c128* out, int accumulate, void* stream, int nz = 0, const qd_c128* lamz_ = nullptr,
+            int trans = 0) {
+  if (nz == 0) nz = nL;
+  const c128* lamz = (const c128*)(lamz_ ? lamz_ : lam);
   QD_CHECK_ARG(alpha && Mt && beta && lam && out, "%s: null pointer", fn);
-  QD_CHECK_ARG(M >= 1 && nL >= 1 && n3 >= 1 && n1 >= 1, "%s: bad sizes", fn);
+  QD_CHECK_ARG(M >= 1 && nL >= 1 && nz >= 1 && n3 >= 1 && n1 >= 1, "%s: bad sizes", fn);
   QD_CHECK_ARG((long)M * nL < (1L << 30) && M < 65536 * 1024, "%s: M*nL too large", fn);
   hipStream_t st = (hipStream_t)stream;
   const int BT = ENS_BT;
@@ -534,18 +603,17 @@ int ens_run(const char* fn, const qd_c128* alpha, const qd_c128* Mt, const qd_c1
   const int tiles = ceil_div(K, CG_KT);
   const int Kp = tiles * CG_KT;
   const int blocks2d = (n3p / BT) * (n1p / BT);
-  // split K so that the grid covers the 256 CUs once (one 512-thread workgroup per CU), with
-  // >= 4 K-tiles per workgroup; fewer splits = fewer partial slabs to write and reduce
-  int S = std::max(1, std::min(ceil_div(256, blocks2d), std::max(1, tiles / 4)));
-  const size_t nx = (size_t)n3p * Kp, nz = (size_t)Kp * n1p, nsl = (size_t)S * n3p * n1p;
+  const SplitPlan plan = split_plan(n3p, n1p, tiles);
+  const int S = plan.S;
+  const size_t nXe = (size_t)n3p * Kp, nZe = (size_t)Kp * n1p, nsl = (size_t)S * n3p * n1p;
   void* w = nullptr;
-  int rc = workspace(WS_2DES, (nx + nz + nsl) * sizeof(c128), &w);
+  int rc = workspace(WS_2DES, (nXe + nZe + nsl) * sizeof(c128), &w);
   if (rc) return rc;
   c128* X = (c128*)w;
-  c128* Z = X + nx;
-  c128* slabs = Z + nz;
+  c128* Z = X + nXe;
+  c128* slabs = Z + nZe;
   const int zbx = n1p / 256 + (n1p % 256 != 0);
-  const bool zfast = nL <= ZMAX && M <= 65535 - 4096;
+  const bool zfast = nL <= ZMAX && nz <= ZMAX && M <= 65535 - 4096;
   const int xbx = ceil_div(Kp, 256), xblocks = xbx * (n3p / UNI_ROWS);
   if (!t1 && zfast && n1p <= 16 * UNI_MAXC) {
     // Z (uniform t1) and, when t3 is uniform too, X in the same launch (separately if the grid
@@ -553,12 +621,12 @@ int ens_run(const char* fn, const qd_c128* alpha, const qd_c128* Mt, const qd_c1
     const bool xin = !t3 && (long)M + xblocks <= 65535;
     hipLaunchKernelGGL(ens_xz_uniform_kernel, dim3(zbx, M + (xin ? xblocks : 0)), dim3(256), 0, st, (const c128*)Mt,
                        (const c128*)beta, (const c128*)lam, M, nL, t1_0, dt1, n1, n1p, Kp, Z, (const c128*)alpha, K,
-                       t3_0, dt3, n3, n3p, xbx, X);
+                       t3_0, dt3, n3, n3p, xbx, X, nz, lamz);
     QD_HIP(hipGetLastError());
     if (!t3 && !xin) {
       hipLaunchKernelGGL(ens_xz_uniform_kernel, dim3(1, xblocks), dim3(256), 0, st, (const c128*)Mt,
                          (const c128*)beta, (const c128*)lam, 0, nL, 0.0, 0.0, n1, n1p, Kp, Z, (const c128*)alpha, K,
-                         t3_0, dt3, n3, n3p, xbx, X);
+                         t3_0, dt3, n3, n3p, xbx, X, nz, lamz);
       QD_HIP(hipGetLastError());
     }
     if (Kp > K) {
@@ -567,7 +635,7 @@ int ens_run(const char* fn, const qd_c128* alpha, const qd_c128* Mt, const qd_c1
     }
     if (t3) {  // X from the array (X part of the combined kernel only)
       hipLaunchKernelGGL(ens_xz_kernel, dim3(zbx, 4096), dim3(256), 0, st, (const c128*)Mt, (const c128*)beta,
-                         (const c128*)lam, 0, nL, t1, n1, n1p, Kp, Z, (const c128*)alpha, t3, n3, n3p, 4096, K, X);
+                         (const c128*)lam, 0, nL, t1, n1, n1p, Kp, Z, (const c128*)alpha, t3, n3, n3p, 4096, K, X, nz, lamz);
       QD_HIP(hipGetLastError());
     }
   } else {
@@ -575,14 +643,14 @@ int ens_run(const char* fn, const qd_c128* alpha, const qd_c128* Mt, const qd_c1
     if (!t3) {  // uniform t3 with an array t1: X blocks only
       hipLaunchKernelGGL(ens_xz_uniform_kernel, dim3(1, xblocks), dim3(256), 0, st, (const c128*)Mt,
                          (const c128*)beta, (const c128*)lam, 0, nL, 0.0, 0.0, n1, n1p, Kp, Z, (const c128*)alpha, K,
-                         t3_0, dt3, n3, n3p, xbx, X);
+                         t3_0, dt3, n3, n3p, xbx, X, nz, lamz);
       QD_HIP(hipGetLastError());
     }
     if (zfast) {
       // X (when from an array) gets as many block rows as Z has (capped): one launch, both writes
       const int xrows = t3 ? std::max(1, std::min(M, 4096)) : 0;
       hipLaunchKernelGGL(ens_xz_kernel, dim3(zbx, M + xrows), dim3(256), 0, st, (const c128*)Mt, (const c128*)beta,
-                         (const c128*)lam, M, nL, t1, n1, n1p, Kp, Z, (const c128*)alpha, t3, n3, n3p, xrows, K, X);
+                         (const c128*)lam, M, nL, t1, n1, n1p, Kp, Z, (const c128*)alpha, t3, n3, n3p, xrows, K, X, nz, lamz);
       QD_HIP(hipGetLastError());
       if (Kp > K) {
         hipLaunchKernelGGL(ens_z_pad_kernel, dim3(64), dim3(256), 0, st, K, Kp, n1p, Z);
@@ -591,19 +659,22 @@ int ens_run(const char* fn, const qd_c128* alpha, const qd_c128* Mt, const qd_c1
     } else {
       if (t3) {
         hipLaunchKernelGGL(ens_xz_kernel, dim3(zbx, 4096), dim3(256), 0, st, (const c128*)Mt, (const c128*)beta,
-                           (const c128*)lam, 0, nL, t1, n1, n1p, Kp, Z, (const c128*)alpha, t3, n3, n3p, 4096, K, X);
+                           (const c128*)lam, 0, nL, t1, n1, n1p, Kp, Z, (const c128*)alpha, t3, n3, n3p, 4096, K, X, nz, lamz);
         QD_HIP(hipGetLastError());
       }
-      hipLaunchKernelGGL(ens_z_generic_kernel, dim3(grid_for(nz, 256)), dim3(256), 0, st, (const c128*)Mt,
-                         (const c128*)beta, (const c128*)lam, M, nL, t1, n1, n1p, Kp, Z);
+      hipLaunchKernelGGL(ens_z_generic_kernel, dim3(grid_for(nZe, 256)), dim3(256), 0, st, (const c128*)Mt,
+                         (const c128*)beta, lamz, M, nL, t1, n1, n1p, Kp, Z, nz);
       QD_HIP(hipGetLastError());
     }
   }
-  hipLaunchKernelGGL(ens_gemm_kernel, dim3(n1p / BT, n3p / BT, S), dim3(CG_WG), 0, st, X, Kp, Z, n1p, tiles, S,
-                     slabs, n3p);
+  launch_ens_gemm(plan, X, Kp, Z, n3p, n1p, tiles, slabs, st);
   QD_HIP(hipGetLastError());
-  hipLaunchKernelGGL(ens_reduce_kernel, dim3(grid_for((size_t)n3 * n1, 256)), dim3(256), 0, st, slabs, S, n3, n1, n3p,
-                     n1p, (c128*)out, accumulate);
+  if (trans)
+    hipLaunchKernelGGL(ens_reduce_trans_kernel, dim3(ceil_div(n1, 16), ceil_div(n3, 16)), dim3(256), 0, st, slabs, S,
+                       n3, n1, n3p, n1p, (c128*)out, accumulate);
+  else
+    hipLaunchKernelGGL(ens_reduce_kernel, dim3(grid_for((size_t)n3 * n1, 256)), dim3(256), 0, st, slabs, S, n3, n1,
+                       n3p, n1p, (c128*)out, accumulate);
   QD_HIP(hipGetLastError());
   return QD_OK;
 }
@@ -625,6 +696,17 @@ extern "C" int qd_response2d_ensemble_uniform(const qd_c128* alpha, const qd_c12
                ZMAX, n1, 16 * UNI_MAXC);
   return ens_run("qd_response2d_ensemble_uniform", alpha, Mt, beta, lam, M, nL, nullptr, t3_0, dt3, n3, nullptr, t1_0,
                  dt1, n1, out, accumulate, stream);
+}
+
+extern "C" int qd_response2d_ensemble_rect(const qd_c128* alpha, const qd_c128* lamx, int nx, const qd_c128* Mt,
+                                           const qd_c128* beta, const qd_c128* lamz, int nz, int M, const double* t3,
+                                           double t3_0, double dt3, int n3, const double* t1, double t1_0, double dt1,
+                                           int n1, int transpose_out, qd_c128* out, int accumulate, void* stream) {
+  QD_CHECK_ARG(lamz, "qd_response2d_ensemble_rect: null pointer");
+  QD_CHECK_ARG(t1 || (nz <= ZMAX && nx <= ZMAX && n1 <= 16 * UNI_MAXC),
+               "qd_response2d_ensemble_rect: uniform t1 needs nx, nz <= %d and n1 <= %d", ZMAX, 16 * UNI_MAXC);
+  return ens_run("qd_response2d_ensemble_rect", alpha, Mt, beta, lamx, M, nx, t3, t3_0, dt3, n3, t1, t1_0, dt1, n1, out,
+                 accumulate, stream, nz, lamz, transpose_out ? 1 : 0);
 }
 
 namespace {
@@ -652,37 +734,47 @@ extern "C" int qd_response2d_t2_dims(int M, int nL, int n3, int n1, int* n3p, in
   return QD_OK;
 }
 
-extern "C" int qd_response2d_t2_operands(const qd_c128* alpha, const qd_c128* Bm, const qd_c128* Cm,
-                                         const qd_c128* beta, const qd_c128* lam, int M, int nL, double t3_0,
-                                         double dt3, int n3, double t1_0, double dt1, int n1, qd_c128* P_,
-                                         qd_c128* Q_, void* stream) {
-  const char* fn = "qd_response2d_t2_operands";
-  QD_CHECK_ARG(alpha && Bm && Cm && beta && lam && P_ && Q_, "%s: null pointer", fn);
-  QD_CHECK_ARG(M >= 1 && nL >= 1 && n3 >= 1 && n1 >= 1, "%s: bad sizes", fn);
-  QD_CHECK_ARG(nL <= ZMAX && n1 <= 16 * UNI_MAXC, "%s: nL=%d (<= %d), n1=%d (<= %d)", fn, nL, ZMAX, n1, 16 * UNI_MAXC);
-  QD_CHECK_ARG(M <= 65535 && (long)M * nL < (1L << 30), "%s: M=%d too large", fn, M);
+extern "C" int qd_response2d_t2_operands_rect(const qd_c128* alpha, const qd_c128* lamp, int np,
+                                              const qd_c128* Bm, const qd_c128* lamr, int nr, const qd_c128* Cm,
+                                              const qd_c128* beta, const qd_c128* lamq, int nq, int M, double t3_0,
+                                              double dt3, int n3, double t1_0, double dt1, int n1, qd_c128* P_,
+                                              qd_c128* Q_, void* stream) {
+  const char* fn = "qd_response2d_t2_operands_rect";
+  QD_CHECK_ARG(alpha && lamp && Bm && lamr && Cm && beta && lamq && P_ && Q_, "%s: null pointer", fn);
+  QD_CHECK_ARG(M >= 1 && np >= 1 && nr >= 1 && nq >= 1 && n3 >= 1 && n1 >= 1, "%s: bad sizes", fn);
+  QD_CHECK_ARG(np <= ZMAX && nr <= ZMAX && nq <= ZMAX && n1 <= 16 * UNI_MAXC,
+               "%s: np=%d nr=%d nq=%d (<= %d), n1=%d (<= %d)", fn, np, nr, nq, ZMAX, n1, 16 * UNI_MAXC);
+  QD_CHECK_ARG(M <= 65535 && (long)M * nr < (1L << 30), "%s: M=%d too large", fn, M);
   hipStream_t st = (hipStream_t)stream;
-  const T2Dims d = t2_dims(M, nL, n3, n1);
+  const T2Dims d = t2_dims(M, nr, n3, n1);
   c128* P = (c128*)P_;
   c128* Q = (c128*)Q_;
-  const int MB = 256 / nL;
+  const int MB = 256 / std::max(np, nr);
   hipLaunchKernelGGL(ens_p_uniform_kernel, dim3(ceil_div(M, MB), d.n3p / UNI_ROWS), dim3(256), 0, st,
-                     (const c128*)alpha, (const c128*)Bm, (const c128*)lam, M, nL, t3_0, dt3, n3, d.n3p, d.Kp, P);
+                     (const c128*)alpha, (const c128*)Bm, (const c128*)lamp, M, np, nr, t3_0, dt3, n3, d.n3p, d.Kp, P);
   QD_HIP(hipGetLastError());
   if (d.Kp > d.K) {
     hipLaunchKernelGGL(ens_p_pad_kernel, dim3(64), dim3(256), 0, st, d.K, d.Kp, d.n3p, P);
     QD_HIP(hipGetLastError());
   }
-  // Q = C_m Y_m: the uniform Z build with Mt := C (Z rows only)
+  // Q = C_m Y_m: the uniform Z build with Mt := C [M][nr][nq] (Z rows only)
   hipLaunchKernelGGL(ens_xz_uniform_kernel, dim3(ceil_div(d.n1p, 256), M), dim3(256), 0, st, (const c128*)Cm,
-                     (const c128*)beta, (const c128*)lam, M, nL, t1_0, dt1, n1, d.n1p, d.Kp, Q, (const c128*)nullptr,
-                     d.K, 0.0, 0.0, n3, d.n3p, 1, (c128*)nullptr);
+                     (const c128*)beta, (const c128*)lamr, M, nr, t1_0, dt1, n1, d.n1p, d.Kp, Q, (const c128*)nullptr,
+                     d.K, 0.0, 0.0, n3, d.n3p, 1, (c128*)nullptr, nq, (const c128*)lamq);
   QD_HIP(hipGetLastError());
   if (d.Kp > d.K) {
     hipLaunchKernelGGL(ens_z_pad_kernel, dim3(64), dim3(256), 0, st, d.K, d.Kp, d.n1p, Q);
     QD_HIP(hipGetLastError());
   }
   return QD_OK;
+}
+
+extern "C" int qd_response2d_t2_operands(const qd_c128* alpha, const qd_c128* Bm, const qd_c128* Cm,
+                                         const qd_c128* beta, const qd_c128* lam, int M, int nL, double t3_0,
+                                         double dt3, int n3, double t1_0, double dt1, int n1, qd_c128* P_,
+                                         qd_c128* Q_, void* stream) {
+  return qd_response2d_t2_operands_rect(alpha, lam, nL, Bm, lam, nL, Cm, beta, lam, nL, M, t3_0, dt3, n3, t1_0, dt1,
+                                        n1, P_, Q_, stream);
 }
 
 extern "C" int qd_response2d_t2_apply(const qd_c128* P, const qd_c128* Q, const qd_c128* lam, int M, int nL, int n3,
@@ -736,8 +828,7 @@ namespace {
 int splitk_gemm(const c128* A, const c128* B, int Mp, int Kp, int Np, int Mo, int No, c128* C, c128* slabs, int S,
                 hipStream_t st) {
   const int tiles = Kp / CG_KT;
-  hipLaunchKernelGGL(ens_gemm_kernel, dim3(Np / ENS_BT, Mp / ENS_BT, S), dim3(CG_WG), 0, st, A, Kp, B, Np, tiles, S,
-                     slabs, Mp);
+  launch_ens_gemm(SplitPlan{ENS_BT, S}, A, Kp, B, Mp, Np, tiles, slabs, st);
   QD_HIP(hipGetLastError());
   hipLaunchKernelGGL(ens_reduce_kernel, dim3(grid_for((size_t)Mo * No, 256)), dim3(256), 0, st, slabs, S, Mo, No, Mp,
                      Np, C, 0);
