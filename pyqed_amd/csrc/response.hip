@@ -139,11 +139,12 @@ __global__ __launch_bounds__(256) void ens_xz_kernel(const c128* Mt, const c128*
 // e^{lam (t0 + (16 l + j) dt)} = e^{lam (t0 + 16 l dt)} * e^{lam j dt}; the coarse factor is a direct
 // exponential, the fine table a product chain of e^{lam dt} (<= 15 products).  A handful of
 // transcendentals per 16-64 outputs instead of one per output; relative error ~1e-14.
-constexpr int UNI_ROWS = 64;  // X rows per block
+constexpr int UNI_ROWS = 64;  // P rows per block (t2 scan)
+constexpr int XU_ROWS = 16;   // materialised uniform X: rows per block (one 16-row group: more, shorter blocks)
 __device__ __forceinline__ void ens_x_uniform_block(int bx, int by, const c128* alpha, const c128* lam, int K, int Kp,
                                                     double t0, double dt, int n3, int n3p, c128* X) {
   const int kk = bx * 256 + threadIdx.x;
-  const int i0 = by * UNI_ROWS;
+  const int i0 = by * XU_ROWS;
   if (kk >= Kp) return;
   const bool col = kk < K;
   const c128 l = col ? lam[kk] : cmk(0, 0);
@@ -153,7 +154,7 @@ __device__ __forceinline__ void ens_x_uniform_block(int bx, int by, const c128* 
   const c128 st = cexp_t(l, dt);
 #pragma unroll
   for (int j = 1; j < 16; ++j) T1[j] = cmul(T1[j - 1], st);
-  for (int g = 0; g < UNI_ROWS / 16; ++g) {
+  for (int g = 0; g < XU_ROWS / 16; ++g) {
     const int ib = i0 + 16 * g;
     const c128 base = cmul(a, cexp_t(l, t0 + (double)ib * dt));
 #pragma unroll
@@ -168,7 +169,7 @@ __device__ __forceinline__ void ens_x_uniform_block(int bx, int by, const c128* 
 // Z rows of member m = blockIdx.y, uniform t1: tables of e^{lam_q t} in LDS (nL x (16 + n1p/16)).
 constexpr int UNI_MAXC = 1024 / 16;
 // One launch, both operands: blockIdx.y < M -> Z rows of member blockIdx.y (blockIdx.x = column
-// block); blockIdx.y >= M -> X block (blockIdx.y - M) in a (Kp/256) x (n3p/UNI_ROWS) tiling.
+// block); blockIdx.y >= M -> X block (blockIdx.y - M) in a (Kp/256) x (n3p/XU_ROWS) tiling.
 __global__ __launch_bounds__(256) void ens_xz_uniform_kernel(const c128* Mt, const c128* beta, const c128* lam, int M,
                                                              int nL, double t0, double dt, int n1, int n1p, int Kp,
                                                              c128* Z, const c128* alpha, int K, double t3_0,
@@ -206,6 +207,83 @@ __global__ __launch_bounds__(256) void ens_xz_uniform_kernel(const c128* Mt, con
   }
 }
 
+// Z rows of G members per block (uniform t1), tables in dynamic LDS: per member Mt_m (nL x nz), the fine
+// table e^{lamz_q j dt} (nz x 16) and the coarse one beta_q e^{lamz_q (t0 + 16 l dt)} (nz x nC).  Every
+// wave takes part in the table phase (G nz (16 + nC) exponentials per block instead of nz (16 + nC) per
+// 256-thread block), and a block then streams G nL full Z rows.  Blocks blockIdx.y >= ceil(M / G) build
+// X blocks instead (materialised uniform X, when the A operand is not generated in the GEMM).
+__global__ __launch_bounds__(256) void ens_z_uniform_kernel(const c128* Mt, const c128* beta, const c128* lamz, int M,
+                                                            int nL, int nz, int G, double t0, double dt, int n1,
+                                                            int n1p, c128* Z, const c128* alpha, const c128* lamx,
+                                                            int K, int Kp, double t3_0, double dt3, int n3, int n3p,
+                                                            int xbx, c128* X) {
+  extern __shared__ c128 zs[];
+  const int nMB = (M + G - 1) / G;
+  if ((int)blockIdx.y >= nMB) {
+    if (blockIdx.x != 0) return;
+    const int xb = blockIdx.y - nMB;
+    ens_x_uniform_block(xb % xbx, xb / xbx, alpha, lamx, K, Kp, t3_0, dt3, n3, n3p, X);
+    return;
+  }
+  const int nC = n1p / 16;
+  const int per = nL * nz + nz * (16 + nC);
+  const int m0 = blockIdx.y * G;
+  const int g = min(G, M - m0);
+  // round 1: every input of the block's members (Mt, lamz, beta) in one parallel load round into LDS
+  c128* sLam = zs + G * per;
+  c128* sBeta = sLam + G * nz;
+  for (int e = threadIdx.x; e < g * nL * nz; e += 256)
+    zs[(e / (nL * nz)) * per + e % (nL * nz)] = Mt[(size_t)m0 * nL * nz + e];
+  for (int e = threadIdx.x; e < g * nz; e += 256) {
+    sLam[e] = lamz[(size_t)m0 * nz + e];
+    sBeta[e] = beta[(size_t)m0 * nz + e];
+  }
+  __syncthreads();
+  // round 2: the exponential tables from LDS operands (no global latency inside the loop)
+  const int tab = nz * (16 + nC);
+  for (int e = threadIdx.x; e < g * tab; e += 256) {
+    const int gi = e / tab, r = e % tab;
+    c128 v;
+    if (r < nz * 16) {
+      v = cexp_t(sLam[gi * nz + r / 16], (double)(r % 16) * dt);
+    } else {
+      const int u = r - nz * 16;
+      const int q = u / nC;
+      v = cmul(sBeta[gi * nz + q], cexp_t(sLam[gi * nz + q], t0 + 16.0 * (double)(u % nC) * dt));
+    }
+    zs[gi * per + nL * nz + r] = v;
+  }
+  __syncthreads();
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= n1p) return;
+  for (int gi = 0; gi < g; ++gi) {
+    const c128* sM = zs + gi * per;
+    const c128* sF = sM + nL * nz;
+    const c128* sC = sF + nz * 16;
+    c128 y[ZMAX];
+#pragma unroll
+    for (int q = 0; q < ZMAX; ++q)
+      y[q] = (q < nz && k < n1) ? cmul(sC[q * nC + (k >> 4)], sF[q * 16 + (k & 15)]) : cmk(0, 0);
+    for (int p = 0; p < nL; ++p) {
+      c128 v = cmk(0, 0);
+#pragma unroll
+      for (int q = 0; q < ZMAX; ++q)
+        if (q < nz) v = cadd(v, cmul(sM[p * nz + q], y[q]));
+      Z[((size_t)(m0 + gi) * nL + p) * n1p + k] = v;
+    }
+  }
+}
+
+// members per block of ens_z_uniform_kernel: tables of <= 32 KB LDS, at most 32 members
+int z_group(int nL, int nz, int n1p) {
+  const int per = nL * nz + nz * (16 + n1p / 16) + 2 * nz;
+  return std::max(1, std::min(32, 2048 / per));
+}
+// its dynamic LDS bytes
+size_t z_lds(int G, int nL, int nz, int n1p) {
+  return (size_t)G * (nL * nz + nz * (16 + n1p / 16) + 2 * nz) * sizeof(c128);
+}
+
 // rows K..Kp-1 of Z are padding
 __global__ void ens_z_pad_kernel(int K, int Kp, int n1p, c128* Z) {
   const size_t tot = (size_t)(Kp - K) * n1p;
@@ -231,6 +309,28 @@ __global__ void ens_z_generic_kernel(const c128* Mt, const c128* beta, const c12
   }
 }
 
+// Uniform t3 without materialising X: X[i][kk] = coarse[i >> 4][kk] * fine[i & 15][kk] with
+//   coarse[c][kk] = i alpha_kk e^{lam_kk (t0 + 16 c dt)},  fine[j][kk] = (e^{lam_kk dt})^j (product chain),
+// the same factors (and roundings) ens_x_uniform_block multiplies, formed by the GEMM's A staging instead
+// (tables: (n3p/16 + 16) x Kp, 1/8 of X at n3p = 256).  Columns kk >= K are zero; rows past n3 inside the
+// last 16-row group are finite and only reach output rows the reduction never reads.
+__global__ __launch_bounds__(256) void ens_xtab_kernel(const c128* alpha, const c128* lam, int K, int Kp, double t0,
+                                                       double dt, int n3, int n3p, c128* coarse, c128* fine) {
+  const int kk = blockIdx.x * 256 + threadIdx.x;
+  if (kk >= Kp) return;
+  const bool col = kk < K;
+  const c128 l = col ? lam[kk] : cmk(0, 0);
+  const c128 a = col ? cmuli(alpha[kk]) : cmk(0, 0);
+  const c128 st = cexp_t(l, dt);
+  c128 f = cmk(1, 0);
+  for (int j = 0; j < 16; ++j) {
+    fine[(size_t)j * Kp + kk] = f;
+    f = cmul(f, st);
+  }
+  for (int c = 0; c < n3p / 16; ++c)
+    coarse[(size_t)c * Kp + kk] = (col && 16 * c < n3) ? cmul(a, cexp_t(l, t0 + (double)(16 * c) * dt)) : cmk(0, 0);
+}
+
 constexpr int ENS_BT = 128;
 #ifndef ENS_PIPE
 #define ENS_PIPE false  // fragment double-buffering (PIPE) fits (250 VGPRs, no scratch) but measured neutral here
@@ -245,6 +345,24 @@ struct EnsXA {
     return cg_ld(X + (size_t)(row0 + (e >> 4)) * Kp + k0 + t * CG_KT + (e & 15));
   }
   __device__ __forceinline__ cg_v2 finish(const Raw& r, int, int, int) const { return r; }
+};
+
+struct EnsXTab {
+  struct Raw {
+    cg_v2 c, f;
+  };
+  const c128* coarse;
+  const c128* fine;
+  int Kp, row0, k0;
+  __device__ __forceinline__ Raw fetch(int t, int e, int) const {
+    const int row = row0 + (e >> 4);
+    const size_t kk = (size_t)k0 + t * CG_KT + (e & 15);
+    return Raw{cg_ld(coarse + (size_t)(row >> 4) * Kp + kk), cg_ld(fine + (size_t)(row & 15) * Kp + kk)};
+  }
+  __device__ __forceinline__ cg_v2 finish(const Raw& r, int, int, int) const {
+    const c128 v = cmul(cmk(r.c.x, r.c.y), cmk(r.f.x, r.f.y));
+    return cg_v2{v.re, v.im};
+  }
 };
 
 template <int BT = ENS_BT>
@@ -275,9 +393,9 @@ __device__ __forceinline__ void ens_tile(int& bn, int& bm, int& s) {
 // grid: (n1p/BT) x (n3p/BT) x S ; each workgroup accumulates K-tiles [t0, t1) of its block.  BT = 64 for
 // problems whose 128-blocks cannot fill the chip with >= 4 K-tiles per workgroup (4x the blocks, 1/4 the
 // split-K slabs to write and reduce).
-template <int BT>
+template <int BT, bool XTAB>
 __global__ __launch_bounds__(CG_WG) void ens_gemm_kernel(const c128* X, int Kp, const c128* Z, int n1p, int tiles,
-                                                         int S, c128* slabs, int n3p) {
+                                                         int S, c128* slabs, int n3p, const c128* fine) {
   __shared__ CgLds<BT> L;
   int bn, bm, s;
   ens_tile(bn, bm, s);
@@ -285,9 +403,14 @@ __global__ __launch_bounds__(CG_WG) void ens_gemm_kernel(const c128* X, int Kp, 
   CgAcc<BT> A;
   c128* slab = slabs + (size_t)s * n3p * n1p;
   if (t1 > t0) {
-    EnsXA pa{X, Kp, bm * BT, t0 * CG_KT};
     EnsZB<BT> pb{Z, n1p, bn * BT, t0 * CG_KT};
-    cg_block_gemm_gen<BT, ENS_PIPE>(t1 - t0, pa, pb, L, A);
+    if constexpr (XTAB) {
+      EnsXTab pa{X, fine, Kp, bm * BT, t0 * CG_KT};  // X = the coarse table
+      cg_block_gemm_gen<BT, ENS_PIPE>(t1 - t0, pa, pb, L, A);
+    } else {
+      EnsXA pa{X, Kp, bm * BT, t0 * CG_KT};
+      cg_block_gemm_gen<BT, ENS_PIPE>(t1 - t0, pa, pb, L, A);
+    }
     cg_epilogue<BT>(A, [&](int row, int col, c128 v) {
       slab[(size_t)(bm * BT + row) * n1p + bn * BT + col] = v;
     });
@@ -299,7 +422,9 @@ __global__ __launch_bounds__(CG_WG) void ens_gemm_kernel(const c128* X, int Kp, 
 
 // (BT, S) for a split-K GEMM of Mp x Np (multiples of 128) over `tiles` K-tiles: 128-blocks with enough
 // splits to cover the 256 CUs once at >= 4 K-tiles per workgroup; 64-blocks when that leaves the chip
-// under-filled or needs more than 16 slabs.  QD_ENS_BT=64/128 forces the block size (A/B runs).
+// under-filled or gives a workgroup fewer than 32 K-tiles (the S partial slabs to write and reduce then
+// cost more than the 64-block's lower operand reuse; measured on the 256 x 256 2DES grid: 64-blocks
+// win at K <= 8k, 128-blocks from K = 32k).  QD_ENS_BT=64/128 forces the block size (A/B runs).
 struct SplitPlan {
   int bt, S;
 };
@@ -313,19 +438,26 @@ SplitPlan split_plan(int Mp, int Np, int tiles) {
     return std::max(1, std::min(ceil_div(256, blocks), std::max(1, tiles / 4)));
   };
   const int S128 = splits(128);
-  const bool small = (Mp / 128) * (Np / 128) * S128 < 256 || S128 > 16;
+  const bool small = (Mp / 128) * (Np / 128) * S128 < 256 || tiles / S128 < 32;
   const int bt = force == 64 || force == 128 ? force : (small ? 64 : 128);
   return {bt, splits(bt)};
 }
 
+// fine != nullptr: X is the coarse table of ens_xtab_kernel (generated A operand)
 void launch_ens_gemm(const SplitPlan& pl, const c128* X, int Kp, const c128* Z, int Mp, int Np, int tiles,
-                     c128* slabs, hipStream_t st) {
-  if (pl.bt == 64)
-    hipLaunchKernelGGL(ens_gemm_kernel<64>, dim3(Np / 64, Mp / 64, pl.S), dim3(CG_WG), 0, st, X, Kp, Z, Np, tiles,
-                       pl.S, slabs, Mp);
-  else
-    hipLaunchKernelGGL(ens_gemm_kernel<128>, dim3(Np / 128, Mp / 128, pl.S), dim3(CG_WG), 0, st, X, Kp, Z, Np, tiles,
-                       pl.S, slabs, Mp);
+                     c128* slabs, hipStream_t st, const c128* fine = nullptr) {
+  const dim3 g(Np / pl.bt, Mp / pl.bt, pl.S);
+  if (pl.bt == 64) {
+    if (fine)
+      hipLaunchKernelGGL((ens_gemm_kernel<64, true>), g, dim3(CG_WG), 0, st, X, Kp, Z, Np, tiles, pl.S, slabs, Mp, fine);
+    else
+      hipLaunchKernelGGL((ens_gemm_kernel<64, false>), g, dim3(CG_WG), 0, st, X, Kp, Z, Np, tiles, pl.S, slabs, Mp, fine);
+  } else {
+    if (fine)
+      hipLaunchKernelGGL((ens_gemm_kernel<128, true>), g, dim3(CG_WG), 0, st, X, Kp, Z, Np, tiles, pl.S, slabs, Mp, fine);
+    else
+      hipLaunchKernelGGL((ens_gemm_kernel<128, false>), g, dim3(CG_WG), 0, st, X, Kp, Z, Np, tiles, pl.S, slabs, Mp, fine);
+  }
 }
 
 // out[i][k] (+)= sum_s slab[s][i][k], fixed order -> deterministic
@@ -614,21 +746,31 @@ int ens_run(const char* fn, const qd_c128* alpha, const qd_c128* Mt, const qd_c1
   c128* slabs = Z + nZe;
   const int zbx = n1p / 256 + (n1p % 256 != 0);
   const bool zfast = nL <= ZMAX && nz <= ZMAX && M <= 65535 - 4096;
-  const int xbx = ceil_div(Kp, 256), xblocks = xbx * (n3p / UNI_ROWS);
-  if (!t1 && zfast && n1p <= 16 * UNI_MAXC) {
-    // Z (uniform t1) and, when t3 is uniform too, X in the same launch (separately if the grid
-    // would exceed 65535 block rows)
-    const bool xin = !t3 && (long)M + xblocks <= 65535;
-    hipLaunchKernelGGL(ens_xz_uniform_kernel, dim3(zbx, M + (xin ? xblocks : 0)), dim3(256), 0, st, (const c128*)Mt,
-                       (const c128*)beta, (const c128*)lam, M, nL, t1_0, dt1, n1, n1p, Kp, Z, (const c128*)alpha, K,
-                       t3_0, dt3, n3, n3p, xbx, X, nz, lamz);
+  const int xbx = ceil_div(Kp, 256), xblocks = xbx * (n3p / XU_ROWS);
+  // uniform t3: the A operand is generated in the GEMM staging from (n3p/16 + 16) x Kp tables held in
+  // the X buffer (QD_ENS_XTAB=0: materialise X as before, for A/B runs)
+  static const bool xtab_on = [] {
+    const char* e = std::getenv("QD_ENS_XTAB");
+    return !(e && e[0] == '0');
+  }();
+  const bool xtab = !t3 && xtab_on && plan.bt == 128;  // 64-blocks are already load-bound in the staging
+  c128* coarse = X;
+  c128* fine = X + (size_t)(n3p / 16) * Kp;
+  if (xtab) {
+    hipLaunchKernelGGL(ens_xtab_kernel, dim3(xbx), dim3(256), 0, st, (const c128*)alpha, (const c128*)lam, K, Kp,
+                       t3_0, dt3, n3, n3p, coarse, fine);
     QD_HIP(hipGetLastError());
-    if (!t3 && !xin) {
-      hipLaunchKernelGGL(ens_xz_uniform_kernel, dim3(1, xblocks), dim3(256), 0, st, (const c128*)Mt,
-                         (const c128*)beta, (const c128*)lam, 0, nL, 0.0, 0.0, n1, n1p, Kp, Z, (const c128*)alpha, K,
-                         t3_0, dt3, n3, n3p, xbx, X, nz, lamz);
-      QD_HIP(hipGetLastError());
-    }
+  }
+  const int G = z_group(nL, nz, n1p);
+  const int nMB = ceil_div(M, G);
+  if (!t1 && nL <= ZMAX && nz <= ZMAX && n1p <= 16 * UNI_MAXC && (long)nMB + xblocks <= 65535) {
+    // Z (uniform t1), G members per block; a materialised uniform X (when not generated in the GEMM) in
+    // the same launch
+    const bool xin = !t3 && !xtab;
+    hipLaunchKernelGGL(ens_z_uniform_kernel, dim3(zbx, nMB + (xin ? xblocks : 0)), dim3(256),
+                       z_lds(G, nL, nz, n1p), st, (const c128*)Mt, (const c128*)beta, lamz, M, nL, nz, G, t1_0,
+                       dt1, n1, n1p, Z, (const c128*)alpha, (const c128*)lam, K, Kp, t3_0, dt3, n3, n3p, xbx, X);
+    QD_HIP(hipGetLastError());
     if (Kp > K) {
       hipLaunchKernelGGL(ens_z_pad_kernel, dim3(64), dim3(256), 0, st, K, Kp, n1p, Z);
       QD_HIP(hipGetLastError());
@@ -640,7 +782,7 @@ int ens_run(const char* fn, const qd_c128* alpha, const qd_c128* Mt, const qd_c1
     }
   } else {
     QD_CHECK_ARG(t1, "%s: uniform t1 needs nL <= %d and n1 <= %d", fn, ZMAX, 16 * UNI_MAXC);
-    if (!t3) {  // uniform t3 with an array t1: X blocks only
+    if (!t3 && !xtab) {  // uniform t3 with an array t1: X blocks only
       hipLaunchKernelGGL(ens_xz_uniform_kernel, dim3(1, xblocks), dim3(256), 0, st, (const c128*)Mt,
                          (const c128*)beta, (const c128*)lam, 0, nL, 0.0, 0.0, n1, n1p, Kp, Z, (const c128*)alpha, K,
                          t3_0, dt3, n3, n3p, xbx, X, nz, lamz);
@@ -667,7 +809,7 @@ int ens_run(const char* fn, const qd_c128* alpha, const qd_c128* Mt, const qd_c1
       QD_HIP(hipGetLastError());
     }
   }
-  launch_ens_gemm(plan, X, Kp, Z, n3p, n1p, tiles, slabs, st);
+  launch_ens_gemm(plan, X, Kp, Z, n3p, n1p, tiles, slabs, st, xtab ? fine : nullptr);
   QD_HIP(hipGetLastError());
   if (trans)
     hipLaunchKernelGGL(ens_reduce_trans_kernel, dim3(ceil_div(n1, 16), ceil_div(n3, 16)), dim3(256), 0, st, slabs, S,
@@ -758,9 +900,11 @@ extern "C" int qd_response2d_t2_operands_rect(const qd_c128* alpha, const qd_c12
     QD_HIP(hipGetLastError());
   }
   // Q = C_m Y_m: the uniform Z build with Mt := C [M][nr][nq] (Z rows only)
-  hipLaunchKernelGGL(ens_xz_uniform_kernel, dim3(ceil_div(d.n1p, 256), M), dim3(256), 0, st, (const c128*)Cm,
-                     (const c128*)beta, (const c128*)lamr, M, nr, t1_0, dt1, n1, d.n1p, d.Kp, Q, (const c128*)nullptr,
-                     d.K, 0.0, 0.0, n3, d.n3p, 1, (c128*)nullptr, nq, (const c128*)lamq);
+  const int G = z_group(nr, nq, d.n1p);
+  hipLaunchKernelGGL(ens_z_uniform_kernel, dim3(ceil_div(d.n1p, 256), ceil_div(M, G)), dim3(256),
+                     z_lds(G, nr, nq, d.n1p), st, (const c128*)Cm,
+                     (const c128*)beta, (const c128*)lamq, M, nr, nq, G, t1_0, dt1, n1, d.n1p, Q, (const c128*)nullptr,
+                     (const c128*)nullptr, d.K, d.Kp, 0.0, 0.0, n3, d.n3p, 1, (c128*)nullptr);
   QD_HIP(hipGetLastError());
   if (d.Kp > d.K) {
     hipLaunchKernelGGL(ens_z_pad_kernel, dim3(64), dim3(256), 0, st, d.K, d.Kp, d.n1p, Q);

@@ -231,15 +231,17 @@ def redfield_superop_batch(E, a_op, spec_vals):
     """Vectorised redfield_tensor (oqs.py:519-570) for M diagonal Hamiltonians E [M, N] sharing one
     Hermitian a_op already in the (shared, identity) eigenbasis; spec_vals [M, N, N] = S(-W).
     Returns R [M, N^2, N^2].  Used to build disorder ensembles (setup)."""
+    E = np.asarray(E, float)
     M, N = E.shape
     I = np.identity(N)
     A = np.asarray(a_op, complex)
-    R = np.empty((M, N * N, N * N), dtype=complex)
     opA = np.kron(A, I) - np.kron(I, A.T)
-    for m in range(M):
-        Lm = spec_vals[m] * A
-        R[m] = -1j * (np.kron(np.diag(E[m]), I) - np.kron(I, np.diag(E[m]))) \
-            - opA @ (np.kron(Lm, I) - np.kron(I, Lm.conj()))
+    Lm = np.asarray(spec_vals) * A[None]
+    # kron(Lm, I) - kron(I, Lm^*) for every member, as [M, N, N, N, N] -> [M, N^2, N^2]
+    D = (np.einsum("mac,bd->mabcd", Lm, I) - np.einsum("ac,mbd->mabcd", I, Lm.conj())).reshape(M, N * N, N * N)
+    diag = (E[:, :, None] - E[:, None, :]).reshape(M, N * N)      # kron(diag E, I) - kron(I, diag E)
+    R = -(opA[None] @ D)
+    R[:, np.arange(N * N), np.arange(N * N)] += -1j * diag
     return R
 
 

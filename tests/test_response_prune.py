@@ -135,3 +135,27 @@ def test_t2scan_pruned_matches_unpruned(M, n3, n1):
     pr = a.apply(t2).cpu().numpy()
     full = T2Scan(lam, alpha, B, C, beta, t3, t1, prune=False).apply(t2).cpu().numpy()
     assert relerr(pr, full) < 1e-12
+
+
+@pytest.mark.gpu
+def test_large_k_generated_x_operand():
+    """K = 36k (no zero columns): the split plan takes 128-blocks, and the uniform t3 side is generated in
+    the GEMM staging from the coarse/fine exponential tables (ens_xtab_kernel) instead of a materialised X.
+    Checked against the closed form and against the array-grid path (materialised X, direct exponentials)."""
+    from pyqed_amd.response import response2d_ensemble
+    dev = torch.device("cuda", 0)
+    M = 4000
+    lam, alpha, Mt, beta = _inputs(M, 9, (), (), seed=5)
+    lam = lam * 0.3
+    t3, t1 = 0.5 * np.arange(200), 0.4 * np.arange(150)
+    S = response2d_ensemble(lam, alpha, Mt, beta, t3, t1).cpu().numpy()
+    ref = np.zeros((len(t3), len(t1)), complex)
+    for lo in range(0, M, 500):
+        sl = slice(lo, lo + 500)
+        X = alpha[sl][:, None, :] * np.exp(t3[None, :, None] * lam[sl][:, None, :])          # [m, i, p]
+        Z = np.einsum("mpq,mqk->mpk", Mt[sl], beta[sl][:, :, None] * np.exp(lam[sl][:, :, None] * t1[None, None, :]))
+        ref += np.einsum("mip,mpk->ik", X, Z)
+    ref *= (-1j) ** 3
+    assert relerr(S, ref) < 1e-12
+    arr = response2d_ensemble(lam, alpha, Mt, beta, torch.from_numpy(t3).to(dev), torch.from_numpy(t1).to(dev))
+    assert relerr(arr.cpu().numpy(), S) < 1e-13
