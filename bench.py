@@ -233,6 +233,17 @@ def bench_2des(dev, world, rank, M_total, reps, n=256):
                    "signature": "lccc", "scaling": "strong", "collective": "RCCL reduce(sum) to rank 0"
                    if world > 1 else "none"},
         "ms_per_grid": round(wall / reps * 1e3, 4),
+        "roofline": {"bound": "mfma", "kernel": "ens_gemm_kernel<128,xtab>" if Kp >= 32768 else "ens_gemm_kernel<64>",
+                     "achieved": round(gemm_flop / (e0.elapsed_time(e1) / reps / 1e3) / 1e12, 3),
+                     "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(gemm_flop / (e0.elapsed_time(e1) / reps / 1e3) / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
+                     "flop_per_grid": gemm_flop,
+                     "traffic": measured_traffic("ens_gemm_kernel_xtab", 1) if (M_total, n, world) == (32768, 256, 1)
+                     else None,
+                     "traffic_unit": "HBM bytes per ens_gemm_kernel launch (PMC FETCH_SIZE+WRITE_SIZE, calibrated; "
+                                     "profiles/pmc_traffic.json)",
+                     "note": "8 n3 n1 K flop per grid (K = members x pruned index set) / event time of the whole grid "
+                             "(operand tables, Z build, GEMM, slab reduction): a lower bound on the GEMM's own rate"},
         "gemm_flop_per_grid_per_rank": gemm_flop,
         "gemm_k_per_member": nk,
         "event_ms_per_grid": round(e0.elapsed_time(e1) / reps, 4),
