@@ -54,6 +54,10 @@ struct LindbladParams {
   unsigned long long* tbuf;  // [B][8] per-phase wall-clock ticks (QD_PHASE_TIMING diagnostics) or null
   unsigned long long stagger;  // start offset (wall-clock ticks) of the odd workgroup group of each XCD
   int stage, rin, rout;        // split path: RK4 stage; stage input / output buffer (0 = rho, 1/2 = scratch 0/1)
+  int ks, ys;                  // split path: K-splits of the k / Y phases (1 = none)
+  c128* kslab;                 // [B][nb^2][ks][BT^2] partial k blocks
+  c128* yslab;                 // [B][nc][nb^2][ys][BT^2] partial Y blocks
+  unsigned* ticket;            // [B][1 + nc][nb^2] arrival counters (zero between launches)
 };
 
 // Per-matrix scratch slots of Np x Np: stage buffer(s), RK4 accumulator, Y_c.
@@ -488,11 +492,67 @@ __device__ __forceinline__ c128* split_buf(const LindbladParams& p, int b, int w
   return p.ws + (size_t)b * (3 + p.nc) * NN + (size_t)(which - 1) * NN;
 }
 
+// Split-K (small batches): the k-phase (2 + nc segments) and Y-phase K-tiles of one output block are dealt
+// to `S` workgroups; each writes its partial block to a slab and takes an arrival ticket, and the last to
+// arrive sums the S slabs in the fixed order s = 0 .. S-1 (deterministic) and runs the block's epilogue.
+// No workgroup waits on another (no co-residency needed); the last arriver resets the ticket for the next
+// launch.  Visibility without L2 write-back fences (MI355X_MICROARCH.md "Valid forms",
+// cdna_hip_programming.md §6 G16): every slab store is an agent-scope relaxed atomic store (write-through
+// `sc1`), drained (vmcnt(0)) before the workgroup barrier and the ticket, and every slab load of the last
+// arriver an agent-scope relaxed atomic load (`sc1`).  (Plain stores + __threadfence() per thread measured
+// 1.5-2x slower than no split at all: each release fence writes back the L2.)
+__device__ __forceinline__ void slab_st(c128* p, c128 v) {
+  __hip_atomic_store(&p->re, v.re, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&p->im, v.im, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ c128 slab_ld(const c128* p) {
+  return cmk(__hip_atomic_load(&p->re, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+             __hip_atomic_load(&p->im, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+template <typename Pol>
+struct CgOffset {  // a K-tile policy shifted by t0 tiles
+  using Raw = typename Pol::Raw;
+  Pol pol;
+  int t0;
+  __device__ __forceinline__ Raw fetch(int t, int e, int q) const { return pol.fetch(t + t0, e, q); }
+  __device__ __forceinline__ cg_v2 finish(const Raw& r, int t, int e, int q) const {
+    return pol.finish(r, t + t0, e, q);
+  }
+};
+
+// tiles [T s / S, T (s+1) / S) of the segment list `segs` (each segment tps tiles deep) into A
+template <int BT>
+__device__ __forceinline__ void split_gemm_range(const CgSeg* segs, int tps, int ld, int T, int s, int S, CgLds<BT>& L,
+                                                 CgAcc<BT>& A) {
+  const int t0 = (int)((long)T * s / S), t1 = (int)((long)T * (s + 1) / S);
+  CgOffset<CgSegA<BT>> pa{CgSegA<BT>{segs, tps, ld}, t0};
+  CgOffset<CgSegB<BT>> pb{CgSegB<BT>{segs, tps, ld}, t0};
+  cg_block_gemm_gen<BT>(t1 - t0, pa, pb, L, A);
+}
+
+// Publish this workgroup's partial block and return true in the last arriver (all threads agree).
+template <int BT>
+__device__ __forceinline__ bool split_arrive(const CgAcc<BT>& A, c128* slab_s, unsigned* ticket, int S) {
+  __shared__ int last;
+  cg_epilogue<BT>(A, [&](int row, int col, c128 v) { slab_st(slab_s + row * BT + col, v); });
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores are complete
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (old == (unsigned)(S - 1));
+    if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return last;
+}
+
 template <int BT>
 __global__ __launch_bounds__(CG_WG) void glf_split_y_kernel(LindbladParams p) {
   __shared__ CgLds<BT> L;
   __shared__ CgSeg segs[1];
-  const int nb = p.Np / BT, bm = blockIdx.x / nb, bn = blockIdx.x % nb, c = blockIdx.y, b = blockIdx.z;
+  const int nb = p.Np / BT, bm = blockIdx.x / nb, bn = blockIdx.x % nb, c = blockIdx.y;
+  const int S = p.ys, b = blockIdx.z / S, s = blockIdx.z % S;
   const int Np = p.Np;
   const size_t NN = (size_t)Np * Np;
   const c128* r = split_buf(p, b, p.rin);
@@ -503,15 +563,49 @@ __global__ __launch_bounds__(CG_WG) void glf_split_y_kernel(LindbladParams p) {
   }
   __syncthreads();
   CgAcc<BT> A;
-  cg_block_gemm<BT>(segs, 1, Np, Np, Np, L, A);
-  cg_epilogue<BT>(A, [&](int row, int col, c128 v) { Yc[(size_t)(bm * BT + row) * Np + bn * BT + col] = v; });
+  auto store = [&](int row, int col, c128 v) { Yc[(size_t)(bm * BT + row) * Np + bn * BT + col] = v; };
+  if (S == 1) {
+    cg_block_gemm<BT>(segs, 1, Np, Np, Np, L, A);
+    cg_epilogue<BT>(A, store);
+    return;
+  }
+  split_gemm_range<BT>(segs, Np / CG_KT, Np, Np / CG_KT, s, S, L, A);
+  const size_t blk = ((size_t)b * p.nc + c) * nb * nb + blockIdx.x;
+  c128* slab = p.yslab + blk * S * BT * BT;
+  if (!split_arrive<BT>(A, slab + (size_t)s * BT * BT, p.ticket + (size_t)(gridDim.z / S) * nb * nb + blk, S)) return;
+  for (int e = threadIdx.x; e < BT * BT; e += CG_WG) {
+    c128 v = slab_ld(slab + e);
+    for (int q = 1; q < S; ++q) v = cadd(v, slab_ld(slab + (size_t)q * BT * BT + e));
+    store(e / BT, e % BT, v);
+  }
+}
+
+// RK4 epilogue of one element of the block (same order as the persistent kernel's rk4_update)
+__device__ __forceinline__ void split_rk4(const LindbladParams& p, c128* rho, c128* acc, c128* rn, size_t idx, c128 k) {
+  const int stage = p.stage;
+  const double dt = p.dt, dt2 = p.dt / 2.0;
+  const c128 r0 = rho[idx];
+  if (stage == 0) {
+    acc[idx] = k;
+    rn[idx] = cadd(r0, cscale(k, dt2));
+  } else if (stage == 1) {
+    acc[idx] = cadd(acc[idx], cscale(k, 2.0));
+    rn[idx] = cadd(r0, cscale(k, dt2));
+  } else if (stage == 2) {
+    acc[idx] = cadd(acc[idx], cscale(k, 2.0));
+    rn[idx] = cadd(r0, cscale(k, dt));
+  } else {
+    const c128 a = cadd(acc[idx], k);
+    rho[idx] = cadd(r0, cscale(cscale(a, 1.0 / 6.0), dt));
+  }
 }
 
 template <int BT>
 __global__ __launch_bounds__(CG_WG) void glf_split_k_kernel(LindbladParams p) {
   __shared__ CgLds<BT> L;
   __shared__ CgSeg segs[2 + MAX_NC];
-  const int nb = p.Np / BT, bm = blockIdx.x / nb, bn = blockIdx.x % nb, b = blockIdx.y;
+  const int nb = p.Np / BT, bm = blockIdx.x / nb, bn = blockIdx.x % nb;
+  const int S = p.ks, b = blockIdx.y / S, s = blockIdx.y % S;
   const int Np = p.Np, nc = p.nc;
   const size_t NN = (size_t)Np * Np;
   const c128* r = split_buf(p, b, p.rin);
@@ -532,26 +626,22 @@ __global__ __launch_bounds__(CG_WG) void glf_split_k_kernel(LindbladParams p) {
   }
   __syncthreads();
   CgAcc<BT> A;
-  cg_block_gemm<BT>(segs, 2 + nc, Np, Np, Np, L, A);
-  const int stage = p.stage;
-  const double dt = p.dt, dt2 = p.dt / 2.0;
-  cg_epilogue<BT>(A, [&](int row, int col, c128 k) {
-    const size_t idx = (size_t)(bm * BT + row) * Np + bn * BT + col;
-    const c128 r0 = rho[idx];
-    if (stage == 0) {
-      acc[idx] = k;
-      rn[idx] = cadd(r0, cscale(k, dt2));
-    } else if (stage == 1) {
-      acc[idx] = cadd(acc[idx], cscale(k, 2.0));
-      rn[idx] = cadd(r0, cscale(k, dt2));
-    } else if (stage == 2) {
-      acc[idx] = cadd(acc[idx], cscale(k, 2.0));
-      rn[idx] = cadd(r0, cscale(k, dt));
-    } else {
-      const c128 a = cadd(acc[idx], k);
-      rho[idx] = cadd(r0, cscale(cscale(a, 1.0 / 6.0), dt));
-    }
-  });
+  if (S == 1) {
+    cg_block_gemm<BT>(segs, 2 + nc, Np, Np, Np, L, A);
+    cg_epilogue<BT>(A, [&](int row, int col, c128 k) {
+      split_rk4(p, rho, acc, rn, (size_t)(bm * BT + row) * Np + bn * BT + col, k);
+    });
+    return;
+  }
+  split_gemm_range<BT>(segs, Np / CG_KT, Np, (2 + nc) * (Np / CG_KT), s, S, L, A);
+  const size_t blk = (size_t)b * nb * nb + blockIdx.x;
+  c128* slab = p.kslab + blk * S * BT * BT;
+  if (!split_arrive<BT>(A, slab + (size_t)s * BT * BT, p.ticket + blk, S)) return;
+  for (int e = threadIdx.x; e < BT * BT; e += CG_WG) {
+    c128 k = slab_ld(slab + e);
+    for (int q = 1; q < S; ++q) k = cadd(k, slab_ld(slab + (size_t)q * BT * BT + e));
+    split_rk4(p, rho, acc, rn, (size_t)(bm * BT + e / BT) * Np + bn * BT + e % BT, k);
+  }
 }
 
 // Observables / snapshot of global step gs (after it; gs = 0: the initial state), one workgroup per matrix.
@@ -658,8 +748,25 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
     if (const char* e = std::getenv("QD_GLF_SPLIT")) use = std::atoi(e) != 0 && !herm && Np >= 64;
     if (use) split_bt = bt;
   }
-  const size_t per = (size_t)(split_bt ? 3 + nc : glf_slots(Np, nc, herm)) * NN;
-  const size_t st_elems = (size_t)B * per + (pad ? (size_t)B * NN : 0);
+  // Split-K of the split path when its blocks leave the chip under-filled: up to 256 workgroups per phase,
+  // >= 3 K-tiles each, at most 4 (k phase) / 8 (Y phase) partial slabs per block.  Measured (N = 128 / 256,
+  // one trajectory, tools/ks_sweep.sh): 4 k-splits 12.0k / 6.9k steps/s, 8: 11.8k / 6.6k, 16: 9.8k / 5.8k,
+  // none: 8.4k / 4.2k.  QD_GLF_SPLITK=0 turns it off; QD_GLF_KS / QD_GLF_YS force the counts (A/B).
+  int ks = 1, ys = 1;
+  if (split_bt) {
+    const long blocks = (long)B * (Np / split_bt) * (Np / split_bt);
+    const int Tk = (2 + nc) * (Np / CG_KT), Ty = Np / CG_KT;
+    ks = (int)std::max(1L, std::min<long>({4L, 256L / blocks, (long)Tk / 3}));
+    ys = nc ? (int)std::max(1L, std::min<long>({8L, 256L / (blocks * nc), (long)Ty / 3})) : 1;
+    if (const char* e = std::getenv("QD_GLF_SPLITK"))
+      if (std::atoi(e) == 0) ks = ys = 1;
+    if (const char* e = std::getenv("QD_GLF_KS")) ks = std::max(1, std::min(Tk, std::atoi(e)));  // A/B overrides
+    if (const char* e = std::getenv("QD_GLF_YS")) ys = nc ? std::max(1, std::min(Ty, std::atoi(e))) : 1;
+  }
+  const size_t per = (size_t)(split_bt ? 3 + nc + (ks > 1 ? ks : 0) + (ys > 1 ? nc * ys : 0)
+                                       : glf_slots(Np, nc, herm)) * NN;
+  const size_t nticket = split_bt ? (size_t)B * (1 + nc) * (Np / split_bt) * (Np / split_bt) : 0;
+  const size_t st_elems = (size_t)B * per + (pad ? (size_t)B * NN : 0) + (nticket + 3) / 4;
   void* wst = nullptr;
   rc = workspace(WS_LINDBLAD, st_elems * sizeof(c128), &wst);
   if (rc) return rc;
@@ -716,6 +823,13 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   p.tbuf = nullptr;
   p.stagger = 0;
   p.stage = p.rin = p.rout = 0;
+  p.ks = ks;
+  p.ys = ys;
+  // split-K slabs after the per-matrix scratch of all B matrices; tickets after the padded copy
+  p.kslab = split_bt ? scratch + (size_t)B * (3 + nc) * NN : nullptr;
+  p.yslab = split_bt ? p.kslab + (size_t)B * (ks > 1 ? ks : 0) * NN : nullptr;
+  p.ticket = split_bt ? (unsigned*)(scratch + (size_t)B * per + (pad ? (size_t)B * NN : 0)) : nullptr;
+  if (split_bt && (ks > 1 || ys > 1)) QD_HIP(hipMemsetAsync(p.ticket, 0, nticket * sizeof(unsigned), st));
   if (const char* e = std::getenv("QD_STAGGER_US")) p.stagger = (unsigned long long)(std::atof(e) * 100.0);  // 100 MHz
 #ifdef QD_PHASE_TIMING
   const bool timing = true;  // diagnostics build: per-phase clocks to stderr
@@ -748,10 +862,10 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
     default: hipLaunchKernelGGL(KERN<128>, GRID, dim3(CG_WG), 0, st, p); break;                  \
   }
         if (nc > 0) {
-          QD_SPLIT(glf_split_y_kernel, dim3(nb * nb, nc, B));
+          QD_SPLIT(glf_split_y_kernel, dim3(nb * nb, nc, B * ys));
           QD_HIP(hipGetLastError());
         }
-        QD_SPLIT(glf_split_k_kernel, dim3(nb * nb, B));
+        QD_SPLIT(glf_split_k_kernel, dim3(nb * nb, B * ks));
         QD_HIP(hipGetLastError());
 #undef QD_SPLIT
       }

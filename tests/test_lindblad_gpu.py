@@ -239,8 +239,9 @@ def test_correlation_3p_1t_matches_reference(tmp_path, monkeypatch):
 @pytest.mark.parametrize("N,nc,B", [(128, 1, 1), (96, 2, 3), (64, 1, 2), (256, 1, 1)])
 def test_lindblad_split_path_matches_persistent_and_oracle(N, nc, B, monkeypatch):
     """Small batches: every output block of a stage phase is its own workgroup (glf_split_*, forced with
-    QD_GLF_SPLIT=1) -- observables, snapshots and the final state against the persistent kernel and the
-    oracle."""
+    QD_GLF_SPLIT=1), with the phases' K-tiles split over workgroups and summed by the last arriver (default)
+    or not (QD_GLF_SPLITK=0) -- observables, snapshots and the final state against the persistent kernel and
+    the oracle."""
     import torch
     from oracle import lindblad as olb
     from pyqed_amd import lindblad_rk4
@@ -251,15 +252,16 @@ def test_lindblad_split_path_matches_persistent_and_oracle(N, nc, B, monkeypatch
     dev = torch.device("cuda", 0)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     out = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("QD_GLF_SPLIT", mode)
+    for mode in ("1", "1nk", "0"):
+        monkeypatch.setenv("QD_GLF_SPLIT", mode[0])
+        monkeypatch.setenv("QD_GLF_SPLITK", "0" if mode == "1nk" else "1")
         rho = t(rho0.copy())
         obs, snap = lindblad_rk4(t(H), t(np.array(cs)), rho, dt, steps, t(E), save_every=2, hermitian=False)
         torch.cuda.synchronize()
         out[mode] = (rho.cpu().numpy(), obs.cpu().numpy(), snap.cpu().numpy())
     ref = olb.lindblad_batch(H, cs, rho0, dt, steps)
     assert relerr(out["1"][0], ref) < TOL
-    for a, b in zip(out["1"], out["0"]):
-        assert relerr(a, b) < 1e-12
+    for a, b, c in zip(out["1"], out["0"], out["1nk"]):
+        assert relerr(a, b) < 1e-12 and relerr(c, b) < 1e-12
     tr = np.einsum("bsii->bs", out["1"][2])
     assert np.max(np.abs(tr - 1)) < 1e-12
