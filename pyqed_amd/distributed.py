@@ -27,6 +27,12 @@ def shard_range(n: int, rank: int, world_size: int) -> tuple[int, int]:
     return n * rank // world_size, n * (rank + 1) // world_size
 
 
+def _real_view(t: torch.Tensor) -> torch.Tensor:
+    """Collectives run on the real view of complex buffers (same storage): dist.reduce, unlike all_reduce,
+    does not convert complex tensors itself, and RCCL has no complex datatype."""
+    return torch.view_as_real(t) if t.is_complex() else t
+
+
 def sharded_sum(local_fn, n_units: int, dst: int | None = 0, group=None) -> torch.Tensor:
     """Evaluate local_fn(lo, hi) -> tensor on this rank's shard of n_units and sum over ranks with one
     collective: reduce to `dst` (dst=None: all_reduce).  Single process: local_fn(0, n_units)."""
@@ -35,9 +41,9 @@ def sharded_sum(local_fn, n_units: int, dst: int | None = 0, group=None) -> torc
     out = local_fn(lo, hi)
     if ws > 1:
         if dst is None:
-            dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
+            dist.all_reduce(_real_view(out), op=dist.ReduceOp.SUM, group=group)
         else:
-            dist.reduce(out, dst=dst, op=dist.ReduceOp.SUM, group=group)
+            dist.reduce(_real_view(out), dst=dst, op=dist.ReduceOp.SUM, group=group)
     return out
 
 
@@ -55,7 +61,8 @@ def sharded_sum_buckets(local_fn, n_units: int, out: torch.Tensor, buckets, dst:
     for b in buckets:
         local_fn(lo, hi, b)
         if ws > 1:
-            works.append(dist.reduce(out[b], dst=dst, op=dist.ReduceOp.SUM, group=group, async_op=True))
+            works.append(dist.reduce(_real_view(out[b]), dst=dst, op=dist.ReduceOp.SUM, group=group,
+                                     async_op=True))
     for w in works:
         w.wait()
     return out
