@@ -216,6 +216,21 @@ int qd_deom_rk4(qd_c128* ados, int B, int nmax, int K, int ns,
                 int ne, qd_c128* trace, void* stream);
 
 /*
+ * qd_deom_rk4 for batches of hierarchies stored ADO-major: ados [nmax][B][ns][ns] (hierarchy index
+ * fastest).  A wavefront then holds one ADO of 64 / 2^ceil(log2 ns^2) hierarchies: its index and
+ * prefactor loads are one request per wave and every neighbour read is one contiguous run.  Same
+ * arguments and results as qd_deom_rk4 otherwise (rho_sys / trace stay [B][nsteps+1]...).
+ * ns^2 <= 64, K <= 8.
+ */
+int qd_deom_rk4_ado_major(qd_c128* ados, int B, int nmax, int K, int ns,
+                          const int32_t* minus, const int32_t* plus, const qd_c128* coef,
+                          const qd_c128* damp, const int32_t* mode, int nmod,
+                          const qd_c128* H, const qd_c128* Hdip, const qd_c128* Q,
+                          const qd_c128* Qdip, const qd_c128* fsys, const qd_c128* fcoup,
+                          double dt, int nsteps, qd_c128* rho_sys, const qd_c128* E,
+                          int ne, qd_c128* trace, void* stream);
+
+/*
  * Single-exponential (high-T Drude) HEOM chain of pyqed/oqs.py:1808-1875
  * (oqs._heom): explicit in-place sweep per step, ADO n updated from the NEW
  * n-1 and the old n, n+1; ADO nado-1 never updated.  ados [B][nado][ns][ns]

@@ -54,6 +54,9 @@ SIGNATURES = {
     "qd_deom_rk4": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_double, c_int,
                             c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "qd_deom_rk4_ado_major": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_double, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "qd_heom_chain_euler": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_double, c_double, c_double,
                                     c_double, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "qd_sandwich": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),

@@ -47,6 +47,7 @@ struct DeomParams {
   c128* snap;          // [B][nsteps+1][ns][ns] (rho_0 after each step) or null
   int B, nmax, K, ns, nmod, stage, step, nsteps;
   double dt;
+  int bminor;  // ADO-major layout [nmax][B][ns][ns] (hierarchy index fastest; group kernel only)
 };
 
 __global__ __launch_bounds__(DEOM_TPB) void deom_stage_kernel(DeomParams p) {
@@ -145,9 +146,14 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) 
   const int e = (int)(t % G);
   const bool live = grp < ngrp;             // uniform within a group
   const bool valid = live && e < ns2;
-  const int n = live ? (int)(grp % p.nmax) : 0;
+  // [B][nmax] layout: grp = b nmax + n, an ADO's neighbours are rows of its own hierarchy;
+  // [nmax][B] layout (bminor): grp = n B + b, a wave holds one ADO of 64 / G hierarchies, so its index /
+  // prefactor loads are one request per wave and each neighbour read is one contiguous 64 / G x 64-B run
+  const int n = live ? (int)(p.bminor ? grp / p.B : grp % p.nmax) : 0;
+  const size_t hb = live ? (p.bminor ? grp % p.B : grp / p.nmax) : 0;   // hierarchy b
+  const size_t rs = p.bminor ? (size_t)p.B * ns2 : (size_t)ns2;         // ADO row stride
   const int ee = e < ns2 ? e : 0;           // padding lanes shadow element 0
-  const c128* X = p.xin + (live ? (grp - n) * ns2 : 0);
+  const c128* X = p.xin + (p.bminor ? hb * ns2 : hb * p.nmax * ns2);
   const int base = (int)(threadIdx.x & 63) & ~(G - 1);
   auto shfl = [&](c128 v, int src) { return cmk(__shfl(v.re, base + src, 64), __shfl(v.im, base + src, 64)); };
   // value of v held by lane `src` of this group (src is a compile-time constant after unrolling)
@@ -192,7 +198,7 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) 
     const int c = e + G * q;
     lc[q] = (live && c < 3 * K) ? p.coef[(size_t)n * K * 3 + c] : cmk(0, 0);
   }
-  const c128 own = live ? X[(size_t)n * ns2 + ee] : cmk(0, 0);
+  const c128 own = live ? X[(size_t)n * rs + ee] : cmk(0, 0);
   const c128 dmp = live ? p.damp[n] : cmk(0, 0);
   const size_t idx = grp * ns2 + e;
   const c128 r0 = valid ? p.rho[idx] : cmk(0, 0);
@@ -212,8 +218,8 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) 
   c128 ym[KMAX], yp[KMAX];
 #pragma unroll
   for (int k = 0; k < KMAX; ++k) {
-    ym[k] = (k < K && im[k] >= 0) ? X[(size_t)im[k] * ns2 + ee] : cmk(0, 0);
-    yp[k] = (k < K && ip[k] >= 0) ? X[(size_t)ip[k] * ns2 + ee] : cmk(0, 0);
+    ym[k] = (k < K && im[k] >= 0) ? X[(size_t)im[k] * rs + ee] : cmk(0, 0);
+    yp[k] = (k < K && ip[k] >= 0) ? X[(size_t)ip[k] * rs + ee] : cmk(0, 0);
   }
   __syncthreads();
 
@@ -282,18 +288,15 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) 
     const c128 a = cadd(a0, d);
     const c128 r1 = cadd(r0, cscale(cscale(a, dt), 1.0 / 6.0));
     p.rho_out[idx] = r1;
-    if (p.snap && n == 0) {
-      const size_t b = grp / p.nmax;
-      p.snap[(b * (p.nsteps + 1) + p.step + 1) * ns2 + e] = r1;
-    }
+    if (p.snap && n == 0) p.snap[(hb * (p.nsteps + 1) + p.step + 1) * ns2 + e] = r1;
   }
 }
 
-__global__ void deom_snap0_kernel(const c128* rho, c128* snap, int B, int nmax, int ns, int nsteps) {
+__global__ void deom_snap0_kernel(const c128* rho, c128* snap, int B, int nmax, int ns, int nsteps, int bminor) {
   const int ns2 = ns * ns;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < B * ns2; e += gridDim.x * blockDim.x) {
     const int b = e / ns2, ij = e % ns2;
-    snap[(size_t)b * (nsteps + 1) * ns2 + ij] = rho[(size_t)b * nmax * ns2 + ij];
+    snap[(size_t)b * (nsteps + 1) * ns2 + ij] = rho[(size_t)b * (bminor ? 1 : nmax) * ns2 + ij];
   }
 }
 
@@ -365,11 +368,12 @@ __global__ __launch_bounds__(256) void heom_chain_sweep_kernel(c128* ados, int n
 
 using namespace qd;
 
-extern "C" int qd_deom_rk4(qd_c128* ados, int B, int nmax, int K, int ns, const int32_t* minus, const int32_t* plus,
-                           const qd_c128* coef, const qd_c128* damp, const int32_t* mode, int nmod, const qd_c128* H,
-                           const qd_c128* Hdip, const qd_c128* Q, const qd_c128* Qdip, const qd_c128* fsys,
-                           const qd_c128* fcoup, double dt, int nsteps, qd_c128* rho_sys, const qd_c128* E, int ne,
-                           qd_c128* trace, void* stream) {
+namespace {
+int deom_run(qd_c128* ados, int B, int nmax, int K, int ns, const int32_t* minus, const int32_t* plus,
+             const qd_c128* coef, const qd_c128* damp, const int32_t* mode, int nmod, const qd_c128* H,
+             const qd_c128* Hdip, const qd_c128* Q, const qd_c128* Qdip, const qd_c128* fsys, const qd_c128* fcoup,
+             double dt, int nsteps, qd_c128* rho_sys, const qd_c128* E, int ne, qd_c128* trace, void* stream,
+             int bminor) {
   QD_CHECK_ARG(ados && minus && plus && coef && damp && mode && H && Q, "qd_deom_rk4: null pointer");
   QD_CHECK_ARG(B >= 1 && nmax >= 1 && K >= 1 && nsteps >= 0, "qd_deom_rk4: bad sizes B=%d nmax=%d K=%d", B, nmax, K);
   QD_CHECK_ARG(ns >= 1 && ns <= DEOM_MAX_NS, "qd_deom_rk4: ns=%d outside [1, %d]", ns, DEOM_MAX_NS);
@@ -393,7 +397,7 @@ extern "C" int qd_deom_rk4(qd_c128* ados, int B, int nmax, int K, int ns, const 
   const qd_c128* fc_h = fcoup;
   if (snap) {
     hipLaunchKernelGGL(deom_snap0_kernel, dim3(std::max(1, std::min(1024, (int)((B * ns2 + 255) / 256)))), dim3(256),
-                       0, st, (const c128*)ados, snap, B, nmax, ns, nsteps);
+                       0, st, (const c128*)ados, snap, B, nmax, ns, nsteps, bminor);
     QD_HIP(hipGetLastError());
   }
   DeomParams p;
@@ -417,10 +421,12 @@ extern "C" int qd_deom_rk4(qd_c128* ados, int B, int nmax, int K, int ns, const 
   p.nmod = nmod;
   p.nsteps = nsteps;
   p.dt = dt;
+  p.bminor = bminor;
   // group kernel when ns^2 <= 64 lanes and K <= 8; else the element kernel
   int G = 1;
   while (G < (int)ns2) G *= 2;
   const bool grp = G <= 64 && K <= 8;
+  QD_CHECK_ARG(!bminor || grp, "qd_deom_rk4_ado_major: needs ns^2 <= 64 and K <= 8 (group kernel)");
   const size_t nthreads = grp ? (size_t)B * nmax * G : tot;
   // A small hierarchy (one at L = 12, K = 5: 24.8k lanes) as 256-thread blocks would occupy ~100 of the
   // 256 CUs, each CU then issuing the loads of 4 waves; 64-thread blocks spread the same lanes over every
@@ -468,6 +474,27 @@ extern "C" int qd_deom_rk4(qd_c128* ados, int B, int nmax, int K, int ns, const 
     QD_HIP(hipGetLastError());
   }
   return QD_OK;
+}
+
+}  // namespace
+
+extern "C" int qd_deom_rk4(qd_c128* ados, int B, int nmax, int K, int ns, const int32_t* minus, const int32_t* plus,
+                           const qd_c128* coef, const qd_c128* damp, const int32_t* mode, int nmod, const qd_c128* H,
+                           const qd_c128* Hdip, const qd_c128* Q, const qd_c128* Qdip, const qd_c128* fsys,
+                           const qd_c128* fcoup, double dt, int nsteps, qd_c128* rho_sys, const qd_c128* E, int ne,
+                           qd_c128* trace, void* stream) {
+  return deom_run(ados, B, nmax, K, ns, minus, plus, coef, damp, mode, nmod, H, Hdip, Q, Qdip, fsys, fcoup, dt, nsteps,
+                  rho_sys, E, ne, trace, stream, 0);
+}
+
+extern "C" int qd_deom_rk4_ado_major(qd_c128* ados, int B, int nmax, int K, int ns, const int32_t* minus,
+                                     const int32_t* plus, const qd_c128* coef, const qd_c128* damp,
+                                     const int32_t* mode, int nmod, const qd_c128* H, const qd_c128* Hdip,
+                                     const qd_c128* Q, const qd_c128* Qdip, const qd_c128* fsys,
+                                     const qd_c128* fcoup, double dt, int nsteps, qd_c128* rho_sys, const qd_c128* E,
+                                     int ne, qd_c128* trace, void* stream) {
+  return deom_run(ados, B, nmax, K, ns, minus, plus, coef, damp, mode, nmod, H, Hdip, Q, Qdip, fsys, fcoup, dt, nsteps,
+                  rho_sys, E, ne, trace, stream, 1);
 }
 
 extern "C" int qd_heom_chain_euler(qd_c128* ados, int B, int nado, int ns, const qd_c128* H, const qd_c128* Q,

@@ -7,6 +7,7 @@ libqdyn qd_deom_rk4 (one kernel launch per RK4 stage).
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -352,8 +353,16 @@ class DEOMSolver:
                                       np.asarray(b.expn), self.lmax)
         c128 = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=complex))).to(dev)
         i32 = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=np.int32))).to(dev)
-        ados = torch.zeros((B, nmax, ns, ns), dtype=torch.complex128, device=dev)
-        ados[:, 0] = c128(rho0)
+        # batches of >= 16 hierarchies run ADO-major ([nmax][B]: coalesced neighbour reads across
+        # hierarchies, wave-uniform index / prefactor loads); QD_DEOM_ADO_MAJOR=0/1 forces the layout
+        am_env = os.environ.get("QD_DEOM_ADO_MAJOR")
+        ado_major = (B >= 16 if am_env is None else am_env != "0") and ns * ns <= 64 and K <= 8
+        if ado_major:
+            ados = torch.zeros((nmax, B, ns, ns), dtype=torch.complex128, device=dev)
+            ados[0] = c128(rho0)
+        else:
+            ados = torch.zeros((B, nmax, ns, ns), dtype=torch.complex128, device=dev)
+            ados[:, 0] = c128(rho0)
         H = c128(self.system)
         Q = c128(np.asarray(self.coupling, dtype=complex).reshape(-1, ns, ns))
         nmod = Q.shape[0]
@@ -368,15 +377,15 @@ class DEOMSolver:
         trace = torch.empty((B, nt + 1, 1), dtype=torch.complex128, device=dev) if p1 is not None else None
         tabs = (i32(self._minus), i32(self._plus), c128(coef), c128(damp), i32(b.mode))
         with torch.cuda.device(dev):
-            rc = _lib.load().qd_deom_rk4(
+            rc = getattr(_lib.load(), "qd_deom_rk4_ado_major" if ado_major else "qd_deom_rk4")(
                 ados.data_ptr(), B, nmax, K, ns, tabs[0].data_ptr(), tabs[1].data_ptr(), tabs[2].data_ptr(),
                 tabs[3].data_ptr(), tabs[4].data_ptr(), nmod, H.data_ptr(), _lib.ptr(Hdip_t), Q.data_ptr(),
                 _lib.ptr(Qdip_t), fs.ctypes.data if fs is not None else None,
                 fc.ctypes.data if fc is not None else None, float(dt), int(nt), rho_sys.data_ptr(),
                 _lib.ptr(p1_t), 1 if p1 is not None else 0, _lib.ptr(trace), _lib.stream_ptr(dev))
-        _lib.check(rc, "qd_deom_rk4")
+        _lib.check(rc, "qd_deom_rk4_ado_major" if ado_major else "qd_deom_rk4")
         torch.cuda.synchronize(dev)
-        self.ddos = ados.cpu().numpy()
+        self.ddos = (ados.transpose(0, 1) if ado_major else ados).cpu().numpy()   # [B][nmax][ns][ns]
         t_save = np.arange(nt + 1) * dt
         t_save[0] = 0
         if p1 is not None:

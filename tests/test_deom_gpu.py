@@ -157,3 +157,36 @@ def test_resolvent_grid2d_ragged_sizes():
                                              ny, out.data_ptr(), _lib.stream_ptr(dev))
         _lib.check(rc, "qd_resolvent_grid2d")
         assert relerr(out.cpu().numpy(), ref) < 1e-12, (n, nx, ny)
+
+
+@pytest.mark.parametrize("ns,B,pulse", [(2, 19, False), (2, 16, True), (3, 5, False)])
+def test_deom_ado_major_batch_layout(ns, B, pulse, monkeypatch):
+    """Batches stored ADO-major ([nmax][B], qd_deom_rk4_ado_major: one ADO of 16 hierarchies per wave) vs the
+    hierarchy-major layout and the oracle: per-hierarchy rho_0 histories, final ADOs, traces; a ragged batch
+    (19: waves straddle two ADOs), a pulsed system / coupling, and ns = 3 (16-lane groups with padding)."""
+    from oracle import deom as od
+    from pyqed_amd.deom import Bath, DEOMSolver
+    w = sp.symbols(r"\omega", real=True)
+    bath = Bath([2 * 0.5 * w / (1.0 + w ** 2)], w, [1.0], [3], [0] * 4)
+    rng = np.random.default_rng(B)
+    A = rng.standard_normal((ns, ns)) + 1j * rng.standard_normal((ns, ns))
+    H = (A + A.conj().T) / 4
+    Q = np.diag(np.arange(ns, dtype=float)).astype(complex) + 0.2 * (np.eye(ns, k=1) + np.eye(ns, k=-1))
+    dip = 0.3 * (np.eye(ns, k=1) + np.eye(ns, k=-1)).astype(complex)
+    f = (lambda t: np.exp(-((t - 0.05) / 0.02) ** 2) * np.cos(3 * t)) if pulse else None
+    psi = rng.standard_normal((B, ns)) + 1j * rng.standard_normal((B, ns))
+    psi /= np.linalg.norm(psi, axis=1, keepdims=True)
+    rho0 = np.einsum("bi,bj->bij", psi, psi.conj())
+    dt, nt, L = 0.005, 10, 5
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("QD_DEOM_ADO_MAJOR", mode)
+        sol = DEOMSolver(H, dip if pulse else None, bath, np.array([Q]), None, f, None, L)
+        t, saved = sol.run_batch(rho0, dt, nt)
+        out[mode] = (saved, sol.ddos)
+    assert relerr(out["1"][0], out["0"][0]) < 1e-13 and relerr(out["1"][1], out["0"][1]) < 1e-13
+    for b in (0, B - 1):
+        tt, ref, _ = od.run(H, dip if pulse else np.zeros((ns, ns)), f if pulse else (lambda t: 0), np.array([Q]),
+                            np.zeros((1, ns, ns)), lambda t: 0, (bath.etal, bath.etar, bath.etaa, bath.expn), L,
+                            rho0[b], dt, nt)
+        assert relerr(out["1"][0][b], ref) < TOL, b
