@@ -153,6 +153,14 @@ int qd_spo2_run(qd_c128* psi, const qd_c128* expVh, const qd_c128* expK, int nx,
                 void* stream);
 
 /*
+ * qd_spo2_run for B independent wavefunctions on one potential: psi [B][nx][ny][ns], snap
+ * [B][nsteps/nout][nx][ny][ns] (or NULL); one launch per pass for the whole batch on the
+ * 256 x 256 register-FFT kernels (ns <= 2), member by member otherwise.
+ */
+int qd_spo2_run_batch(qd_c128* psi, int B, const qd_c128* expVh, const qd_c128* expK, int nx,
+                      int ny, int ns, int nsteps, int nout, qd_c128* snap, void* stream);
+
+/*
  * qd_spo2_run with the two other SPO2 step structures of pyqed/wpd.py:
  *   expKy != NULL: Jacobi KEO (_KEO_jacobi, wpd.py:850-887): FFT_y, * expKy[i][ky]
  *                  (row i's factor exp(-i ky^2/(2 I(x_i)) dt)), FFT_x, * expK, IFFT2;

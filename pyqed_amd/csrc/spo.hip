@@ -566,12 +566,17 @@ __device__ __forceinline__ void fft256_wave(c128 (&x)[NS][4], const Q16Tw& t, c1
 // sit in the same lane of every wave: they are exchanged through LDS (one workgroup barrier per point
 // operator).  Same flags and arithmetic order of the point work as the LDS kernels:
 // [IFFT_y] -> V/2 -> [snapshot] -> [V/2] -> [FFT_y] -> [k_y phase].
+// Batches of wavefunctions (qd_spo2_run_batch): blockIdx.y = member w, psi / snap offset by w * wstride /
+// w * sstride (the point operators are shared).
 template <int NS>
 __global__ __launch_bounds__(64 * NS) void spo2_row_q16_kernel(c128* psi, const c128* U, const c128* twy, int flags,
-                                                               c128* snap, const c128* expKy) {
+                                                               c128* snap, const c128* expKy, size_t wstride = 0,
+                                                               size_t sstride = 0) {
   __shared__ c128 S[NS * 272];
   __shared__ c128 Xs[NS * 256];   // point-operator exchange: [state][lane * 4 + a]
   const int i = blockIdx.x, c = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 2, s = lane & 3;
+  psi += blockIdx.y * wstride;
+  if (snap) snap += blockIdx.y * sstride;
   c128 x[1][4], u[4][NS], ky[4];
   const size_t row = (size_t)i * 256;
 #pragma unroll
@@ -623,9 +628,10 @@ __global__ __launch_bounds__(64 * NS) void spo2_row_q16_kernel(c128* psi, const 
 // that XCD's L2 lines.
 template <int NS>
 __global__ __launch_bounds__(64) void spo2_col_q16_kernel(c128* psi, const c128* expKT, const c128* twx, int ncols,
-                                                          int pitch) {
+                                                          int pitch, size_t wstride = 0) {
   __shared__ c128 S[272];
   const int b = blockIdx.x, c = blockIdx.y;
+  psi += blockIdx.z * wstride;
   const int j = (ncols % 8 == 0) ? (b % 8) * (ncols / 8) + b / 8 : b;
   const int lane = threadIdx.x, g = lane >> 2, s = lane & 3;
   c128 x[1][4], kf[4];
@@ -813,6 +819,70 @@ extern "C" int qd_spo2_run_ex(qd_c128* psi_, const qd_c128* expVh_, const qd_c12
 extern "C" int qd_spo2_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* expK_, int nx, int ny, int ns,
                            int nsteps, int nout, qd_c128* snap_, void* stream) {
   return qd_spo2_run_ex(psi_, expVh_, nullptr, expK_, nullptr, nx, ny, ns, nsteps, nout, snap_, stream);
+}
+
+extern "C" int qd_spo2_run_batch(qd_c128* psi_, int B, const qd_c128* expVh_, const qd_c128* expK_, int nx, int ny,
+                                 int ns, int nsteps, int nout, qd_c128* snap_, void* stream) {
+  QD_CHECK_ARG(psi_ && expVh_ && expK_, "qd_spo2_run_batch: null pointer");
+  QD_CHECK_ARG(B >= 1 && B <= 65535, "qd_spo2_run_batch: B=%d outside [1, 65535]", B);
+  QD_CHECK_ARG(nsteps >= 0 && nout >= 1, "qd_spo2_run_batch: nsteps=%d nout=%d", nsteps, nout);
+  const size_t grid_elems = (size_t)nx * ny * ns;
+  const int nsave = nsteps / nout;
+  if (!(nx == 256 && ny == 256 && ns <= 2 && q16_enabled())) {
+    // other shapes: one member at a time on the single-wavefunction path
+    for (int w = 0; w < B; ++w) {
+      const int rc = qd_spo2_run_ex(psi_ + w * grid_elems, expVh_, nullptr, expK_, nullptr, nx, ny, ns, nsteps, nout,
+                                    snap_ ? snap_ + (size_t)w * nsave * grid_elems : nullptr, stream);
+      if (rc) return rc;
+    }
+    return QD_OK;
+  }
+  if (nsteps == 0) return QD_OK;
+  hipStream_t st = (hipStream_t)stream;
+  c128* psi = (c128*)psi_;
+  const c128* U = (const c128*)expVh_;
+  c128* snap = (c128*)snap_;
+  void* w = nullptr;
+  const size_t nkt = (size_t)nx * ny;
+  int rc = workspace(WS_SPO, (nkt + nx + ny) * sizeof(c128), &w);
+  if (rc) return rc;
+  c128* expKT = (c128*)w;
+  c128* twx = expKT + nkt;
+  c128* twy = twx + nx;
+  if ((rc = twiddles(nx, st, twx))) return rc;
+  if ((rc = twiddles(ny, st, twy))) return rc;
+  hipLaunchKernelGGL(transpose_scale_kernel, dim3((int)std::min<size_t>((nkt + 255) / 256, 4096)), dim3(256), 0, st,
+                     (const c128*)expK_, nx, ny, 1.0 / ((double)nx * ny), expKT);
+  QD_HIP(hipGetLastError());
+  const size_t sstride = (size_t)nsave * grid_elems;
+  auto row = [&](int flags, c128* sp) {
+    if (ns == 1)
+      hipLaunchKernelGGL(spo2_row_q16_kernel<1>, dim3(nx, B), dim3(64), 0, st, psi, U, twy, flags, sp,
+                         (const c128*)nullptr, grid_elems, sstride);
+    else
+      hipLaunchKernelGGL(spo2_row_q16_kernel<2>, dim3(nx, B), dim3(128), 0, st, psi, U, twy, flags, sp,
+                         (const c128*)nullptr, grid_elems, sstride);
+  };
+  auto col = [&]() {
+    if (ns == 1)
+      hipLaunchKernelGGL(spo2_col_q16_kernel<1>, dim3(ny, 1, B), dim3(64), 0, st, psi, (const c128*)expKT,
+                         (const c128*)twx, ny, ny, grid_elems);
+    else
+      hipLaunchKernelGGL(spo2_col_q16_kernel<2>, dim3(ny, 2, B), dim3(64), 0, st, psi, (const c128*)expKT,
+                         (const c128*)twx, ny, ny, grid_elems);
+  };
+  // the Strang step sequence of qd_spo2_run_ex (both V/2 halves, wpd.py:723-730)
+  row(ROW_VH1 | ROW_FWD, nullptr);
+  QD_HIP(hipGetLastError());
+  for (int s = 1; s <= nsteps; ++s) {
+    col();
+    QD_HIP(hipGetLastError());
+    const bool take = snap && (s % nout == 0);
+    c128* sp = take ? snap + (size_t)(s / nout - 1) * grid_elems : nullptr;
+    row(ROW_INV | ROW_VH1 | (take ? ROW_SNAP : 0) | (s < nsteps ? ROW_VH2 | ROW_FWD : 0), sp);
+    QD_HIP(hipGetLastError());
+  }
+  return QD_OK;
 }
 
 extern "C" int qd_spo1d_run(qd_c128* psi_, const qd_c128* expV_, const qd_c128* expVh_, const qd_c128* expK_, int nx,

@@ -331,6 +331,32 @@ class SPO2(_PointPropagators):
             states = [host[k] for k in range(nsnap)]
         return psi.cpu().numpy(), states
 
+    def run_batch(self, psi0s, dt=0.01, nt=1, nout=1, device=None):
+        """Extension: B independent wavepackets psi0s [B, nx, ny, ns] on one potential, Strang steps as
+        run(return_states=True) for each (qd_spo2_run_batch: one launch per pass for the whole batch).
+        Returns (final states [B, nx, ny, ns], snapshots [B, nt//nout, nx, ny, ns]) as device tensors."""
+        if self.coords != 'linear':
+            raise NotImplementedError("run_batch: linear coordinates only")
+        self.build(dt=dt)
+        dev = device or default_device()
+        _lib.ensure_device(dev)
+        psi = psi0s if isinstance(psi0s, torch.Tensor) else _dev_c128(psi0s, dev)
+        psi = psi.to(device=dev, dtype=torch.complex128).contiguous().clone()
+        B = psi.shape[0]
+        if tuple(psi.shape[1:]) != (self.nx, self.ny, self.ns):
+            raise ValueError(f"psi0s must be [B, {self.nx}, {self.ny}, {self.ns}]")
+        nsnap = nt // nout
+        snap = torch.empty((B, nsnap, self.nx, self.ny, self.ns), dtype=torch.complex128, device=dev) if nsnap \
+            else None
+        _, eVh = self._point_ops_dev(dev, need_full=False)
+        eK = _dev_c128(self.exp_K, dev)
+        with torch.cuda.device(dev):
+            rc = _lib.load().qd_spo2_run_batch(psi.data_ptr(), B, eVh.data_ptr(), eK.data_ptr(), self.nx, self.ny,
+                                               self.ns, int(nsnap * nout), int(nout), _lib.ptr(snap),
+                                               _lib.stream_ptr(dev))
+        _lib.check(rc, "qd_spo2_run_batch")
+        return psi, snap
+
     def run(self, psi0, e_ops=[], dt=0.01, nt=1, t0=0., nout=1, return_states=True):
         """wpd.py:692-758.  return_states=True: psilist = [psi0] + the state after every nout
         Strang steps (nt//nout*nout steps).  return_states=False: the merged-V arithmetic runs

@@ -208,3 +208,35 @@ def test_device_point_propagators_match_eigh(ns, cplx):
     w2, u2 = np.linalg.eigh(v)                              # lazy host eigen data
     assert np.array_equal(sol.d2a, u2)
     assert (sol.apes is None) if cplx else np.array_equal(sol.apes, w2)
+
+
+@pytest.mark.parametrize("n,ns,B", [(256, 2, 5), (256, 1, 3), (64, 2, 2)])
+def test_spo2_run_batch_vs_single_and_oracle(n, ns, B):
+    """SPO2.run_batch (qd_spo2_run_batch: one launch per pass for B wavepackets; 256x256 register-FFT kernels
+    with a batch grid axis, member by member for other shapes): every member equals run() of that member
+    and the oracle's Strang steps, snapshots included."""
+    from oracle import spo as ospo
+    from pyqed_amd.wpd import SPO2
+    x = np.linspace(-6, 6, n)
+    X, Y = np.meshgrid(x, x, indexing="ij")
+    v = np.zeros((n, n, ns, ns))
+    for a in range(ns):
+        v[:, :, a, a] = 0.5 * ((X + (-1) ** a) ** 2 + Y ** 2) + 0.1 * a
+    for a in range(ns - 1):
+        v[:, :, a, a + 1] = v[:, :, a + 1, a] = 0.2 * X
+    rng = np.random.default_rng(B)
+    psi0 = np.zeros((B, n, n, ns), complex)
+    for b in range(B):
+        x0, k0 = rng.uniform(-2, 2), rng.uniform(-1, 1)
+        psi0[b, :, :, b % ns] = np.exp(-((X - x0) ** 2 + Y ** 2) / 2 + 1j * k0 * X) / np.sqrt(np.pi)
+    sol = SPO2(x, x, mass=[1.0, 1.0], nstates=ns)
+    sol.set_dpes(v)
+    nt, nout, dt = 6, 2, 0.05
+    psi, snap = sol.run_batch(psi0, dt=dt, nt=nt, nout=nout)
+    psi, snap = psi.cpu().numpy(), snap.cpu().numpy()
+    for b in (0, B - 1):
+        r = sol.run(psi0[b], dt=dt, nt=nt, nout=nout)
+        assert relerr(psi[b], r.psi) < 1e-13
+        assert relerr(snap[b], np.array(r.psilist[1:])) < 1e-13
+        ref = ospo.spo2_run(sol.exp_V_half, sol.exp_K, psi0[b], nt, nout)
+        assert relerr(np.array([psi0[b]] + list(snap[b])), np.array(ref)) < TOL
