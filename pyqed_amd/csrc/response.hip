@@ -275,9 +275,16 @@ __global__ __launch_bounds__(256) void ens_z_uniform_kernel(const c128* Mt, cons
 }
 
 // members per block of ens_z_uniform_kernel: tables of <= 32 KB LDS, at most 32 members
-int z_group(int nL, int nz, int n1p) {
+// and at least 1024 member blocks when M allows (M = 4096: 0.128 -> 0.116 ms per 256 x 256 grid; no change at
+// M = 32k, where the LDS cap binds); QD_Z_MINBLOCKS overrides the 1024 (A/B, tools/zblocks_ab.sh)
+int z_group(int nL, int nz, int n1p, int M) {
   const int per = nL * nz + nz * (16 + n1p / 16) + 2 * nz;
-  return std::max(1, std::min(32, 2048 / per));
+  const int G = std::max(1, std::min(32, 2048 / per));
+  static const int mb = [] {
+    const char* e = std::getenv("QD_Z_MINBLOCKS");
+    return e ? std::atoi(e) : 1024;
+  }();
+  return mb > 0 ? std::max(1, std::min(G, M / mb)) : G;
 }
 // its dynamic LDS bytes
 size_t z_lds(int G, int nL, int nz, int n1p) {
@@ -734,7 +741,6 @@ int ens_run(const char* fn, const qd_c128* alpha, const qd_c128* Mt, const qd_c1
   const int K = M * nL;
   const int tiles = ceil_div(K, CG_KT);
   const int Kp = tiles * CG_KT;
-  const int blocks2d = (n3p / BT) * (n1p / BT);
   const SplitPlan plan = split_plan(n3p, n1p, tiles);
   const int S = plan.S;
   const size_t nXe = (size_t)n3p * Kp, nZe = (size_t)Kp * n1p, nsl = (size_t)S * n3p * n1p;
@@ -761,7 +767,7 @@ int ens_run(const char* fn, const qd_c128* alpha, const qd_c128* Mt, const qd_c1
                        t3_0, dt3, n3, n3p, coarse, fine);
     QD_HIP(hipGetLastError());
   }
-  const int G = z_group(nL, nz, n1p);
+  const int G = z_group(nL, nz, n1p, M);
   const int nMB = ceil_div(M, G);
   if (!t1 && nL <= ZMAX && nz <= ZMAX && n1p <= 16 * UNI_MAXC && (long)nMB + xblocks <= 65535) {
     // Z (uniform t1), G members per block; a materialised uniform X (when not generated in the GEMM) in
@@ -900,7 +906,7 @@ extern "C" int qd_response2d_t2_operands_rect(const qd_c128* alpha, const qd_c12
     QD_HIP(hipGetLastError());
   }
   // Q = C_m Y_m: the uniform Z build with Mt := C [M][nr][nq] (Z rows only)
-  const int G = z_group(nr, nq, d.n1p);
+  const int G = z_group(nr, nq, d.n1p, M);
   hipLaunchKernelGGL(ens_z_uniform_kernel, dim3(ceil_div(d.n1p, 256), ceil_div(M, G)), dim3(256),
                      z_lds(G, nr, nq, d.n1p), st, (const c128*)Cm,
                      (const c128*)beta, (const c128*)lamq, M, nr, nq, G, t1_0, dt1, n1, d.n1p, Q, (const c128*)nullptr,
