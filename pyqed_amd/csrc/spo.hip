@@ -650,6 +650,53 @@ __global__ __launch_bounds__(64) void spo2_col_q16_kernel(c128* psi, const c128*
   for (int a = 0; a < 4; ++a) psi[((size_t)(64 * a + 16 * s + g) * pitch + j) * NS + c] = x[0][a];
 }
 
+// Column pass for batches (qd_spo2_run_batch), coalesced: one 512-thread workgroup per 4 adjacent columns
+// and both states of one wavefunction (8 lines, wave w = column j0 + w / 2, state w % 2).  The 256 x 4 x 2
+// tile is read row by row as 128-B contiguous pieces into LDS, each wave runs the register FFT of its line
+// (FFT_x -> * exp_K / (nx ny) -> IFFT_x), the lines go back through LDS and out as 128-B rows.  (The
+// single-wavefunction pass reads each column directly with an 8 KB stride: fine from L2 for one grid,
+// L2-request-bound for a batch.)  NS = 2, nx = ny = 256.
+__global__ __launch_bounds__(512) void spo2_col_tile_kernel(c128* psi, const c128* expKT, const c128* twx,
+                                                            size_t wstride) {
+  __shared__ c128 T[256 * 9];        // [row][8 lines + 1 pad]
+  __shared__ c128 S[8 * 272];        // per-wave FFT exchange
+  psi += blockIdx.y * wstride;
+  const int j0 = blockIdx.x * 4;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 2, s = lane & 3;
+  c128 v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {      // element e = row * 8 + (column - j0) * 2 + state: 128 B per row
+    const int e = tid + 512 * q, r = e >> 3, cs = e & 7;
+    v[q] = psi[((size_t)r * 256 + j0) * 2 + cs];
+  }
+  const int j = j0 + (w >> 1), c = w & 1;
+  c128 x[1][4], kf[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) kf[a] = expKT[(size_t)j * 256 + 64 * a + 16 * s + g];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = tid + 512 * q;
+    T[(e >> 3) * 9 + (e & 7)] = v[q];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int a = 0; a < 4; ++a) x[0][a] = T[(64 * a + 16 * s + g) * 9 + w];
+  const Q16Tw t = q16_twiddles(twx, g, s);
+  fft256_wave<false, 1>(x, t, S + w * 272, g, s);
+#pragma unroll
+  for (int a = 0; a < 4; ++a) x[0][a] = cmul(x[0][a], kf[a]);
+  fft256_wave<true, 1>(x, t, S + w * 272, g, s);
+  __syncthreads();                   // every wave has read its line of T
+#pragma unroll
+  for (int a = 0; a < 4; ++a) T[(64 * a + 16 * s + g) * 9 + w] = x[0][a];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = tid + 512 * q, r = e >> 3, cs = e & 7;
+    psi[((size_t)r * 256 + j0) * 2 + cs] = T[r * 9 + cs];
+  }
+}
+
 bool q16_enabled() {
   static const int on = [] {
     const char* e = getenv("QD_SPO_Q16");
@@ -863,10 +910,17 @@ extern "C" int qd_spo2_run_batch(qd_c128* psi_, int B, const qd_c128* expVh_, co
       hipLaunchKernelGGL(spo2_row_q16_kernel<2>, dim3(nx, B), dim3(128), 0, st, psi, U, twy, flags, sp,
                          (const c128*)nullptr, grid_elems, sstride);
   };
+  static const bool tile_col = [] {  // QD_SPO_COLTILE=0: the per-column pass (A/B)
+    const char* e = getenv("QD_SPO_COLTILE");
+    return !(e && e[0] == '0');
+  }();
   auto col = [&]() {
     if (ns == 1)
       hipLaunchKernelGGL(spo2_col_q16_kernel<1>, dim3(ny, 1, B), dim3(64), 0, st, psi, (const c128*)expKT,
                          (const c128*)twx, ny, ny, grid_elems);
+    else if (tile_col)
+      hipLaunchKernelGGL(spo2_col_tile_kernel, dim3(ny / 4, B), dim3(512), 0, st, psi, (const c128*)expKT,
+                         (const c128*)twx, grid_elems);
     else
       hipLaunchKernelGGL(spo2_col_q16_kernel<2>, dim3(ny, 2, B), dim3(64), 0, st, psi, (const c128*)expKT,
                          (const c128*)twx, ny, ny, grid_elems);
