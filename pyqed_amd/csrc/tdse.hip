@@ -11,6 +11,8 @@
 // each stage with lanes over rows (coalesced), so a stage is one GEMV.
 #include "qd_common.hpp"
 
+#include <cstdlib>
+
 namespace qd {
 namespace {
 
@@ -139,6 +141,174 @@ __global__ __launch_bounds__(TD_TPB) void tdse_rk4_kernel(const c128* mHT, c128*
   for (int r = threadIdx.x; r < N; r += TD_TPB) pg[r] = psi[r];
 }
 
+// ---- row-parallel path (small batches, any N): the persistent kernel runs one wavefunction on one CU,
+// which leaves the chip idle and re-streams H through that CU every stage (N = 2048: ~1 ms per stage).
+// Here every stage is one launch: a wave per row r computes k_r = -i sum_j H[r][j] x_j (lanes over j,
+// coalesced 1 KB row pieces, fixed-order wave reduction) and lane 0 runs the RK4 update of element r
+// (same arithmetic order as the persistent kernel).  Buffers per wavefunction: psi (in place), two stage
+// inputs and the accumulator.  Observables: a wave per (row, E_m) forms conj(psi_r) (E_m psi)_r, then one
+// block per (b, m) sums the rows in fixed order.
+__device__ __forceinline__ c128 wave_row_dot(const c128* row, const c128* x, int N) {
+  const int lane = threadIdx.x & 63;
+  double sr = 0.0, si = 0.0;
+  for (int j = lane; j < N; j += 64) {
+    const c128 h = row[j], v = x[j];
+    sr += h.re * v.re - h.im * v.im;
+    si += h.re * v.im + h.im * v.re;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    sr += __shfl_xor(sr, off, 64);
+    si += __shfl_xor(si, off, 64);
+  }
+  return cmk(sr, si);
+}
+
+// grid (ceil(N / 4), ceil(B / NB)), 256 threads: wave w of block x handles row r = 4 x + w for the (up to
+// NB) wavefunctions of group blockIdx.y.  NB = 1 is the launched form: reading each H row once for 8
+// wavefunctions (NB = 8) measured 2x slower at N = 2048, B = 8 (8 dependent loads per lane per row piece,
+// 1/8 of the waves in flight), since the H rows of one stage stay L2/MALL-resident across the B waves anyway.
+template <int NB>
+__global__ __launch_bounds__(256) void tdse_row_stage_kernel(const c128* H, c128* psi_g, c128* ws, int N, int B,
+                                                             double dt, int stage) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= N) return;
+  const int b0 = blockIdx.y * NB;
+  const int nb = min(NB, B - b0);
+  const int lane = threadIdx.x & 63;
+  const c128* row = H + (size_t)r * N;
+  double sr[NB], si[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) sr[q] = si[q] = 0.0;
+  // stage inputs: stage 0 psi, stage 1 x0, stage 2 x1, stage 3 x0 (x0, x1, acc per wavefunction in ws)
+  auto xin = [&](int b) -> const c128* {
+    return stage == 0 ? psi_g + (size_t)b * N : ws + (size_t)b * 3 * N + ((stage & 1) ? 0 : N);
+  };
+  for (int j = lane; j < N; j += 64) {
+    const c128 h = row[j];
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      if (q < nb) {
+        const c128 v = xin(b0 + q)[j];
+        sr[q] += h.re * v.re - h.im * v.im;
+        si[q] += h.re * v.im + h.im * v.re;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      sr[q] += __shfl_xor(sr[q], off, 64);
+      si[q] += __shfl_xor(si[q], off, 64);
+    }
+  }
+  if (lane != 0) return;
+  const double dt2 = dt / 2.0;
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    if (q >= nb) break;
+    const size_t b = b0 + q;
+    c128* psi = psi_g + b * N;
+    c128* x0 = ws + b * 3 * N;
+    c128* acc = x0 + 2 * N;
+    c128* xout = (stage & 1) ? x0 + N : x0;   // stage 0: x0, stage 1: x1, stage 2: x0
+    const c128 k = cmulmi(cmk(sr[q], si[q]));
+    const c128 p = psi[r];
+    if (stage == 0) {
+      acc[r] = k;
+      xout[r] = cadd(p, cscale(k, dt2));
+    } else if (stage == 1) {
+      acc[r] = cadd(acc[r], cscale(k, 2.0));
+      xout[r] = cadd(p, cscale(k, dt2));
+    } else if (stage == 2) {
+      acc[r] = cadd(acc[r], cscale(k, 2.0));
+      xout[r] = cadd(p, cscale(k, dt));
+    } else {
+      const c128 a = cadd(acc[r], k);
+      psi[r] = cadd(p, cscale(cscale(a, 1.0 / 6.0), dt));
+    }
+  }
+}
+
+// part[b][m][r] = conj(psi_r) (E_m psi)_r ; grid (ceil(N / 4), B * ne)
+__global__ __launch_bounds__(256) void tdse_obs_rows_kernel(const c128* E, int ne, const c128* psi_g, int N,
+                                                            c128* part) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= N) return;
+  const int b = blockIdx.y / ne, m = blockIdx.y % ne;
+  const c128* psi = psi_g + (size_t)b * N;
+  const c128 y = wave_row_dot(E + ((size_t)m * N + r) * N, psi, N);
+  if ((threadIdx.x & 63) == 0) part[((size_t)b * ne + m) * N + r] = cmul(cconj(psi[r]), y);
+}
+
+// obs[b][idx][m] = sum_r part[b][m][r] (per-thread strided partials, wave butterfly, 4-wave sum: fixed order)
+__global__ __launch_bounds__(256) void tdse_obs_sum_kernel(const c128* part, int ne, int N, int nsave, int idx,
+                                                           c128* obs) {
+  __shared__ c128 red[4];
+  const int b = blockIdx.x / ne, m = blockIdx.x % ne;
+  const c128* p = part + ((size_t)b * ne + m) * N;
+  double sr = 0.0, si = 0.0;
+  for (int r = threadIdx.x; r < N; r += 256) {
+    sr += p[r].re;
+    si += p[r].im;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    sr += __shfl_xor(sr, off, 64);
+    si += __shfl_xor(si, off, 64);
+  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cmk(sr, si);
+  __syncthreads();
+  if (threadIdx.x == 0) obs[((size_t)b * (nsave + 1) + idx) * ne + m] = cadd(cadd(red[0], red[1]), cadd(red[2], red[3]));
+}
+
+__global__ void tdse_snap_kernel(const c128* psi, int B, int N, int nsave, int idx, c128* snap) {
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < (size_t)B * N; e += (size_t)gridDim.x * blockDim.x)
+    snap[((e / N) * nsave + idx - 1) * N + e % N] = psi[e];
+}
+
+int tdse_rows_run(const c128* H, c128* psi, int B, int N, double dt, int nsteps, int save_every, c128* snap,
+                  const c128* E, int ne, c128* obs, hipStream_t st) {
+  const int nsave = save_every > 0 ? nsteps / save_every : 0;
+  void* w = nullptr;
+  const size_t ws_elems = (size_t)B * 3 * N + (size_t)B * (ne ? ne : 0) * N;
+  int rc = workspace(WS_MISC, ws_elems * sizeof(c128), &w);
+  if (rc) return rc;
+  c128* ws = (c128*)w;
+  c128* part = ws + (size_t)B * 3 * N;
+  const dim3 rows((N + 3) / 4, B);
+  auto observe = [&](int idx) -> int {
+    if (ne && obs) {
+      hipLaunchKernelGGL(tdse_obs_rows_kernel, dim3((N + 3) / 4, B * ne), dim3(256), 0, st, E, ne, (const c128*)psi, N,
+                         part);
+      QD_HIP(hipGetLastError());
+      hipLaunchKernelGGL(tdse_obs_sum_kernel, dim3(B * ne), dim3(256), 0, st, (const c128*)part, ne, N, nsave, idx,
+                         obs);
+      QD_HIP(hipGetLastError());
+    }
+    return QD_OK;
+  };
+  QD_CHECK_ARG((size_t)B * (ne ? ne : 1) <= 65535, "qd_tdse_rk4: B * ne too large for the row path");
+  if ((rc = observe(0))) return rc;
+  for (int s = 0; s < nsteps; ++s) {
+    for (int stage = 0; stage < 4; ++stage) {
+      hipLaunchKernelGGL(tdse_row_stage_kernel<1>, rows, dim3(256), 0, st, H, psi, ws, N, B, dt, stage);
+      QD_HIP(hipGetLastError());
+    }
+    if (save_every > 0 && (s + 1) % save_every == 0) {
+      const int idx = (s + 1) / save_every;
+      if (snap) {
+        hipLaunchKernelGGL(tdse_snap_kernel, dim3((int)std::min<size_t>(((size_t)B * N + 255) / 256, 4096)), dim3(256),
+                           0, st, (const c128*)psi, B, N, nsave, idx, snap);
+        QD_HIP(hipGetLastError());
+      }
+      if ((rc = observe(idx))) return rc;
+    }
+  }
+  return QD_OK;
+}
+
 }  // namespace
 }  // namespace qd
 
@@ -147,10 +317,20 @@ using namespace qd;
 extern "C" int qd_tdse_rk4(const qd_c128* H, qd_c128* psi, int B, int N, double dt, int nsteps, int save_every,
                            qd_c128* snap, const qd_c128* E, int ne, qd_c128* obs, void* stream) {
   QD_CHECK_ARG(H && psi, "qd_tdse_rk4: null pointer");
-  QD_CHECK_ARG(N >= 1 && N <= TD_MAXN && B >= 1 && nsteps >= 0, "qd_tdse_rk4: bad sizes N=%d B=%d", N, B);
+  QD_CHECK_ARG(N >= 1 && B >= 1 && nsteps >= 0, "qd_tdse_rk4: bad sizes N=%d B=%d", N, B);
   QD_CHECK_ARG(ne >= 0 && (ne == 0 || (E && obs)), "qd_tdse_rk4: E/obs null but ne=%d", ne);
   QD_CHECK_ARG(!obs || save_every > 0 || nsteps == 0, "qd_tdse_rk4: observables need save_every > 0");
   hipStream_t st = (hipStream_t)stream;
+  // row-parallel path (a wave per row per stage) unless QD_TDSE_ROWS=0 asks for the persistent kernel
+  // (one workgroup per wavefunction, N <= 2048; kept for A/B runs):
+  // measured (tools/tdse_bench.py, wavefunction-steps/s, persistent -> rows): N = 64, B = 1: 33k -> 97k;
+  // B = 256: 8.5M -> 9.3M; N = 1024, B = 1: 239 -> 33.6k; B = 64: 16k -> 230k; N = 2048, B = 1: 55 -> 17.6k;
+  // N = 4096 (rows only): 6.1k.  The rows path wins at every measured size, so it is the default.
+  bool rows = true;
+  if (const char* e = std::getenv("QD_TDSE_ROWS")) rows = N > TD_MAXN || std::atoi(e) != 0;
+  if (rows)
+    return tdse_rows_run((const c128*)H, (c128*)psi, B, N, dt, nsteps, save_every, (c128*)snap, (const c128*)E, ne,
+                         ne ? (c128*)obs : nullptr, st);
   const size_t NN = (size_t)N * N;
   void* w = nullptr;
   int rc = workspace(WS_MISC, (1 + ne) * NN * sizeof(c128), &w);

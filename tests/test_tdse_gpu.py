@@ -101,3 +101,41 @@ def test_driven_batch_vs_oracle():
         o, psit, _ = ot.driven_dynamics(H0, [(Hd[0], f)], psi0[b], dt, (nblk + 1) * nout, [H0], nout)
         assert relerr(obs[b].cpu().numpy(), o) < TOL
         assert relerr(snap[b].cpu().numpy(), psit[:, 1:].T) < TOL
+
+
+@pytest.mark.parametrize("N,B,save_every", [(300, 1, 2), (2500, 2, 3), (1024, 64, 5)])
+def test_tdse_row_path_vs_persistent_and_oracle(N, B, save_every, monkeypatch):
+    """Row-parallel TDSE path (a wave per row and stage launch; default for small batches, the only path past
+    N = 2048): snapshots and observables (E_m = H, diag) against the persistent kernel (N <= 2048) and the
+    oracle's RK4 (oracle.tdse.quantum_dynamics restates mol.py:1603-1691)."""
+    import torch
+    from oracle import tdse as otd
+    from pyqed_amd.mol import tdse_rk4
+    rng = np.random.default_rng(N + B)
+    A = rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N))
+    H = (A + A.conj().T) / 2 / np.sqrt(N)
+    Ed = np.diag(np.linspace(0, 1, N)).astype(complex)
+    psi0 = rng.standard_normal((B, N)) + 1j * rng.standard_normal((B, N))
+    psi0 /= np.linalg.norm(psi0, axis=1, keepdims=True)
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    steps, dt = 6, 0.02
+    out = {}
+    for mode in (("1", "0") if N <= 2048 else ("1",)):
+        monkeypatch.setenv("QD_TDSE_ROWS", mode)
+        psi = t(psi0.copy())
+        snap, obs = tdse_rk4(t(H), psi, dt, steps, save_every=save_every, e_ops=t(np.array([H, Ed])))
+        out[mode] = (psi.cpu().numpy(), snap.cpu().numpy(), obs.cpu().numpy())
+    if "0" in out:
+        for a, b in zip(out["1"], out["0"]):
+            assert relerr(a, b) < 1e-13
+    psi, snap, obs = out["1"]
+    ref = psi0[0].copy()
+    for s in range(steps):
+        ref = otd._rk4(ref, H, dt)
+        if (s + 1) % save_every == 0:
+            assert relerr(snap[0][(s + 1) // save_every - 1], ref) < 1e-12
+    assert relerr(psi[0], ref) < 1e-12
+    e0 = np.vdot(psi0[0], H @ psi0[0])
+    assert abs(obs[0, 0, 0] - e0) < 1e-12 * max(1, abs(e0))
+    assert np.allclose(np.linalg.norm(psi, axis=1), 1, atol=1e-10)
