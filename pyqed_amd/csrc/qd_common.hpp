@@ -42,7 +42,8 @@ void set_error(const char* fmt, ...);
 // Per-device growable workspace, owned by the library (freed by qd_shutdown).
 // Never handed to the caller.  Slot ids keep independent users apart.
 enum WsSlot { WS_LINDBLAD = 0, WS_LINDBLAD_OPS = 1, WS_SPO = 2, WS_DEOM = 3,
-              WS_SUPEROP = 4, WS_2DES = 5, WS_MISC = 6, WS_2DES_OPS = 7, WS_NSLOTS = 8 };
+              WS_SUPEROP = 4, WS_2DES = 5, WS_MISC = 6, WS_2DES_OPS = 7, WS_TDSE_H = 8,
+              WS_NSLOTS = 9 };
 int workspace(WsSlot slot, size_t bytes, void** ptr);
 void free_workspaces();
 

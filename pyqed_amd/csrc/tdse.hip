@@ -29,6 +29,16 @@ __global__ void tdse_prep_kernel(const c128* H, const c128* E, int ne, int N, c1
   }
 }
 
+// Ht = H0 - sum_d f_d Hd_d, row-major (driven step block of the row-parallel path; f on the device)
+__global__ void tdse_driven_h_kernel(const c128* H0, const c128* Hd, int nd, const c128* f, int N, c128* Ht) {
+  const size_t NN = (size_t)N * N;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < NN; e += (size_t)gridDim.x * blockDim.x) {
+    c128 h = H0[e];
+    for (int d = 0; d < nd; ++d) h = csub(h, cmul(f[d], Hd[d * NN + e]));
+    Ht[e] = h;
+  }
+}
+
 // mHT[j][r] = -i (H0 - sum_d f_d Hd_d)[r][j]   (driven step block; f on the device)
 __global__ void tdse_driven_prep_kernel(const c128* H0, const c128* Hd, int nd, const c128* f, int N, c128* mHT) {
   const size_t NN = (size_t)N * N;
@@ -268,9 +278,11 @@ __global__ void tdse_snap_kernel(const c128* psi, int B, int N, int nsave, int i
     snap[((e / N) * nsave + idx - 1) * N + e % N] = psi[e];
 }
 
+// save0 / nsave_total: this launch's first save index and the run's number of saves (driven runs call it once
+// per block of save_every steps, like the persistent kernel); obs row 0 (t0) only when save0 == 0.
 int tdse_rows_run(const c128* H, c128* psi, int B, int N, double dt, int nsteps, int save_every, c128* snap,
-                  const c128* E, int ne, c128* obs, hipStream_t st) {
-  const int nsave = save_every > 0 ? nsteps / save_every : 0;
+                  const c128* E, int ne, c128* obs, hipStream_t st, int save0 = 0, int nsave_total = -1) {
+  const int nsave = nsave_total >= 0 ? nsave_total : (save_every > 0 ? nsteps / save_every : 0);
   void* w = nullptr;
   const size_t ws_elems = (size_t)B * 3 * N + (size_t)B * (ne ? ne : 0) * N;
   int rc = workspace(WS_MISC, ws_elems * sizeof(c128), &w);
@@ -290,14 +302,14 @@ int tdse_rows_run(const c128* H, c128* psi, int B, int N, double dt, int nsteps,
     return QD_OK;
   };
   QD_CHECK_ARG((size_t)B * (ne ? ne : 1) <= 65535, "qd_tdse_rk4: B * ne too large for the row path");
-  if ((rc = observe(0))) return rc;
+  if (save0 == 0 && (rc = observe(0))) return rc;
   for (int s = 0; s < nsteps; ++s) {
     for (int stage = 0; stage < 4; ++stage) {
       hipLaunchKernelGGL(tdse_row_stage_kernel<1>, rows, dim3(256), 0, st, H, psi, ws, N, B, dt, stage);
       QD_HIP(hipGetLastError());
     }
     if (save_every > 0 && (s + 1) % save_every == 0) {
-      const int idx = (s + 1) / save_every;
+      const int idx = save0 + (s + 1) / save_every;
       if (snap) {
         hipLaunchKernelGGL(tdse_snap_kernel, dim3((int)std::min<size_t>(((size_t)B * N + 255) / 256, 4096)), dim3(256),
                            0, st, (const c128*)psi, B, N, nsave, idx, snap);
@@ -351,10 +363,37 @@ extern "C" int qd_tdse_driven_rk4(const qd_c128* H0, const qd_c128* Hd, int nd, 
                                   int B, int N, double dt, int nblocks, int nout, qd_c128* snap, const qd_c128* E,
                                   int ne, qd_c128* obs, void* stream) {
   QD_CHECK_ARG(H0 && psi && (nd == 0 || (Hd && fvals)), "qd_tdse_driven_rk4: null pointer");
-  QD_CHECK_ARG(N >= 1 && N <= TD_MAXN && B >= 1 && nblocks >= 0 && nout >= 1 && nd >= 0 && nd <= 16,
+  QD_CHECK_ARG(N >= 1 && B >= 1 && nblocks >= 0 && nout >= 1 && nd >= 0 && nd <= 16,
                "qd_tdse_driven_rk4: bad sizes N=%d B=%d nblocks=%d nout=%d nd=%d", N, B, nblocks, nout, nd);
   QD_CHECK_ARG(ne >= 0 && (ne == 0 || (E && obs)), "qd_tdse_driven_rk4: E/obs null but ne=%d", ne);
   hipStream_t st = (hipStream_t)stream;
+  bool rows = true;  // row-parallel path as qd_tdse_rk4 (QD_TDSE_ROWS=0: persistent kernel, N <= 2048)
+  if (const char* e = std::getenv("QD_TDSE_ROWS")) rows = N > TD_MAXN || std::atoi(e) != 0;
+  if (rows) {
+    const size_t NN = (size_t)N * N, fl = (size_t)nblocks * nd;
+    void* w = nullptr;
+    int rc = workspace(WS_TDSE_H, (NN + fl) * sizeof(c128), &w);  // H(t) + drive values (WS_MISC: the row path)
+    if (rc) return rc;
+    c128* Ht = (c128*)w;
+    c128* fdev = Ht + NN;
+    if (fl) QD_HIP(hipMemcpyAsync(fdev, fvals, fl * sizeof(c128), hipMemcpyHostToDevice, st));
+    const int blocks = (int)std::min<size_t>((NN + 255) / 256, 4096);
+    if (nblocks == 0) {  // observables at t0 only
+      return tdse_rows_run((const c128*)H0, (c128*)psi, B, N, dt, 0, nout, nullptr, (const c128*)E, ne,
+                           ne ? (c128*)obs : nullptr, st, 0, 0);
+    }
+    // H constant within a block of nout steps (mol.py:1944-1951 evaluates calcH(t) once per block)
+    for (int k = 0; k < nblocks; ++k) {
+      hipLaunchKernelGGL(tdse_driven_h_kernel, dim3(blocks), dim3(256), 0, st, (const c128*)H0, (const c128*)Hd, nd,
+                         (const c128*)fdev + (size_t)k * nd, N, Ht);
+      QD_HIP(hipGetLastError());
+      if ((rc = tdse_rows_run(Ht, (c128*)psi, B, N, dt, nout, nout, (c128*)snap, (const c128*)E, ne,
+                              ne ? (c128*)obs : nullptr, st, k, nblocks)))
+        return rc;
+    }
+    return QD_OK;
+  }
+  QD_CHECK_ARG(N <= TD_MAXN, "qd_tdse_driven_rk4: N=%d > %d on the persistent kernel", N, TD_MAXN);
   const size_t NN = (size_t)N * N;
   const size_t fl = (size_t)nblocks * nd;
   void* w = nullptr;
