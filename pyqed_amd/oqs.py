@@ -334,6 +334,20 @@ def _redfield(R, rho0, evecs=None, Nt=1, dt=0.005, t0=0, e_ops=[], return_result
             basis_transform(ev, Ed, inverse=False)
     W = Ed.transpose(1, 2).reshape(len(e_ops), N * N).contiguous() if Ed is not None else None  # vec(E^T)
     v = rho.reshape(1, N * N).contiguous()
+    if return_result is False:
+        # oqs.py:406-431: 'obs.dat' gets one line per step, "t" after the increment followed by the
+        # observables of the state BEFORE the step, and the final vec(rho) (eigenbasis) is returned.  The
+        # reference evaluates obs_dm(vec(rho), e) = e.dot(vec).diagonal(), which fails for any e_op (an
+        # N x N operator against an N^2 vector); that failure is reproduced, so only empty e_ops run.
+        if len(e_ops):
+            raise ValueError(f"shapes ({N},{N}) and ({N * N},) not aligned: {N} (dim 1) != {N * N} (dim 0)")
+        superop_rk4(Rd, v, dt, Nt, None, save_every=0)
+        t = t0
+        with open('obs.dat', 'w') as f_obs:
+            for _ in range(Nt):
+                t += dt
+                f_obs.write('{} \n'.format(t))
+        return v[0].cpu().numpy()
     rho0_eb = rho[0].cpu().numpy()
     obs, snap = superop_rk4(Rd, v, dt, Nt, W, save_every=1)
     result = Result(dt=dt, Nt=Nt, rho0=rho0_eb)
