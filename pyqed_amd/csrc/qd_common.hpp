@@ -43,7 +43,7 @@ void set_error(const char* fmt, ...);
 // Never handed to the caller.  Slot ids keep independent users apart.
 enum WsSlot { WS_LINDBLAD = 0, WS_LINDBLAD_OPS = 1, WS_SPO = 2, WS_DEOM = 3,
               WS_SUPEROP = 4, WS_2DES = 5, WS_MISC = 6, WS_2DES_OPS = 7, WS_TDSE_H = 8,
-              WS_NSLOTS = 9 };
+              WS_TDSE_GEMM = 9, WS_NSLOTS = 10 };
 int workspace(WsSlot slot, size_t bytes, void** ptr);
 void free_workspaces();
 
@@ -80,5 +80,10 @@ template <int CTRL>
 __device__ __forceinline__ int dpp_qi(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false); }
 
 inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
+
+// Split-K complex fp64 MFMA GEMM (response.hip): slabs[s] = A [Mp][Kp] x B [Kp][Np] over K slice s, S <= max_S
+// slices (returned); Mp, Np multiples of 128, Kp of 16.
+int cgemm_splitk_slabs(const c128* A, const c128* B, int Mp, int Kp, int Np, c128* slabs, int max_S, int* S_out,
+                       hipStream_t st);
 
 }  // namespace qd

@@ -991,6 +991,20 @@ int splits_for(int Mp, int Np, int Kp) {
 }
 }  // namespace
 
+// Split-K complex GEMM for other translation units (TDSE batches): partial products of A [Mp][Kp] * B [Kp][Np]
+// (row-major, Mp and Np multiples of 128, Kp of 16) into S slabs [S][Mp][Np]; S is returned through *S_out
+// (<= max_S).  The caller sums the slabs in order s = 0 .. S-1.
+int qd::cgemm_splitk_slabs(const c128* A, const c128* B, int Mp, int Kp, int Np, c128* slabs, int max_S, int* S_out,
+                           hipStream_t st) {
+  QD_CHECK_ARG(Mp % 128 == 0 && Np % 128 == 0 && Kp % CG_KT == 0, "cgemm_splitk_slabs: bad padding");
+  SplitPlan pl = split_plan(Mp, Np, Kp / CG_KT);
+  pl.S = std::min(pl.S, max_S);
+  launch_ens_gemm(pl, A, Kp, B, Mp, Np, Kp / CG_KT, slabs, st);
+  QD_HIP(hipGetLastError());
+  *S_out = pl.S;
+  return QD_OK;
+}
+
 extern "C" int qd_resolvent_grid2d(const qd_c128* a, const qd_c128* M, const qd_c128* v, const qd_c128* lam, int n,
                                    const double* wx, int nx, const double* wy, int ny, qd_c128* out, void* stream) {
   const char* fn = "qd_resolvent_grid2d";

@@ -12,6 +12,7 @@
 #include "qd_common.hpp"
 
 #include <cstdlib>
+#include <functional>
 
 namespace qd {
 namespace {
@@ -278,8 +279,58 @@ __global__ void tdse_snap_kernel(const c128* psi, int B, int N, int nsave, int i
     snap[((e / N) * nsave + idx - 1) * N + e % N] = psi[e];
 }
 
+// ---- batches at larger N: one stage is the GEMM K^T = X^T (-iH)^T ([Bp][Np] x [Np][Np], the split-K MFMA
+// engine of the 2DES grids), which reads H once per stage for the whole batch instead of once per
+// wavefunction; the slab sum and the RK4 update are one elementwise kernel.  All state in padded [Bp][Np]
+// buffers (padding stays zero: zero rows of X, zero columns of (-iH)^T).
+__global__ void tdse_pad_h_kernel(const c128* H, int N, int Np, c128* mHTp) {
+  const size_t tot = (size_t)Np * Np;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    const int j = (int)(e / Np), r = (int)(e % Np);
+    mHTp[e] = (j < N && r < N) ? cmulmi(H[(size_t)r * N + j]) : cmk(0, 0);   // (-iH)^T [j][r]
+  }
+}
+
+// dir 0: pad psi [B][N] -> P [Bp][Np]; dir 1: unpad P -> psi
+__global__ void tdse_pad_psi_kernel(c128* psi, int B, int N, int Bp, int Np, c128* P, int dir) {
+  const size_t tot = (size_t)Bp * Np;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    const int b = (int)(e / Np), r = (int)(e % Np);
+    const bool in = b < B && r < N;
+    if (dir == 0) P[e] = in ? psi[(size_t)b * N + r] : cmk(0, 0);
+    else if (in) psi[(size_t)b * N + r] = P[e];
+  }
+}
+
+// k = sum_s slabs[s] (fixed order), then the RK4 update of every padded element
+__global__ void tdse_gemm_rk4_kernel(const c128* slabs, int S, size_t tot, c128* P, c128* x0, c128* x1, c128* acc,
+                                     double dt, int stage) {
+  const double dt2 = dt / 2.0;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    c128 k = slabs[e];
+    for (int q = 1; q < S; ++q) k = cadd(k, slabs[(size_t)q * tot + e]);
+    const c128 p = P[e];
+    if (stage == 0) {
+      acc[e] = k;
+      x0[e] = cadd(p, cscale(k, dt2));
+    } else if (stage == 1) {
+      acc[e] = cadd(acc[e], cscale(k, 2.0));
+      x1[e] = cadd(p, cscale(k, dt2));
+    } else if (stage == 2) {
+      acc[e] = cadd(acc[e], cscale(k, 2.0));
+      x0[e] = cadd(p, cscale(k, dt));
+    } else {
+      const c128 a = cadd(acc[e], k);
+      P[e] = cadd(p, cscale(cscale(a, 1.0 / 6.0), dt));
+    }
+  }
+}
+
 // save0 / nsave_total: this launch's first save index and the run's number of saves (driven runs call it once
 // per block of save_every steps, like the persistent kernel); obs row 0 (t0) only when save0 == 0.
+int tdse_gemm_steps(const c128* H, c128* psi, int B, int N, double dt, int nsteps, hipStream_t st, int save_every,
+                    const std::function<int(int)>& at_step);
+
 int tdse_rows_run(const c128* H, c128* psi, int B, int N, double dt, int nsteps, int save_every, c128* snap,
                   const c128* E, int ne, c128* obs, hipStream_t st, int save0 = 0, int nsave_total = -1) {
   const int nsave = nsave_total >= 0 ? nsave_total : (save_every > 0 ? nsteps / save_every : 0);
@@ -303,6 +354,24 @@ int tdse_rows_run(const c128* H, c128* psi, int B, int N, double dt, int nsteps,
   };
   QD_CHECK_ARG((size_t)B * (ne ? ne : 1) <= 65535, "qd_tdse_rk4: B * ne too large for the row path");
   if (save0 == 0 && (rc = observe(0))) return rc;
+  auto save = [&](int s) -> int {  // after step s (0-based), psi [B][N] current
+    if (save_every > 0 && (s + 1) % save_every == 0) {
+      const int idx = save0 + (s + 1) / save_every;
+      if (snap) {
+        hipLaunchKernelGGL(tdse_snap_kernel, dim3((int)std::min<size_t>(((size_t)B * N + 255) / 256, 4096)), dim3(256),
+                           0, st, (const c128*)psi, B, N, nsave, idx, snap);
+        QD_HIP(hipGetLastError());
+      }
+      return observe(idx);
+    }
+    return QD_OK;
+  };
+  // batches: MFMA GEMM stages where they win (tools/tdse_bench.py, wavefunction-steps/s, rows -> GEMM:
+  // N = 1024, B = 64: 230k -> 523k; N = 2048, B = 256: 31k -> 427k; N = 256, B = 64: 1.77M -> 1.08M, B = 256:
+  // 2.42M -> 4.06M); QD_TDSE_GEMM=0 keeps the row kernel
+  const char* ge = std::getenv("QD_TDSE_GEMM");
+  if (((B >= 64 && N >= 512) || (B >= 128 && N >= 256)) && !(ge && ge[0] == '0'))
+    return tdse_gemm_steps(H, psi, B, N, dt, nsteps, st, save_every, save);
   for (int s = 0; s < nsteps; ++s) {
     for (int stage = 0; stage < 4; ++stage) {
       hipLaunchKernelGGL(tdse_row_stage_kernel<1>, rows, dim3(256), 0, st, H, psi, ws, N, B, dt, stage);
@@ -318,6 +387,44 @@ int tdse_rows_run(const c128* H, c128* psi, int B, int N, double dt, int nsteps,
       if ((rc = observe(idx))) return rc;
     }
   }
+  return QD_OK;
+}
+
+int tdse_gemm_steps(const c128* H, c128* psi, int B, int N, double dt, int nsteps, hipStream_t st, int save_every,
+                    const std::function<int(int)>& at_step) {
+  const int Bp = ceil_div(B, 128) * 128, Np = ceil_div(N, 128) * 128;
+  const size_t NN = (size_t)Np * Np, BN = (size_t)Bp * Np;
+  constexpr int MAXS = 16;
+  void* w = nullptr;
+  int rc = workspace(WS_TDSE_GEMM, (NN + 4 * BN + (size_t)MAXS * BN) * sizeof(c128), &w);
+  if (rc) return rc;
+  c128* mHTp = (c128*)w;
+  c128* P = mHTp + NN;
+  c128* x0 = P + BN;
+  c128* x1 = x0 + BN;
+  c128* acc = x1 + BN;
+  c128* slabs = acc + BN;
+  const int g1 = (int)std::min<size_t>((NN + 255) / 256, 8192), g2 = (int)std::min<size_t>((BN + 255) / 256, 8192);
+  hipLaunchKernelGGL(tdse_pad_h_kernel, dim3(g1), dim3(256), 0, st, H, N, Np, mHTp);
+  hipLaunchKernelGGL(tdse_pad_psi_kernel, dim3(g2), dim3(256), 0, st, psi, B, N, Bp, Np, P, 0);
+  QD_HIP(hipGetLastError());
+  for (int s = 0; s < nsteps; ++s) {
+    for (int stage = 0; stage < 4; ++stage) {
+      const c128* xin = stage == 0 ? P : ((stage & 1) ? x0 : x1);   // stage 1: x0, 2: x1, 3: x0
+      int S = 1;
+      if ((rc = cgemm_splitk_slabs(xin, mHTp, Bp, Np, Np, slabs, MAXS, &S, st))) return rc;
+      hipLaunchKernelGGL(tdse_gemm_rk4_kernel, dim3(g2), dim3(256), 0, st, (const c128*)slabs, S, BN, P, x0, x1, acc,
+                         dt, stage);
+      QD_HIP(hipGetLastError());
+    }
+    if (save_every > 0 && (s + 1) % save_every == 0) {  // saves read psi [B][N]: unpad first
+      hipLaunchKernelGGL(tdse_pad_psi_kernel, dim3(g2), dim3(256), 0, st, psi, B, N, Bp, Np, P, 1);
+      QD_HIP(hipGetLastError());
+      if ((rc = at_step(s))) return rc;
+    }
+  }
+  hipLaunchKernelGGL(tdse_pad_psi_kernel, dim3(g2), dim3(256), 0, st, psi, B, N, Bp, Np, P, 1);
+  QD_HIP(hipGetLastError());
   return QD_OK;
 }
 

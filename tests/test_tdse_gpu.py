@@ -103,11 +103,12 @@ def test_driven_batch_vs_oracle():
         assert relerr(snap[b].cpu().numpy(), psit[:, 1:].T) < TOL
 
 
-@pytest.mark.parametrize("N,B,save_every", [(300, 1, 2), (2500, 2, 3), (1024, 64, 5)])
+@pytest.mark.parametrize("N,B,save_every", [(300, 1, 2), (2500, 2, 3), (1024, 64, 5), (600, 130, 2)])
 def test_tdse_row_path_vs_persistent_and_oracle(N, B, save_every, monkeypatch):
-    """Row-parallel TDSE path (a wave per row and stage launch; default for small batches, the only path past
-    N = 2048): snapshots and observables (E_m = H, diag) against the persistent kernel (N <= 2048) and the
-    oracle's RK4 (oracle.tdse.quantum_dynamics restates mol.py:1603-1691)."""
+    """Row-parallel TDSE path (a wave per row and stage launch; the only path past N = 2048) and, for batches of
+    >= 32 at N >= 256, the MFMA GEMM stages (padded [Bp][Np] state, split-K slabs): snapshots and observables
+    (E_m = H, diag) against the persistent kernel (N <= 2048) and the oracle's RK4 (oracle.tdse restates
+    mol.py:1603-1691); B = 64 / 130 and N = 600 exercise the GEMM's padding to multiples of 128."""
     import torch
     from oracle import tdse as otd
     from pyqed_amd.mol import tdse_rk4
