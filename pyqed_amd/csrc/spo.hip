@@ -342,10 +342,10 @@ __global__ __launch_bounds__(C * NS * L / 4 < 64 ? 64 : C * NS * L / 4) void spo
 // Middle-axis pass of a 3D grid psi [nx][ny][nz][ns] viewed as [outer][L][inner]
 // (inner = nz*ns): each workgroup transforms C consecutive inner indices of one
 // outer index i along the L axis (chunks of C*16 B per row: coalesced).
-template <int L, bool INV>
-__global__ __launch_bounds__(256) void spo_mid_kernel(c128* psi, const c128* tw_g, int inner, int C) {
+template <int L, int C, bool INV>
+__global__ __launch_bounds__(256) void spo_mid_kernel(c128* psi, const c128* tw_g, int inner) {
   __shared__ c128 tw[L];
-  __shared__ c128 A[1024], Bf[1024];  // layout [c][j], C * L <= 1024
+  __shared__ c128 A[C * L], Bf[C * L];  // layout [c][j]; LDS sized to the C transforms of this block
   const int chunks = inner / C;
   const int i = blockIdx.x / chunks, c0 = (blockIdx.x % chunks) * C;
   c128* base = psi + (size_t)i * L * inner + c0;
@@ -1005,7 +1005,46 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
     QD_HIP(hipGetLastError());
     return QD_OK;
   };
+  // Mid pass: C consecutive inner indices (C * 16 B per row read) per block. C is the largest of
+  // 16 / 8 / 4 that still gives >= 4 blocks per CU (on its own worth ~1% at 64^3 x 2: 512 -> 1024
+  // blocks; C = 4 costs 13% at 128^3); QD_SPO3_MID_C overrides it for sweeps.
+  int midC = 4;
+  for (int c : {16, 8}) {
+    if (c * ny <= 1024 && inner % c == 0 && (size_t)nx * (inner / c) >= 1024) { midC = c; break; }
+  }
+  if (const char* e = getenv("QD_SPO3_MID_C")) {
+    const int c = atoi(e);
+    if ((c == 4 || c == 8 || c == 16) && c * ny <= 1024 && inner % c == 0) midC = c;
+  }
+  while (midC > 1 && inner % midC) midC >>= 1;  // inner = nz * ns >= 16 keeps midC >= 4
+  // x pass: the latency-shaped two-column kernel (colC = 0), or the LDS-staged kernel over colC
+  // columns x ns states per block (colC * ns * 16 B contiguous per row); QD_SPO3_COL_C overrides
+  // (0 = two-column kernel) for sweeps (tools/spo3_midc_sweep.sh).
+  // Default: at <= 64^3 x 2 points the LDS-staged kernel with the mid pass's row width
+  // (colC * ns == midC, 128 B rows at 64^3 x 2: 41.1 -> 33.4 us per step); above that the
+  // two-column kernel (128^3 x 2: 142 us either way, 146 us with colC * ns == midC).
+  int colC = 0;
+  if (nk * ns <= (size_t)1 << 19 && midC % ns == 0) {
+    const int c = midC / ns;
+    if ((c == 2 || c == 4 || c == 8) && nyz % c == 0 && c * ns * (nx / 4) <= 256) colC = c;
+  }
+  if (const char* e = getenv("QD_SPO3_COL_C")) {
+    const int c = atoi(e);
+    if (c == 0 || ((c == 2 || c == 4 || c == 8) && nyz % c == 0 && c * ns * (nx / 4) <= 256)) colC = c;
+  }
   auto col = [&]() -> int {
+    if (colC) {
+      const int threads = std::max(64, colC * ns * (nx / 4));
+      const size_t lds = (size_t)(nx + 2 * colC * ns * nx) * sizeof(c128);
+#define COLCALLC(L)                                                                                                   \
+  if (colC == 2) hipLaunchKernelGGL((spo2_col_kernel<L, 2>), dim3(nyz / 2), dim3(threads), lds, st, psi, expKT, twx, nyz, ns); \
+  else if (colC == 4) hipLaunchKernelGGL((spo2_col_kernel<L, 4>), dim3(nyz / 4), dim3(threads), lds, st, psi, expKT, twx, nyz, ns); \
+  else hipLaunchKernelGGL((spo2_col_kernel<L, 8>), dim3(nyz / 8), dim3(threads), lds, st, psi, expKT, twx, nyz, ns)
+      QD_FFT_DISPATCH(nx, COLCALLC)
+#undef COLCALLC
+      QD_HIP(hipGetLastError());
+      return QD_OK;
+    }
     if (fast) return col_fast(nx, ns, nyz, psi, expKT, twx, st);
 #define COLCALL3(L) \
   hipLaunchKernelGGL((spo2_col_kernel<L, 2>), dim3(nyz / 2), dim3(col_threads), col_lds, st, psi, expKT, twx, nyz, ns)
@@ -1015,22 +1054,24 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
     return QD_OK;
   };
   auto mid = [&](bool inv) -> int {
-    // C = 1024 / ny transforms of ny/4 threads = 256 threads; needs inner % C == 0
-    int C = 1024 / ny;  // transforms per workgroup (C * ny/4 = 256 threads)
-    while (C > 1 && inner % C) C >>= 1;
-    const int grid = nx * (inner / C);
-    const int threads = std::max(64, C * (ny / 4));
-#define MIDCALL(L)                                                                                              \
-  if (inv) hipLaunchKernelGGL((spo_mid_kernel<L, true>), dim3(grid), dim3(threads), 0, st, psi, twy, inner, C); \
-  else hipLaunchKernelGGL((spo_mid_kernel<L, false>), dim3(grid), dim3(threads), 0, st, psi, twy, inner, C)
+    const int grid = nx * (inner / midC);
+    const int threads = std::max(64, midC * (ny / 4));
+#define MIDCALL_C(L, C)                                                                                      \
+  if (inv) hipLaunchKernelGGL((spo_mid_kernel<L, C, true>), dim3(grid), dim3(threads), 0, st, psi, twy, inner); \
+  else hipLaunchKernelGGL((spo_mid_kernel<L, C, false>), dim3(grid), dim3(threads), 0, st, psi, twy, inner)
+#define MIDCALL(L)                   \
+  if (midC == 16) { MIDCALL_C(L, 16); } \
+  else if (midC == 8) { MIDCALL_C(L, 8); } \
+  else { MIDCALL_C(L, 4); }
     switch (ny) {
       case 16: MIDCALL(16); break;
       case 32: MIDCALL(32); break;
       case 64: MIDCALL(64); break;
-      case 128: MIDCALL(128); break;
-      case 256: MIDCALL(256); break;
+      case 128: if (midC >= 8) { MIDCALL_C(128, 8); } else { MIDCALL_C(128, 4); } break;
+      case 256: { MIDCALL_C(256, 4); } break;
     }
 #undef MIDCALL
+#undef MIDCALL_C
     QD_HIP(hipGetLastError());
     return QD_OK;
   };

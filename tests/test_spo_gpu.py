@@ -124,8 +124,14 @@ def test_spo3_matches_reference():
     assert relerr(r.psi, g["psi"]) < TOL
 
 
-def test_spo3_example_size_vs_oracle():
-    """examples/spo.py size: 64^3 x 2, vs the NumPy fftn restatement, and norm conservation."""
+@pytest.mark.parametrize("mid_c,col_c", [(None, None), ("4", "2"), ("8", "4"), ("16", "8"), ("8", None), (None, "0")])
+def test_spo3_example_size_vs_oracle(mid_c, col_c, monkeypatch):
+    """examples/spo.py size: 64^3 x 2, vs the NumPy fftn restatement, and norm conservation; every
+    mid-axis and x-axis block width (QD_SPO3_MID_C / QD_SPO3_COL_C; None = the default launch)."""
+    if mid_c is not None:
+        monkeypatch.setenv("QD_SPO3_MID_C", mid_c)
+    if col_c is not None:
+        monkeypatch.setenv("QD_SPO3_COL_C", col_c)
     from oracle import spo as ospo
     from pyqed_amd.wpd import SPO3
     x, X, Y, Z, psi0 = _spo3_model(64)
