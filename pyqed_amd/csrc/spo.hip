@@ -1020,11 +1020,11 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
   // x pass: the latency-shaped two-column kernel (colC = 0), or the LDS-staged kernel over colC
   // columns x ns states per block (colC * ns * 16 B contiguous per row); QD_SPO3_COL_C overrides
   // (0 = two-column kernel) for sweeps (tools/spo3_midc_sweep.sh).
-  // Default: at <= 64^3 x 2 points the LDS-staged kernel with the mid pass's row width
+  // Default: at <= 64^3 x 2 points and midC >= 8 the LDS-staged kernel with the mid pass's row width
   // (colC * ns == midC, 128 B rows at 64^3 x 2: 41.1 -> 33.4 us per step); above that the
   // two-column kernel (128^3 x 2: 142 us either way, 146 us with colC * ns == midC).
   int colC = 0;
-  if (nk * ns <= (size_t)1 << 19 && midC % ns == 0) {
+  if (nk * ns <= (size_t)1 << 19 && midC >= 8 && midC % ns == 0) {  // 32^3 x 2 (midC = 4): 15.4 vs 16.6 us
     const int c = midC / ns;
     if ((c == 2 || c == 4 || c == 8) && nyz % c == 0 && c * ns * (nx / 4) <= 256) colC = c;
   }

@@ -12,7 +12,7 @@ from pyqed_amd import _lib  # noqa: E402
 from pyqed_amd.wpd import SPO3  # noqa: E402
 
 dev = torch.device("cuda", 0)
-for n in (64, 128):
+for n in [int(v) for v in os.environ.get("SPO3_SIZES", "64,128").split(",")]:
     x = np.linspace(-6, 6, n)
     X, Y, Z = np.meshgrid(x, x, x, indexing="ij")
     sol = SPO3(x, x, x, masses=[1.0, 1.0, 1.0], nstates=2)
