@@ -387,7 +387,7 @@ int deom_run(qd_c128* ados, int B, int nmax, int K, int ns, const int32_t* minus
   const bool need_snap = rho_sys || trace;
   const size_t snap_elems = need_snap && !rho_sys ? (size_t)B * (nsteps + 1) * ns2 : 0;
   void* w = nullptr;
-  int rc = workspace(WS_DEOM, (3 * tot + snap_elems) * sizeof(c128), &w);
+  int rc = workspace(WS_DEOM, (3 * tot + snap_elems) * sizeof(c128), &w, st);
   if (rc) return rc;
   c128* acc = (c128*)w;
   c128* xs[2] = {acc + tot, acc + 2 * tot};
@@ -509,7 +509,7 @@ extern "C" int qd_heom_chain_euler(qd_c128* ados, int B, int nado, int ns, const
   c128* snap = (c128*)rho_sys;
   if (!snap && obs) {
     void* w = nullptr;
-    int rc = workspace(WS_DEOM, (size_t)B * (nsteps + 1) * ns2 * sizeof(c128), &w);
+    int rc = workspace(WS_DEOM, (size_t)B * (nsteps + 1) * ns2 * sizeof(c128), &w, st);
     if (rc) return rc;
     snap = (c128*)w;
   }

@@ -155,7 +155,7 @@ extern "C" int qd_fft_axis(qd_c128* data, int outer, int n, int inner, int inver
   QD_CHECK_ARG(pow2 || n <= 3200, "qd_fft_axis: n=%d: powers of two up to 1024 or any n up to 3200", n);
   if (pow2) {
     void* w = nullptr;
-    int rc = workspace(WS_MISC, n * sizeof(c128), &w);
+    int rc = workspace(WS_MISC, n * sizeof(c128), &w, st);
     if (rc) return rc;
     hipLaunchKernelGGL(twiddles_kernel, dim3((n + 255) / 256), dim3(256), 0, st, n, (c128*)w);
     QD_HIP(hipGetLastError());

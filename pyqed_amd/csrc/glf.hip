@@ -40,7 +40,7 @@ constexpr int MAX_NE = 16;
 struct LindbladParams {
   const c128* Cop;  // [nc][Np][Np]  L_c   (Lindblad: C_c)
   const c128* mK;   // [Np][Np]      P     (Lindblad: -iK)
-  const c128* iKd;  // [Np][Np]      Q     (Lindblad: iK^+)
+  const c128* iKd;  // [Np][Np]      Q     (Lindblad: iH - S/2)
   const c128* Cd;   // [nc][Np][Np]  R_c   (Lindblad: C_c^+)
   const c128* eT;   // [ne][Np][Np]  E_m^T
   c128* rho;        // [B][Np][Np]   state (in/out)
@@ -347,25 +347,29 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
 }
 
 // ---------------------------------------------------------------- operator prep
-// K = H - (i/2) sum_c C_c^+ C_c ; writes -iK, iK^+ (transposed), padded C, C^+, E^T.
+// S = sum_c C_c^+ C_c, K = H - (i/2) S.  Writes P = -iK, Q = iH - S/2 = i(H + (i/2) S), padded C, C^+, E^T,
+// so that P rho + rho Q + sum_c C rho C^+ is oqs.liouvillian (oqs.py:697-714) term by term:
+// -i(H rho - rho H) - (1/2)(S rho + rho S) + sum_c C rho C^+.  Q is formed from H itself (not from K^+), so
+// a non-Hermitian H gives the reference's -i[H, rho] exactly.
 __global__ void lindblad_prep_kernel(const c128* H, const c128* C, int nc, const c128* E, int ne, int N, int Np,
                                      c128* Cop, c128* mK, c128* iKd, c128* Cd, c128* eT) {
   const size_t NN = (size_t)Np * Np;
   for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < NN; e += (size_t)gridDim.x * blockDim.x) {
     const int i = (int)(e / Np), j = (int)(e % Np);
     const bool in = (i < N) && (j < N);
-    c128 K = cmk(0, 0);
+    c128 K = cmk(0, 0), Qv = cmk(0, 0);
     if (in) {
-      K = H[(size_t)i * N + j];
+      const c128 h = H[(size_t)i * N + j];
       c128 s = cmk(0, 0);
       for (int c = 0; c < nc; ++c) {
         const c128* Cc = C + (size_t)c * N * N;
         for (int k = 0; k < N; ++k) s = cadd(s, cmul(cconj(Cc[(size_t)k * N + i]), Cc[(size_t)k * N + j]));
       }
-      K = csub(K, cmuli(cscale(s, 0.5)));  // K - (i/2) s
+      K = csub(h, cmuli(cscale(s, 0.5)));    // H - (i/2) S
+      Qv = csub(cmuli(h), cscale(s, 0.5));   // iH - S/2
     }
-    mK[e] = cmulmi(K);                             // (-iK)[i][j]
-    iKd[(size_t)j * Np + i] = cmuli(cconj(K));     // (iK^+)[j][i] = i conj(K[i][j])
+    mK[e] = cmulmi(K);  // P[i][j] = (-iK)[i][j]
+    iKd[e] = Qv;        // Q[i][j]
     for (int c = 0; c < nc; ++c) {
       const c128 v = in ? C[(size_t)c * N * N + (size_t)i * N + j] : cmk(0, 0);
       Cop[c * NN + e] = v;
@@ -501,6 +505,17 @@ __device__ __forceinline__ c128* split_buf(const LindbladParams& p, int b, int w
 // `sc1`), drained (vmcnt(0)) before the workgroup barrier and the ticket, and every slab load of the last
 // arriver an agent-scope relaxed atomic load (`sc1`).  (Plain stores + __threadfence() per thread measured
 // 1.5-2x slower than no split at all: each release fence writes back the L2.)
+// Invariant this relies on (MI355X_MICROARCH.md "Valid forms", hand-off table row 1 -- the sc1 form that
+// replaces an agent release/acquire pair; keep ALL of these when editing):
+//   (1) every store of a slab is slab_st (agent-scope atomic store = global_store ... sc1, write-through);
+//   (2) every load of a slab by the last arriver is slab_ld (agent-scope atomic load = global_load ... sc1),
+//       never a plain or flat load, so no stale L1/L2 line can serve it;
+//   (3) every storing wave drains its stores (s_waitcnt vmcnt(0)) before the workgroup barrier, and ONE lane
+//       takes the ticket behind that barrier for all the workgroup's stores;
+//   (4) the consumer is the workgroup whose fetch_add returned S-1; its other waves load only after the second
+//       __syncthreads(), which they join after lane 0's add has returned.
+// __syncthreads() is also the compiler barrier that keeps the slab stores above, and the slab loads below, the
+// ticket; the asm's "memory" clobber keeps the stores above the drain.
 __device__ __forceinline__ void slab_st(c128* p, c128 v) {
   __hip_atomic_store(&p->re, v.re, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(&p->im, v.im, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -680,24 +695,27 @@ namespace {
 enum GlfSource { GLF_FROM_LINDBLAD = 0, GLF_FROM_OPERATORS = 1 };
 
 // Shared driver of qd_lindblad_rk4 / qd_glf_rk4.
-// K(t) = K0 - sum_d f_d Hd_d ; mK = -iK ; iKd = iK^+   (time-dependent Hamiltonian of
-// _lindblad_driven, oqs.py:1725-1732: H(t) = H0 - sum_i f_i(t) H_i, constant within a step)
-__global__ void driven_update_kernel(const c128* K0, const c128* Hd, int nd, const c128* f, int N, int Np, c128* mK,
-                                     c128* iKd) {
+// H(t) = H0 - sum_d f_d Hd_d (time-dependent Hamiltonian of _lindblad_driven, oqs.py:1725-1732, constant
+// within a step; f is complex, so H(t) need not be Hermitian):  P = P0 + i sum_d f_d Hd_d,
+// Q = Q0 - i sum_d f_d Hd_d, with P0 = -iK0 and Q0 = iH0 - S/2 saved at the start of the run.
+__global__ void driven_update_kernel(const c128* P0, const c128* Q0, const c128* Hd, int nd, const c128* f, int N,
+                                     int Np, c128* mK, c128* iKd) {
   const size_t NN = (size_t)Np * Np;
   for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < NN; e += (size_t)gridDim.x * blockDim.x) {
     const int i = (int)(e / Np), j = (int)(e % Np);
-    c128 K = K0[e];
+    c128 fh = cmk(0, 0);
     if (i < N && j < N)
-      for (int d = 0; d < nd; ++d) K = csub(K, cmul(f[d], Hd[(size_t)d * N * N + (size_t)i * N + j]));
-    mK[e] = cmulmi(K);
-    iKd[(size_t)j * Np + i] = cmuli(cconj(K));
+      for (int d = 0; d < nd; ++d) fh = cadd(fh, cmul(f[d], Hd[(size_t)d * N * N + (size_t)i * N + j]));
+    mK[e] = cadd(P0[e], cmuli(fh));
+    iKd[e] = csub(Q0[e], cmuli(fh));
   }
 }
 
-__global__ void save_k0_kernel(const c128* mK, size_t NN, c128* K0) {
-  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < NN; e += (size_t)gridDim.x * blockDim.x)
-    K0[e] = cmuli(mK[e]);  // K = i * (-iK)
+__global__ void save_pq0_kernel(const c128* mK, const c128* iKd, size_t NN, c128* P0, c128* Q0) {
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < NN; e += (size_t)gridDim.x * blockDim.x) {
+    P0[e] = mK[e];
+    Q0[e] = iKd[e];
+  }
 }
 
 __global__ void scale_kernel(c128* a, size_t n, double s) {
@@ -711,18 +729,19 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
             const qd_c128* fvals = nullptr, int herm = 0) {
   const int Np = padded_dim(N);
   const size_t NN = (size_t)Np * Np;
-  // operator workspace: Cop(L), mK(P), iKd(Q), Cd(R), eT, [K0, f scratch for driven runs]
-  const size_t ops_elems = (size_t)(2 + 2 * nc + ne + (nd ? 1 : 0)) * NN + (size_t)nd * nsteps;
+  // operator workspace: Cop(L), mK(P), iKd(Q), Cd(R), eT, [P0, Q0, f scratch for driven runs]
+  const size_t ops_elems = (size_t)(2 + 2 * nc + ne + (nd ? 2 : 0)) * NN + (size_t)nd * nsteps;
   void* wops = nullptr;
-  int rc = workspace(WS_LINDBLAD_OPS, ops_elems * sizeof(c128), &wops);
+  int rc = workspace(WS_LINDBLAD_OPS, ops_elems * sizeof(c128), &wops, st);
   if (rc) return rc;
   c128* Cop = (c128*)wops;
   c128* mK = Cop + (size_t)nc * NN;
   c128* iKd = mK + NN;
   c128* Cd = iKd + NN;
   c128* eT = Cd + (size_t)nc * NN;
-  c128* K0 = eT + (size_t)ne * NN;
-  c128* fdev = K0 + (nd ? NN : 0);
+  c128* P0 = eT + (size_t)ne * NN;
+  c128* Q0 = P0 + (nd ? NN : 0);
+  c128* fdev = Q0 + (nd ? NN : 0);
   // state workspace: per-matrix scratch (+ padded rho when N != Np)
   const bool pad = (Np != N);
   if (Np > 128) herm = 0;  // the Hermitian path is single-block
@@ -768,7 +787,7 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   const size_t nticket = split_bt ? (size_t)B * (1 + nc) * (Np / split_bt) * (Np / split_bt) : 0;
   const size_t st_elems = (size_t)B * per + (pad ? (size_t)B * NN : 0) + (nticket + 3) / 4;
   void* wst = nullptr;
-  rc = workspace(WS_LINDBLAD, st_elems * sizeof(c128), &wst);
+  rc = workspace(WS_LINDBLAD, st_elems * sizeof(c128), &wst, st);
   if (rc) return rc;
   c128* scratch = (c128*)wst;
   c128* rho_p = pad ? scratch + (size_t)B * per : rho;
@@ -787,7 +806,8 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
     QD_HIP(hipGetLastError());
   }
   if (nd) {
-    hipLaunchKernelGGL(save_k0_kernel, dim3(blocks), dim3(threads), 0, st, (const c128*)mK, NN, K0);
+    hipLaunchKernelGGL(save_pq0_kernel, dim3(blocks), dim3(threads), 0, st, (const c128*)mK, (const c128*)iKd, NN,
+                       P0, Q0);
     QD_HIP(hipGetLastError());
     if (nsteps > 0)
       QD_HIP(hipMemcpyAsync(fdev, fvals, (size_t)nd * nsteps * sizeof(c128), hipMemcpyHostToDevice, st));
@@ -895,7 +915,7 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
     // one launch per step: H(t_k) is constant within a step (oqs.py:1780-1786 evaluates it once per step)
     p.nsteps = 1;
     for (int k = 0; k < nsteps; ++k) {
-      hipLaunchKernelGGL(driven_update_kernel, dim3(blocks), dim3(threads), 0, st, (const c128*)K0, Hd, nd,
+      hipLaunchKernelGGL(driven_update_kernel, dim3(blocks), dim3(threads), 0, st, (const c128*)P0, (const c128*)Q0, Hd, nd,
                          (const c128*)fdev + (size_t)k * nd, N, Np, mK, iKd);
       QD_HIP(hipGetLastError());
       p.step0 = k;
@@ -1006,7 +1026,7 @@ int sandwich_run(const c128* V, const c128* Lm, const c128* Rm, c128* A, int B, 
   const size_t NN = (size_t)Np * Np;
   const bool pad = Np != N;
   void* w = nullptr;
-  int rc = workspace(WS_MISC, (2 * NN + (size_t)B * NN * (pad ? 2 : 1)) * sizeof(c128), &w);
+  int rc = workspace(WS_MISC, (2 * NN + (size_t)B * NN * (pad ? 2 : 1)) * sizeof(c128), &w, st);
   if (rc) return rc;
   c128* Vl = (c128*)w;
   c128* Vr = Vl + NN;

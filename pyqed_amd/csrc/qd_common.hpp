@@ -39,12 +39,16 @@ void set_error(const char* fmt, ...);
     }                                                                       \
   } while (0)
 
-// Per-device growable workspace, owned by the library (freed by qd_shutdown).
-// Never handed to the caller.  Slot ids keep independent users apart.
+// Growable scratch owned by the library (freed by qd_shutdown), never handed to the caller.
+// Keyed by (device, stream, slot): calls on distinct streams never share scratch, so the library is
+// re-entrant for distinct streams (SURVEY.md §8(b) threading contract).  Buffers are allocated and
+// released stream-ordered (hipMallocAsync / hipFreeAsync on `st`), so growing one stream's buffer
+// never waits on, or frees memory still queued on, any other stream.  Concurrent calls on the SAME
+// stream from different host threads are not supported (their scratch would alias).
 enum WsSlot { WS_LINDBLAD = 0, WS_LINDBLAD_OPS = 1, WS_SPO = 2, WS_DEOM = 3,
               WS_SUPEROP = 4, WS_2DES = 5, WS_MISC = 6, WS_2DES_OPS = 7, WS_TDSE_H = 8,
               WS_TDSE_GEMM = 9, WS_NSLOTS = 10 };
-int workspace(WsSlot slot, size_t bytes, void** ptr);
+int workspace(WsSlot slot, size_t bytes, void** ptr, hipStream_t st);
 void free_workspaces();
 
 // ---------------------------------------------------------------- complex

@@ -2,8 +2,9 @@
 // workspace cache of libqdyn.
 #include "qd_common.hpp"
 
+#include <map>
 #include <mutex>
-#include <vector>
+#include <tuple>
 
 namespace qd {
 
@@ -21,26 +22,25 @@ struct Workspace {
   size_t bytes = 0;
 };
 
+// (device, stream, slot) -> buffer.  See qd_common.hpp: distinct streams never share scratch.
 static std::mutex g_ws_mu;
-// [device][slot]
-static std::vector<std::vector<Workspace>> g_ws;
+static std::map<std::tuple<int, uintptr_t, int>, Workspace> g_ws;
 
-int workspace(WsSlot slot, size_t bytes, void** ptr) {
+int workspace(WsSlot slot, size_t bytes, void** ptr, hipStream_t st) {
   int dev = 0;
   QD_HIP(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(g_ws_mu);
-  if ((int)g_ws.size() <= dev) g_ws.resize(dev + 1, std::vector<Workspace>(WS_NSLOTS));
-  Workspace& w = g_ws[dev][slot];
+  Workspace& w = g_ws[std::make_tuple(dev, (uintptr_t)st, (int)slot)];
   if (w.bytes < bytes) {
     if (w.ptr) {
-      // the previous buffer may still be in use by queued work
-      QD_HIP(hipDeviceSynchronize());
-      QD_HIP(hipFree(w.ptr));
+      // stream-ordered release: runs after the work already queued on `st` that uses the buffer,
+      // without waiting for it here and without touching other streams
+      QD_HIP(hipFreeAsync(w.ptr, st));
       w.ptr = nullptr;
       w.bytes = 0;
     }
     size_t want = bytes + bytes / 8;  // grow geometrically-ish
-    hipError_t e = hipMalloc(&w.ptr, want);
+    hipError_t e = hipMallocAsync(&w.ptr, want, st);
     if (e != hipSuccess) {
       w.ptr = nullptr;
       set_error("workspace allocation of %zu bytes failed: %s", want, hipGetErrorString(e));
@@ -56,17 +56,16 @@ void free_workspaces() {
   std::lock_guard<std::mutex> lk(g_ws_mu);
   int cur = 0;
   (void)hipGetDevice(&cur);
-  for (size_t d = 0; d < g_ws.size(); ++d) {
-    for (auto& w : g_ws[d]) {
-      if (w.ptr) {
-        (void)hipSetDevice((int)d);
-        (void)hipDeviceSynchronize();
-        (void)hipFree(w.ptr);
-      }
-      w.ptr = nullptr;
-      w.bytes = 0;
+  for (auto& kv : g_ws) {
+    Workspace& w = kv.second;
+    if (w.ptr) {
+      // the owning stream may already be destroyed: wait for the device, then free
+      (void)hipSetDevice(std::get<0>(kv.first));
+      (void)hipDeviceSynchronize();
+      (void)hipFree(w.ptr);
     }
   }
+  g_ws.clear();
   (void)hipSetDevice(cur);
 }
 

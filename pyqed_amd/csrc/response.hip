@@ -704,7 +704,7 @@ extern "C" int qd_response_cube(const qd_c128* alpha, const qd_c128* B, const qd
   hipStream_t st = (hipStream_t)stream;
   void* w = nullptr;
   const size_t ny = (size_t)n1 * nL, nw = (size_t)n2 * nL * n1;
-  int rc = workspace(WS_2DES, (ny + nw) * sizeof(c128), &w);
+  int rc = workspace(WS_2DES, (ny + nw) * sizeof(c128), &w, st);
   if (rc) return rc;
   c128* Y = (c128*)w;
   c128* W = Y + ny;
@@ -745,7 +745,7 @@ int ens_run(const char* fn, const qd_c128* alpha, const qd_c128* Mt, const qd_c1
   const int S = plan.S;
   const size_t nXe = (size_t)n3p * Kp, nZe = (size_t)Kp * n1p, nsl = (size_t)S * n3p * n1p;
   void* w = nullptr;
-  int rc = workspace(WS_2DES, (nXe + nZe + nsl) * sizeof(c128), &w);
+  int rc = workspace(WS_2DES, (nXe + nZe + nsl) * sizeof(c128), &w, st);
   if (rc) return rc;
   c128* X = (c128*)w;
   c128* Z = X + nXe;
@@ -940,7 +940,7 @@ extern "C" int qd_response2d_t2_apply(const qd_c128* P, const qd_c128* Q, const 
   const int S = std::max(1, std::min(ceil_div(256, blocks2d), std::max(1, d.tiles / 4)));
   const size_t nE = (size_t)n2 * d.Kp, nsl = (size_t)S * d.n3p * ldz;
   void* w = nullptr;
-  int rc = workspace(WS_2DES, (nE + nsl) * sizeof(c128), &w);
+  int rc = workspace(WS_2DES, (nE + nsl) * sizeof(c128), &w, st);
   if (rc) return rc;
   c128* E = (c128*)w;
   c128* slabs = E + nE;
@@ -964,7 +964,7 @@ extern "C" int qd_response2d_t2scan(const qd_c128* alpha, const qd_c128* Bm, con
   QD_CHECK_ARG(M >= 1 && nL >= 1 && n3 >= 1 && n1 >= 1 && n2 >= 1, "%s: bad sizes", fn);
   const T2Dims d = t2_dims(M, nL, n3, n1);
   void* w = nullptr;
-  int rc = workspace(WS_2DES_OPS, ((size_t)d.n3p * d.Kp + (size_t)d.Kp * d.n1p) * sizeof(c128), &w);
+  int rc = workspace(WS_2DES_OPS, ((size_t)d.n3p * d.Kp + (size_t)d.Kp * d.n1p) * sizeof(c128), &w, (hipStream_t)stream);
   if (rc) return rc;
   qd_c128* P = (qd_c128*)w;
   qd_c128* Q = P + (size_t)d.n3p * d.Kp;
@@ -1018,7 +1018,7 @@ extern "C" int qd_resolvent_grid2d(const qd_c128* a, const qd_c128* M, const qd_
   const size_t nM = (size_t)np_ * np_, nZ = (size_t)np_ * nyp, nW = (size_t)np_ * nyp, nX = (size_t)nxp * np_;
   const size_t nsl = std::max((size_t)S1 * np_ * nyp, (size_t)S2 * nxp * nyp);
   void* w = nullptr;
-  int rc = workspace(WS_2DES, (nM + nZ + nW + nX + nsl) * sizeof(c128), &w);
+  int rc = workspace(WS_2DES, (nM + nZ + nW + nX + nsl) * sizeof(c128), &w, st);
   if (rc) return rc;
   c128* Mp = (c128*)w;
   c128* Z = Mp + nM;

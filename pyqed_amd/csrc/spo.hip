@@ -793,7 +793,7 @@ extern "C" int qd_spo2_run_ex(qd_c128* psi_, const qd_c128* expVh_, const qd_c12
   c128* snap = (c128*)snap_;
   void* w = nullptr;
   const size_t nkt = (size_t)nx * ny;
-  int rc = workspace(WS_SPO, (nkt + nx + ny) * sizeof(c128), &w);
+  int rc = workspace(WS_SPO, (nkt + nx + ny) * sizeof(c128), &w, st);
   if (rc) return rc;
   c128* expKT = (c128*)w;
   c128* twx = expKT + nkt;
@@ -891,7 +891,7 @@ extern "C" int qd_spo2_run_batch(qd_c128* psi_, int B, const qd_c128* expVh_, co
   c128* snap = (c128*)snap_;
   void* w = nullptr;
   const size_t nkt = (size_t)nx * ny;
-  int rc = workspace(WS_SPO, (nkt + nx + ny) * sizeof(c128), &w);
+  int rc = workspace(WS_SPO, (nkt + nx + ny) * sizeof(c128), &w, st);
   if (rc) return rc;
   c128* expKT = (c128*)w;
   c128* twx = expKT + nkt;
@@ -946,7 +946,7 @@ extern "C" int qd_spo1d_run(qd_c128* psi_, const qd_c128* expV_, const qd_c128* 
   QD_CHECK_ARG(B >= 1 && nt >= 0 && nout >= 1, "qd_spo1d_run: B=%d nt=%d nout=%d", B, nt, nout);
   hipStream_t st = (hipStream_t)stream;
   void* w = nullptr;
-  int rc = workspace(WS_MISC, nx * sizeof(c128), &w);
+  int rc = workspace(WS_MISC, nx * sizeof(c128), &w, st);
   if (rc) return rc;
   c128* tw = (c128*)w;
   if ((rc = twiddles(nx, st, tw))) return rc;
@@ -976,7 +976,7 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
   const int nyz = ny * nz;
   const size_t nk = (size_t)nx * nyz;
   void* w = nullptr;
-  int rc = workspace(WS_SPO, (nk + nx + ny + nz) * sizeof(c128), &w);
+  int rc = workspace(WS_SPO, (nk + nx + ny + nz) * sizeof(c128), &w, st);
   if (rc) return rc;
   c128* expKT = (c128*)w;
   c128* twx = expKT + nk;

@@ -129,7 +129,7 @@ extern "C" int qd_superop_rk4(const qd_c128* L_, qd_c128* v_, int B, int N2, dou
   c128* snap = (c128*)snap_;
   const size_t tot = (size_t)B * N2;
   void* w = nullptr;
-  int rc = workspace(WS_SUPEROP, 3 * tot * sizeof(c128), &w);
+  int rc = workspace(WS_SUPEROP, 3 * tot * sizeof(c128), &w, st);
   if (rc) return rc;
   c128* acc = (c128*)w;
   c128* xs[2] = {acc + tot, acc + 2 * tot};

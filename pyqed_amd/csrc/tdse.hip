@@ -336,7 +336,7 @@ int tdse_rows_run(const c128* H, c128* psi, int B, int N, double dt, int nsteps,
   const int nsave = nsave_total >= 0 ? nsave_total : (save_every > 0 ? nsteps / save_every : 0);
   void* w = nullptr;
   const size_t ws_elems = (size_t)B * 3 * N + (size_t)B * (ne ? ne : 0) * N;
-  int rc = workspace(WS_MISC, ws_elems * sizeof(c128), &w);
+  int rc = workspace(WS_MISC, ws_elems * sizeof(c128), &w, st);
   if (rc) return rc;
   c128* ws = (c128*)w;
   c128* part = ws + (size_t)B * 3 * N;
@@ -396,7 +396,7 @@ int tdse_gemm_steps(const c128* H, c128* psi, int B, int N, double dt, int nstep
   const size_t NN = (size_t)Np * Np, BN = (size_t)Bp * Np;
   constexpr int MAXS = 16;
   void* w = nullptr;
-  int rc = workspace(WS_TDSE_GEMM, (NN + 4 * BN + (size_t)MAXS * BN) * sizeof(c128), &w);
+  int rc = workspace(WS_TDSE_GEMM, (NN + 4 * BN + (size_t)MAXS * BN) * sizeof(c128), &w, st);
   if (rc) return rc;
   c128* mHTp = (c128*)w;
   c128* P = mHTp + NN;
@@ -452,7 +452,7 @@ extern "C" int qd_tdse_rk4(const qd_c128* H, qd_c128* psi, int B, int N, double 
                          ne ? (c128*)obs : nullptr, st);
   const size_t NN = (size_t)N * N;
   void* w = nullptr;
-  int rc = workspace(WS_MISC, (1 + ne) * NN * sizeof(c128), &w);
+  int rc = workspace(WS_MISC, (1 + ne) * NN * sizeof(c128), &w, st);
   if (rc) return rc;
   c128* mHT = (c128*)w;
   c128* ET = mHT + NN;
@@ -479,7 +479,7 @@ extern "C" int qd_tdse_driven_rk4(const qd_c128* H0, const qd_c128* Hd, int nd, 
   if (rows) {
     const size_t NN = (size_t)N * N, fl = (size_t)nblocks * nd;
     void* w = nullptr;
-    int rc = workspace(WS_TDSE_H, (NN + fl) * sizeof(c128), &w);  // H(t) + drive values (WS_MISC: the row path)
+    int rc = workspace(WS_TDSE_H, (NN + fl) * sizeof(c128), &w, st);  // H(t) + drive values (WS_MISC: the row path)
     if (rc) return rc;
     c128* Ht = (c128*)w;
     c128* fdev = Ht + NN;
@@ -504,7 +504,7 @@ extern "C" int qd_tdse_driven_rk4(const qd_c128* H0, const qd_c128* Hd, int nd, 
   const size_t NN = (size_t)N * N;
   const size_t fl = (size_t)nblocks * nd;
   void* w = nullptr;
-  int rc = workspace(WS_MISC, ((1 + ne) * NN + fl) * sizeof(c128), &w);
+  int rc = workspace(WS_MISC, ((1 + ne) * NN + fl) * sizeof(c128), &w, st);
   if (rc) return rc;
   c128* mHT = (c128*)w;
   c128* ET = mHT + NN;

@@ -42,7 +42,7 @@ def pade_approximation_distribution(N, BoseFermi=1, pade=1):
     if pade == 0:
         return matsubara_approximation_distribution(N, BoseFermi)
     if pade == 3:
-        raise NotImplementedError("pade=3 (extended PSD) is not implemented in pyqed_amd")
+        return _extended_psd(N, BoseFermi)
     if N == 0:
         return [], []
     M = 2 * N + pade // 2
@@ -64,6 +64,47 @@ def pade_approximation_distribution(N, BoseFermi=1, pade=1):
         num = np.prod([zeta2[k] - xi2[j] for k in range(nz)]) if nz else 1.0
         den = np.prod([xi2[k] - xi2[j] for k in range(N) if k != j]) if N > 1 else 1.0
         resi[j] = 0.5 * s * num / den
+    return xi, resi
+
+
+def _extended_psd(N, BoseFermi):
+    """Extended [N/N] Pade spectrum decomposition (pade=3; heom/deom.py:163-206; Hu, Xu, Yan, JCP 134,
+    244106 (2011)): the Bose/Fermi function as a continued fraction whose 2N+2 coefficients d_k are closed
+    forms in k.  Poles xi_j = 2 / eps_j from the N largest eigenvalues of the symmetric tridiagonal matrix with
+    off-diagonals 1/sqrt(d_{k+1} d_{k+2}), k < 2N; the residue at xi_j is the last term of the three-term
+    recurrence that evaluates the continued fraction's numerator at z^2 = xi_j^2, with the partial fractions
+    scaled so that the recurrence stays bounded (factor t_i / (xi_i^2 - xi_j^2), t_i the ratio of consecutive
+    partial sums of the odd coefficients)."""
+    a = 3.0 if BoseFermi == 1 else 1.0
+    n1 = N + 1
+    i = np.arange(1, n1, dtype=float)
+    d = np.empty(2 * n1)
+    d[0] = 0.25 / a
+    d[1:2 * n1 - 1:2] = -4.0 * i * i * (a + 2.0 * i - 2.0) ** 2 * (a + 4.0 * i - 2.0)
+    d[2:2 * n1 - 1:2] = -0.25 * (a + 4.0 * i) / (i * (i + 1.0) * (a + 2.0 * i - 2.0) * (a + 2.0 * i))
+    d[-1] = -4.0 * (N + 1.0) ** 2 * (a + 2.0 * N) ** 2 * (a + 4.0 * N + 2.0)
+    odd_cum = np.cumsum(d[1::2])  # sum_{k <= i} d_{2k+1}, i = 0 .. N
+    M = 2 * N + 1
+    off = 1.0 / np.sqrt(d[1:M] * d[2:M + 1])
+    xi = 2.0 / _tridiag_eigs_desc(off, M)[:N]
+    xi2 = xi * xi
+    resi = np.zeros(N)
+    for j in range(N):
+        z2 = xi2[j]
+        prev2, prev1 = 0.0, 0.5  # eta_{-1}, eta_0
+        r_prev = 0.0
+        t = 0.25 / d[1]
+        for k in range(n1):
+            q = t if (k == j or k == N) else t / (xi2[k] - z2)
+            g = 2.0 * math.sqrt(abs(q))   # magnitude factor of the even coefficient
+            h = g if q > 0 else -g        # signed factor of the odd coefficient
+            e_even = d[2 * k] * g * prev1 - 0.25 * g * r_prev * z2 * prev2
+            e_odd = d[2 * k + 1] * h * e_even - 0.25 * h * g * z2 * prev1
+            prev2, prev1 = e_even, e_odd
+            r_prev = h
+            if k != N:
+                t = odd_cum[k] / odd_cum[k + 1]
+        resi[j] = prev1
     return xi, resi
 
 

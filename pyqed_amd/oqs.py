@@ -39,7 +39,7 @@ def lindblad_rk4(H: torch.Tensor, c_ops: torch.Tensor | None, rho: torch.Tensor,
 
     hermitian: use the Hermitian-state kernel (qd_lindblad_rk4_herm: L[rho] = X + X^+,
     1 + 2nc complex GEMMs per RHS instead of 2 + 2nc, one persistent workgroup per matrix).
-    None = auto: on when every rho in the batch equals its conjugate transpose bit for bit,
+    None = auto: on when H and every rho in the batch equal their conjugate transposes bit for bit,
     N <= 128 and the batch fills the chip (B >= HERM_MIN_BATCH); smaller batches run the general
     kernel, whose split path spreads each matrix over many workgroups (qd_lindblad_rk4: 8.3k
     instead of 1.3k steps/s for one N = 128 trajectory).  The Lindblad generator preserves
@@ -67,8 +67,14 @@ def lindblad_rk4(H: torch.Tensor, c_ops: torch.Tensor | None, rho: torch.Tensor,
     nsave = nsteps // save_every if save_every > 0 else 0
     snap = torch.empty((B, nsave, N, N), dtype=torch.complex128, device=dev) if nsave else None
     st = stream if stream is not None else _lib.stream_ptr(dev)
+    # X + X^+ equals the reference's -i[H, rho] + D[rho] only for Hermitian H and rho (oqs.py:697-714 uses
+    # rho H, not rho H^+), so the Hermitian kernel is gated on both, bit for bit.
+    h_herm = bool(torch.equal(H, H.transpose(-1, -2).conj()))
     if hermitian is None:
-        hermitian = N <= 128 and B >= HERM_MIN_BATCH and bool(torch.equal(rho, rho.transpose(-1, -2).conj()))
+        hermitian = (N <= 128 and B >= HERM_MIN_BATCH and h_herm
+                     and bool(torch.equal(rho, rho.transpose(-1, -2).conj())))
+    elif hermitian and not h_herm:
+        raise ValueError("hermitian=True needs a Hermitian H (the X + X^+ form drops the anti-Hermitian part of H)")
     fn = "qd_lindblad_rk4_herm" if hermitian else "qd_lindblad_rk4"
     with torch.cuda.device(dev):
         rc = getattr(_lib.load(), fn)(_lib.ptr(H), _lib.ptr(c_ops), nc, _lib.ptr(rho), B, N, float(dt),
@@ -334,7 +340,7 @@ def _redfield(R, rho0, evecs=None, Nt=1, dt=0.005, t0=0, e_ops=[], return_result
             basis_transform(ev, Ed, inverse=False)
     W = Ed.transpose(1, 2).reshape(len(e_ops), N * N).contiguous() if Ed is not None else None  # vec(E^T)
     v = rho.reshape(1, N * N).contiguous()
-    if return_result is False:
+    if return_result == False:  # noqa: E712  (same truthiness as oqs.py:406)
         # oqs.py:406-431: 'obs.dat' gets one line per step, "t" after the increment followed by the
         # observables of the state BEFORE the step, and the final vec(rho) (eigenbasis) is returned.  The
         # reference evaluates obs_dm(vec(rho), e) = e.dot(vec).diagonal(), which fails for any e_op (an

@@ -52,7 +52,10 @@ class ResultSPO2(Result):
         dx, dy = interval(x), interval(y)
         xAve = [np.einsum('ijn, i, ijn', psi.conj(), x, psi) * dx * dy for psi in self.psilist]
         yAve = [np.einsum('ijn, j, ijn', psi.conj(), y, psi) * dx * dy for psi in self.psilist]
+        xAve = np.real_if_close(xAve)  # wpd.py:150-151
+        yAve = np.real_if_close(yAve)
         self.xAve = [xAve, yAve]
+        np.savez('xAve', xAve, yAve)  # wpd.py:159 writes xAve.npz in the CWD
         return xAve, yAve
 
 

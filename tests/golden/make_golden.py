@@ -569,6 +569,29 @@ def deom_bath():
 
 
 @golden
+def deom_bath_pade3():
+    """Extended PSD (pade=3, heom/deom.py:163-206) poles / residues for Bose and Fermi, and Drude baths decomposed
+    with it through decompose_spectrum_pade(..., pade=3) (heom/deom.py:226-307)."""
+    import sympy as sp
+    from pyqed.heom.deom import decompose_spectrum_pade, pade_approximation_distribution
+    out = {}
+    for bf in (1, 2):
+        for N in range(1, 8):
+            pole, resi = pade_approximation_distribution(N, bf, 3)
+            out[f"bf{bf}_N{N}_pole"] = np.asarray(pole)
+            out[f"bf{bf}_N{N}_resi"] = np.asarray(resi)
+    w_sp = sp.symbols(r"\omega", real=True)
+    for lam, gam, beta, tag in [(0.5, 1.0, 1.0, "d4"), (0.2, 2.0, 0.5, "g2")]:
+        spe = 2 * lam * gam * w_sp / (gam ** 2 + w_sp ** 2)
+        for npsd in (2, 4):
+            etal, etar, etaa, expn = decompose_spectrum_pade(spe, w_sp, beta, npsd, pade=3)
+            for k, v in zip(("etal", "etar", "etaa", "expn"), (etal, etar, etaa, expn)):
+                out[f"{tag}_n{npsd}_{k}"] = np.asarray(v, dtype=complex)
+            out[f"{tag}_n{npsd}_params"] = np.array([lam, gam, beta])
+    save("deom_bath_pade3", **out)
+
+
+@golden
 def deom_keys():
     """Graded ADO index (init_/gen_keys, heom/deom.py:1048-1064, 555-638)."""
     from pyqed.heom.deom import gen_keys
@@ -690,6 +713,84 @@ def deom_run_bench():
     out = _deom_case(lmax=12, npsd=4, nt=3, dt=0.01)
     out.pop("ado_final")
     save("deom_run_bench", **out)
+
+
+# ----------------------------------------------------------------- BASELINE-size pins
+@golden
+def lindblad_n128_long():
+    """Config d1 size, 60 steps (the bench runs many steps; the 3-step lindblad_n128 pins only the start)."""
+    _lindblad_case("lindblad_n128_long", N=128, nc=1, ne=2, Nt=60, dt=5e-3, seed=15, keep_all=False)
+
+
+@golden
+def redfield_n128():
+    """Config d1 Redfield half at its benchmarked size: N = 128, one Hermitian a_op, flat spectrum 0.05
+    (oqs.py:519-570 redfield_tensor, then RedfieldSolver.evolve -> _redfield, oqs.py:57-81, 364-459).  The csr R
+    has N^4 = 2.7e8 nonzeros; a few of its rows are kept (R[rows, :]) to pin the tensor itself."""
+    import pyqed.oqs as oqs
+    N, Nt, dt = 128, 6, 0.02
+    rng = np.random.default_rng(5)
+    a = rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N))
+    H = (a + a.conj().T) / 2 / np.sqrt(N)
+    x = rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N))
+    a_op = 0.2 * (x + x.conj().T) / 2 / np.sqrt(N)
+    E = np.array([_herm(rng, N, 1 / np.sqrt(N)), np.diag(np.arange(N) / N).astype(complex)])
+    psi = rng.standard_normal(N) + 1j * rng.standard_normal(N)
+    psi /= np.linalg.norm(psi)
+    rho0 = np.outer(psi, psi.conj())
+    sol = oqs.RedfieldSolver(H, c_ops=[a_op], spectra=[SPECTRA["flat005"]])
+    R, evecs = sol.redfield_tensor()
+    rows = np.array([0, 1, 129, 8191, 16383])
+    R_rows = R[rows, :].toarray()
+    r = sol.evolve(rho0, dt=dt, Nt=Nt, e_ops=list(E))
+    save("redfield_n128", H=H, a_op=a_op, E=E, rho0=rho0, dt=dt, Nt=Nt, spectrum="flat005", evecs=evecs,
+         R_rows=R_rows, R_row_index=rows, R_nnz=R.nnz, observables=r.observables, rho_final=r.rholist[-1])
+
+
+@golden
+def corr4_2des_256():
+    """Config d5 at its benchmarked grid: correlation_4op_3t(..., 'lccc', tau = 0.5 arange(256)) (oqs.py:268-357)
+    on the 3-level ladder (Redfield a_op diag(0,1,2), flat 0.05); (t3, t1) slices at t2 index 0 and 37, for the
+    unperturbed ladder and for members 0 and 1 of bench.py's static-disorder ensemble (seed 3)."""
+    import pyqed.oqs as oqs
+    tau = 0.5 * np.arange(256)
+    rng = np.random.default_rng(3)
+    dE = np.array([0.0, 0.05, 0.08]) * rng.standard_normal((2, 3))
+    Es = [np.array([0.0, 1.0, 1.5])] + [np.array([0.0, 1.0, 1.5]) + dE[m] for m in range(2)]
+    out = dict(tau=tau, E=np.array(Es), j=np.array([0, 37]))
+    for m, E in enumerate(Es):
+        H, dip, a, rho0 = _three_level(E)
+        sol = oqs.RedfieldSolver(H, c_ops=[a], spectra=[SPECTRA["flat005"]])
+        sol.redfield_tensor()
+        sol.propagator(tau)
+        cube = sol.correlation_4op_3t(rho0, [dip, dip, dip, dip], "lccc", tau)
+        out[f"m{m}_j0"] = cube[:, 0, :]
+        out[f"m{m}_j37"] = cube[:, 37, :]
+        del cube
+    save("corr4_2des_256", **out)
+
+
+@golden
+def spo2_256():
+    """Config d2 at its benchmarked size: SPO2.run (wpd.py:692-758) on 256 x 256 x 2 with the bench potential,
+    dt = 0.05, 20 Strang steps (return_states=True); the final state and the populations along the way."""
+    from pyqed.wpd import SPO2
+    n, nt, nout, dt = 256, 20, 5, 0.05
+    x, y, v0, v1, c, psi0 = spo2_model(n)
+    sol = SPO2(x, y, mass=[1.0, 1.0], nstates=2)
+    sol.set_DPES([v0, v1], [[[0, 1], c]])
+    r = sol.run(psi0, dt=dt, nt=nt, nout=nout)
+    dx = x[1] - x[0]
+    pops = np.array([[np.vdot(p[:, :, k], p[:, :, k]).real * dx * dx for k in range(2)] for p in r.psilist])
+    save("spo2_256", dt=dt, nt=nt, nout=nout, n=n, psi_final=r.psilist[-1], populations=pops,
+         n_psilist=len(r.psilist), times=r.times, exp_K_row7=sol.exp_K[7], exp_V_half_row100=sol.exp_V_half[100])
+
+
+@golden
+def deom_run_bench_long():
+    """Config d4 (L = 12, npsd = 4 -> K = 5, 6188 ADOs) for 25 steps at the bench's dt = 0.002 (DEOMSolver.run,
+    heom/deom.py:1072-1114): Tr(p1 rho_0) along the way and the final ADO set."""
+    save("deom_run_bench_long", **_deom_case(lmax=12, npsd=4, nt=25, dt=0.002))
 
 
 if __name__ == "__main__":

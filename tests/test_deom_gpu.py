@@ -19,7 +19,7 @@ def _solver(g, pulses):
     return DEOMSolver(g["H"], g["sdip"], bath, g["Q"], g["cdip"], fs, fc, int(g["lmax"]))
 
 
-@pytest.mark.parametrize("name", ["deom_run_small", "deom_run_pulsed", "deom_run_bench"])
+@pytest.mark.parametrize("name", ["deom_run_small", "deom_run_pulsed", "deom_run_bench", "deom_run_bench_long"])
 def test_deom_run_matches_reference(name):
     g = load_golden(name)
     pulses = bool(g["pulses"])

@@ -30,6 +30,30 @@ def test_bath_decomposition_matches_reference(tag, lam, gam):
             assert relerr(getattr(b, k), g[f"{tag}_n{npsd}_{k}"]) < 1e-12, (npsd, k)
 
 
+def test_extended_psd_pade3_matches_reference():
+    """pade=3 (extended PSD, heom/deom.py:163-206) for Bose and Fermi, N = 1 .. 7."""
+    from pyqed_amd.deom import pade_approximation_distribution
+    g = load_golden("deom_bath_pade3")
+    for bf in (1, 2):
+        for N in range(1, 8):
+            pole, resi = pade_approximation_distribution(N, bf, 3)
+            assert relerr(pole, g[f"bf{bf}_N{N}_pole"]) < 1e-13, (bf, N)
+            assert relerr(resi, g[f"bf{bf}_N{N}_resi"]) < 1e-12, (bf, N)
+    pole, resi = pade_approximation_distribution(0, 1, 3)
+    assert len(pole) == 0 and len(resi) == 0
+
+
+@pytest.mark.parametrize("tag,npsd", [("d4", 2), ("d4", 4), ("g2", 2), ("g2", 4)])
+def test_bath_decomposition_pade3_matches_reference(tag, npsd):
+    from pyqed_amd.deom import decompose_spectrum_pade
+    g = load_golden("deom_bath_pade3")
+    lam, gam, beta = g[f"{tag}_n{npsd}_params"]
+    w = sp.symbols(r"\omega", real=True)
+    got = decompose_spectrum_pade(2 * lam * gam * w / (gam ** 2 + w ** 2), w, beta, npsd, pade=3)
+    for k, v in zip(("etal", "etar", "etaa", "expn"), got):
+        assert relerr(v, g[f"{tag}_n{npsd}_{k}"]) < 1e-12, k
+
+
 @pytest.mark.parametrize("L,K", [(3, 2), (10, 3), (4, 3), (12, 5)])
 def test_ado_keys_bit_exact(L, K):
     from pyqed_amd.deom import ado_hash, ado_tables

@@ -11,7 +11,8 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-10
 
 
-@pytest.mark.parametrize("name", ["lindblad_n4", "lindblad_n16", "lindblad_n40_noc", "lindblad_n128"])
+@pytest.mark.parametrize("name", ["lindblad_n4", "lindblad_n16", "lindblad_n40_noc", "lindblad_n128",
+                                  "lindblad_n128_long"])
 def test_lindblad_solver_matches_reference_golden(name):
     from scipy.sparse import csr_matrix, issparse
     from pyqed_amd import LindbladSolver
@@ -265,3 +266,93 @@ def test_lindblad_split_path_matches_persistent_and_oracle(N, nc, B, monkeypatch
         assert relerr(a, b) < 1e-12 and relerr(c, b) < 1e-12
     tr = np.einsum("bsii->bs", out["1"][2])
     assert np.max(np.abs(tr - 1)) < 1e-12
+
+
+@pytest.mark.parametrize("B", [2, 200])
+def test_lindblad_non_hermitian_H_matches_oracle(B):
+    """oqs.liouvillian (oqs.py:697-714) is -i(H rho - rho H) + D[rho] for ANY H: a non-Hermitian H must give the
+    same result on the GPU (P = -i(H - i S/2), Q = iH - S/2 formed from H itself, glf.hip lindblad_prep_kernel).
+    B = 200 would take the Hermitian kernel if only rho were checked; hermitian=True must refuse this H."""
+    import torch
+    from oracle import lindblad as olb
+    from pyqed_amd import lindblad_rk4
+    N, steps, dt = 48, 6, 1e-2
+    rng = np.random.default_rng(11)
+    H = (rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N))) / np.sqrt(N)  # not Hermitian
+    _, cs = olb.synthetic_lindblad(N, nc=1)
+    rho0 = olb.random_pure_states(B, N)
+    dev = torch.device("cuda", 0)
+    Ht, Ct = torch.from_numpy(H).to(dev), torch.from_numpy(np.array(cs)).to(dev)
+    rho = torch.from_numpy(rho0.copy()).to(dev)
+    lindblad_rk4(Ht, Ct, rho, dt, steps)
+    sel = [0, B - 1]
+    ref = olb.lindblad_batch(H, cs, rho0[sel], dt, steps)
+    assert relerr(rho.cpu().numpy()[sel], ref) < TOL
+    with pytest.raises(ValueError):
+        lindblad_rk4(Ht, Ct, torch.from_numpy(rho0.copy()).to(dev), dt, steps, hermitian=True)
+
+
+def test_lindblad_driven_complex_drive_matches_oracle():
+    """_lindblad_driven (oqs.py:1699-1806) with a complex drive f(t): H(t) = H0 - f(t) H1 is then not Hermitian,
+    and the right-hand product must still be rho H(t) (driven_update_kernel forms P and Q from H(t))."""
+    from pyqed_amd import LindbladSolver
+    from oracle import lindblad as olb
+    N, Nt, dt, t0 = 12, 15, 0.02, 0.1
+    rng = np.random.default_rng(4)
+    H0, cs = olb.synthetic_lindblad(N, nc=1)
+    A = rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N))
+    H1 = (A + A.conj().T) / 2
+    E = np.diag(np.arange(N)).astype(complex)
+    f = lambda t: np.exp(1j * 3.0 * t) * 0.4
+    rho0 = olb.random_pure_states(1, N)[0]
+    r = LindbladSolver([H0, [H1, f]], [cs[0]]).run(rho0, dt=dt, Nt=Nt, t0=t0, e_ops=[E])
+    rho, t, obs = rho0.copy(), t0, []
+    for k in range(Nt):
+        t += dt
+        rho = olb.rk4(rho, olb.liouvillian, dt, H0 - f(t) * H1, [cs[0]])
+        obs.append(olb.obs_dm(rho, E))
+    got = np.asarray(r.observables).reshape(-1)
+    assert relerr(got[-Nt:], np.array(obs)) < TOL
+    last = r.rholist[-1]
+    assert relerr(last.toarray() if hasattr(last, "toarray") else np.asarray(last), rho) < TOL
+
+
+def test_lindblad_concurrent_streams_match_oracle():
+    """the library is re-entrant for distinct streams.  Two batches (persistent Hermitian kernel,
+    B = 200, and the split-K general path, B = 8) are launched back to back on two streams, and again from two
+    host threads, so their kernels overlap; each must match the oracle (workspaces keyed by (device, stream),
+    qd_runtime.hip)."""
+    import threading
+    import torch
+    from oracle import lindblad as olb
+    from pyqed_amd import lindblad_rk4
+    N, steps, dt = 128, 6, 1e-2
+    H, cs = olb.synthetic_lindblad(N, nc=1)
+    dev = torch.device("cuda", 0)
+    Ht, Ct = torch.from_numpy(H).to(dev), torch.from_numpy(np.array(cs)).to(dev)
+    r0 = {"a": olb.random_pure_states(200, N, seed=5), "b": olb.random_pure_states(8, N, seed=6)}
+    sel = {"a": [0, 77, 199], "b": [0, 7]}
+    ref = {k: olb.lindblad_batch(H, cs, r0[k][sel[k]], dt, steps) for k in r0}
+    streams = {k: torch.cuda.Stream(dev) for k in r0}
+
+    def run(k, out):
+        with torch.cuda.stream(streams[k]):
+            rho = torch.from_numpy(r0[k].copy()).to(dev)
+            lindblad_rk4(Ht, Ct, rho, dt, steps, stream=streams[k].cuda_stream)
+            out[k] = rho
+
+    for mode in ("sequential", "threads"):
+        torch.cuda.synchronize()
+        out = {}
+        if mode == "sequential":
+            for k in r0:
+                run(k, out)
+        else:
+            th = [threading.Thread(target=run, args=(k, out)) for k in r0]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+        torch.cuda.synchronize()
+        for k in r0:
+            assert relerr(out[k].cpu().numpy()[sel[k]], ref[k]) < TOL, (mode, k)

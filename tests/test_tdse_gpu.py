@@ -78,13 +78,15 @@ def test_driven_mol_two_pulses():
     assert relerr(got, g["b_psilist"]) < TOL
 
 
-def test_driven_batch_vs_oracle():
-    """Batched driven kernel vs the oracle for several wavefunctions, nout > 1."""
+@pytest.mark.parametrize("N,B", [(40, 3), (512, 64)])
+def test_driven_batch_vs_oracle(N, B):
+    """Batched driven kernel vs the oracle for several wavefunctions, nout > 1; (512, 64) takes the MFMA GEMM
+    stage path of the driven run."""
     import torch
     from oracle import tdse as ot
     from pyqed_amd.mol import tdse_driven_rk4
     rng = np.random.default_rng(5)
-    N, B, nout, nblk, dt = 40, 3, 4, 6, 0.03
+    nout, nblk, dt = 4, 6, 0.03
     A = rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N))
     H0 = (A + A.conj().T) / 2 / np.sqrt(N)
     Hd = np.array([np.diag(np.arange(N) / N).astype(complex)])
@@ -103,12 +105,19 @@ def test_driven_batch_vs_oracle():
         assert relerr(snap[b].cpu().numpy(), psit[:, 1:].T) < TOL
 
 
+@pytest.mark.parametrize("gemm", ["auto", "0"])
 @pytest.mark.parametrize("N,B,save_every", [(300, 1, 2), (2500, 2, 3), (1024, 64, 5), (600, 130, 2)])
-def test_tdse_row_path_vs_persistent_and_oracle(N, B, save_every, monkeypatch):
-    """Row-parallel TDSE path (a wave per row and stage launch; the only path past N = 2048) and, for batches of
-    >= 32 at N >= 256, the MFMA GEMM stages (padded [Bp][Np] state, split-K slabs): snapshots and observables
-    (E_m = H, diag) against the persistent kernel (N <= 2048) and the oracle's RK4 (oracle.tdse restates
-    mol.py:1603-1691); B = 64 / 130 and N = 600 exercise the GEMM's padding to multiples of 128."""
+def test_tdse_row_path_vs_persistent_and_oracle(N, B, save_every, gemm, monkeypatch):
+    """Row-parallel TDSE path (a wave per row and stage launch; the only path past N = 2048) and, where
+    tdse.hip's dispatch takes it ((B >= 64 and N >= 512) or (B >= 128 and N >= 256)), the MFMA GEMM stages
+    (padded [Bp][Np] state, split-K slabs): snapshots and observables (E_m = H, diag) against the persistent
+    kernel (N <= 2048) and the oracle's RK4 (oracle.tdse restates mol.py:1603-1691); B = 64 / 130 and N = 600
+    exercise the GEMM's padding to multiples of 128.  gemm="0" (QD_TDSE_GEMM=0) keeps the row kernel at the
+    batch sizes the GEMM would otherwise take."""
+    if gemm == "0":
+        if B < 64:
+            pytest.skip("the GEMM path is not taken at this batch size either way")
+        monkeypatch.setenv("QD_TDSE_GEMM", "0")
     import torch
     from oracle import tdse as otd
     from pyqed_amd.mol import tdse_rk4
