@@ -159,6 +159,85 @@ def cpu_baseline_redfield(sol, dt=1e-3, budget_s=5.0):
                       f"nonzeros) runs ~0.42 steps/s here (SURVEY.md §8(a5))"}
 
 
+def bench_superop(dev, steps=10, N=128, dt=1e-3, batch=64, gemm_steps=2):
+    """Dense L vec(rho) RK4 (BASELINE.json configs[1] "dense L.vec(rho) RK4", SURVEY §8(d) d1 GEMV alternative):
+    the N = 128 Lindblad superoperator (16384^2 c128 = 4 GiB) built on the device, then (a) one density matrix on the
+    HBM-streaming GEMV (16 N^4 B of L per stage) and (b) a batch on the MFMA GEMM stages."""
+    import torch
+    from oracle import lindblad as olb  # seeded input synthesis only
+    from pyqed_amd.oqs import lindblad_superop, superop_rk4
+    H, cs = olb.synthetic_lindblad(N, nc=1)
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+    L = lindblad_superop(t(H), t(np.array(cs)))
+    N2 = N * N
+    stream = torch.cuda.current_stream(dev)
+
+    def timed(v, k):
+        superop_rk4(L, v, dt, 1)
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(stream)
+        superop_rk4(L, v, dt, k)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        return time.perf_counter() - t0, e0.elapsed_time(e1) / 1e3
+
+    v1 = t(olb.random_pure_states(1, N, seed=3).reshape(1, N2))
+    wall, ev = timed(v1, steps)
+    bytes_per_step = 4 * 16.0 * N2 * N2
+    tr1 = abs(complex(torch.diagonal(v1.reshape(N, N)).sum().item()) - 1)
+    vb = t(olb.random_pure_states(batch, N, seed=4).reshape(batch, N2))
+    wall_b, ev_b = timed(vb, gemm_steps)
+    Bp = 64 if batch <= 64 else (batch + 127) // 128 * 128
+    flop_b = 4 * 8.0 * N2 * N2 * Bp
+    del L
+    torch.cuda.empty_cache()
+    return {
+        "value": round(steps / wall, 2), "unit": "density-matrix steps/s (one rho, dense L vec(rho))",
+        "config": {"workload": "lindblad_n128_dense_superop_rk4_fp64 (BASELINE.json configs[1], dense L.vec(rho))",
+                   "N": N, "N2": N2, "L_bytes": 16 * N2 * N2, "dt": dt, "steps": steps,
+                   "kernel": "superop_rows_kernel<1,4,4> (VALU GEMV, L streamed nontemporal)"},
+        "us_per_step": round(ev / steps * 1e6, 1),
+        "roofline": {"bound": "hbm", "kernel": "superop_rows_kernel<1,4,4>",
+                     "achieved": round(bytes_per_step * steps / ev / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(bytes_per_step * steps / ev / 1e9 / HBM_PEAK_GBS, 4),
+                     "bytes_per_step": bytes_per_step, "traffic": None},
+        "trace_err": tr1,
+        "batched": {"batch": batch, "steps": gemm_steps, "dm_steps_per_s": round(batch * gemm_steps / wall_b, 1),
+                    "ms_per_step": round(ev_b / gemm_steps * 1e3, 3),
+                    "roofline": {"bound": "mfma", "kernel": "ens_gemm_kernel<64> (L x X[N2][64] split-K)",
+                                 "achieved": round(flop_b * gemm_steps / ev_b / 1e12, 3),
+                                 "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                 "frac": round(flop_b * gemm_steps / ev_b / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
+                                 "flop_per_step": flop_b,
+                                 "note": "executed flops (batch padded to the 64-wide block); L read once per stage"}},
+    }, (H, cs)
+
+
+def cpu_baseline_superop(H, cs, dt=1e-3, budget_s=6.0):
+    """NumPy dense GEMV form of _redfield's rhs = R.dot(rho) (oqs.py:462-463) with the N = 128 dense L (built here
+    by the host kron restatement of superoperator.liouvillian), one density matrix, BLAS threads as set."""
+    from oracle import lindblad as olb
+    N = H.shape[0]
+    I = np.eye(N)
+    L = -1j * (np.kron(H, I) - np.kron(I, H.T))
+    for c in cs:
+        cdc = c.conj().T @ c
+        L += np.kron(c, c.conj()) - 0.5 * (np.kron(cdc, I) + np.kron(I, cdc.T))
+    v = olb.random_pure_states(1, N, seed=3).reshape(N * N)
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        v = olb.rk4(v, lambda x: L @ x, dt)
+        steps += 1
+    el = time.perf_counter() - t0
+    del L
+    threads = os.environ.get("OMP_NUM_THREADS") or os.environ.get("OPENBLAS_NUM_THREADS") or str(os.cpu_count())
+    return {"value": round(steps / el, 3), "unit": "density-matrix steps/s", "kind": "port",
+            "cores": int(threads) if threads.isdigit() else threads,
+            "sample": f"{steps} RK4 steps of a dense NumPy L @ vec(rho) (N = 128, L 4 GiB) in {el:.1f}s"}
+
+
 def twodes_inputs(M, seed=3):
     """BASELINE config d5: 3-level ladder E=[0,1,1.5] + static disorder (seed 3), Redfield with
     a_op = diag(0,1,2), flat spectrum 0.05, signature 'lccc', t2 = 0, t1 = t3 = 0.5*arange(256)."""
@@ -191,14 +270,20 @@ def bench_2des(dev, world, rank, M_total, reps, n=256):
     t = 0.5 * np.arange(n)  # uniform host grid -> exponential-table operand build (no device time arrays)
     out = torch.empty((n, n), dtype=torch.complex128, device=dev)
 
-    def local(a, b):
-        # this rank's members are already resident on its GPU (inputs in HBM before timing)
-        return response2d_ensemble(lam_t, alpha_t, Mt_t, beta_t, t, t, out=out, accumulate=False)
+    from pyqed_amd.distributed import ReducePipeline
+    # a sequence of `reps` grids; each grid's RCCL reduce(sum) to rank 0 runs asynchronously behind the next
+    # grid's compute (two output buffers), and every reduce has completed before the timed region ends
+    pipe = ReducePipeline((n, n), torch.complex128, dev, depth=2, dst=0)
 
     def once():
-        return sharded_sum(local, M_total, dst=0)   # one RCCL reduce(sum) of the 1 MiB grid when world > 1
+        buf = pipe.next_buffer()
+        # this rank's members are already resident on its GPU (inputs in HBM before timing)
+        response2d_ensemble(lam_t, alpha_t, Mt_t, beta_t, t, t, out=buf, accumulate=False)
+        pipe.submit(buf)
+        return buf
 
     out = once()
+    pipe.finish()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -208,7 +293,8 @@ def bench_2des(dev, world, rank, M_total, reps, n=256):
     t0 = time.perf_counter()
     e0.record(stream)
     for _ in range(reps):
-        once()
+        out = once()
+    pipe.finish()
     e1.record(stream)
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
@@ -230,8 +316,9 @@ def bench_2des(dev, world, rank, M_total, reps, n=256):
         "unit": "grid-points/s ((t3,t1) points x ensemble members)",
         "config": {"workload": "2des_3level_256x256_redfield_ensemble (BASELINE.json configs[4])",
                    "grid": [n, n], "ensemble_members": M_total, "members_per_rank": hi - lo, "t2": 0.0,
-                   "signature": "lccc", "scaling": "strong", "collective": "RCCL reduce(sum) to rank 0"
-                   if world > 1 else "none"},
+                   "signature": "lccc", "scaling": "strong",
+                   "collective": "RCCL reduce(sum) of each 1 MiB grid to rank 0, pipelined behind the next grid's "
+                                 "compute (2 output buffers)" if world > 1 else "none"},
         "ms_per_grid": round(wall / reps * 1e3, 4),
         "roofline": {"bound": "mfma", "kernel": "ens_gemm_kernel<128,xtab>" if Kp >= 32768 else "ens_gemm_kernel<64>",
                      "achieved": round(gemm_flop / (e0.elapsed_time(e1) / reps / 1e3) / 1e12, 3),
@@ -573,6 +660,7 @@ def main():
     ap.add_argument("--deom-batch", type=int, default=64)
     ap.add_argument("--no-deom", action="store_true")
     ap.add_argument("--no-redfield", action="store_true")
+    ap.add_argument("--no-superop", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -644,12 +732,24 @@ def main():
         twodes, sig, ens_in = bench_2des(dev, world, rank, args.ens, args.ens_reps)
         if rank == 0:
             twodes["signal_abs_max"] = float(sig.abs().max().item())
+        if world == 1 and args.ens >= 8:
+            # the 8-GPU expectation from one GPU: an 8-way member shard timed alone (its reduce is pipelined
+            # behind the next grid's compute at N > 1, so the shard's compute bounds the per-grid time)
+            shard, _, _ = bench_2des(dev, 1, 0, args.ens // 8, args.ens_reps)
+            twodes["shard_1of8"] = {
+                "members": args.ens // 8, "ms_per_grid": shard["ms_per_grid"],
+                "event_ms_per_grid": shard["event_ms_per_grid"], "roofline": shard["roofline"],
+                "projected_8gpu_speedup_compute_only": round(twodes["ms_per_grid"] / shard["ms_per_grid"], 3)}
         if args.t2 > 0:
             twodes["t2scan"] = bench_2des_t2scan(dev, world, rank, args.ens, args.t2, args.t2_reps)
 
     redfield = None
     if not args.no_redfield:
         redfield, rf_sol = bench_redfield(dev, args.steps, B)
+
+    superop = None
+    if not args.no_superop:
+        superop, so_in = bench_superop(dev)
 
     spo = None
     if not args.no_spo:
@@ -709,6 +809,10 @@ def main():
             if world == 1 and not args.no_cpu:
                 redfield["cpu_baseline"] = cpu_baseline_redfield(rf_sol)
             out.setdefault("secondary", {})["redfield"] = redfield
+        if superop is not None:
+            if world == 1 and not args.no_cpu:
+                superop["cpu_baseline"] = cpu_baseline_superop(*so_in)
+            out.setdefault("secondary", {})["superop"] = superop
         if spo is not None:
             if world == 1 and not args.no_cpu:
                 spo["cpu_baseline"] = cpu_baseline_spo2()

@@ -294,11 +294,33 @@ int qd_spo3_run(qd_c128* psi, const qd_c128* expVh, const qd_c128* expK, int nx,
  * dense superoperator.  L [N2][N2], v [B][N2] in/out (row-major vec(rho)),
  * W [ne][N2]: obs[b][k][m] = sum_j W[m][j] v_k[b][j] for k = 0..nsteps
  * (W = vec(E^T) gives Tr(E rho)), snap [B][nsteps/save_every][N2] or NULL.
- * HBM-bound: 16 N2^2 bytes per stage per group of 4 vectors.
+ * B < 48 (QD_SUPEROP_GEMM_MIN): HBM-bound GEMV, 16 N2^2 bytes per stage per group
+ * of <= 8 vectors.  B >= 48: one complex-fp64 MFMA GEMM per stage (L read once
+ * per stage for the whole batch) with a fused RK4 epilogue.
  */
 int qd_superop_rk4(const qd_c128* L, qd_c128* v, int B, int N2, double dt,
                    int nsteps, const qd_c128* W, int ne, qd_c128* obs,
                    qd_c128* snap, int save_every, void* stream);
+
+/*
+ * Dense Liouville-space generator of d rho/dt = P rho + rho Q + sum_c L_c rho R_c
+ * on row-major vec(rho): out[(a,b),(c,d)] = P[a][c] d_bd + d_ac Q[d][b]
+ * + sum_c L_c[a][c] R_c[d][b]  ([N^2][N^2], the kron(A, I) / kron(I, A^T)
+ * conventions of pyqed/superoperator.py:200-270).  Replaces the host kron
+ * assembly of superoperator.liouvillian (superoperator.py:29-58) and of
+ * redfield_tensor's R (oqs.py:563-570) for dense operators.
+ */
+int qd_superop_from_glf(const qd_c128* P, const qd_c128* Q, const qd_c128* Lops,
+                        const qd_c128* Rops, int nc, int N, qd_c128* out,
+                        void* stream);
+
+/*
+ * Dense Lindblad superoperator of oqs.liouvillian (oqs.py:697-714) /
+ * superoperator.liouvillian (superoperator.py:29-58): H [N][N], C [nc][N][N],
+ * out [N^2][N^2] (N = 128: 4 GiB).
+ */
+int qd_superop_lindblad(const qd_c128* H, const qd_c128* C, int nc, int N,
+                        qd_c128* out, void* stream);
 
 /* ------------------------------------------------------------ response --- */
 /*

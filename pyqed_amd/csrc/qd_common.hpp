@@ -47,7 +47,7 @@ void set_error(const char* fmt, ...);
 // stream from different host threads are not supported (their scratch would alias).
 enum WsSlot { WS_LINDBLAD = 0, WS_LINDBLAD_OPS = 1, WS_SPO = 2, WS_DEOM = 3,
               WS_SUPEROP = 4, WS_2DES = 5, WS_MISC = 6, WS_2DES_OPS = 7, WS_TDSE_H = 8,
-              WS_TDSE_GEMM = 9, WS_NSLOTS = 10 };
+              WS_TDSE_GEMM = 9, WS_SUPEROP_OPS = 10, WS_NSLOTS = 11 };
 int workspace(WsSlot slot, size_t bytes, void** ptr, hipStream_t st);
 void free_workspaces();
 
@@ -86,7 +86,7 @@ __device__ __forceinline__ int dpp_qi(int v) { return __builtin_amdgcn_update_dp
 inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
 // Split-K complex fp64 MFMA GEMM (response.hip): slabs[s] = A [Mp][Kp] x B [Kp][Np] over K slice s, S <= max_S
-// slices (returned); Mp, Np multiples of 128, Kp of 16.
+// slices (returned); Mp a multiple of 128, Np of 64 (64-wide column blocks) or 128, Kp of 16.
 int cgemm_splitk_slabs(const c128* A, const c128* B, int Mp, int Kp, int Np, c128* slabs, int max_S, int* S_out,
                        hipStream_t st);
 

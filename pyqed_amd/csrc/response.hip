@@ -444,10 +444,15 @@ SplitPlan split_plan(int Mp, int Np, int tiles) {
     const int blocks = (Mp / bt) * (Np / bt);
     return std::max(1, std::min(ceil_div(256, blocks), std::max(1, tiles / 4)));
   };
+  static const int force_s = [] {   // QD_ENS_S: split count override (A/B sweeps)
+    const char* e = std::getenv("QD_ENS_S");
+    return e ? std::atoi(e) : 0;
+  }();
   const int S128 = splits(128);
   const bool small = (Mp / 128) * (Np / 128) * S128 < 256 || tiles / S128 < 32;
   const int bt = force == 64 || force == 128 ? force : (small ? 64 : 128);
-  return {bt, splits(bt)};
+  const int S = force_s > 0 ? std::max(1, std::min(force_s, tiles)) : splits(bt);
+  return {bt, S};
 }
 
 // fine != nullptr: X is the coarse table of ens_xtab_kernel (generated A operand)
@@ -996,8 +1001,15 @@ int splits_for(int Mp, int Np, int Kp) {
 // (<= max_S).  The caller sums the slabs in order s = 0 .. S-1.
 int qd::cgemm_splitk_slabs(const c128* A, const c128* B, int Mp, int Kp, int Np, c128* slabs, int max_S, int* S_out,
                            hipStream_t st) {
-  QD_CHECK_ARG(Mp % 128 == 0 && Np % 128 == 0 && Kp % CG_KT == 0, "cgemm_splitk_slabs: bad padding");
-  SplitPlan pl = split_plan(Mp, Np, Kp / CG_KT);
+  QD_CHECK_ARG(Mp % 128 == 0 && Np % 64 == 0 && Kp % CG_KT == 0, "cgemm_splitk_slabs: bad padding");
+  const int tiles = Kp / CG_KT;
+  SplitPlan pl;
+  if (Np % 128 == 0) {
+    pl = split_plan(Mp, Np, tiles);
+  } else {  // 64-wide column blocks (skinny B, e.g. a batch of <= 64 vectors): >= 512 workgroups, >= 8 K-tiles each
+    const int blocks = (Mp / 64) * (Np / 64);
+    pl = {64, std::max(1, std::min(ceil_div(512, blocks), std::max(1, tiles / 8)))};
+  }
   pl.S = std::min(pl.S, max_S);
   launch_ens_gemm(pl, A, Kp, B, Mp, Np, Kp / CG_KT, slabs, st);
   QD_HIP(hipGetLastError());

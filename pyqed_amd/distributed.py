@@ -2,7 +2,8 @@
 
 The hot path shards only where units are independent:
   * 2DES disorder ensemble: members split into contiguous ranges, each rank evaluates its
-    partial (t3, t1) grid, ONE reduce(sum) of the 1 MiB grid to rank 0 (strong scaling);
+    partial (t3, t1) grid, ONE reduce(sum) of the 1 MiB grid to rank 0 (strong scaling); a sequence of
+    grids pipelines those reduces behind the next grid's compute (ReducePipeline);
     a waiting-time scan reduces its [n2, n3, n1] stack in buckets, each bucket's reduce overlapped
     with the next bucket's compute (sharded_sum_buckets);
   * Lindblad / DEOM / SPO batches: independent replicas per rank, no collective.
@@ -66,6 +67,46 @@ def sharded_sum_buckets(local_fn, n_units: int, out: torch.Tensor, buckets, dst:
     for w in works:
         w.wait()
     return out
+
+
+class ReducePipeline:
+    """Sum-reduce a SEQUENCE of per-rank partial grids to `dst`, each reduce overlapping the compute of the next
+    grid (one reduce per grid, hidden behind compute instead of serialised after it).
+
+    Grids rotate over `depth` output buffers.  next_buffer() returns the buffer for the next grid after making the
+    current stream wait (stream-side, no host block) for the reduce that last used it; submit(buf) issues that
+    grid's reduce asynchronously on RCCL's stream (which first waits for the compute already queued on the current
+    stream); finish() makes the current stream wait for every outstanding reduce.  Rank `dst` then holds the sum of
+    every grid in the buffer it was computed in.  Single process: no collective, the buffers just rotate."""
+
+    def __init__(self, shape, dtype, device, depth: int = 2, dst: int = 0, group=None):
+        self.bufs = [torch.empty(shape, dtype=dtype, device=device) for _ in range(max(1, depth))]
+        self.works = [None] * len(self.bufs)
+        self.dst, self.group = dst, group
+        self.rank, self.ws = world()
+        self.i = 0
+
+    def next_buffer(self) -> torch.Tensor:
+        j = self.i % len(self.bufs)
+        if self.works[j] is not None:
+            self.works[j].wait()
+            self.works[j] = None
+        return self.bufs[j]
+
+    def submit(self, buf: torch.Tensor):
+        j = self.i % len(self.bufs)
+        if buf is not self.bufs[j]:
+            raise ValueError("submit() takes the buffer next_buffer() returned")
+        if self.ws > 1:
+            self.works[j] = dist.reduce(_real_view(buf), dst=self.dst, op=dist.ReduceOp.SUM, group=self.group,
+                                        async_op=True)
+        self.i += 1
+
+    def finish(self):
+        for j, w in enumerate(self.works):
+            if w is not None:
+                w.wait()
+                self.works[j] = None
 
 
 def ensemble_2des(lam, alpha, Mt, beta, t3, t1, dst=0, group=None):

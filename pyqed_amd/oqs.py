@@ -310,7 +310,12 @@ def superop_rk4(L: torch.Tensor, v: torch.Tensor, dt, nsteps, W: torch.Tensor | 
     W [ne,N2] observable weights.  Returns (obs [B,nsteps+1,ne] | None, snap [B,nsave,N2] | None)."""
     dev = v.device
     _lib.ensure_device(dev)
+    for name, t in (("L", L), ("v", v), ("W", W)):
+        if t is not None and (t.dtype != torch.complex128 or t.device != dev or not t.is_contiguous()):
+            raise ValueError(f"{name} must be a contiguous complex128 tensor on {dev}")
     B, N2 = v.shape
+    if tuple(L.shape) != (N2, N2) or (W is not None and (W.dim() != 2 or W.shape[1] != N2)):
+        raise ValueError(f"superop_rk4: L {tuple(L.shape)} / W shapes do not match v {tuple(v.shape)}")
     ne = 0 if W is None else W.shape[0]
     obs = torch.empty((B, nsteps + 1, ne), dtype=torch.complex128, device=dev) if ne else None
     nsave = nsteps // save_every if save_every > 0 else 0
@@ -321,6 +326,36 @@ def superop_rk4(L: torch.Tensor, v: torch.Tensor, dt, nsteps, W: torch.Tensor | 
                                         _lib.stream_ptr(dev))
     _lib.check(rc, "qd_superop_rk4")
     return obs, snap
+
+
+def lindblad_superop(H: torch.Tensor, c_ops: torch.Tensor | None) -> torch.Tensor:
+    """Dense Lindblad superoperator [N^2, N^2] built on the device (qd_superop_lindblad): the matrix of
+    oqs.liouvillian (oqs.py:697-714) on row-major vec(rho), i.e. superoperator.liouvillian (superoperator.py:29-58)
+    without the host kron assembly (N = 128: 4 GiB)."""
+    dev = H.device
+    _lib.ensure_device(dev)
+    N = H.shape[0]
+    nc = 0 if c_ops is None else c_ops.shape[0]
+    out = torch.empty((N * N, N * N), dtype=torch.complex128, device=dev)
+    with torch.cuda.device(dev):
+        rc = _lib.load().qd_superop_lindblad(_lib.ptr(H), _lib.ptr(c_ops), nc, N, out.data_ptr(), _lib.stream_ptr(dev))
+    _lib.check(rc, "qd_superop_lindblad")
+    return out
+
+
+def glf_superop(P: torch.Tensor, Q: torch.Tensor, L: torch.Tensor | None, R: torch.Tensor | None) -> torch.Tensor:
+    """Dense superoperator of d rho/dt = P rho + rho Q + sum_c L_c rho R_c on row-major vec(rho)
+    (qd_superop_from_glf), e.g. RedfieldSolver.glf_terms() -> the reference's R (oqs.py:563-570)."""
+    dev = P.device
+    _lib.ensure_device(dev)
+    N = P.shape[0]
+    nc = 0 if L is None else L.shape[0]
+    out = torch.empty((N * N, N * N), dtype=torch.complex128, device=dev)
+    with torch.cuda.device(dev):
+        rc = _lib.load().qd_superop_from_glf(_lib.ptr(P), _lib.ptr(Q), _lib.ptr(L), _lib.ptr(R), nc, N, out.data_ptr(),
+                                             _lib.stream_ptr(dev))
+    _lib.check(rc, "qd_superop_from_glf")
+    return out
 
 
 def _redfield(R, rho0, evecs=None, Nt=1, dt=0.005, t0=0, e_ops=[], return_result=True):

@@ -161,3 +161,51 @@ def test_native_rccl_reduce_single_rank():
         assert lib.qd_comm_init(1, 0, uid) != 0                                            # double init
     finally:
         _lib.check(lib.qd_comm_destroy(), "qd_comm_destroy")
+
+
+def _worker_pipeline(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pyqed_amd.distributed import ReducePipeline, shard_range
+    lam, alpha, Mt, beta, t = _inputs()
+    lo, hi = shard_range(len(lam), rank, world)
+    part = _slice_sum(lam, alpha, Mt, beta, t, lo, hi)
+    pipe = ReducePipeline((len(t), len(t)), torch.complex128, "cpu", depth=2, dst=0)
+    got = {}
+    ngrid = 5
+    for g in range(ngrid):
+        buf = pipe.next_buffer()
+        if g >= 2 and rank == 0:       # this buffer last held grid g-2, whose reduce has now completed
+            got[g - 2] = buf.numpy().copy()
+        buf.copy_(torch.from_numpy((g + 1) * part))
+        pipe.submit(buf)
+    pipe.finish()
+    if rank == 0:
+        for g in (ngrid - 2, ngrid - 1):
+            got[g] = pipe.bufs[g % 2].numpy().copy()
+    q.put((rank, got))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_reduce_pipeline_gloo():
+    """ReducePipeline (a sequence of grids, each reduce overlapping the next grid's compute, 2 rotating buffers):
+    rank 0 ends up with the exact cross-rank sum of every grid in the sequence."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_pipeline, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    lam, alpha, Mt, beta, t = _inputs()
+    full = _slice_sum(lam, alpha, Mt, beta, t, 0, len(lam))
+    got = res[0][1]
+    assert sorted(got) == list(range(5))
+    for g in range(5):
+        assert np.allclose(got[g], (g + 1) * full, rtol=1e-12, atol=1e-12 * np.abs(full).max()), g
