@@ -239,6 +239,36 @@ int qd_deom_rk4_ado_major(qd_c128* ados, int B, int nmax, int K, int ns,
                           int ne, qd_c128* trace, void* stream);
 
 /*
+ * One RK4 stage of a BAND of the ADO hierarchy (tier-banded sharding of one
+ * hierarchy over ranks; DEOMSolver.run / rk4 / rem_cal,
+ * pyqed/heom/deom.py:641-766, 1072-1114, split across processes).  Rows
+ * [0, n_own) of rho / xin / xout are the band's ADOs, rows [n_own, n_loc) of xin
+ * the halo copies of neighbours owned by other bands; minus / plus [n_own][K]
+ * are LOCAL row indices (-1 absent); coef [n_own][K][3], damp [n_own] the band's
+ * slices of qd_deom_rk4's tables.  stage 0..3 (RK4 order of deom.py:725-766;
+ * stage 0 reads xin = rho); fs / fc the pulse values at the stage's time.  snap
+ * [nsteps+1][ns][ns] (band owning ADO 0 only, else NULL) gets rho_0 after step
+ * `step` at stage 3.  ns <= 16; ns <= 8 group kernel, 9..16 MFMA tiles.
+ */
+int qd_deom_stage(qd_c128* rho, const qd_c128* xin, qd_c128* xout, qd_c128* acc,
+                  int n_own, int K, int ns, const int32_t* minus,
+                  const int32_t* plus, const qd_c128* coef, const qd_c128* damp,
+                  const int32_t* mode, int nmod, const qd_c128* H,
+                  const qd_c128* Hdip, const qd_c128* Q, const qd_c128* Qdip,
+                  double fs_re, double fs_im, double fc_re, double fc_im,
+                  int stage, double dt, qd_c128* snap, int step, int nsteps,
+                  void* stream);
+
+/* dst[i][:] = src[idx[i]][:], i < n, rows of row_elems complex (halo packing). */
+int qd_gather_rows(const qd_c128* src, const int32_t* idx, int n, int row_elems,
+                   qd_c128* dst, void* stream);
+
+/* obs[s][m] = Tr(E_m rho_0(s)), s < nsnap: DEOMSolver.run's Tr(p1 rho_0)
+ * (heom/deom.py:1100,1113) from a snapshot stack [nsnap][ns][ns]. */
+int qd_deom_trace(const qd_c128* snap, const qd_c128* E, int ne, int nsnap,
+                  int ns, qd_c128* obs, void* stream);
+
+/*
  * Single-exponential (high-T Drude) HEOM chain of pyqed/oqs.py:1808-1875
  * (oqs._heom): explicit in-place sweep per step, ADO n updated from the NEW
  * n-1 and the old n, n+1; ADO nado-1 never updated.  ados [B][nado][ns][ns]

@@ -193,3 +193,25 @@ def correlation_4op_3t(P, nmax, ns, ops, rho0, T, w_x, w_y, if_full=True, cut_of
             y = A1V @ ((1 / (-lam - 1j * w_x[i])).reshape(-1, 1) * (G @ ((1 / (-lam - 1j * w_y[j])).reshape(-1, 1) * VA4)))
             cw[i, j] = np.trace(y[:ns * ns, 0].reshape(ns, ns))
     return cw
+
+
+def band_rhs(x_loc, n_own, minus, plus, coef, damp, mode, H, Q):
+    """rem_cal (:641-673) for the owned rows of a band with precomputed prefactors: x_loc [n_loc, ns, ns] holds the
+    owned rows then the halo rows, minus / plus [n_own, K] local rows (-1 absent), coef [n_own, K, 3] =
+    (cL, cR, cP) = (-i sqrt(n_k) etal_k / sqrt(etaa_k), +i sqrt(n_k) etar_k / sqrt(etaa_k), -i sqrt(n_k + 1)
+    sqrt(etaa_k)), damp [n_own] = -sum_k n_k expn_k."""
+    K = minus.shape[1]
+    d = np.empty((n_own,) + x_loc.shape[1:], dtype=complex)
+    for n in range(n_own):
+        r = x_loc[n]
+        v = damp[n] * r - 1j * (H @ r - r @ H)
+        for k in range(K):
+            q = Q[mode[k]]
+            if minus[n, k] >= 0:
+                y = x_loc[minus[n, k]]
+                v = v + coef[n, k, 0] * (q @ y) + coef[n, k, 1] * (y @ q)
+            if plus[n, k] >= 0:
+                y = x_loc[plus[n, k]]
+                v = v + coef[n, k, 2] * (q @ y - y @ q)
+        d[n] = v
+    return d

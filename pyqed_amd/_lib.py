@@ -59,6 +59,11 @@ SIGNATURES = {
     "qd_deom_rk4_ado_major": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_double, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "qd_deom_stage": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                              c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_double,
+                              c_double, c_double, c_double, c_int, c_double, c_void_p, c_int, c_int, c_void_p]),
+    "qd_gather_rows": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "qd_deom_trace": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "qd_heom_chain_euler": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_double, c_double, c_double,
                                     c_double, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "qd_sandwich": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),

@@ -292,6 +292,149 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) 
   }
 }
 
+// MFMA tile kernel for 9 <= ns <= 16 (zero-padded to 16 in registers), NM <= 2 bath modes, K <= 21: one wave per
+// ADO.  The stencil regrouped by mode m:
+//   d rho_n = damp_n x - iH x + x iH + sum_m (Q_m SL_m + SR_m Q_m),
+//   SL_m = sum_{k: mode k = m} (cL_k x_{n-e_k} + cP_k x_{n+e_k}),  SR_m = sum_k (cR_k x_{n-e_k} - cP_k x_{n+e_k}),
+// i.e. two complex 16 x 16(1+NM) x 16 GEMMs per ADO on v_mfma_f64_16x16x4_f64:
+//   D  = [-iH | Q_1 .. Q_NM] [x; SL_1 ..]   (B operand = the D-register layout of x and SL: no data movement)
+//   D += [x | SR_1 ..] [iH; Q_1 ..]          (A operand = the transposed layout: one 16 x 17 LDS transpose per block)
+// Every matrix is loaded once in the MFMA D layout (lane l: rows (l>>4) + 4r, column l&15; 4 x 256-B row pieces
+// per load instruction); neighbour loads are branch-free (absent neighbours read the ADO's own row with a zero
+// coefficient) so the compiler can issue them ahead.  The RK4 epilogue is the group kernel's.
+template <int NM>
+__global__ __launch_bounds__(256) void deom_stage_mfma16_kernel(DeomParams p) {
+  extern __shared__ c128 deom_lds[];
+  c128* sH = deom_lds;                            // [16][16] H(t), zero padded
+  c128* sQ = deom_lds + 256;                      // [NM][16][16] Q_m(t)
+  c128* sT = deom_lds + 256 * (1 + NM) + (threadIdx.x >> 6) * (16 * 17);   // this wave's transpose tile
+  const int ns = p.ns, ns2 = ns * ns, K = p.K;
+  for (int e = threadIdx.x; e < 256 * (1 + NM); e += 256) {
+    const int mtx = e >> 8, i = (e >> 4) & 15, j = e & 15;
+    c128 v = cmk(0, 0);
+    if (i < ns && j < ns) {
+      const int q = i * ns + j;
+      if (mtx == 0) v = p.Hdip ? cadd(p.H[q], cmul(p.Hdip[q], p.fs)) : p.H[q];
+      else v = p.Qdip ? cadd(p.Q[(mtx - 1) * ns2 + q], cmul(p.Qdip[(mtx - 1) * ns2 + q], p.fc)) : p.Q[(mtx - 1) * ns2 + q];
+    }
+    deom_lds[e] = v;
+  }
+  const long total = (long)p.B * p.nmax;
+  const long g0 = blockIdx.x * 4L + (threadIdx.x >> 6);
+  const bool valid = g0 < total;                  // out-of-range waves compute a copy and store nothing
+  const long grp = valid ? g0 : total - 1;
+  const int n = (int)(grp % p.nmax);
+  const long hb = grp / p.nmax;
+  const c128* X = p.xin + hb * p.nmax * ns2;
+  const int lane = threadIdx.x & 63, col = lane & 15, rq = lane >> 4;
+  const bool colv = col < ns;
+  auto ld = [&](const c128* M, int r) -> c128 {
+    const int i = rq + 4 * r;
+    return (colv && i < ns) ? M[i * ns + col] : cmk(0, 0);
+  };
+  int myidx = -1;
+  c128 mycf = cmk(0, 0);
+  if (lane < 2 * K) myidx = lane < K ? p.minus[(size_t)n * K + lane] : p.plus[(size_t)n * K + lane - K];
+  if (lane < 3 * K) mycf = p.coef[(size_t)n * K * 3 + lane];
+  const size_t own = (size_t)grp * ns2;
+  c128 x[4], r0[4], a0[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    x[r] = ld(X + (size_t)n * ns2, r);
+    r0[r] = ld(p.rho + own, r);
+    a0[r] = p.stage > 0 ? ld(p.acc + own, r) : cmk(0, 0);
+  }
+  const c128 dmp = p.damp[n];
+  c128 SL[NM][4], SR[NM][4];
+#pragma unroll
+  for (int m = 0; m < NM; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) SL[m][r] = SR[m][r] = cmk(0, 0);
+  auto shc = [&](c128 v, int src) { return cmk(__shfl(v.re, src, 64), __shfl(v.im, src, 64)); };
+#pragma unroll 2
+  for (int k = 0; k < K; ++k) {
+    const int m = NM == 1 ? 0 : p.mode[k];
+    const int im = __shfl(myidx, k, 64), ip = __shfl(myidx, K + k, 64);
+    const c128 cL = im >= 0 ? shc(mycf, 3 * k) : cmk(0, 0);
+    const c128 cR = im >= 0 ? shc(mycf, 3 * k + 1) : cmk(0, 0);
+    const c128 cP = ip >= 0 ? shc(mycf, 3 * k + 2) : cmk(0, 0);
+    const c128* ym = X + (size_t)(im >= 0 ? im : n) * ns2;
+    const c128* yp = X + (size_t)(ip >= 0 ? ip : n) * ns2;
+    c128 vm[4], vp[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      vm[r] = ld(ym, r);
+      vp[r] = ld(yp, r);
+    }
+#pragma unroll
+    for (int mm = 0; mm < NM; ++mm) {
+      if (mm != m) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        SL[mm][r] = cadd(SL[mm][r], cadd(cmul(cL, vm[r]), cmul(cP, vp[r])));
+        SR[mm][r] = cadd(SR[mm][r], csub(cmul(cR, vm[r]), cmul(cP, vp[r])));
+      }
+    }
+  }
+  __syncthreads();  // H(t) / Q(t) in LDS
+  d4 Dre = d4{0.0, 0.0, 0.0, 0.0}, Dim = d4{0.0, 0.0, 0.0, 0.0};
+  auto cmfma = [&](c128 a, c128 b) {  // D += a b (complex, one 16x16x4 k-step)
+    Dre = __builtin_amdgcn_mfma_f64_16x16x4f64(a.re, b.re, Dre, 0, 0, 0);
+    Dim = __builtin_amdgcn_mfma_f64_16x16x4f64(a.re, b.im, Dim, 0, 0, 0);
+    Dre = __builtin_amdgcn_mfma_f64_16x16x4f64(-a.im, b.im, Dre, 0, 0, 0);
+    Dim = __builtin_amdgcn_mfma_f64_16x16x4f64(a.im, b.re, Dim, 0, 0, 0);
+  };
+  // GEMM 1: A = [-iH | Q_m] (lane: row l&15, column 4q + (l>>4)), B = [x; SL_m] in D layout (register q)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) cmfma(cmulmi(sH[(lane & 15) * 16 + 4 * q + rq]), x[q]);
+#pragma unroll
+  for (int m = 0; m < NM; ++m)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cmfma(sQ[m * 256 + (lane & 15) * 16 + 4 * q + rq], SL[m][q]);
+  // GEMM 2: A = [x | SR_m] transposed through LDS, B = [iH; Q_m] (lane: row 4q + (l>>4), column l&15)
+  auto gemm2_block = [&](const c128* Y, const c128* Bm, bool iH) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sT[(rq + 4 * r) * 17 + col] = Y[r];
+    __syncthreads();
+    c128 a[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[q] = sT[(lane & 15) * 17 + 4 * q + rq];
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const c128 b = Bm[(4 * q + rq) * 16 + col];
+      cmfma(a[q], iH ? cmuli(b) : b);
+    }
+  };
+  gemm2_block(x, sH, true);
+#pragma unroll
+  for (int m = 0; m < NM; ++m) gemm2_block(SR[m], sQ + m * 256, false);
+
+  const double dt = p.dt;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = rq + 4 * r;
+    if (!(valid && colv && i < ns)) continue;
+    const c128 d = cadd(cmk(Dre[r], Dim[r]), cmul(dmp, x[r]));
+    const size_t idx = own + (size_t)i * ns + col;
+    if (p.stage == 0) {
+      p.acc[idx] = d;
+      p.xout[idx] = cadd(r0[r], cscale(d, dt / 2));
+    } else if (p.stage == 1) {
+      p.acc[idx] = cadd(a0[r], cscale(d, 2.0));
+      p.xout[idx] = cadd(r0[r], cscale(d, dt / 2));
+    } else if (p.stage == 2) {
+      p.acc[idx] = cadd(a0[r], cscale(d, 2.0));
+      p.xout[idx] = cadd(r0[r], cscale(d, dt));
+    } else {
+      const c128 a = cadd(a0[r], d);
+      const c128 r1 = cadd(r0[r], cscale(cscale(a, dt), 1.0 / 6.0));
+      p.rho_out[idx] = r1;
+      if (p.snap && n == 0) p.snap[(hb * (p.nsteps + 1) + p.step + 1) * ns2 + (size_t)i * ns + col] = r1;
+    }
+  }
+}
+
 __global__ void deom_snap0_kernel(const c128* rho, c128* snap, int B, int nmax, int ns, int nsteps, int bminor) {
   const int ns2 = ns * ns;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < B * ns2; e += gridDim.x * blockDim.x) {
@@ -369,6 +512,57 @@ __global__ __launch_bounds__(256) void heom_chain_sweep_kernel(c128* ados, int n
 using namespace qd;
 
 namespace {
+// Launch one RK4 stage of the hierarchy described by p (kernel chosen from ns, K, nmod, layout).
+int deom_launch_stage(const DeomParams& p, hipStream_t st) {
+  const int ns = p.ns, K = p.K, nmod = p.nmod, B = p.B, nmax = p.nmax, bminor = p.bminor;
+  const size_t ns2 = (size_t)ns * ns;
+  const size_t tot = (size_t)B * nmax * ns2;
+  // group kernel when ns^2 <= 64 lanes and K <= 8; MFMA tile kernel for 9 <= ns <= 16 (nmod <= 2, K <= 21);
+  // else the element kernel (QD_DEOM_MFMA=0 keeps ns > 8 on the element kernel, for A/B runs)
+  int G = 1;
+  while (G < (int)ns2) G *= 2;
+  const bool grp = G <= 64 && K <= 8;
+  const char* mf_env = getenv("QD_DEOM_MFMA");
+  const bool mfma = !grp && !bminor && ns >= 9 && ns <= 16 && nmod <= 2 && K <= 21 && !(mf_env && mf_env[0] == '0');
+  QD_CHECK_ARG(!bminor || grp, "qd_deom_rk4_ado_major: needs ns^2 <= 64 and K <= 8 (group kernel)");
+  const size_t nthreads = grp ? (size_t)B * nmax * G : tot;
+  // A small hierarchy (one at L = 12, K = 5: 24.8k lanes) as 256-thread blocks would occupy ~100 of the
+  // 256 CUs, each CU then issuing the loads of 4 waves; 64-thread blocks spread the same lanes over every
+  // CU.  QD_DEOM_TPB overrides (64 or 256) for A/B runs.
+  int tpb = (nthreads + DEOM_TPB - 1) / DEOM_TPB < 1024 ? 64 : DEOM_TPB;
+  if (const char* s = getenv("QD_DEOM_TPB")) tpb = atoi(s) == 64 ? 64 : DEOM_TPB;
+  if (!grp) tpb = DEOM_TPB;
+  const int grid = (int)((nthreads + tpb - 1) / tpb);
+  const size_t lds = (size_t)(1 + nmod) * ns2 * sizeof(c128);   // H(t), Q(t) of the group kernel
+  auto launch_stage = [&]() {
+    if (mfma) {
+      const int wg = (int)(((long)B * nmax + 3) / 4);
+      const size_t lds_m = (size_t)(256 * (1 + nmod) + 4 * 16 * 17) * sizeof(c128);
+      if (nmod == 1) hipLaunchKernelGGL(deom_stage_mfma16_kernel<1>, dim3(wg), dim3(256), lds_m, st, p);
+      else hipLaunchKernelGGL(deom_stage_mfma16_kernel<2>, dim3(wg), dim3(256), lds_m, st, p);
+      return;
+    }
+    if (!grp) {
+      hipLaunchKernelGGL(deom_stage_kernel, dim3(grid), dim3(tpb), 0, st, p);
+      return;
+    }
+    switch (G) {
+      case 1: hipLaunchKernelGGL((deom_stage_grp_kernel<1, 8, false>), dim3(grid), dim3(tpb), lds, st, p); break;
+      case 4:  // ns = 2; registers sized to K (ym/yp/indices scale with KMAX)
+        if (K <= 4) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 4, true>), dim3(grid), dim3(tpb), lds, st, p);
+        else if (K <= 6) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 6, true>), dim3(grid), dim3(tpb), lds, st, p);
+        else hipLaunchKernelGGL((deom_stage_grp_kernel<4, 8, true>), dim3(grid), dim3(tpb), lds, st, p);
+        break;
+      case 16: hipLaunchKernelGGL((deom_stage_grp_kernel<16, 8, false>), dim3(grid), dim3(tpb), lds, st, p); break;
+      case 32: hipLaunchKernelGGL((deom_stage_grp_kernel<32, 8, false>), dim3(grid), dim3(tpb), lds, st, p); break;
+      default: hipLaunchKernelGGL((deom_stage_grp_kernel<64, 8, false>), dim3(grid), dim3(tpb), lds, st, p); break;
+    }
+  };
+  launch_stage();
+  QD_HIP(hipGetLastError());
+  return QD_OK;
+}
+
 int deom_run(qd_c128* ados, int B, int nmax, int K, int ns, const int32_t* minus, const int32_t* plus,
              const qd_c128* coef, const qd_c128* damp, const int32_t* mode, int nmod, const qd_c128* H,
              const qd_c128* Hdip, const qd_c128* Q, const qd_c128* Qdip, const qd_c128* fsys, const qd_c128* fcoup,
@@ -422,37 +616,6 @@ int deom_run(qd_c128* ados, int B, int nmax, int K, int ns, const int32_t* minus
   p.nsteps = nsteps;
   p.dt = dt;
   p.bminor = bminor;
-  // group kernel when ns^2 <= 64 lanes and K <= 8; else the element kernel
-  int G = 1;
-  while (G < (int)ns2) G *= 2;
-  const bool grp = G <= 64 && K <= 8;
-  QD_CHECK_ARG(!bminor || grp, "qd_deom_rk4_ado_major: needs ns^2 <= 64 and K <= 8 (group kernel)");
-  const size_t nthreads = grp ? (size_t)B * nmax * G : tot;
-  // A small hierarchy (one at L = 12, K = 5: 24.8k lanes) as 256-thread blocks would occupy ~100 of the
-  // 256 CUs, each CU then issuing the loads of 4 waves; 64-thread blocks spread the same lanes over every
-  // CU.  QD_DEOM_TPB overrides (64 or 256) for A/B runs.
-  int tpb = (nthreads + DEOM_TPB - 1) / DEOM_TPB < 1024 ? 64 : DEOM_TPB;
-  if (const char* s = getenv("QD_DEOM_TPB")) tpb = atoi(s) == 64 ? 64 : DEOM_TPB;
-  if (!grp) tpb = DEOM_TPB;
-  const int grid = (int)((nthreads + tpb - 1) / tpb);
-  const size_t lds = (size_t)(1 + nmod) * ns2 * sizeof(c128);   // H(t), Q(t) of the group kernel
-  auto launch_stage = [&]() {
-    if (!grp) {
-      hipLaunchKernelGGL(deom_stage_kernel, dim3(grid), dim3(tpb), 0, st, p);
-      return;
-    }
-    switch (G) {
-      case 1: hipLaunchKernelGGL((deom_stage_grp_kernel<1, 8, false>), dim3(grid), dim3(tpb), lds, st, p); break;
-      case 4:  // ns = 2; registers sized to K (ym/yp/indices scale with KMAX)
-        if (K <= 4) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 4, true>), dim3(grid), dim3(tpb), lds, st, p);
-        else if (K <= 6) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 6, true>), dim3(grid), dim3(tpb), lds, st, p);
-        else hipLaunchKernelGGL((deom_stage_grp_kernel<4, 8, true>), dim3(grid), dim3(tpb), lds, st, p);
-        break;
-      case 16: hipLaunchKernelGGL((deom_stage_grp_kernel<16, 8, false>), dim3(grid), dim3(tpb), lds, st, p); break;
-      case 32: hipLaunchKernelGGL((deom_stage_grp_kernel<32, 8, false>), dim3(grid), dim3(tpb), lds, st, p); break;
-      default: hipLaunchKernelGGL((deom_stage_grp_kernel<64, 8, false>), dim3(grid), dim3(tpb), lds, st, p); break;
-    }
-  };
   static const int stage_time[4] = {0, 1, 1, 2};
   for (int s = 0; s < nsteps; ++s) {
     p.step = s;
@@ -463,8 +626,7 @@ int deom_run(qd_c128* ados, int B, int nmax, int K, int ns, const int32_t* minus
       const int ti = s * 3 + stage_time[stage];
       p.fs = fs_h ? cmk(fs_h[ti].re, fs_h[ti].im) : cmk(0, 0);
       p.fc = fc_h ? cmk(fc_h[ti].re, fc_h[ti].im) : cmk(0, 0);
-      launch_stage();
-      QD_HIP(hipGetLastError());
+      if (int rc2 = deom_launch_stage(p, st)) return rc2;
     }
   }
   if (trace) {
@@ -495,6 +657,85 @@ extern "C" int qd_deom_rk4_ado_major(qd_c128* ados, int B, int nmax, int K, int 
                                      int ne, qd_c128* trace, void* stream) {
   return deom_run(ados, B, nmax, K, ns, minus, plus, coef, damp, mode, nmod, H, Hdip, Q, Qdip, fsys, fcoup, dt, nsteps,
                   rho_sys, E, ne, trace, stream, 1);
+}
+
+// One RK4 stage over a band of ADOs (tier-banded sharding of one hierarchy): rows [0, n_own) of
+// rho / xin / xout are this band's ADOs, rows [n_own, n_loc) of xin the halo copies of the neighbours other bands
+// own; minus / plus [n_own][K] hold LOCAL row indices (-1 = absent).  Stage s reads xin (s = 0: rho), writes the
+// owned rows of xout (s < 3) and acc, and at s = 3 the owned rows of rho; snap (band owning ADO 0 only) receives
+// rho_0 after the step.  Same kernels and arithmetic as qd_deom_rk4.
+extern "C" int qd_deom_stage(qd_c128* rho, const qd_c128* xin, qd_c128* xout, qd_c128* acc, int n_own, int K, int ns,
+                             const int32_t* minus, const int32_t* plus, const qd_c128* coef, const qd_c128* damp,
+                             const int32_t* mode, int nmod, const qd_c128* H, const qd_c128* Hdip, const qd_c128* Q,
+                             const qd_c128* Qdip, double fs_re, double fs_im, double fc_re, double fc_im, int stage,
+                             double dt, qd_c128* snap, int step, int nsteps, void* stream) {
+  QD_CHECK_ARG(rho && xin && acc && minus && plus && coef && damp && mode && H && Q, "qd_deom_stage: null pointer");
+  QD_CHECK_ARG(stage >= 0 && stage <= 3 && (stage == 3 || xout), "qd_deom_stage: bad stage %d / null xout", stage);
+  QD_CHECK_ARG(n_own >= 1 && K >= 1, "qd_deom_stage: bad sizes n_own=%d K=%d", n_own, K);
+  QD_CHECK_ARG(ns >= 1 && ns <= DEOM_MAX_NS, "qd_deom_stage: ns=%d outside [1, %d]", ns, DEOM_MAX_NS);
+  QD_CHECK_ARG(nmod >= 1 && nmod <= DEOM_MAX_NMOD, "qd_deom_stage: nmod=%d outside [1, %d]", nmod, DEOM_MAX_NMOD);
+  QD_CHECK_ARG(!snap || (step >= 0 && step < nsteps), "qd_deom_stage: snapshot step %d outside [0, %d)", step, nsteps);
+  DeomParams p;
+  p.rho = (const c128*)rho;
+  p.rho_out = (c128*)rho;
+  p.xin = (const c128*)xin;
+  p.xout = (c128*)xout;
+  p.acc = (c128*)acc;
+  p.minus = minus;
+  p.plus = plus;
+  p.coef = (const c128*)coef;
+  p.damp = (const c128*)damp;
+  p.mode = mode;
+  p.H = (const c128*)H;
+  p.Hdip = (const c128*)Hdip;
+  p.Q = (const c128*)Q;
+  p.Qdip = (const c128*)Qdip;
+  p.fs = cmk(fs_re, fs_im);
+  p.fc = cmk(fc_re, fc_im);
+  p.snap = (c128*)snap;
+  p.B = 1;
+  p.nmax = n_own;
+  p.K = K;
+  p.ns = ns;
+  p.nmod = nmod;
+  p.stage = stage;
+  p.step = step;
+  p.nsteps = nsteps;
+  p.dt = dt;
+  p.bminor = 0;
+  return deom_launch_stage(p, (hipStream_t)stream);
+}
+
+namespace {
+__global__ void gather_rows_kernel(const c128* src, const int32_t* idx, int n, int row, c128* dst) {
+  const size_t tot = (size_t)n * row;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x)
+    dst[e] = src[(size_t)idx[e / row] * row + e % row];
+}
+}  // namespace
+
+// dst[i][:] = src[idx[i]][:] for i < n, rows of `row_elems` complex (packs a band's halo rows for the exchange)
+extern "C" int qd_gather_rows(const qd_c128* src, const int32_t* idx, int n, int row_elems, qd_c128* dst,
+                              void* stream) {
+  QD_CHECK_ARG(n >= 0 && row_elems >= 1, "qd_gather_rows: bad sizes n=%d row=%d", n, row_elems);
+  if (n == 0) return QD_OK;
+  QD_CHECK_ARG(src && idx && dst, "qd_gather_rows: null pointer");
+  const size_t tot = (size_t)n * row_elems;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((int)std::min<size_t>((tot + 255) / 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, (const c128*)src, idx, n, row_elems, (c128*)dst);
+  QD_HIP(hipGetLastError());
+  return QD_OK;
+}
+
+// obs[s][m] = Tr(E_m rho_0(s)) for s < nsnap (DEOMSolver.run's Tr(p1 rho_0), heom/deom.py:1100,1113)
+extern "C" int qd_deom_trace(const qd_c128* snap, const qd_c128* E, int ne, int nsnap, int ns, qd_c128* obs,
+                             void* stream) {
+  QD_CHECK_ARG(snap && E && obs && ne >= 1 && nsnap >= 1 && ns >= 1, "qd_deom_trace: bad arguments");
+  const int n = nsnap * ne;
+  hipLaunchKernelGGL(deom_trace_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0,
+                     (hipStream_t)stream, (const c128*)snap, (const c128*)E, ne, 1, ns, nsnap, (c128*)obs);
+  QD_HIP(hipGetLastError());
+  return QD_OK;
 }
 
 extern "C" int qd_heom_chain_euler(qd_c128* ados, int B, int nado, int ns, const qd_c128* H, const qd_c128* Q,

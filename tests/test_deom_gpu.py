@@ -190,3 +190,72 @@ def test_deom_ado_major_batch_layout(ns, B, pulse, monkeypatch):
                             np.zeros((1, ns, ns)), lambda t: 0, (bath.etal, bath.etar, bath.etaa, bath.expn), L,
                             rho0[b], dt, nt)
         assert relerr(out["1"][0][b], ref) < TOL, b
+
+
+def _multi_mode_model(ns, nmod, npsd, L, seed=3):
+    from pyqed_amd.deom import Bath, DEOMSolver
+    rng = np.random.default_rng(seed)
+    A = rng.standard_normal((ns, ns)) + 1j * rng.standard_normal((ns, ns))
+    H = (A + A.conj().T) / 2 / np.sqrt(ns)
+    Qs = []
+    for m in range(nmod):
+        B = rng.standard_normal((ns, ns))
+        Qs.append(((B + B.T) / 2 / np.sqrt(ns)).astype(complex))
+    w = sp.symbols(r"\omega", real=True)
+    spes = [2 * lam * gam * w / (gam ** 2 + w ** 2) for lam, gam in [(0.4, 1.0), (0.2, 2.0)][:nmod]]
+    mode = [m for m in range(nmod) for _ in range(1 + npsd)]
+    bath = Bath(spes, w, [1.0] * nmod, [npsd] * nmod, mode)
+    sdip = np.diag(np.linspace(0, 1, ns)).astype(complex)
+    fs = lambda t: 0.2 * np.cos(3 * t)
+    fc = lambda t: 0.05 * np.sin(t)
+    cdip = np.array([0.3 * q for q in Qs])
+    sol = DEOMSolver(H, sdip, bath, np.array(Qs), cdip, fs, fc, L)
+    rho0 = np.zeros((ns, ns), complex)
+    rho0[0, 0] = 1
+    return sol, bath, H, np.array(Qs), sdip, cdip, fs, fc, rho0, mode
+
+
+@pytest.mark.parametrize("ns,nmod,npsd,L", [(16, 1, 1, 3), (12, 2, 1, 2), (9, 1, 2, 3), (16, 2, 0, 3)])
+def test_deom_mfma16_matches_oracle(ns, nmod, npsd, L, monkeypatch):
+    """The MFMA tile kernel (9 <= ns <= 16: two 16 x 16(1+nmod) x 16 complex GEMMs per ADO on v_mfma_f64_16x16x4_f64,
+    zero padding to 16) for 1 and 2 bath modes with driven H(t), Q(t): against the oracle (oracle.deom.run restates
+    DEOMSolver.run, heom/deom.py:1072-1114) and against the element-per-thread kernel (QD_DEOM_MFMA=0)."""
+    from oracle import deom as od
+    sol, bath, H, Qs, sdip, cdip, fs, fc, rho0, mode = _multi_mode_model(ns, nmod, npsd, L)
+    nt, dt = 4, 0.02
+    P1 = np.eye(ns, dtype=complex)[::-1]
+    _, tr_ref, ados_ref = od.run(H, sdip, fs, Qs, cdip, fc, (bath.etal, bath.etar, bath.etaa, bath.expn), L, rho0,
+                                 dt, nt, P1, mode=mode)
+    out = {}
+    for env in ("1", "0"):
+        monkeypatch.setenv("QD_DEOM_MFMA", env)
+        t, tr = sol.run_batch(rho0[None], dt, nt, P1)
+        out[env] = (tr[0], sol.ddos[0].copy())
+    assert relerr(out["1"][0], tr_ref) < TOL
+    assert relerr(out["1"][1], ados_ref) < TOL
+    assert relerr(out["1"][1], out["0"][1]) < 1e-13
+
+
+@pytest.mark.parametrize("ns,npsd,L,nbands", [(2, 4, 12, 8), (2, 1, 5, 3), (12, 1, 4, 4), (16, 2, 3, 2)])
+def test_deom_tier_bands_loopback_matches_single(ns, npsd, L, nbands):
+    """Tier-banded sharding on the GPU (pyqed_amd.deom_shard, qd_deom_stage + qd_gather_rows, all bands in one
+    process with device-side halo copies): Tr(p1 rho_0) and the final hierarchy equal the single-process
+    qd_deom_rk4 run (same kernels per ADO).  (2, 4, 12, 8) is the bench hierarchy (6188 ADOs) over 8 bands."""
+    from pyqed_amd.deom_shard import ShardedDEOM
+    if ns == 2:
+        g = {"H": np.array([[1, 1], [1, -1]], complex), "Q": np.array([[[0, 1], [1, 0]]], complex),
+             "sdip": np.array([[0, 1], [1, 0]], complex), "cdip": np.array([np.diag([1.0, -1.0]).astype(complex)]),
+             "lam": 0.5, "gam": 1.0, "beta": 1.0, "npsd": npsd, "lmax": L}
+        sol = _solver(g, True)
+        rho0 = np.zeros((2, 2), complex)
+        rho0[0, 0] = 1
+    else:
+        sol, *_, rho0, _ = _multi_mode_model(ns, 1, npsd, L)
+    nt, dt = 5, 0.005
+    P1 = np.eye(ns, dtype=complex)[::-1].copy()
+    sh = ShardedDEOM(sol, nbands=nbands, loopback=True)
+    t, tr = sh.run(rho0, dt, nt, P1)
+    ados = sh.gather_ados()
+    _, tr1 = sol.run_batch(rho0[None], dt, nt, P1)
+    assert relerr(tr, tr1[0]) < 1e-13
+    assert relerr(ados, sol.ddos[0]) < 1e-13

@@ -209,3 +209,113 @@ def test_reduce_pipeline_gloo():
     assert sorted(got) == list(range(5))
     for g in range(5):
         assert np.allclose(got[g], (g + 1) * full, rtol=1e-12, atol=1e-12 * np.abs(full).max()), g
+
+
+# ---------------------------------------------------------------- tier-banded DEOM
+def _deom_model(ns=3, npsd=2, L=4, pulsed=True):
+    import sympy as sp
+    from pyqed_amd.deom import Bath, DEOMSolver
+    rng = np.random.default_rng(17)
+    A = rng.standard_normal((ns, ns)) + 1j * rng.standard_normal((ns, ns))
+    H = (A + A.conj().T) / 2
+    Qm = np.diag(np.linspace(-1, 1, ns)).astype(complex)
+    w = sp.symbols(r"\omega", real=True)
+    bath = Bath([2 * 0.5 * 1.0 * w / (1.0 + w ** 2)], w, [1.0], [npsd], [0] * (1 + npsd))
+    sdip = np.roll(np.eye(ns), 1, axis=1).astype(complex)
+    sdip = sdip + sdip.T
+    fs = (lambda t: 0.3 * np.sin(2 * t)) if pulsed else None
+    fc = (lambda t: 0.1 * np.cos(t)) if pulsed else None
+    cdip = np.array([0.5 * Qm]) if pulsed else None
+    sol = DEOMSolver(H, sdip if pulsed else None, bath, np.array([Qm]), cdip, fs, fc, L)
+    rho0 = np.zeros((ns, ns), complex)
+    rho0[0, 0] = 1
+    return sol, bath, H, Qm, sdip, cdip, fs, fc, rho0
+
+
+def _host_stage(band, stage, step, dt, fs, fc, xin, xout):
+    """Host (numpy) restatement of qd_deom_stage's arithmetic for a band: oracle.deom.band_rhs + the kernel's RK4
+    bookkeeping (deom.py:725-766 order)."""
+    from oracle import deom as od
+    ns = band.ns
+    p = band.plan
+    H = band.H.numpy() + (band.Hdip.numpy() * fs if band.Hdip is not None else 0)
+    Q = band.Q.numpy() + (band.Qdip.numpy() * fc if band.Qdip is not None else 0)
+    d = od.band_rhs(xin.numpy(), p.n_own, p.minus, p.plus, band.coef.numpy(), band.damp.numpy(), band.mode.numpy(),
+                    H, Q)
+    r0 = band.bufs["rho"][:p.n_own].numpy()
+    acc = band.acc.numpy()
+    if stage == 0:
+        acc[...] = d
+        xout[:p.n_own] = torch.from_numpy(r0 + d * (dt / 2))
+    elif stage == 1:
+        acc += d * 2.0
+        xout[:p.n_own] = torch.from_numpy(r0 + d * (dt / 2))
+    elif stage == 2:
+        acc += d * 2.0
+        xout[:p.n_own] = torch.from_numpy(r0 + d * dt)
+    else:
+        band.bufs["rho"][:p.n_own] = torch.from_numpy(r0 + (acc + d) * dt / 6.0)
+
+
+def _worker_deom_bands(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pyqed_amd.deom_shard import ShardedDEOM
+    sol, *_, rho0 = _deom_model()
+    sh = ShardedDEOM(sol, stage_fn=_host_stage, device="cpu")
+    P1 = np.diag([1.0, 0, 0]).astype(complex)
+    t, tr = sh.run(rho0, 0.01, 6, P1)
+    ados = sh.gather_ados()
+    q.put((rank, tr, ados, [(p.lo, p.hi, len(p.halo), sorted(p.recv), sorted(p.send)) for p in sh.plans]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_deom_tier_bands_gloo():
+    """One hierarchy (ns = 3, K = 3, L = 4: 35 ADOs, driven H(t), Q(t)) split into 2 tier bands over 2 gloo ranks,
+    halo rows exchanged by send / recv after every RK4 stage (TorchExchange): Tr(p1 rho_0) on rank 0 and the
+    gathered final hierarchy equal the single-process oracle run (oracle.deom.run restates DEOMSolver.run,
+    heom/deom.py:1072-1114)."""
+    from oracle import deom as od
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_deom_bands, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sol, bath, H, Qm, sdip, cdip, fs, fc, rho0 = _deom_model()
+    P1 = np.diag([1.0, 0, 0]).astype(complex)
+    _, tr_ref, ados_ref = od.run(H, sdip, fs, np.array([Qm]), cdip, fc, (bath.etal, bath.etar, bath.etaa, bath.expn),
+                                 4, rho0, 0.01, 6, P1)
+    assert res[1][1] is None and res[1][2] is None
+    assert np.allclose(res[0][1], tr_ref, rtol=1e-12, atol=1e-13)
+    assert np.allclose(res[0][2], ados_ref, rtol=1e-11, atol=1e-13)
+    plans = res[0][3]
+    assert plans[0][:2] == (0, 17) and plans[1][:2] == (17, 35)
+    assert plans[0][3] == [1] and plans[1][3] == [0]          # each band reads halo rows from the other
+
+
+def test_deom_band_plans_properties():
+    """make_plans on the bench hierarchy (L = 12, K = 5, 6188 ADOs) over 8 bands: the bands tile [0, nmax), every
+    stencil neighbour of an owned ADO is either owned or in the halo, local tables point at the right global rows,
+    and the send lists are the receivers' halo rows."""
+    from pyqed_amd.deom import ado_tables
+    from pyqed_amd.deom_shard import make_plans
+    keys, minus, plus, _ = ado_tables(12, 5)
+    plans = make_plans(minus, plus, 8)
+    assert plans[0].lo == 0 and plans[-1].hi == len(keys)
+    assert all(a.hi == b.lo for a, b in zip(plans, plans[1:]))
+    for p in plans:
+        glob = np.concatenate([np.arange(p.lo, p.hi), p.halo])
+        for tab, loc in ((minus, p.minus), (plus, p.plus)):
+            t = tab[p.lo:p.hi]
+            assert np.array_equal(loc < 0, t < 0)
+            assert np.array_equal(glob[loc[loc >= 0]], t[t >= 0])
+        for q, (s, c) in p.recv.items():
+            assert np.array_equal(plans[q].send[p.rank] + plans[q].lo, p.halo[s:s + c])
