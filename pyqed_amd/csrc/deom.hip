@@ -48,7 +48,9 @@ struct DeomParams {
   int B, nmax, K, ns, nmod, stage, step, nsteps;
   double dt;
   int bminor;  // ADO-major layout [nmax][B][ns][ns] (hierarchy index fastest; group kernel only)
+  int xsplit;  // group kernel: 0 = flat lane numbering; X in {1, 2, 4, 8} = hierarchies dealt to X block classes
 };
+
 
 __global__ __launch_bounds__(DEOM_TPB) void deom_stage_kernel(DeomParams p) {
   __shared__ c128 sH[DEOM_MAX_NS * DEOM_MAX_NS];
@@ -140,17 +142,32 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) 
   c128* sH = deom_lds;
   c128* sQ = deom_lds + p.ns * p.ns;
   const int ns = NS2 ? 2 : p.ns, ns2 = ns * ns, K = p.K;
-  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  const size_t ngrp = (size_t)p.B * p.nmax;
-  const size_t grp = t / G;                 // b * nmax + n
-  const int e = (int)(t % G);
-  const bool live = grp < ngrp;             // uniform within a group
+  // [B][nmax] layout: an ADO's neighbours are rows of its own hierarchy;
+  // [nmax][B] layout (bminor): a wave holds one ADO of up to 64 / G hierarchies, so its index / prefactor loads
+  // are one request per wave and each neighbour read is one contiguous run of 64-B rows.
+  // xsplit = X > 0: block class c = blockIdx % 8 < X owns hierarchies [c B/X, (c+1) B/X) for every ADO, classes
+  // >= X exit at once.  Blocks b and b + 8 share an XCD (round-robin dispatch, MI355X_MICROARCH.md "Workgroup
+  // dispatch"), so one XCD reads only its own hierarchies' rows and the 2K neighbour reads of an ADO hit that
+  // XCD's L2 instead of coming from the Infinity Cache eight times over.  Placement is a speed matter only.
+  // 32-bit lane arithmetic (the host checks B nmax G < 2^31): one integer division per lane
+  unsigned cls = 0, u;
+  if (p.xsplit > 0) {
+    cls = blockIdx.x & 7;
+    if (cls >= (unsigned)p.xsplit) return;  // whole block exits before any barrier
+    u = (blockIdx.x >> 3) * blockDim.x + threadIdx.x;
+  } else {
+    u = blockIdx.x * blockDim.x + threadIdx.x;
+  }
+  const unsigned Bx = p.xsplit > 0 ? (unsigned)(p.B / p.xsplit) : (unsigned)p.B;
+  const unsigned lgrp = u / G;              // b nmax + n, or n B + b (bminor), within the class
+  const int e = (int)(u % G);
+  const bool live = lgrp < Bx * (unsigned)p.nmax;   // uniform within a group
+  const unsigned q = p.bminor ? Bx : (unsigned)p.nmax;
+  const unsigned hi = lgrp / q, lo = lgrp - hi * q;
+  const int n = live ? (int)(p.bminor ? hi : lo) : 0;
+  const size_t hb = (size_t)cls * Bx + (live ? (p.bminor ? lo : hi) : 0);   // hierarchy b
+  const size_t grp = p.bminor ? (size_t)n * p.B + hb : hb * p.nmax + n;     // flat row of rho / acc / xout
   const bool valid = live && e < ns2;
-  // [B][nmax] layout: grp = b nmax + n, an ADO's neighbours are rows of its own hierarchy;
-  // [nmax][B] layout (bminor): grp = n B + b, a wave holds one ADO of 64 / G hierarchies, so its index /
-  // prefactor loads are one request per wave and each neighbour read is one contiguous 64 / G x 64-B run
-  const int n = live ? (int)(p.bminor ? grp / p.B : grp % p.nmax) : 0;
-  const size_t hb = live ? (p.bminor ? grp % p.B : grp / p.nmax) : 0;   // hierarchy b
   const size_t rs = p.bminor ? (size_t)p.B * ns2 : (size_t)ns2;         // ADO row stride
   const int ee = e < ns2 ? e : 0;           // padding lanes shadow element 0
   const c128* X = p.xin + (p.bminor ? hb * ns2 : hb * p.nmax * ns2);
@@ -249,29 +266,36 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) 
     comm = cadd(comm, csub(cmul(sH[i * ns + l], colv(own, l)), cmul(rowv(own, l), sH[l * ns + j])));
   });
   d = cadd(d, cmulmi(comm));
+  // Dissipaton terms regrouped by bath mode m (as the MFMA tile kernel below):
+  //   sum_{k: mode m} cL y_- Q.. = Q_m SL_m + SR_m Q_m,  SL_m = sum_k (cL_k y_{n-e_k} + cP_k y_{n+e_k}),
+  //   SR_m = sum_k (cR_k y_{n-e_k} - cP_k y_{n+e_k}),
+  // so a lane scales its own neighbour elements per k (absent neighbours were loaded as 0) and the 2 x 2 ... ns x ns
+  // products and their lane exchanges run once per run of equal modes instead of three times per k.
+  c128 SL = cmk(0, 0), SR = cmk(0, 0);
+  auto flush = [&](int m) {
+    const c128* Qm = sQ + m * ns2;
+    c128 t = cmk(0, 0);
+    for_l([&](int l) { t = cadd(t, cadd(cmul(Qm[i * ns + l], colv(SL, l)), cmul(rowv(SR, l), Qm[l * ns + j]))); });
+    d = cadd(d, t);
+  };
+  int mcur = p.mode[0];
 #pragma unroll
   for (int k = 0; k < KMAX; ++k) {
     if (k >= K) break;
-    const c128* Qm = sQ + p.mode[k] * ns2;
+    const int m = p.mode[k];
+    if (m != mcur) {   // wave-uniform
+      flush(mcur);
+      SL = SR = cmk(0, 0);
+      mcur = m;
+    }
     const c128 cL = bc(lc[(3 * k) / G], (3 * k) % G);
     const c128 cR = bc(lc[(3 * k + 1) / G], (3 * k + 1) % G);
     const c128 cP = bc(lc[(3 * k + 2) / G], (3 * k + 2) % G);
-    if (im[k] >= 0) {
-      c128 qy = cmk(0, 0), yq = cmk(0, 0);
-      for_l([&](int l) {
-        qy = cadd(qy, cmul(Qm[i * ns + l], colv(ym[k], l)));
-        yq = cadd(yq, cmul(rowv(ym[k], l), Qm[l * ns + j]));
-      });
-      d = cadd(d, cadd(cmul(cL, qy), cmul(cR, yq)));
-    }
-    if (ip[k] >= 0) {
-      c128 c = cmk(0, 0);
-      for_l([&](int l) {
-        c = cadd(c, csub(cmul(Qm[i * ns + l], colv(yp[k], l)), cmul(rowv(yp[k], l), Qm[l * ns + j])));
-      });
-      d = cadd(d, cmul(cP, c));
-    }
+    const c128 py = cmul(cP, yp[k]);
+    SL = cadd(SL, cadd(cmul(cL, ym[k]), py));
+    SR = cadd(SR, csub(cmul(cR, ym[k]), py));
   }
+  flush(mcur);
   if (!valid) return;
 
   const double dt = p.dt;
@@ -525,6 +549,7 @@ int deom_launch_stage(const DeomParams& p, hipStream_t st) {
   const char* mf_env = getenv("QD_DEOM_MFMA");
   const bool mfma = !grp && !bminor && ns >= 9 && ns <= 16 && nmod <= 2 && K <= 21 && !(mf_env && mf_env[0] == '0');
   QD_CHECK_ARG(!bminor || grp, "qd_deom_rk4_ado_major: needs ns^2 <= 64 and K <= 8 (group kernel)");
+  QD_CHECK_ARG(!grp || (size_t)B * nmax * G < (1u << 31), "qd_deom_rk4: B nmax = %zu ADO rows exceed the 32-bit lane range", (size_t)B * nmax);
   const size_t nthreads = grp ? (size_t)B * nmax * G : tot;
   // A small hierarchy (one at L = 12, K = 5: 24.8k lanes) as 256-thread blocks would occupy ~100 of the
   // 256 CUs, each CU then issuing the loads of 4 waves; 64-thread blocks spread the same lanes over every
@@ -532,30 +557,46 @@ int deom_launch_stage(const DeomParams& p, hipStream_t st) {
   int tpb = (nthreads + DEOM_TPB - 1) / DEOM_TPB < 1024 ? 64 : DEOM_TPB;
   if (const char* s = getenv("QD_DEOM_TPB")) tpb = atoi(s) == 64 ? 64 : DEOM_TPB;
   if (!grp) tpb = DEOM_TPB;
-  const int grid = (int)((nthreads + tpb - 1) / tpb);
+  int grid = (int)((nthreads + tpb - 1) / tpb);
+  // XCD classes for the group kernel (p.xsplit, see the kernel): batches of 8k hierarchies are dealt over the
+  // 8 block classes by default; QD_DEOM_XCD = 0 (flat), 1, 2, 4 or 8 overrides where B allows it.
+  DeomParams q = p;
+  q.xsplit = 0;
+  if (grp) {
+    int X = (B >= 8 && B % 8 == 0) ? 8 : 0;
+    if (const char* s = getenv("QD_DEOM_XCD")) {
+      const int v = atoi(s);
+      X = (v == 1 || v == 2 || v == 4 || v == 8) && B % v == 0 ? v : 0;
+    }
+    if (X > 0) {
+      q.xsplit = X;
+      const size_t per = (size_t)(B / X) * nmax * G;   // lanes per class
+      grid = 8 * (int)((per + tpb - 1) / tpb);
+    }
+  }
   const size_t lds = (size_t)(1 + nmod) * ns2 * sizeof(c128);   // H(t), Q(t) of the group kernel
   auto launch_stage = [&]() {
     if (mfma) {
       const int wg = (int)(((long)B * nmax + 3) / 4);
       const size_t lds_m = (size_t)(256 * (1 + nmod) + 4 * 16 * 17) * sizeof(c128);
-      if (nmod == 1) hipLaunchKernelGGL(deom_stage_mfma16_kernel<1>, dim3(wg), dim3(256), lds_m, st, p);
-      else hipLaunchKernelGGL(deom_stage_mfma16_kernel<2>, dim3(wg), dim3(256), lds_m, st, p);
+      if (nmod == 1) hipLaunchKernelGGL(deom_stage_mfma16_kernel<1>, dim3(wg), dim3(256), lds_m, st, q);
+      else hipLaunchKernelGGL(deom_stage_mfma16_kernel<2>, dim3(wg), dim3(256), lds_m, st, q);
       return;
     }
     if (!grp) {
-      hipLaunchKernelGGL(deom_stage_kernel, dim3(grid), dim3(tpb), 0, st, p);
+      hipLaunchKernelGGL(deom_stage_kernel, dim3(grid), dim3(tpb), 0, st, q);
       return;
     }
     switch (G) {
-      case 1: hipLaunchKernelGGL((deom_stage_grp_kernel<1, 8, false>), dim3(grid), dim3(tpb), lds, st, p); break;
+      case 1: hipLaunchKernelGGL((deom_stage_grp_kernel<1, 8, false>), dim3(grid), dim3(tpb), lds, st, q); break;
       case 4:  // ns = 2; registers sized to K (ym/yp/indices scale with KMAX)
-        if (K <= 4) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 4, true>), dim3(grid), dim3(tpb), lds, st, p);
-        else if (K <= 6) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 6, true>), dim3(grid), dim3(tpb), lds, st, p);
-        else hipLaunchKernelGGL((deom_stage_grp_kernel<4, 8, true>), dim3(grid), dim3(tpb), lds, st, p);
+        if (K <= 4) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 4, true>), dim3(grid), dim3(tpb), lds, st, q);
+        else if (K <= 6) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 6, true>), dim3(grid), dim3(tpb), lds, st, q);
+        else hipLaunchKernelGGL((deom_stage_grp_kernel<4, 8, true>), dim3(grid), dim3(tpb), lds, st, q);
         break;
-      case 16: hipLaunchKernelGGL((deom_stage_grp_kernel<16, 8, false>), dim3(grid), dim3(tpb), lds, st, p); break;
-      case 32: hipLaunchKernelGGL((deom_stage_grp_kernel<32, 8, false>), dim3(grid), dim3(tpb), lds, st, p); break;
-      default: hipLaunchKernelGGL((deom_stage_grp_kernel<64, 8, false>), dim3(grid), dim3(tpb), lds, st, p); break;
+      case 16: hipLaunchKernelGGL((deom_stage_grp_kernel<16, 8, false>), dim3(grid), dim3(tpb), lds, st, q); break;
+      case 32: hipLaunchKernelGGL((deom_stage_grp_kernel<32, 8, false>), dim3(grid), dim3(tpb), lds, st, q); break;
+      default: hipLaunchKernelGGL((deom_stage_grp_kernel<64, 8, false>), dim3(grid), dim3(tpb), lds, st, q); break;
     }
   };
   launch_stage();

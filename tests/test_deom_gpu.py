@@ -192,6 +192,40 @@ def test_deom_ado_major_batch_layout(ns, B, pulse, monkeypatch):
         assert relerr(out["1"][0][b], ref) < TOL, b
 
 
+@pytest.mark.parametrize("ns,B", [(2, 16), (2, 1), (3, 8)])
+def test_deom_xcd_block_classes(ns, B, monkeypatch):
+    """Hierarchies dealt to XCD block classes (QD_DEOM_XCD = 1/2/4/8; default 8 when 8 | B) in both batch layouts:
+    only the lane -> (ADO, hierarchy) map changes, so every split must give bit-identical histories and final ADOs to
+    the flat numbering (QD_DEOM_XCD=0), and match the oracle (heom/deom.py:1072-1114)."""
+    from oracle import deom as od
+    from pyqed_amd.deom import Bath, DEOMSolver
+    w = sp.symbols(r"\omega", real=True)
+    bath = Bath([2 * 0.5 * w / (1.0 + w ** 2)], w, [1.0], [3], [0] * 4)
+    rng = np.random.default_rng(7 + B)
+    A = rng.standard_normal((ns, ns)) + 1j * rng.standard_normal((ns, ns))
+    H = (A + A.conj().T) / 4
+    Q = np.diag(np.arange(ns, dtype=float)).astype(complex) + 0.2 * (np.eye(ns, k=1) + np.eye(ns, k=-1))
+    psi = rng.standard_normal((B, ns)) + 1j * rng.standard_normal((B, ns))
+    psi /= np.linalg.norm(psi, axis=1, keepdims=True)
+    rho0 = np.einsum("bi,bj->bij", psi, psi.conj())
+    dt, nt, L = 0.005, 8, 6
+    splits = [x for x in ("0", "1", "2", "4", "8") if x == "0" or B % int(x) == 0]
+    for layout in ("0", "1"):
+        monkeypatch.setenv("QD_DEOM_ADO_MAJOR", layout)
+        out = {}
+        for x in splits:
+            monkeypatch.setenv("QD_DEOM_XCD", x)
+            sol = DEOMSolver(H, None, bath, np.array([Q]), None, None, None, L)
+            _, saved = sol.run_batch(rho0, dt, nt)
+            out[x] = (saved, sol.ddos)
+        for x in splits[1:]:
+            assert np.array_equal(out[x][0], out["0"][0]) and np.array_equal(out[x][1], out["0"][1]), (layout, x)
+    monkeypatch.delenv("QD_DEOM_XCD")
+    tt, ref, _ = od.run(H, np.zeros((ns, ns)), lambda t: 0, np.array([Q]), np.zeros((1, ns, ns)), lambda t: 0,
+                        (bath.etal, bath.etar, bath.etaa, bath.expn), L, rho0[B - 1], dt, nt)
+    assert relerr(out["0"][0][B - 1], ref) < TOL
+
+
 def _multi_mode_model(ns, nmod, npsd, L, seed=3):
     from pyqed_amd.deom import Bath, DEOMSolver
     rng = np.random.default_rng(seed)
