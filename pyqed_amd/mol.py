@@ -141,6 +141,55 @@ def driven_dynamics(H, psi0, dt=0.01, Nt=1, e_ops=None, nout=1, t0=0.0, return_r
     return result
 
 
+def _driven_dynamics(H, psi0, edip, E, dt=0.001, Nt=1, e_ops=None, nout=1, t0=0.0, sparse=True):
+    """mol.py:1772-1859: full vector dipole edip [N, N, 3] in a polarized field E(t) -> 3-vector,
+    H(t) = H - einsum('ija, a -> ij', edip, E(t)), held for each block of nout RK4 steps at the block's start time
+    (t advanced by dt*nout after a block); Nt//nout - 1 blocks.  On the GPU this is qd_tdse_driven_rk4 with the
+    three dipole components as drives.  As the reference: result.psilist holds only the states after each block
+    (csr columns), observables (Nt//nout, n_e) include t0, result.psi = psit [nstates, Nt//nout].  The reference's
+    sparse=False branch never defines psi and raises; only the sparse (default) arithmetic exists."""
+    import torch
+    from scipy.sparse import csr_matrix
+    from ._util import default_device, stack_ops, to_numpy
+    if not sparse:
+        raise NotImplementedError("_driven_dynamics(sparse=False): the reference's dense branch never sets psi")
+    if e_ops is None:
+        e_ops = []
+    dev = default_device()
+    H0 = to_numpy(H, np.complex128)
+    N = H0.shape[0]
+    ed = np.asarray(to_numpy(edip, np.complex128))
+    if ed.shape[:2] != (N, N) or ed.ndim != 3:
+        raise ValueError(f"edip must be [N, N, ncomp] with N = {N}, got {ed.shape}")
+    nc = ed.shape[2]
+    p0 = to_numpy(psi0, np.complex128).reshape(N)
+    nblocks = max(Nt // nout - 1, 0)
+    fvals = np.zeros((nblocks, nc), dtype=np.complex128)
+    for k in range(nblocks):
+        fvals[k] = np.asarray(E(t0 + k * dt * nout), dtype=np.complex128).reshape(nc)
+    psi = torch.from_numpy(p0.copy()).to(dev).reshape(1, N)
+    Hdt = torch.from_numpy(np.ascontiguousarray(np.moveaxis(ed, 2, 0))).to(dev)
+    Ed = stack_ops(e_ops, N, dev)
+    snap, obs = tdse_driven_rk4(torch.from_numpy(np.ascontiguousarray(H0)).to(dev), Hdt, fvals, psi, dt, nout,
+                                e_ops=Ed)
+    states = snap[0].cpu().numpy() if snap is not None else np.zeros((0, N), complex)
+    nrec = Nt // nout
+    result = Result(dt=dt, Nt=Nt, psi0=psi0, t0=t0, nout=nout)
+    observables = np.zeros((nrec, len(e_ops)), dtype=complex)
+    if obs is not None:
+        o = obs[0].cpu().numpy()
+        observables[:nblocks + 1] = o[:nrec]
+    psit = np.zeros((N, nrec), dtype=complex)
+    if nrec:
+        psit[:, 0] = p0
+    for k in range(nblocks):
+        psit[:, k + 1] = states[k]
+    result.psilist = [csr_matrix(states[k].reshape(N, 1)) for k in range(nblocks)]
+    result.psi = psit
+    result.observables = observables
+    return result
+
+
 def _quantum_dynamics(H, psi0, dt=0.001, Nt=1, e_ops=[], t0=0.0, nout=1, store_states=True, output='obs.dat'):
     """mol.py:1603-1691 (store_states=True): (Nt//nout - 1)*nout RK4 steps; psilist = [psi0] + the
     state after every nout steps; observables (Nt//nout, n_e) at those states."""
@@ -181,7 +230,8 @@ class SESolver:
 
     def run(self, psi0=None, dt=0.01, Nt=1, e_ops=None, nout=1, t0=0.0, edip=None, pulse=None, use_sparse=True):
         """mol.py:1392-1459: time-independent H -> _quantum_dynamics; with a pulse (or a list of
-        pulses with a list of dipoles) -> driven_dynamics, H(t) = H - sum_i f_i(t) edip_i."""
+        pulses with a list of dipoles) -> driven_dynamics, H(t) = H - sum_i f_i(t) edip_i; a full [N, N, 3]
+        dipole with a single pulse -> _driven_dynamics with the pulse's vector field pulse.E(t)."""
         if psi0 is None:
             psi0 = self.groundstate
         if pulse is None:
@@ -194,7 +244,10 @@ class SESolver:
         if np.ndim(edip) == 2:
             return driven_dynamics(H=[self.H, [edip, pulse.efield]], psi0=psi0, dt=dt, Nt=Nt, e_ops=e_ops,
                                    nout=nout, t0=t0, use_sparse=use_sparse)
-        raise NotImplementedError("full 3D dipole with a vector pulse (mol._driven_dynamics) is not on the GPU path")
+        if np.ndim(edip) == 3:
+            return _driven_dynamics(H=self.H, psi0=psi0, edip=edip, E=pulse.E, dt=dt, Nt=Nt, e_ops=e_ops, nout=nout,
+                                    t0=t0)
+        return None
 
 
 class Mol:

@@ -579,20 +579,62 @@ class RedfieldSolver:
         torch.cuda.synchronize(dev)
         return result
 
-    # ---- Liouville-space Green's functions (eigen / SOS form)
+    # ---- Liouville-space Green's functions
+    def _propagator_eom(self, R, t):
+        """phys.expm(R, t, 'EOM') (phys.py:2049-2097): U_0 = I, U_{k+1} = rk4(U_k, ldo, dt, R) with ldo(b, A) = A.b
+        and dt = t[1] - t[0], i.e. d U/dt = R U.  On the GPU each column of U is one vector of the batched dense
+        superoperator RK4 (qd_superop_rk4: MFMA GEMM stages once the batch fills 64-wide blocks), every step saved.
+        Returns U (nL, nL, len(t)) with U[:, :, k] = U_k, as np.dstack of the reference's list."""
+        from scipy.sparse import issparse
+        t = np.asarray(t, dtype=float)
+        Nt = len(t)
+        Rd = R.toarray() if issparse(R) else np.asarray(R)
+        nL = Rd.shape[0]
+        U = np.empty((nL, nL, Nt), dtype=complex)
+        U[:, :, 0] = np.eye(nL)
+        if Nt > 1:
+            dev = default_device()
+            L = torch.from_numpy(np.ascontiguousarray(Rd.astype(complex))).to(dev)
+            v = torch.eye(nL, dtype=torch.complex128, device=dev)       # row b = column b of U
+            _, snap = superop_rk4(L, v, float(t[1] - t[0]), Nt - 1, save_every=1)
+            U[:, :, 1:] = snap.permute(2, 0, 1).cpu().numpy()          # snap[b, k, a] = U_{k+1}[a, b]
+        return U
+
     def propagator(self, t, method='SOS'):
-        """oqs.py:160-214 (SOS): U (nL, nL, nt) on the GPU; G = -1j U."""
+        """oqs.py:160-214: U (nL, nL, nt); G = -1j U.  'SOS' / 'eseries': eigen form on the GPU; 'EOM': the
+        reference's RK4 propagation of the identity (phys.expm) on the dense-superoperator RK4 kernel."""
         if self.R is None:
             raise TypeError('Redfield tensor is not computed. Please call redfield_tensor()')
-        if method not in ['eseries', 'SOS']:
-            raise NotImplementedError(f"propagator method {method!r}: only 'SOS'/'eseries' run on the GPU")
-        from .response import sos_eig, sos_propagator
-        lam, U1, U2 = sos_eig(self.R)
-        t = np.asarray(t, dtype=float)
-        self._sos = (lam, U1, U2, t)
-        self.U = sos_propagator(lam, U1, U2, t).cpu().numpy()
+        if method == 'EOM':
+            self.U = self._propagator_eom(self.R, t)
+        elif method in ['eseries', 'SOS']:
+            from .response import sos_eig, sos_propagator
+            lam, U1, U2 = sos_eig(self.R)
+            t = np.asarray(t, dtype=float)
+            self._sos = (lam, U1, U2, t)
+            self.U = sos_propagator(lam, U1, U2, t).cpu().numpy()
+        else:
+            # the reference falls through to `self.G = -1j * self.U` with U unset
+            raise NotImplementedError(f"propagator method {method!r}: choose 'SOS', 'eseries' or 'EOM'")
         self.G = -1j * self.U
         return self.U
+
+    def gf(self, t, w=None, secular=False, k=1, domain='time', method='EOM'):
+        """Liouville-space Green's function with Redfield dissipation (oqs.py:136-158).
+        'EOM': -1j * expm(R, t), i.e. -1j U_k for every t_k as an (nL, nL, nt) array (the reference multiplies the
+        expm list by -1j, which raises; the array is its evident meaning).  'eseries' / 'diag' / 'diagonalization':
+        getG(1j R, t) (oqs.py:465-508), G(t) = -1j exp(R t) in the eigen form, evaluated on the GPU."""
+        if self.R is None:
+            self.redfield_tensor(secular=secular)
+        if method == 'EOM':
+            return -1j * self._propagator_eom(self.R, t)
+        if method in ['eseries', 'diag', 'diagonalization']:
+            if domain != 'time':
+                raise NotImplementedError("gf: only domain='time' (getG's 'freq' branch needs w and U2^*)")
+            from .response import sos_eig, sos_propagator
+            lam, U1, U2 = sos_eig(self.R)
+            return -1j * sos_propagator(lam, U1, U2, np.asarray(t, dtype=float)).cpu().numpy()
+        return None
 
     def correlation_4op_3t(self, rho0, oplist, signature, tau):
         """<<I|A G(tau3) B G(tau2) C G(tau1) D|rho0>> cube [i=tau3, j=tau2, k=tau1] (oqs.py:268-357)."""

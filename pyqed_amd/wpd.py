@@ -337,9 +337,8 @@ class SPO2(_PointPropagators):
     def run_batch(self, psi0s, dt=0.01, nt=1, nout=1, device=None):
         """Extension: B independent wavepackets psi0s [B, nx, ny, ns] on one potential, Strang steps as
         run(return_states=True) for each (qd_spo2_run_batch: one launch per pass for the whole batch).
-        Returns (final states [B, nx, ny, ns], snapshots [B, nt//nout, nx, ny, ns]) as device tensors."""
-        if self.coords != 'linear':
-            raise NotImplementedError("run_batch: linear coordinates only")
+        Returns (final states [B, nx, ny, ns], snapshots [B, nt//nout, nx, ny, ns]) as device tensors.
+        Jacobi coordinates run the _KEO_jacobi step structure (qd_spo2_run_ex) member by member."""
         self.build(dt=dt)
         dev = device or default_device()
         _lib.ensure_device(dev)
@@ -352,6 +351,17 @@ class SPO2(_PointPropagators):
         snap = torch.empty((B, nsnap, self.nx, self.ny, self.ns), dtype=torch.complex128, device=dev) if nsnap \
             else None
         _, eVh = self._point_ops_dev(dev, need_full=False)
+        if self.coords == 'jacobi':
+            eK = _dev_c128(np.broadcast_to(self.exp_Kx[:, None], (self.nx, self.ny)), dev)
+            eKy = _dev_c128(self.exp_Ky, dev)
+            with torch.cuda.device(dev):
+                for b in range(B):
+                    rc = _lib.load().qd_spo2_run_ex(psi[b].data_ptr(), eVh.data_ptr(), None, eK.data_ptr(),
+                                                    eKy.data_ptr(), self.nx, self.ny, self.ns, int(nsnap * nout),
+                                                    int(nout), snap[b].data_ptr() if nsnap else None,
+                                                    _lib.stream_ptr(dev))
+                    _lib.check(rc, "qd_spo2_run_ex")
+            return psi, snap
         eK = _dev_c128(self.exp_K, dev)
         with torch.cuda.device(dev):
             rc = _lib.load().qd_spo2_run_batch(psi.data_ptr(), B, eVh.data_ptr(), eK.data_ptr(), self.nx, self.ny,
@@ -462,9 +472,15 @@ class SPO3(_PointPropagators):
         return v
 
     def build(self, dt, inertia=None):
-        """wpd.py:1210-1340 (linear): exp_K on the 'ij' grid, exp(-i V dt/2) per point."""
+        """wpd.py:1210-1340 (linear): exp_K on the 'ij' grid, exp(-i V dt/2) per point.
+        coords='jacobi' is not a working path of the reference: its SPO3._KEO_jacobi (wpd.py:1434-1469) contracts the
+        4-index wavefunction [nx, ny, nz, ns] with 'ij, ija -> ija' (the 2-D SPO2 form), which numpy rejects, and its
+        build never forms a z kinetic factor; there is no step structure to reproduce, so it is refused here."""
+        if self.coords == 'jacobi':
+            raise NotImplementedError("SPO3 with coords='jacobi': the reference's _KEO_jacobi (wpd.py:1434-1469) is the "
+                                      "2-D SPO2 operator applied to a 3-D grid and fails there; no 3-D Jacobi KEO exists")
         if self.coords != 'linear':
-            raise NotImplementedError("only linear coordinates run on the GPU path")
+            raise ValueError(f"unknown coordinates {self.coords!r}")
         self.kx = 2. * np.pi * fftfreq(self.nx, self.dx)
         self.ky = 2. * np.pi * fftfreq(self.ny, self.dy)
         self.kz = 2. * np.pi * fftfreq(self.nz, self.dz)

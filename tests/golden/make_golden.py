@@ -265,6 +265,35 @@ def tdse_driven():
     save("tdse_driven", **out)
 
 
+def vector_field(t, p):
+    """Polarized test field E(t) (3-vector) of the tdse_driven3d fixture: a Gaussian carrier per component."""
+    amp, om, tc, tau = p[:, 0], p[:, 1], p[:, 2], p[:, 3]
+    return amp * np.cos(om * t) * np.exp(-((t - tc) / tau) ** 2)
+
+
+@golden
+def tdse_driven3d():
+    """SESolver.run with a full [N, N, 3] dipole -> mol._driven_dynamics (mol.py:1441-1445, 1772-1859)."""
+    from pyqed.mol import SESolver
+    rng = np.random.default_rng(41)
+    N = 5
+    H = np.diag(np.linspace(0.0, 1.2, N)).astype(complex) + 0.05 * _herm(rng, N)
+    edip = np.stack([_herm(rng, N, 0.4) for _ in range(3)], axis=2)
+    E = [_herm(rng, N) for _ in range(2)]
+    psi0 = np.zeros(N, complex); psi0[0] = 1.0
+    fp = np.array([[0.3, 0.9, 1.0, 0.8], [0.2, 1.1, 1.5, 1.0], [0.1, 0.7, 0.5, 2.0]])
+
+    class VPulse:
+        def E(self, t):
+            return vector_field(t, fp)
+
+    r = SESolver(H).run(psi0=psi0, dt=0.04, Nt=60, e_ops=[csr_matrix(e) for e in E], nout=3, edip=edip,
+                        pulse=VPulse())
+    save("tdse_driven3d", H=H, edip=edip, E=np.array(E), psi0=psi0, dt=0.04, Nt=60, nout=3, field=fp,
+         obs=r.observables, psit=r.psi,
+         psilist=np.array([np.asarray(x.toarray()).reshape(N) for x in r.psilist]))
+
+
 @golden
 def photon_echo():
     """sos.photon_echo (signal/sos.py:962-1052) via Mol.photon_echo (mol.py:804-829)."""
@@ -359,6 +388,29 @@ def redfield_n4():
 @golden
 def redfield_n6_k2():
     _redfield_case("redfield_n6_k2", N=6, nk=2, Nt=8, dt=0.02, seed=22, spectrum="flat005")
+
+
+@golden
+def redfield_eom():
+    """RedfieldSolver.propagator(t, 'EOM') (oqs.py:160-200 -> phys.expm, phys.py:2049-2097) and
+    gf(t, method='eseries') (oqs.py:136-158 -> getG, oqs.py:465-508) on an N = 4 system.  In the imported package
+    the name `expm` that oqs.py binds is a later star-import's one-argument expm, so propagator('EOM') raises
+    TypeError there; the fixture calls the function oqs.py means, pyqed.phys.expm(R, t), directly."""
+    import contextlib
+    import io
+    import pyqed.oqs as oqs
+    from pyqed.phys import expm as phys_expm
+    rng = np.random.default_rng(31)
+    N = 4
+    H = _herm(rng, N)
+    a_ops = [_herm(rng, N, 0.5)]
+    sol = oqs.RedfieldSolver(H, c_ops=a_ops, spectra=[SPECTRA["tanh"]])
+    R, evecs = sol.redfield_tensor()
+    t = 0.05 * np.arange(12)
+    with contextlib.redirect_stdout(io.StringIO()):
+        U = np.dstack([u.toarray() for u in phys_expm(sol.R, t)])
+    G = sol.gf(t, method="eseries")
+    save("redfield_eom", H=H, a_ops=np.array(a_ops), spectrum="tanh", t=t, R=R.toarray(), U_eom=U, G_eseries=G)
 
 
 def _three_level(E=(0.0, 1.0, 1.5)):

@@ -22,6 +22,27 @@ def test_redfield_evolve_matches_reference(name):
     assert relerr(np.array(r.rholist), g["rholist"]) < TOL
 
 
+def test_redfield_propagator_eom_and_gf_match_reference():
+    """propagator(t, 'EOM') = phys.expm(R, t) (RK4 of the identity, oqs.py:185-200, phys.py:2049-2097) on the
+    batched dense-superoperator kernel, gf(t, 'EOM') = -1j of it, and gf(t, 'eseries') = getG(1j R, t)
+    (oqs.py:136-158, 465-508), against the reference's outputs; 'SOS' agrees with 'EOM' to the RK4 truncation error (3e-5 here)."""
+    from pyqed_amd import RedfieldSolver
+    g = load_golden("redfield_eom")
+    sol = RedfieldSolver(g["H"], c_ops=list(g["a_ops"]), spectra=[SPECTRA[str(g["spectrum"])]])
+    sol.redfield_tensor()
+    t = g["t"]
+    U = sol.propagator(t, method="EOM")
+    assert U.shape == g["U_eom"].shape
+    assert relerr(U, g["U_eom"]) < TOL
+    assert relerr(sol.G, -1j * g["U_eom"]) < TOL
+    assert relerr(sol.gf(t, method="EOM"), -1j * g["U_eom"]) < TOL
+    assert relerr(sol.gf(t, method="eseries"), g["G_eseries"]) < 1e-9
+    U_sos = sol.propagator(t, method="SOS")
+    assert relerr(U_sos, g["U_eom"]) < 1e-4   # RK4 truncation at dt = 0.05
+    with pytest.raises(NotImplementedError):
+        sol.propagator(t, method="krylov")
+
+
 def test_basis_transform_batched():
     import torch
     from pyqed_amd.oqs import basis_transform

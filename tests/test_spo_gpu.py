@@ -170,6 +170,28 @@ def test_spo2_jacobi_matches_reference():
     assert relerr(np.array(r.psilist), g["psilist"]) < 1e-11
 
 
+def test_spo2_jacobi_run_batch_and_spo3_jacobi_refused():
+    """SPO2.run_batch in Jacobi coordinates (member by member on the _KEO_jacobi step structure) equals run() of each
+    member and the reference's psilist for the golden member; SPO3 coords='jacobi' is refused, as the reference's
+    3-D _KEO_jacobi (wpd.py:1434-1469) cannot contract a 3-D grid."""
+    from pyqed_amd import SPO2, SPO3
+    g = load_golden("spo2_jacobi_32")
+    a, b = g["inertia"]
+    sol = SPO2(g["x"], g["y"], mass=[1.0, lambda r: a + b * r ** 2], nstates=2, coords='jacobi')
+    sol.set_DPES([g["v0"], g["v1"]], [[[0, 1], g["coupling"]]])
+    dt, nt, nout = float(g["dt"]), int(g["nt"]), int(g["nout"])
+    psi0 = np.stack([g["psi0"], np.roll(g["psi0"], 3, axis=0)])
+    psi, snap = sol.run_batch(psi0, dt=dt, nt=nt, nout=nout)
+    psi, snap = psi.cpu().numpy(), snap.cpu().numpy()
+    assert relerr(np.array([g["psi0"]] + list(snap[0])), g["psilist"]) < 1e-11
+    r1 = sol.run(psi0[1], dt=dt, nt=nt, nout=nout)
+    assert relerr(snap[1], np.array(r1.psilist[1:])) < 1e-13 and relerr(psi[1], r1.psi) < 1e-13
+    x = np.linspace(-3, 3, 16)
+    s3 = SPO3(x, x, x, masses=[1.0, 1.0, 1.0], nstates=2, coords='jacobi')
+    with pytest.raises(NotImplementedError):
+        s3.build(0.01)
+
+
 def test_spo2_merged_equals_strang_unitary():
     """For a Hermitian potential the merged structure V/2 (K V)^n K V/2 equals n + 1 Strang steps up to
     rounding (V/2 V/2 = V)."""

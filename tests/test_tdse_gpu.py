@@ -64,6 +64,30 @@ def test_driven_sesolver_single_pulse():
     assert relerr(got, g["a_psilist"]) < TOL
 
 
+def test_driven_sesolver_vector_dipole():
+    """SESolver.run(edip=[N, N, 3], pulse with a vector field .E) -> mol._driven_dynamics (mol.py:1441-1445,
+    1772-1859): the three dipole components are the drives of qd_tdse_driven_rk4; psilist holds only the block
+    states (csr), observables include t0."""
+    from scipy.sparse import issparse
+    from pyqed_amd.mol import SESolver
+    g = load_golden("tdse_driven3d")
+    fp = g["field"]
+
+    class VPulse:
+        def E(self, t):
+            amp, om, tc, tau = fp[:, 0], fp[:, 1], fp[:, 2], fp[:, 3]
+            return amp * np.cos(om * t) * np.exp(-((t - tc) / tau) ** 2)
+
+    r = SESolver(g["H"]).run(psi0=g["psi0"], dt=float(g["dt"]), Nt=int(g["Nt"]), e_ops=list(g["E"]),
+                             nout=int(g["nout"]), edip=g["edip"], pulse=VPulse())
+    assert r.observables.shape == g["obs"].shape
+    assert relerr(r.observables, g["obs"]) < TOL
+    assert relerr(r.psi, g["psit"]) < TOL
+    assert len(r.psilist) == len(g["psilist"]) and all(issparse(x) for x in r.psilist)
+    got = np.array([np.asarray(x.toarray()).reshape(-1) for x in r.psilist])
+    assert relerr(got, g["psilist"]) < TOL
+
+
 def test_driven_mol_two_pulses():
     """Mol.run(pulse=[p1, p2]) with self.edip a list of dipoles, t0 != 0 (mol.py:660-675)."""
     from pyqed_amd.mol import Mol
