@@ -547,6 +547,84 @@ def bench_spo2(dev, steps, n=256, dt=0.05):
     }
 
 
+def bench_spo3(dev, steps=200, n=64, dt=0.05):
+    """SPO3 at the examples/spo.py grid, 64^3 x 2 diabatic states (wpd.SPO3.run, wpd.py:1105-1432): one wavepacket,
+    device-resident, HIP events over `steps` Strang steps (qd_spo3_run: z-row pass with V/2, mid-axis pass, x pass
+    with exp_K, inverse mid-axis pass), plus SPO3.run end to end."""
+    import torch
+    from pyqed_amd import _lib
+    from pyqed_amd.wpd import SPO3
+    x = np.linspace(-6, 6, n)
+    X, Y, Z = np.meshgrid(x, x, x, indexing="ij")
+    sol = SPO3(x, x, x, masses=[1.0, 1.0, 1.0], nstates=2)
+    sol.set_DPES([0.5 * ((X + 1) ** 2 + Y ** 2 + Z ** 2), 0.5 * ((X - 1) ** 2 + Y ** 2 + Z ** 2)], [[[0, 1], 0.2 * X]])
+    sol.build(dt)
+    psi0 = np.zeros((n, n, n, 2), complex)
+    psi0[..., 1] = np.exp(-((X + 1) ** 2 + Y ** 2 + Z ** 2) / 2) / np.pi ** 0.75
+    psi = torch.from_numpy(psi0).to(dev)
+    eVh = torch.from_numpy(sol.exp_V_half).to(dev)
+    eK = torch.from_numpy(sol.exp_K).to(dev)
+    lib = _lib.load()
+    st = _lib.stream_ptr(dev)
+
+    def run(k):
+        _lib.check(lib.qd_spo3_run(psi.data_ptr(), eVh.data_ptr(), eK.data_ptr(), n, n, n, 2, k, k, None, st),
+                   "qd_spo3_run")
+
+    run(5)
+    torch.cuda.synchronize(dev)
+    stream = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    run(steps)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    ev = e0.elapsed_time(e1) / 1e3
+    norm = float((psi.abs() ** 2).sum().item() / (np.abs(psi0) ** 2).sum())
+    # bytes per step of the four passes: psi (n^3 x 2 c128) read + written by each, exp_V_half (n^3 x 4) and
+    # exp_K (n^3) read once
+    bytes_per_step = (4 * 2 * n ** 3 * 2 + n ** 3 * 4 + n ** 3) * 16
+    tr = time.perf_counter()
+    sol.run(psi0, dt=dt, nt=100, nout=100)
+    run_wall = time.perf_counter() - tr
+    ach = bytes_per_step / (ev / steps) / 1e9
+    return {
+        "value": round(steps / ev, 1), "unit": "SPO steps/s", "us_per_step": round(ev / steps * 1e6, 2),
+        "config": {"workload": "spo3_64x64x64x2 (examples/spo.py grid; SURVEY §8(f) SPO3 64^3)", "grid": [n, n, n],
+                   "nstates": 2, "dt": dt, "steps": steps},
+        "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_step": bytes_per_step,
+                     "note": "four passes over an 8 MiB state that stays in the Infinity Cache: dependent-pass "
+                             "latency, not bytes, bounds one wavepacket"},
+        "norm_ratio": norm, "run_100_steps_wall_s": round(run_wall, 4),
+    }
+
+
+def cpu_baseline_spo3(n=64, dt=0.05, budget_s=5.0):
+    from oracle import spo as ospo
+    x = np.linspace(-6, 6, n)
+    X, Y, Z = np.meshgrid(x, x, x, indexing="ij")
+    v = np.zeros((n, n, n, 2, 2))
+    v[..., 0, 0] = 0.5 * ((X + 1) ** 2 + Y ** 2 + Z ** 2)
+    v[..., 1, 1] = 0.5 * ((X - 1) ** 2 + Y ** 2 + Z ** 2)
+    v[..., 0, 1] = v[..., 1, 0] = 0.2 * X
+    w, u = np.linalg.eigh(v)
+    eVh = (u * np.exp(-1j * w * dt / 2)[..., None, :]) @ np.conj(np.swapaxes(u, -1, -2))
+    kx = 2 * np.pi * np.fft.fftfreq(n, x[1] - x[0])
+    KX, KY, KZ = np.meshgrid(kx, kx, kx, indexing="ij")
+    eK = np.exp(-1j * (KX ** 2 + KY ** 2 + KZ ** 2) / 2 * dt)
+    psi = np.zeros((n, n, n, 2), complex)
+    psi[..., 1] = np.exp(-((X + 1) ** 2 + Y ** 2 + Z ** 2) / 2)
+    t0 = time.perf_counter()
+    k = 0
+    while time.perf_counter() - t0 < budget_s:
+        psi = ospo.spo3_run(eVh, eK, psi, 2, 2)[-1]
+        k += 2
+    el = time.perf_counter() - t0
+    return {"value": round(k / el, 2), "unit": "SPO steps/s", "cores": 1, "kind": "port",
+            "sample": f"{k} Strang steps of the numpy.fft restatement of SPO3.run at {n}^3 x 2 in {el:.1f}s"}
+
+
 def cpu_baseline_spo2(n=256, dt=0.05, budget_s=5.0):
     from oracle import spo as ospo
     x = np.linspace(-6, 6, n)
@@ -690,6 +768,7 @@ def main():
     ap.add_argument("--t2-reps", type=int, default=3)
     ap.add_argument("--spo-steps", type=int, default=1000)
     ap.add_argument("--no-spo", action="store_true")
+    ap.add_argument("--no-spo3", action="store_true")
     ap.add_argument("--deom-steps", type=int, default=200)
     ap.add_argument("--deom-batch", type=int, default=64)
     ap.add_argument("--no-deom", action="store_true")
@@ -750,16 +829,29 @@ def main():
     tr = torch.diagonal(rho, dim1=1, dim2=2).sum(-1)
     tr_err = float((tr - 1).abs().max().item())
 
-    # single-trajectory latency (B=1), informational
-    # (the auto dispatch of LindbladSolver.run: one matrix runs the general kernel's split path)
-    r1 = rho[:1].clone()
-    lindblad_rk4(Ht, Ct, r1, args.dt, 2)
-    torch.cuda.synchronize(dev)
-    s1 = 100
-    ta = time.perf_counter()
-    lindblad_rk4(Ht, Ct, r1, args.dt, s1)
-    torch.cuda.synchronize(dev)
-    single_rate = s1 / (time.perf_counter() - ta)
+    # smaller batches (B in {1, 64, 256}), event-timed on the launch stream; the auto dispatch
+    # (below HERM_MIN_BATCH = 192 matrices) runs the general kernel's split path, so its executed flops are the
+    # general kernel's
+    batch_sweep = {}
+    for Bs in (1, 64):
+        rs = rho[:Bs].clone()
+        lindblad_rk4(Ht, Ct, rs, args.dt, 2)
+        torch.cuda.synchronize(dev)
+        ss = 100
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        lindblad_rk4(Ht, Ct, rs, args.dt, ss)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        sec = e0.elapsed_time(e1) / 1e3
+        tf = lindblad_flops_per_step(N, nc) * Bs * ss / sec / 1e12
+        batch_sweep[str(Bs)] = {
+            "dm_steps_per_s": round(Bs * ss / sec, 1), "us_per_step": round(sec / ss * 1e6, 2),
+            "path": "glf split-K (general kernel)",
+            "roofline": {"bound": "mfma", "achieved": round(tf, 3), "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(tf / FP64_MFMA_PEAK_TFLOPS, 4),
+                         "flop_per_dm_step": lindblad_flops_per_step(N, nc)}}
+    single_rate = batch_sweep["1"]["dm_steps_per_s"]
 
     twodes = None
     if not args.no_2des:
@@ -788,6 +880,10 @@ def main():
     spo = None
     if not args.no_spo:
         spo = bench_spo2(dev, args.spo_steps)
+
+    spo3 = None
+    if not args.no_spo3:
+        spo3 = bench_spo3(dev)
 
     deom = None
     if not args.no_deom:
@@ -831,6 +927,7 @@ def main():
                 "launch_ms": round(kern_s * 1e3, 3),
             },
             "single_trajectory_steps_per_s": round(single_rate, 2),
+            "batch_sweep": batch_sweep,
             "trace_err": tr_err,
         }
         if world == 1 and not args.no_cpu:
@@ -851,6 +948,10 @@ def main():
             if world == 1 and not args.no_cpu:
                 spo["cpu_baseline"] = cpu_baseline_spo2()
             out.setdefault("secondary", {})["spo2"] = spo
+        if spo3 is not None:
+            if world == 1 and not args.no_cpu:
+                spo3["cpu_baseline"] = cpu_baseline_spo3()
+            out.setdefault("secondary", {})["spo3"] = spo3
         if deom is not None:
             if world == 1 and not args.no_cpu:
                 deom["cpu_baseline"] = cpu_baseline_deom()
