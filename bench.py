@@ -650,59 +650,72 @@ def cpu_baseline_spo2(n=256, dt=0.05, budget_s=5.0):
             "sample": f"{k} Strang steps of the scipy.fftpack restatement of SPO2.run at {n}x{n}x2 in {el:.1f}s"}
 
 
-def bench_deom(dev, steps, batch):
-    """BASELINE config d4: spin-boson H = sz + sx, Q = sx, Drude lambda=0.5 gamma=1 beta=1, Pade npsd=4
-    (K=5), L=12 -> 6188 ADOs.  dt=0.002 (RK4 stability: dt*L*max Re expn < 2.8; the SURVEY value 0.01
-    diverges).  One hierarchy and a batch of independent hierarchies (ADO-major layout), state resident on the
-    device, `steps` RK4 steps timed by HIP events on the launch stream; DEOMSolver.run end to end is timed too."""
-    import sympy as sp
+def _deom_event_rate(dev, sol, bath, H, Q, B, steps, dt=0.002):
+    """RK4 steps/s of B independent hierarchies of `sol` (device-resident state; HIP events on the launch stream
+    around `steps` steps = 4 stage launches each).  B >= 16 runs the ADO-major layout."""
     import torch
     from pyqed_amd import _lib
-    from pyqed_amd.deom import Bath, DEOMSolver, ado_coefficients
-    w = sp.symbols(r"\omega", real=True)
-    bath = Bath([2 * 0.5 * 1.0 * w / (1.0 + w ** 2)], w, [1.0], [4], [0] * 5)
-    sx = np.array([[0, 1], [1, 0]], complex)
-    sz = np.diag([1.0, -1.0]).astype(complex)
-    sol = DEOMSolver(sz + sx, None, bath, np.array([sx]), None, None, None, 12)
-    rho0 = np.zeros((2, 2), complex)
-    rho0[0, 0] = 1
-    sol.run_batch(rho0[None], 0.01, 5)
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    sol.run(rho0.copy(), 0.002, steps)
-    wall_run = time.perf_counter() - t0
-    ns, K, nmax = 2, sol.nind, sol.nmax
+    from pyqed_amd.deom import ado_coefficients
+    ns, K, nmax = H.shape[0], sol.nind, sol.nmax
     coef, damp = ado_coefficients(sol.keys, np.asarray(bath.etal), np.asarray(bath.etar), np.asarray(bath.etaa),
                                   np.asarray(bath.expn), sol.lmax)
     c128 = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=complex))).to(dev)
     i32 = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=np.int32))).to(dev)
     tabs = (i32(sol._minus), i32(sol._plus), c128(coef), c128(damp), i32(bath.mode))
-    H, Q = c128(sz + sx), c128(sx[None])
+    Hd, Qd = c128(H), c128(Q)
     lib = _lib.load()
     st = _lib.stream_ptr(dev)
-    rate = {}
-    for B in (1, batch):
-        ado_major = B >= 16
-        fn = lib.qd_deom_rk4_ado_major if ado_major else lib.qd_deom_rk4
-        ados = torch.zeros((nmax, B, ns, ns) if ado_major else (B, nmax, ns, ns), dtype=torch.complex128, device=dev)
-        (ados[0] if ado_major else ados[:, 0])[..., 0, 0] = 1
-        rho_sys = torch.empty((B, steps + 1, ns, ns), dtype=torch.complex128, device=dev)
+    ado_major = B >= 16
+    fn = lib.qd_deom_rk4_ado_major if ado_major else lib.qd_deom_rk4
+    ados = torch.zeros((nmax, B, ns, ns) if ado_major else (B, nmax, ns, ns), dtype=torch.complex128, device=dev)
+    (ados[0] if ado_major else ados[:, 0])[..., 0, 0] = 1
+    rho_sys = torch.empty((B, steps + 1, ns, ns), dtype=torch.complex128, device=dev)
 
-        def run(n):
-            rc = fn(ados.data_ptr(), B, nmax, K, ns, *(t.data_ptr() for t in tabs), 1, H.data_ptr(), None,
-                    Q.data_ptr(), None, None, None, 0.002, n, rho_sys.data_ptr(), None, 0, None, st)
-            _lib.check(rc, "qd_deom_rk4")
+    def run(n):
+        rc = fn(ados.data_ptr(), B, nmax, K, ns, *(t.data_ptr() for t in tabs), Qd.shape[0], Hd.data_ptr(), None,
+                Qd.data_ptr(), None, None, None, dt, n, rho_sys.data_ptr(), None, 0, None, st)
+        _lib.check(rc, "qd_deom_rk4")
 
-        run(5)
-        torch.cuda.synchronize(dev)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        run(steps)
-        e1.record()
-        torch.cuda.synchronize(dev)
-        rate[B] = steps / (e0.elapsed_time(e1) / 1e3)
-        tr = torch.diagonal(rho_sys[:, -1], dim1=-2, dim2=-1).sum(-1)
-        assert float((tr - 1).abs().max()) < 1e-10
+    run(5)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    run(steps)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    tr = torch.diagonal(rho_sys[:, -1], dim1=-2, dim2=-1).sum(-1)
+    assert float((tr - 1).abs().max()) < 1e-10
+    return steps / (e0.elapsed_time(e1) / 1e3)
+
+
+def bench_deom(dev, steps, batch):
+    """BASELINE config d4: spin-boson H = sz + sx, Q = sx, Drude lambda=0.5 gamma=1 beta=1, Pade npsd=4
+    (K=5), L=12 -> 6188 ADOs.  dt=0.002 (RK4 stability: dt*L*max Re expn < 2.8; the SURVEY value 0.01
+    diverges).  One hierarchy and a batch of independent hierarchies (ADO-major layout), state resident on the
+    device, `steps` RK4 steps timed by HIP events on the launch stream; DEOMSolver.run end to end is timed too;
+    the "~10k ADO" stretch hierarchy of SURVEY §8(d) d4 (npsd=5, K=6: 18,564 ADOs) as one more line."""
+    import sympy as sp
+    import torch
+    from pyqed_amd.deom import Bath, DEOMSolver
+    w = sp.symbols(r"\omega", real=True)
+    sx = np.array([[0, 1], [1, 0]], complex)
+    sz = np.diag([1.0, -1.0]).astype(complex)
+    rho0 = np.zeros((2, 2), complex)
+    rho0[0, 0] = 1
+    bath = Bath([2 * 0.5 * 1.0 * w / (1.0 + w ** 2)], w, [1.0], [4], [0] * 5)
+    sol = DEOMSolver(sz + sx, None, bath, np.array([sx]), None, None, None, 12)
+    sol.run_batch(rho0[None], 0.01, 5)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    sol.run(rho0.copy(), 0.002, steps)
+    wall_run = time.perf_counter() - t0
+    nmax = sol.nmax
+    rate = {B: _deom_event_rate(dev, sol, bath, sz + sx, sx[None], B, steps) for B in (1, batch)}
+    bath5 = Bath([2 * 0.5 * 1.0 * w / (1.0 + w ** 2)], w, [1.0], [5], [0] * 6)
+    sol5 = DEOMSolver(sz + sx, None, bath5, np.array([sx]), None, None, None, 12)
+    sol5.check_()
+    sol5.init_()
+    rate5 = _deom_event_rate(dev, sol5, bath5, sz + sx, sx[None], 1, steps, dt=0.001)
     single = rate[1]
     # SURVEY §8(d) d4: per RK4 step ~4.75 MB of ADO traffic per hierarchy = 768 B per ADO-step
     # (4 stages x (read stage input, rho, acc + write next input, acc) of 64-B ADO rows)
@@ -719,6 +732,8 @@ def bench_deom(dev, steps, batch):
                                  "achieved": round(ado_b * bytes_per_ado_step / 1e9, 1), "peak": HBM_PEAK_GBS,
                                  "unit": "GB/s", "frac": round(ado_b * bytes_per_ado_step / 1e9 / HBM_PEAK_GBS, 4),
                                  "bytes_per_ado_step": bytes_per_ado_step}},
+        "stretch_npsd5": {"nmax": sol5.nmax, "K": sol5.nind, "L": 12, "dt": 0.001, "steps_per_s": round(rate5, 1),
+                          "ado_steps_per_s": round(rate5 * sol5.nmax, 1)},
         "roofline": {"bound": "hbm", "achieved": round(bytes_per_step * single / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(bytes_per_step * single / 1e9 / HBM_PEAK_GBS, 4),
                      "bytes_per_step": bytes_per_step,
