@@ -41,6 +41,28 @@ def measured_traffic(kernel: str, units: float):
     return (d["read_bytes_per_unit"] + d["write_bytes_per_unit"]) * units
 
 
+def synthetic_lindblad(N, seed_h=0, seed_c=1, nc=1, gamma=0.1):
+    """Seeded BASELINE config d1 inputs: GUE H/sqrt(N), dense Ginibre c_op * 0.1/sqrt(N) (the
+    same draws as the tests' oracle.lindblad.synthetic_lindblad; kept here so the timed legs import no oracle)."""
+    rng = np.random.default_rng(seed_h)
+    A = rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N))
+    H = (A + A.conj().T) / 2 / np.sqrt(N)
+    rng = np.random.default_rng(seed_c)
+    cs = []
+    for _ in range(nc):
+        C = rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N))
+        cs.append(gamma * C / np.sqrt(N))
+    return H, cs
+
+
+def random_pure_states(B, N, seed=2):
+    """B seeded random pure-state density matrices [B, N, N]."""
+    rng = np.random.default_rng(seed)
+    psi = rng.standard_normal((B, N)) + 1j * rng.standard_normal((B, N))
+    psi /= np.linalg.norm(psi, axis=1, keepdims=True)
+    return np.einsum("bi,bj->bij", psi, psi.conj())
+
+
 def lindblad_flops_per_step(N: int, nc: int, hermitian: bool = False) -> float:
     # 4 RK4 stages x (complex N^3 GEMMs per RHS) x 8 real flop per complex MAC.
     # general GLF kernel: (-iK)r, r(iK^+), C r, (C r)C^+      -> 2 + 2*nc GEMMs
@@ -101,13 +123,12 @@ def bench_redfield(dev, steps, B, N=128, dt=1e-3, warmup=3):
     """Redfield propagation in the H eigenbasis (RedfieldSolver.evolve's kernel, Hermitian-state GLF form:
     X = P rho + A rho Lam^+, d rho/dt = X + X^+), B independent density matrices."""
     import torch
-    from oracle import lindblad as olb
     from pyqed_amd.oqs import glf_rk4
     sol = redfield_inputs(N)
     P, Ls, Ws = sol.glf_terms_herm()
     t = lambda x: torch.from_numpy(np.ascontiguousarray(np.asarray(x, complex))).to(dev)
     Pd, Ld, Wd = t(P), t(Ls), t(Ws)
-    rho = t(olb.random_pure_states(B, N, seed=7))
+    rho = t(random_pure_states(B, N, seed=7))
     glf_rk4(Pd, None, Ld, Wd, rho, dt, warmup, hermitian=True)
     torch.cuda.synchronize(dev)
     stream = torch.cuda.current_stream(dev)
@@ -164,9 +185,8 @@ def bench_superop(dev, steps=10, N=128, dt=1e-3, batch=64, gemm_steps=2):
     the N = 128 Lindblad superoperator (16384^2 c128 = 4 GiB) built on the device, then (a) one density matrix on the
     HBM-streaming GEMV (16 N^4 B of L per stage) and (b) a batch on the MFMA GEMM stages."""
     import torch
-    from oracle import lindblad as olb  # seeded input synthesis only
     from pyqed_amd.oqs import lindblad_superop, superop_rk4
-    H, cs = olb.synthetic_lindblad(N, nc=1)
+    H, cs = synthetic_lindblad(N, nc=1)
     t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)
     L = lindblad_superop(t(H), t(np.array(cs)))
     N2 = N * N
@@ -183,11 +203,11 @@ def bench_superop(dev, steps=10, N=128, dt=1e-3, batch=64, gemm_steps=2):
         torch.cuda.synchronize(dev)
         return time.perf_counter() - t0, e0.elapsed_time(e1) / 1e3
 
-    v1 = t(olb.random_pure_states(1, N, seed=3).reshape(1, N2))
+    v1 = t(random_pure_states(1, N, seed=3).reshape(1, N2))
     wall, ev = timed(v1, steps)
     bytes_per_step = 4 * 16.0 * N2 * N2
     tr1 = abs(complex(torch.diagonal(v1.reshape(N, N)).sum().item()) - 1)
-    vb = t(olb.random_pure_states(batch, N, seed=4).reshape(batch, N2))
+    vb = t(random_pure_states(batch, N, seed=4).reshape(batch, N2))
     wall_b, ev_b = timed(vb, gemm_steps)
     Bp = 64 if batch <= 64 else (batch + 127) // 128 * 128
     flop_b = 4 * 8.0 * N2 * N2 * Bp
@@ -803,12 +823,11 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    from oracle import lindblad as olb  # input synthesis only (seeded); compute is libqdyn
     from pyqed_amd import lindblad_rk4
 
     N, nc, B = args.N, args.nc, args.batch
-    H, cs = olb.synthetic_lindblad(N, nc=nc)
-    rho0 = olb.random_pure_states(B, N, seed=2 + rank)
+    H, cs = synthetic_lindblad(N, nc=nc)
+    rho0 = random_pure_states(B, N, seed=2 + rank)
     Ht = torch.from_numpy(H).to(dev)
     Ct = torch.from_numpy(np.array(cs)).to(dev) if nc else None
     rho = torch.from_numpy(rho0).to(dev)
