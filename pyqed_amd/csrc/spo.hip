@@ -568,7 +568,9 @@ __device__ __forceinline__ void fft256_wave(c128 (&x)[NS][4], const Q16Tw& t, c1
 // [IFFT_y] -> V/2 -> [snapshot] -> [V/2] -> [FFT_y] -> [k_y phase].
 // Batches of wavefunctions (qd_spo2_run_batch): blockIdx.y = member w, psi / snap offset by w * wstride /
 // w * sstride (the point operators are shared).
-template <int NS>
+// KY: the Jacobi k_y factor is compiled in only where used (its 4 per-lane values would otherwise hold 16 VGPRs
+// through the whole pass: 142 -> under 128 VGPRs, 3 -> 4 waves per SIMD for the linear case).
+template <int NS, bool KY>
 __global__ __launch_bounds__(64 * NS) void spo2_row_q16_kernel(c128* psi, const c128* U, const c128* twy, int flags,
                                                                c128* snap, const c128* expKy, size_t wstride = 0,
                                                                size_t sstride = 0) {
@@ -587,7 +589,7 @@ __global__ __launch_bounds__(64 * NS) void spo2_row_q16_kernel(c128* psi, const 
 #pragma unroll
       for (int b = 0; b < NS; ++b) u[a][b] = U[(pt * NS + c) * NS + b];   // row c of the point's operator
     }
-    ky[a] = (flags & ROW_KY) ? expKy[pt] : cmk(1, 0);
+    if constexpr (KY) ky[a] = expKy[pt];
   }
   const Q16Tw t = q16_twiddles(twy, g, s);
   c128* Sw = S + c * 272;
@@ -614,9 +616,11 @@ __global__ __launch_bounds__(64 * NS) void spo2_row_q16_kernel(c128* psi, const 
   }
   if (flags & ROW_VH2) point_op();
   if (flags & ROW_FWD) fft256_wave<false, 1>(x, t, Sw, g, s);
-  if (flags & ROW_KY) {
+  if constexpr (KY) {
+    if (flags & ROW_KY) {
 #pragma unroll
-    for (int a = 0; a < 4; ++a) x[0][a] = cmul(ky[a], x[0][a]);
+      for (int a = 0; a < 4; ++a) x[0][a] = cmul(ky[a], x[0][a]);
+    }
   }
 #pragma unroll
   for (int a = 0; a < 4; ++a) psi[(row + 64 * a + 16 * s + g) * NS + c] = x[0][a];
@@ -730,8 +734,11 @@ int twiddles(int L, hipStream_t st, c128* tw) {
 int row_fast(int L, int ns, int rows, int flags, c128* psi, const c128* U, const c128* tw, c128* snap,
              const c128* expKy, hipStream_t st) {
   if (L == 256 && q16_enabled()) {
-    if (ns == 1) hipLaunchKernelGGL(spo2_row_q16_kernel<1>, dim3(rows), dim3(64), 0, st, psi, U, tw, flags, snap, expKy);
-    else hipLaunchKernelGGL(spo2_row_q16_kernel<2>, dim3(rows), dim3(128), 0, st, psi, U, tw, flags, snap, expKy);
+    const bool ky = (flags & ROW_KY) && expKy;
+#define RQ16(NS, KYV) hipLaunchKernelGGL((spo2_row_q16_kernel<NS, KYV>), dim3(rows), dim3(64 * NS), 0, st, psi, U, tw, flags, snap, expKy)
+    if (ns == 1) { if (ky) RQ16(1, true); else RQ16(1, false); }
+    else { if (ky) RQ16(2, true); else RQ16(2, false); }
+#undef RQ16
     QD_HIP(hipGetLastError());
     return QD_OK;
   }
@@ -904,10 +911,10 @@ extern "C" int qd_spo2_run_batch(qd_c128* psi_, int B, const qd_c128* expVh_, co
   const size_t sstride = (size_t)nsave * grid_elems;
   auto row = [&](int flags, c128* sp) {
     if (ns == 1)
-      hipLaunchKernelGGL(spo2_row_q16_kernel<1>, dim3(nx, B), dim3(64), 0, st, psi, U, twy, flags, sp,
+      hipLaunchKernelGGL((spo2_row_q16_kernel<1, false>), dim3(nx, B), dim3(64), 0, st, psi, U, twy, flags, sp,
                          (const c128*)nullptr, grid_elems, sstride);
     else
-      hipLaunchKernelGGL(spo2_row_q16_kernel<2>, dim3(nx, B), dim3(128), 0, st, psi, U, twy, flags, sp,
+      hipLaunchKernelGGL((spo2_row_q16_kernel<2, false>), dim3(nx, B), dim3(128), 0, st, psi, U, twy, flags, sp,
                          (const c128*)nullptr, grid_elems, sstride);
   };
   static const bool tile_col = [] {  // QD_SPO_COLTILE=0: the per-column pass (A/B)
