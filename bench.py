@@ -222,7 +222,10 @@ def bench_superop(dev, steps=10, N=128, dt=1e-3, batch=64, gemm_steps=2):
         "roofline": {"bound": "hbm", "kernel": "superop_rows_kernel<1,4,4>",
                      "achieved": round(bytes_per_step * steps / ev / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(bytes_per_step * steps / ev / 1e9 / HBM_PEAK_GBS, 4),
-                     "bytes_per_step": bytes_per_step, "traffic": None},
+                     "bytes_per_step": bytes_per_step,
+                     "traffic": measured_traffic("superop_rows_kernel<1,4,4>", 1) if N == 128 else None,
+                     "traffic_unit": "HBM bytes per RK4 step (PMC FETCH_SIZE+WRITE_SIZE, calibrated; "
+                                     "profiles/pmc_traffic.json)"},
         "trace_err": tr1,
         "batched": {"batch": batch, "steps": gemm_steps, "dm_steps_per_s": round(batch * gemm_steps / wall_b, 1),
                     "ms_per_step": round(ev_b / gemm_steps * 1e3, 3),
@@ -751,7 +754,11 @@ def bench_deom(dev, steps, batch):
                     "roofline": {"bound": "hbm", "kernel": "deom_stage_grp_kernel<4,6,true>",
                                  "achieved": round(ado_b * bytes_per_ado_step / 1e9, 1), "peak": HBM_PEAK_GBS,
                                  "unit": "GB/s", "frac": round(ado_b * bytes_per_ado_step / 1e9 / HBM_PEAK_GBS, 4),
-                                 "bytes_per_ado_step": bytes_per_ado_step}},
+                                 "bytes_per_ado_step": bytes_per_ado_step,
+                                 "traffic": measured_traffic("deom_stage_grp_kernel<4,6,true>_64h", nmax * batch / 4)
+                                 if batch == 64 else None,
+                                 "traffic_unit": "HBM bytes per stage launch (PMC FETCH_SIZE+WRITE_SIZE, calibrated; "
+                                                 "profiles/pmc_traffic.json)"}},
         "stretch_npsd5": {"nmax": sol5.nmax, "K": sol5.nind, "L": 12, "dt": 0.001, "steps_per_s": round(rate5, 1),
                           "ado_steps_per_s": round(rate5 * sol5.nmax, 1)},
         "roofline": {"bound": "hbm", "achieved": round(bytes_per_step * single / 1e9, 1), "peak": HBM_PEAK_GBS,
