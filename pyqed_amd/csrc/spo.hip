@@ -367,6 +367,50 @@ __global__ __launch_bounds__(256) void spo_mid_kernel(c128* psi, const c128* tw_
   }
 }
 
+// Latency-shaped middle-axis pass (same transforms and arithmetic as spo_mid_kernel): the block size is fixed at
+// compile time (BD = C L / 4 threads, IT = 4 elements per thread), so every global load of the pass (the C
+// columns of 16-B pieces and the twiddles) is issued before the first wait and every store after the transform:
+// one load round trip + one store drain per pass instead of IT dependent load / LDS-store iterations.
+template <int L, int C, bool INV>
+__global__ __launch_bounds__(C * L / 4 < 64 ? 64 : C * L / 4) void spo_mid_fast_kernel(c128* psi, const c128* tw_g,
+                                                                                       int inner) {
+  constexpr int BD = C * L / 4 < 64 ? 64 : C * L / 4;
+  constexpr int IT = (L * C + BD - 1) / BD;
+  constexpr bool FULL = (L * C) % BD == 0;
+  __shared__ c128 tw[L];
+  __shared__ c128 A[C * L], Bf[C * L];  // layout [c][j]
+  const int chunks = inner / C;
+  const int i = blockIdx.x / chunks, c0 = (blockIdx.x % chunks) * C;
+  c128* base = psi + (size_t)i * L * inner + c0;
+  const int tid = threadIdx.x;
+  c128 v[IT];
+#pragma unroll
+  for (int n = 0; n < IT; ++n) {
+    const int e = tid + n * BD;  // c = e % C fastest: C * 16 B contiguous per row j
+    v[n] = (FULL || e < L * C) ? base[(size_t)(e / C) * inner + e % C] : cmk(0, 0);
+  }
+  static_assert(L <= BD, "one twiddle per thread");
+  const c128 twv = tid < L ? tw_g[tid] : cmk(0, 0);
+  if (tid < L) tw[tid] = twv;
+#pragma unroll
+  for (int n = 0; n < IT; ++n) {
+    const int e = tid + n * BD;
+    if (FULL || e < L * C) A[(e % C) * L + e / C] = v[n];
+  }
+  __syncthreads();
+  constexpr int T = L / 4;
+  const int f = tid / T, t = tid % T;
+  const bool active = f < C;
+  const int fo = (active ? f : 0) * L;
+  c128* r = fft_lds<L, INV>(A + fo, Bf + fo, tw, t, active);
+  const c128* cur = (r == A + fo) ? A : Bf;
+#pragma unroll
+  for (int n = 0; n < IT; ++n) {
+    const int e = tid + n * BD;
+    if (FULL || e < L * C) base[(size_t)(e / C) * inner + e % C] = cur[(e % C) * L + e / C];
+  }
+}
+
 // expKT[j][i] = expK[i][j] * scale
 __global__ void transpose_scale_kernel(const c128* expK, int nx, int ny, double scale, c128* expKT) {
   const size_t tot = (size_t)nx * ny;
@@ -1039,7 +1083,24 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
     const int c = atoi(e);
     if (c == 0 || ((c == 2 || c == 4 || c == 8) && nyz % c == 0 && c * ns * (nx / 4) <= 256)) colC = c;
   }
+  // QD_SPO3_FAST=0: the generic LDS-staged mid / x kernels instead of the latency-shaped ones (A/B runs)
+  const char* f3e = getenv("QD_SPO3_FAST");
+  const bool fast3 = !(f3e && f3e[0] == '0');
   auto col = [&]() -> int {
+    if (colC && fast && fast3) {
+      const int threads = std::max(64, colC * ns * (nx / 4));
+      const size_t lds = (size_t)(nx + 2 * colC * ns * nx) * sizeof(c128);
+#define COLFASTC(L)                                                                                                       if (colC == 2) { if (ns == 1) hipLaunchKernelGGL((spo2_col_fast_kernel<L, 2, 1>), dim3(nyz / 2), dim3(threads), lds, st, psi, expKT, twx, nyz);                    else hipLaunchKernelGGL((spo2_col_fast_kernel<L, 2, 2>), dim3(nyz / 2), dim3(threads), lds, st, psi, expKT, twx, nyz); }   else if (colC == 4) { if (ns == 1) hipLaunchKernelGGL((spo2_col_fast_kernel<L, 4, 1>), dim3(nyz / 4), dim3(threads), lds, st, psi, expKT, twx, nyz);                    else hipLaunchKernelGGL((spo2_col_fast_kernel<L, 4, 2>), dim3(nyz / 4), dim3(threads), lds, st, psi, expKT, twx, nyz); }   else { if (ns == 1) hipLaunchKernelGGL((spo2_col_fast_kernel<L, 8, 1>), dim3(nyz / 8), dim3(threads), lds, st, psi, expKT, twx, nyz);          else hipLaunchKernelGGL((spo2_col_fast_kernel<L, 8, 2>), dim3(nyz / 8), dim3(threads), lds, st, psi, expKT, twx, nyz); }
+      switch (nx) {
+        case 16: COLFASTC(16); break;
+        case 32: COLFASTC(32); break;
+        case 64: COLFASTC(64); break;
+        default: return QD_EINVAL;   // colC is set only at <= 64^3 x 2 points
+      }
+#undef COLFASTC
+      QD_HIP(hipGetLastError());
+      return QD_OK;
+    }
     if (colC) {
       const int threads = std::max(64, colC * ns * (nx / 4));
       const size_t lds = (size_t)(nx + 2 * colC * ns * nx) * sizeof(c128);
@@ -1063,6 +1124,24 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
   auto mid = [&](bool inv) -> int {
     const int grid = nx * (inner / midC);
     const int threads = std::max(64, midC * (ny / 4));
+    if (fast3 && midC * ny / 4 <= 256 && ny <= 64) {
+#define MIDF_C(L, C)                                                                                               \
+  if (inv) hipLaunchKernelGGL((spo_mid_fast_kernel<L, C, true>), dim3(grid), dim3(threads), 0, st, psi, twy, inner); \
+  else hipLaunchKernelGGL((spo_mid_fast_kernel<L, C, false>), dim3(grid), dim3(threads), 0, st, psi, twy, inner)
+#define MIDF(L)                          \
+  if (midC == 16) { MIDF_C(L, 16); }     \
+  else if (midC == 8) { MIDF_C(L, 8); }  \
+  else { MIDF_C(L, 4); }
+      switch (ny) {
+        case 16: MIDF(16); break;
+        case 32: MIDF(32); break;
+        default: MIDF(64); break;
+      }
+#undef MIDF
+#undef MIDF_C
+      QD_HIP(hipGetLastError());
+      return QD_OK;
+    }
 #define MIDCALL_C(L, C)                                                                                      \
   if (inv) hipLaunchKernelGGL((spo_mid_kernel<L, C, true>), dim3(grid), dim3(threads), 0, st, psi, twy, inner); \
   else hipLaunchKernelGGL((spo_mid_kernel<L, C, false>), dim3(grid), dim3(threads), 0, st, psi, twy, inner)

@@ -124,10 +124,15 @@ def test_spo3_matches_reference():
     assert relerr(r.psi, g["psi"]) < TOL
 
 
-@pytest.mark.parametrize("mid_c,col_c", [(None, None), ("4", "2"), ("8", "4"), ("16", "8"), ("8", None), (None, "0")])
-def test_spo3_example_size_vs_oracle(mid_c, col_c, monkeypatch):
+@pytest.mark.parametrize("mid_c,col_c,fast", [(None, None, None), ("4", "2", None), ("8", "4", None),
+                                               ("16", "8", None), ("8", None, None), (None, "0", None),
+                                               (None, None, "0"), ("16", "8", "0")])
+def test_spo3_example_size_vs_oracle(mid_c, col_c, fast, monkeypatch):
     """examples/spo.py size: 64^3 x 2, vs the NumPy fftn restatement, and norm conservation; every
-    mid-axis and x-axis block width (QD_SPO3_MID_C / QD_SPO3_COL_C; None = the default launch)."""
+    mid-axis and x-axis block width (QD_SPO3_MID_C / QD_SPO3_COL_C; None = the default launch), on the
+    latency-shaped mid / x kernels (default) and the generic LDS-staged ones (QD_SPO3_FAST=0)."""
+    if fast is not None:
+        monkeypatch.setenv("QD_SPO3_FAST", fast)
     if mid_c is not None:
         monkeypatch.setenv("QD_SPO3_MID_C", mid_c)
     if col_c is not None:
