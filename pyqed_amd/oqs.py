@@ -623,14 +623,14 @@ class RedfieldSolver:
         """Liouville-space Green's function with Redfield dissipation (oqs.py:136-158).
         'EOM': -1j * expm(R, t), i.e. -1j U_k for every t_k as an (nL, nL, nt) array (the reference multiplies the
         expm list by -1j, which raises; the array is its evident meaning).  'eseries' / 'diag' / 'diagonalization':
-        getG(1j R, t) (oqs.py:465-508), G(t) = -1j exp(R t) in the eigen form, evaluated on the GPU."""
+        getG(1j R, t) (oqs.py:465-508), G(t) = -1j exp(R t) in the eigen form, evaluated on the GPU.  As in the
+        reference, `w`, `k` and `domain` are accepted and unused (gf calls getG(1j R, t) with getG's default
+        domain='time')."""
         if self.R is None:
             self.redfield_tensor(secular=secular)
         if method == 'EOM':
             return -1j * self._propagator_eom(self.R, t)
         if method in ['eseries', 'diag', 'diagonalization']:
-            if domain != 'time':
-                raise NotImplementedError("gf: only domain='time' (getG's 'freq' branch needs w and U2^*)")
             from .response import sos_eig, sos_propagator
             lam, U1, U2 = sos_eig(self.R)
             return -1j * sos_propagator(lam, U1, U2, np.asarray(t, dtype=float)).cpu().numpy()

@@ -37,6 +37,8 @@ def test_redfield_propagator_eom_and_gf_match_reference():
     assert relerr(sol.G, -1j * g["U_eom"]) < TOL
     assert relerr(sol.gf(t, method="EOM"), -1j * g["U_eom"]) < TOL
     assert relerr(sol.gf(t, method="eseries"), g["G_eseries"]) < 1e-9
+    # the reference's gf never forwards `domain` to getG (time domain whatever is asked)
+    assert relerr(sol.gf(t, method="eseries", domain="freq"), g["G_eseries"]) < 1e-9
     U_sos = sol.propagator(t, method="SOS")
     assert relerr(U_sos, g["U_eom"]) < 1e-4   # RK4 truncation at dt = 0.05
     with pytest.raises(NotImplementedError):
