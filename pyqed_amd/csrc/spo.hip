@@ -670,6 +670,67 @@ __global__ __launch_bounds__(64 * NS) void spo2_row_q16_kernel(c128* psi, const 
   for (int a = 0; a < 4; ++a) psi[(row + 64 * a + 16 * s + g) * NS + c] = x[0][a];
 }
 
+// Row pass for batches (qd_spo2_run_batch, ns = 2): one workgroup per (row i, MB members), wave w = (member
+// w >> 1, state w & 1).  The point operators of row i are shared by every member: the workgroup stages them in
+// LDS once (16 KB, two loads per thread) instead of every wave loading its 8 values per lane from L2 (two thirds of
+// the single-row kernel's loads).  The FFT exchange buffers double as the point-operator exchange (they are never
+// live at the same time).  Same arithmetic and order as spo2_row_q16_kernel<2, false>.
+template <int MB>
+__global__ __launch_bounds__(128 * MB) void spo2_row_q16_batch_kernel(c128* psi, const c128* U, const c128* twy,
+                                                                      int flags, c128* snap, int B, size_t wstride,
+                                                                      size_t sstride) {
+  __shared__ c128 Us[256 * 4];          // [point][row c][col b]
+  __shared__ c128 S[2 * MB * 272];      // per-wave FFT exchange; per member [2][256] point-operator exchange
+  const int i = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 2, s = lane & 3;
+  const int m = w >> 1, c = w & 1;
+  const int member = blockIdx.y * MB + m;
+  const bool live = member < B;          // uniform per wave; dead waves still join the barriers
+  c128* ps = psi + (size_t)(live ? member : 0) * wstride;
+  const size_t row = (size_t)i * 256;
+  c128 x[1][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) x[0][a] = ps[(row + 64 * a + 16 * s + g) * 2 + c];
+  const bool vh = flags & (ROW_VH1 | ROW_VH2);
+  if (vh) {
+#pragma unroll
+    for (int q = 0; q < 1024 / (128 * MB); ++q) {
+      const int e = threadIdx.x + 128 * MB * q;
+      Us[e] = U[row * 4 + e];
+    }
+  }
+  const Q16Tw t = q16_twiddles(twy, g, s);
+  c128* Sw = S + w * 272;
+  c128* Xs = S + m * 2 * 272;            // member m's exchange: [state][lane * 4 + a] (2 x 256 <= 2 x 272)
+  if (vh) __syncthreads();
+  auto point_op = [&]() {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) Xs[c * 256 + lane * 4 + a] = x[0][a];
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int pt = 64 * a + 16 * s + g;
+      c128 acc = cmk(0, 0);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc = cadd(acc, cmul(Us[pt * 4 + c * 2 + b], Xs[b * 256 + lane * 4 + a]));
+      x[0][a] = acc;
+    }
+    __syncthreads();   // Xs aliases the FFT buffers and is rewritten by the next operator
+  };
+  if (flags & ROW_INV) fft256_wave<true, 1>(x, t, Sw, g, s);
+  if (flags & (ROW_VH1 | ROW_VH2)) __syncthreads();   // every wave is done with its FFT buffer before Xs reuses it
+  if (flags & ROW_VH1) point_op();
+  if ((flags & ROW_SNAP) && live) {
+    c128* sn = snap + (size_t)member * sstride;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) sn[(row + 64 * a + 16 * s + g) * 2 + c] = x[0][a];
+  }
+  if (flags & ROW_VH2) point_op();
+  if (flags & ROW_FWD) fft256_wave<false, 1>(x, t, Sw, g, s);
+  if (!live) return;
+#pragma unroll
+  for (int a = 0; a < 4; ++a) ps[(row + 64 * a + 16 * s + g) * 2 + c] = x[0][a];
+}
+
 // Column pass of spo2_col_fast_kernel for L = nx = 256: one 64-lane workgroup per (column j, state c)
 // (no state mixing in this pass): FFT_x -> * exp_K / (nx ny) -> IFFT_x.  Blocks of one XCD (blockIdx.x
 // % 8) take a contiguous run of columns, so the pieces that adjacent columns read from one row share
@@ -953,10 +1014,20 @@ extern "C" int qd_spo2_run_batch(qd_c128* psi_, int B, const qd_c128* expVh_, co
                      (const c128*)expK_, nx, ny, 1.0 / ((double)nx * ny), expKT);
   QD_HIP(hipGetLastError());
   const size_t sstride = (size_t)nsave * grid_elems;
+  // ns = 2: MB members per workgroup sharing the staged point operators (QD_SPO_ROWMB = 1 / 2 / 4, default 2; 1 = the
+  // single-row kernel with a batch grid axis)
+  const char* mbe = getenv("QD_SPO_ROWMB");
+  const int rowmb = mbe ? atoi(mbe) : 2;   // 64 wavepackets: MB = 1 405k, 2 438k, 4 418k wavepacket-steps/s
   auto row = [&](int flags, c128* sp) {
     if (ns == 1)
       hipLaunchKernelGGL((spo2_row_q16_kernel<1, false>), dim3(nx, B), dim3(64), 0, st, psi, U, twy, flags, sp,
                          (const c128*)nullptr, grid_elems, sstride);
+    else if (rowmb == 4)
+      hipLaunchKernelGGL(spo2_row_q16_batch_kernel<4>, dim3(nx, (B + 3) / 4), dim3(512), 0, st, psi, U, twy, flags,
+                         sp, B, grid_elems, sstride);
+    else if (rowmb == 2)
+      hipLaunchKernelGGL(spo2_row_q16_batch_kernel<2>, dim3(nx, (B + 1) / 2), dim3(256), 0, st, psi, U, twy, flags,
+                         sp, B, grid_elems, sstride);
     else
       hipLaunchKernelGGL((spo2_row_q16_kernel<2, false>), dim3(nx, B), dim3(128), 0, st, psi, U, twy, flags, sp,
                          (const c128*)nullptr, grid_elems, sstride);

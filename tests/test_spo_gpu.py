@@ -243,11 +243,15 @@ def test_device_point_propagators_match_eigh(ns, cplx):
     assert (sol.apes is None) if cplx else np.array_equal(sol.apes, w2)
 
 
-@pytest.mark.parametrize("n,ns,B", [(256, 2, 5), (256, 1, 3), (64, 2, 2)])
-def test_spo2_run_batch_vs_single_and_oracle(n, ns, B):
+@pytest.mark.parametrize("n,ns,B,rowmb", [(256, 2, 5, None), (256, 2, 6, "4"), (256, 2, 3, "1"), (256, 1, 3, None),
+                                          (64, 2, 2, None)])
+def test_spo2_run_batch_vs_single_and_oracle(n, ns, B, rowmb, monkeypatch):
     """SPO2.run_batch (qd_spo2_run_batch: one launch per pass for B wavepackets; 256x256 register-FFT kernels
     with a batch grid axis, member by member for other shapes): every member equals run() of that member
-    and the oracle's Strang steps, snapshots included."""
+    and the oracle's Strang steps, snapshots included.  ns = 2 row passes run MB members per workgroup sharing the
+    staged point operators (QD_SPO_ROWMB: default 2, 4, or 1 = one member per workgroup); ragged last groups."""
+    if rowmb is not None:
+        monkeypatch.setenv("QD_SPO_ROWMB", rowmb)
     from oracle import spo as ospo
     from pyqed_amd.wpd import SPO2
     x = np.linspace(-6, 6, n)
