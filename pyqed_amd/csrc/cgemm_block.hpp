@@ -198,6 +198,75 @@ __device__ __forceinline__ void cg_block_gemm_gen(int T, APol& pa, BPol& pb, CgL
   }
 }
 
+// The same engine with the global loads issued two K-tiles ahead (two register sets, loop unrolled by two so
+// the set index is a compile-time constant): a tile's loads have two tiles of MFMA work to arrive instead of
+// three k-steps, for blocks whose MFMA time per K-tile is short (BT = 64: 1.9 us per tile per SIMD) next to
+// the fabric latency of operands served from the Infinity Cache.  Same results as cg_block_gemm_gen
+// (identical MFMA order).
+template <int BT, bool PIPE = false, typename APol, typename BPol>
+__device__ __forceinline__ void cg_block_gemm_gen2(int T, APol& pa, BPol& pb, CgLds<BT>& L, CgAcc<BT>& acc) {
+  constexpr int MW = CgCfg<BT>::MW, NW = CgCfg<BT>::NW, WC = CgCfg<BT>::WC, WR = CgCfg<BT>::WR;
+  const int wave = threadIdx.x >> 6;
+  const bool active = wave < WR * WC;
+  const int wr0 = (wave / WC) * (MW * 16);
+  const int wc0 = (wave % WC) * (NW * 16);
+#pragma unroll
+  for (int mi = 0; mi < MW; ++mi)
+#pragma unroll
+    for (int nj = 0; nj < NW; ++nj) {
+      acc.re[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
+      acc.im[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
+    }
+  constexpr int NLD = cg_nld<BT>();
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  typename APol::Raw ra[2][NLD];
+  typename BPol::Raw rb[2][NLD];
+  auto load = [&](int t, auto slot) {
+#pragma unroll
+    for (int q = 0; q < NLD; ++q) {
+      const int e = tid + CG_WG * q;
+      ra[slot()][q] = pa.fetch(t, e, q);
+      rb[slot()][q] = pb.fetch(t, e, q);
+    }
+  };
+  auto store = [&](int t, int buf, auto slot) {
+#pragma unroll
+    for (int q = 0; q < NLD; ++q) {
+      const int e = tid + CG_WG * q;
+      cg_st_lds(&L.a[buf][(e >> 4) * CG_SA + (e & 15)], pa.finish(ra[slot()][q], t, e, q));
+      cg_st_lds(&L.b[buf][e], pb.finish(rb[slot()][q], t, e, q));
+    }
+  };
+  struct S0 { constexpr int operator()() const { return 0; } };
+  struct S1 { constexpr int operator()() const { return 1; } };
+  load(0, S0{});
+  if (T > 1) load(1, S1{});
+  store(0, 0, S0{});
+  __syncthreads();
+  // iteration t: tile t+1 sits in register set (t+1)&1 and goes to LDS during tile t's MFMAs; tile t+2 is
+  // loaded into set t&1 (tile t left it at iteration t-1)
+  auto step = [&](int t, auto cur, auto nxt) {
+    if (t + 2 < T) load(t + 2, cur);
+    const bool more = (t + 1) < T;
+    auto mid = [&]() {
+      if (more) store(t + 1, (t + 1) & 1, nxt);
+    };
+    if (active) {
+      cg_compute_tile<BT, PIPE>(L, t & 1, acc, wr0, wc0, mid);
+    } else {
+      mid();
+    }
+    __syncthreads();
+  };
+  int t = 0;
+  for (; t + 1 < T; t += 2) {
+    step(t, S0{}, S1{});
+    step(t + 1, S1{}, S0{});
+  }
+  if (t < T) step(t, S0{}, S1{});
+}
+
 // Policies that read row-major complex tiles from memory through segment tables in LDS.
 template <int BT>
 struct CgSegA {

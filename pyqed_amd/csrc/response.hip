@@ -400,7 +400,7 @@ __device__ __forceinline__ void ens_tile(int& bn, int& bm, int& s) {
 // grid: (n1p/BT) x (n3p/BT) x S ; each workgroup accumulates K-tiles [t0, t1) of its block.  BT = 64 for
 // problems whose 128-blocks cannot fill the chip with >= 4 K-tiles per workgroup (4x the blocks, 1/4 the
 // split-K slabs to write and reduce).
-template <int BT, bool XTAB>
+template <int BT, bool XTAB, int DEPTH = 1>
 __global__ __launch_bounds__(CG_WG) void ens_gemm_kernel(const c128* X, int Kp, const c128* Z, int n1p, int tiles,
                                                          int S, c128* slabs, int n3p, const c128* fine) {
   __shared__ CgLds<BT> L;
@@ -416,7 +416,10 @@ __global__ __launch_bounds__(CG_WG) void ens_gemm_kernel(const c128* X, int Kp, 
       cg_block_gemm_gen<BT, ENS_PIPE>(t1 - t0, pa, pb, L, A);
     } else {
       EnsXA pa{X, Kp, bm * BT, t0 * CG_KT};
-      cg_block_gemm_gen<BT, ENS_PIPE>(t1 - t0, pa, pb, L, A);
+      if constexpr (DEPTH == 2)
+        cg_block_gemm_gen2<BT, ENS_PIPE>(t1 - t0, pa, pb, L, A);
+      else
+        cg_block_gemm_gen<BT, ENS_PIPE>(t1 - t0, pa, pb, L, A);
     }
     cg_epilogue<BT>(A, [&](int row, int col, c128 v) {
       slab[(size_t)(bm * BT + row) * n1p + bn * BT + col] = v;
@@ -459,9 +462,15 @@ SplitPlan split_plan(int Mp, int Np, int tiles) {
 void launch_ens_gemm(const SplitPlan& pl, const c128* X, int Kp, const c128* Z, int Mp, int Np, int tiles,
                      c128* slabs, hipStream_t st, const c128* fine = nullptr) {
   const dim3 g(Np / pl.bt, Mp / pl.bt, pl.S);
+  // QD_ENS_DEPTH=1/2: K-tiles of global loads in flight on the 64-block path (read per call: tests switch it)
+  // 4,096-member shard: 0.111 ms per grid at 2 vs 0.113 at 1 (tools/ens_depth_ab.sh)
+  const char* de = std::getenv("QD_ENS_DEPTH");
+  const int depth = de ? std::atoi(de) : 2;
   if (pl.bt == 64) {
     if (fine)
       hipLaunchKernelGGL((ens_gemm_kernel<64, true>), g, dim3(CG_WG), 0, st, X, Kp, Z, Np, tiles, pl.S, slabs, Mp, fine);
+    else if (depth == 2)
+      hipLaunchKernelGGL((ens_gemm_kernel<64, false, 2>), g, dim3(CG_WG), 0, st, X, Kp, Z, Np, tiles, pl.S, slabs, Mp, fine);
     else
       hipLaunchKernelGGL((ens_gemm_kernel<64, false>), g, dim3(CG_WG), 0, st, X, Kp, Z, Np, tiles, pl.S, slabs, Mp, fine);
   } else {

@@ -731,6 +731,86 @@ __global__ __launch_bounds__(128 * MB) void spo2_row_q16_batch_kernel(c128* psi,
   for (int a = 0; a < 4; ++a) ps[(row + 64 * a + 16 * s + g) * 2 + c] = x[0][a];
 }
 
+// Row pass for batches, one wave per (row i, member): the wave holds both states of its points (x[c][a] =
+// psi[64 a + 16 s + g][c]), so the point operators are lane-local (no state exchange through LDS, no workgroup
+// barrier but the one after the operator staging) and every lane loads 32 contiguous bytes per point.  The MB
+// waves of a workgroup are MB members of one row and share the row's point operators, staged in LDS once.  The
+// two states' 256-point transforms run one after the other through one 272-entry exchange buffer per wave (LDS
+// per workgroup 16 KB + MB x 4.25 KB: four workgroups of MB = 4 per CU).  Same arithmetic and order as
+// spo2_row_q16_kernel<2, false>, so the results are bit-identical.
+template <int MB>
+__global__ __launch_bounds__(64 * MB) void spo2_row_wave_kernel(c128* psi, const c128* U, const c128* twy, int flags,
+                                                                c128* snap, int B, size_t wstride, size_t sstride) {
+  __shared__ c128 Us[256 * 4];          // [point][row c][col b]
+  __shared__ c128 S[MB * 272];          // per-wave FFT exchange
+  const int i = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 2, s = lane & 3;
+  const int member = blockIdx.y * MB + w;
+  const bool live = member < B;          // uniform per wave; dead waves still join the staging barrier
+  c128* ps = psi + (size_t)(live ? member : 0) * wstride;
+  const size_t row = (size_t)i * 256;
+  c128 x[2][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const size_t pt = row + 64 * a + 16 * s + g;
+    x[0][a] = ps[pt * 2];
+    x[1][a] = ps[pt * 2 + 1];
+  }
+  const bool vh = flags & (ROW_VH1 | ROW_VH2);
+  if (vh) {
+#pragma unroll
+    for (int q = 0; q < 1024 / (64 * MB); ++q) {
+      const int e = threadIdx.x + 64 * MB * q;
+      Us[e] = U[row * 4 + e];
+    }
+  }
+  const Q16Tw t = q16_twiddles(twy, g, s);
+  c128* Sw = S + w * 272;
+  auto line = [&](int c) -> c128 (&)[1][4] { return *reinterpret_cast<c128(*)[1][4]>(&x[c][0]); };
+  if (vh) __syncthreads();
+  if (!live) return;
+  auto point_op = [&]() {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int pt = 64 * a + 16 * s + g;
+      c128 y[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        c128 acc = cmk(0, 0);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc = cadd(acc, cmul(Us[pt * 4 + c * 2 + b], x[b][a]));
+        y[c] = acc;
+      }
+      x[0][a] = y[0];
+      x[1][a] = y[1];
+    }
+  };
+  if (flags & ROW_INV) {
+    fft256_wave<true, 1>(line(0), t, Sw, g, s);
+    fft256_wave<true, 1>(line(1), t, Sw, g, s);
+  }
+  if (flags & ROW_VH1) point_op();
+  if (flags & ROW_SNAP) {
+    c128* sn = snap + (size_t)member * sstride;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const size_t pt = row + 64 * a + 16 * s + g;
+      sn[pt * 2] = x[0][a];
+      sn[pt * 2 + 1] = x[1][a];
+    }
+  }
+  if (flags & ROW_VH2) point_op();
+  if (flags & ROW_FWD) {
+    fft256_wave<false, 1>(line(0), t, Sw, g, s);
+    fft256_wave<false, 1>(line(1), t, Sw, g, s);
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const size_t pt = row + 64 * a + 16 * s + g;
+    ps[pt * 2] = x[0][a];
+    ps[pt * 2 + 1] = x[1][a];
+  }
+}
+
 // Column pass of spo2_col_fast_kernel for L = nx = 256: one 64-lane workgroup per (column j, state c)
 // (no state mixing in this pass): FFT_x -> * exp_K / (nx ny) -> IFFT_x.  Blocks of one XCD (blockIdx.x
 // % 8) take a contiguous run of columns, so the pieces that adjacent columns read from one row share
@@ -803,6 +883,66 @@ __global__ __launch_bounds__(512) void spo2_col_tile_kernel(c128* psi, const c12
   for (int q = 0; q < 4; ++q) {
     const int e = tid + 512 * q, r = e >> 3, cs = e & 7;
     psi[((size_t)r * 256 + j0) * 2 + cs] = T[r * 9 + cs];
+  }
+}
+
+// Column pass for batches with NC adjacent columns per 64 NC-thread workgroup and one wave per column holding
+// both states (x[c][a], c = state): the 256 x NC x 2 tile is read and written as NC x 32-B contiguous row pieces
+// (256 B at NC = 8), and the waves' FFT exchange buffers live inside the tile (it is dead between the line reads
+// and the write-back), so the workgroup's LDS is the tile alone (NC = 8: 68 KB, two workgroups per CU as the
+// 4-column kernel).  Same arithmetic per line as spo2_col_tile_kernel.  NS = 2, nx = ny = 256.
+template <int NC>
+__global__ __launch_bounds__(64 * NC) void spo2_col_tile8_kernel(c128* psi, const c128* expKT, const c128* twx,
+                                                                 size_t wstride) {
+  constexpr int TW = 2 * NC + 1;     // tile row stride: 2 NC lines + 1 pad
+  __shared__ c128 T[256 * TW];       // [row][lines]; per-wave FFT exchange T + w * 272 in between
+  psi += blockIdx.y * wstride;
+  const int j0 = blockIdx.x * NC;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 2, s = lane & 3;
+  const int j = j0 + w;
+  {
+    c128 v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {    // element e = row * 2 NC + (column - j0) * 2 + state
+      const int e = tid + 64 * NC * q, r = e / (2 * NC), cs = e % (2 * NC);
+      v[q] = psi[((size_t)r * 256 + j0) * 2 + cs];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = tid + 64 * NC * q;
+      T[(e / (2 * NC)) * TW + e % (2 * NC)] = v[q];
+    }
+  }
+  c128 kf[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) kf[a] = expKT[(size_t)j * 256 + 64 * a + 16 * s + g];
+  __syncthreads();
+  c128 x[2][4];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int a = 0; a < 4; ++a) x[c][a] = T[(64 * a + 16 * s + g) * TW + 2 * w + c];
+  const Q16Tw t = q16_twiddles(twx, g, s);
+  __syncthreads();                   // every wave has its lines: the tile becomes the FFT exchange
+  c128* Sw = T + w * 272;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    c128(&xl)[1][4] = *reinterpret_cast<c128(*)[1][4]>(&x[c][0]);
+    fft256_wave<false, 1>(xl, t, Sw, g, s);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) x[c][a] = cmul(x[c][a], kf[a]);
+    fft256_wave<true, 1>(xl, t, Sw, g, s);
+  }
+  __syncthreads();                   // every wave is done with its exchange region
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int a = 0; a < 4; ++a) T[(64 * a + 16 * s + g) * TW + 2 * w + c] = x[c][a];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int e = tid + 64 * NC * q, r = e / (2 * NC), cs = e % (2 * NC);
+    psi[((size_t)r * 256 + j0) * 2 + cs] = T[r * TW + cs];
   }
 }
 
@@ -1018,10 +1158,23 @@ extern "C" int qd_spo2_run_batch(qd_c128* psi_, int B, const qd_c128* expVh_, co
   // single-row kernel with a batch grid axis)
   const char* mbe = getenv("QD_SPO_ROWMB");
   const int rowmb = mbe ? atoi(mbe) : 2;   // 64 wavepackets: MB = 1 405k, 2 438k, 4 418k wavepacket-steps/s
+  // QD_SPO_ROWWAVE: members per workgroup of the wave-per-member row kernel (2 / 4 / 8; 0 = the group kernels above,
+  // which an explicit QD_SPO_ROWMB also selects); 64 wavepackets: group MB = 2 428k, wave MB = 4 476k
+  const char* rwe = getenv("QD_SPO_ROWWAVE");
+  const int rowwave = rwe ? atoi(rwe) : (mbe ? 0 : 4);
   auto row = [&](int flags, c128* sp) {
     if (ns == 1)
       hipLaunchKernelGGL((spo2_row_q16_kernel<1, false>), dim3(nx, B), dim3(64), 0, st, psi, U, twy, flags, sp,
                          (const c128*)nullptr, grid_elems, sstride);
+    else if (rowwave == 4)
+      hipLaunchKernelGGL(spo2_row_wave_kernel<4>, dim3(nx, (B + 3) / 4), dim3(256), 0, st, psi, U, twy, flags, sp, B,
+                         grid_elems, sstride);
+    else if (rowwave == 8)
+      hipLaunchKernelGGL(spo2_row_wave_kernel<8>, dim3(nx, (B + 7) / 8), dim3(512), 0, st, psi, U, twy, flags, sp, B,
+                         grid_elems, sstride);
+    else if (rowwave == 2)
+      hipLaunchKernelGGL(spo2_row_wave_kernel<2>, dim3(nx, (B + 1) / 2), dim3(128), 0, st, psi, U, twy, flags, sp, B,
+                         grid_elems, sstride);
     else if (rowmb == 4)
       hipLaunchKernelGGL(spo2_row_q16_batch_kernel<4>, dim3(nx, (B + 3) / 4), dim3(512), 0, st, psi, U, twy, flags,
                          sp, B, grid_elems, sstride);
@@ -1032,15 +1185,19 @@ extern "C" int qd_spo2_run_batch(qd_c128* psi_, int B, const qd_c128* expVh_, co
       hipLaunchKernelGGL((spo2_row_q16_kernel<2, false>), dim3(nx, B), dim3(128), 0, st, psi, U, twy, flags, sp,
                          (const c128*)nullptr, grid_elems, sstride);
   };
-  static const bool tile_col = [] {  // QD_SPO_COLTILE=0: the per-column pass (A/B)
-    const char* e = getenv("QD_SPO_COLTILE");
-    return !(e && e[0] == '0');
-  }();
+  const char* cte = getenv("QD_SPO_COLTILE");   // 0: the per-column pass, 4 / 8 / 16: column tiles
+  const int coltile = cte ? atoi(cte) : 8;   // 64 wavepackets: 4 -> 477k, 8 -> 503k wavepacket-steps/s
   auto col = [&]() {
     if (ns == 1)
       hipLaunchKernelGGL(spo2_col_q16_kernel<1>, dim3(ny, 1, B), dim3(64), 0, st, psi, (const c128*)expKT,
                          (const c128*)twx, ny, ny, grid_elems);
-    else if (tile_col)
+    else if (coltile == 8)
+      hipLaunchKernelGGL(spo2_col_tile8_kernel<8>, dim3(ny / 8, B), dim3(512), 0, st, psi, (const c128*)expKT,
+                         (const c128*)twx, grid_elems);
+    else if (coltile == 16)
+      hipLaunchKernelGGL(spo2_col_tile8_kernel<16>, dim3(ny / 16, B), dim3(1024), 0, st, psi, (const c128*)expKT,
+                         (const c128*)twx, grid_elems);
+    else if (coltile != 0)
       hipLaunchKernelGGL(spo2_col_tile_kernel, dim3(ny / 4, B), dim3(512), 0, st, psi, (const c128*)expKT,
                          (const c128*)twx, grid_elems);
     else

@@ -244,13 +244,21 @@ def test_device_point_propagators_match_eigh(ns, cplx):
 
 
 @pytest.mark.parametrize("n,ns,B,rowmb", [(256, 2, 5, None), (256, 2, 6, "4"), (256, 2, 3, "1"), (256, 1, 3, None),
-                                          (64, 2, 2, None)])
+                                          (64, 2, 2, None), (256, 2, 6, "wave4"), (256, 2, 5, "wave8"),
+                                          (256, 2, 3, "wave2"), (256, 2, 3, "col8"), (256, 2, 2, "col4"),
+                                          (256, 2, 3, "col16")])
 def test_spo2_run_batch_vs_single_and_oracle(n, ns, B, rowmb, monkeypatch):
     """SPO2.run_batch (qd_spo2_run_batch: one launch per pass for B wavepackets; 256x256 register-FFT kernels
     with a batch grid axis, member by member for other shapes): every member equals run() of that member
     and the oracle's Strang steps, snapshots included.  ns = 2 row passes run MB members per workgroup sharing the
-    staged point operators (QD_SPO_ROWMB: default 2, 4, or 1 = one member per workgroup); ragged last groups."""
-    if rowmb is not None:
+    staged point operators (QD_SPO_ROWMB: default 2, 4, or 1 = one member per workgroup; QD_SPO_ROWWAVE: one wave
+    per member holding both states, 2 / 4 / 8 members per workgroup, default 4); column pass over 4- or 8-column
+    tiles (QD_SPO_COLTILE 4 / 8 / 16, default 8); ragged last groups."""
+    if rowmb is not None and rowmb.startswith("col"):
+        monkeypatch.setenv("QD_SPO_COLTILE", rowmb[3:])
+    elif rowmb is not None and rowmb.startswith("wave"):
+        monkeypatch.setenv("QD_SPO_ROWWAVE", rowmb[4:])
+    elif rowmb is not None:
         monkeypatch.setenv("QD_SPO_ROWMB", rowmb)
     from oracle import spo as ospo
     from pyqed_amd.wpd import SPO2
