@@ -946,6 +946,222 @@ __global__ __launch_bounds__(64 * NC) void spo2_col_tile8_kernel(c128* psi, cons
   }
 }
 
+// ---------------------------------------------------------------- 64-point transforms on 16 lanes
+// L = 64 = 4 x 16 (n = 4 m + q, k = k1 + 16 k2):
+//   X[k1 + 16 k2] = sum_q w4^(q k2) [w64^(q k1) X_q[k1]],  X_q = 16-point DFT of x[4 m + q]
+// A group of 16 lanes (lane l = 4 qq + s of the group) transforms one line held in LDS (any stride):
+// quad qq runs the 16-point DFT of x[4 m + qq] (dft16_quad: lane s loads x[16 a + 4 s + qq]), scales output
+// k1 = s + 4 d by w64^(qq k1), the 64 values are exchanged through the line's own storage (slot 4 k1 + q),
+// and lane l finishes X[l + 16 k2] (k2 = 0..3) with one register DFT4.  Returns the result in v (natural order
+// X[l + 16 k2] in v[k2]); the line's storage holds exchange values afterwards.  Twiddles t = q64_twiddles of the
+// 64-entry table w64^k (they depend on the lane only).  INV: conjugated twiddles, no scaling.
+__device__ __forceinline__ Q16Tw q64_twiddles(const c128* tw, int qq, int s) {
+  Q16Tw t;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    t.a[q] = tw[16 * ((q * s) & 3)];
+    t.b[q] = tw[4 * ((s * ((s - q) & 3)) & 15)];
+    t.d[q] = tw[(qq * (s + 4 * q)) & 63];
+  }
+  return t;
+}
+
+// The transform from registers already in the input layout (v[a] = x[16 a + 4 s + qq]); `line` is exchange space.
+template <bool INV>
+__device__ __forceinline__ void fft64_regs(c128* line, int stride, const Q16Tw& t, int qq, int s, c128 (&v)[4]) {
+  dft16_quad<INV>(v, t);
+#pragma unroll
+  for (int d = 0; d < 4; ++d) v[d] = twmul(v[d], t.d[d], INV);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int d = 0; d < 4; ++d) line[(4 * (s + 4 * d) + qq) * stride] = v[d];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int l = 4 * qq + s;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = line[(4 * l + q) * stride];
+  dft4<INV>(v);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool INV>
+__device__ __forceinline__ void fft64_group(c128* line, int stride, const Q16Tw& t, int qq, int s, c128 (&v)[4]) {
+#pragma unroll
+  for (int a = 0; a < 4; ++a) v[a] = line[(16 * a + 4 * s + qq) * stride];
+  fft64_regs<INV>(line, stride, t, qq, s, v);
+}
+
+// Middle-axis pass at L = 64 with the register transform (same tiles and loads as spo_mid_fast_kernel<64, C>):
+// the C columns (C x 16 B per row) are staged in LDS, each 16-lane group transforms one column line in place
+// (fft64_group, wave barriers only), and the tile is stored back.
+template <int C, bool INV>
+__global__ __launch_bounds__(16 * C) void spo_mid64_kernel(c128* psi, const c128* tw_g, int inner) {
+  constexpr int BD = 16 * C, LS = 65;  // line stride (padded)
+  __shared__ c128 A[C * LS];
+  __shared__ c128 tw[64];
+  const int chunks = inner / C;
+  const int i = blockIdx.x / chunks, c0 = (blockIdx.x % chunks) * C;
+  c128* base = psi + (size_t)i * 64 * inner + c0;
+  const int tid = threadIdx.x, g = tid >> 4, lane16 = tid & 15, qq = lane16 >> 2, s = lane16 & 3;
+  c128 v[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int e = tid + BD * n;
+    v[n] = base[(size_t)(e / C) * inner + e % C];
+  }
+  if (tid < 64) tw[tid] = tw_g[tid];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int e = tid + BD * n;
+    A[(e % C) * LS + e / C] = v[n];
+  }
+  __syncthreads();
+  const Q16Tw t = q64_twiddles(tw, qq, s);
+  c128* line = A + g * LS;
+  fft64_group<INV>(line, 1, t, qq, s, v);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) line[lane16 + 16 * k] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int e = tid + BD * n;
+    base[(size_t)(e / C) * inner + e % C] = A[(e % C) * LS + e / C];
+  }
+}
+
+// Column (x) pass at L = nx = 64 with the register transform (same tiles and loads as spo2_col_fast_kernel<64, C,
+// NS>): W = C NS lines (column-major over states) staged in LDS, each 16-lane group runs FFT_x -> * exp_K /
+// (nx ny nz) -> IFFT_x on one line in registers (natural order between the transforms).
+template <int C, int NS>
+__global__ __launch_bounds__(16 * C * NS) void spo_col64_kernel(c128* psi, const c128* expKT, const c128* tw_g,
+                                                                int ny) {
+  constexpr int W = C * NS, BD = 16 * W, LS = 65;
+  __shared__ c128 A[W * LS];
+  __shared__ c128 tw[64];
+  const int j0 = blockIdx.x * C;
+  const int tid = threadIdx.x, g = tid >> 4, lane16 = tid & 15, qq = lane16 >> 2, s = lane16 & 3;
+  c128 v[4], kf[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int e = tid + BD * n;   // row i = e / W, line w = e % W (coalesced W x 16 B per row)
+    v[n] = psi[((size_t)(e / W) * ny + j0) * NS + e % W];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) kf[k] = expKT[(size_t)(j0 + g / NS) * 64 + lane16 + 16 * k];
+  if (tid < 64) tw[tid] = tw_g[tid];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int e = tid + BD * n;
+    A[(e % W) * LS + e / W] = v[n];
+  }
+  __syncthreads();
+  const Q16Tw t = q64_twiddles(tw, qq, s);
+  c128* line = A + g * LS;
+  fft64_group<false>(line, 1, t, qq, s, v);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) line[lane16 + 16 * k] = cmul(v[k], kf[k]);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  fft64_group<true>(line, 1, t, qq, s, v);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) line[lane16 + 16 * k] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int e = tid + BD * n;
+    psi[((size_t)(e / W) * ny + j0) * NS + e % W] = A[(e % W) * LS + e / W];
+  }
+}
+
+// Row pass along a 64-point contiguous axis (SPO3's z lines, psi [rows][64][NS]) with the register transform:
+// one 16-lane group per row holding every state of its points, so the point operators are lane-local; 16 rows
+// per 256-thread workgroup, each with NS x 64 entries of LDS exchange space.  The row's values come straight
+// from global memory in the transform's input layout (lane l = 4 qq + s: points 16 a + 4 s + qq, NS x 16 B
+// contiguous per point) and leave in natural order (points l + 16 k).  Same flags as spo2_row_kernel:
+// [IFFT] -> V/2 -> [snapshot] -> [V/2] -> [FFT].
+template <int NS>
+__global__ __launch_bounds__(256) void spo_row64_kernel(c128* psi, const c128* U, const c128* tw_g, int flags,
+                                                        c128* snap) {
+  __shared__ c128 E[16 * NS * 64];      // per row: [state][64]
+  __shared__ c128 tw[64];
+  const int tid = threadIdx.x, grp = tid >> 4, lane16 = tid & 15, qq = lane16 >> 2, s = lane16 & 3;
+  const size_t row = (size_t)blockIdx.x * 16 + grp;
+  c128* pr = psi + row * 64 * NS;
+  c128* ex = E + grp * NS * 64;
+  c128 x[NS][4];
+  const bool inv = flags & ROW_INV;
+  // input layout: points 16 a + 4 s + qq (transform input) when the pass starts with the IFFT, else natural
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int p = inv ? 16 * a + 4 * s + qq : lane16 + 16 * a;
+#pragma unroll
+    for (int c = 0; c < NS; ++c) x[c][a] = pr[p * NS + c];
+  }
+  if (tid < 64) tw[tid] = tw_g[tid];
+  __syncthreads();
+  const Q16Tw t = q64_twiddles(tw, qq, s);
+  if (inv) {
+#pragma unroll
+    for (int c = 0; c < NS; ++c) fft64_regs<true>(ex + c * 64, 1, t, qq, s, x[c]);
+  }
+  // from here the lane holds the points lane16 + 16 k
+  if (flags & (ROW_VH1 | ROW_VH2 | ROW_SNAP)) {
+    c128 u[4][NS * NS];
+    if (flags & (ROW_VH1 | ROW_VH2)) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int e = 0; e < NS * NS; ++e) u[k][e] = U[((row * 64) + lane16 + 16 * k) * NS * NS + e];
+    }
+    auto point_op = [&]() {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        c128 q[NS];
+#pragma unroll
+        for (int a = 0; a < NS; ++a) {
+          c128 acc = cmk(0, 0);
+#pragma unroll
+          for (int b = 0; b < NS; ++b) acc = cadd(acc, cmul(u[k][a * NS + b], x[b][k]));
+          q[a] = acc;
+        }
+#pragma unroll
+        for (int a = 0; a < NS; ++a) x[a][k] = q[a];
+      }
+    };
+    if (flags & ROW_VH1) point_op();
+    if (flags & ROW_SNAP) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int c = 0; c < NS; ++c) snap[(row * 64 + lane16 + 16 * k) * NS + c] = x[c][k];
+    }
+    if (flags & ROW_VH2) point_op();
+  }
+  if (flags & ROW_FWD) {
+    // natural -> transform input layout through the row's exchange space, then the forward transform
+#pragma unroll
+    for (int c = 0; c < NS; ++c) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ex[c * 64 + lane16 + 16 * k] = x[c][k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int c = 0; c < NS; ++c) fft64_group<false>(ex + c * 64, 1, t, qq, s, x[c]);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int c = 0; c < NS; ++c) pr[(lane16 + 16 * k) * NS + c] = x[c][k];
+}
+
 bool q16_enabled() {
   static const int on = [] {
     const char* e = getenv("QD_SPO_Q16");
@@ -984,6 +1200,14 @@ int row_fast(int L, int ns, int rows, int flags, c128* psi, const c128* U, const
     if (ns == 1) { if (ky) RQ16(1, true); else RQ16(1, false); }
     else { if (ky) RQ16(2, true); else RQ16(2, false); }
 #undef RQ16
+    QD_HIP(hipGetLastError());
+    return QD_OK;
+  }
+  // L = 64: register transform, 16 lanes per row (QD_SPO_ROW64=0: the LDS Stockham kernel; A/B, tests)
+  const char* r64e = getenv("QD_SPO_ROW64");
+  if (L == 64 && rows % 16 == 0 && !(flags & ROW_KY) && !(r64e && r64e[0] == '0')) {
+    if (ns == 1) hipLaunchKernelGGL(spo_row64_kernel<1>, dim3(rows / 16), dim3(256), 0, st, psi, U, tw, flags, snap);
+    else hipLaunchKernelGGL(spo_row64_kernel<2>, dim3(rows / 16), dim3(256), 0, st, psi, U, tw, flags, snap);
     QD_HIP(hipGetLastError());
     return QD_OK;
   }
@@ -1314,7 +1538,19 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
   // QD_SPO3_FAST=0: the generic LDS-staged mid / x kernels instead of the latency-shaped ones (A/B runs)
   const char* f3e = getenv("QD_SPO3_FAST");
   const bool fast3 = !(f3e && f3e[0] == '0');
+  // QD_SPO_ROW64=0: the LDS Stockham kernels at L = 64 instead of the 64-point register transforms (A/B, tests)
+  const char* r64e = getenv("QD_SPO_ROW64");
+  const bool r64 = !(r64e && r64e[0] == '0');
   auto col = [&]() -> int {
+    if (colC && fast && fast3 && r64 && nx == 64) {
+#define COL64(CC)                                                                                                    \
+  if (ns == 1) hipLaunchKernelGGL((spo_col64_kernel<CC, 1>), dim3(nyz / CC), dim3(16 * CC), 0, st, psi, expKT, twx, nyz); \
+  else hipLaunchKernelGGL((spo_col64_kernel<CC, 2>), dim3(nyz / CC), dim3(32 * CC), 0, st, psi, expKT, twx, nyz)
+      if (colC == 2) { COL64(2); } else if (colC == 4) { COL64(4); } else { COL64(8); }
+#undef COL64
+      QD_HIP(hipGetLastError());
+      return QD_OK;
+    }
     if (colC && fast && fast3) {
       const int threads = std::max(64, colC * ns * (nx / 4));
       const size_t lds = (size_t)(nx + 2 * colC * ns * nx) * sizeof(c128);
@@ -1352,6 +1588,15 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
   auto mid = [&](bool inv) -> int {
     const int grid = nx * (inner / midC);
     const int threads = std::max(64, midC * (ny / 4));
+    if (fast3 && r64 && ny == 64) {
+#define MID64(C)                                                                                                  \
+  if (inv) hipLaunchKernelGGL((spo_mid64_kernel<C, true>), dim3(grid), dim3(16 * C), 0, st, psi, twy, inner); \
+  else hipLaunchKernelGGL((spo_mid64_kernel<C, false>), dim3(grid), dim3(16 * C), 0, st, psi, twy, inner)
+      if (midC == 16) { MID64(16); } else if (midC == 8) { MID64(8); } else { MID64(4); }
+#undef MID64
+      QD_HIP(hipGetLastError());
+      return QD_OK;
+    }
     if (fast3 && midC * ny / 4 <= 256 && ny <= 64) {
 #define MIDF_C(L, C)                                                                                               \
   if (inv) hipLaunchKernelGGL((spo_mid_fast_kernel<L, C, true>), dim3(grid), dim3(threads), 0, st, psi, twy, inner); \

@@ -124,13 +124,18 @@ def test_spo3_matches_reference():
     assert relerr(r.psi, g["psi"]) < TOL
 
 
-@pytest.mark.parametrize("mid_c,col_c,fast", [(None, None, None), ("4", "2", None), ("8", "4", None),
-                                               ("16", "8", None), ("8", None, None), (None, "0", None),
-                                               (None, None, "0"), ("16", "8", "0")])
-def test_spo3_example_size_vs_oracle(mid_c, col_c, fast, monkeypatch):
+@pytest.mark.parametrize("mid_c,col_c,fast,r64", [(None, None, None, None), ("4", "2", None, None),
+                                                   ("8", "4", None, None), ("16", "8", None, None),
+                                                   ("8", None, None, None), (None, "0", None, None),
+                                                   (None, None, "0", None), ("16", "8", "0", None),
+                                                   (None, None, None, "0"), ("16", "8", "0", "0")])
+def test_spo3_example_size_vs_oracle(mid_c, col_c, fast, r64, monkeypatch):
     """examples/spo.py size: 64^3 x 2, vs the NumPy fftn restatement, and norm conservation; every
     mid-axis and x-axis block width (QD_SPO3_MID_C / QD_SPO3_COL_C; None = the default launch), on the
-    latency-shaped mid / x kernels (default) and the generic LDS-staged ones (QD_SPO3_FAST=0)."""
+    latency-shaped mid / x kernels (default) and the generic LDS-staged ones (QD_SPO3_FAST=0), with the z pass on
+    the 64-point register transform (default) or the LDS Stockham kernel (QD_SPO_ROW64=0)."""
+    if r64 is not None:
+        monkeypatch.setenv("QD_SPO_ROW64", r64)
     if fast is not None:
         monkeypatch.setenv("QD_SPO3_FAST", fast)
     if mid_c is not None:
@@ -147,6 +152,31 @@ def test_spo3_example_size_vs_oracle(mid_c, col_c, fast, monkeypatch):
     ref, psi = ospo.spo3_run(sol.exp_V_half, sol.exp_K, psi0, 4, 2)
     assert relerr(np.array(r.psilist), np.array(ref)) < TOL
     assert abs(np.vdot(r.psi, r.psi).real / np.vdot(psi0, psi0).real - 1) < 1e-12
+
+
+@pytest.mark.parametrize("nx,nout", [(64, 1), (32, 3)])
+def test_spo3_row64_single_state_and_shapes(nx, nout):
+    """The 64-point register z pass with one electronic state and nx != 64: vs the NumPy fftn restatement,
+    snapshots every nout steps, and equal to the LDS Stockham z pass (QD_SPO_ROW64=0)."""
+    import os
+    from oracle import spo as ospo
+    from pyqed_amd.wpd import SPO3
+    x = np.linspace(-6, 6, nx)
+    yz = np.linspace(-6, 6, 64)
+    X, Y, Z = np.meshgrid(x, yz, yz, indexing="ij")
+    rng = np.random.default_rng(nx)
+    psi0 = (np.exp(-((X + 1) ** 2 + Y ** 2 + Z ** 2) / 2 + 1j * rng.uniform(-1, 1) * Z) / np.pi ** 0.75)[..., None]
+    sol = SPO3(x, yz, yz, masses=[1.0, 1.0, 1.0], nstates=1)
+    sol.set_DPES([0.5 * (X ** 2 + Y ** 2 + Z ** 2) + 0.05 * X * Y * Z], [])
+    r = sol.run(psi0=psi0, dt=0.1, nt=6, nout=nout)
+    ref, _ = ospo.spo3_run(sol.exp_V_half, sol.exp_K, psi0, 6, nout)
+    assert relerr(np.array(r.psilist), np.array(ref)) < TOL
+    os.environ["QD_SPO_ROW64"] = "0"
+    try:
+        r0 = sol.run(psi0=psi0, dt=0.1, nt=6, nout=nout)
+    finally:
+        del os.environ["QD_SPO_ROW64"]
+    assert relerr(np.array(r.psilist), np.array(r0.psilist)) < 1e-13
 
 
 @pytest.mark.parametrize("return_states", [True, False])
