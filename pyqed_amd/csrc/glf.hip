@@ -232,7 +232,15 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
             else Xd[(size_t)row * Np + col] = v;
           });
           __syncthreads();
-          for (int rd = 0; rd < 2; ++rd) {
+          // Every stage quantity is exactly Hermitian (k_ji = conj(k_ij) bit for bit, and the RK4 updates are
+          // elementwise with real coefficients), so each (i, j), i <= j, is computed once and its mirror written
+          // as the conjugate: rho and acc are read on the upper triangle only, acc is kept there only (the
+          // epilogue is its only reader), rn and rho are written in full (the GEMMs, observables and the caller
+          // read them).  Round 0: the off-diagonal tile (0, 1) (TS^2 pairs); round 1: the upper triangles of the
+          // diagonal tiles, TS (TS + 1) / 2 each, folded (rows u and TS - 1 - u of a tile share one run of
+          // TS + 1 elements).  Half the elements, loads and dependent round trips of the full-matrix epilogue.
+          auto round = [&](auto rdc) {
+            constexpr int rd = decltype(rdc)::value;
             if (rd == 1) {  // diagonal tiles: global -> LDS
               __syncthreads();
               for (int q = 0; q < PER; ++q) {
@@ -242,41 +250,72 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
               }
               __syncthreads();
             }
-            // global loads of a chunk are issued together; k (from LDS) is formed only at its use, so
-            // a chunk holds 2 c128 + 1 index per element while its loads are in flight
-            for (int q0 = 0; q0 < PER; q0 += CH) {
-              int idx[CH];
+            constexpr int TRI = TS * (TS + 1) / 2;
+            constexpr int NE = rd == 0 ? TS * TS : 2 * TRI;
+            constexpr int NPER = (NE + CG_WG - 1) / CG_WG;
+            // element e of this round -> global (gi, gj), gi <= gj
+            auto place = [&](int e, int& gi, int& gj) {
+              if (rd == 0) {
+                gi = e / TS;
+                gj = TS + e % TS;
+              } else {
+                const int ts = e / TRI, f = e % TRI, u = f / (TS + 1), v = f % (TS + 1);
+                const bool lo = v < TS - u;
+                const int ra = lo ? u : TS - 1 - u;
+                gi = ts * TS + ra;
+                gj = ts * TS + (lo ? u + v : ra + v - (TS - u));
+              }
+            };
+            for (int q0 = 0; q0 < NPER; q0 += CH) {
               c128 r0[CH], a0[CH];
 #pragma unroll
               for (int q = 0; q < CH; ++q) {
                 const int e = tid + CG_WG * (q0 + q);
-                const int ts = e / (TS * TS), rem = e % (TS * TS), ra = rem / TS, cc = rem % TS;
-                const int gc = (rd == 0 ? 1 - ts : ts) * TS + cc;  // off-diagonal: column block 1 - ts
-                idx[q] = (ts * TS + ra) * Np + gc;
-                r0[q] = rho[idx[q]];
-                a0[q] = stage == 0 ? cmk(0, 0) : acc[idx[q]];
+                if (q0 + q < NPER && (NE % CG_WG == 0 || e < NE)) {
+                  int gi, gj;
+                  place(e, gi, gj);
+                  r0[q] = rho[gi * Np + gj];
+                  a0[q] = stage == 0 ? cmk(0, 0) : acc[gi * Np + gj];
+                }
               }
 #pragma unroll
               for (int q = 0; q < CH; ++q) {
                 const int e = tid + CG_WG * (q0 + q);
-                const int ts = e / (TS * TS), rem = e % (TS * TS), ra = rem / TS, cc = rem % TS;
-                const c128* own = ts == 0 ? T0 : T1;
-                const c128* mir = rd == 0 ? (ts == 0 ? T1 : T0) : own;
+                if (q0 + q >= NPER || (NE % CG_WG != 0 && e >= NE)) continue;
+                int gi, gj;
+                place(e, gi, gj);
+                // k_ij = X_ij + conj(X_ji): round 0 X_ij in T0 (tile (0,1)), X_ji in T1 (tile (1,0)); round 1
+                // both in the diagonal tile's own buffer
+                const int ra = gi % TS, cc = gj % TS;
+                const c128* own = (rd == 1 && gi >= TS) ? T1 : T0;
+                const c128* mir = rd == 0 ? T1 : own;
                 const c128 k = cadd(own[ra * LD + cc], cconj(mir[cc * LD + ra]));
+                const int id = gi * Np + gj, mid = gj * Np + gi;   // (i, j) and its mirror (j, i)
+                const bool off = gi != gj;
                 if (stage == 0) {
-                  acc[idx[q]] = k;
-                  rn[idx[q]] = cadd(r0[q], cscale(k, dt2));
+                  acc[id] = k;
+                  const c128 v = cadd(r0[q], cscale(k, dt2));
+                  rn[id] = v;
+                  if (off) rn[mid] = cconj(v);
                 } else if (stage < 3) {
-                  acc[idx[q]] = cadd(a0[q], cscale(k, 2.0));
-                  rn[idx[q]] = cadd(r0[q], cscale(k, stage == 1 ? dt2 : dt));
+                  acc[id] = cadd(a0[q], cscale(k, 2.0));
+                  const c128 v = cadd(r0[q], cscale(k, stage == 1 ? dt2 : dt));
+                  rn[id] = v;
+                  if (off) rn[mid] = cconj(v);
                 } else {
                   const c128 r1 = cadd(r0[q], cscale(cscale(cadd(a0[q], k), 1.0 / 6.0), dt));
-                  rho[idx[q]] = r1;
-                  rn[idx[q]] = r1;
+                  rho[id] = r1;
+                  rn[id] = r1;
+                  if (off) {
+                    rho[mid] = cconj(r1);
+                    rn[mid] = cconj(r1);
+                  }
                 }
               }
             }
-          }
+          };
+          round(std::integral_constant<int, 0>{});
+          round(std::integral_constant<int, 1>{});
           __syncthreads();
         }
         QD_TMARK(3);
