@@ -207,64 +207,63 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
         __syncthreads();
         cg_block_gemm<BT>(segs, 1 + nc, Np, Np, Np, L, A);
         QD_TMARK(2);
-        // k = X + X^+ through LDS, two rounds of two TS x TS tiles (TS = BT/2; the GEMM staging buffers
-        // are free).  The accumulator fragments of the off-diagonal pair X(0,1), X(1,0) go to LDS and those
-        // of the diagonal tiles to Y_0's slot (Y is dead once the GEMM has returned), so no accumulator stays
-        // live past one epilogue.  Round 0 finalises the off-diagonal pair from LDS; round 1 reloads the
-        // diagonal tiles (coalesced rows) into LDS and finalises them.  Each element reads its own value
-        // and its mirror from LDS; the loads of a chunk of elements are issued together.
+        // k = X + X^+ formed in LDS on the upper triangle only (TS = BT/2; the GEMM staging buffers are free).
+        // Every stage quantity is exactly Hermitian (k_ji = conj(k_ij) bit for bit, and the RK4 updates are
+        // elementwise with real coefficients), so each (i, j), i <= j, is computed once and its mirror written as
+        // the conjugate.  Pass A stores the accumulator's upper elements: tile (0, 1) into T01 [TS][TS + 1] and the
+        // diagonal tiles' upper triangles into Tt (packed, folded: rows u and TS - 1 - u of a tile share one run of
+        // TS + 1 slots); pass B adds the conjugate of every lower element at its mirror slot.  The accumulator
+        // stays in registers through both passes (no global round trip of the diagonal tiles).  The RK4 update then
+        // reads rho and acc on the upper triangle only, keeps acc there only (the epilogue is its only reader) and
+        // writes rn and rho in full (the GEMMs, observables and the caller read them).
         {
-          constexpr int TS = BT / 2, LD = TS + 1;
-          static_assert(2 * TS * LD * sizeof(c128) <= sizeof(CgLds<BT>), "LDS transpose buffer");
-          constexpr int PER = BT * BT / 2 / CG_WG;  // elements per thread per round
+          constexpr int TS = BT / 2, LD = TS + 1, TRI = TS * (TS + 1) / 2;
+          static_assert((TS * LD + 2 * TRI) * sizeof(c128) <= sizeof(CgLds<BT>), "LDS k buffers");
           #ifndef QD_EPI_CH
 #define QD_EPI_CH 4
 #endif
-          constexpr int CH = PER < QD_EPI_CH ? PER : QD_EPI_CH;
-          c128* T0 = reinterpret_cast<c128*>(&L);
-          c128* T1 = T0 + TS * LD;
-          c128* Xd = Y;
+          c128* T01 = reinterpret_cast<c128*>(&L);
+          c128* Tt = T01 + TS * LD;
           int tid = threadIdx.x;
           asm volatile("" : "+v"(tid));  // keep the per-element index math inside the stage loop (no LICM + spill)
+          // folded packed slot of (ra, cc), ra <= cc, within a diagonal tile
+          auto slot = [&](int ra, int cc) {
+            const bool top = ra < TS / 2;
+            const int u = top ? ra : TS - 1 - ra;
+            return u * (TS + 1) + (top ? 0 : TS - u) + (cc - ra);
+          };
           cg_epilogue<BT>(A, [&](int row, int col, c128 v) {
-            const int ti = row / TS, tj = col / TS;
-            if (ti != tj) (ti == 0 ? T0 : T1)[(row - ti * TS) * LD + (col - tj * TS)] = v;
-            else Xd[(size_t)row * Np + col] = v;
+            const int ti = row / TS, tj = col / TS, ra = row - ti * TS, cc = col - tj * TS;
+            if (ti < tj) T01[ra * LD + cc] = v;
+            else if (ti == tj && ra < cc) Tt[ti * TRI + slot(ra, cc)] = v;
+            else if (ti == tj && ra == cc) Tt[ti * TRI + slot(ra, cc)] = cadd(v, cconj(v));
           });
           __syncthreads();
-          // Every stage quantity is exactly Hermitian (k_ji = conj(k_ij) bit for bit, and the RK4 updates are
-          // elementwise with real coefficients), so each (i, j), i <= j, is computed once and its mirror written
-          // as the conjugate: rho and acc are read on the upper triangle only, acc is kept there only (the
-          // epilogue is its only reader), rn and rho are written in full (the GEMMs, observables and the caller
-          // read them).  Round 0: the off-diagonal tile (0, 1) (TS^2 pairs); round 1: the upper triangles of the
-          // diagonal tiles, TS (TS + 1) / 2 each, folded (rows u and TS - 1 - u of a tile share one run of
-          // TS + 1 elements).  Half the elements, loads and dependent round trips of the full-matrix epilogue.
+          cg_epilogue<BT>(A, [&](int row, int col, c128 v) {
+            const int ti = row / TS, tj = col / TS, ra = row - ti * TS, cc = col - tj * TS;
+            c128* t = ti > tj ? &T01[cc * LD + ra] : (ti == tj && ra > cc) ? &Tt[ti * TRI + slot(cc, ra)] : nullptr;
+            if (t) *t = cadd(*t, cconj(v));
+          });
+          __syncthreads();
+          // round 0: tile (0, 1), element e -> (e / TS, TS + e % TS), k at T01; round 1: the two folded diagonal
+          // triangles, element e -> k at Tt[e]
           auto round = [&](auto rdc) {
             constexpr int rd = decltype(rdc)::value;
-            if (rd == 1) {  // diagonal tiles: global -> LDS
-              __syncthreads();
-              for (int q = 0; q < PER; ++q) {
-                const int e = tid + CG_WG * q;
-                const int ts = e / (TS * TS), rem = e % (TS * TS), ra = rem / TS, cc = rem % TS;
-                (ts == 0 ? T0 : T1)[ra * LD + cc] = Xd[(size_t)(ts * TS + ra) * Np + ts * TS + cc];
-              }
-              __syncthreads();
-            }
-            constexpr int TRI = TS * (TS + 1) / 2;
             constexpr int NE = rd == 0 ? TS * TS : 2 * TRI;
             constexpr int NPER = (NE + CG_WG - 1) / CG_WG;
-            // element e of this round -> global (gi, gj), gi <= gj
-            auto place = [&](int e, int& gi, int& gj) {
+            constexpr int CH = NPER < QD_EPI_CH ? NPER : QD_EPI_CH;
+            auto place = [&](int e, int& gi, int& gj) -> const c128* {
               if (rd == 0) {
                 gi = e / TS;
                 gj = TS + e % TS;
-              } else {
-                const int ts = e / TRI, f = e % TRI, u = f / (TS + 1), v = f % (TS + 1);
-                const bool lo = v < TS - u;
-                const int ra = lo ? u : TS - 1 - u;
-                gi = ts * TS + ra;
-                gj = ts * TS + (lo ? u + v : ra + v - (TS - u));
+                return &T01[gi * LD + e % TS];
               }
+              const int ts = e / TRI, ff = e % TRI, u = ff / (TS + 1), v = ff % (TS + 1);
+              const bool lo = v < TS - u;
+              const int ra = lo ? u : TS - 1 - u;
+              gi = ts * TS + ra;
+              gj = ts * TS + (lo ? u + v : ra + v - (TS - u));
+              return &Tt[e];
             };
             for (int q0 = 0; q0 < NPER; q0 += CH) {
               c128 r0[CH], a0[CH];
@@ -283,13 +282,7 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
                 const int e = tid + CG_WG * (q0 + q);
                 if (q0 + q >= NPER || (NE % CG_WG != 0 && e >= NE)) continue;
                 int gi, gj;
-                place(e, gi, gj);
-                // k_ij = X_ij + conj(X_ji): round 0 X_ij in T0 (tile (0,1)), X_ji in T1 (tile (1,0)); round 1
-                // both in the diagonal tile's own buffer
-                const int ra = gi % TS, cc = gj % TS;
-                const c128* own = (rd == 1 && gi >= TS) ? T1 : T0;
-                const c128* mir = rd == 0 ? T1 : own;
-                const c128 k = cadd(own[ra * LD + cc], cconj(mir[cc * LD + ra]));
+                const c128 k = *place(e, gi, gj);
                 const int id = gi * Np + gj, mid = gj * Np + gi;   // (i, j) and its mirror (j, i)
                 const bool off = gi != gj;
                 if (stage == 0) {
