@@ -549,7 +549,13 @@ def bench_spo2(dev, steps, n=256, dt=0.05):
                "roofline": {"bound": "hbm", "achieved": round(bbytes * bsteps / bev / 1e9, 1), "peak": HBM_PEAK_GBS,
                             "unit": "GB/s", "frac": round(bbytes * bsteps / bev / 1e9 / HBM_PEAK_GBS, 4),
                             "bytes_per_step": bbytes,
-                            "note": "same row / column kernels with a batch grid axis; working set 134 MiB"}}
+                            "traffic": (measured_traffic("spo2_row_wave_kernel<4>_64wp", Bw)
+                                        + measured_traffic("spo2_col_tile8_kernel<8>_64wp", Bw))
+                            if (n, Bw) == (256, 64) and measured_traffic("spo2_row_wave_kernel<4>_64wp", 1) else None,
+                            "traffic_unit": "HBM bytes per batched Strang step (row + column pass; PMC FETCH_SIZE+"
+                                            "WRITE_SIZE, calibrated; profiles/pmc_traffic.json)",
+                            "note": "wave-per-member row pass (lane-local 2x2 point operators) + 8-column tile "
+                                    "column pass; working set 134 MiB"}}
     return {
         "value": round(steps / wall, 1), "unit": "SPO steps/s",
         "batched": batched,
