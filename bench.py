@@ -70,6 +70,14 @@ def lindblad_flops_per_step(N: int, nc: int, hermitian: bool = False) -> float:
     return 4.0 * ((1 if hermitian else 2) + 2 * nc) * 8.0 * N ** 3
 
 
+def lindblad_executed_flops_per_step(N: int, nc: int, hermitian: bool = False) -> float:
+    # What the MFMA units execute: the Hermitian kernel at 128-blocks (N_p = 128) skips the Hermitian part's
+    # redundant lower-left 64 x 64 block (glf.hip / cgemm_block.hpp cg_herm_x_gemm: 1/4 of each (C r)C^+ GEMM).
+    if hermitian and N == 128:
+        return 4.0 * (1 + nc + 0.75 * nc) * 8.0 * N ** 3
+    return lindblad_flops_per_step(N, nc, hermitian)
+
+
 def cpu_baseline(N, nc, dt, budget_s=10.0):
     """Reference-faithful csr restatement (oracle.lindblad.lindblad_csr), bounded sample."""
     from oracle import lindblad as olb
@@ -970,6 +978,14 @@ def main():
                 if (N, nc) == (128, 1) else None,
                 "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE+WRITE_SIZE, calibrated; profiles/pmc_traffic.json)",
                 "flop_per_dm_step": lindblad_flops_per_step(N, nc, herm),
+                "flop_note": "flop_per_dm_step = the Hermitian GLF form, 4 x (1 + 2 n_c) x 8 N^3 (the round-1 "
+                             "accounting); the kernel executes executed_flop_per_dm_step of it (the redundant "
+                             "lower-left block of (C r)C^+ is skipped), executed_frac is that rate over the peak",
+                "executed_flop_per_dm_step": lindblad_executed_flops_per_step(N, nc, herm),
+                "executed_tflops": round(lindblad_executed_flops_per_step(N, nc, herm) * B * args.steps / kern_s / 1e12,
+                                         3),
+                "executed_frac": round(lindblad_executed_flops_per_step(N, nc, herm) * B * args.steps / kern_s / 1e12
+                                       / FP64_MFMA_PEAK_TFLOPS, 4),
                 "general_path_equiv_tflops": round(lindblad_flops_per_step(N, nc) * B * args.steps / kern_s / 1e12, 3),
                 "launch_ms": round(kern_s * 1e3, 3),
             },

@@ -296,13 +296,143 @@ struct CgSegB {
 // `segs` should live in LDS (or be uniform): it is indexed at run time, and a
 // private array indexed at run time would be placed in scratch memory.
 // Ends with a workgroup barrier, so LDS may be reused immediately after.
-template <int BT>
+template <int BT, bool PIPE = false>
 __device__ __forceinline__ void cg_block_gemm(const CgSeg* segs, int nseg, int K, int lda, int ldb, CgLds<BT>& L,
                                               CgAcc<BT>& acc) {
   const int tps = K / CG_KT;
   CgSegA<BT> pa{segs, tps, lda};
   CgSegB<BT> pb{segs, tps, ldb};
-  cg_block_gemm_gen<BT>(nseg * tps, pa, pb, L, acc);
+  cg_block_gemm_gen<BT, PIPE>(nseg * tps, pa, pb, L, acc);
+}
+
+// ---------------------------------------------------------------- Hermitian X GEMM (BT = 128)
+// X = A r + B W over two K segments (A r: segment 0; B W: segment 1, W = C^+ / 2), for k = X + X^+ of a
+// Hermitian right-hand side.  Only k on the upper blocks is used, and B W (= C r C^+ / 2) is itself Hermitian,
+// so segment 1 need not reach the lower-left 64 x 64 block (1, 0): there X = A r alone, and the upper-right
+// block (0, 1) takes the full C r C^+ instead of its half (A fragment doubled: 2 a x b / 2 is exact), so that
+// k_ij = X_ij + conj(X_ji) = (A r)_ij + conj((A r)_ji) + (C r C^+)_ij on the off-diagonal blocks and as before on
+// the diagonal ones.  The wave -> tile layout spreads block (1, 0) over every wave (each owns row tiles i and 4 + i
+// and column tiles {2h, 2h+1, 4+2h, 5+2h}, i = wave / 2, h = wave % 2), so skipping its tiles in segment 1 takes
+// 2 of 8 tiles from every wave alike: 1/4 of segment 1's MFMAs, 1/12 of a stage's.
+struct CgHermLayout {
+  static __device__ __forceinline__ int row0(int wave, int mi) { return mi * 64 + (wave >> 1) * 16; }
+  static __device__ __forceinline__ int col0(int wave, int nj) { return (nj >> 1) * 64 + (2 * (wave & 1) + (nj & 1)) * 16; }
+};
+
+template <typename Mid>
+__device__ __forceinline__ void cg_herm_compute_tile(const CgLds<128>& L, int buf, CgAcc<128>& acc, int wave, bool seg1,
+                                                     Mid mid) {
+  constexpr int BT = 128, MW = 2, NW = 4, NQ = CG_KT / 4;
+  const int lane = threadIdx.x & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    if (q == CG_STAGE_AT) {
+      cg_sched_fence();
+      mid();
+      cg_sched_fence();
+    }
+    const int kk = 4 * q;
+    c128 a[MW], b[NW];
+#pragma unroll
+    for (int mi = 0; mi < MW; ++mi) a[mi] = L.a[buf][(CgHermLayout::row0(wave, mi) + lr) * CG_SA + kk + lk];
+#pragma unroll
+    for (int nj = 0; nj < NW; ++nj) b[nj] = L.b[buf][(kk + lk) * BT + CgHermLayout::col0(wave, nj) + lr];
+    // block (0, 1) in the Hermitian segments: the doubled fragment (exact); a[0] itself elsewhere
+    const double s2 = seg1 ? 2.0 : 1.0;
+    const c128 a2 = cmk(a[0].re * s2, a[0].im * s2);
+#pragma unroll
+    for (int mi = 0; mi < MW; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < NW; ++nj) {
+        if (mi == 1 && nj < 2 && seg1) continue;   // block (1, 0): no Hermitian part
+        const c128& av = (mi == 0 && nj >= 2) ? a2 : a[mi];
+        acc.re[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.re, b[nj].re, acc.re[mi][nj], 0, 0, 0);
+        acc.im[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.re, b[nj].im, acc.im[mi][nj], 0, 0, 0);
+      }
+#pragma unroll
+    for (int mi = 0; mi < MW; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < NW; ++nj) {
+        if (mi == 1 && nj < 2 && seg1) continue;
+        const c128& av = (mi == 0 && nj >= 2) ? a2 : a[mi];
+        acc.re[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av.im, b[nj].im, acc.re[mi][nj], 0, 0, 0);
+        acc.im[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.im, b[nj].re, acc.im[mi][nj], 0, 0, 0);
+      }
+  }
+  if (CG_STAGE_AT >= NQ) {
+    cg_sched_fence();
+    mid();
+  }
+}
+
+// segs[0] = (A, r), segs[1..nseg-1] = (B_c, W_c); K = the common depth (tps = K / 16 K-tiles per segment).
+// hermitian_part: sum_c B_c W_c is Hermitian (segments >= 1 skip block (1, 0) and double block (0, 1)); otherwise
+// every tile takes every segment (the plain X GEMM on this layout).  All threads call it; ends with a workgroup
+// barrier.  Visit the result with cg_herm_epilogue.
+__device__ __forceinline__ void cg_herm_x_gemm(const CgSeg* segs, int nseg, int K, int lda, int ldb, CgLds<128>& L,
+                                               CgAcc<128>& acc, bool hermitian_part) {
+  constexpr int BT = 128, MW = 2, NW = 4;
+  const int wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int mi = 0; mi < MW; ++mi)
+#pragma unroll
+    for (int nj = 0; nj < NW; ++nj) {
+      acc.re[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
+      acc.im[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
+    }
+  const int tps = K / CG_KT, T = nseg * tps;
+  CgSegA<BT> pa{segs, tps, lda};
+  CgSegB<BT> pb{segs, tps, ldb};
+  constexpr int NLD = cg_nld<BT>();
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  cg_v2 ra[NLD], rb[NLD];
+  auto load = [&](int t) {
+#pragma unroll
+    for (int q = 0; q < NLD; ++q) {
+      const int e = tid + CG_WG * q;
+      ra[q] = pa.fetch(t, e, q);
+      rb[q] = pb.fetch(t, e, q);
+    }
+  };
+  auto store = [&](int t, int buf) {
+#pragma unroll
+    for (int q = 0; q < NLD; ++q) {
+      const int e = tid + CG_WG * q;
+      cg_st_lds(&L.a[buf][(e >> 4) * CG_SA + (e & 15)], ra[q]);
+      cg_st_lds(&L.b[buf][e], rb[q]);
+    }
+  };
+  load(0);
+  store(0, 0);
+  __syncthreads();
+  for (int t = 0; t < T; ++t) {
+    const bool more = (t + 1) < T;
+    if (more) load(t + 1);
+    auto mid = [&]() {
+      if (more) store(t + 1, (t + 1) & 1);
+    };
+    cg_herm_compute_tile(L, t & 1, acc, wave, hermitian_part && t >= tps, mid);
+    __syncthreads();
+  }
+}
+
+template <typename F>
+__device__ __forceinline__ void cg_herm_epilogue(const CgAcc<128>& acc, F&& f) {
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const int wave = tid >> 6, lane = tid & 63;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int nj = 0; nj < 4; ++nj) {
+        const int row = CgHermLayout::row0(wave, mi) + (lane >> 4) + 4 * r;
+        const int col = CgHermLayout::col0(wave, nj) + (lane & 15);
+        f(row, col, cmk(acc.re[mi][nj][r], acc.im[mi][nj][r]));
+      }
 }
 
 // Visit every accumulator element: f(row, col, value) with row/col inside the block.

@@ -50,6 +50,8 @@ struct LindbladParams {
   int N, Np, nc, ne, nsteps, save_every, nsave;
   int step0, total_steps;  // this launch runs global steps step0 .. step0+nsteps-1 of total_steps
   int herm;                // Hermitian fast path (Lindblad, rho exactly Hermitian, single block)
+  int hseg;                // Hermitian path: sum_c L_c r W_c is itself Hermitian (Lindblad C r C^+ / 2; not Redfield's
+                           // sum A r Lam^+), so its redundant lower-left block may be skipped (cg_herm_x_gemm)
   double dt;
   unsigned long long* tbuf;  // [B][8] per-phase wall-clock ticks (QD_PHASE_TIMING diagnostics) or null
   unsigned long long stagger;  // start offset (wall-clock ticks) of the odd workgroup group of each XCD
@@ -120,6 +122,13 @@ __device__ void wg_observables(const c128* rho, const c128* eT, int ne, size_t N
   }
 }
 
+#ifndef GLF_HERM_X
+#define GLF_HERM_X 1   // Hermitian kernel at BT = 128: X GEMM without the Hermitian part on block (1, 0) (A/B: 0)
+#endif
+#ifndef GLF_HERM_PIPE
+#define GLF_HERM_PIPE false   // fragment double-buffering in the Hermitian kernel's GEMMs (A/B builds)
+#endif
+
 template <int BT, bool HERM>
 __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
   __shared__ CgLds<BT> L;
@@ -187,7 +196,7 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
             segs[0].B = r;
           }
           __syncthreads();
-          cg_block_gemm<BT>(segs, 1, Np, Np, Np, L, A);
+          cg_block_gemm<BT, GLF_HERM_PIPE>(segs, 1, Np, Np, Np, L, A);
           QD_TMARK(0);
           c128* Yc = Y + (size_t)c * NN;
           cg_epilogue<BT>(A, [&](int row, int col, c128 v) { Yc[(size_t)row * Np + col] = v; });
@@ -205,7 +214,13 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
           }
         }
         __syncthreads();
-        cg_block_gemm<BT>(segs, 1 + nc, Np, Np, Np, L, A);
+        constexpr bool HX = BT == 128 && GLF_HERM_X;   // lower-left block without the Hermitian part (cgemm_block.hpp)
+        if constexpr (HX) cg_herm_x_gemm(segs, 1 + nc, Np, Np, Np, L, A, p.hseg != 0);
+        else cg_block_gemm<BT, GLF_HERM_PIPE>(segs, 1 + nc, Np, Np, Np, L, A);
+        auto visit = [&](auto&& f) {
+          if constexpr (HX) cg_herm_epilogue(A, f);
+          else cg_epilogue<BT>(A, f);
+        };
         QD_TMARK(2);
         // k = X + X^+ formed in LDS on the upper triangle only (TS = BT/2; the GEMM staging buffers are free).
         // Every stage quantity is exactly Hermitian (k_ji = conj(k_ij) bit for bit, and the RK4 updates are
@@ -232,14 +247,14 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
             const int u = top ? ra : TS - 1 - ra;
             return u * (TS + 1) + (top ? 0 : TS - u) + (cc - ra);
           };
-          cg_epilogue<BT>(A, [&](int row, int col, c128 v) {
+          visit([&](int row, int col, c128 v) {
             const int ti = row / TS, tj = col / TS, ra = row - ti * TS, cc = col - tj * TS;
             if (ti < tj) T01[ra * LD + cc] = v;
             else if (ti == tj && ra < cc) Tt[ti * TRI + slot(ra, cc)] = v;
             else if (ti == tj && ra == cc) Tt[ti * TRI + slot(ra, cc)] = cadd(v, cconj(v));
           });
           __syncthreads();
-          cg_epilogue<BT>(A, [&](int row, int col, c128 v) {
+          visit([&](int row, int col, c128 v) {
             const int ti = row / TS, tj = col / TS, ra = row - ti * TS, cc = col - tj * TS;
             c128* t = ti > tj ? &T01[cc * LD + ra] : (ti == tj && ra > cc) ? &Tt[ti * TRI + slot(cc, ra)] : nullptr;
             if (t) *t = cadd(*t, cconj(v));
@@ -872,6 +887,7 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   p.step0 = 0;
   p.total_steps = nsteps;
   p.herm = herm;
+  p.hseg = herm && src == GLF_FROM_LINDBLAD;
   p.tbuf = nullptr;
   p.stagger = 0;
   p.stage = p.rin = p.rout = 0;
