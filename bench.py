@@ -356,7 +356,7 @@ def bench_2des(dev, world, rank, M_total, reps, n=256):
                      "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(gemm_flop / (e0.elapsed_time(e1) / reps / 1e3) / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
                      "flop_per_grid": gemm_flop,
-                     "traffic": measured_traffic("ens_gemm_kernel_xtab", 1) if (M_total, n, world) == (32768, 256, 1)
+                     "traffic": measured_traffic("ens_gemm_kernel_xtab", 1) if (M_total, n, world) == (65536, 256, 1)
                      else None,
                      "traffic_unit": "HBM bytes per ens_gemm_kernel launch (PMC FETCH_SIZE+WRITE_SIZE, calibrated; "
                                      "profiles/pmc_traffic.json)",
@@ -466,7 +466,7 @@ def bench_2des_t2scan(dev, world, rank, M_total, n2, reps, n=256):
                      "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(gemm_flop / ev_apply / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
                      "flop_per_scan": gemm_flop,
-                     "traffic": measured_traffic("ens_t2_gemm_kernel_pruned", 1) if (M_total, n, world) == (32768, 256, 1) else None,
+                     "traffic": measured_traffic("ens_t2_gemm_kernel_pruned", 1) if (M_total, n, world) == (65536, 256, 1) else None,
                      "traffic_unit": "HBM bytes per ens_t2_gemm_kernel launch (4 waiting times; PMC FETCH_SIZE+WRITE_SIZE, "
                                      "calibrated; profiles/pmc_traffic.json)",
                      "note": "8 n3 n1 n2 K flop per scan (K = members x nL) / event time of the bucket applies "
@@ -816,8 +816,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--general", action="store_true",
                     help="force the general (non-Hermitian) GLF kernel instead of the Hermitian one")
-    ap.add_argument("--ens", type=int, default=32768,
-                    help="2DES disorder-ensemble members (total; strong scaling: enough work to split 8 ways)")
+    ap.add_argument("--ens", type=int, default=65536,
+                    help="2DES disorder-ensemble members (total; strong scaling: enough work to split 8 ways; "
+                         "65,536 leaves each of 8 ranks 8,192 members, 0.2 ms per grid)")
     ap.add_argument("--ens-reps", type=int, default=20)
     ap.add_argument("--no-2des", action="store_true")
     ap.add_argument("--t2", type=int, default=16, help="2DES waiting times per scan (0 = skip the scan leg)")

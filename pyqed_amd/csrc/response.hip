@@ -906,9 +906,11 @@ extern "C" int qd_response2d_t2_operands_rect(const qd_c128* alpha, const qd_c12
   QD_CHECK_ARG(M >= 1 && np >= 1 && nr >= 1 && nq >= 1 && n3 >= 1 && n1 >= 1, "%s: bad sizes", fn);
   QD_CHECK_ARG(np <= ZMAX && nr <= ZMAX && nq <= ZMAX && n1 <= 16 * UNI_MAXC,
                "%s: np=%d nr=%d nq=%d (<= %d), n1=%d (<= %d)", fn, np, nr, nq, ZMAX, n1, 16 * UNI_MAXC);
-  QD_CHECK_ARG(M <= 65535 && (long)M * nr < (1L << 30), "%s: M=%d too large", fn, M);
+  QD_CHECK_ARG((long)M * nr < (1L << 30), "%s: M=%d too large", fn, M);
   hipStream_t st = (hipStream_t)stream;
   const T2Dims d = t2_dims(M, nr, n3, n1);
+  // the Z-build grid's y extent is the number of member groups (<= 65535)
+  QD_CHECK_ARG(ceil_div(M, z_group(nr, nq, d.n1p, M)) <= 65535, "%s: M=%d too large", fn, M);
   c128* P = (c128*)P_;
   c128* Q = (c128*)Q_;
   const int MB = 256 / std::max(np, nr);
