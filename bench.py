@@ -925,25 +925,38 @@ def main():
         if args.t2 > 0:
             twodes["t2scan"] = bench_2des_t2scan(dev, world, rank, args.ens, args.t2, args.t2_reps)
 
+    # the remaining legs run no collective: a failure in one is reported in its place (stderr + an "error" entry)
+    # and cannot take the primary line or another rank down with it
+    def guarded(fn, *a):
+        try:
+            return fn(*a)
+        except Exception as e:  # noqa: BLE001
+            import traceback
+            traceback.print_exc()
+            return {"error": f"{type(e).__name__}: {e}"}
+
+    def pair(r):
+        return r if isinstance(r, tuple) else (r, None)
+
     redfield = None
     if not args.no_redfield:
-        redfield, rf_sol = bench_redfield(dev, args.steps, B)
+        redfield, rf_sol = pair(guarded(bench_redfield, dev, args.steps, B))
 
     superop = None
     if not args.no_superop:
-        superop, so_in = bench_superop(dev)
+        superop, so_in = pair(guarded(bench_superop, dev))
 
     spo = None
     if not args.no_spo:
-        spo = bench_spo2(dev, args.spo_steps)
+        spo = guarded(bench_spo2, dev, args.spo_steps)
 
     spo3 = None
     if not args.no_spo3:
-        spo3 = bench_spo3(dev)
+        spo3 = guarded(bench_spo3, dev)
 
     deom = None
     if not args.no_deom:
-        deom = bench_deom(dev, args.deom_steps, args.deom_batch)
+        deom = guarded(bench_deom, dev, args.deom_steps, args.deom_batch)
 
     if rank == 0:
         total_dm_steps = B * args.steps * world
@@ -1001,23 +1014,23 @@ def main():
                 twodes["cpu_baseline"] = cpu_baseline_2des(*ens_in)
             out.setdefault("secondary", {})["2des"] = twodes
         if redfield is not None:
-            if world == 1 and not args.no_cpu:
+            if world == 1 and not args.no_cpu and "error" not in redfield:
                 redfield["cpu_baseline"] = cpu_baseline_redfield(rf_sol)
             out.setdefault("secondary", {})["redfield"] = redfield
         if superop is not None:
-            if world == 1 and not args.no_cpu:
+            if world == 1 and not args.no_cpu and "error" not in superop:
                 superop["cpu_baseline"] = cpu_baseline_superop(*so_in)
             out.setdefault("secondary", {})["superop"] = superop
         if spo is not None:
-            if world == 1 and not args.no_cpu:
+            if world == 1 and not args.no_cpu and "error" not in spo:
                 spo["cpu_baseline"] = cpu_baseline_spo2()
             out.setdefault("secondary", {})["spo2"] = spo
         if spo3 is not None:
-            if world == 1 and not args.no_cpu:
+            if world == 1 and not args.no_cpu and "error" not in spo3:
                 spo3["cpu_baseline"] = cpu_baseline_spo3()
             out.setdefault("secondary", {})["spo3"] = spo3
         if deom is not None:
-            if world == 1 and not args.no_cpu:
+            if world == 1 and not args.no_cpu and "error" not in deom:
                 deom["cpu_baseline"] = cpu_baseline_deom()
             out.setdefault("secondary", {})["deom"] = deom
         print(json.dumps(out), flush=True)
