@@ -7,7 +7,7 @@
 set -e
 PART=${1:-stats}
 R=$PWD
-OUT=$R/gpurun_out/prof_r02b
+OUT=$R/gpurun_out/${PROF_TAG:-prof_r02b}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 if [ "$PART" = stats ]; then
