@@ -886,11 +886,13 @@ def main():
     tr_err = float((tr - 1).abs().max().item())
 
     # smaller batches (B in {1, 64, 256}), event-timed on the launch stream; the auto dispatch
-    # (below HERM_MIN_BATCH = 192 matrices) runs the general kernel's split path, so its executed flops are the
-    # general kernel's
+    # runs B = 64 (Hermitian states, 16 <= B < 192) on the Hermitian pair-block split path and B = 1 on the
+    # general kernel's split-K path; each entry's flops are its own path's (Hermitian GLF form / general kernel)
+    from pyqed_amd.oqs import HERM_SPLIT_MIN_BATCH
     batch_sweep = {}
     for Bs in (1, 64):
         rs = rho[:Bs].clone()
+        hs = Bs >= HERM_SPLIT_MIN_BATCH and not args.general and N <= 128
         lindblad_rk4(Ht, Ct, rs, args.dt, 2)
         torch.cuda.synchronize(dev)
         ss = 100
@@ -900,13 +902,13 @@ def main():
         e1.record(stream)
         torch.cuda.synchronize(dev)
         sec = e0.elapsed_time(e1) / 1e3
-        tf = lindblad_flops_per_step(N, nc) * Bs * ss / sec / 1e12
+        fl = lindblad_flops_per_step(N, nc, hs)
+        tf = fl * Bs * ss / sec / 1e12
         batch_sweep[str(Bs)] = {
             "dm_steps_per_s": round(Bs * ss / sec, 1), "us_per_step": round(sec / ss * 1e6, 2),
-            "path": "glf split-K (general kernel)",
+            "path": "Hermitian pair-block split (glf_split_hk)" if hs else "glf split-K (general kernel)",
             "roofline": {"bound": "mfma", "achieved": round(tf, 3), "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(tf / FP64_MFMA_PEAK_TFLOPS, 4),
-                         "flop_per_dm_step": lindblad_flops_per_step(N, nc)}}
+                         "frac": round(tf / FP64_MFMA_PEAK_TFLOPS, 4), "flop_per_dm_step": fl}}
     single_rate = batch_sweep["1"]["dm_steps_per_s"]
 
     twodes = None

@@ -706,6 +706,107 @@ __global__ __launch_bounds__(CG_WG) void glf_split_k_kernel(LindbladParams p) {
   }
 }
 
+// ---- Hermitian split path (Lindblad, exactly Hermitian rho, batches below the persistent kernel's range)
+// k = X + X^+ with X = P r + sum_c Y_c (C_c^+ / 2) (the persistent Hermitian kernel's form), one workgroup per block
+// PAIR (bm <= bn) of the upper block triangle instead of one per block: the pair's workgroup computes
+//   X(bm, bn) with the Hermitian part C r C^+ in full (A operand Y doubled in the staging, exact), and
+//   X(bn, bm) = (P r)(bn, bm) only (C r C^+ is Hermitian, so its lower block is redundant),
+// and forms k on the upper block, k_ij = X_ij + conj(X_ji), through an LDS transpose; a diagonal block takes the
+// half-weighted X and its own transpose.  The RK4 update runs on the upper elements (rho / acc read there, acc kept
+// there only) and writes each mirror as the conjugate.  Work per stage at n_c = 1 and nb x nb blocks: nb^2 Y blocks
+// + nb(nb-1)/2 x 3 + nb x 2 X segment-blocks, against nb^2 x 4 for the general split path (nb = 4: 42 vs 64).
+template <int BT>
+struct CgSegAScaled {   // CgSegA with the segments >= 1 multiplied by `scale` as they are staged
+  using Raw = cg_v2;
+  const CgSeg* segs;
+  int tps, lda;
+  double scale;
+  __device__ __forceinline__ Raw fetch(int t, int e, int) const {
+    const CgSeg sg = segs[t / tps];
+    return cg_ld(sg.A + (size_t)(e >> 4) * lda + (t % tps) * CG_KT + (e & 15));
+  }
+  __device__ __forceinline__ cg_v2 finish(const Raw& r, int t, int, int) const {
+    return t >= tps ? cg_v2{r.x * scale, r.y * scale} : r;
+  }
+};
+
+__device__ __forceinline__ void split_herm_rk4(const LindbladParams& p, c128* rho, c128* acc, c128* rn, int gi, int gj,
+                                               c128 k) {
+  const int stage = p.stage, Np = p.Np;
+  const double dt = p.dt, dt2 = p.dt / 2.0;
+  const size_t id = (size_t)gi * Np + gj, mid = (size_t)gj * Np + gi;
+  const bool off = gi != gj;
+  const c128 r0 = rho[id];
+  if (stage < 3) {
+    acc[id] = stage == 0 ? k : cadd(acc[id], cscale(k, 2.0));
+    const c128 v = cadd(r0, cscale(k, stage == 2 ? dt : dt2));
+    rn[id] = v;
+    if (off) rn[mid] = cconj(v);
+  } else {
+    const c128 r1 = cadd(r0, cscale(cscale(cadd(acc[id], k), 1.0 / 6.0), dt));
+    rho[id] = r1;
+    if (off) rho[mid] = cconj(r1);
+  }
+}
+
+template <int BT>
+__global__ __launch_bounds__(CG_WG) void glf_split_hk_kernel(LindbladParams p) {
+  __shared__ CgLds<BT> L;
+  __shared__ CgSeg segs[1 + MAX_NC];
+  const int nb = p.Np / BT;
+  int pi = blockIdx.x, bm = 0;   // pair index -> (bm, bn), row-major over the upper block triangle
+  while (pi >= nb - bm) {
+    pi -= nb - bm;
+    ++bm;
+  }
+  const int bn = bm + pi, b = blockIdx.y;
+  const int Np = p.Np, nc = p.nc;
+  const size_t NN = (size_t)Np * Np;
+  const c128* r = split_buf(p, b, p.rin);
+  c128* rn = p.rout ? split_buf(p, b, p.rout) : nullptr;
+  c128* rho = p.rho + (size_t)b * NN;
+  c128* ws = p.ws + (size_t)b * (3 + nc) * NN;
+  c128* acc = ws + 2 * NN;
+  const c128* Y = ws + 3 * NN;
+  const int tps = Np / CG_KT;
+  if (threadIdx.x == 0) {
+    segs[0].A = p.mK + (size_t)bm * BT * Np;
+    segs[0].B = r + bn * BT;
+    for (int c = 0; c < nc; ++c) {
+      segs[1 + c].A = Y + (size_t)c * NN + (size_t)bm * BT * Np;
+      segs[1 + c].B = p.Cd + (size_t)c * NN + bn * BT;
+    }
+  }
+  __syncthreads();
+  CgAcc<BT> XU, XL;
+  {
+    CgSegAScaled<BT> pa{segs, tps, Np, bm < bn ? 2.0 : 1.0};
+    CgSegB<BT> pb{segs, tps, Np};
+    cg_block_gemm_gen<BT>((1 + nc) * tps, pa, pb, L, XU);
+  }
+  if (bm < bn) {
+    if (threadIdx.x == 0) {
+      segs[0].A = p.mK + (size_t)bn * BT * Np;
+      segs[0].B = r + bm * BT;
+    }
+    __syncthreads();
+    CgSegA<BT> pa{segs, tps, Np};
+    CgSegB<BT> pb{segs, tps, Np};
+    cg_block_gemm_gen<BT>(tps, pa, pb, L, XL);
+  }
+  constexpr int LD = BT + 1;
+  static_assert(BT * LD * sizeof(c128) <= sizeof(CgLds<BT>), "LDS transpose buffer");
+  c128* T = reinterpret_cast<c128*>(&L);
+  auto put = [&](int row, int col, c128 v) { T[row * LD + col] = v; };
+  if (bm < bn) cg_epilogue<BT>(XL, put);
+  else cg_epilogue<BT>(XU, put);
+  __syncthreads();
+  cg_epilogue<BT>(XU, [&](int row, int col, c128 v) {
+    if (bm == bn && row > col) return;
+    split_herm_rk4(p, rho, acc, rn, bm * BT + row, bn * BT + col, cadd(v, cconj(T[col * LD + row])));
+  });
+}
+
 // Observables / snapshot of global step gs (after it; gs = 0: the initial state), one workgroup per matrix.
 __global__ __launch_bounds__(CG_WG) void glf_split_obs_kernel(LindbladParams p, int gs) {
   __shared__ c128 sred[CG_WG / 64];
@@ -798,6 +899,7 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   // below ~192 matrices at Np <= 128 (6.6x at one trajectory) and at every batch size above Np = 128;
   // the block is the largest BT < Np that still gives >= 512 workgroups, else 32.
   int split_bt = 0;
+  bool hsplit = false;
   {
     int bt = 32;
     for (int v : {128, 64}) {
@@ -813,6 +915,19 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
     bool use = !herm && Np >= 64 && (Np > 128 || B < 192);
     if (const char* e = std::getenv("QD_GLF_SPLIT")) use = std::atoi(e) != 0 && !herm && Np >= 64;
     if (use) split_bt = bt;
+    // Hermitian Lindblad batches below the persistent kernel's range: the pair-block split path
+    // (glf_split_hk_kernel; QD_GLF_HSPLIT=0 keeps the persistent Hermitian kernel)
+    const char* hse = std::getenv("QD_GLF_HSPLIT");
+    // N = 128 (tools/glf_hsplit_sweep.sh): 32-blocks 198k / 233k / 258k / 264k DM-steps/s at 64 / 128 / 192 / 224
+    // matrices against 82k / 164k / 242k / 278k for the persistent kernel, so the split path runs below 208;
+    // 64-blocks are no better overall (172k / 231k / 232k / 247k).  QD_GLF_HSPLIT_MAX / _BT override (A/B).
+    const char* hme = std::getenv("QD_GLF_HSPLIT_MAX");
+    const int hmax = hme ? std::atoi(hme) : 208;
+    if (herm && src == GLF_FROM_LINDBLAD && Np >= 64 && Np <= 128 && B < hmax && !(hse && hse[0] == '0')) {
+      hsplit = true;
+      split_bt = 32;
+      if (const char* e = std::getenv("QD_GLF_HSPLIT_BT")) split_bt = std::atoi(e) == 64 && Np % 64 == 0 ? 64 : 32;
+    }
   }
   // Split-K of the split path when its blocks leave the chip under-filled: up to 256 workgroups per phase,
   // >= 3 K-tiles each, at most 4 (k phase) / 8 (Y phase) partial slabs per block.  Measured (N = 128 / 256,
@@ -822,7 +937,7 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   if (split_bt) {
     const long blocks = (long)B * (Np / split_bt) * (Np / split_bt);
     const int Tk = (2 + nc) * (Np / CG_KT), Ty = Np / CG_KT;
-    ks = (int)std::max(1L, std::min<long>({4L, 256L / blocks, (long)Tk / 3}));
+    ks = hsplit ? 1 : (int)std::max(1L, std::min<long>({4L, 256L / blocks, (long)Tk / 3}));
     ys = nc ? (int)std::max(1L, std::min<long>({8L, 256L / (blocks * nc), (long)Ty / 3})) : 1;
     if (const char* e = std::getenv("QD_GLF_SPLITK"))
       if (std::atoi(e) == 0) ks = ys = 1;
@@ -933,7 +1048,14 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
           QD_SPLIT(glf_split_y_kernel, dim3(nb * nb, nc, B * ys));
           QD_HIP(hipGetLastError());
         }
-        QD_SPLIT(glf_split_k_kernel, dim3(nb * nb, B * ks));
+        if (hsplit) {   // split_bt is 32 or 64 here
+          if (split_bt == 64)
+            hipLaunchKernelGGL(glf_split_hk_kernel<64>, dim3(nb * (nb + 1) / 2, B), dim3(CG_WG), 0, st, p);
+          else
+            hipLaunchKernelGGL(glf_split_hk_kernel<32>, dim3(nb * (nb + 1) / 2, B), dim3(CG_WG), 0, st, p);
+        } else {
+          QD_SPLIT(glf_split_k_kernel, dim3(nb * nb, B * ks));
+        }
         QD_HIP(hipGetLastError());
 #undef QD_SPLIT
       }

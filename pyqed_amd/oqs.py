@@ -25,7 +25,9 @@ except Exception:  # pragma: no cover
 # --------------------------------------------------------------------------- functional
 # Below this many matrices the general kernel's split path (a workgroup per output block and phase)
 # outruns the persistent Hermitian kernel (one workgroup per matrix): tools/glf_split_bench.py.
-HERM_MIN_BATCH = 192
+HERM_MIN_BATCH = 192        # Redfield (glf_rk4): persistent Hermitian kernel from this batch size
+HERM_SPLIT_MIN_BATCH = 16   # Lindblad: Hermitian kernels from this batch size (qd_lindblad_rk4_herm runs its
+                            # pair-block split path below 208 matrices and the persistent kernel from there)
 
 
 def lindblad_rk4(H: torch.Tensor, c_ops: torch.Tensor | None, rho: torch.Tensor, dt: float, nsteps: int,
@@ -40,10 +42,12 @@ def lindblad_rk4(H: torch.Tensor, c_ops: torch.Tensor | None, rho: torch.Tensor,
     hermitian: use the Hermitian-state kernel (qd_lindblad_rk4_herm: L[rho] = X + X^+,
     1 + 2nc complex GEMMs per RHS instead of 2 + 2nc, one persistent workgroup per matrix).
     None = auto: on when H and every rho in the batch equal their conjugate transposes bit for bit,
-    N <= 128 and the batch fills the chip (B >= HERM_MIN_BATCH); smaller batches run the general
-    kernel, whose split path spreads each matrix over many workgroups (qd_lindblad_rk4: 8.3k
-    instead of 1.3k steps/s for one N = 128 trajectory).  The Lindblad generator preserves
-    Hermiticity, and the Hermitian kernel keeps it exact at every stage.
+    N <= 128 and B >= HERM_SPLIT_MIN_BATCH.  From 208 matrices the library runs the persistent
+    Hermitian kernel (one workgroup per matrix); below that its pair-block split path
+    (one workgroup per upper block pair, 2/3 of the general split path's GEMM work); smaller batches run
+    the general kernel's split path, which spreads each matrix over many workgroups (qd_lindblad_rk4:
+    8.3k instead of 1.3k steps/s for one N = 128 trajectory).  The Lindblad generator preserves
+    Hermiticity, and the Hermitian kernels keep it exact at every stage.
     """
     squeeze = rho.dim() == 2
     if squeeze:
@@ -71,7 +75,7 @@ def lindblad_rk4(H: torch.Tensor, c_ops: torch.Tensor | None, rho: torch.Tensor,
     # rho H, not rho H^+), so the Hermitian kernel is gated on both, bit for bit.
     h_herm = bool(torch.equal(H, H.transpose(-1, -2).conj()))
     if hermitian is None:
-        hermitian = (N <= 128 and B >= HERM_MIN_BATCH and h_herm
+        hermitian = (N <= 128 and B >= HERM_SPLIT_MIN_BATCH and h_herm
                      and bool(torch.equal(rho, rho.transpose(-1, -2).conj())))
     elif hermitian and not h_herm:
         raise ValueError("hermitian=True needs a Hermitian H (the X + X^+ form drops the anti-Hermitian part of H)")

@@ -197,6 +197,44 @@ def test_lindblad_hermitian_kernel_matches_general(N, nc, B):
         assert relerr(a, b) < TOL
 
 
+@pytest.mark.parametrize("N,nc,B,bt", [(128, 1, 16, None), (128, 1, 64, None), (128, 2, 20, None),
+                                       (128, 1, 40, "64"), (64, 1, 24, None), (100, 1, 17, None)])
+def test_lindblad_hermitian_split_path(N, nc, B, bt, monkeypatch):
+    """Hermitian batches below the persistent kernel's range run the pair-block split path (glf_split_hk_kernel:
+    one workgroup per upper block pair, the Hermitian part C r C^+ only on the upper block; 32-blocks, 64-blocks
+    forced by QD_GLF_HSPLIT_BT; N = 100 is zero-padded to 128): vs the oracle, the persistent Hermitian kernel
+    (QD_GLF_HSPLIT=0) and the general kernel, exactly Hermitian, with observables and snapshots."""
+    if bt is not None:
+        monkeypatch.setenv("QD_GLF_HSPLIT_BT", bt)
+    import torch
+    from oracle import lindblad as olb
+    from pyqed_amd import lindblad_rk4
+    H, cs = olb.synthetic_lindblad(N, nc=nc)
+    rho0 = olb.random_pure_states(B, N, seed=N + B)
+    steps, dt = 6, 1e-2
+    ref = olb.lindblad_batch(H, cs, rho0, dt, steps)
+    dev = torch.device("cuda", 0)
+    Ht = torch.from_numpy(H).to(dev)
+    Ct = torch.from_numpy(np.array(cs)).to(dev)
+    E = torch.eye(N, dtype=torch.complex128, device=dev).unsqueeze(0)
+    out = {}
+    for tag, herm, env in (("split", None, None), ("persistent", True, "0"), ("general", False, None)):
+        if env is None:
+            monkeypatch.delenv("QD_GLF_HSPLIT", raising=False)
+        else:
+            monkeypatch.setenv("QD_GLF_HSPLIT", env)
+        rho = torch.from_numpy(rho0.copy()).to(dev)
+        obs, snap = lindblad_rk4(Ht, Ct, rho, dt, steps, e_ops=E, save_every=3, hermitian=herm)
+        torch.cuda.synchronize()
+        out[tag] = (rho.cpu().numpy(), obs.cpu().numpy(), snap.cpu().numpy())
+    r = out["split"][0]
+    assert relerr(r, ref) < TOL
+    assert np.array_equal(r, np.conj(np.swapaxes(r, 1, 2)))
+    for other in ("persistent", "general"):
+        for a, b in zip(out["split"], out[other]):
+            assert relerr(a, b) < TOL
+
+
 def test_lindblad_auto_dispatch_non_hermitian_state():
     """A non-Hermitian initial operator (e.g. A rho, as in the correlation functions) must take
     the general kernel under hermitian=None."""
