@@ -49,6 +49,7 @@ struct DeomParams {
   double dt;
   int bminor;  // ADO-major layout [nmax][B][ns][ns] (hierarchy index fastest; group kernel only)
   int xsplit;  // group kernel: 0 = flat lane numbering; X in {1, 2, 4, 8} = hierarchies dealt to X block classes
+  int ntst;    // group kernel: non-temporal rho / acc accesses (host: state beyond the Infinity Cache's share)
 };
 
 
@@ -136,6 +137,23 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_kernel(DeomParams p) {
 // then every neighbour element (round trip 2).  NS2: ns = 2 (G = 4) with every exchange of the
 // 2 x 2 products a quad DPP move.  Every lane of a group follows the same branches (they share the
 // ADO), so no exchange reads an inactive lane.  H(t), Q(t) go to dynamic LDS ((1 + nmod) ns^2).
+typedef double deom_d2 __attribute__((ext_vector_type(2)));
+// The RK4 state rho / acc is read and written once per stage by its own lane.  p.ntst: non-temporal accesses for
+// those streams, so that they do not evict the stage input rows the 2K neighbour reads hit in the caches (set by
+// the host for batches whose state outgrows the Infinity Cache; below that the plain accesses keep acc resident
+// there from one stage to the next).
+__device__ __forceinline__ c128 ld_once(const c128* q, bool nt) {
+  if (nt) {
+    const deom_d2 v = __builtin_nontemporal_load((const deom_d2*)q);
+    return cmk(v.x, v.y);
+  }
+  return *q;
+}
+__device__ __forceinline__ void st_once(c128* q, c128 v, bool nt) {
+  if (nt) __builtin_nontemporal_store(deom_d2{v.re, v.im}, (deom_d2*)q);
+  else *q = v;
+}
+
 template <int G, int KMAX, bool NS2>
 __global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) {
   extern __shared__ c128 deom_lds[];
@@ -218,8 +236,8 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) 
   const c128 own = live ? X[(size_t)n * rs + ee] : cmk(0, 0);
   const c128 dmp = live ? p.damp[n] : cmk(0, 0);
   const size_t idx = grp * ns2 + e;
-  const c128 r0 = valid ? p.rho[idx] : cmk(0, 0);
-  const c128 a0 = (valid && p.stage > 0) ? p.acc[idx] : cmk(0, 0);
+  const c128 r0 = valid ? ld_once(p.rho + idx, p.ntst) : cmk(0, 0);
+  const c128 a0 = (valid && p.stage > 0) ? ld_once(p.acc + idx, p.ntst) : cmk(0, 0);
   for (int q = threadIdx.x; q < ns2; q += blockDim.x)
     sH[q] = p.Hdip ? cadd(p.H[q], cmul(p.Hdip[q], p.fs)) : p.H[q];
   for (int q = threadIdx.x; q < p.nmod * ns2; q += blockDim.x)
@@ -300,13 +318,13 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) 
 
   const double dt = p.dt;
   if (p.stage == 0) {
-    p.acc[idx] = d;
+    st_once(p.acc + idx, d, p.ntst);
     p.xout[idx] = cadd(r0, cscale(d, dt / 2));
   } else if (p.stage == 1) {
-    p.acc[idx] = cadd(a0, cscale(d, 2.0));
+    st_once(p.acc + idx, cadd(a0, cscale(d, 2.0)), p.ntst);
     p.xout[idx] = cadd(r0, cscale(d, dt / 2));
   } else if (p.stage == 2) {
-    p.acc[idx] = cadd(a0, cscale(d, 2.0));
+    st_once(p.acc + idx, cadd(a0, cscale(d, 2.0)), p.ntst);
     p.xout[idx] = cadd(r0, cscale(d, dt));
   } else {
     const c128 a = cadd(a0, d);
@@ -574,6 +592,11 @@ int deom_launch_stage(const DeomParams& p, hipStream_t st) {
       grid = 8 * (int)((per + tpb - 1) / tpb);
     }
   }
+  // non-temporal rho / acc from 64 MB of state per buffer (four buffers of 25 MB at 64 hierarchies of the bench
+  // hierarchy stay in the 256 MB Infinity Cache: 32.7 vs 34.2 us per stage plain / non-temporal; at 256, 101 MB
+  // each: 127 vs 116 us, profiles/r02/deom/nontemporal_state_ab.txt); QD_DEOM_NT = 0 / 1 forces either
+  q.ntst = tot * sizeof(c128) >= ((size_t)64 << 20);
+  if (const char* s = getenv("QD_DEOM_NT")) q.ntst = atoi(s) != 0;
   const size_t lds = (size_t)(1 + nmod) * ns2 * sizeof(c128);   // H(t), Q(t) of the group kernel
   auto launch_stage = [&]() {
     if (mfma) {

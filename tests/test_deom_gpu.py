@@ -196,7 +196,9 @@ def test_deom_ado_major_batch_layout(ns, B, pulse, monkeypatch):
 def test_deom_xcd_block_classes(ns, B, monkeypatch):
     """Hierarchies dealt to XCD block classes (QD_DEOM_XCD = 1/2/4/8; default 8 when 8 | B) in both batch layouts:
     only the lane -> (ADO, hierarchy) map changes, so every split must give bit-identical histories and final ADOs to
-    the flat numbering (QD_DEOM_XCD=0), and match the oracle (heom/deom.py:1072-1114)."""
+    the flat numbering (QD_DEOM_XCD=0), and match the oracle (heom/deom.py:1072-1114).  "nt": the default split
+    with non-temporal RK4 state accesses forced on (QD_DEOM_NT=1, by default only for state beyond 64 MB per
+    buffer): a cache policy, so bit-identical too."""
     from oracle import deom as od
     from pyqed_amd.deom import Bath, DEOMSolver
     w = sp.symbols(r"\omega", real=True)
@@ -209,18 +211,22 @@ def test_deom_xcd_block_classes(ns, B, monkeypatch):
     psi /= np.linalg.norm(psi, axis=1, keepdims=True)
     rho0 = np.einsum("bi,bj->bij", psi, psi.conj())
     dt, nt, L = 0.005, 8, 6
-    splits = [x for x in ("0", "1", "2", "4", "8") if x == "0" or B % int(x) == 0]
+    splits = [x for x in ("0", "1", "2", "4", "8") if x == "0" or B % int(x) == 0] + ["nt"]
     for layout in ("0", "1"):
         monkeypatch.setenv("QD_DEOM_ADO_MAJOR", layout)
         out = {}
         for x in splits:
-            monkeypatch.setenv("QD_DEOM_XCD", x)
+            if x == "nt":
+                monkeypatch.delenv("QD_DEOM_XCD")
+                monkeypatch.setenv("QD_DEOM_NT", "1")
+            else:
+                monkeypatch.setenv("QD_DEOM_XCD", x)
             sol = DEOMSolver(H, None, bath, np.array([Q]), None, None, None, L)
             _, saved = sol.run_batch(rho0, dt, nt)
             out[x] = (saved, sol.ddos)
+        monkeypatch.delenv("QD_DEOM_NT")
         for x in splits[1:]:
             assert np.array_equal(out[x][0], out["0"][0]) and np.array_equal(out[x][1], out["0"][1]), (layout, x)
-    monkeypatch.delenv("QD_DEOM_XCD")
     tt, ref, _ = od.run(H, np.zeros((ns, ns)), lambda t: 0, np.array([Q]), np.zeros((1, ns, ns)), lambda t: 0,
                         (bath.etal, bath.etar, bath.etaa, bath.expn), L, rho0[B - 1], dt, nt)
     assert relerr(out["0"][0][B - 1], ref) < TOL
