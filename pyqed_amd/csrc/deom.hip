@@ -155,7 +155,7 @@ __device__ __forceinline__ void st_once(c128* q, c128 v, bool nt) {
 }
 
 template <int G, int KMAX, bool NS2>
-__global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) {
+__device__ __forceinline__ void deom_stage_grp_body(const DeomParams& p) {
   extern __shared__ c128 deom_lds[];
   c128* sH = deom_lds;
   c128* sQ = deom_lds + p.ns * p.ns;
@@ -332,6 +332,11 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) 
     p.rho_out[idx] = r1;
     if (p.snap && n == 0) p.snap[(hb * (p.nsteps + 1) + p.step + 1) * ns2 + e] = r1;
   }
+}
+
+template <int G, int KMAX, bool NS2>
+__global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) {
+  deom_stage_grp_body<G, KMAX, NS2>(p);
 }
 
 // MFMA tile kernel for 9 <= ns <= 16 (zero-padded to 16 in registers), NM <= 2 bath modes, K <= 21: one wave per
@@ -614,6 +619,8 @@ int deom_launch_stage(const DeomParams& p, hipStream_t st) {
       case 1: hipLaunchKernelGGL((deom_stage_grp_kernel<1, 8, false>), dim3(grid), dim3(tpb), lds, st, q); break;
       case 4:  // ns = 2; registers sized to K (ym/yp/indices scale with KMAX)
         if (K <= 4) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 4, true>), dim3(grid), dim3(tpb), lds, st, q);
+        // K = 5 (the bench bath, Pade npsd = 4): 104 instead of 116 VGPRs, same speed (profiles/r02/deom/kmax5_ab.txt)
+        else if (K == 5) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 5, true>), dim3(grid), dim3(tpb), lds, st, q);
         else if (K <= 6) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 6, true>), dim3(grid), dim3(tpb), lds, st, q);
         else hipLaunchKernelGGL((deom_stage_grp_kernel<4, 8, true>), dim3(grid), dim3(tpb), lds, st, q);
         break;
