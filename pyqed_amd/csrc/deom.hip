@@ -154,7 +154,21 @@ __device__ __forceinline__ void st_once(c128* q, c128 v, bool nt) {
   else *q = v;
 }
 
-template <int G, int KMAX, bool NS2>
+// a load through the constant address space: wave-uniform addresses become scalar loads (s_load) of tables the
+// stage kernels never write
+template <typename T>
+__device__ __forceinline__ T ld_uniform(const T* q) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return *(const __attribute__((address_space(4))) T*)q;
+#else
+  return *q;   // host pass of the device function only (never executed)
+#endif
+}
+
+// UNI: every wave holds lanes of ONE ADO (ADO-major layout, B / xsplit a multiple of 64 / G), so the ADO's
+// neighbour indices, prefactors and damping are wave-uniform scalar loads instead of per-group vector loads
+// broadcast by DPP moves.
+template <int G, int KMAX, bool NS2, bool UNI = false>
 __device__ __forceinline__ void deom_stage_grp_body(const DeomParams& p) {
   extern __shared__ c128 deom_lds[];
   c128* sH = deom_lds;
@@ -218,23 +232,26 @@ __device__ __forceinline__ void deom_stage_grp_body(const DeomParams& p) {
   };
 
   // round trip 1: this lane's share of the indices and prefactors, own element, RK4 state, H/Q -> LDS
-  constexpr int NI = (KMAX + G - 1) / G;
-  constexpr int NC = (3 * KMAX + G - 1) / G;
+  constexpr int NI = UNI ? 1 : (KMAX + G - 1) / G;
+  constexpr int NC = UNI ? 1 : (3 * KMAX + G - 1) / G;
+  const int nu = UNI ? __builtin_amdgcn_readfirstlane(n) : n;
   int lm[NI], lp[NI];
   c128 lc[NC];
+  if constexpr (!UNI) {
 #pragma unroll
-  for (int q = 0; q < NI; ++q) {
-    const int k = e + G * q;
-    lm[q] = (live && k < K) ? p.minus[(size_t)n * K + k] : -1;
-    lp[q] = (live && k < K) ? p.plus[(size_t)n * K + k] : -1;
-  }
+    for (int q = 0; q < NI; ++q) {
+      const int k = e + G * q;
+      lm[q] = (live && k < K) ? p.minus[(size_t)n * K + k] : -1;
+      lp[q] = (live && k < K) ? p.plus[(size_t)n * K + k] : -1;
+    }
 #pragma unroll
-  for (int q = 0; q < NC; ++q) {
-    const int c = e + G * q;
-    lc[q] = (live && c < 3 * K) ? p.coef[(size_t)n * K * 3 + c] : cmk(0, 0);
+    for (int q = 0; q < NC; ++q) {
+      const int c = e + G * q;
+      lc[q] = (live && c < 3 * K) ? p.coef[(size_t)n * K * 3 + c] : cmk(0, 0);
+    }
   }
   const c128 own = live ? X[(size_t)n * rs + ee] : cmk(0, 0);
-  const c128 dmp = live ? p.damp[n] : cmk(0, 0);
+  const c128 dmp = UNI ? ld_uniform(p.damp + nu) : (live ? p.damp[n] : cmk(0, 0));
   const size_t idx = grp * ns2 + e;
   const c128 r0 = valid ? ld_once(p.rho + idx, p.ntst) : cmk(0, 0);
   const c128 a0 = (valid && p.stage > 0) ? ld_once(p.acc + idx, p.ntst) : cmk(0, 0);
@@ -245,8 +262,13 @@ __device__ __forceinline__ void deom_stage_grp_body(const DeomParams& p) {
   int im[KMAX], ip[KMAX];
 #pragma unroll
   for (int k = 0; k < KMAX; ++k) {
-    im[k] = bci(lm[k / G], k % G);
-    ip[k] = bci(lp[k / G], k % G);
+    if constexpr (UNI) {
+      im[k] = k < K ? ld_uniform(p.minus + (size_t)nu * K + k) : -1;
+      ip[k] = k < K ? ld_uniform(p.plus + (size_t)nu * K + k) : -1;
+    } else {
+      im[k] = bci(lm[k / G], k % G);
+      ip[k] = bci(lp[k / G], k % G);
+    }
   }
 
   // round trip 2: every neighbour element this lane owns
@@ -306,9 +328,17 @@ __device__ __forceinline__ void deom_stage_grp_body(const DeomParams& p) {
       SL = SR = cmk(0, 0);
       mcur = m;
     }
-    const c128 cL = bc(lc[(3 * k) / G], (3 * k) % G);
-    const c128 cR = bc(lc[(3 * k + 1) / G], (3 * k + 1) % G);
-    const c128 cP = bc(lc[(3 * k + 2) / G], (3 * k + 2) % G);
+    c128 cL, cR, cP;
+    if constexpr (UNI) {
+      const c128* cf = p.coef + ((size_t)nu * K + k) * 3;
+      cL = ld_uniform(cf);
+      cR = ld_uniform(cf + 1);
+      cP = ld_uniform(cf + 2);
+    } else {
+      cL = bc(lc[(3 * k) / G], (3 * k) % G);
+      cR = bc(lc[(3 * k + 1) / G], (3 * k + 1) % G);
+      cP = bc(lc[(3 * k + 2) / G], (3 * k + 2) % G);
+    }
     const c128 py = cmul(cP, yp[k]);
     SL = cadd(SL, cadd(cmul(cL, ym[k]), py));
     SR = cadd(SR, csub(cmul(cR, ym[k]), py));
@@ -334,9 +364,9 @@ __device__ __forceinline__ void deom_stage_grp_body(const DeomParams& p) {
   }
 }
 
-template <int G, int KMAX, bool NS2>
+template <int G, int KMAX, bool NS2, bool UNI = false>
 __global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) {
-  deom_stage_grp_body<G, KMAX, NS2>(p);
+  deom_stage_grp_body<G, KMAX, NS2, UNI>(p);
 }
 
 // MFMA tile kernel for 9 <= ns <= 16 (zero-padded to 16 in registers), NM <= 2 bath modes, K <= 21: one wave per
@@ -603,6 +633,10 @@ int deom_launch_stage(const DeomParams& p, hipStream_t st) {
   q.ntst = tot * sizeof(c128) >= ((size_t)64 << 20);
   if (const char* s = getenv("QD_DEOM_NT")) q.ntst = atoi(s) != 0;
   const size_t lds = (size_t)(1 + nmod) * ns2 * sizeof(c128);   // H(t), Q(t) of the group kernel
+  // wave-uniform ADO (scalar tables): ADO-major, classes of a multiple of 64 / G hierarchies, 64-multiple blocks
+  const char* ue = getenv("QD_DEOM_UNI");
+  const bool uni = grp && G == 4 && bminor && q.xsplit > 0 && (B / q.xsplit) % (64 / G) == 0 && tpb % 64 == 0 &&
+                   !(ue && ue[0] == '0');
   auto launch_stage = [&]() {
     if (mfma) {
       const int wg = (int)(((long)B * nmax + 3) / 4);
@@ -617,12 +651,19 @@ int deom_launch_stage(const DeomParams& p, hipStream_t st) {
     }
     switch (G) {
       case 1: hipLaunchKernelGGL((deom_stage_grp_kernel<1, 8, false>), dim3(grid), dim3(tpb), lds, st, q); break;
-      case 4:  // ns = 2; registers sized to K (ym/yp/indices scale with KMAX)
-        if (K <= 4) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 4, true>), dim3(grid), dim3(tpb), lds, st, q);
-        // K = 5 (the bench bath, Pade npsd = 4): 104 instead of 116 VGPRs, same speed (profiles/r02/deom/kmax5_ab.txt)
-        else if (K == 5) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 5, true>), dim3(grid), dim3(tpb), lds, st, q);
-        else if (K <= 6) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 6, true>), dim3(grid), dim3(tpb), lds, st, q);
-        else hipLaunchKernelGGL((deom_stage_grp_kernel<4, 8, true>), dim3(grid), dim3(tpb), lds, st, q);
+      case 4:  // ns = 2; registers sized to K (ym/yp/indices scale with KMAX); K = 5 (the bench bath, Pade npsd = 4):
+               // 104 instead of 116 VGPRs, same speed (profiles/r02/deom/kmax5_ab.txt)
+        if (uni) {
+          if (K <= 4) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 4, true, true>), dim3(grid), dim3(tpb), lds, st, q);
+          else if (K == 5) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 5, true, true>), dim3(grid), dim3(tpb), lds, st, q);
+          else if (K <= 6) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 6, true, true>), dim3(grid), dim3(tpb), lds, st, q);
+          else hipLaunchKernelGGL((deom_stage_grp_kernel<4, 8, true, true>), dim3(grid), dim3(tpb), lds, st, q);
+        } else {
+          if (K <= 4) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 4, true>), dim3(grid), dim3(tpb), lds, st, q);
+          else if (K == 5) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 5, true>), dim3(grid), dim3(tpb), lds, st, q);
+          else if (K <= 6) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 6, true>), dim3(grid), dim3(tpb), lds, st, q);
+          else hipLaunchKernelGGL((deom_stage_grp_kernel<4, 8, true>), dim3(grid), dim3(tpb), lds, st, q);
+        }
         break;
       case 16: hipLaunchKernelGGL((deom_stage_grp_kernel<16, 8, false>), dim3(grid), dim3(tpb), lds, st, q); break;
       case 32: hipLaunchKernelGGL((deom_stage_grp_kernel<32, 8, false>), dim3(grid), dim3(tpb), lds, st, q); break;

@@ -192,17 +192,18 @@ def test_deom_ado_major_batch_layout(ns, B, pulse, monkeypatch):
         assert relerr(out["1"][0][b], ref) < TOL, b
 
 
-@pytest.mark.parametrize("ns,B", [(2, 16), (2, 1), (3, 8)])
-def test_deom_xcd_block_classes(ns, B, monkeypatch):
+@pytest.mark.parametrize("ns,B,npsd", [(2, 16, 3), (2, 1, 3), (3, 8, 3), (2, 32, 4)])
+def test_deom_xcd_block_classes(ns, B, npsd, monkeypatch):
     """Hierarchies dealt to XCD block classes (QD_DEOM_XCD = 1/2/4/8; default 8 when 8 | B) in both batch layouts:
     only the lane -> (ADO, hierarchy) map changes, so every split must give bit-identical histories and final ADOs to
     the flat numbering (QD_DEOM_XCD=0), and match the oracle (heom/deom.py:1072-1114).  "nt": the default split
     with non-temporal RK4 state accesses forced on (QD_DEOM_NT=1, by default only for state beyond 64 MB per
-    buffer): a cache policy, so bit-identical too."""
+    buffer): a cache policy, so bit-identical too.  ns = 2 ADO-major classes of 16k hierarchies (B = 16 at X = 1,
+    B = 32 at X = 1 / 2) run the wave-uniform kernel with scalar table loads (K = 4, and K = 5 at npsd = 4)."""
     from oracle import deom as od
     from pyqed_amd.deom import Bath, DEOMSolver
     w = sp.symbols(r"\omega", real=True)
-    bath = Bath([2 * 0.5 * w / (1.0 + w ** 2)], w, [1.0], [3], [0] * 4)
+    bath = Bath([2 * 0.5 * w / (1.0 + w ** 2)], w, [1.0], [npsd], [0] * (npsd + 1))
     rng = np.random.default_rng(7 + B)
     A = rng.standard_normal((ns, ns)) + 1j * rng.standard_normal((ns, ns))
     H = (A + A.conj().T) / 4
