@@ -198,24 +198,26 @@ def test_lindblad_hermitian_kernel_matches_general(N, nc, B):
 
 
 @pytest.mark.parametrize("N,nc,B,bt", [(128, 1, 16, None), (128, 1, 64, None), (128, 2, 20, None),
-                                       (128, 1, 40, "64"), (64, 1, 24, None), (100, 1, 17, None)])
+                                       (128, 1, 40, "64"), (64, 1, 24, None), (100, 1, 17, None),
+                                       (128, 0, 16, None), (64, 3, 18, "64")])
 def test_lindblad_hermitian_split_path(N, nc, B, bt, monkeypatch):
     """Hermitian batches below the persistent kernel's range run the pair-block split path (glf_split_hk_kernel:
     one workgroup per upper block pair, the Hermitian part C r C^+ only on the upper block; 32-blocks, 64-blocks
-    forced by QD_GLF_HSPLIT_BT; N = 100 is zero-padded to 128): vs the oracle, the persistent Hermitian kernel
+    forced by QD_GLF_HSPLIT_BT; N = 100 is zero-padded to 128; no collapse operators, three): vs the oracle, the persistent Hermitian kernel
     (QD_GLF_HSPLIT=0) and the general kernel, exactly Hermitian, with observables and snapshots."""
     if bt is not None:
         monkeypatch.setenv("QD_GLF_HSPLIT_BT", bt)
     import torch
     from oracle import lindblad as olb
     from pyqed_amd import lindblad_rk4
-    H, cs = olb.synthetic_lindblad(N, nc=nc)
+    H, cs = olb.synthetic_lindblad(N, nc=max(nc, 1))
+    cs = cs[:nc]
     rho0 = olb.random_pure_states(B, N, seed=N + B)
     steps, dt = 6, 1e-2
     ref = olb.lindblad_batch(H, cs, rho0, dt, steps)
     dev = torch.device("cuda", 0)
     Ht = torch.from_numpy(H).to(dev)
-    Ct = torch.from_numpy(np.array(cs)).to(dev)
+    Ct = torch.from_numpy(np.array(cs)).to(dev) if nc else None
     E = torch.eye(N, dtype=torch.complex128, device=dev).unsqueeze(0)
     out = {}
     for tag, herm, env in (("split", None, None), ("persistent", True, "0"), ("general", False, None)):
