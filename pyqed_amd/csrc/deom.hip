@@ -50,6 +50,7 @@ struct DeomParams {
   int bminor;  // ADO-major layout [nmax][B][ns][ns] (hierarchy index fastest; group kernel only)
   int xsplit;  // group kernel: 0 = flat lane numbering; X in {1, 2, 4, 8} = hierarchies dealt to X block classes
   int ntst;    // group kernel: non-temporal rho / acc accesses (host: state beyond the Infinity Cache's share)
+  int bchunk;  // group kernel, ADO-major: hierarchies of a class walked in chunks of bchunk (0 = all at once)
 };
 
 
@@ -194,10 +195,20 @@ __device__ __forceinline__ void deom_stage_grp_body(const DeomParams& p) {
   const unsigned lgrp = u / G;              // b nmax + n, or n B + b (bminor), within the class
   const int e = (int)(u % G);
   const bool live = lgrp < Bx * (unsigned)p.nmax;   // uniform within a group
-  const unsigned q = p.bminor ? Bx : (unsigned)p.nmax;
-  const unsigned hi = lgrp / q, lo = lgrp - hi * q;
+  // bchunk = C > 0 (ADO-major): the class's hierarchies are walked in chunks of C, every ADO of one chunk before
+  // the next chunk, so the neighbour rows the resident waves read (tiers l - 1 .. l + 1 of C hierarchies) stay
+  // within the XCD's L2 instead of spanning all Bx hierarchies of the class
+  unsigned lch = lgrp, boff = 0;
+  if (p.bminor && p.bchunk > 0) {
+    const unsigned per = (unsigned)p.bchunk * (unsigned)p.nmax;
+    const unsigned ch = lgrp / per;
+    lch = lgrp - ch * per;
+    boff = ch * (unsigned)p.bchunk;
+  }
+  const unsigned q = p.bminor ? (p.bchunk > 0 ? (unsigned)p.bchunk : Bx) : (unsigned)p.nmax;
+  const unsigned hi = lch / q, lo = lch - hi * q;
   const int n = live ? (int)(p.bminor ? hi : lo) : 0;
-  const size_t hb = (size_t)cls * Bx + (live ? (p.bminor ? lo : hi) : 0);   // hierarchy b
+  const size_t hb = (size_t)cls * Bx + (live ? (p.bminor ? boff + lo : hi) : 0);   // hierarchy b
   const size_t grp = p.bminor ? (size_t)n * p.B + hb : hb * p.nmax + n;     // flat row of rho / acc / xout
   const bool valid = live && e < ns2;
   const size_t rs = p.bminor ? (size_t)p.B * ns2 : (size_t)ns2;         // ADO row stride
@@ -633,9 +644,20 @@ int deom_launch_stage(const DeomParams& p, hipStream_t st) {
   q.ntst = tot * sizeof(c128) >= ((size_t)64 << 20);
   if (const char* s = getenv("QD_DEOM_NT")) q.ntst = atoi(s) != 0;
   const size_t lds = (size_t)(1 + nmod) * ns2 * sizeof(c128);   // H(t), Q(t) of the group kernel
-  // wave-uniform ADO (scalar tables): ADO-major, classes of a multiple of 64 / G hierarchies, 64-multiple blocks
+  // hierarchy chunks of 16 in classes of more (ADO-major): 256 hierarchies = 8 classes of 32, see the kernel;
+  // QD_DEOM_BCHUNK overrides (0 = off, else a divisor of the class size)
+  q.bchunk = 0;
+  if (grp && bminor && q.xsplit > 0) {
+    const int Bx = B / q.xsplit;
+    int c = (Bx > 16 && Bx % 16 == 0) ? 16 : 0;
+    if (const char* s = getenv("QD_DEOM_BCHUNK")) c = atoi(s);
+    q.bchunk = (c > 0 && c < Bx && Bx % c == 0) ? c : 0;
+  }
+  // wave-uniform ADO (scalar tables): ADO-major, classes (chunks) of a multiple of 64 / G hierarchies, 64-multiple
+  // blocks
   const char* ue = getenv("QD_DEOM_UNI");
-  const bool uni = grp && G == 4 && bminor && q.xsplit > 0 && (B / q.xsplit) % (64 / G) == 0 && tpb % 64 == 0 &&
+  const int wb = q.bchunk > 0 ? q.bchunk : (q.xsplit > 0 ? B / q.xsplit : 0);
+  const bool uni = grp && G == 4 && bminor && q.xsplit > 0 && wb % (64 / G) == 0 && tpb % 64 == 0 &&
                    !(ue && ue[0] == '0');
   auto launch_stage = [&]() {
     if (mfma) {
