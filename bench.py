@@ -72,9 +72,10 @@ def lindblad_flops_per_step(N: int, nc: int, hermitian: bool = False) -> float:
 
 def lindblad_executed_flops_per_step(N: int, nc: int, hermitian: bool = False) -> float:
     # What the MFMA units execute: the Hermitian kernel at 128-blocks (N_p = 128) skips the Hermitian part's
-    # redundant lower-left 64 x 64 block (glf.hip / cgemm_block.hpp cg_herm_x_gemm: 1/4 of each (C r)C^+ GEMM).
+    # redundant 16 x 16 tiles below the diagonal (glf.hip / cgemm_block.hpp cg_herm_x_gemm: 28 of the 64 tiles of
+    # each (C r)C^+ GEMM, so 36/64 of it runs).
     if hermitian and N == 128:
-        return 4.0 * (1 + nc + 0.75 * nc) * 8.0 * N ** 3
+        return 4.0 * (1 + nc + (36.0 / 64.0) * nc) * 8.0 * N ** 3
     return lindblad_flops_per_step(N, nc, hermitian)
 
 
@@ -996,7 +997,8 @@ def main():
                 "flop_per_dm_step": lindblad_flops_per_step(N, nc, herm),
                 "flop_note": "flop_per_dm_step = the Hermitian GLF form, 4 x (1 + 2 n_c) x 8 N^3 (the round-1 "
                              "accounting); the kernel executes executed_flop_per_dm_step of it (the redundant "
-                             "lower-left block of (C r)C^+ is skipped), executed_frac is that rate over the peak",
+                             "16 x 16 tiles of (C r)C^+ below the diagonal are skipped), executed_frac is that rate "
+                             "over the peak",
                 "executed_flop_per_dm_step": lindblad_executed_flops_per_step(N, nc, herm),
                 "executed_tflops": round(lindblad_executed_flops_per_step(N, nc, herm) * B * args.steps / kern_s / 1e12,
                                          3),

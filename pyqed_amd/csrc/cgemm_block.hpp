@@ -307,46 +307,66 @@ __device__ __forceinline__ void cg_block_gemm(const CgSeg* segs, int nseg, int K
 
 // ---------------------------------------------------------------- Hermitian X GEMM (BT = 128)
 // X = A r + B W over two K segments (A r: segment 0; B W: segment 1, W = C^+ / 2), for k = X + X^+ of a
-// Hermitian right-hand side.  Only k on the upper blocks is used, and B W (= C r C^+ / 2) is itself Hermitian,
-// so segment 1 need not reach the lower-left 64 x 64 block (1, 0): there X = A r alone, and the upper-right
-// block (0, 1) takes the full C r C^+ instead of its half (A fragment doubled: 2 a x b / 2 is exact), so that
-// k_ij = X_ij + conj(X_ji) = (A r)_ij + conj((A r)_ji) + (C r C^+)_ij on the off-diagonal blocks and as before on
-// the diagonal ones.  The wave -> tile layout spreads block (1, 0) over every wave (each owns row tiles i and 4 + i
-// and column tiles {2h, 2h+1, 4+2h, 5+2h}, i = wave / 2, h = wave % 2), so skipping its tiles in segment 1 takes
-// 2 of 8 tiles from every wave alike: 1/4 of segment 1's MFMAs, 1/12 of a stage's.
+// Hermitian right-hand side.  Only k on the upper triangle is used, and B W (= C r C^+ / 2) is itself Hermitian, so
+// segment 1 need not reach the 16 x 16 tiles below the diagonal: there X = A r alone, and each tile above the diagonal
+// takes the full C r C^+ instead of its half (A fragment doubled: 2 a x b / 2 is exact), so that
+// k_ij = X_ij + conj(X_ji) = (A r)_ij + conj((A r)_ji) + (C r C^+)_ij for every i < j (diagonal tiles keep the half
+// in both triangles).  Tile layout (16-tiles R, C in 0..7): wave w = 2 i + h owns row tiles {i, 7 - i} and the
+// column tiles of kHermCols[w]; the two waves of a row pair split the 8 columns so that one holds 4 and the other 5
+// of the pair's 9 tiles with R <= C, placed so that each SIMD's two waves (w, w + 4) hold 9: segment 1 is 36 tiles,
+// 9 per SIMD, against 12 per SIMD when only the lower-left 64 x 64 block was skipped.
 struct CgHermLayout {
-  static __device__ __forceinline__ int row0(int wave, int mi) { return mi * 64 + (wave >> 1) * 16; }
-  static __device__ __forceinline__ int col0(int wave, int nj) { return (nj >> 1) * 64 + (2 * (wave & 1) + (nj & 1)) * 16; }
+  // column tiles of wave w, nibble nj (waves 0..3 in the low word, 4..7 in the high one)
+  static __device__ __forceinline__ int ctile(int wave, int nj) {
+    constexpr unsigned long long lo = 0x3210ULL | (0x7654ULL << 16) | (0x7610ULL << 32) | (0x5432ULL << 48);
+    constexpr unsigned long long hi = 0x7432ULL | (0x6510ULL << 16) | (0x5410ULL << 32) | (0x7632ULL << 48);
+    const unsigned long long t = wave < 4 ? lo : hi;
+    return (int)((t >> ((wave & 3) * 16 + nj * 4)) & 15);
+  }
+  static __device__ __forceinline__ int rtile(int wave, int mi) { return mi == 0 ? (wave >> 1) : 7 - (wave >> 1); }
+  static __device__ __forceinline__ int row0(int wave, int mi) { return rtile(wave, mi) * 16; }
+  static __device__ __forceinline__ int col0(int wave, int nj) { return ctile(wave, nj) * 16; }
 };
 
-template <typename Mid>
-__device__ __forceinline__ void cg_herm_compute_tile(const CgLds<128>& L, int buf, CgAcc<128>& acc, int wave, bool seg1,
-                                                     Mid mid) {
-  constexpr int BT = 128, MW = 2, NW = 4, NQ = CG_KT / 4;
+// Tile roles of wave w in the Hermitian segments, bit mi * 4 + nj: below the diagonal (skipped) / above it (A doubled).
+constexpr int cg_herm_ctile(int w, int nj) {
+  constexpr unsigned short cols[8] = {0x3210, 0x7654, 0x7610, 0x5432, 0x7432, 0x6510, 0x5410, 0x7632};
+  return (cols[w] >> (nj * 4)) & 15;
+}
+constexpr unsigned cg_herm_mask(int w, bool below) {
+  unsigned m = 0;
+  for (int mi = 0; mi < 2; ++mi)
+    for (int nj = 0; nj < 4; ++nj) {
+      const int R = mi == 0 ? (w >> 1) : 7 - (w >> 1), C = cg_herm_ctile(w, nj);
+      if (below ? R > C : R < C) m |= 1u << (mi * 4 + nj);
+    }
+  return m;
+}
+
+// k-steps [Q0, Q1) of one K-tile of the Hermitian X GEMM for a wave whose tile roles SK (skip) / DB (doubled A) are
+// compile-time constants (segment 0 runs with SK = DB = 0): no per-tile selects or branches in the MFMA stream.
+template <int W, unsigned SK, unsigned DB, int Q0, int Q1>
+__device__ __forceinline__ void cg_herm_ksteps(const CgLds<128>& L, int buf, CgAcc<128>& acc) {
+  constexpr int BT = 128, MW = 2, NW = 4;
   const int lane = threadIdx.x & 63;
   const int lr = lane & 15, lk = lane >> 4;
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    if (q == CG_STAGE_AT) {
-      cg_sched_fence();
-      mid();
-      cg_sched_fence();
-    }
+  for (int q = Q0; q < Q1; ++q) {
     const int kk = 4 * q;
-    c128 a[MW], b[NW];
+    c128 a[MW], a2[MW], b[NW];
 #pragma unroll
-    for (int mi = 0; mi < MW; ++mi) a[mi] = L.a[buf][(CgHermLayout::row0(wave, mi) + lr) * CG_SA + kk + lk];
+    for (int mi = 0; mi < MW; ++mi) {
+      a[mi] = L.a[buf][(16 * (mi == 0 ? (W >> 1) : 7 - (W >> 1)) + lr) * CG_SA + kk + lk];
+      if ((DB >> (mi * 4)) & 15u) a2[mi] = cmk(a[mi].re + a[mi].re, a[mi].im + a[mi].im);   // doubled (exact)
+    }
 #pragma unroll
-    for (int nj = 0; nj < NW; ++nj) b[nj] = L.b[buf][(kk + lk) * BT + CgHermLayout::col0(wave, nj) + lr];
-    // block (0, 1) in the Hermitian segments: the doubled fragment (exact); a[0] itself elsewhere
-    const double s2 = seg1 ? 2.0 : 1.0;
-    const c128 a2 = cmk(a[0].re * s2, a[0].im * s2);
+    for (int nj = 0; nj < NW; ++nj) b[nj] = L.b[buf][(kk + lk) * BT + 16 * cg_herm_ctile(W, nj) + lr];
 #pragma unroll
     for (int mi = 0; mi < MW; ++mi)
 #pragma unroll
       for (int nj = 0; nj < NW; ++nj) {
-        if (mi == 1 && nj < 2 && seg1) continue;   // block (1, 0): no Hermitian part
-        const c128& av = (mi == 0 && nj >= 2) ? a2 : a[mi];
+        if (SK & (1u << (mi * 4 + nj))) continue;   // below the diagonal: no Hermitian part
+        const c128& av = (DB & (1u << (mi * 4 + nj))) ? a2[mi] : a[mi];
         acc.re[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.re, b[nj].re, acc.re[mi][nj], 0, 0, 0);
         acc.im[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.re, b[nj].im, acc.im[mi][nj], 0, 0, 0);
       }
@@ -354,26 +374,56 @@ __device__ __forceinline__ void cg_herm_compute_tile(const CgLds<128>& L, int bu
     for (int mi = 0; mi < MW; ++mi)
 #pragma unroll
       for (int nj = 0; nj < NW; ++nj) {
-        if (mi == 1 && nj < 2 && seg1) continue;
-        const c128& av = (mi == 0 && nj >= 2) ? a2 : a[mi];
+        if (SK & (1u << (mi * 4 + nj))) continue;
+        const c128& av = (DB & (1u << (mi * 4 + nj))) ? a2[mi] : a[mi];
         acc.re[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av.im, b[nj].im, acc.re[mi][nj], 0, 0, 0);
         acc.im[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.im, b[nj].re, acc.im[mi][nj], 0, 0, 0);
       }
   }
-  if (CG_STAGE_AT >= NQ) {
+}
+
+// K-tiles [t0, t1) of the X GEMM (of T in all) with the tile roles SK / DB fixed at compile time: tile t + 1's global
+// loads are in flight during tile t's MFMAs and its LDS stores issue behind the first CG_STAGE_AT k-steps.
+template <int W, unsigned SK, unsigned DB>
+__device__ __forceinline__ void cg_herm_x_range(int t0, int t1, int T, const CgSegA<128>& pa, const CgSegB<128>& pb,
+                                                CgLds<128>& L, CgAcc<128>& acc, int tid, cg_v2* ra, cg_v2* rb) {
+  constexpr int NLD = cg_nld<128>(), NQ = CG_KT / 4, QS = CG_STAGE_AT < NQ ? CG_STAGE_AT : NQ;
+  for (int t = t0; t < t1; ++t) {
+    const bool more = (t + 1) < T;
+    if (more) {
+#pragma unroll
+      for (int q = 0; q < NLD; ++q) {
+        const int e = tid + CG_WG * q;
+        ra[q] = pa.fetch(t + 1, e, q);
+        rb[q] = pb.fetch(t + 1, e, q);
+      }
+    }
+    cg_herm_ksteps<W, SK, DB, 0, QS>(L, t & 1, acc);
     cg_sched_fence();
-    mid();
+    if (more) {
+#pragma unroll
+      for (int q = 0; q < NLD; ++q) {
+        const int e = tid + CG_WG * q;
+        cg_st_lds(&L.a[(t + 1) & 1][(e >> 4) * CG_SA + (e & 15)], ra[q]);
+        cg_st_lds(&L.b[(t + 1) & 1][e], rb[q]);
+      }
+    }
+    cg_sched_fence();
+    if constexpr (QS < NQ) cg_herm_ksteps<W, SK, DB, QS, NQ>(L, t & 1, acc);
+    __syncthreads();
   }
 }
 
 // segs[0] = (A, r), segs[1..nseg-1] = (B_c, W_c); K = the common depth (tps = K / 16 K-tiles per segment).
-// hermitian_part: sum_c B_c W_c is Hermitian (segments >= 1 skip block (1, 0) and double block (0, 1)); otherwise
-// every tile takes every segment (the plain X GEMM on this layout).  All threads call it; ends with a workgroup
-// barrier.  Visit the result with cg_herm_epilogue.
+// hermitian_part: sum_c B_c W_c is Hermitian (segments >= 1 skip the tiles below the diagonal and double those above
+// it, CgHermLayout); otherwise every tile takes every segment (the plain X GEMM on this layout).  Each wave runs the
+// Hermitian segments with its own compile-time tile roles (one code path per wave for the whole range, so the MFMA
+// stream carries no selects or branches).  All threads call it; ends with a workgroup barrier.  Visit the result with
+// cg_herm_epilogue.
 __device__ __forceinline__ void cg_herm_x_gemm(const CgSeg* segs, int nseg, int K, int lda, int ldb, CgLds<128>& L,
                                                CgAcc<128>& acc, bool hermitian_part) {
   constexpr int BT = 128, MW = 2, NW = 4;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #pragma unroll
   for (int mi = 0; mi < MW; ++mi)
 #pragma unroll
@@ -388,34 +438,28 @@ __device__ __forceinline__ void cg_herm_x_gemm(const CgSeg* segs, int nseg, int 
   int tid = threadIdx.x;
   asm volatile("" : "+v"(tid));
   cg_v2 ra[NLD], rb[NLD];
-  auto load = [&](int t) {
 #pragma unroll
-    for (int q = 0; q < NLD; ++q) {
-      const int e = tid + CG_WG * q;
-      ra[q] = pa.fetch(t, e, q);
-      rb[q] = pb.fetch(t, e, q);
-    }
-  };
-  auto store = [&](int t, int buf) {
-#pragma unroll
-    for (int q = 0; q < NLD; ++q) {
-      const int e = tid + CG_WG * q;
-      cg_st_lds(&L.a[buf][(e >> 4) * CG_SA + (e & 15)], ra[q]);
-      cg_st_lds(&L.b[buf][e], rb[q]);
-    }
-  };
-  load(0);
-  store(0, 0);
-  __syncthreads();
-  for (int t = 0; t < T; ++t) {
-    const bool more = (t + 1) < T;
-    if (more) load(t + 1);
-    auto mid = [&]() {
-      if (more) store(t + 1, (t + 1) & 1);
-    };
-    cg_herm_compute_tile(L, t & 1, acc, wave, hermitian_part && t >= tps, mid);
-    __syncthreads();
+  for (int q = 0; q < NLD; ++q) {
+    const int e = tid + CG_WG * q;
+    cg_st_lds(&L.a[0][(e >> 4) * CG_SA + (e & 15)], pa.fetch(0, e, q));
+    cg_st_lds(&L.b[0][e], pb.fetch(0, e, q));
   }
+  __syncthreads();
+  auto run = [&](auto wc) {
+    constexpr int W = decltype(wc)::value;
+    if (!hermitian_part) {
+      cg_herm_x_range<W, 0u, 0u>(0, T, T, pa, pb, L, acc, tid, ra, rb);
+      return;
+    }
+    cg_herm_x_range<W, 0u, 0u>(0, tps, T, pa, pb, L, acc, tid, ra, rb);
+    cg_herm_x_range<W, cg_herm_mask(W, true), cg_herm_mask(W, false)>(tps, T, T, pa, pb, L, acc, tid, ra, rb);
+  };
+#define QD_HT(w) \
+  case w: run(std::integral_constant<int, w>{}); break;
+  switch (wave) {
+    QD_HT(0) QD_HT(1) QD_HT(2) QD_HT(3) QD_HT(4) QD_HT(5) QD_HT(6) default: QD_HT(7)
+  }
+#undef QD_HT
 }
 
 template <typename F>
