@@ -987,6 +987,8 @@ def main():
             "roofline": {
                 "bound": "mfma",
                 "kernel": kname,
+                "kernel_symbol": (f"qd::lindblad_rk4_kernel<{min(128, N)}, {'true, true' if herm else 'false, false'}>"
+                                  " (rocprofv3 name)"),
                 "achieved": round(achieved, 3),
                 "peak": FP64_MFMA_PEAK_TFLOPS,
                 "unit": "TFLOP/s",

@@ -346,7 +346,7 @@ constexpr unsigned cg_herm_mask(int w, bool below) {
 // k-steps [Q0, Q1) of one K-tile of the Hermitian X GEMM for a wave whose tile roles SK (skip) / DB (doubled A) are
 // compile-time constants (segment 0 runs with SK = DB = 0): no per-tile selects or branches in the MFMA stream.
 template <int W, unsigned SK, unsigned DB, int Q0, int Q1>
-__device__ __forceinline__ void cg_herm_ksteps(const CgLds<128>& L, int buf, CgAcc<128>& acc) {
+__device__ __forceinline__ void cg_herm_ksteps(const CgLds<128>& L, int buf, CgAcc<128>& acc, int wave) {
   constexpr int BT = 128, MW = 2, NW = 4;
   const int lane = threadIdx.x & 63;
   const int lr = lane & 15, lk = lane >> 4;
@@ -356,11 +356,13 @@ __device__ __forceinline__ void cg_herm_ksteps(const CgLds<128>& L, int buf, CgA
     c128 a[MW], a2[MW], b[NW];
 #pragma unroll
     for (int mi = 0; mi < MW; ++mi) {
-      a[mi] = L.a[buf][(16 * (mi == 0 ? (W >> 1) : 7 - (W >> 1)) + lr) * CG_SA + kk + lk];
+      const int r0 = 16 * (mi == 0 ? (W >> 1) : 7 - (W >> 1));
+      a[mi] = L.a[buf][(r0 + lr) * CG_SA + kk + lk];
       if ((DB >> (mi * 4)) & 15u) a2[mi] = cmk(a[mi].re + a[mi].re, a[mi].im + a[mi].im);   // doubled (exact)
     }
 #pragma unroll
-    for (int nj = 0; nj < NW; ++nj) b[nj] = L.b[buf][(kk + lk) * BT + 16 * cg_herm_ctile(W, nj) + lr];
+    for (int nj = 0; nj < NW; ++nj)
+      b[nj] = L.b[buf][(kk + lk) * BT + 16 * cg_herm_ctile(W, nj) + lr];
 #pragma unroll
     for (int mi = 0; mi < MW; ++mi)
 #pragma unroll
@@ -384,9 +386,11 @@ __device__ __forceinline__ void cg_herm_ksteps(const CgLds<128>& L, int buf, CgA
 
 // K-tiles [t0, t1) of the X GEMM (of T in all) with the tile roles SK / DB fixed at compile time: tile t + 1's global
 // loads are in flight during tile t's MFMAs and its LDS stores issue behind the first CG_STAGE_AT k-steps.
+// The code path of wave W: its tile addresses are constants.
 template <int W, unsigned SK, unsigned DB>
 __device__ __forceinline__ void cg_herm_x_range(int t0, int t1, int T, const CgSegA<128>& pa, const CgSegB<128>& pb,
-                                                CgLds<128>& L, CgAcc<128>& acc, int tid, cg_v2* ra, cg_v2* rb) {
+                                                CgLds<128>& L, CgAcc<128>& acc, int wave, int tid, cg_v2* ra,
+                                                cg_v2* rb) {
   constexpr int NLD = cg_nld<128>(), NQ = CG_KT / 4, QS = CG_STAGE_AT < NQ ? CG_STAGE_AT : NQ;
   for (int t = t0; t < t1; ++t) {
     const bool more = (t + 1) < T;
@@ -398,7 +402,7 @@ __device__ __forceinline__ void cg_herm_x_range(int t0, int t1, int T, const CgS
         rb[q] = pb.fetch(t + 1, e, q);
       }
     }
-    cg_herm_ksteps<W, SK, DB, 0, QS>(L, t & 1, acc);
+    cg_herm_ksteps<W, SK, DB, 0, QS>(L, t & 1, acc, wave);
     cg_sched_fence();
     if (more) {
 #pragma unroll
@@ -409,19 +413,19 @@ __device__ __forceinline__ void cg_herm_x_range(int t0, int t1, int T, const CgS
       }
     }
     cg_sched_fence();
-    if constexpr (QS < NQ) cg_herm_ksteps<W, SK, DB, QS, NQ>(L, t & 1, acc);
+    if constexpr (QS < NQ) cg_herm_ksteps<W, SK, DB, QS, NQ>(L, t & 1, acc, wave);
     __syncthreads();
   }
 }
 
 // segs[0] = (A, r), segs[1..nseg-1] = (B_c, W_c); K = the common depth (tps = K / 16 K-tiles per segment).
-// hermitian_part: sum_c B_c W_c is Hermitian (segments >= 1 skip the tiles below the diagonal and double those above
-// it, CgHermLayout); otherwise every tile takes every segment (the plain X GEMM on this layout).  Each wave runs the
+// sum_c B_c W_c must be Hermitian (segments >= 1 skip the tiles below the diagonal and double those above it,
+// CgHermLayout; GLF operands without that property use cg_herm_x_gemm_q's plain X GEMM).  Each wave runs the
 // Hermitian segments with its own compile-time tile roles (one code path per wave for the whole range, so the MFMA
 // stream carries no selects or branches).  All threads call it; ends with a workgroup barrier.  Visit the result with
 // cg_herm_epilogue.
 __device__ __forceinline__ void cg_herm_x_gemm(const CgSeg* segs, int nseg, int K, int lda, int ldb, CgLds<128>& L,
-                                               CgAcc<128>& acc, bool hermitian_part) {
+                                               CgAcc<128>& acc) {
   constexpr int BT = 128, MW = 2, NW = 4;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #pragma unroll
@@ -447,12 +451,8 @@ __device__ __forceinline__ void cg_herm_x_gemm(const CgSeg* segs, int nseg, int 
   __syncthreads();
   auto run = [&](auto wc) {
     constexpr int W = decltype(wc)::value;
-    if (!hermitian_part) {
-      cg_herm_x_range<W, 0u, 0u>(0, T, T, pa, pb, L, acc, tid, ra, rb);
-      return;
-    }
-    cg_herm_x_range<W, 0u, 0u>(0, tps, T, pa, pb, L, acc, tid, ra, rb);
-    cg_herm_x_range<W, cg_herm_mask(W, true), cg_herm_mask(W, false)>(tps, T, T, pa, pb, L, acc, tid, ra, rb);
+    cg_herm_x_range<W, 0u, 0u>(0, tps, T, pa, pb, L, acc, wave, tid, ra, rb);
+    cg_herm_x_range<W, cg_herm_mask(W, true), cg_herm_mask(W, false)>(tps, T, T, pa, pb, L, acc, wave, tid, ra, rb);
   };
 #define QD_HT(w) \
   case w: run(std::integral_constant<int, w>{}); break;
@@ -475,6 +475,135 @@ __device__ __forceinline__ void cg_herm_epilogue(const CgAcc<128>& acc, F&& f) {
       for (int nj = 0; nj < 4; ++nj) {
         const int row = CgHermLayout::row0(wave, mi) + (lane >> 4) + 4 * r;
         const int col = CgHermLayout::col0(wave, nj) + (lane & 15);
+        f(row, col, cmk(acc.re[mi][nj][r], acc.im[mi][nj][r]));
+      }
+}
+
+// Quadrant layout (the Redfield GLF operands, no Hermitian segment; and the round-2 first version of the Lindblad
+// skip).  Hermitian right-hand side.  Only k on the upper blocks is used, and B W (= C r C^+ / 2) is itself Hermitian,
+// so segment 1 need not reach the lower-left 64 x 64 block (1, 0): there X = A r alone, and the upper-right
+// block (0, 1) takes the full C r C^+ instead of its half (A fragment doubled: 2 a x b / 2 is exact), so that
+// k_ij = X_ij + conj(X_ji) = (A r)_ij + conj((A r)_ji) + (C r C^+)_ij on the off-diagonal blocks and as before on
+// the diagonal ones.  The wave -> tile layout spreads block (1, 0) over every wave (each owns row tiles i and 4 + i
+// and column tiles {2h, 2h+1, 4+2h, 5+2h}, i = wave / 2, h = wave % 2), so skipping its tiles in segment 1 takes
+// 2 of 8 tiles from every wave alike: 1/4 of segment 1's MFMAs, 1/12 of a stage's.
+struct CgHermLayoutQ {
+  static __device__ __forceinline__ int row0(int wave, int mi) { return mi * 64 + (wave >> 1) * 16; }
+  static __device__ __forceinline__ int col0(int wave, int nj) { return (nj >> 1) * 64 + (2 * (wave & 1) + (nj & 1)) * 16; }
+};
+
+template <typename Mid>
+__device__ __forceinline__ void cg_herm_compute_tile_q(const CgLds<128>& L, int buf, CgAcc<128>& acc, int wave, bool seg1,
+                                                     Mid mid) {
+  constexpr int BT = 128, MW = 2, NW = 4, NQ = CG_KT / 4;
+  const int lane = threadIdx.x & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    if (q == CG_STAGE_AT) {
+      cg_sched_fence();
+      mid();
+      cg_sched_fence();
+    }
+    const int kk = 4 * q;
+    c128 a[MW], b[NW];
+#pragma unroll
+    for (int mi = 0; mi < MW; ++mi) a[mi] = L.a[buf][(CgHermLayoutQ::row0(wave, mi) + lr) * CG_SA + kk + lk];
+#pragma unroll
+    for (int nj = 0; nj < NW; ++nj) b[nj] = L.b[buf][(kk + lk) * BT + CgHermLayoutQ::col0(wave, nj) + lr];
+    // block (0, 1) in the Hermitian segments: the doubled fragment (exact); a[0] itself elsewhere
+    const double s2 = seg1 ? 2.0 : 1.0;
+    const c128 a2 = cmk(a[0].re * s2, a[0].im * s2);
+#pragma unroll
+    for (int mi = 0; mi < MW; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < NW; ++nj) {
+        if (mi == 1 && nj < 2 && seg1) continue;   // block (1, 0): no Hermitian part
+        const c128& av = (mi == 0 && nj >= 2) ? a2 : a[mi];
+        acc.re[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.re, b[nj].re, acc.re[mi][nj], 0, 0, 0);
+        acc.im[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.re, b[nj].im, acc.im[mi][nj], 0, 0, 0);
+      }
+#pragma unroll
+    for (int mi = 0; mi < MW; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < NW; ++nj) {
+        if (mi == 1 && nj < 2 && seg1) continue;
+        const c128& av = (mi == 0 && nj >= 2) ? a2 : a[mi];
+        acc.re[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av.im, b[nj].im, acc.re[mi][nj], 0, 0, 0);
+        acc.im[mi][nj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.im, b[nj].re, acc.im[mi][nj], 0, 0, 0);
+      }
+  }
+  if (CG_STAGE_AT >= NQ) {
+    cg_sched_fence();
+    mid();
+  }
+}
+
+// segs[0] = (A, r), segs[1..nseg-1] = (B_c, W_c); K = the common depth (tps = K / 16 K-tiles per segment).
+// hermitian_part: sum_c B_c W_c is Hermitian (segments >= 1 skip block (1, 0) and double block (0, 1)); otherwise
+// every tile takes every segment (the plain X GEMM on this layout).  All threads call it; ends with a workgroup
+// barrier.  Visit the result with cg_herm_epilogue_q.
+__device__ __forceinline__ void cg_herm_x_gemm_q(const CgSeg* segs, int nseg, int K, int lda, int ldb, CgLds<128>& L,
+                                               CgAcc<128>& acc, bool hermitian_part) {
+  constexpr int BT = 128, MW = 2, NW = 4;
+  const int wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int mi = 0; mi < MW; ++mi)
+#pragma unroll
+    for (int nj = 0; nj < NW; ++nj) {
+      acc.re[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
+      acc.im[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
+    }
+  const int tps = K / CG_KT, T = nseg * tps;
+  CgSegA<BT> pa{segs, tps, lda};
+  CgSegB<BT> pb{segs, tps, ldb};
+  constexpr int NLD = cg_nld<BT>();
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  cg_v2 ra[NLD], rb[NLD];
+  auto load = [&](int t) {
+#pragma unroll
+    for (int q = 0; q < NLD; ++q) {
+      const int e = tid + CG_WG * q;
+      ra[q] = pa.fetch(t, e, q);
+      rb[q] = pb.fetch(t, e, q);
+    }
+  };
+  auto store = [&](int t, int buf) {
+#pragma unroll
+    for (int q = 0; q < NLD; ++q) {
+      const int e = tid + CG_WG * q;
+      cg_st_lds(&L.a[buf][(e >> 4) * CG_SA + (e & 15)], ra[q]);
+      cg_st_lds(&L.b[buf][e], rb[q]);
+    }
+  };
+  load(0);
+  store(0, 0);
+  __syncthreads();
+  for (int t = 0; t < T; ++t) {
+    const bool more = (t + 1) < T;
+    if (more) load(t + 1);
+    auto mid = [&]() {
+      if (more) store(t + 1, (t + 1) & 1);
+    };
+    cg_herm_compute_tile_q(L, t & 1, acc, wave, hermitian_part && t >= tps, mid);
+    __syncthreads();
+  }
+}
+
+template <typename F>
+__device__ __forceinline__ void cg_herm_epilogue_q(const CgAcc<128>& acc, F&& f) {
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const int wave = tid >> 6, lane = tid & 63;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int nj = 0; nj < 4; ++nj) {
+        const int row = CgHermLayoutQ::row0(wave, mi) + (lane >> 4) + 4 * r;
+        const int col = CgHermLayoutQ::col0(wave, nj) + (lane & 15);
         f(row, col, cmk(acc.re[mi][nj][r], acc.im[mi][nj][r]));
       }
 }

@@ -129,7 +129,9 @@ __device__ void wg_observables(const c128* rho, const c128* eT, int ne, size_t N
 #define GLF_HERM_PIPE false   // fragment double-buffering in the Hermitian kernel's GEMMs (A/B builds)
 #endif
 
-template <int BT, bool HERM>
+// HSEG (Hermitian kernel only): sum_c L_c r W_c is itself Hermitian (Lindblad C r C^+ / 2), so the X GEMM skips its
+// tiles below the diagonal (cg_herm_x_gemm); without it (Redfield's GLF operands) the plain X GEMM (cg_herm_x_gemm_q).
+template <int BT, bool HERM, bool HSEG = false>
 __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
   __shared__ CgLds<BT> L;
   __shared__ c128 sred[CG_WG / 64];
@@ -214,11 +216,13 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
           }
         }
         __syncthreads();
-        constexpr bool HX = BT == 128 && GLF_HERM_X;   // lower-left block without the Hermitian part (cgemm_block.hpp)
-        if constexpr (HX) cg_herm_x_gemm(segs, 1 + nc, Np, Np, Np, L, A, p.hseg != 0);
+        constexpr bool HX = BT == 128 && GLF_HERM_X;   // tiles without the Hermitian part (cgemm_block.hpp)
+        if constexpr (HX && HSEG) cg_herm_x_gemm(segs, 1 + nc, Np, Np, Np, L, A);
+        else if constexpr (HX) cg_herm_x_gemm_q(segs, 1 + nc, Np, Np, Np, L, A, false);
         else cg_block_gemm<BT, GLF_HERM_PIPE>(segs, 1 + nc, Np, Np, Np, L, A);
         auto visit = [&](auto&& f) {
-          if constexpr (HX) cg_herm_epilogue(A, f);
+          if constexpr (HX && HSEG) cg_herm_epilogue(A, f);
+          else if constexpr (HX) cg_herm_epilogue_q(A, f);
           else cg_epilogue<BT>(A, f);
         };
         QD_TMARK(2);
@@ -1073,7 +1077,8 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
       if (herm) hipLaunchKernelGGL((lindblad_rk4_kernel<64, true>), dim3(B), dim3(CG_WG), 0, st, p);
       else hipLaunchKernelGGL((lindblad_rk4_kernel<64, false>), dim3(B), dim3(CG_WG), 0, st, p);
     } else {
-      if (herm) hipLaunchKernelGGL((lindblad_rk4_kernel<128, true>), dim3(B), dim3(CG_WG), 0, st, p);
+      if (herm && p.hseg) hipLaunchKernelGGL((lindblad_rk4_kernel<128, true, true>), dim3(B), dim3(CG_WG), 0, st, p);
+      else if (herm) hipLaunchKernelGGL((lindblad_rk4_kernel<128, true>), dim3(B), dim3(CG_WG), 0, st, p);
       else hipLaunchKernelGGL((lindblad_rk4_kernel<128, false>), dim3(B), dim3(CG_WG), 0, st, p);
     }
     QD_HIP(hipGetLastError());
