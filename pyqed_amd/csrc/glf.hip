@@ -123,7 +123,7 @@ __device__ void wg_observables(const c128* rho, const c128* eT, int ne, size_t N
 }
 
 #ifndef GLF_HERM_X
-#define GLF_HERM_X 1   // Hermitian kernel at BT = 128: X GEMM without the Hermitian part on block (1, 0) (A/B: 0)
+#define GLF_HERM_X 1   // Hermitian kernel at BT = 128: X GEMM on the CgHermLayout tiles (Lindblad: no Hermitian part below the diagonal; A/B: 0)
 #endif
 #ifndef GLF_HERM_PIPE
 #define GLF_HERM_PIPE false   // fragment double-buffering in the Hermitian kernel's GEMMs (A/B builds)
