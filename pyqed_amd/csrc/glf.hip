@@ -51,7 +51,7 @@ struct LindbladParams {
   int step0, total_steps;  // this launch runs global steps step0 .. step0+nsteps-1 of total_steps
   int herm;                // Hermitian fast path (Lindblad, rho exactly Hermitian, single block)
   int hseg;                // Hermitian path: sum_c L_c r W_c is itself Hermitian (Lindblad C r C^+ / 2; not Redfield's
-                           // sum A r Lam^+), so its redundant lower-left block may be skipped (cg_herm_x_gemm)
+                           // sum A r Lam^+), so its redundant tiles below the diagonal may be skipped (cg_herm_x_gemm)
   double dt;
   unsigned long long* tbuf;  // [B][8] per-phase wall-clock ticks (QD_PHASE_TIMING diagnostics) or null
   unsigned long long stagger;  // start offset (wall-clock ticks) of the odd workgroup group of each XCD
