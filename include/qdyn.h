@@ -8,8 +8,10 @@
  *     (qd_c128, byte-identical to numpy/torch complex128);
  *   - matrices are row-major and contiguous; vec(rho) is row-major
  *     (rho.flatten(), reference pyqed/superoperator.py:125-150);
- *   - the caller owns every buffer it passes; the library only keeps internal
- *     workspaces (released by qd_shutdown);
+ *   - the caller owns every buffer it passes; the library's own scratch is
+ *     call-scoped (stream-ordered hipMallocAsync / hipFreeAsync from the device's
+ *     default memory pool, released when the entry point returns; the pool keeps
+ *     it reserved until qd_shutdown trims it);
  *   - calls are asynchronous on `stream` (a hipStream_t, NULL = default stream);
  *   - return 0 on success, a negative QD_E* code on failure; the message is
  *     available from qd_last_error() (thread-local).
@@ -46,8 +48,12 @@ int qd_version(void);                 /* e.g. 100 = 0.1.0                      *
 const char* qd_last_error(void);      /* thread-local message of last failure */
 int qd_init(int device);              /* hipSetDevice + warm-up               */
 int qd_device_count(int* count);      /* host pointer                         */
-int qd_shutdown(void);                /* frees cached workspaces              */
+int qd_shutdown(void);                /* trims the scratch memory pools       */
 int qd_synchronize(void* stream);     /* hipStreamSynchronize                 */
+/* Current device's scratch pool: bytes reserved and bytes in use (host pointers).
+ * In use returns to 0 once every stream that called the library has drained;
+ * reserved is bounded by the peak concurrent scratch, not by the number of streams. */
+int qd_workspace_stats(size_t* reserved, size_t* used);
 
 /* ------------------------------------------------------------ Lindblad --- */
 /*

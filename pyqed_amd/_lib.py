@@ -36,6 +36,7 @@ SIGNATURES = {
     "qd_device_count": (c_int, [ctypes.POINTER(c_int)]),
     "qd_shutdown": (c_int, []),
     "qd_synchronize": (c_int, [c_void_p]),
+    "qd_workspace_stats": (c_int, [ctypes.POINTER(c_size_t), ctypes.POINTER(c_size_t)]),
     "qd_lindblad_rk4": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_double, c_int,
                                 c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "qd_lindblad_rk4_herm": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_double, c_int,

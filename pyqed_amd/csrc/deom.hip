@@ -702,6 +702,7 @@ int deom_run(qd_c128* ados, int B, int nmax, int K, int ns, const int32_t* minus
              const qd_c128* Hdip, const qd_c128* Q, const qd_c128* Qdip, const qd_c128* fsys, const qd_c128* fcoup,
              double dt, int nsteps, qd_c128* rho_sys, const qd_c128* E, int ne, qd_c128* trace, void* stream,
              int bminor) {
+  WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   QD_CHECK_ARG(ados && minus && plus && coef && damp && mode && H && Q, "qd_deom_rk4: null pointer");
   QD_CHECK_ARG(B >= 1 && nmax >= 1 && K >= 1 && nsteps >= 0, "qd_deom_rk4: bad sizes B=%d nmax=%d K=%d", B, nmax, K);
   QD_CHECK_ARG(ns >= 1 && ns <= DEOM_MAX_NS, "qd_deom_rk4: ns=%d outside [1, %d]", ns, DEOM_MAX_NS);
@@ -875,6 +876,7 @@ extern "C" int qd_deom_trace(const qd_c128* snap, const qd_c128* E, int ne, int 
 extern "C" int qd_heom_chain_euler(qd_c128* ados, int B, int nado, int ns, const qd_c128* H, const qd_c128* Q,
                                    double gamma, double D0_re, double D0_im, double dt, int nsteps, qd_c128* rho_sys,
                                    const qd_c128* E, int ne, qd_c128* obs, void* stream) {
+  WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   QD_CHECK_ARG(ados && H && Q, "qd_heom_chain_euler: null pointer");
   QD_CHECK_ARG(B >= 1 && nado >= 2 && nsteps >= 0, "qd_heom_chain_euler: bad sizes B=%d nado=%d", B, nado);
   QD_CHECK_ARG(ns >= 1 && ns <= 16, "qd_heom_chain_euler: ns=%d outside [1, 16]", ns);

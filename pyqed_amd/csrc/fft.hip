@@ -146,6 +146,7 @@ using namespace qd;
 
 extern "C" int qd_fft_axis(qd_c128* data, int outer, int n, int inner, int inverse, int shift, double scale,
                            const double* freq, double x0, void* stream) {
+  WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   QD_CHECK_ARG(data, "qd_fft_axis: null pointer");
   QD_CHECK_ARG(outer >= 1 && inner >= 1 && n >= 1, "qd_fft_axis: bad sizes");
   QD_CHECK_ARG((long)outer * inner < (1L << 31), "qd_fft_axis: batch too large");

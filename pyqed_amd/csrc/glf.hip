@@ -879,6 +879,7 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
             const c128* Rop, int nc, c128* rho, int B, int N, double dt, int nsteps, const c128* E, int ne,
             c128* obs, c128* snap, int save_every, hipStream_t st, const c128* Hd = nullptr, int nd = 0,
             const qd_c128* fvals = nullptr, int herm = 0) {
+  WsScope wss_(st);  // call-scoped scratch (qd_runtime.hip)
   const int Np = padded_dim(N);
   const size_t NN = (size_t)Np * Np;
   // operator workspace: Cop(L), mK(P), iKd(Q), Cd(R), eT, [P0, Q0, f scratch for driven runs]
@@ -927,7 +928,7 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
     // 64-blocks are no better overall (172k / 231k / 232k / 247k).  QD_GLF_HSPLIT_MAX / _BT override (A/B).
     const char* hme = std::getenv("QD_GLF_HSPLIT_MAX");
     const int hmax = hme ? std::atoi(hme) : 208;
-    if (herm && src == GLF_FROM_LINDBLAD && Np >= 64 && Np <= 128 && B < hmax && !(hse && hse[0] == '0')) {
+    if (herm && src == GLF_FROM_LINDBLAD && Np == 128 && B < hmax && !(hse && hse[0] == '0')) {
       hsplit = true;
       split_bt = 32;
       if (const char* e = std::getenv("QD_GLF_HSPLIT_BT")) split_bt = std::atoi(e) == 64 && Np % 64 == 0 ? 64 : 32;
@@ -1197,6 +1198,7 @@ extern "C" int qd_glf_rk4_herm(const qd_c128* P, const qd_c128* L, const qd_c128
 namespace {
 // shared driver: A[b] <- Vl A[b] Vr for b < B; mode 0/1 = V^+ . V / V . V^+, mode 2 = L . R
 int sandwich_run(const c128* V, const c128* Lm, const c128* Rm, c128* A, int B, int N, int mode, hipStream_t st) {
+  WsScope wss_(st);  // call-scoped scratch (qd_runtime.hip)
   const int Np = padded_dim(N);
   const size_t NN = (size_t)Np * Np;
   const bool pad = Np != N;

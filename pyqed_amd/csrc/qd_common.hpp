@@ -39,16 +39,25 @@ void set_error(const char* fmt, ...);
     }                                                                       \
   } while (0)
 
-// Growable scratch owned by the library (freed by qd_shutdown), never handed to the caller.
-// Keyed by (device, stream, slot): calls on distinct streams never share scratch, so the library is
-// re-entrant for distinct streams (SURVEY.md §8(b) threading contract).  Buffers are allocated and
-// released stream-ordered (hipMallocAsync / hipFreeAsync on `st`), so growing one stream's buffer
-// never waits on, or frees memory still queued on, any other stream.  Concurrent calls on the SAME
-// stream from different host threads are not supported (their scratch would alias).
+// Library-owned scratch, never handed to the caller (qd_runtime.hip).  Every entry point that needs
+// scratch opens a WsScope on its stream; workspace() then returns a fresh stream-ordered allocation
+// (hipMallocAsync on `st`, default memory pool with a max release threshold) that the scope releases
+// with hipFreeAsync on the same stream when the entry point returns.  Distinct streams / host threads
+// never share live scratch (SURVEY.md §8(b) threading contract), and the pool's reserved memory is
+// bounded by the peak concurrent use, not by the number of streams seen (qd_workspace_stats).
 enum WsSlot { WS_LINDBLAD = 0, WS_LINDBLAD_OPS = 1, WS_SPO = 2, WS_DEOM = 3,
               WS_SUPEROP = 4, WS_2DES = 5, WS_MISC = 6, WS_2DES_OPS = 7, WS_TDSE_H = 8,
               WS_TDSE_GEMM = 9, WS_SUPEROP_OPS = 10, WS_NSLOTS = 11 };
+struct WsScope {
+  hipStream_t st;
+  size_t mark;
+  explicit WsScope(hipStream_t s);
+  ~WsScope();
+  WsScope(const WsScope&) = delete;
+  WsScope& operator=(const WsScope&) = delete;
+};
 int workspace(WsSlot slot, size_t bytes, void** ptr, hipStream_t st);
+int pool_stats(size_t* reserved, size_t* used);
 void free_workspaces();
 
 // ---------------------------------------------------------------- complex

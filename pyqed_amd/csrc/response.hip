@@ -713,6 +713,7 @@ extern "C" int qd_sos_propagator(const qd_c128* U1, const qd_c128* U2, const qd_
 extern "C" int qd_response_cube(const qd_c128* alpha, const qd_c128* B, const qd_c128* C, const qd_c128* beta,
                                 const qd_c128* lam, int nL, const double* t3, int n3, const double* t2, int n2,
                                 const double* t1, int n1, qd_c128* out, void* stream) {
+  WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   QD_CHECK_ARG(alpha && B && C && beta && lam && t3 && t2 && t1 && out, "qd_response_cube: null pointer");
   QD_CHECK_ARG(nL >= 1 && nL <= 4096 && n3 >= 1 && n2 >= 1 && n1 >= 1, "qd_response_cube: bad sizes");
   hipStream_t st = (hipStream_t)stream;
@@ -744,6 +745,7 @@ int ens_run(const char* fn, const qd_c128* alpha, const qd_c128* Mt, const qd_c1
             int nL, const double* t3, double t3_0, double dt3, int n3, const double* t1, double t1_0, double dt1,
             int n1, qd_c128* out, int accumulate, void* stream, int nz = 0, const qd_c128* lamz_ = nullptr,
             int trans = 0) {
+  WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   if (nz == 0) nz = nL;
   const c128* lamz = (const c128*)(lamz_ ? lamz_ : lam);
   QD_CHECK_ARG(alpha && Mt && beta && lam && out, "%s: null pointer", fn);
@@ -945,6 +947,7 @@ extern "C" int qd_response2d_t2_operands(const qd_c128* alpha, const qd_c128* Bm
 
 extern "C" int qd_response2d_t2_apply(const qd_c128* P, const qd_c128* Q, const qd_c128* lam, int M, int nL, int n3,
                                       int n1, const double* t2, int n2, qd_c128* out, int accumulate, void* stream) {
+  WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   const char* fn = "qd_response2d_t2_apply";
   QD_CHECK_ARG(P && Q && lam && t2 && out, "%s: null pointer", fn);
   QD_CHECK_ARG(M >= 1 && nL >= 1 && n3 >= 1 && n1 >= 1 && n2 >= 1 && n2 <= 65535, "%s: bad sizes", fn);
@@ -975,6 +978,7 @@ extern "C" int qd_response2d_t2scan(const qd_c128* alpha, const qd_c128* Bm, con
                                     const qd_c128* lam, int M, int nL, double t3_0, double dt3, int n3,
                                     const double* t2, int n2, double t1_0, double dt1, int n1, qd_c128* out,
                                     int accumulate, void* stream) {
+  WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   const char* fn = "qd_response2d_t2scan";
   QD_CHECK_ARG(alpha && Bm && Cm && beta && lam && t2 && out, "%s: null pointer", fn);
   QD_CHECK_ARG(M >= 1 && nL >= 1 && n3 >= 1 && n1 >= 1 && n2 >= 1, "%s: bad sizes", fn);
@@ -1030,6 +1034,7 @@ int qd::cgemm_splitk_slabs(const c128* A, const c128* B, int Mp, int Kp, int Np,
 
 extern "C" int qd_resolvent_grid2d(const qd_c128* a, const qd_c128* M, const qd_c128* v, const qd_c128* lam, int n,
                                    const double* wx, int nx, const double* wy, int ny, qd_c128* out, void* stream) {
+  WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   const char* fn = "qd_resolvent_grid2d";
   QD_CHECK_ARG(a && M && v && lam && wx && wy && out, "%s: null pointer", fn);
   QD_CHECK_ARG(n >= 1 && nx >= 1 && ny >= 1 && n <= 65536 && nx <= 65536 && ny <= 65536, "%s: bad sizes", fn);

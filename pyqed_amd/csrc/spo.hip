@@ -1256,6 +1256,7 @@ using namespace qd;
 extern "C" int qd_spo2_run_ex(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* expV_, const qd_c128* expK_,
                               const qd_c128* expKy_, int nx, int ny, int ns, int nsteps, int nout, qd_c128* snap_,
                               void* stream) {
+  WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   QD_CHECK_ARG(psi_ && expVh_ && expK_, "qd_spo2_run_ex: null pointer");
   QD_CHECK_ARG(pow2_in_range(nx) && pow2_in_range(ny), "qd_spo2_run_ex: nx=%d, ny=%d must be powers of 2 in [16, 1024]",
                nx, ny);
@@ -1346,6 +1347,7 @@ extern "C" int qd_spo2_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
 
 extern "C" int qd_spo2_run_batch(qd_c128* psi_, int B, const qd_c128* expVh_, const qd_c128* expK_, int nx, int ny,
                                  int ns, int nsteps, int nout, qd_c128* snap_, void* stream) {
+  WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   QD_CHECK_ARG(psi_ && expVh_ && expK_, "qd_spo2_run_batch: null pointer");
   QD_CHECK_ARG(B >= 1 && B <= 65535, "qd_spo2_run_batch: B=%d outside [1, 65535]", B);
   QD_CHECK_ARG(nsteps >= 0 && nout >= 1, "qd_spo2_run_batch: nsteps=%d nout=%d", nsteps, nout);
@@ -1444,6 +1446,7 @@ extern "C" int qd_spo2_run_batch(qd_c128* psi_, int B, const qd_c128* expVh_, co
 
 extern "C" int qd_spo1d_run(qd_c128* psi_, const qd_c128* expV_, const qd_c128* expVh_, const qd_c128* expK_, int nx,
                             int B, int nt, int nout, qd_c128* snap_, void* stream) {
+  WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   QD_CHECK_ARG(psi_ && expV_ && expVh_ && expK_, "qd_spo1d_run: null pointer");
   QD_CHECK_ARG(pow2_in_range(nx), "qd_spo1d_run: nx=%d must be a power of 2 in [16, 1024]", nx);
   QD_CHECK_ARG(B >= 1 && nt >= 0 && nout >= 1, "qd_spo1d_run: B=%d nt=%d nout=%d", B, nt, nout);
@@ -1465,6 +1468,7 @@ extern "C" int qd_spo1d_run(qd_c128* psi_, const qd_c128* expV_, const qd_c128* 
 
 extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* expK_, int nx, int ny, int nz, int ns,
                            int nsteps, int nout, qd_c128* snap_, void* stream) {
+  WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   QD_CHECK_ARG(psi_ && expVh_ && expK_, "qd_spo3_run: null pointer");
   QD_CHECK_ARG(pow2_in_range(nx) && pow2_in_range(ny) && pow2_in_range(nz) && nx <= 256 && ny <= 256 && nz <= 256,
                "qd_spo3_run: nx, ny, nz must be powers of 2 in [16, 256]");

@@ -245,6 +245,7 @@ int launch_rows(int nb, const c128* L, int N2, const c128* xin, c128* xo, c128* 
 // per stage for the whole batch; below the threshold the VALU GEMV streams L once per group of <= 8 vectors.
 extern "C" int qd_superop_rk4(const qd_c128* L_, qd_c128* v_, int B, int N2, double dt, int nsteps, const qd_c128* W_,
                               int ne, qd_c128* obs_, qd_c128* snap_, int save_every, void* stream) {
+  WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   QD_CHECK_ARG(L_ && v_, "qd_superop_rk4: null pointer");
   QD_CHECK_ARG(B >= 1 && N2 >= 1 && nsteps >= 0, "qd_superop_rk4: bad sizes B=%d N2=%d", B, N2);
   QD_CHECK_ARG(ne == 0 || (W_ && obs_), "qd_superop_rk4: W/obs null but ne=%d", ne);
@@ -345,6 +346,7 @@ extern "C" int qd_superop_from_glf(const qd_c128* P, const qd_c128* Q, const qd_
 
 // Dense Lindblad superoperator (oqs.liouvillian as a matrix on row-major vec(rho)), [N^2][N^2] into `out`.
 extern "C" int qd_superop_lindblad(const qd_c128* H, const qd_c128* C, int nc, int N, qd_c128* out, void* stream) {
+  WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   QD_CHECK_ARG(H && out && (nc == 0 || C), "qd_superop_lindblad: null pointer");
   QD_CHECK_ARG(N >= 1 && N <= 512 && nc >= 0, "qd_superop_lindblad: bad sizes N=%d nc=%d", N, nc);
   hipStream_t st = (hipStream_t)stream;

@@ -333,6 +333,7 @@ int tdse_gemm_steps(const c128* H, c128* psi, int B, int N, double dt, int nstep
 
 int tdse_rows_run(const c128* H, c128* psi, int B, int N, double dt, int nsteps, int save_every, c128* snap,
                   const c128* E, int ne, c128* obs, hipStream_t st, int save0 = 0, int nsave_total = -1) {
+  WsScope wss_(st);  // call-scoped scratch (qd_runtime.hip)
   const int nsave = nsave_total >= 0 ? nsave_total : (save_every > 0 ? nsteps / save_every : 0);
   void* w = nullptr;
   const size_t ws_elems = (size_t)B * 3 * N + (size_t)B * (ne ? ne : 0) * N;
@@ -392,6 +393,7 @@ int tdse_rows_run(const c128* H, c128* psi, int B, int N, double dt, int nsteps,
 
 int tdse_gemm_steps(const c128* H, c128* psi, int B, int N, double dt, int nsteps, hipStream_t st, int save_every,
                     const std::function<int(int)>& at_step) {
+  WsScope wss_(st);  // call-scoped scratch (qd_runtime.hip)
   const int Bp = ceil_div(B, 128) * 128, Np = ceil_div(N, 128) * 128;
   const size_t NN = (size_t)Np * Np, BN = (size_t)Bp * Np;
   constexpr int MAXS = 16;
@@ -435,6 +437,7 @@ using namespace qd;
 
 extern "C" int qd_tdse_rk4(const qd_c128* H, qd_c128* psi, int B, int N, double dt, int nsteps, int save_every,
                            qd_c128* snap, const qd_c128* E, int ne, qd_c128* obs, void* stream) {
+  WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   QD_CHECK_ARG(H && psi, "qd_tdse_rk4: null pointer");
   QD_CHECK_ARG(N >= 1 && B >= 1 && nsteps >= 0, "qd_tdse_rk4: bad sizes N=%d B=%d", N, B);
   QD_CHECK_ARG(ne >= 0 && (ne == 0 || (E && obs)), "qd_tdse_rk4: E/obs null but ne=%d", ne);
@@ -469,6 +472,7 @@ extern "C" int qd_tdse_rk4(const qd_c128* H, qd_c128* psi, int B, int N, double 
 extern "C" int qd_tdse_driven_rk4(const qd_c128* H0, const qd_c128* Hd, int nd, const qd_c128* fvals, qd_c128* psi,
                                   int B, int N, double dt, int nblocks, int nout, qd_c128* snap, const qd_c128* E,
                                   int ne, qd_c128* obs, void* stream) {
+  WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   QD_CHECK_ARG(H0 && psi && (nd == 0 || (Hd && fvals)), "qd_tdse_driven_rk4: null pointer");
   QD_CHECK_ARG(N >= 1 && B >= 1 && nblocks >= 0 && nout >= 1 && nd >= 0 && nd <= 16,
                "qd_tdse_driven_rk4: bad sizes N=%d B=%d nblocks=%d nout=%d nd=%d", N, B, nblocks, nout, nd);

@@ -162,14 +162,19 @@ class TorchExchange:
     def __init__(self, group=None):
         self.group = group
 
+    def _peer(self, q):
+        """Band q is group rank q; P2POp takes global ranks."""
+        import torch.distributed as dist
+        return q if self.group is None else dist.get_global_rank(self.group, q)
+
     def __call__(self, bands, name):
         import torch.distributed as dist
         (b,) = bands
         ops = []
         for q in sorted(b.plan.send):
-            ops.append(dist.P2POp(dist.isend, b.pack(name, q), q, group=self.group))
+            ops.append(dist.P2POp(dist.isend, b.pack(name, q), self._peer(q), group=self.group))
         for q in sorted(b.plan.recv):
-            ops.append(dist.P2POp(dist.irecv, b.halo_view(name, q), q, group=self.group))
+            ops.append(dist.P2POp(dist.irecv, b.halo_view(name, q), self._peer(q), group=self.group))
         if ops:
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
@@ -220,6 +225,9 @@ class ShardedDEOM:
         solver.init_()
         self.solver = solver
         rank, ws = world()
+        if group is not None:  # bands are numbered by the rank within `group`
+            import torch.distributed as dist
+            rank, ws = dist.get_rank(group), dist.get_world_size(group)
         self.loopback = (ws == 1) if loopback is None else loopback
         self.rank = 0 if self.loopback else rank
         self.nbands = (nbands or 2) if self.loopback else ws
@@ -267,7 +275,8 @@ class ShardedDEOM:
         if not self.loopback and self.nbands > 1:
             import torch.distributed as dist
             got = [None] * self.nbands if self.rank == 0 else None
-            dist.gather_object(own, got, dst=0, group=self.group)
+            dst = 0 if self.group is None else dist.get_global_rank(self.group, 0)
+            dist.gather_object(own, got, dst=dst, group=self.group)
             if self.rank != 0:
                 return None
             own = [x for part in got for x in part]

@@ -121,3 +121,65 @@ def test_spo2_256_matches_reference():
     dx = x[1] - x[0]
     pops = np.array([[np.vdot(p[:, :, k], p[:, :, k]).real * dx * dx for k in range(2)] for p in r.psilist])
     assert relerr(pops, g["populations"]) < TOL
+
+
+@pytest.mark.gpu
+def test_redfield_n128_bench_kernel_batch256_matches_reference():
+    """the bench's Redfield kernel itself (qd_glf_rk4_herm, persistent Hermitian kernel, B = 256,
+    N = 128, bench.py bench_redfield) pinned to the reference fixture: member 0 is the fixture's rho0 in the H
+    eigenbasis, members 1..255 seeded pure states.  Member 0's observables Tr(e~ rho~) and its back-transformed final
+    state must equal RedfieldSolver.evolve's reference outputs (oqs.py:364-459); member 255 is checked against a
+    dense NumPy restatement of the same RHS (X + X^+, X = P rho + sum A rho Lam^+) built with oracle.lindblad.rk4."""
+    import torch
+    from oracle import lindblad as olb
+    from pyqed_amd import RedfieldSolver
+    from pyqed_amd.oqs import glf_rk4
+    g = load_golden("redfield_n128")
+    sol = RedfieldSolver(g["H"], c_ops=[g["a_op"]], spectra=[SPECTRA[str(g["spectrum"])]])
+    sol.redfield_tensor()
+    P, Ls, Ws = sol.glf_terms_herm()
+    V = sol.evecs.astype(complex)
+    N, Nt, dt, B = 128, int(g["Nt"]), float(g["dt"]), 256
+    r0 = V.conj().T @ g["rho0"] @ V
+    r0 = 0.5 * (r0 + r0.conj().T)
+    rho = np.concatenate([r0[None], olb.random_pure_states(B - 1, N, seed=11)])
+    E = np.array([V.conj().T @ e @ V for e in g["E"]])
+    dev = torch.device("cuda", 0)
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(np.asarray(x, complex))).to(dev)
+    rd = t(rho)
+    obs, _ = glf_rk4(t(P), None, t(Ls), t(Ws), rd, dt, Nt, t(E), hermitian=True)
+    assert relerr(obs[0, 1:].cpu().numpy(), g["observables"]) < TOL
+    out = rd.cpu().numpy()
+    assert relerr(V @ out[0] @ V.conj().T, g["rho_final"]) < TOL
+
+    def rhs(r):
+        X = P @ r + sum(a @ r @ w for a, w in zip(Ls, Ws))
+        return X + X.conj().T
+
+    ref = rho[-1].copy()
+    for _ in range(Nt):
+        ref = olb.rk4(ref, lambda r, *a: rhs(r), dt)
+    assert relerr(out[-1], ref) < TOL
+
+
+@pytest.mark.gpu
+def test_2des_256_t2scan_matches_reference():
+    """the bench's waiting-time scan (T2Scan operands + bucketed apply, bench.py
+    bench_2des_t2scan) at the benchmarked 256 x 256 grid against the reference's correlation_4op_3t slices at
+    t2 = tau[0] and tau[37] (corr4_2des_256), member by member and summed over members."""
+    from pyqed_amd.response import T2Scan, ensemble_factors_bc, response2d_t2scan
+    g = load_golden("corr4_2des_256")
+    tau = g["tau"]
+    lam, U1, U2, ops, rho0 = _two_des_members(g)
+    alpha, Bm, Cm, beta = ensemble_factors_bc(lam, U1, U2, ops, rho0.flatten())
+    t2 = np.array([tau[0], tau[37]])
+    tot = 0
+    for m in range(len(g["E"])):
+        S = response2d_t2scan(lam[m:m + 1], alpha[m:m + 1], Bm[m:m + 1], Cm[m:m + 1], beta[m:m + 1], tau, t2,
+                              tau).cpu().numpy()
+        for k, j in enumerate((0, 37)):
+            assert relerr(S[k], g[f"m{m}_j{j}"]) < TOL, (m, j)
+        tot = tot + np.array([g[f"m{m}_j0"], g[f"m{m}_j37"]])
+    sc = T2Scan(lam, alpha, Bm, Cm, beta, tau, tau)
+    S = np.concatenate([sc.apply(t2[:1]).cpu().numpy(), sc.apply(t2[1:]).cpu().numpy()])
+    assert relerr(S, tot) < TOL

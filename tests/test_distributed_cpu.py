@@ -319,3 +319,47 @@ def test_deom_band_plans_properties():
             assert np.array_equal(glob[loc[loc >= 0]], t[t >= 0])
         for q, (s, c) in p.recv.items():
             assert np.array_equal(plans[q].send[p.rank] + plans[q].lo, p.halo[s:s + c])
+
+
+def _worker_deom_bands_subgroup(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sub = dist.new_group([1, 2])       # every rank must take part in new_group
+    if rank in (1, 2):
+        from pyqed_amd.deom_shard import ShardedDEOM
+        sol, *_, rho0 = _deom_model()
+        sh = ShardedDEOM(sol, stage_fn=_host_stage, device="cpu", group=sub)
+        P1 = np.diag([1.0, 0, 0]).astype(complex)
+        t, tr = sh.run(rho0, 0.01, 6, P1)
+        ados = sh.gather_ados()
+        q.put((rank, tr, ados))
+    else:
+        q.put((rank, None, None))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_deom_tier_bands_subgroup_gloo():
+    """ShardedDEOM on a process SUBgroup (global ranks 1, 2 of 3).  Bands are numbered by the rank within
+    the group and peers are mapped to global ranks for the P2P ops and the final gather, so group rank 0 (global
+    rank 1) returns the oracle's Tr(p1 rho_0) and final hierarchy."""
+    from oracle import deom as od
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_deom_bands_subgroup, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sol, bath, H, Qm, sdip, cdip, fs, fc, rho0 = _deom_model()
+    P1 = np.diag([1.0, 0, 0]).astype(complex)
+    _, tr_ref, ados_ref = od.run(H, sdip, fs, np.array([Qm]), cdip, fc, (bath.etal, bath.etar, bath.etaa, bath.expn),
+                                 4, rho0, 0.01, 6, P1)
+    assert res[0][1] is None and res[2][1] is None and res[2][2] is None
+    assert np.allclose(res[1][1], tr_ref, rtol=1e-12, atol=1e-13)
+    assert np.allclose(res[1][2], ados_ref, rtol=1e-11, atol=1e-13)

@@ -396,3 +396,41 @@ def test_lindblad_concurrent_streams_match_oracle():
         torch.cuda.synchronize()
         for k in r0:
             assert relerr(out[k].cpu().numpy()[sel[k]], ref[k]) < TOL, (mode, k)
+
+
+def test_workspace_bounded_over_many_streams():
+    """scratch must not grow with the number of streams a caller uses.  Library scratch is
+    call-scoped (qd_runtime.hip: hipMallocAsync / hipFreeAsync from the device pool), so after 24 calls on 24 fresh
+    streams nothing is in use and the pool's reservation is what one call needs, not 24x that; each call still
+    matches the oracle."""
+    import ctypes
+    import torch
+    from oracle import lindblad as olb
+    from pyqed_amd import lindblad_rk4, _lib
+    N, steps, dt = 64, 3, 1e-2
+    H, cs = olb.synthetic_lindblad(N, nc=1)
+    dev = torch.device("cuda", 0)
+    Ht, Ct = torch.from_numpy(H).to(dev), torch.from_numpy(np.array(cs)).to(dev)
+    r0 = olb.random_pure_states(4, N, seed=9)
+    ref = olb.lindblad_batch(H, cs, r0, dt, steps)
+    lib = _lib.load()
+
+    def stats():
+        res, used = ctypes.c_size_t(0), ctypes.c_size_t(0)
+        _lib.check(lib.qd_workspace_stats(ctypes.byref(res), ctypes.byref(used)), "qd_workspace_stats")
+        return res.value, used.value
+
+    reserved = []
+    for k in range(24):
+        s = torch.cuda.Stream(dev)
+        with torch.cuda.stream(s):
+            rho = torch.from_numpy(r0.copy()).to(dev)
+            lindblad_rk4(Ht, Ct, rho, dt, steps, stream=s.cuda_stream)
+        s.synchronize()
+        assert relerr(rho.cpu().numpy(), ref) < TOL, k
+        res, used = stats()
+        assert used == 0, (k, used)
+        reserved.append(res)
+        del s
+    assert reserved[0] > 0
+    assert max(reserved) <= 2 * reserved[0], reserved
