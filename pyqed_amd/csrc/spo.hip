@@ -1172,6 +1172,12 @@ bool q16_enabled() {
 
 bool pow2_in_range(int n) { return n >= 16 && n <= 1024 && (n & (n - 1)) == 0; }
 
+// QD_SPO_GENERIC=1 routes every grid through spo_gen.hip (A/B and tests of the any-size engine)
+bool force_generic() {
+  const char* e = getenv("QD_SPO_GENERIC");
+  return e && e[0] == '1';
+}
+
 // L dispatch helpers
 #define QD_FFT_DISPATCH(L, CALL) \
   switch (L) {                   \
@@ -1249,6 +1255,13 @@ int col_fast(int L, int ns, int cols, c128* psi, const c128* expKT, const c128* 
 }
 
 }  // namespace
+
+// spo_gen.hip: every grid the specialised power-of-two kernels below do not cover
+int spo_generic_run(c128* psi, const c128* expVh, const c128* expV, const c128* expK, const c128* expKy,
+                    const int* dims, int D, int ns, int nsteps, int nout, c128* snap, hipStream_t st);
+int spo1d_generic_run(c128* psi, const c128* expV, const c128* expVh, const c128* expK, int nx, int B, int nt,
+                      int nout, c128* snap, hipStream_t st);
+
 }  // namespace qd
 
 using namespace qd;
@@ -1258,12 +1271,21 @@ extern "C" int qd_spo2_run_ex(qd_c128* psi_, const qd_c128* expVh_, const qd_c12
                               void* stream) {
   WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   QD_CHECK_ARG(psi_ && expVh_ && expK_, "qd_spo2_run_ex: null pointer");
-  QD_CHECK_ARG(pow2_in_range(nx) && pow2_in_range(ny), "qd_spo2_run_ex: nx=%d, ny=%d must be powers of 2 in [16, 1024]",
-               nx, ny);
-  QD_CHECK_ARG(ns >= 1 && ns <= SPO_MAX_NS, "qd_spo2_run_ex: ns=%d outside [1, %d]", ns, SPO_MAX_NS);
+  QD_CHECK_ARG(nx >= 1 && ny >= 1 && ns >= 1, "qd_spo2_run_ex: nx=%d ny=%d ns=%d", nx, ny, ns);
   QD_CHECK_ARG(nsteps >= 0 && nout >= 1, "qd_spo2_run_ex: nsteps=%d nout=%d", nsteps, nout);
-  QD_CHECK_ARG(ns * (ny / 4) <= 256, "qd_spo2_run_ex: ns*ny/4 = %d > 256 threads", ns * (ny / 4));
   if (nsteps == 0 && !expV_) return QD_OK;
+  {
+    // the power-of-two LDS / register kernels below: L in [16, 1024], ns <= 8, one transform set per
+    // workgroup; every other grid runs the any-size engine (spo_gen.hip)
+    const size_t row_lds = (size_t)(ny + 2 * ns * ny) * sizeof(c128), col_lds = (size_t)(nx + 4 * ns * nx) * sizeof(c128);
+    const bool special = pow2_in_range(nx) && pow2_in_range(ny) && ns <= SPO_MAX_NS && ns * (ny / 4) <= 256 &&
+                         ns * (nx / 4) <= 256 && row_lds <= 160 * 1024 && col_lds <= 160 * 1024 && !force_generic();
+    if (!special) {
+      const int dims[2] = {nx, ny};
+      return spo_generic_run((c128*)psi_, (const c128*)expVh_, (const c128*)expV_, (const c128*)expK_,
+                             (const c128*)expKy_, dims, 2, ns, nsteps, nout, (c128*)snap_, (hipStream_t)stream);
+    }
+  }
   hipStream_t st = (hipStream_t)stream;
   c128* psi = (c128*)psi_;
   const c128* expVh = (const c128*)expVh_;
@@ -1448,8 +1470,10 @@ extern "C" int qd_spo1d_run(qd_c128* psi_, const qd_c128* expV_, const qd_c128* 
                             int B, int nt, int nout, qd_c128* snap_, void* stream) {
   WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   QD_CHECK_ARG(psi_ && expV_ && expVh_ && expK_, "qd_spo1d_run: null pointer");
-  QD_CHECK_ARG(pow2_in_range(nx), "qd_spo1d_run: nx=%d must be a power of 2 in [16, 1024]", nx);
-  QD_CHECK_ARG(B >= 1 && nt >= 0 && nout >= 1, "qd_spo1d_run: B=%d nt=%d nout=%d", B, nt, nout);
+  QD_CHECK_ARG(nx >= 1 && B >= 1 && nt >= 0 && nout >= 1, "qd_spo1d_run: nx=%d B=%d nt=%d nout=%d", nx, B, nt, nout);
+  if (!pow2_in_range(nx) || force_generic())
+    return spo1d_generic_run((c128*)psi_, (const c128*)expV_, (const c128*)expVh_, (const c128*)expK_, nx, B, nt, nout,
+                             (c128*)snap_, (hipStream_t)stream);
   hipStream_t st = (hipStream_t)stream;
   void* w = nullptr;
   int rc = workspace(WS_MISC, nx * sizeof(c128), &w, st);
@@ -1470,12 +1494,20 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
                            int nsteps, int nout, qd_c128* snap_, void* stream) {
   WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   QD_CHECK_ARG(psi_ && expVh_ && expK_, "qd_spo3_run: null pointer");
-  QD_CHECK_ARG(pow2_in_range(nx) && pow2_in_range(ny) && pow2_in_range(nz) && nx <= 256 && ny <= 256 && nz <= 256,
-               "qd_spo3_run: nx, ny, nz must be powers of 2 in [16, 256]");
-  QD_CHECK_ARG(ns >= 1 && ns <= SPO_MAX_NS && ns * (nz / 4) <= 256 && ns * (nx / 4) <= 256,
-               "qd_spo3_run: ns=%d too large for the grid", ns);
+  QD_CHECK_ARG(nx >= 1 && ny >= 1 && nz >= 1 && ns >= 1, "qd_spo3_run: nx=%d ny=%d nz=%d ns=%d", nx, ny, nz, ns);
   QD_CHECK_ARG(nsteps >= 0 && nout >= 1, "qd_spo3_run: nsteps=%d nout=%d", nsteps, nout);
   if (nsteps == 0) return QD_OK;
+  {
+    const size_t row_lds = (size_t)(nz + 2 * ns * nz) * sizeof(c128), col_lds = (size_t)(nx + 4 * ns * nx) * sizeof(c128);
+    const bool special = pow2_in_range(nx) && pow2_in_range(ny) && pow2_in_range(nz) && nx <= 256 && ny <= 256 &&
+                         nz <= 256 && ns <= SPO_MAX_NS && ns * (nz / 4) <= 256 && ns * (nx / 4) <= 256 &&
+                         row_lds <= 160 * 1024 && col_lds <= 160 * 1024 && !force_generic();
+    if (!special) {
+      const int dims[3] = {nx, ny, nz};
+      return spo_generic_run((c128*)psi_, (const c128*)expVh_, nullptr, (const c128*)expK_, nullptr, dims, 3, ns,
+                             nsteps, nout, (c128*)snap_, (hipStream_t)stream);
+    }
+  }
   hipStream_t st = (hipStream_t)stream;
   c128* psi = (c128*)psi_;
   const c128* expVh = (const c128*)expVh_;

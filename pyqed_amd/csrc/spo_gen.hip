@@ -1,0 +1,752 @@
+// spo_gen.hip — split-operator propagation on ANY grid (every size the reference's SPO classes accept).
+//
+// The reference transforms with scipy.fftpack / numpy.fft (pocketfft), which take every length
+// (wpd.py:225-273 SPO, :692-758 SPO2, :1349-1411 SPO3).  spo.hip's register / Stockham kernels cover
+// powers of two in [16, 1024]; this file serves every other grid with the same pass structure:
+//
+//   axis plan per grid axis of length L (plan_axis):
+//     MIXED      mixed-radix Stockham autosort in LDS: radix 4, 2, 3, 5 butterflies in closed form, any
+//                other prime p <= 61 as a direct p-point DFT stage; natural-order output, fp64 twiddles
+//                exp(-2 pi i m / L) from sincospi, L <= 5120 (two LDS lines of L complex values)
+//     BLUESTEIN  lengths with a prime factor > 61: chirp-z, X_k = c_k sum_n (x_n c_n) conj(c_{k-n}),
+//                c_n = exp(-pi i n^2 / L) (n^2 mod 2L exact in integers), the convolution as an M-point
+//                mixed-radix FFT pair in LDS, M = the smallest 2^a 3^b 5^c >= 2L - 1 (M <= 5120)
+//     DIRECT     everything longer: O(L^2) DFT straight from HBM / L2, twiddle index (n k) mod L exact
+//
+//   one fused LDS pass per axis (spo_axis_kernel): a tile of G outer rows x C consecutive inner columns
+//   (C * 16 B contiguous per line element, the whole [L][ns] row when C == ns) is loaded once, then
+//     [IFFT] -> [U1 point op] -> [snapshot] -> [U2 point op] -> [FFT] -> [k_y phase] -> [FFT * K * IFFT]
+//   run on it in LDS and it is stored once.  Point operators (exp(-i V dt/2) per grid point, any ns)
+//   need every state of a point, i.e. the last (contiguous) axis with C == ns; KMUL (exp_K / N) is the
+//   outermost axis's FFT -> multiply -> IFFT.  The step sequence is spo.hip's (qd_spo2_run_ex /
+//   qd_spo3_run): both V/2 halves of every Strang step applied, as the reference's return_states=True
+//   arithmetic (wpd.py:723-730), or the merged V structure (wpd.py:736-755).
+//   A pass that does not fit the LDS budget (DIRECT axes, ns * M too large for a fused row) runs
+//   unfused: axis transforms, a point-operator kernel (thread per (point, state), any ns) and a
+//   k-space multiply, with one grid-sized scratch buffer.
+//
+//   SPO (1D, wpd.py:225-273): one persistent workgroup per wavepacket, all steps in LDS when the line
+//   fits; otherwise one launch sequence per step.
+#include "qd_common.hpp"
+
+#include <cstdlib>
+#include <vector>
+
+namespace qd {
+namespace spog {
+
+constexpr int MAX_ST = 32;
+constexpr size_t LDS_MAX = 163840;            // one workgroup may hold all 160 KiB on gfx950
+constexpr size_t LDS_SOFT = 65536;            // tile target: two or more workgroups per CU
+constexpr int GEN_MAXP = 61;                  // largest prime run as a direct radix stage
+constexpr int MAX_LDS_M = (int)(LDS_MAX / (2 * sizeof(c128)));   // 5120
+
+enum Kind { MIXED = 0, BLUESTEIN = 1, DIRECT = 2 };
+
+struct Fft {           // device-side plan of one axis, passed by value
+  int L, M, kind, nst;
+  int R[MAX_ST];
+  int Ns[MAX_ST];
+  const c128* tw;      // exp(-2 pi i m / M), m < M (DIRECT: M = L)
+  const c128* chirp;   // BLUESTEIN: exp(-pi i n^2 / L), n < L
+  const c128* bhat;    // BLUESTEIN: (1/M) FFT_M(b), b_m = conj(c_|m|) wrapped
+};
+
+enum Flags { F_INV = 1, F_PT1 = 2, F_SNAP = 4, F_PT2 = 8, F_FWD = 16, F_KY = 32, F_KMUL = 64 };
+
+struct AxisArgs {
+  c128* psi;
+  int O, L, I, C, G, flags, ns;
+  const c128* U1;      // [points][ns][ns] (F_PT1)
+  const c128* U2;      // (F_PT2)
+  c128* snap;          // (F_SNAP) same layout as psi
+  const c128* K;       // (F_KMUL) exp_K / N over the grid points, [L][I / ns]
+  const c128* Ky;      // (F_KY) [O][L]
+};
+
+// ---------------------------------------------------------------- device FFT
+// One Stockham stage over nl lines of length M: butterfly j of a line reads src[j + r M/R] (r < R) times
+// tw^(r k M/(Ns R)), k = j mod Ns, and writes the R-point DFT to dst[(j / Ns) Ns R + k + q Ns].
+template <bool INV>
+__device__ __forceinline__ void stage(const c128* __restrict__ src, c128* __restrict__ dst, int nl, int M, int R,
+                                      int Ns, const c128* __restrict__ tw) {
+  const int nb = M / R;
+  const int tot = nl * nb;
+  const int tstep = M / (Ns * R);
+  for (int f = threadIdx.x; f < tot; f += blockDim.x) {
+    const int l = f / nb, j = f - l * nb;
+    const c128* s = src + (size_t)l * M;
+    c128* d = dst + (size_t)l * M;
+    const int k = j % Ns;
+    const int db = (j / Ns) * Ns * R + k;
+    auto ld = [&](int r) {
+      const c128 x = s[j + r * nb];
+      if (r == 0 || k == 0) return x;
+      c128 w = tw[r * k * tstep];
+      if (INV) w = cconj(w);
+      return cmul(x, w);
+    };
+    if (R == 4) {
+      const c128 x0 = ld(0), x1 = ld(1), x2 = ld(2), x3 = ld(3);
+      const c128 a0 = cadd(x0, x2), a1 = csub(x0, x2), b0 = cadd(x1, x3), b1 = csub(x1, x3);
+      const c128 ib1 = INV ? cmuli(b1) : cmulmi(b1);
+      d[db] = cadd(a0, b0);
+      d[db + Ns] = cadd(a1, ib1);
+      d[db + 2 * Ns] = csub(a0, b0);
+      d[db + 3 * Ns] = csub(a1, ib1);
+    } else if (R == 2) {
+      const c128 x0 = ld(0), x1 = ld(1);
+      d[db] = cadd(x0, x1);
+      d[db + Ns] = csub(x0, x1);
+    } else if (R == 3) {
+      const double c = -0.5, sn = 0.86602540378443864676;   // cos, sin(2 pi / 3)
+      const c128 x0 = ld(0), x1 = ld(1), x2 = ld(2);
+      const c128 t = cadd(x1, x2), u = csub(x1, x2);
+      const c128 a = cadd(x0, cscale(t, c));
+      const c128 b = INV ? cmuli(cscale(u, sn)) : cmulmi(cscale(u, sn));   // -+ i s (x1 - x2)
+      d[db] = cadd(x0, t);
+      d[db + Ns] = cadd(a, b);
+      d[db + 2 * Ns] = csub(a, b);
+    } else if (R == 5) {
+      const double c1 = 0.30901699437494742410, c2 = -0.80901699437494742410;   // cos(2 pi/5), cos(4 pi/5)
+      const double s1 = 0.95105651629515357212, s2 = 0.58778525229247312917;    // sin(2 pi/5), sin(4 pi/5)
+      const c128 x0 = ld(0), x1 = ld(1), x2 = ld(2), x3 = ld(3), x4 = ld(4);
+      const c128 t1 = cadd(x1, x4), t2 = cadd(x2, x3), t3 = csub(x1, x4), t4 = csub(x2, x3);
+      const c128 a1 = cadd(x0, cadd(cscale(t1, c1), cscale(t2, c2)));
+      const c128 a2 = cadd(x0, cadd(cscale(t1, c2), cscale(t2, c1)));
+      const c128 b1r = cadd(cscale(t3, s1), cscale(t4, s2));
+      const c128 b2r = csub(cscale(t3, s2), cscale(t4, s1));
+      const c128 b1 = INV ? cmuli(b1r) : cmulmi(b1r), b2 = INV ? cmuli(b2r) : cmulmi(b2r);
+      d[db] = cadd(x0, cadd(t1, t2));
+      d[db + Ns] = cadd(a1, b1);
+      d[db + 4 * Ns] = csub(a1, b1);
+      d[db + 2 * Ns] = cadd(a2, b2);
+      d[db + 3 * Ns] = csub(a2, b2);
+    } else {  // any prime R <= GEN_MAXP: y_q = sum_r x_r w_R^(r q), w_R^m = tw[m M/R]
+      for (int q = 0; q < R; ++q) {
+        c128 acc = cmk(0.0, 0.0);
+        int e = 0;  // r q mod R
+        for (int r = 0; r < R; ++r) {
+          c128 w = tw[e * nb];
+          if (INV) w = cconj(w);
+          acc = cadd(acc, cmul(ld(r), w));
+          e += q;
+          if (e >= R) e -= R;
+        }
+        d[db + q * Ns] = acc;
+      }
+    }
+  }
+}
+
+// Mixed-radix transform of nl lines (cur -> result in cur; oth is the ping-pong buffer).  Every thread
+// of the workgroup must call it (barriers); it starts and ends behind a barrier.
+template <bool INV>
+__device__ __forceinline__ void stockham(const Fft& p, c128*& cur, c128*& oth, int nl, int M) {
+  for (int s = 0; s < p.nst; ++s) {
+    stage<INV>(cur, oth, nl, M, p.R[s], p.Ns[s], p.tw);
+    __syncthreads();
+    c128* t = cur;
+    cur = oth;
+    oth = t;
+  }
+}
+
+// Length-L DFT (INV: conjugate kernel, no scaling) of nl lines held in the first L slots of each M-slot
+// line of cur.  Result in cur (first L slots).
+template <bool INV>
+__device__ __forceinline__ void lds_fft(const Fft& p, c128*& cur, c128*& oth, int nl) {
+  const int M = p.M, L = p.L;
+  if (p.kind == BLUESTEIN) {
+    const int tot = nl * M;
+    for (int f = threadIdx.x; f < tot; f += blockDim.x) {
+      const int n = f % M;
+      c128 v = cmk(0.0, 0.0);
+      if (n < L) {
+        c128 ch = p.chirp[n];
+        if (INV) ch = cconj(ch);
+        v = cmul(cur[f], ch);
+      }
+      cur[f] = v;
+    }
+    __syncthreads();
+    stockham<false>(p, cur, oth, nl, M);
+    for (int f = threadIdx.x; f < tot; f += blockDim.x) {
+      c128 b = p.bhat[f % M];
+      if (INV) b = cconj(b);
+      cur[f] = cmul(cur[f], b);
+    }
+    __syncthreads();
+    stockham<true>(p, cur, oth, nl, M);
+    for (int f = threadIdx.x; f < tot; f += blockDim.x) {
+      const int n = f % M;
+      if (n < L) {
+        c128 ch = p.chirp[n];
+        if (INV) ch = cconj(ch);
+        cur[f] = cmul(cur[f], ch);
+      }
+    }
+    __syncthreads();
+  } else {
+    stockham<INV>(p, cur, oth, nl, M);
+  }
+}
+
+// ---------------------------------------------------------------- fused axis pass
+__global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
+  extern __shared__ c128 sm[];
+  const int M = p.M, L = a.L, C = a.C, G = a.G, I = a.I;
+  const int nl = G * C;
+  c128* cur = sm;
+  c128* oth = sm + (size_t)nl * M;
+  const int o0 = blockIdx.x * G, i0 = blockIdx.y * C;
+  const int gv = min(G, a.O - o0), cv = min(C, I - i0);
+  const int tot = G * L * C;
+  for (int f = threadIdx.x; f < tot; f += blockDim.x) {
+    const int g = f / (L * C), r = f - g * (L * C), e = r / C, c = r - e * C;
+    cur[(g * C + c) * M + e] =
+        (g < gv && c < cv) ? a.psi[((size_t)(o0 + g) * L + e) * I + i0 + c] : cmk(0.0, 0.0);
+  }
+  __syncthreads();
+  if (a.flags & F_INV) lds_fft<true>(p, cur, oth, nl);
+  auto point_op = [&](const c128* U) {   // C == I == ns: line g * ns + s holds state s of row g
+    const int ns = a.ns;
+    const int n = G * L * ns;
+    for (int f = threadIdx.x; f < n; f += blockDim.x) {
+      const int g = f / (L * ns), r = f - g * (L * ns), e = r / ns, s = r - e * ns;
+      if (g >= gv) continue;
+      const c128* u = U + (((size_t)(o0 + g) * L + e) * ns + s) * ns;
+      c128 acc = cmk(0.0, 0.0);
+      for (int b = 0; b < ns; ++b) acc = cadd(acc, cmul(u[b], cur[(g * ns + b) * M + e]));
+      oth[(g * ns + s) * M + e] = acc;
+    }
+    __syncthreads();
+    c128* t = cur;
+    cur = oth;
+    oth = t;
+  };
+  if (a.flags & F_PT1) point_op(a.U1);
+  if (a.flags & F_SNAP) {
+    for (int f = threadIdx.x; f < tot; f += blockDim.x) {
+      const int g = f / (L * C), r = f - g * (L * C), e = r / C, c = r - e * C;
+      if (g < gv && c < cv) a.snap[((size_t)(o0 + g) * L + e) * I + i0 + c] = cur[(g * C + c) * M + e];
+    }
+  }
+  if (a.flags & F_PT2) point_op(a.U2);
+  if (a.flags & F_FWD) lds_fft<false>(p, cur, oth, nl);
+  if (a.flags & F_KY) {
+    for (int f = threadIdx.x; f < tot; f += blockDim.x) {
+      const int g = f / (L * C), r = f - g * (L * C), e = r / C, c = r - e * C;
+      if (g < gv) cur[(g * C + c) * M + e] = cmul(a.Ky[(size_t)(o0 + g) * L + e], cur[(g * C + c) * M + e]);
+    }
+    __syncthreads();
+  }
+  if (a.flags & F_KMUL) {   // outermost axis (O == 1): FFT -> * exp_K / N -> IFFT
+    lds_fft<false>(p, cur, oth, nl);
+    const int pts = I / a.ns;
+    for (int f = threadIdx.x; f < tot; f += blockDim.x) {
+      const int r = f % (L * C), e = r / C, c = r - e * C;
+      if (c < cv) cur[c * M + e] = cmul(cur[c * M + e], a.K[(size_t)e * pts + (i0 + c) / a.ns]);
+    }
+    __syncthreads();
+    lds_fft<true>(p, cur, oth, nl);
+  }
+  for (int f = threadIdx.x; f < tot; f += blockDim.x) {
+    const int g = f / (L * C), r = f - g * (L * C), e = r / C, c = r - e * C;
+    if (g < gv && c < cv) a.psi[((size_t)(o0 + g) * L + e) * I + i0 + c] = cur[(g * C + c) * M + e];
+  }
+}
+
+// ---------------------------------------------------------------- unfused kernels
+// Direct DFT along one axis, out of place: dst[o][k][i] = sum_n src[o][n][i] w^(n k) (w = exp(-+2 pi i / L)).
+// Block (x, y): outputs k in [256 x, 256 x + 256) of lines y, y + gridDim.y, ...; input staged 256 points at a
+// time in LDS, per-output accumulators in LDS (flat loops: any blockDim).
+template <bool INV>
+__global__ __launch_bounds__(256) void dft_axis_kernel(const c128* __restrict__ src, c128* __restrict__ dst, long O,
+                                                       int L, long I, const c128* __restrict__ tw) {
+  __shared__ c128 xs[256];
+  __shared__ c128 acc[256];
+  const long nlines = O * I;
+  const int k0 = blockIdx.x * 256;
+  const int nk = min(256, L - k0);
+  for (long line = blockIdx.y; line < nlines; line += gridDim.y) {
+    const long o = line / I, i = line - o * I;
+    const c128* s = src + (size_t)o * L * I + i;
+    for (int t = threadIdx.x; t < 256; t += blockDim.x) acc[t] = cmk(0.0, 0.0);
+    for (int n0 = 0; n0 < L; n0 += 256) {
+      const int cnt = min(256, L - n0);
+      __syncthreads();
+      for (int t = threadIdx.x; t < cnt; t += blockDim.x) xs[t] = s[(size_t)(n0 + t) * I];
+      __syncthreads();
+      for (int kk = threadIdx.x; kk < nk; kk += blockDim.x) {
+        const long k = k0 + kk;
+        long e = ((long)n0 * k) % L;
+        c128 a = acc[kk];
+        for (int t = 0; t < cnt; ++t) {
+          c128 w = tw[e];
+          if (INV) w = cconj(w);
+          a = cadd(a, cmul(xs[t], w));
+          e += k;
+          if (e >= L) e -= L;
+        }
+        acc[kk] = a;
+      }
+    }
+    __syncthreads();
+    for (int kk = threadIdx.x; kk < nk; kk += blockDim.x) dst[(size_t)o * L * I + (size_t)(k0 + kk) * I + i] = acc[kk];
+    __syncthreads();
+  }
+}
+
+// dst[p][s] = sum_b U[p][s][b] src[p][b], one thread per (point, state), any ns
+__global__ void pointop_kernel(const c128* __restrict__ src, c128* __restrict__ dst, const c128* __restrict__ U,
+                               long npts, int ns) {
+  const long n = npts * ns;
+  for (long f = blockIdx.x * (long)blockDim.x + threadIdx.x; f < n; f += (long)gridDim.x * blockDim.x) {
+    const long pt = f / ns;
+    const c128* u = U + (size_t)f * ns;
+    const c128* x = src + (size_t)pt * ns;
+    c128 acc = cmk(0.0, 0.0);
+    for (int b = 0; b < ns; ++b) acc = cadd(acc, cmul(u[b], x[b]));
+    dst[f] = acc;
+  }
+}
+
+// psi[p][s] *= K[p / rep_div % rep_mod ...]: psi element f multiplies K[(f / ns) / kdiv] (kdiv = 1: K per
+// point; used for exp_K / N on the whole grid and the Jacobi k_y phase per (row, k_y))
+__global__ void kmul_kernel(c128* psi, const c128* __restrict__ K, long n, int ns) {
+  for (long f = blockIdx.x * (long)blockDim.x + threadIdx.x; f < n; f += (long)gridDim.x * blockDim.x)
+    psi[f] = cmul(psi[f], K[f / ns]);
+}
+
+__global__ void scale_copy_kernel(const c128* __restrict__ src, c128* __restrict__ dst, long n, double s) {
+  for (long f = blockIdx.x * (long)blockDim.x + threadIdx.x; f < n; f += (long)gridDim.x * blockDim.x)
+    dst[f] = cscale(src[f], s);
+}
+
+// ---------------------------------------------------------------- plan tables
+__global__ void twiddle_table_kernel(int M, c128* tw) {
+  for (int m = blockIdx.x * blockDim.x + threadIdx.x; m < M; m += gridDim.x * blockDim.x) {
+    double s, c;
+    sincospi(-2.0 * (double)m / (double)M, &s, &c);
+    tw[m] = cmk(c, s);
+  }
+}
+
+// c_n = exp(-pi i n^2 / L) with n^2 mod 2L exact; b_m = conj(c_|m|) wrapped into M slots
+__global__ void chirp_kernel(int L, int M, c128* chirp, c128* b) {
+  for (int m = blockIdx.x * blockDim.x + threadIdx.x; m < M; m += gridDim.x * blockDim.x) {
+    const int n = m < L ? m : (M - m < L ? M - m : -1);
+    c128 v = cmk(0.0, 0.0);
+    if (n >= 0) {
+      const long q = ((long)n * n) % (2L * L);
+      double s, c;
+      sincospi(-(double)q / (double)L, &s, &c);
+      if (m < L) chirp[m] = cmk(c, s);
+      v = cmk(c, -s);
+    }
+    b[m] = v;
+  }
+}
+
+// bhat[k] = (1/M) sum_m b[m] exp(-2 pi i m k / M) (direct, exact index (m k) mod M)
+__global__ void bhat_kernel(int M, const c128* __restrict__ b, const c128* __restrict__ tw, c128* bhat) {
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < M; k += gridDim.x * blockDim.x) {
+    c128 acc = cmk(0.0, 0.0);
+    long e = 0;
+    for (int m = 0; m < M; ++m) {
+      acc = cadd(acc, cmul(b[m], tw[e]));
+      e += k;
+      if (e >= M) e -= M;
+    }
+    bhat[k] = cscale(acc, 1.0 / M);
+  }
+}
+
+// ---------------------------------------------------------------- 1D persistent SPO
+// SPO.run (wpd.py:250-270): V/2; for blk in 1..nt//nout-1: nout x [K, V], snapshot; K; V/2.
+// One workgroup per wavepacket, the line resident in LDS for the whole run.
+__global__ __launch_bounds__(256) void spo1d_gen_kernel(Fft p, c128* psi, const c128* eV, const c128* eVh,
+                                                        const c128* eK, int nt, int nout, c128* snap) {
+  extern __shared__ c128 sm[];
+  const int L = p.L, M = p.M;
+  c128* cur = sm;
+  c128* oth = sm + M;
+  const int b = blockIdx.x;
+  c128* x = psi + (size_t)b * L;
+  const double inv = 1.0 / L;
+  for (int k = threadIdx.x; k < L; k += blockDim.x) cur[k] = cmul(eVh[k], x[k]);
+  __syncthreads();
+  const int nblk = nt / nout;
+  const int nsnap = nblk > 0 ? nblk - 1 : 0;
+  auto kstep = [&]() {
+    lds_fft<false>(p, cur, oth, 1);
+    for (int k = threadIdx.x; k < L; k += blockDim.x) cur[k] = cmul(cur[k], cscale(eK[k], inv));
+    __syncthreads();
+    lds_fft<true>(p, cur, oth, 1);
+  };
+  for (int blk = 1; blk < nblk; ++blk) {
+    for (int s = 0; s < nout; ++s) {
+      kstep();
+      for (int k = threadIdx.x; k < L; k += blockDim.x) cur[k] = cmul(eV[k], cur[k]);
+      __syncthreads();
+    }
+    if (snap)
+      for (int k = threadIdx.x; k < L; k += blockDim.x) snap[((size_t)b * nsnap + (blk - 1)) * L + k] = cur[k];
+  }
+  kstep();
+  for (int k = threadIdx.x; k < L; k += blockDim.x) x[k] = cmul(eVh[k], cur[k]);
+}
+
+// ---------------------------------------------------------------- host planning
+bool all_factors_small(int n, int maxp) {
+  for (int p = 2; (long)p * p <= n; ++p)
+    while (n % p == 0) {
+      if (p > maxp) return false;
+      n /= p;
+    }
+  return n <= maxp;
+}
+
+int next_smooth(int n) {  // smallest 2^a 3^b 5^c >= n
+  for (int m = n;; ++m) {
+    int r = m;
+    for (int p : {2, 3, 5})
+      while (r % p == 0) r /= p;
+    if (r == 1) return m;
+  }
+}
+
+void factor_stages(int M, Fft& f) {
+  f.nst = 0;
+  int ns = 1, n = M;
+  auto push = [&](int r) {
+    f.R[f.nst] = r;
+    f.Ns[f.nst] = ns;
+    ++f.nst;
+    ns *= r;
+    n /= r;
+  };
+  while (n % 4 == 0) push(4);
+  while (n % 2 == 0) push(2);
+  while (n % 3 == 0) push(3);
+  while (n % 5 == 0) push(5);
+  int p = 7;
+  while (n > 1) {
+    while (n % p == 0) push(p);
+    p += 2;
+  }
+}
+
+// Kind and table sizes of an axis of length L (count of c128 table slots in *tab).
+void plan_kind(int L, int* kind, int* M, size_t* tab) {
+  const char* e = getenv("QD_SPO_FORCE_KIND");   // tests: 1 = Bluestein, 2 = direct wherever legal
+  const int force = e ? atoi(e) : 0;
+  if (force == 2) {
+    *kind = DIRECT;
+    *M = L;
+    *tab = L;
+    return;
+  }
+  if (force != 1 && L <= MAX_LDS_M && all_factors_small(L, GEN_MAXP)) {
+    *kind = MIXED;
+    *M = L;
+    *tab = L;
+    return;
+  }
+  const int m = next_smooth(2 * L - 1);
+  if (L >= 2 && m <= MAX_LDS_M) {
+    *kind = BLUESTEIN;
+    *M = m;
+    *tab = (size_t)3 * m + L;   // tw[M], chirp[L], b[M], bhat[M]
+    return;
+  }
+  *kind = DIRECT;
+  *M = L;
+  *tab = L;
+}
+
+int plan_axis(int L, c128* tab, Fft& f, hipStream_t st) {
+  int kind, M;
+  size_t n;
+  plan_kind(L, &kind, &M, &n);
+  f.L = L;
+  f.M = M;
+  f.kind = kind;
+  f.tw = tab;
+  f.chirp = f.bhat = nullptr;
+  f.nst = 0;
+  hipLaunchKernelGGL(twiddle_table_kernel, dim3((M + 255) / 256), dim3(256), 0, st, M, tab);
+  QD_HIP(hipGetLastError());
+  if (kind != DIRECT) factor_stages(M, f);
+  if (f.nst > MAX_ST) {
+    set_error("spo: FFT plan of length %d needs %d stages (max %d)", M, f.nst, MAX_ST);
+    return QD_EINVAL;
+  }
+  if (kind == BLUESTEIN) {
+    c128* chirp = tab + M;
+    c128* b = chirp + L;
+    c128* bhat = b + M;
+    hipLaunchKernelGGL(chirp_kernel, dim3((M + 255) / 256), dim3(256), 0, st, L, M, chirp, b);
+    hipLaunchKernelGGL(bhat_kernel, dim3((M + 255) / 256), dim3(256), 0, st, M, (const c128*)b, (const c128*)tab, bhat);
+    QD_HIP(hipGetLastError());
+    f.chirp = chirp;
+    f.bhat = bhat;
+  }
+  return QD_OK;
+}
+
+size_t plan_slots(int L) {
+  int k, M;
+  size_t n;
+  plan_kind(L, &k, &M, &n);
+  return n;
+}
+
+inline int grid_for(long n) { return (int)std::max<long>(1, std::min<long>((n + 255) / 256, 8192)); }
+
+// ---------------------------------------------------------------- executor
+struct Exec {
+  int D = 0;
+  int n[3] = {1, 1, 1};
+  int ns = 1;
+  long npts = 0;
+  Fft f[3];
+  hipStream_t st = nullptr;
+  c128* psi = nullptr;
+  c128* tmp = nullptr;     // grid-sized scratch (unfused passes)
+  const c128* Ks = nullptr;   // exp_K / N
+  const c128* Ky = nullptr;   // Jacobi k_y phase [n0][n1] (D == 2)
+
+  long outer(int d) const { long o = 1; for (int k = 0; k < d; ++k) o *= n[k]; return o; }
+  long inner(int d) const { long i = ns; for (int k = d + 1; k < D; ++k) i *= n[k]; return i; }
+
+  int launch_axis(int d, int flags, int C, int G, const c128* U1, const c128* U2, c128* snap) {
+    AxisArgs a;
+    a.psi = psi;
+    a.O = (int)outer(d);
+    a.L = n[d];
+    a.I = (int)inner(d);
+    a.C = C;
+    a.G = G;
+    a.flags = flags;
+    a.ns = ns;
+    a.U1 = U1;
+    a.U2 = U2;
+    a.snap = snap;
+    a.K = Ks;
+    a.Ky = Ky;
+    const size_t lds = (size_t)2 * G * C * f[d].M * sizeof(c128);
+    (void)hipFuncSetAttribute((const void*)spo_axis_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
+    hipLaunchKernelGGL(spo_axis_kernel, dim3((a.O + G - 1) / G, (a.I + C - 1) / C), dim3(256), lds, st, f[d], a);
+    QD_HIP(hipGetLastError());
+    return QD_OK;
+  }
+
+  // lines-per-tile choice for an LDS pass over axis d; C == I (whole rows) required for point ops
+  bool tile(int d, bool rows, int* C, int* G) const {
+    const long I = inner(d), O = outer(d);
+    const size_t line = (size_t)2 * f[d].M * sizeof(c128);
+    int c;
+    if (rows) {
+      c = (int)I;
+    } else {
+      c = (int)std::min<long>(I, 8);
+      while (c > 1 && (size_t)c * line > LDS_SOFT) c >>= 1;
+    }
+    if ((size_t)c * line > LDS_MAX) return false;
+    int g = 1;
+    if (c == I) {   // whole rows: stack rows until ~1024 elements per tile or the LDS target
+      while (g < O && (long)g * c * n[d] < 1024 && (size_t)(2 * g) * c * line <= LDS_SOFT) g *= 2;
+      g = (int)std::min<long>(g, O);
+    }
+    *C = c;
+    *G = g;
+    return true;
+  }
+
+  int transform(int d, bool inv) {
+    if (f[d].kind != DIRECT) {
+      int C, G;
+      if (tile(d, false, &C, &G)) return launch_axis(d, inv ? F_INV : F_FWD, C, G, nullptr, nullptr, nullptr);
+    }
+    // direct DFT from HBM into the scratch grid, then back
+    const long O = outer(d), I = inner(d);
+    const int L = n[d];
+    const long lines = O * I;
+    const dim3 grid((L + 255) / 256, (unsigned)std::min<long>(lines, 65535));
+    if (inv)
+      hipLaunchKernelGGL(dft_axis_kernel<true>, grid, dim3(256), 0, st, (const c128*)psi, tmp, O, L, I, f[d].tw);
+    else
+      hipLaunchKernelGGL(dft_axis_kernel<false>, grid, dim3(256), 0, st, (const c128*)psi, tmp, O, L, I, f[d].tw);
+    QD_HIP(hipGetLastError());
+    QD_HIP(hipMemcpyAsync(psi, tmp, (size_t)npts * ns * sizeof(c128), hipMemcpyDeviceToDevice, st));
+    return QD_OK;
+  }
+
+  int pointop(const c128* U) {
+    hipLaunchKernelGGL(pointop_kernel, dim3(grid_for(npts * ns)), dim3(256), 0, st, (const c128*)psi, tmp, U, npts, ns);
+    QD_HIP(hipGetLastError());
+    QD_HIP(hipMemcpyAsync(psi, tmp, (size_t)npts * ns * sizeof(c128), hipMemcpyDeviceToDevice, st));
+    return QD_OK;
+  }
+
+  int kmul(const c128* K) {
+    hipLaunchKernelGGL(kmul_kernel, dim3(grid_for(npts * ns)), dim3(256), 0, st, psi, K, npts * ns, ns);
+    QD_HIP(hipGetLastError());
+    return QD_OK;
+  }
+
+  // One pass over axis d with the ops of `flags` (F_PT*, F_SNAP, F_KY: last axis; F_KMUL: axis 0).
+  int pass(int d, int flags, const c128* U1, const c128* U2, c128* snap) {
+    const bool pt = flags & (F_PT1 | F_PT2 | F_SNAP | F_KY);
+    if (f[d].kind != DIRECT) {
+      int C, G;
+      if (tile(d, pt, &C, &G)) return launch_axis(d, flags, C, G, U1, U2, snap);
+    }
+    int rc;
+    if ((flags & F_INV) && (rc = transform(d, true))) return rc;
+    if ((flags & F_PT1) && (rc = pointop(U1))) return rc;
+    if (flags & F_SNAP)
+      QD_HIP(hipMemcpyAsync(snap, psi, (size_t)npts * ns * sizeof(c128), hipMemcpyDeviceToDevice, st));
+    if ((flags & F_PT2) && (rc = pointop(U2))) return rc;
+    if ((flags & F_FWD) && (rc = transform(d, false))) return rc;
+    if ((flags & F_KY) && (rc = kmul(Ky))) return rc;
+    if (flags & F_KMUL) {
+      if ((rc = transform(d, false))) return rc;
+      if ((rc = kmul(Ks))) return rc;
+      if ((rc = transform(d, true))) return rc;
+    }
+    return QD_OK;
+  }
+};
+
+// Strang / merged step sequence of qd_spo2_run_ex / qd_spo3_run on a D-dimensional grid (D = 2, 3).
+int run_nd(Exec& x, const c128* Uh, const c128* Ufull, int nsteps, int nout, c128* snap, bool ky) {
+  const int D = x.D, last = D - 1;
+  const int kyf = ky ? F_KY : 0;
+  const size_t grid_elems = (size_t)x.npts * x.ns;
+  int rc;
+  if ((rc = x.pass(last, F_PT1 | F_FWD | kyf, Uh, nullptr, nullptr))) return rc;
+  for (int d = last - 1; d >= 1; --d)
+    if ((rc = x.pass(d, F_FWD, nullptr, nullptr, nullptr))) return rc;
+  for (int s = 1; s <= nsteps; ++s) {
+    if ((rc = x.pass(0, F_KMUL, nullptr, nullptr, nullptr))) return rc;
+    for (int d = 1; d < last; ++d)
+      if ((rc = x.pass(d, F_INV, nullptr, nullptr, nullptr))) return rc;
+    const bool take = snap && (s % nout == 0);
+    c128* sp = take ? snap + (size_t)(s / nout - 1) * grid_elems : nullptr;
+    int flags = F_INV | F_PT1 | (take ? F_SNAP : 0);
+    if (Ufull) flags |= F_FWD | kyf;
+    else if (s < nsteps) flags |= F_PT2 | F_FWD | kyf;
+    if ((rc = x.pass(last, flags, Ufull ? Ufull : Uh, Uh, sp))) return rc;
+    if (flags & F_FWD)
+      for (int d = last - 1; d >= 1; --d)
+        if ((rc = x.pass(d, F_FWD, nullptr, nullptr, nullptr))) return rc;
+  }
+  if (Ufull) {   // merged tail (wpd.py:752-755): K, then V/2
+    if ((rc = x.pass(0, F_KMUL, nullptr, nullptr, nullptr))) return rc;
+    for (int d = 1; d < last; ++d)
+      if ((rc = x.pass(d, F_INV, nullptr, nullptr, nullptr))) return rc;
+    if ((rc = x.pass(last, F_INV | F_PT1, Uh, nullptr, nullptr))) return rc;
+  }
+  return QD_OK;
+}
+
+}  // namespace spog
+
+// Generic SPO2 / SPO3 run (any grid, any ns).  dims = {nx, ny} or {nx, ny, nz}; expK [dims] unscaled;
+// expKy [nx][ny] (2D Jacobi) or null; expV (merged V structure) or null.
+int spo_generic_run(c128* psi, const c128* expVh, const c128* expV, const c128* expK, const c128* expKy,
+                    const int* dims, int D, int ns, int nsteps, int nout, c128* snap, hipStream_t st) {
+  using namespace spog;
+  WsScope wss_(st);
+  Exec x;
+  x.D = D;
+  x.ns = ns;
+  x.st = st;
+  x.psi = psi;
+  x.npts = 1;
+  for (int d = 0; d < D; ++d) {
+    x.n[d] = dims[d];
+    x.npts *= dims[d];
+  }
+  size_t slots = (size_t)x.npts * ns + x.npts;   // tmp grid + exp_K / N
+  for (int d = 0; d < D; ++d) slots += plan_slots(dims[d]);
+  void* w = nullptr;
+  int rc = workspace(WS_SPO, slots * sizeof(c128), &w, st);
+  if (rc) return rc;
+  x.tmp = (c128*)w;
+  c128* ks = x.tmp + (size_t)x.npts * ns;
+  c128* tab = ks + x.npts;
+  for (int d = 0; d < D; ++d) {
+    if ((rc = plan_axis(dims[d], tab, x.f[d], st))) return rc;
+    tab += plan_slots(dims[d]);
+  }
+  hipLaunchKernelGGL(scale_copy_kernel, dim3(grid_for(x.npts)), dim3(256), 0, st, expK, ks, x.npts,
+                     1.0 / (double)x.npts);
+  QD_HIP(hipGetLastError());
+  x.Ks = ks;
+  x.Ky = expKy;
+  return run_nd(x, expVh, expV, nsteps, nout, snap, expKy != nullptr);
+}
+
+// Generic 1D SPO.run (any nx), B wavepackets [B][nx].
+int spo1d_generic_run(c128* psi, const c128* expV, const c128* expVh, const c128* expK, int nx, int B, int nt,
+                      int nout, c128* snap, hipStream_t st) {
+  using namespace spog;
+  WsScope wss_(st);
+  const long n = (long)nx * B;
+  const size_t slots = plan_slots(nx) + (size_t)2 * n + nx;
+  void* w = nullptr;
+  int rc = workspace(WS_MISC, slots * sizeof(c128), &w, st);
+  if (rc) return rc;
+  c128* tab = (c128*)w;
+  c128* tmp = tab + plan_slots(nx);
+  c128* ks = tmp + 2 * n;
+  Fft f;
+  if ((rc = plan_axis(nx, tab, f, st))) return rc;
+  if (f.kind != DIRECT) {
+    const size_t lds = (size_t)2 * f.M * sizeof(c128);
+    (void)hipFuncSetAttribute((const void*)spo1d_gen_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
+    hipLaunchKernelGGL(spo1d_gen_kernel, dim3(B), dim3(256), lds, st, f, psi, expV, expVh, expK, nt, nout, snap);
+    QD_HIP(hipGetLastError());
+    return QD_OK;
+  }
+  // DIRECT lines: one launch sequence per step on the [B][nx] grid (the axis is the last one, I = 1)
+  hipLaunchKernelGGL(scale_copy_kernel, dim3(grid_for(nx)), dim3(256), 0, st, expK, ks, (long)nx, 1.0 / nx);
+  QD_HIP(hipGetLastError());
+  const dim3 grid((nx + 255) / 256, (unsigned)std::min<long>(B, 65535));
+  auto vmul = [&](const c128* V) -> int {   // psi[b][k] *= V[k]
+    for (int b = 0; b < B; ++b)
+      hipLaunchKernelGGL(kmul_kernel, dim3(grid_for(nx)), dim3(256), 0, st, psi + (size_t)b * nx, V, (long)nx, 1);
+    QD_HIP(hipGetLastError());
+    return QD_OK;
+  };
+  auto kstep = [&]() -> int {
+    hipLaunchKernelGGL(dft_axis_kernel<false>, grid, dim3(256), 0, st, (const c128*)psi, tmp, (long)B, nx, 1L, f.tw);
+    for (int b = 0; b < B; ++b)
+      hipLaunchKernelGGL(kmul_kernel, dim3(grid_for(nx)), dim3(256), 0, st, tmp + (size_t)b * nx, (const c128*)ks,
+                         (long)nx, 1);
+    hipLaunchKernelGGL(dft_axis_kernel<true>, grid, dim3(256), 0, st, (const c128*)tmp, psi, (long)B, nx, 1L, f.tw);
+    QD_HIP(hipGetLastError());
+    return QD_OK;
+  };
+  if ((rc = vmul(expVh))) return rc;
+  const int nblk = nt / nout;
+  const int nsnap = nblk > 0 ? nblk - 1 : 0;
+  for (int blk = 1; blk < nblk; ++blk) {
+    for (int s = 0; s < nout; ++s) {
+      if ((rc = kstep())) return rc;
+      if ((rc = vmul(expV))) return rc;
+    }
+    if (snap)
+      for (int b = 0; b < B; ++b)
+        QD_HIP(hipMemcpyAsync(snap + ((size_t)b * nsnap + (blk - 1)) * nx, psi + (size_t)b * nx, nx * sizeof(c128),
+                              hipMemcpyDeviceToDevice, st));
+  }
+  if ((rc = kstep())) return rc;
+  return vmul(expVh);
+}
+
+}  // namespace qd

@@ -838,6 +838,103 @@ def spo2_256():
          n_psilist=len(r.psilist), times=r.times, exp_K_row7=sol.exp_K[7], exp_V_half_row100=sol.exp_V_half[100])
 
 
+def spo2_model_rect(nx, ny, ns=2, L=6.0):
+    """spo2_model on an nx x ny grid with ns surfaces: 1/2((X + 1 - a)^2 + Y^2) + 0.05 a, couplings 0.2 X / (1 + |a-b|)
+    between neighbours a, a + 1 (ns > 2 exercises the host eigh build, wpd.py:583-623)."""
+    x = np.linspace(-L, L, nx)
+    y = np.linspace(-L * 0.9, L * 0.9, ny)
+    X, Y = np.meshgrid(x, y, indexing="ij")
+    surfaces = [0.5 * ((X + 1 - a) ** 2 + Y ** 2) + 0.05 * a for a in range(ns)]
+    couplings = [[[a, a + 1], 0.2 * X + 0.05 * Y] for a in range(ns - 1)]
+    psi0 = np.zeros((nx, ny, ns), dtype=complex)
+    psi0[:, :, 0] = np.exp(-((X + 1.5) ** 2 + Y ** 2) / 2 + 0.5j * X) / np.sqrt(np.pi)
+    return x, y, surfaces, couplings, psi0
+
+
+def _spo2_rect_case(name, nx, ny, ns, nt, nout, dt, full=True):
+    """SPO2.run (wpd.py:692-758, return_states=True) on a non-power-of-two grid: the reference transforms any
+    length with scipy.fftpack (wpd.py:837-848).  full=False keeps a strided sample of each state (large grids)."""
+    from pyqed.wpd import SPO2
+    x, y, surfaces, couplings, psi0 = spo2_model_rect(nx, ny, ns)
+    sol = SPO2(x, y, mass=[1.0, 1.3], nstates=ns)
+    sol.set_DPES(surfaces, couplings)
+    r = sol.run(psi0, dt=dt, nt=nt, nout=nout)
+    dx, dy = x[1] - x[0], y[1] - y[0]
+    pops = np.array([[np.vdot(p[:, :, k], p[:, :, k]).real * dx * dy for k in range(ns)] for p in r.psilist])
+    out = dict(nx=nx, ny=ny, ns=ns, dt=dt, nt=nt, nout=nout, populations=pops, n_psilist=len(r.psilist),
+               times=r.times)
+    if full:
+        out["psilist"] = np.array(r.psilist)
+    else:
+        out["psi_final_sample"] = r.psilist[-1][::16, ::16]
+        out["psi_final_row"] = r.psilist[-1][nx // 2]
+        out["psi_final_col"] = r.psilist[-1][:, ny // 3]
+    save(name, **out)
+
+
+@golden
+def spo2_20x20():
+    _spo2_rect_case("spo2_20x20", 20, 20, 2, nt=6, nout=2, dt=0.05)
+
+
+@golden
+def spo2_96x80():
+    _spo2_rect_case("spo2_96x80", 96, 80, 2, nt=4, nout=2, dt=0.05)
+
+
+@golden
+def spo2_67x45_ns3():
+    """67 is a prime above the direct-radix limit (Bluestein axis); three surfaces."""
+    _spo2_rect_case("spo2_67x45_ns3", 67, 45, 3, nt=4, nout=2, dt=0.05)
+
+
+@golden
+def spo2_12x10_ns9():
+    """Nine surfaces (above round 2's ns <= 8 cap)."""
+    _spo2_rect_case("spo2_12x10_ns9", 12, 10, 9, nt=3, nout=1, dt=0.05)
+
+
+@golden
+def spo2_1024():
+    """1024 x 1024 x 2 (round 2 refused ns * n / 4 > 256): 3 Strang steps; strided sample + one row / column."""
+    _spo2_rect_case("spo2_1024", 1024, 1024, 2, nt=3, nout=1, dt=0.05, full=False)
+
+
+@golden
+def spo3_24x20x18():
+    """SPO3 (wpd.py:1105-1432, numpy fftn) on a 24 x 20 x 18 x 2 grid."""
+    from pyqed.wpd import SPO3
+    x, y, z = np.linspace(-6, 6, 24), np.linspace(-5, 5, 20), np.linspace(-5.5, 5.5, 18)
+    X, Y, Z = np.meshgrid(x, y, z, indexing="ij")
+    sol = SPO3(x, y, z, masses=[1.0, 1.2, 0.9], nstates=2)
+    sol.set_DPES([0.5 * ((X + 1) ** 2 + Y ** 2 + Z ** 2), 0.5 * ((X - 1) ** 2 + Y ** 2 + Z ** 2)],
+                 [[[0, 1], 0.2 * X]])
+    psi0 = np.zeros((24, 20, 18, 2), dtype=complex)
+    psi0[..., 1] = np.exp(-((X + 1) ** 2 + Y ** 2 + Z ** 2) / 2 + 0.3j * Y) / np.pi ** 0.75
+    r = sol.run(psi0=psi0, dt=0.2, nt=4, nout=2)
+    save("spo3_24x20x18", dt=0.2, nt=4, nout=2, psilist=np.array(r.psilist), psi=r.psi)
+
+
+@golden
+def spo1d_any():
+    """SPO.run (wpd.py:225-273) on 50, 97 (prime: Bluestein), 200, 2053 (prime, M = 4320) and 6000 (beyond the
+    LDS line: direct DFT) points."""
+    from pyqed.wpd import SPO
+    out = {}
+    for n, nt, nout in ((50, 12, 3), (97, 7, 2), (200, 10, 1), (2053, 4, 1), (6000, 3, 1)):
+        x = np.linspace(-8, 8, n)
+        psi0 = (np.exp(-(x + 2) ** 2 / 2 + 1j * 0.5 * x) / np.pi ** 0.25).astype(complex)
+        sol = SPO(x, mass=1.0)
+        sol.set_potential(lambda x: x ** 2 / 2)
+        r = sol.run(psi0, dt=0.01, nt=nt, nout=nout)
+        out[f"n{n}_nt"] = nt
+        out[f"n{n}_nout"] = nout
+        out[f"n{n}_psilist"] = np.array(r.psilist).reshape(-1, n)
+        out[f"n{n}_psi"] = r.psi
+    out["sizes"] = np.array([50, 97, 200, 2053, 6000])
+    save("spo1d_any", **out)
+
+
 @golden
 def deom_run_bench_long():
     """Config d4 (L = 12, npsd = 4 -> K = 5, 6188 ADOs) for 25 steps at the bench's dt = 0.002 (DEOMSolver.run,

@@ -230,3 +230,52 @@ def test_deom_corr4_oracle_matches_reference():
         assert relerr(cw, g["cw_" + lcr]) < 1e-12, lcr
     cw = od.correlation_4op_3t(P, *args, [sz, sx, sx, sz], g["rho0"], float(g["T"]), g["wx"], g["wy"], if_full=False)
     assert relerr(cw, g["cw_cut_llll"]) < 1e-12
+
+
+@pytest.mark.parametrize("name", ["spo2_20x20", "spo2_96x80", "spo2_67x45_ns3", "spo2_12x10_ns9"])
+def test_spo2_rect_oracle_matches_reference(name):
+    """Non-power-of-two grids and ns > 2 (make_golden _spo2_rect_case): the oracle's SPO2 restatement equals the
+    reference run (scipy.fftpack takes every length, wpd.py:837-848)."""
+    from oracle import spo
+    from spo_models import spo2_model_rect, spo2_potential
+    g = load_golden(name)
+    nx, ny, ns = int(g["nx"]), int(g["ny"]), int(g["ns"])
+    x, y, surfaces, couplings, psi0 = spo2_model_rect(nx, ny, ns)
+    v = spo2_potential(surfaces, couplings, ns)
+    eVh, eK = spo.spo2_build(x, y, v, (1.0, 1.3), float(g["dt"]))
+    psilist = spo.spo2_run(eVh, eK, psi0, int(g["nt"]), int(g["nout"]))
+    assert len(psilist) == int(g["n_psilist"])
+    assert relerr(np.array(psilist), g["psilist"]) < 1e-12
+
+
+def test_spo3_rect_oracle_matches_reference():
+    from oracle import spo
+    from spo_models import spo3_model
+    g = load_golden("spo3_24x20x18")
+    (x, y, z), masses, surfaces, couplings, psi0 = spo3_model()
+    ns = 2
+    v = np.zeros(psi0.shape + (ns,))
+    v[..., 0, 0], v[..., 1, 1] = surfaces
+    v[..., 0, 1] = v[..., 1, 0] = couplings[0][1]
+    w, u = np.linalg.eigh(v)
+    ud = np.conj(np.swapaxes(u, -1, -2))
+    eVh = (u * np.exp(-1j * w * float(g["dt"]) / 2)[..., None, :]) @ ud
+    from scipy.fftpack import fftfreq
+    ks = [2 * np.pi * fftfreq(len(a), a[1] - a[0]) for a in (x, y, z)]
+    Kx, Ky, Kz = np.meshgrid(*ks, indexing="ij")
+    eK = np.exp(-1j * (Kx ** 2 / 2 / masses[0] + Ky ** 2 / 2 / masses[1] + Kz ** 2 / 2 / masses[2]) * float(g["dt"]))
+    psilist, psi = spo.spo3_run(eVh, eK, psi0, int(g["nt"]), int(g["nout"]))
+    assert relerr(np.array(psilist), g["psilist"]) < 1e-12
+    assert relerr(psi, g["psi"]) < 1e-12
+
+
+def test_spo1d_any_oracle_matches_reference():
+    from oracle import spo
+    from spo_models import spo1d_model
+    g = load_golden("spo1d_any")
+    for n in g["sizes"]:
+        x, psi0 = spo1d_model(int(n))
+        pl, psi = spo.spo1d_run(x, x ** 2 / 2, psi0, 0.01, int(g[f"n{n}_nt"]), int(g[f"n{n}_nout"]))
+        assert relerr(psi, g[f"n{n}_psi"]) < 1e-12, n
+        if len(pl):
+            assert relerr(np.array(pl), g[f"n{n}_psilist"]) < 1e-12, n
