@@ -548,15 +548,14 @@ __global__ void deom_trace_kernel(const c128* snap, const c128* E, int ne, int B
 
 // oqs._heom (pyqed/oqs.py:1808-1875): single-exponential chain, explicit in-place sweep per
 // step (ADO n uses the already-updated n-1, the old n and n+1; ADO nado-1 is never updated).
-// One workgroup per hierarchy, one thread per matrix element, ADOs in global memory.
+// One workgroup per hierarchy, threads loop over the ns^2 matrix elements (any ns); the new ADO n is
+// staged in `tmp` (ns^2 per hierarchy) and copied in behind a barrier.
 __global__ __launch_bounds__(256) void heom_chain_sweep_kernel(c128* ados, int nado, int ns, const c128* H,
                                                                const c128* Q, double gamma, c128 D0, double dt,
-                                                               int nsteps, c128* snap) {
+                                                               int nsteps, c128* snap, c128* tmp_all) {
   const int ns2 = ns * ns;
   c128* A = ados + (size_t)blockIdx.x * nado * ns2;
-  const int t = threadIdx.x;
-  const bool act = t < ns2;
-  const int i = act ? t / ns : 0, j = act ? t % ns : 0;
+  c128* tmp = tmp_all + (size_t)blockIdx.x * ns2;
   auto comm = [&](const c128* X, const c128* Y, int ii, int jj) {  // (X Y - Y X)[ii][jj]
     c128 s = cmk(0, 0);
     for (int l = 0; l < ns; ++l) s = cadd(s, csub(cmul(X[ii * ns + l], Y[l * ns + jj]), cmul(Y[ii * ns + l], X[l * ns + jj])));
@@ -567,14 +566,16 @@ __global__ __launch_bounds__(256) void heom_chain_sweep_kernel(c128* ados, int n
     for (int l = 0; l < ns; ++l) s = cadd(s, cadd(cmul(X[ii * ns + l], Y[l * ns + jj]), cmul(Y[ii * ns + l], X[l * ns + jj])));
     return s;
   };
-  if (snap && act) snap[(size_t)blockIdx.x * (nsteps + 1) * ns2 + t] = A[t];
+  if (snap)
+    for (int t = threadIdx.x; t < ns2; t += blockDim.x) snap[(size_t)blockIdx.x * (nsteps + 1) * ns2 + t] = A[t];
   for (int s = 0; s < nsteps; ++s) {
     for (int n = 0; n < nado - 1; ++n) {
-      c128 v = cmk(0, 0);
-      if (act) {
+      for (int t = threadIdx.x; t < ns2; t += blockDim.x) {
+        const int i = t / ns, j = t % ns;
         const c128* xn = A + (size_t)n * ns2;
         const c128* xp = A + (size_t)(n + 1) * ns2;
         const c128 x = xn[t];
+        c128 v;
         if (n == 0) {
           v = csub(csub(x, cscale(cmuli(comm(H, xn, i, j)), dt)), cscale(comm(Q, xp, i, j), dt));
         } else {
@@ -585,12 +586,120 @@ __global__ __launch_bounds__(256) void heom_chain_sweep_kernel(c128* ados, int n
           inner = cadd(inner, cscale(mix, (double)n));
           v = cadd(x, cadd(coh, cscale(inner, dt)));
         }
+        tmp[t] = v;
       }
       __syncthreads();
-      if (act) A[(size_t)n * ns2 + t] = v;
+      for (int t = threadIdx.x; t < ns2; t += blockDim.x) A[(size_t)n * ns2 + t] = tmp[t];
       __syncthreads();
     }
-    if (snap && act) snap[((size_t)blockIdx.x * (nsteps + 1) + s + 1) * ns2 + t] = A[t];
+    if (snap)
+      for (int t = threadIdx.x; t < ns2; t += blockDim.x)
+        snap[((size_t)blockIdx.x * (nsteps + 1) + s + 1) * ns2 + t] = A[t];
+  }
+}
+
+// ---------------------------------------------------------------- any ns, any number of modes
+// Tiled stage kernel for hierarchies the register / MFMA-16 kernels do not cover (ns > 16, more than
+// DEOM_MAX_NMOD coupling operators, or K beyond their tables).  Grouping the stencil by mode m,
+//   d_n = damp_n x_n + [-i H(t) | Q_1 .. Q_M] [x_n ; Y_1 .. Y_M] + [x_n | Z_1 .. Z_M] [i H(t) ; Q_1 .. Q_M],
+//   Y_m = sum_{k: mode k = m} cL_nk x_{n-e_k} + cP_nk x_{n+e_k},   Z_m = sum_{k: mode k = m} cR_nk x_{n-e_k} - cP_nk x_{n+e_k},
+// i.e. one complex GEMM of inner dimension 2 (1 + M) ns per ADO.  One workgroup per 16 x 16 output tile of one
+// ADO (256 threads, one element each); the A / B operand tiles (16 x 16) are staged in LDS chunk by chunk, the
+// neighbour combinations Y_m / Z_m formed while loading (no scratch), H(t) = H + f_s Hdip, Q(t) = Q + f_c Qdip
+// likewise.  Same RK4 epilogue as deom_stage_kernel.  Flat-loop form (tools/cpu_emu runs it on the host).
+constexpr int DEOM_TT = 16;
+
+__global__ __launch_bounds__(256) void deom_stage_tile_kernel(DeomParams p) {
+  __shared__ c128 sA[DEOM_TT][DEOM_TT + 1];
+  __shared__ c128 sB[DEOM_TT][DEOM_TT + 1];
+  __shared__ c128 sacc[DEOM_TT * DEOM_TT];
+  const int ns = p.ns, ns2 = ns * ns, K = p.K;
+  const int nt = (ns + DEOM_TT - 1) / DEOM_TT;
+  const long tile = blockIdx.x;
+  const int tj = (int)(tile % nt), ti = (int)((tile / nt) % nt);
+  const long bn = tile / ((long)nt * nt);
+  const int n = (int)(bn % p.nmax);
+  const size_t bbase = (size_t)(bn - n) * ns2;
+  const c128* X = p.xin + bbase;
+  const c128* xn = X + (size_t)n * ns2;
+  const int* mi = p.minus + (size_t)n * K;
+  const int* pl = p.plus + (size_t)n * K;
+  const c128* cf = p.coef + (size_t)n * K * 3;
+  const int i0 = ti * DEOM_TT, j0 = tj * DEOM_TT;
+  auto hq = [&](int seg, int r, int c) {   // segment 0: H(t), segment m + 1: Q_m(t)
+    if (seg == 0) return p.Hdip ? cadd(p.H[r * ns + c], cmul(p.Hdip[r * ns + c], p.fs)) : p.H[r * ns + c];
+    const size_t o = (size_t)(seg - 1) * ns2 + r * ns + c;
+    return p.Qdip ? cadd(p.Q[o], cmul(p.Qdip[o], p.fc)) : p.Q[o];
+  };
+  auto mix = [&](int m, int r, int c, bool right) {   // Y_m (left) / Z_m (right) element (r, c)
+    c128 v = cmk(0.0, 0.0);
+    for (int k = 0; k < K; ++k) {
+      if (p.mode[k] != m) continue;
+      const int a = mi[k], b = pl[k];
+      if (a >= 0) v = cadd(v, cmul(cf[3 * k + (right ? 1 : 0)], X[(size_t)a * ns2 + r * ns + c]));
+      if (b >= 0) {
+        const c128 t = cmul(cf[3 * k + 2], X[(size_t)b * ns2 + r * ns + c]);
+        v = right ? csub(v, t) : cadd(v, t);
+      }
+    }
+    return v;
+  };
+  for (int f = threadIdx.x; f < DEOM_TT * DEOM_TT; f += blockDim.x) sacc[f] = cmk(0.0, 0.0);
+  for (int side = 0; side < 2; ++side) {
+    for (int seg = 0; seg <= p.nmod; ++seg) {
+      for (int l0 = 0; l0 < ns; l0 += DEOM_TT) {
+        __syncthreads();
+        for (int f = threadIdx.x; f < DEOM_TT * DEOM_TT; f += blockDim.x) {
+          const int r = f / DEOM_TT, c = f % DEOM_TT;
+          const int ia = i0 + r, la = l0 + c;     // A[ia][la]
+          const int lb = l0 + r, jb = j0 + c;     // B[lb][jb]
+          c128 a = cmk(0.0, 0.0), b = cmk(0.0, 0.0);
+          if (side == 0) {           // [-i H | Q_m] x [x_n ; Y_m]
+            if (ia < ns && la < ns) a = seg == 0 ? cmulmi(hq(0, ia, la)) : hq(seg, ia, la);
+            if (lb < ns && jb < ns) b = seg == 0 ? xn[lb * ns + jb] : mix(seg - 1, lb, jb, false);
+          } else {                   // [x_n | Z_m] x [i H ; Q_m]
+            if (ia < ns && la < ns) a = seg == 0 ? xn[ia * ns + la] : mix(seg - 1, ia, la, true);
+            if (lb < ns && jb < ns) b = seg == 0 ? cmuli(hq(0, lb, jb)) : hq(seg, lb, jb);
+          }
+          sA[r][c] = a;
+          sB[r][c] = b;
+        }
+        __syncthreads();
+        for (int f = threadIdx.x; f < DEOM_TT * DEOM_TT; f += blockDim.x) {
+          const int r = f / DEOM_TT, c = f % DEOM_TT;
+          c128 s = sacc[f];
+          for (int kk = 0; kk < DEOM_TT; ++kk) s = cadd(s, cmul(sA[r][kk], sB[kk][c]));
+          sacc[f] = s;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const double dt = p.dt;
+  for (int f = threadIdx.x; f < DEOM_TT * DEOM_TT; f += blockDim.x) {
+    const int i = i0 + f / DEOM_TT, j = j0 + f % DEOM_TT;
+    if (i >= ns || j >= ns) continue;
+    const size_t e = bbase + (size_t)n * ns2 + (size_t)i * ns + j;
+    const c128 d = cadd(sacc[f], cmul(p.damp[n], xn[i * ns + j]));
+    const c128 r0 = p.rho[e];
+    if (p.stage == 0) {
+      p.acc[e] = d;
+      p.xout[e] = cadd(r0, cscale(d, dt / 2));
+    } else if (p.stage == 1) {
+      p.acc[e] = cadd(p.acc[e], cscale(d, 2.0));
+      p.xout[e] = cadd(r0, cscale(d, dt / 2));
+    } else if (p.stage == 2) {
+      p.acc[e] = cadd(p.acc[e], cscale(d, 2.0));
+      p.xout[e] = cadd(r0, cscale(d, dt));
+    } else {
+      const c128 a = cadd(p.acc[e], d);
+      const c128 r1 = cadd(r0, cscale(cscale(a, dt), 1.0 / 6.0));
+      p.rho_out[e] = r1;
+      if (p.snap && n == 0) {
+        const size_t b = bn / p.nmax;
+        p.snap[(b * (p.nsteps + 1) + p.step + 1) * ns2 + i * ns + j] = r1;
+      }
+    }
   }
 }
 
@@ -659,7 +768,17 @@ int deom_launch_stage(const DeomParams& p, hipStream_t st) {
   const int wb = q.bchunk > 0 ? q.bchunk : (q.xsplit > 0 ? B / q.xsplit : 0);
   const bool uni = grp && G == 4 && bminor && q.xsplit > 0 && wb % (64 / G) == 0 && tpb % 64 == 0 &&
                    !(ue && ue[0] == '0');
+  // the tiled kernel: everything the element kernel's LDS tables (ns <= 16, nmod <= 8) do not hold
+  // (QD_DEOM_TILED=1 forces it wherever the layout allows, for tests / A/B)
+  const char* te = getenv("QD_DEOM_TILED");
+  const bool tiled = !bminor && ((!grp && !mfma && (ns > DEOM_MAX_NS || nmod > DEOM_MAX_NMOD)) || (te && te[0] == '1'));
   auto launch_stage = [&]() {
+    if (tiled) {
+      q.xsplit = 0;
+      const int nt = (ns + DEOM_TT - 1) / DEOM_TT;
+      hipLaunchKernelGGL(deom_stage_tile_kernel, dim3((unsigned)((long)B * nmax * nt * nt)), dim3(256), 0, st, q);
+      return;
+    }
     if (mfma) {
       const int wg = (int)(((long)B * nmax + 3) / 4);
       const size_t lds_m = (size_t)(256 * (1 + nmod) + 4 * 16 * 17) * sizeof(c128);
@@ -705,8 +824,7 @@ int deom_run(qd_c128* ados, int B, int nmax, int K, int ns, const int32_t* minus
   WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   QD_CHECK_ARG(ados && minus && plus && coef && damp && mode && H && Q, "qd_deom_rk4: null pointer");
   QD_CHECK_ARG(B >= 1 && nmax >= 1 && K >= 1 && nsteps >= 0, "qd_deom_rk4: bad sizes B=%d nmax=%d K=%d", B, nmax, K);
-  QD_CHECK_ARG(ns >= 1 && ns <= DEOM_MAX_NS, "qd_deom_rk4: ns=%d outside [1, %d]", ns, DEOM_MAX_NS);
-  QD_CHECK_ARG(nmod >= 1 && nmod <= DEOM_MAX_NMOD, "qd_deom_rk4: nmod=%d outside [1, %d]", nmod, DEOM_MAX_NMOD);
+  QD_CHECK_ARG(ns >= 1 && nmod >= 1, "qd_deom_rk4: ns=%d nmod=%d", ns, nmod);
   QD_CHECK_ARG(!Hdip || fsys, "qd_deom_rk4: Hdip given without fsys");
   QD_CHECK_ARG(!Qdip || fcoup, "qd_deom_rk4: Qdip given without fcoup");
   QD_CHECK_ARG(!trace || (E && ne >= 1), "qd_deom_rk4: trace requested without observables");
@@ -807,8 +925,7 @@ extern "C" int qd_deom_stage(qd_c128* rho, const qd_c128* xin, qd_c128* xout, qd
   QD_CHECK_ARG(rho && xin && acc && minus && plus && coef && damp && mode && H && Q, "qd_deom_stage: null pointer");
   QD_CHECK_ARG(stage >= 0 && stage <= 3 && (stage == 3 || xout), "qd_deom_stage: bad stage %d / null xout", stage);
   QD_CHECK_ARG(n_own >= 1 && K >= 1, "qd_deom_stage: bad sizes n_own=%d K=%d", n_own, K);
-  QD_CHECK_ARG(ns >= 1 && ns <= DEOM_MAX_NS, "qd_deom_stage: ns=%d outside [1, %d]", ns, DEOM_MAX_NS);
-  QD_CHECK_ARG(nmod >= 1 && nmod <= DEOM_MAX_NMOD, "qd_deom_stage: nmod=%d outside [1, %d]", nmod, DEOM_MAX_NMOD);
+  QD_CHECK_ARG(ns >= 1 && nmod >= 1, "qd_deom_stage: ns=%d nmod=%d", ns, nmod);
   QD_CHECK_ARG(!snap || (step >= 0 && step < nsteps), "qd_deom_stage: snapshot step %d outside [0, %d)", step, nsteps);
   DeomParams p;
   p.rho = (const c128*)rho;
@@ -879,19 +996,19 @@ extern "C" int qd_heom_chain_euler(qd_c128* ados, int B, int nado, int ns, const
   WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   QD_CHECK_ARG(ados && H && Q, "qd_heom_chain_euler: null pointer");
   QD_CHECK_ARG(B >= 1 && nado >= 2 && nsteps >= 0, "qd_heom_chain_euler: bad sizes B=%d nado=%d", B, nado);
-  QD_CHECK_ARG(ns >= 1 && ns <= 16, "qd_heom_chain_euler: ns=%d outside [1, 16]", ns);
+  QD_CHECK_ARG(ns >= 1, "qd_heom_chain_euler: ns=%d", ns);
   QD_CHECK_ARG(!obs || (E && ne >= 1), "qd_heom_chain_euler: obs requested without observables");
   hipStream_t st = (hipStream_t)stream;
   const size_t ns2 = (size_t)ns * ns;
   c128* snap = (c128*)rho_sys;
-  if (!snap && obs) {
-    void* w = nullptr;
-    int rc = workspace(WS_DEOM, (size_t)B * (nsteps + 1) * ns2 * sizeof(c128), &w, st);
-    if (rc) return rc;
-    snap = (c128*)w;
-  }
+  const size_t snap_elems = (!snap && obs) ? (size_t)B * (nsteps + 1) * ns2 : 0;
+  void* w = nullptr;
+  int rc = workspace(WS_DEOM, (snap_elems + (size_t)B * ns2) * sizeof(c128), &w, st);
+  if (rc) return rc;
+  c128* tmp = (c128*)w;
+  if (snap_elems) snap = tmp + (size_t)B * ns2;
   hipLaunchKernelGGL(heom_chain_sweep_kernel, dim3(B), dim3(256), 0, st, (c128*)ados, nado, ns, (const c128*)H,
-                     (const c128*)Q, gamma, cmk(D0_re, D0_im), dt, nsteps, snap);
+                     (const c128*)Q, gamma, cmk(D0_re, D0_im), dt, nsteps, snap, tmp);
   QD_HIP(hipGetLastError());
   if (obs) {
     const int n = B * (nsteps + 1) * ne;

@@ -279,3 +279,15 @@ def test_spo1d_any_oracle_matches_reference():
         assert relerr(psi, g[f"n{n}_psi"]) < 1e-12, n
         if len(pl):
             assert relerr(np.array(pl), g[f"n{n}_psilist"]) < 1e-12, n
+
+
+@pytest.mark.parametrize("tag", ["ex", "mild"])
+def test_heom_chain_oracle_matches_reference(tag):
+    """oracle.heom restates HEOM/heom.py:275-347 (RK4) and oqs.py:1808-1875 (Euler sweep)."""
+    from oracle import heom as oh
+    g = load_golden("heom_chain")
+    sx = np.array([[0, 1], [1, 0]], complex)
+    args = (g["H"], g["Q"], g["rho0"], [g["Q"], sx], float(g[f"{tag}_temperature"]), float(g[f"{tag}_cutoff"]),
+            float(g[f"{tag}_reorganization"]), int(g[f"{tag}_nado"]), float(g[f"{tag}_dt"]), int(g[f"{tag}_nt"]))
+    assert relerr(oh.chain_rk4(*args), g[f"{tag}_rk4"]) < 1e-12
+    assert relerr(oh.chain_euler(*args), g[f"{tag}_euler"]) < 1e-12

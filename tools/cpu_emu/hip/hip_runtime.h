@@ -66,5 +66,10 @@ inline hipError_t hipFuncSetAttribute(const void*, int, int) { return 0; }
         }                                                                          \
   } while (0)
 // DPP intrinsics: declared for the templates in qd_common.hpp; kernels that use them do not run here
-int __builtin_amdgcn_mov_dpp(int, int, int, int, bool);
-int __builtin_amdgcn_update_dpp(int, int, int, int, int, bool);
+inline int __builtin_amdgcn_mov_dpp(int v, int, int, int, bool) { abort(); return v; }
+inline int __builtin_amdgcn_update_dpp(int, int v, int, int, int, bool) { abort(); return v; }
+typedef double emu_d4 __attribute__((ext_vector_type(4)));
+inline emu_d4 __builtin_amdgcn_mfma_f64_16x16x4f64(double, double, emu_d4 c, int, int, int) { abort(); return c; }
+inline int __builtin_amdgcn_readfirstlane(int v) { return v; }
+template <typename T> T __shfl(T v, int, int = 64) { abort(); return v; }
+#define __HIP_MEMORY_SCOPE_AGENT 0
