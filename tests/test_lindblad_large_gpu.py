@@ -1,0 +1,66 @@
+"""Lindblad / Redfield beyond round 2's caps: N > 1024 (split path), more than 16 collapse
+operators and observables, many drive terms — against the oracle (oracle/lindblad.py, the restatement of
+oqs._lindblad / liouvillian, oqs.py:697-714, 1596-1696, pinned to the reference in tests/test_oracle_golden.py)."""
+import numpy as np
+import pytest
+
+from conftest import relerr
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-10
+
+
+def test_lindblad_n1100_matches_oracle():
+    """N = 1100 (padded to 1152; round 2 refused N > 1024), one collapse operator, 2 RK4 steps, 2 density matrices."""
+    import torch
+    from oracle import lindblad as olb
+    from pyqed_amd import lindblad_rk4
+    N, steps, dt = 1100, 2, 1e-2
+    H, cs = olb.synthetic_lindblad(N, nc=1)
+    rho0 = olb.random_pure_states(2, N, seed=3)
+    ref = olb.lindblad_batch(H, cs, rho0, dt, steps)
+    dev = torch.device("cuda", 0)
+    rho = torch.from_numpy(rho0.copy()).to(dev)
+    lindblad_rk4(torch.from_numpy(H).to(dev), torch.from_numpy(np.array(cs)).to(dev), rho, dt, steps)
+    assert relerr(rho.cpu().numpy(), ref) < TOL
+
+
+def test_lindblad_many_collapse_ops_and_observables_match_oracle():
+    """LindbladSolver.run with 20 collapse operators and 20 observables (N = 40, 8 steps): observables including t0
+    and the final state (oqs._lindblad contract) against the oracle's csr-free restatement."""
+    from oracle import lindblad as olb
+    from pyqed_amd import LindbladSolver
+    N, nc, ne, Nt, dt = 40, 20, 20, 8, 5e-3
+    rng = np.random.default_rng(20)
+    H, _ = olb.synthetic_lindblad(N, nc=1)
+    cs = [0.05 * (rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N))) / np.sqrt(N) for _ in range(nc)]
+    es = []
+    for _ in range(ne):
+        a = rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N))
+        es.append((a + a.conj().T) / 2)
+    rho0 = olb.random_pure_states(1, N, seed=4)[0]
+    obs_ref, rholist_ref, rho_ref = olb.lindblad(H, rho0, cs, es, Nt, dt)
+    r = LindbladSolver(H, cs).run(rho0, dt=dt, Nt=Nt, e_ops=es)
+    assert r.observables.shape == (Nt + 1, ne)
+    assert relerr(r.observables, obs_ref) < TOL
+    last = r.rholist[-1]
+    assert relerr(last.toarray() if hasattr(last, "toarray") else np.asarray(last), rho_ref) < TOL
+
+
+def test_glf_many_pairs_batch_matches_oracle():
+    """qd_lindblad_rk4 on a batch of 4 with 40 collapse operators (the persistent / split kernels' segment tables),
+    N = 64."""
+    import torch
+    from oracle import lindblad as olb
+    from pyqed_amd import lindblad_rk4
+    N, nc, B, steps, dt = 64, 40, 4, 4, 5e-3
+    rng = np.random.default_rng(40)
+    H, _ = olb.synthetic_lindblad(N, nc=1)
+    cs = np.array([0.03 * (rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N))) / np.sqrt(N)
+                   for _ in range(nc)])
+    rho0 = olb.random_pure_states(B, N, seed=5)
+    ref = olb.lindblad_batch(H, list(cs), rho0, dt, steps)
+    dev = torch.device("cuda", 0)
+    rho = torch.from_numpy(rho0.copy()).to(dev)
+    lindblad_rk4(torch.from_numpy(H).to(dev), torch.from_numpy(cs).to(dev), rho, dt, steps)
+    assert relerr(rho.cpu().numpy(), ref) < TOL
