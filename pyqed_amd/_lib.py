@@ -50,6 +50,7 @@ SIGNATURES = {
                                c_void_p, c_void_p]),
     "qd_spo2_run": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "qd_spo_expv": (c_int, [c_void_p, c_int, c_long, c_int, c_double, c_void_p, c_void_p, c_void_p]),
+    "qd_spo_expm": (c_int, [c_void_p, c_int, c_long, c_int, c_double, c_void_p, c_void_p, c_void_p]),
     "qd_spo2_run_batch": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                   c_void_p]),
     "qd_spo1d_run": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,

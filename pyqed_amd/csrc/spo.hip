@@ -1261,6 +1261,8 @@ int spo_generic_run(c128* psi, const c128* expVh, const c128* expV, const c128* 
                     const int* dims, int D, int ns, int nsteps, int nout, c128* snap, hipStream_t st);
 int spo1d_generic_run(c128* psi, const c128* expV, const c128* expVh, const c128* expK, int nx, int B, int nt,
                       int nout, c128* snap, hipStream_t st);
+int spo_expm_run(const void* v, int v_complex, int herm, long npts, int ns, double dt, c128* expV, c128* expVh,
+                 hipStream_t st);
 
 }  // namespace qd
 
@@ -1689,9 +1691,11 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
 extern "C" int qd_spo_expv(const void* v, int v_complex, long npts, int ns, double dt, qd_c128* expV_,
                            qd_c128* expVh_, void* stream) {
   QD_CHECK_ARG(v && expVh_, "qd_spo_expv: null pointer");
-  QD_CHECK_ARG(ns == 1 || ns == 2, "qd_spo_expv: ns=%d (the device build covers ns <= 2)", ns);
+  QD_CHECK_ARG(ns >= 1 && ns <= 32, "qd_spo_expv: ns=%d outside [1, 32]", ns);
   QD_CHECK_ARG(npts >= 0, "qd_spo_expv: npts=%ld", npts);
   if (npts == 0) return QD_OK;
+  if (ns > 2)   // scaling-and-squaring Taylor exponential of the Hermitian matrix eigh reads (spo_gen.hip)
+    return spo_expm_run(v, v_complex, 1, npts, ns, dt, (c128*)expV_, (c128*)expVh_, (hipStream_t)stream);
   const int grid = (int)std::min<long>((npts + 255) / 256, 8192);
   if (v_complex)
     hipLaunchKernelGGL(spo_expv_kernel<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, v, npts, ns, dt,
@@ -1701,4 +1705,13 @@ extern "C" int qd_spo_expv(const void* v, int v_complex, long npts, int ns, doub
                        (c128*)expV_, (c128*)expVh_);
   QD_HIP(hipGetLastError());
   return QD_OK;
+}
+
+extern "C" int qd_spo_expm(const qd_c128* v, int hermitian, long npts, int ns, double dt, qd_c128* expV_,
+                           qd_c128* expVh_, void* stream) {
+  QD_CHECK_ARG(v && expVh_, "qd_spo_expm: null pointer");
+  QD_CHECK_ARG(ns >= 1 && ns <= 32, "qd_spo_expm: ns=%d outside [1, 32]", ns);
+  QD_CHECK_ARG(npts >= 0, "qd_spo_expm: npts=%ld", npts);
+  if (npts == 0) return QD_OK;
+  return spo_expm_run(v, 1, hermitian ? 1 : 0, npts, ns, dt, (c128*)expV_, (c128*)expVh_, (hipStream_t)stream);
 }

@@ -398,6 +398,101 @@ __global__ __launch_bounds__(256) void spo1d_gen_kernel(Fft p, c128* psi, const 
   for (int k = threadIdx.x; k < L; k += blockDim.x) x[k] = cmul(eVh[k], cur[k]);
 }
 
+// ---------------------------------------------------------------- point propagators, any ns
+// exp(-i V tau) per grid point for the SPO build (wpd.py:585-623 SPO2, :1290-1330 SPO3: eigh -> U e^{-iw tau} U^+;
+// wpd.py:960-985 SPO2NH: eig -> U_R e^{-iw tau} U_R^-1).  Both are the matrix exponential; here it is evaluated
+// directly, by scaling and squaring a degree-18 Taylor polynomial (||X|| <= 1/2 after scaling: truncation
+// < 1e-22), so no eigenvectors are needed on the device.  exp(-i V dt) = exp(-i V dt/2)^2 (one more product).
+// herm: the Hermitian matrix LAPACK's eigh sees (lower triangle, real diagonal); otherwise the full matrix.
+// One workgroup per grid point (grid-stride), lane e = i ns + j owns element (i, j); products through LDS.
+template <bool CPLX>
+__global__ __launch_bounds__(1024) void spo_expm_kernel(const void* v_, int herm, long npts, int ns, double dt,
+                                                        c128* expV, c128* expVh) {
+  extern __shared__ c128 sm[];
+  const int ns2 = ns * ns;
+  c128* X = sm;
+  c128* T = X + ns2;
+  c128* S = T + ns2;
+  c128* W = S + ns2;
+  __shared__ int sh_s;
+  const int e = threadIdx.x;
+  const bool own = e < ns2;
+  const int i = own ? e / ns : 0, j = own ? e % ns : 0;
+  auto vat = [&](long p, int r, int c) {
+    const size_t o = (size_t)p * ns2 + (size_t)r * ns + c;
+    return CPLX ? ((const c128*)v_)[o] : cmk(((const double*)v_)[o], 0.0);
+  };
+  auto matmul = [&](const c128* A, const c128* B, c128* C, double scale) {   // C = scale A B
+    __syncthreads();
+    c128 acc = cmk(0.0, 0.0);
+    if (own)
+      for (int l = 0; l < ns; ++l) acc = cadd(acc, cmul(A[i * ns + l], B[l * ns + j]));
+    __syncthreads();
+    if (own) C[e] = cscale(acc, scale);
+    __syncthreads();
+  };
+  for (long p = blockIdx.x; p < npts; p += gridDim.x) {
+    c128 h = cmk(0.0, 0.0);
+    if (own) {
+      if (herm) {
+        if (i == j) h = cmk(vat(p, i, i).re, 0.0);
+        else h = i > j ? vat(p, i, j) : cconj(vat(p, j, i));
+      } else {
+        h = vat(p, i, j);
+      }
+    }
+    // ||V tau||_inf (max row sum), tau = dt / 2
+    const double tau = 0.5 * dt;
+    if (own) W[e] = cmk(sqrt(h.re * h.re + h.im * h.im), 0.0);
+    __syncthreads();
+    if (e < ns) {
+      double r = 0.0;
+      for (int l = 0; l < ns; ++l) r += W[e * ns + l].re;
+      T[e] = cmk(r, 0.0);
+    }
+    __syncthreads();
+    if (e == 0) {
+      double nrm = 0.0;
+      for (int l = 0; l < ns; ++l) nrm = fmax(nrm, T[l].re);
+      nrm *= fabs(tau);
+      int sq = 0;
+      while (nrm > 0.5) {
+        nrm *= 0.5;
+        ++sq;
+      }
+      sh_s = sq;
+    }
+    __syncthreads();
+    const int sq = sh_s;
+    __syncthreads();
+    const double sc = tau / (double)(1L << sq);
+    // X = -i V tau / 2^sq ; S = I + X ; T = X
+    if (own) {
+      X[e] = cmulmi(cscale(h, sc));
+      T[e] = X[e];
+      S[e] = cadd(X[e], cmk(i == j ? 1.0 : 0.0, 0.0));
+    }
+    for (int k = 2; k <= 18; ++k) {
+      matmul(T, X, W, 1.0 / k);   // W = T X / k
+      if (own) {
+        T[e] = W[e];
+        S[e] = cadd(S[e], W[e]);
+      }
+    }
+    for (int q = 0; q < sq; ++q) {
+      matmul(S, S, W, 1.0);
+      if (own) S[e] = W[e];
+    }
+    __syncthreads();
+    if (own) expVh[(size_t)p * ns2 + e] = S[e];
+    if (expV) {
+      matmul(S, S, W, 1.0);
+      if (own) expV[(size_t)p * ns2 + e] = W[e];
+    }
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------- host planning
 bool all_factors_small(int n, int maxp) {
   for (int p = 2; (long)p * p <= n; ++p)
@@ -689,6 +784,21 @@ int spo_generic_run(c128* psi, const c128* expVh, const c128* expV, const c128* 
   x.Ks = ks;
   x.Ky = expKy;
   return run_nd(x, expVh, expV, nsteps, nout, snap, expKy != nullptr);
+}
+
+// exp(-i V dt/2), exp(-i V dt) per point for any ns <= 32 (spo_expm_kernel).
+int spo_expm_run(const void* v, int v_complex, int herm, long npts, int ns, double dt, c128* expV, c128* expVh,
+                 hipStream_t st) {
+  using namespace spog;
+  const int threads = std::max(64, ((ns * ns + 63) / 64) * 64);
+  const size_t lds = (size_t)4 * ns * ns * sizeof(c128);
+  const int grid = (int)std::min<long>(npts, 16384);
+  if (v_complex)
+    hipLaunchKernelGGL(spo_expm_kernel<true>, dim3(grid), dim3(threads), lds, st, v, herm, npts, ns, dt, expV, expVh);
+  else
+    hipLaunchKernelGGL(spo_expm_kernel<false>, dim3(grid), dim3(threads), lds, st, v, herm, npts, ns, dt, expV, expVh);
+  QD_HIP(hipGetLastError());
+  return QD_OK;
 }
 
 // Generic 1D SPO.run (any nx), B wavepackets [B][nx].

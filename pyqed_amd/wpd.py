@@ -126,11 +126,11 @@ class _PointPropagators:
     """exp_V / exp_V_half of a Hermitian diabatic potential, built on the device.
 
     The reference's build (wpd.py:585-623, SPO3 :1290-1330) loops over grid points calling eigh and
-    forming U e^{-i w tau} U^+.  For ns <= 2 qd_spo_expv evaluates the same point propagators in
-    closed form on the GPU (LAPACK conventions: lower triangle, real diagonal); they stay on the
-    device for the run and are copied to the host only when exp_V / exp_V_half are read.  The
-    eigen data (d2a = U, apes = w) are host eigh results computed on first access.  ns > 2 builds
-    on the host with a vectorised eigh (setup, like the reference).
+    forming U e^{-i w tau} U^+.  qd_spo_expv evaluates the same point propagators on the GPU (LAPACK
+    conventions: lower triangle, real diagonal): in closed form for ns <= 2, as a scaling-and-squaring
+    matrix exponential for 2 < ns <= 32; they stay on the device for the run and are copied to the
+    host only when exp_V / exp_V_half are read.  The eigen data (d2a = U, apes = w) are host eigh
+    results computed on first access.  ns > 32 builds on the host with a vectorised eigh.
     """
     _eV_dev = _eVh_dev = None
     _exp_V_host = _exp_V_half_host = None
@@ -188,7 +188,7 @@ class _PointPropagators:
     def _build_point_ops(self, dt):
         v = self._pot()
         ns = v.shape[-1]
-        if ns > 2:
+        if ns > 32:   # beyond the device exponential's workgroup (ns^2 <= 1024 lanes): host eigh, as the reference
             w, u = self._host_eig()
             ud = np.conj(np.swapaxes(u, -1, -2))
             self.exp_V = (u * np.exp(-1j * w * dt)[..., None, :]) @ ud
@@ -394,21 +394,61 @@ class SPO2NH(SPO2):
         self.right_eigenstates = None
         super().__init__(x, y, *args, **kwargs)
 
+    _ur = _ovlp = None
+
     def build(self, dt):
+        """wpd.py:960-985.  exp_V = U_R e^{-i w dt} U_R^-1 is the matrix exponential exp(-i V dt); it is evaluated on
+        the GPU (qd_spo_expm, scaling and squaring, no eigenvectors) for ns <= 32.  The right eigenvectors and their
+        overlap (right_eigenstates, ovlp_rr; nonherm.eig order, eigenvalues by argsort) are host eig results made
+        on first access (position() reads ovlp_rr)."""
         nx, ny = self.nx, self.ny
         self.kx = 2. * np.pi * fftfreq(nx, interval(self.x))
         self.ky = 2. * np.pi * fftfreq(ny, interval(self.y))
         self._build_keo(dt)
         v = np.asarray(self.v, dtype=complex)
-        w, ur = np.linalg.eig(v)
+        self._ur = self._ovlp = None
+        ns = v.shape[-1]
+        if ns > 32:
+            ur = self.right_eigenstates
+            w = self._w
+            ul = np.linalg.inv(ur)
+            self.exp_V = (ur * np.exp(-1j * w * dt)[..., None, :]) @ ul
+            self.exp_V_half = (ur * np.exp(-1j * w * dt / 2)[..., None, :]) @ ul
+            return
+        dev = default_device()
+        _lib.ensure_device(dev)
+        vd = _dev_c128(v, dev)
+        eV = torch.empty(v.shape, dtype=torch.complex128, device=dev)
+        eVh = torch.empty_like(eV)
+        with torch.cuda.device(dev):
+            rc = _lib.load().qd_spo_expm(vd.data_ptr(), 0, int(v.size // (ns * ns)), ns, float(dt), eV.data_ptr(),
+                                         eVh.data_ptr(), _lib.stream_ptr(dev))
+        _lib.check(rc, "qd_spo_expm")
+        self.exp_V, self.exp_V_half = None, None
+        self._eV_dev, self._eVh_dev = eV, eVh
+
+    def _host_eig_nh(self):
+        w, ur = np.linalg.eig(np.asarray(self.v, dtype=complex))
         idx = np.argsort(w, axis=-1)
-        w = np.take_along_axis(w, idx, axis=-1)
-        ur = np.take_along_axis(ur, idx[..., None, :], axis=-1)
-        ul = np.linalg.inv(ur)
-        self.right_eigenstates = ur
-        self.ovlp_rr = np.conj(np.swapaxes(ur, -1, -2)) @ ur
-        self.exp_V = (ur * np.exp(-1j * w * dt)[..., None, :]) @ ul
-        self.exp_V_half = (ur * np.exp(-1j * w * dt / 2)[..., None, :]) @ ul
+        self._w = np.take_along_axis(w, idx, axis=-1)
+        self._ur = np.take_along_axis(ur, idx[..., None, :], axis=-1)
+        self._ovlp = np.conj(np.swapaxes(self._ur, -1, -2)) @ self._ur
+
+    @property
+    def right_eigenstates(self):
+        if self._ur is None and getattr(self, "v", None) is not None:
+            self._host_eig_nh()
+        return self._ur
+
+    @right_eigenstates.setter
+    def right_eigenstates(self, u):
+        self._ur = u
+
+    @property
+    def ovlp_rr(self):
+        if self._ovlp is None and getattr(self, "v", None) is not None:
+            self._host_eig_nh()
+        return self._ovlp
 
     def position(self, psilist):
         """wpd.py:997-1017 (no plot, no xAve.npz file)."""
