@@ -787,6 +787,111 @@ def bench_deom(dev, steps, batch):
     }
 
 
+def time_reduce_one_rank(dev, reps=50):
+    """One 1 MiB RCCL reduce(sum) (the 256 x 256 c128 2DES grid) on a one-rank communicator through the C-ABI
+    (qd_comm_init / qd_reduce_sum), HIP events on the launch stream: the per-grid RCCL launch cost that the 8-GPU
+    projection adds (one rank cannot time the xGMI transfer itself)."""
+    import ctypes
+    import torch
+    from pyqed_amd import _lib
+    lib = _lib.load()
+    uid = ctypes.create_string_buffer(128)
+    _lib.check(lib.qd_comm_unique_id(uid), "qd_comm_unique_id")
+    _lib.check(lib.qd_comm_init(1, 0, uid), "qd_comm_init")
+    try:
+        x = torch.zeros(256 * 256, dtype=torch.complex128, device=dev)
+        st = _lib.stream_ptr(dev)
+        for _ in range(5):
+            _lib.check(lib.qd_reduce_sum(x.data_ptr(), x.numel(), 0, st), "qd_reduce_sum")
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            _lib.check(lib.qd_reduce_sum(x.data_ptr(), x.numel(), 0, st), "qd_reduce_sum")
+        e1.record()
+        torch.cuda.synchronize(dev)
+        return e0.elapsed_time(e1) / reps
+    finally:
+        _lib.check(lib.qd_comm_destroy(), "qd_comm_destroy")
+
+
+def _deom_banded_cases():
+    """(name, solver, rho0, dt) of the tier-banded leg: BASELINE.json configs[3] (spin-boson, ns = 2, L = 12, K = 5,
+    6188 ADOs) and a capacity-style hierarchy whose per-ADO work is ns^3-heavy (ns = 96 GUE H, Q = diag, Drude
+    npsd = 3 -> K = 4, L = 4: 70 ADOs of 147 KB, 10.3 MB of state; the tiled stage kernel)."""
+    import sympy as sp
+    from pyqed_amd.deom import Bath, DEOMSolver
+    w = sp.symbols(r"\omega", real=True)
+    sx = np.array([[0, 1], [1, 0]], complex)
+    sz = np.diag([1.0, -1.0]).astype(complex)
+    r0 = np.zeros((2, 2), complex)
+    r0[0, 0] = 1
+    bath = Bath([2 * 0.5 * 1.0 * w / (1.0 + w ** 2)], w, [1.0], [4], [0] * 5)
+    cases = [("spin_boson_L12_K5 (configs[3])", DEOMSolver(sz + sx, None, bath, np.array([sx]), None, None, None, 12),
+              r0, 0.002)]
+    ns = 96
+    rng = np.random.default_rng(96)
+    a = rng.standard_normal((ns, ns)) + 1j * rng.standard_normal((ns, ns))
+    H = (a + a.conj().T) / 2 / np.sqrt(ns)
+    Q = np.diag(np.linspace(-1, 1, ns)).astype(complex)
+    bath3 = Bath([2 * 0.3 * w / (1.0 + w ** 2)], w, [1.0], [3], [0] * 4)
+    rb = np.zeros((ns, ns), complex)
+    rb[0, 0] = 1
+    cases.append((f"ns{ns}_L4_K4", DEOMSolver(H, None, bath3, np.array([Q]), None, None, None, 4), rb, 0.002))
+    return cases
+
+
+def bench_deom_banded(dev, world, rank, steps=40):
+    """ONE hierarchy tier-banded over the ranks (BASELINE.json configs[3]: "ADOs sharded over
+    8xMI355X via xGMI"): one band per rank, one RCCL all-gather of the bands' export rows per RK4 stage
+    (deom_shard.CollectiveExchange), HIP stage kernels per band.  World 1: the same 8-band partition in one process
+    (LoopbackExchange, device-side copies) so the halo cost is known without a second GPU.  Timed: `steps` RK4 steps
+    of device-resident bands between barriers + device syncs, max over ranks; beside it the unbanded qd_deom_rk4 rate
+    of the same hierarchy on one GPU (rank 0)."""
+    import torch
+    import torch.distributed as dist
+    from pyqed_amd.deom_shard import ShardedDEOM, run_bands
+    out = {}
+    for name, sol, rho0, dt in _deom_banded_cases():
+        sol.check_()
+        sol.init_()
+        single = None
+        if rank == 0:   # the unbanded kernel sequence on this GPU, device-resident state, HIP events
+            Qm = np.asarray(sol.coupling, dtype=complex).reshape(-1, sol.nsys, sol.nsys)
+            single = 1e3 / _deom_event_rate(dev, sol, sol.bath, np.asarray(sol.system, complex), Qm, 1, steps, dt)
+        nb = world if world > 1 else 8
+        sh = ShardedDEOM(sol, nbands=nb, loopback=world == 1, device=dev, exchange="allgather")
+        fs, fc = sh.setup(dt, steps)
+        run_bands(sh.bands, sh.exchange, rho0, dt, 2, fs, fc)          # warm-up
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        run_bands(sh.bands, sh.exchange, rho0, dt, steps, fs, fc)
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        ns = sol.nsys
+        halo = [len(p.halo) for p in sh.plans]
+        own = [p.n_own for p in sh.plans]
+        ent = {"nmax": sol.nmax, "ns": ns, "K": sol.nind, "L": sol.lmax, "bands": nb,
+               "exchange": "loopback (device copies, one GPU)" if world == 1 else "RCCL all-gather per stage",
+               "ms_per_step": round(el / steps * 1e3, 4), "steps": steps,
+               "ado_steps_per_s": round(sol.nmax * steps / el, 1),
+               "max_halo_over_owned": round(max(h / o for h, o in zip(halo, own)), 3),
+               "state_bytes": sol.nmax * ns * ns * 16}
+        if world > 1:
+            ent["allgather_bytes_per_stage"] = sh.exchange.bytes_per_exchange
+        if single is not None:
+            ent["one_gpu_unbanded_ms_per_step"] = round(single, 4)
+            ent["speedup_vs_one_gpu"] = round(single / (el / steps * 1e3), 3)
+        out[name] = ent
+    return out
+
+
 def cpu_baseline_deom(budget_s=8.0):
     import sympy as sp
     from oracle import deom as od
@@ -830,6 +935,7 @@ def main():
     ap.add_argument("--deom-steps", type=int, default=200)
     ap.add_argument("--deom-batch", type=int, default=64)
     ap.add_argument("--no-deom", action="store_true")
+    ap.add_argument("--no-deom-banded", action="store_true", help="skip the tier-banded DEOM leg")
     ap.add_argument("--no-redfield", action="store_true")
     ap.add_argument("--no-superop", action="store_true")
     args = ap.parse_args()
@@ -925,6 +1031,18 @@ def main():
                 "members": args.ens // 8, "ms_per_grid": shard["ms_per_grid"],
                 "event_ms_per_grid": shard["event_ms_per_grid"], "roofline": shard["roofline"],
                 "projected_8gpu_speedup_compute_only": round(twodes["ms_per_grid"] / shard["ms_per_grid"], 3)}
+            try:
+                red = time_reduce_one_rank(dev)
+                sh8 = twodes["shard_1of8"]
+                sh8["reduce_1mib_one_rank_ms"] = round(red, 4)
+                # serial bound (reduce after every grid) and the pipelined one (ReducePipeline overlaps grid i's
+                # reduce with grid i + 1's compute, so the slower of the two paces the grids)
+                sh8["projected_8gpu_speedup_serial_reduce"] = round(twodes["ms_per_grid"] / (shard["ms_per_grid"] + red),
+                                                                    3)
+                sh8["projected_8gpu_speedup_pipelined"] = round(twodes["ms_per_grid"] / max(shard["ms_per_grid"], red),
+                                                                3)
+            except Exception as e:  # noqa: BLE001 (the projection is informational)
+                twodes["shard_1of8"]["reduce_error"] = f"{type(e).__name__}: {e}"
         if args.t2 > 0:
             twodes["t2scan"] = bench_2des_t2scan(dev, world, rank, args.ens, args.t2, args.t2_reps)
 
@@ -960,6 +1078,14 @@ def main():
     deom = None
     if not args.no_deom:
         deom = guarded(bench_deom, dev, args.deom_steps, args.deom_batch)
+
+    # one hierarchy tier-banded over the ranks (collective: every rank takes part; world 1: 8-band loopback)
+    deom_banded = None
+    if not args.no_deom and not args.no_deom_banded:
+        if world > 1:
+            deom_banded = bench_deom_banded(dev, world, rank)
+        else:
+            deom_banded = guarded(bench_deom_banded, dev, world, rank)
 
     if rank == 0:
         total_dm_steps = B * args.steps * world
@@ -1041,6 +1167,8 @@ def main():
             if world == 1 and not args.no_cpu and "error" not in deom:
                 deom["cpu_baseline"] = cpu_baseline_deom()
             out.setdefault("secondary", {})["deom"] = deom
+        if deom_banded is not None:
+            out.setdefault("secondary", {})["deom_banded"] = deom_banded
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

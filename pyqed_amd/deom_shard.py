@@ -180,6 +180,58 @@ class TorchExchange:
                 w.wait()
 
 
+class CollectiveExchange:
+    """Halo exchange as ONE all-gather per stage (one band per rank): every rank packs the union of its owned rows
+    any peer reads (its export set, padded to the largest export of all bands), all ranks all-gather those, and each
+    rank copies its halo rows out of the gathered block with one precomputed index (torch index_select).  More bytes
+    than the point-to-point exchange (every rank receives every export set), but a single standard collective per
+    stage (RCCL all-gather over xGMI with "nccl"), no send / recv pairing to get wrong; the bench's multi-GPU leg
+    uses it."""
+
+    def __init__(self, plans, rank, ns, device, group=None):
+        self.group, self.rank, self.ns = group, rank, ns
+        self.dev = torch.device(device)
+        exp = []
+        for p in plans:
+            rows = np.unique(np.concatenate(list(p.send.values()))) if p.send else np.zeros(0, np.int32)
+            exp.append(rows.astype(np.int32))
+        self.E = max(1, max(len(e) for e in exp))
+        self.world = len(plans)
+        me = plans[rank]
+        idx = []
+        for q in sorted(me.recv):
+            pos = np.searchsorted(exp[q], plans[q].send[rank])
+            idx.append(q * self.E + pos)
+        self.n_halo = len(me.halo)
+        self.halo_idx = torch.from_numpy(np.concatenate(idx).astype(np.int64) if idx else np.zeros(0, np.int64)).to(
+            self.dev)
+        self.export = torch.from_numpy(exp[rank]).to(self.dev)
+        z = lambda n: torch.zeros((n, ns, ns), dtype=torch.complex128, device=self.dev)
+        self.sendbuf, self.recvbuf = z(self.E), z(self.world * self.E)
+        self.bytes_per_exchange = self.world * self.E * ns * ns * 16
+
+    def __call__(self, bands, name):
+        import torch.distributed as dist
+        (b,) = bands
+        src = b.bufs[name]
+        n = len(self.export)
+        if n:
+            if self.dev.type == "cuda":
+                with torch.cuda.device(self.dev):
+                    rc = _lib.load().qd_gather_rows(src.data_ptr(), self.export.data_ptr(), n, self.ns * self.ns,
+                                                    self.sendbuf.data_ptr(), _lib.stream_ptr(self.dev))
+                _lib.check(rc, "qd_gather_rows")
+            else:
+                torch.index_select(src, 0, self.export.long(), out=self.sendbuf[:n])
+        if dist.get_backend(self.group) == "nccl":
+            dist.all_gather_into_tensor(self.recvbuf, self.sendbuf, group=self.group)
+        else:
+            dist.all_gather(list(self.recvbuf.chunk(self.world)), self.sendbuf, group=self.group)
+        if self.n_halo:
+            n0 = b.plan.n_own
+            src[n0:n0 + self.n_halo] = torch.index_select(self.recvbuf, 0, self.halo_idx)
+
+
 class LoopbackExchange:
     """All bands in one process: each band's halo rows are copied from the owners' packed rows (same plans)."""
 
@@ -219,7 +271,8 @@ class ShardedDEOM:
     run(rho0, dt, nt, p1) returns (t_save, Tr(p1 rho_0) [nt+1] or rho_0 stack [nt+1, ns, ns]) on the rank owning
     ADO 0 (rank 0) and (t_save, None) elsewhere; gather_ados() assembles the final hierarchy on rank 0."""
 
-    def __init__(self, solver, nbands=None, loopback=None, device=None, group=None, stage_fn=None):
+    def __init__(self, solver, nbands=None, loopback=None, device=None, group=None, stage_fn=None,
+                 exchange="p2p"):
         from .deom import ado_coefficients
         solver.check_()
         solver.init_()
@@ -239,9 +292,14 @@ class ShardedDEOM:
                                                 np.asarray(b.etaa), np.asarray(b.expn), solver.lmax)
         self.plans = make_plans(solver._minus, solver._plus, self.nbands)
         self.group, self.stage_fn = group, stage_fn
+        if exchange not in ("p2p", "allgather"):
+            raise ValueError(f"exchange must be 'p2p' or 'allgather', got {exchange!r}")
+        self.exchange_kind = exchange
         self.bands = None
+        self.exchange = None
 
-    def run(self, rho0, dt, nt, p1=None):
+    def setup(self, dt, nt):
+        """Bands (tables and state on the device) and the exchange for an nt-step run; returns the pulse tables."""
         s = self.solver
         ns = s.nsys
         Q = np.asarray(s.coupling, dtype=complex).reshape(-1, ns, ns)
@@ -250,8 +308,20 @@ class ShardedDEOM:
         mine = self.plans if self.loopback else [self.plans[self.rank]]
         self.bands = [DeomBand(p, self.coef, self.damp, np.asarray(s.bath.mode), s.system, Q, Hdip, Qdip, ns, nt,
                                self.device, self.stage_fn) for p in mine]
-        exch = LoopbackExchange() if self.loopback else TorchExchange(self.group)
-        run_bands(self.bands, exch, rho0, dt, nt, fs, fc)
+        if self.loopback:
+            exch = LoopbackExchange()
+        elif self.exchange_kind == "allgather":
+            exch = CollectiveExchange(self.plans, self.rank, ns, self.device, self.group)
+        else:
+            exch = TorchExchange(self.group)
+        self.exchange = exch
+        return fs, fc
+
+    def run(self, rho0, dt, nt, p1=None):
+        s = self.solver
+        ns = s.nsys
+        fs, fc = self.setup(dt, nt)
+        run_bands(self.bands, self.exchange, rho0, dt, nt, fs, fc)
         t_save = np.arange(nt + 1) * dt
         root = [b for b in self.bands if b.plan.lo == 0]
         if not root:

@@ -363,3 +363,42 @@ def test_deom_tier_bands_subgroup_gloo():
     assert res[0][1] is None and res[2][1] is None and res[2][2] is None
     assert np.allclose(res[1][1], tr_ref, rtol=1e-12, atol=1e-13)
     assert np.allclose(res[1][2], ados_ref, rtol=1e-11, atol=1e-13)
+
+
+def _worker_deom_bands_allgather(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pyqed_amd.deom_shard import ShardedDEOM
+    sol, *_, rho0 = _deom_model()
+    sh = ShardedDEOM(sol, stage_fn=_host_stage, device="cpu", exchange="allgather")
+    P1 = np.diag([1.0, 0, 0]).astype(complex)
+    t, tr = sh.run(rho0, 0.01, 6, P1)
+    ados = sh.gather_ados()
+    q.put((rank, tr, ados, sh.exchange.E, sh.exchange.n_halo))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_deom_tier_bands_allgather_gloo():
+    """The bench's multi-GPU DEOM exchange (CollectiveExchange: one all-gather of every band's export rows per stage,
+    halo rows picked by a precomputed index) over 3 gloo ranks equals the single-process oracle run."""
+    from oracle import deom as od
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_deom_bands_allgather, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sol, bath, H, Qm, sdip, cdip, fs, fc, rho0 = _deom_model()
+    P1 = np.diag([1.0, 0, 0]).astype(complex)
+    _, tr_ref, ados_ref = od.run(H, sdip, fs, np.array([Qm]), cdip, fc, (bath.etal, bath.etar, bath.etaa, bath.expn),
+                                 4, rho0, 0.01, 6, P1)
+    assert np.allclose(res[0][1], tr_ref, rtol=1e-12, atol=1e-13)
+    assert np.allclose(res[0][2], ados_ref, rtol=1e-11, atol=1e-13)
+    assert all(r[4] > 0 for r in res)          # every band has halo rows
