@@ -703,6 +703,109 @@ __global__ __launch_bounds__(256) void deom_stage_tile_kernel(DeomParams p) {
   }
 }
 
+// MFMA form of the tiled kernel (same regrouping, same epilogue) for ns >= 17: one wave per 16 x 16 output tile,
+// the four waves of a workgroup on a 2 x 2 block of tiles of one ADO (their A / B strips meet in the CU's L1).  Each
+// 16-wide chunk of the inner dimension is 4 v_mfma_f64_16x16x4_f64 k-steps x 4 real products; lane l holds
+// A[i0 + (l & 15)][l0 + 4q + (l >> 4)] and B[l0 + 4q + (l >> 4)][j0 + (l & 15)] (the layouts of
+// deom_stage_mfma16_kernel), D rows (l >> 4) + 4r, column l & 15.  Y_m / Z_m elements are formed from the
+// neighbours while loading (wave-uniform k loop, scalar table loads).
+__global__ __launch_bounds__(256) void deom_stage_tmfma_kernel(DeomParams p) {
+  const int ns = p.ns, ns2 = ns * ns, K = p.K;
+  const int nt = (ns + 15) / 16, nbk = (nt + 1) / 2;
+  const long blk = blockIdx.x;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int bj = (int)(blk % nbk), bi = (int)((blk / nbk) % nbk);
+  const long bn = __builtin_amdgcn_readfirstlane((int)(blk / ((long)nbk * nbk)));
+  const int ti = 2 * bi + (wv >> 1), tj = 2 * bj + (wv & 1);
+  if (ti >= nt || tj >= nt) return;          // wave-uniform; no workgroup barrier below
+  const int n = (int)(bn % p.nmax);
+  const size_t bbase = (size_t)(bn - n) * ns2;
+  const c128* X = p.xin + bbase;
+  const c128* xn = X + (size_t)n * ns2;
+  const int* mi = p.minus + (size_t)n * K;
+  const int* pl = p.plus + (size_t)n * K;
+  const c128* cf = p.coef + (size_t)n * K * 3;
+  const int i0 = ti * 16, j0 = tj * 16;
+  const int lr = lane & 15, rq = lane >> 4;
+  auto hq = [&](int seg, int r, int c) -> c128 {
+    if (r >= ns || c >= ns) return cmk(0.0, 0.0);
+    if (seg == 0) return p.Hdip ? cadd(p.H[r * ns + c], cmul(p.Hdip[r * ns + c], p.fs)) : p.H[r * ns + c];
+    const size_t o = (size_t)(seg - 1) * ns2 + r * ns + c;
+    return p.Qdip ? cadd(p.Q[o], cmul(p.Qdip[o], p.fc)) : p.Q[o];
+  };
+  auto xat = [&](int r, int c) -> c128 { return (r < ns && c < ns) ? xn[r * ns + c] : cmk(0.0, 0.0); };
+  auto mix = [&](int m, int r, int c, bool right) -> c128 {
+    c128 v = cmk(0.0, 0.0);
+    if (r >= ns || c >= ns) return v;
+    for (int k = 0; k < K; ++k) {
+      if (p.mode[k] != m) continue;
+      const int a = mi[k], b = pl[k];
+      if (a >= 0) v = cadd(v, cmul(cf[3 * k + (right ? 1 : 0)], X[(size_t)a * ns2 + r * ns + c]));
+      if (b >= 0) {
+        const c128 t = cmul(cf[3 * k + 2], X[(size_t)b * ns2 + r * ns + c]);
+        v = right ? csub(v, t) : cadd(v, t);
+      }
+    }
+    return v;
+  };
+  d4 Dre = d4{0.0, 0.0, 0.0, 0.0}, Dim = d4{0.0, 0.0, 0.0, 0.0};
+  auto cmfma = [&](c128 a, c128 b) {
+    Dre = __builtin_amdgcn_mfma_f64_16x16x4f64(a.re, b.re, Dre, 0, 0, 0);
+    Dim = __builtin_amdgcn_mfma_f64_16x16x4f64(a.re, b.im, Dim, 0, 0, 0);
+    Dre = __builtin_amdgcn_mfma_f64_16x16x4f64(-a.im, b.im, Dre, 0, 0, 0);
+    Dim = __builtin_amdgcn_mfma_f64_16x16x4f64(a.im, b.re, Dim, 0, 0, 0);
+  };
+  for (int seg = 0; seg <= p.nmod; ++seg) {
+    for (int l0 = 0; l0 < ns; l0 += 16) {
+      c128 a[4], b[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {   // left: [-iH | Q_m] x [x_n ; Y_m]
+        const int l = l0 + 4 * q + rq;
+        a[q] = seg == 0 ? cmulmi(hq(0, i0 + lr, l)) : hq(seg, i0 + lr, l);
+        b[q] = seg == 0 ? xat(l, j0 + lr) : mix(seg - 1, l, j0 + lr, false);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cmfma(a[q], b[q]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {   // right: [x_n | Z_m] x [iH ; Q_m]
+        const int l = l0 + 4 * q + rq;
+        a[q] = seg == 0 ? xat(i0 + lr, l) : mix(seg - 1, i0 + lr, l, true);
+        b[q] = seg == 0 ? cmuli(hq(0, l, j0 + lr)) : hq(seg, l, j0 + lr);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cmfma(a[q], b[q]);
+    }
+  }
+  const double dt = p.dt;
+  const c128 dmp = p.damp[n];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = i0 + rq + 4 * r, j = j0 + lr;
+    if (i >= ns || j >= ns) continue;
+    const size_t e = bbase + (size_t)n * ns2 + (size_t)i * ns + j;
+    const c128 d = cadd(cmk(Dre[r], Dim[r]), cmul(dmp, xn[i * ns + j]));
+    const c128 r0 = p.rho[e];
+    if (p.stage == 0) {
+      p.acc[e] = d;
+      p.xout[e] = cadd(r0, cscale(d, dt / 2));
+    } else if (p.stage == 1) {
+      p.acc[e] = cadd(p.acc[e], cscale(d, 2.0));
+      p.xout[e] = cadd(r0, cscale(d, dt / 2));
+    } else if (p.stage == 2) {
+      p.acc[e] = cadd(p.acc[e], cscale(d, 2.0));
+      p.xout[e] = cadd(r0, cscale(d, dt));
+    } else {
+      const c128 a = cadd(p.acc[e], d);
+      const c128 r1 = cadd(r0, cscale(cscale(a, dt), 1.0 / 6.0));
+      p.rho_out[e] = r1;
+      if (p.snap && n == 0) {
+        const size_t b = bn / p.nmax;
+        p.snap[(b * (p.nsteps + 1) + p.step + 1) * ns2 + i * ns + j] = r1;
+      }
+    }
+  }
+}
+
 }  // namespace
 }  // namespace qd
 
@@ -775,6 +878,13 @@ int deom_launch_stage(const DeomParams& p, hipStream_t st) {
   auto launch_stage = [&]() {
     if (tiled) {
       q.xsplit = 0;
+      // ns >= 17: MFMA tiles (QD_DEOM_TMFMA=0 keeps the VALU tile kernel, for A/B runs and tests)
+      const char* tm = getenv("QD_DEOM_TMFMA");
+      if (ns >= 17 && !(tm && tm[0] == '0')) {
+        const int nt = (ns + 15) / 16, nbk = (nt + 1) / 2;
+        hipLaunchKernelGGL(deom_stage_tmfma_kernel, dim3((unsigned)((long)B * nmax * nbk * nbk)), dim3(256), 0, st, q);
+        return;
+      }
       const int nt = (ns + DEOM_TT - 1) / DEOM_TT;
       hipLaunchKernelGGL(deom_stage_tile_kernel, dim3((unsigned)((long)B * nmax * nt * nt)), dim3(256), 0, st, q);
       return;

@@ -47,9 +47,13 @@ def _check(ns, L, nbath=1, npsd=2, nt=5, dt=0.01):
     assert relerr(sol.ddos, ados_ref) < TOL
 
 
-@pytest.mark.parametrize("ns,L", [(24, 3), (40, 2), (17, 2)])
-def test_deom_large_ns_matches_oracle(ns, L):
-    """ns = 24 / 40 / 17 (K = 3 Pade terms, driven H(t) and Q(t)): tiles of 16 with ragged edges."""
+@pytest.mark.parametrize("ns,L,tmfma", [(24, 3, None), (40, 2, None), (17, 2, None), (33, 2, None), (24, 3, "0"),
+                                        (40, 2, "0")])
+def test_deom_large_ns_matches_oracle(ns, L, tmfma, monkeypatch):
+    """ns = 17 / 24 / 33 / 40 (K = 3 Pade terms, driven H(t) and Q(t)): 16 x 16 MFMA tiles in 2 x 2 blocks with
+    ragged edges (deom_stage_tmfma_kernel), and the VALU tile kernel (QD_DEOM_TMFMA=0)."""
+    if tmfma is not None:
+        monkeypatch.setenv("QD_DEOM_TMFMA", tmfma)
     _check(ns, L)
 
 
