@@ -927,7 +927,10 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
     // 64-blocks are no better overall (172k / 231k / 232k / 247k).  QD_GLF_HSPLIT_MAX / _BT override (A/B).
     const char* hme = std::getenv("QD_GLF_HSPLIT_MAX");
     const int hmax = hme ? std::atoi(hme) : 208;
-    if (herm && src == GLF_FROM_LINDBLAD && Np == 128 && B < hmax && !(hse && hse[0] == '0')) {
+    // Np = 64 only on request (QD_GLF_HSPLIT_NP64=1) until its crossover is measured
+    const char* h64 = std::getenv("QD_GLF_HSPLIT_NP64");
+    const bool np_ok = Np == 128 || (Np == 64 && h64 && h64[0] == '1');
+    if (herm && src == GLF_FROM_LINDBLAD && np_ok && B < hmax && !(hse && hse[0] == '0')) {
       hsplit = true;
       split_bt = 32;
       if (const char* e = std::getenv("QD_GLF_HSPLIT_BT")) split_bt = std::atoi(e) == 64 && Np % 64 == 0 ? 64 : 32;
