@@ -207,6 +207,8 @@ def test_lindblad_hermitian_split_path(N, nc, B, bt, monkeypatch):
     (QD_GLF_HSPLIT=0) and the general kernel, exactly Hermitian, with observables and snapshots."""
     if bt is not None:
         monkeypatch.setenv("QD_GLF_HSPLIT_BT", bt)
+    if N <= 64:   # N_p = 64 runs the pair-block path only on request (the general split-K path is faster there)
+        monkeypatch.setenv("QD_GLF_HSPLIT_NP64", "1")
     import torch
     from oracle import lindblad as olb
     from pyqed_amd import lindblad_rk4
@@ -434,3 +436,19 @@ def test_workspace_bounded_over_many_streams():
         del s
     assert reserved[0] > 0
     assert max(reserved) <= 2 * reserved[0], reserved
+
+
+@pytest.mark.parametrize("N,B", [(64, 24), (48, 100), (64, 200)])
+def test_lindblad_np64_hermitian_dispatch_matches_oracle(N, B):
+    """Default dispatch for exactly Hermitian batches at N_p = 64 (the general split-K path below 160 matrices, the
+    persistent Hermitian kernel above; profiles/r03/lindblad/hsplit_np64_sweep.txt) against the oracle."""
+    import torch
+    from oracle import lindblad as olb
+    from pyqed_amd import lindblad_rk4
+    H, cs = olb.synthetic_lindblad(N, nc=1)
+    rho0 = olb.random_pure_states(B, N, seed=N + B)
+    ref = olb.lindblad_batch(H, cs, rho0[:3], 1e-2, 5)
+    dev = torch.device("cuda", 0)
+    rho = torch.from_numpy(rho0.copy()).to(dev)
+    lindblad_rk4(torch.from_numpy(H).to(dev), torch.from_numpy(np.array(cs)).to(dev), rho, 1e-2, 5)
+    assert relerr(rho.cpu().numpy()[:3], ref) < TOL
