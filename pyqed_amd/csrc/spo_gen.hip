@@ -30,6 +30,7 @@
 #include "qd_common.hpp"
 
 #include <cstdlib>
+#include <functional>
 #include <vector>
 
 namespace qd {
@@ -57,6 +58,7 @@ enum Flags { F_INV = 1, F_PT1 = 2, F_SNAP = 4, F_PT2 = 8, F_FWD = 16, F_KY = 32,
 struct AxisArgs {
   c128* psi;
   int O, L, I, C, G, flags, ns;
+  int twl;             // 1: twiddles staged in LDS (M more c128 of dynamic LDS)
   const c128* U1;      // [points][ns][ns] (F_PT1)
   const c128* U2;      // (F_PT2)
   c128* snap;          // (F_SNAP) same layout as psi
@@ -142,9 +144,9 @@ __device__ __forceinline__ void stage(const c128* __restrict__ src, c128* __rest
 // Mixed-radix transform of nl lines (cur -> result in cur; oth is the ping-pong buffer).  Every thread
 // of the workgroup must call it (barriers); it starts and ends behind a barrier.
 template <bool INV>
-__device__ __forceinline__ void stockham(const Fft& p, c128*& cur, c128*& oth, int nl, int M) {
+__device__ __forceinline__ void stockham(const Fft& p, const c128* tw, c128*& cur, c128*& oth, int nl, int M) {
   for (int s = 0; s < p.nst; ++s) {
-    stage<INV>(cur, oth, nl, M, p.R[s], p.Ns[s], p.tw);
+    stage<INV>(cur, oth, nl, M, p.R[s], p.Ns[s], tw);
     __syncthreads();
     c128* t = cur;
     cur = oth;
@@ -155,7 +157,7 @@ __device__ __forceinline__ void stockham(const Fft& p, c128*& cur, c128*& oth, i
 // Length-L DFT (INV: conjugate kernel, no scaling) of nl lines held in the first L slots of each M-slot
 // line of cur.  Result in cur (first L slots).
 template <bool INV>
-__device__ __forceinline__ void lds_fft(const Fft& p, c128*& cur, c128*& oth, int nl) {
+__device__ __forceinline__ void lds_fft(const Fft& p, const c128* tw, c128*& cur, c128*& oth, int nl) {
   const int M = p.M, L = p.L;
   if (p.kind == BLUESTEIN) {
     const int tot = nl * M;
@@ -170,14 +172,14 @@ __device__ __forceinline__ void lds_fft(const Fft& p, c128*& cur, c128*& oth, in
       cur[f] = v;
     }
     __syncthreads();
-    stockham<false>(p, cur, oth, nl, M);
+    stockham<false>(p, tw, cur, oth, nl, M);
     for (int f = threadIdx.x; f < tot; f += blockDim.x) {
       c128 b = p.bhat[f % M];
       if (INV) b = cconj(b);
       cur[f] = cmul(cur[f], b);
     }
     __syncthreads();
-    stockham<true>(p, cur, oth, nl, M);
+    stockham<true>(p, tw, cur, oth, nl, M);
     for (int f = threadIdx.x; f < tot; f += blockDim.x) {
       const int n = f % M;
       if (n < L) {
@@ -188,7 +190,7 @@ __device__ __forceinline__ void lds_fft(const Fft& p, c128*& cur, c128*& oth, in
     }
     __syncthreads();
   } else {
-    stockham<INV>(p, cur, oth, nl, M);
+    stockham<INV>(p, tw, cur, oth, nl, M);
   }
 }
 
@@ -199,6 +201,13 @@ __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
   const int nl = G * C;
   c128* cur = sm;
   c128* oth = sm + (size_t)nl * M;
+  // twiddles: staged in LDS behind the two line buffers when the host reserved room (a.twl), else read from HBM/L2
+  const c128* tw = p.tw;
+  if (a.twl) {
+    c128* stw = oth + (size_t)nl * M;
+    for (int m = threadIdx.x; m < M; m += blockDim.x) stw[m] = p.tw[m];
+    tw = stw;
+  }
   const int o0 = blockIdx.x * G, i0 = blockIdx.y * C;
   const int gv = min(G, a.O - o0), cv = min(C, I - i0);
   const int tot = G * L * C;
@@ -208,7 +217,7 @@ __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
         (g < gv && c < cv) ? a.psi[((size_t)(o0 + g) * L + e) * I + i0 + c] : cmk(0.0, 0.0);
   }
   __syncthreads();
-  if (a.flags & F_INV) lds_fft<true>(p, cur, oth, nl);
+  if (a.flags & F_INV) lds_fft<true>(p, tw, cur, oth, nl);
   auto point_op = [&](const c128* U) {   // C == I == ns: line g * ns + s holds state s of row g
     const int ns = a.ns;
     const int n = G * L * ns;
@@ -233,7 +242,7 @@ __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
     }
   }
   if (a.flags & F_PT2) point_op(a.U2);
-  if (a.flags & F_FWD) lds_fft<false>(p, cur, oth, nl);
+  if (a.flags & F_FWD) lds_fft<false>(p, tw, cur, oth, nl);
   if (a.flags & F_KY) {
     for (int f = threadIdx.x; f < tot; f += blockDim.x) {
       const int g = f / (L * C), r = f - g * (L * C), e = r / C, c = r - e * C;
@@ -242,14 +251,14 @@ __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
     __syncthreads();
   }
   if (a.flags & F_KMUL) {   // outermost axis (O == 1): FFT -> * exp_K / N -> IFFT
-    lds_fft<false>(p, cur, oth, nl);
+    lds_fft<false>(p, tw, cur, oth, nl);
     const int pts = I / a.ns;
     for (int f = threadIdx.x; f < tot; f += blockDim.x) {
       const int r = f % (L * C), e = r / C, c = r - e * C;
       if (c < cv) cur[c * M + e] = cmul(cur[c * M + e], a.K[(size_t)e * pts + (i0 + c) / a.ns]);
     }
     __syncthreads();
-    lds_fft<true>(p, cur, oth, nl);
+    lds_fft<true>(p, tw, cur, oth, nl);
   }
   for (int f = threadIdx.x; f < tot; f += blockDim.x) {
     const int g = f / (L * C), r = f - g * (L * C), e = r / C, c = r - e * C;
@@ -324,6 +333,33 @@ __global__ void scale_copy_kernel(const c128* __restrict__ src, c128* __restrict
     dst[f] = cscale(src[f], s);
 }
 
+// psi[f] *= K[f % L] (one factor per line position, every line of the batch)
+__global__ void bcast_mul_kernel(c128* psi, const c128* __restrict__ K, long n, int L) {
+  for (long f = blockIdx.x * (long)blockDim.x + threadIdx.x; f < n; f += (long)gridDim.x * blockDim.x)
+    psi[f] = cmul(psi[f], K[f % L]);
+}
+
+// Four-step twiddle of a line viewed as [L1][L2]: element (k1, n2) *= w_L^(+-n2 k1) (index (n2 k1) mod L exact)
+__global__ void fourstep_twiddle_kernel(c128* psi, long n, int L1, int L2, const c128* __restrict__ twL, int inv) {
+  const long L = (long)L1 * L2;
+  for (long f = blockIdx.x * (long)blockDim.x + threadIdx.x; f < n; f += (long)gridDim.x * blockDim.x) {
+    const long r = f % L;
+    const long k1 = r / L2, n2 = r - k1 * L2;
+    c128 w = twL[(n2 * k1) % L];
+    if (inv) w = cconj(w);
+    psi[f] = cmul(psi[f], w);
+  }
+}
+
+// exp_K in the four-step's k order: Kp[k1 L2 + k2] = scale * K[k1 + L1 k2]
+__global__ void fourstep_kperm_kernel(const c128* __restrict__ K, c128* Kp, int L1, int L2, double scale) {
+  const long L = (long)L1 * L2;
+  for (long r = blockIdx.x * (long)blockDim.x + threadIdx.x; r < L; r += (long)gridDim.x * blockDim.x) {
+    const long k1 = r / L2, k2 = r - k1 * L2;
+    Kp[r] = cscale(K[k1 + (long)L1 * k2], scale);
+  }
+}
+
 // ---------------------------------------------------------------- plan tables
 __global__ void twiddle_table_kernel(int M, c128* tw) {
   for (int m = blockIdx.x * blockDim.x + threadIdx.x; m < M; m += gridDim.x * blockDim.x) {
@@ -367,11 +403,17 @@ __global__ void bhat_kernel(int M, const c128* __restrict__ b, const c128* __res
 // SPO.run (wpd.py:250-270): V/2; for blk in 1..nt//nout-1: nout x [K, V], snapshot; K; V/2.
 // One workgroup per wavepacket, the line resident in LDS for the whole run.
 __global__ __launch_bounds__(256) void spo1d_gen_kernel(Fft p, c128* psi, const c128* eV, const c128* eVh,
-                                                        const c128* eK, int nt, int nout, c128* snap) {
+                                                        const c128* eK, int nt, int nout, c128* snap, int twl) {
   extern __shared__ c128 sm[];
   const int L = p.L, M = p.M;
   c128* cur = sm;
   c128* oth = sm + M;
+  const c128* tw = p.tw;
+  if (twl) {
+    c128* stw = sm + 2 * M;
+    for (int m = threadIdx.x; m < M; m += blockDim.x) stw[m] = p.tw[m];
+    tw = stw;
+  }
   const int b = blockIdx.x;
   c128* x = psi + (size_t)b * L;
   const double inv = 1.0 / L;
@@ -380,10 +422,10 @@ __global__ __launch_bounds__(256) void spo1d_gen_kernel(Fft p, c128* psi, const 
   const int nblk = nt / nout;
   const int nsnap = nblk > 0 ? nblk - 1 : 0;
   auto kstep = [&]() {
-    lds_fft<false>(p, cur, oth, 1);
+    lds_fft<false>(p, tw, cur, oth, 1);
     for (int k = threadIdx.x; k < L; k += blockDim.x) cur[k] = cmul(cur[k], cscale(eK[k], inv));
     __syncthreads();
-    lds_fft<true>(p, cur, oth, 1);
+    lds_fft<true>(p, tw, cur, oth, 1);
   };
   for (int blk = 1; blk < nblk; ++blk) {
     for (int s = 0; s < nout; ++s) {
@@ -631,7 +673,9 @@ struct Exec {
     a.snap = snap;
     a.K = Ks;
     a.Ky = Ky;
-    const size_t lds = (size_t)2 * G * C * f[d].M * sizeof(c128);
+    size_t lds = (size_t)2 * G * C * f[d].M * sizeof(c128);
+    a.twl = lds + (size_t)f[d].M * sizeof(c128) <= LDS_MAX;
+    if (a.twl) lds += (size_t)f[d].M * sizeof(c128);
     (void)hipFuncSetAttribute((const void*)spo_axis_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
     hipLaunchKernelGGL(spo_axis_kernel, dim3((a.O + G - 1) / G, (a.I + C - 1) / C), dim3(256), lds, st, f[d], a);
     QD_HIP(hipGetLastError());
@@ -645,14 +689,14 @@ struct Exec {
     int c;
     if (rows) {
       c = (int)I;
-    } else {
+    } else {   // 8 consecutive columns (128-B rows) when that still leaves >= 256 tiles, else fewer
       c = (int)std::min<long>(I, 8);
-      while (c > 1 && (size_t)c * line > LDS_SOFT) c >>= 1;
+      while (c > 1 && ((size_t)c * line > LDS_SOFT || ((I + c - 1) / c) * O < 256)) c >>= 1;
     }
     if ((size_t)c * line > LDS_MAX) return false;
     int g = 1;
-    if (c == I) {   // whole rows: stack rows until ~1024 elements per tile or the LDS target
-      while (g < O && (long)g * c * n[d] < 1024 && (size_t)(2 * g) * c * line <= LDS_SOFT) g *= 2;
+    if (c == I) {   // whole rows: stack short rows (< 256 elements per tile) while >= 256 tiles remain
+      while (g < O && (long)g * c * n[d] < 256 && O / (2 * g) >= 256 && (size_t)(2 * g) * c * line <= LDS_SOFT) g *= 2;
       g = (int)std::min<long>(g, O);
     }
     *C = c;
@@ -817,31 +861,80 @@ int spo1d_generic_run(c128* psi, const c128* expV, const c128* expVh, const c128
   Fft f;
   if ((rc = plan_axis(nx, tab, f, st))) return rc;
   if (f.kind != DIRECT) {
-    const size_t lds = (size_t)2 * f.M * sizeof(c128);
+    const int twl = (size_t)3 * f.M * sizeof(c128) <= LDS_MAX;
+    const size_t lds = (size_t)(2 + twl) * f.M * sizeof(c128);
     (void)hipFuncSetAttribute((const void*)spo1d_gen_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
-    hipLaunchKernelGGL(spo1d_gen_kernel, dim3(B), dim3(256), lds, st, f, psi, expV, expVh, expK, nt, nout, snap);
+    hipLaunchKernelGGL(spo1d_gen_kernel, dim3(B), dim3(256), lds, st, f, psi, expV, expVh, expK, nt, nout, snap, twl);
     QD_HIP(hipGetLastError());
     return QD_OK;
   }
-  // DIRECT lines: one launch sequence per step on the [B][nx] grid (the axis is the last one, I = 1)
-  hipLaunchKernelGGL(scale_copy_kernel, dim3(grid_for(nx)), dim3(256), 0, st, expK, ks, (long)nx, 1.0 / nx);
-  QD_HIP(hipGetLastError());
-  const dim3 grid((nx + 255) / 256, (unsigned)std::min<long>(B, 65535));
+  // Lines beyond the LDS plans.  Smooth lengths L = L1 L2 with both factors LDS-plannable run the four-step FFT:
+  // the line viewed as [L1][L2] (n = L2 n1 + n2), FFT_L1 over n1 (stride L2), twiddle w_L^(n2 k1), FFT_L2 over n2
+  // (contiguous) leaves X[k1 + L1 k2] at L2 k1 + k2; the kinetic factor is applied in that order (exp_K permuted once)
+  // and the inverse runs the same passes backwards, so no transpose is ever made.  Other lengths: direct DFT.
+  const char* fk = getenv("QD_SPO_FORCE_KIND");
+  int L1 = 0;
+  if (!(fk && fk[0] == '2')) {
+    int best = 0;
+    for (int a = 2; (long)a * a <= nx; ++a) {
+      if (nx % a) continue;
+      const int b2 = nx / a;
+      if (a <= MAX_LDS_M && b2 <= MAX_LDS_M && all_factors_small(a, GEN_MAXP) && all_factors_small(b2, GEN_MAXP))
+        best = a;   // the largest divisor <= sqrt(L): the most balanced split
+    }
+    L1 = best;
+  }
+  const long total = n;
   auto vmul = [&](const c128* V) -> int {   // psi[b][k] *= V[k]
-    for (int b = 0; b < B; ++b)
-      hipLaunchKernelGGL(kmul_kernel, dim3(grid_for(nx)), dim3(256), 0, st, psi + (size_t)b * nx, V, (long)nx, 1);
+    hipLaunchKernelGGL(bcast_mul_kernel, dim3(grid_for(total)), dim3(256), 0, st, psi, V, total, nx);
     QD_HIP(hipGetLastError());
     return QD_OK;
   };
-  auto kstep = [&]() -> int {
-    hipLaunchKernelGGL(dft_axis_kernel<false>, grid, dim3(256), 0, st, (const c128*)psi, tmp, (long)B, nx, 1L, f.tw);
-    for (int b = 0; b < B; ++b)
-      hipLaunchKernelGGL(kmul_kernel, dim3(grid_for(nx)), dim3(256), 0, st, tmp + (size_t)b * nx, (const c128*)ks,
-                         (long)nx, 1);
-    hipLaunchKernelGGL(dft_axis_kernel<true>, grid, dim3(256), 0, st, (const c128*)tmp, psi, (long)B, nx, 1L, f.tw);
+  std::function<int()> kstep;
+  Exec x;
+  c128* tab2 = nullptr;
+  if (L1 > 0) {
+    const int L2 = nx / L1;
+    void* w2 = nullptr;
+    if ((rc = workspace(WS_MISC, (plan_slots(L1) + plan_slots(L2)) * sizeof(c128), &w2, st))) return rc;
+    tab2 = (c128*)w2;
+    x.D = 3;
+    x.n[0] = B;
+    x.n[1] = L1;
+    x.n[2] = L2;
+    x.ns = 1;
+    x.npts = total;
+    x.st = st;
+    x.psi = psi;
+    x.tmp = tmp;
+    if ((rc = plan_axis(L1, tab2, x.f[1], st))) return rc;
+    if ((rc = plan_axis(L2, tab2 + plan_slots(L1), x.f[2], st))) return rc;
+    hipLaunchKernelGGL(fourstep_kperm_kernel, dim3(grid_for(nx)), dim3(256), 0, st, expK, ks, L1, L2, 1.0 / nx);
     QD_HIP(hipGetLastError());
-    return QD_OK;
-  };
+    kstep = [&, L2]() -> int {
+      int r;
+      if ((r = x.pass(1, F_FWD, nullptr, nullptr, nullptr))) return r;
+      hipLaunchKernelGGL(fourstep_twiddle_kernel, dim3(grid_for(total)), dim3(256), 0, st, psi, total, L1, L2, f.tw, 0);
+      if ((r = x.pass(2, F_FWD, nullptr, nullptr, nullptr))) return r;
+      hipLaunchKernelGGL(bcast_mul_kernel, dim3(grid_for(total)), dim3(256), 0, st, psi, (const c128*)ks, total, nx);
+      if ((r = x.pass(2, F_INV, nullptr, nullptr, nullptr))) return r;
+      hipLaunchKernelGGL(fourstep_twiddle_kernel, dim3(grid_for(total)), dim3(256), 0, st, psi, total, L1, L2, f.tw, 1);
+      if ((r = x.pass(1, F_INV, nullptr, nullptr, nullptr))) return r;
+      QD_HIP(hipGetLastError());
+      return QD_OK;
+    };
+  } else {   // direct DFT lines, one launch sequence per step on the [B][nx] grid
+    hipLaunchKernelGGL(scale_copy_kernel, dim3(grid_for(nx)), dim3(256), 0, st, expK, ks, (long)nx, 1.0 / nx);
+    QD_HIP(hipGetLastError());
+    const dim3 grid((nx + 255) / 256, (unsigned)std::min<long>(B, 65535));
+    kstep = [&, grid]() -> int {
+      hipLaunchKernelGGL(dft_axis_kernel<false>, grid, dim3(256), 0, st, (const c128*)psi, tmp, (long)B, nx, 1L, f.tw);
+      hipLaunchKernelGGL(bcast_mul_kernel, dim3(grid_for(total)), dim3(256), 0, st, tmp, (const c128*)ks, total, nx);
+      hipLaunchKernelGGL(dft_axis_kernel<true>, grid, dim3(256), 0, st, (const c128*)tmp, psi, (long)B, nx, 1L, f.tw);
+      QD_HIP(hipGetLastError());
+      return QD_OK;
+    };
+  }
   if ((rc = vmul(expVh))) return rc;
   const int nblk = nt / nout;
   const int nsnap = nblk > 0 ? nblk - 1 : 0;

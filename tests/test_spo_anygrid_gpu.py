@@ -119,3 +119,17 @@ def test_spo1d_any_grid_matches_reference():
         assert relerr(r.psi, g[f"n{n}_psi"]) < TOL, n
         if len(r.psilist):
             assert relerr(np.array(r.psilist), g[f"n{n}_psilist"]) < TOL, n
+
+
+def test_spo1d_long_line_direct_dft_matches_reference(monkeypatch):
+    """The 6000-point line runs the four-step FFT by default (6000 = 75 x 80); QD_SPO_FORCE_KIND=2 sends it through the
+    direct O(L^2) DFT instead — both against the reference fixture."""
+    from pyqed_amd import SPO
+    g = load_golden("spo1d_any")
+    n = 6000
+    x, psi0 = spo1d_model(n)
+    monkeypatch.setenv("QD_SPO_FORCE_KIND", "2")
+    sol = SPO(x, mass=1.0)
+    sol.set_potential(lambda q: q ** 2 / 2)
+    r = sol.run(psi0, dt=0.01, nt=int(g[f"n{n}_nt"]), nout=int(g[f"n{n}_nout"]))
+    assert relerr(r.psi, g[f"n{n}_psi"]) < TOL
