@@ -897,14 +897,6 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   // state workspace: per-matrix scratch (+ padded rho when N != Np)
   const bool pad = (Np != N);
   if (Np > 128) herm = 0;  // the Hermitian path is single-block
-  // N_p = 64 Hermitian Lindblad batches below 160 matrices: the general split-K path is the fastest there
-  // (tools/glf_hsplit_np64_sweep.py, profiles/r03/lindblad/hsplit_np64_sweep.txt: B = 64 702k vs 666k pair-block
-  // split vs 483k persistent DM-steps/s; B = 128 1.03M / 1.05M / 0.94M; from B = 192 the persistent Hermitian
-  // kernel leads, 1.40M vs 1.18M / 1.27M)
-  {
-    const char* h64 = std::getenv("QD_GLF_HSPLIT_NP64");
-    if (herm && src == GLF_FROM_LINDBLAD && Np == 64 && B < 160 && !(h64 && h64[0] == '1')) herm = 0;
-  }
   // Split path (glf_split_*): each output block of a phase is a workgroup, for batches too small to
   // occupy the chip with one persistent workgroup per matrix.  QD_GLF_SPLIT=0 / 1 forces it off / on.
   // Measured (tools/glf_split_bench.py, N = 128 / 256, B = 1 .. 256): the split path wins for every batch

@@ -28,6 +28,9 @@ except Exception:  # pragma: no cover
 HERM_MIN_BATCH = 192        # Redfield (glf_rk4): persistent Hermitian kernel from this batch size
 HERM_SPLIT_MIN_BATCH = 16   # Lindblad: Hermitian kernels from this batch size (qd_lindblad_rk4_herm runs its
                             # pair-block split path below 208 matrices and the persistent kernel from there)
+HERM_NP64_MIN_BATCH = 160   # 33 <= N <= 64 (padded to 64): the general split-K path up to here
+                            # (profiles/r03/lindblad/hsplit_np64_sweep.txt: B = 64 702k general vs 483k persistent
+                            # Hermitian DM-steps/s; B = 192 1.18M vs 1.40M)
 
 
 def lindblad_rk4(H: torch.Tensor, c_ops: torch.Tensor | None, rho: torch.Tensor, dt: float, nsteps: int,
@@ -75,7 +78,8 @@ def lindblad_rk4(H: torch.Tensor, c_ops: torch.Tensor | None, rho: torch.Tensor,
     # rho H, not rho H^+), so the Hermitian kernel is gated on both, bit for bit.
     h_herm = bool(torch.equal(H, H.transpose(-1, -2).conj()))
     if hermitian is None:
-        hermitian = (N <= 128 and B >= HERM_SPLIT_MIN_BATCH and h_herm
+        min_b = HERM_NP64_MIN_BATCH if 32 < N <= 64 else HERM_SPLIT_MIN_BATCH
+        hermitian = (N <= 128 and B >= min_b and h_herm
                      and bool(torch.equal(rho, rho.transpose(-1, -2).conj())))
     elif hermitian and not h_herm:
         raise ValueError("hermitian=True needs a Hermitian H (the X + X^+ form drops the anti-Hermitian part of H)")

@@ -440,8 +440,9 @@ def test_workspace_bounded_over_many_streams():
 
 @pytest.mark.parametrize("N,B", [(64, 24), (48, 100), (64, 200)])
 def test_lindblad_np64_hermitian_dispatch_matches_oracle(N, B):
-    """Default dispatch for exactly Hermitian batches at N_p = 64 (the general split-K path below 160 matrices, the
-    persistent Hermitian kernel above; profiles/r03/lindblad/hsplit_np64_sweep.txt) against the oracle."""
+    """Default dispatch (hermitian=None) for exactly Hermitian batches at N_p = 64 (the general split-K path below
+    160 matrices, the persistent Hermitian kernel above; profiles/r03/lindblad/hsplit_np64_sweep.txt) against the
+    oracle."""
     import torch
     from oracle import lindblad as olb
     from pyqed_amd import lindblad_rk4
