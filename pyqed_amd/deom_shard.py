@@ -225,6 +225,11 @@ class CollectiveExchange:
                 torch.index_select(src, 0, self.export.long(), out=self.sendbuf[:n])
         if dist.get_backend(self.group) == "nccl":
             dist.all_gather_into_tensor(self.recvbuf, self.sendbuf, group=self.group)
+        elif self.dev.type == "cuda":   # gloo with device bands (tests: ranks sharing one GPU): stage through host
+            host = self.sendbuf.cpu()
+            parts = [torch.empty_like(host) for _ in range(self.world)]
+            dist.all_gather(parts, host, group=self.group)
+            self.recvbuf.copy_(torch.cat(parts).to(self.dev))
         else:
             dist.all_gather(list(self.recvbuf.chunk(self.world)), self.sendbuf, group=self.group)
         if self.n_halo:
