@@ -124,6 +124,9 @@ __device__ void wg_observables(const c128* rho, const c128* eT, int ne, size_t N
 #ifndef GLF_HERM_X
 #define GLF_HERM_X 1   // Hermitian kernel at BT = 128: X GEMM on the CgHermLayout tiles (Lindblad: no Hermitian part below the diagonal; A/B: 0)
 #endif
+#ifndef GLF_EPI_PF
+#define GLF_EPI_PF 4   // Hermitian epilogue: rho / acc loads kept this many update slots ahead (0: chunks of QD_EPI_CH)
+#endif
 #ifndef GLF_HERM_PIPE
 #define GLF_HERM_PIPE false   // fragment double-buffering in the Hermitian kernel's GEMMs (A/B builds)
 #endif
@@ -265,24 +268,96 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
           __syncthreads();
           // round 0: tile (0, 1), element e -> (e / TS, TS + e % TS), k at T01; round 1: the two folded diagonal
           // triangles, element e -> k at Tt[e]
+          auto place_rd = [&](auto rdc, int e, int& gi, int& gj) -> const c128* {
+            constexpr int rd = decltype(rdc)::value;
+            if (rd == 0) {
+              gi = e / TS;
+              gj = TS + e % TS;
+              return &T01[gi * LD + e % TS];
+            }
+            const int ts = e / TRI, ff = e % TRI, u = ff / (TS + 1), v = ff % (TS + 1);
+            const bool lo = v < TS - u;
+            const int ra = lo ? u : TS - 1 - u;
+            gi = ts * TS + ra;
+            gj = ts * TS + (lo ? u + v : ra + v - (TS - u));
+            return &Tt[e];
+          };
+          // RK4 update of one upper element (i, j) with k, writing the mirror (j, i) as the conjugate
+          auto update = [&](int gi, int gj, c128 k, c128 r0v, c128 a0v) {
+            const int id = gi * Np + gj, mid = gj * Np + gi;
+            const bool off = gi != gj;
+            if (stage == 0) {
+              acc[id] = k;
+              const c128 v = cadd(r0v, cscale(k, dt2));
+              rn[id] = v;
+              if (off) rn[mid] = cconj(v);
+            } else if (stage < 3) {
+              acc[id] = cadd(a0v, cscale(k, 2.0));
+              const c128 v = cadd(r0v, cscale(k, stage == 1 ? dt2 : dt));
+              rn[id] = v;
+              if (off) rn[mid] = cconj(v);
+            } else {
+              const c128 r1 = cadd(r0v, cscale(cscale(cadd(a0v, k), 1.0 / 6.0), dt));
+              rho[id] = r1;
+              rn[id] = r1;
+              if (off) {
+                rho[mid] = cconj(r1);
+                rn[mid] = cconj(r1);
+              }
+            }
+          };
+#if GLF_EPI_PF
+          // Software-pipelined update over both rounds (NP0 + NP1 slots per thread): the rho / acc loads of slot
+          // q + GLF_EPI_PF are issued before slot q is updated, so the chain of load round trips (one per chunk)
+          // overlaps.  Loads and stores touch disjoint elements across slots (reads: the upper triangle; each slot
+          // writes its own element and its mirror).
+          {
+            constexpr int NE0 = TS * TS, NE1 = 2 * TRI;
+            constexpr int NP0 = (NE0 + CG_WG - 1) / CG_WG, NP1 = (NE1 + CG_WG - 1) / CG_WG;
+            constexpr int NS = NP0 + NP1;
+            c128 r0[1], a0[1];
+            auto slot_ok = [&](int q, int& e) {
+              e = tid + CG_WG * (q < NP0 ? q : q - NP0);
+              return q < NP0 ? (NE0 % CG_WG == 0 || e < NE0) : (NE1 % CG_WG == 0 || e < NE1);
+            };
+            // a window of W = GLF_EPI_PF slots of loads in flight ahead of the slot being updated: a runtime loop over
+            // chunks of W slots, buffer j of the window reloaded with slot q + W right after slot q is updated
+            constexpr int W = GLF_EPI_PF;
+            (void)r0;
+            (void)a0;
+            c128 rb[W], ab[W];
+            auto issue_to = [&](int q, c128& rv, c128& av) {
+              int e;
+              if (q >= NS || !slot_ok(q, e)) return;
+              int gi, gj;
+              if (q < NP0) place_rd(std::integral_constant<int, 0>{}, e, gi, gj);
+              else place_rd(std::integral_constant<int, 1>{}, e, gi, gj);
+              rv = rho[gi * Np + gj];
+              av = stage == 0 ? cmk(0, 0) : acc[gi * Np + gj];
+            };
+#pragma unroll
+            for (int j = 0; j < W; ++j) issue_to(j, rb[j], ab[j]);
+            for (int q0 = 0; q0 < NS; q0 += W) {
+#pragma unroll
+              for (int j = 0; j < W; ++j) {
+                const int q = q0 + j;
+                int e;
+                if (q < NS && slot_ok(q, e)) {
+                  int gi, gj;
+                  const c128 k = q < NP0 ? *place_rd(std::integral_constant<int, 0>{}, e, gi, gj)
+                                         : *place_rd(std::integral_constant<int, 1>{}, e, gi, gj);
+                  update(gi, gj, k, rb[j], ab[j]);
+                }
+                issue_to(q + W, rb[j], ab[j]);
+              }
+            }
+          }
+#else
           auto round = [&](auto rdc) {
             constexpr int rd = decltype(rdc)::value;
             constexpr int NE = rd == 0 ? TS * TS : 2 * TRI;
             constexpr int NPER = (NE + CG_WG - 1) / CG_WG;
             constexpr int CH = NPER < QD_EPI_CH ? NPER : QD_EPI_CH;
-            auto place = [&](int e, int& gi, int& gj) -> const c128* {
-              if (rd == 0) {
-                gi = e / TS;
-                gj = TS + e % TS;
-                return &T01[gi * LD + e % TS];
-              }
-              const int ts = e / TRI, ff = e % TRI, u = ff / (TS + 1), v = ff % (TS + 1);
-              const bool lo = v < TS - u;
-              const int ra = lo ? u : TS - 1 - u;
-              gi = ts * TS + ra;
-              gj = ts * TS + (lo ? u + v : ra + v - (TS - u));
-              return &Tt[e];
-            };
             for (int q0 = 0; q0 < NPER; q0 += CH) {
               c128 r0[CH], a0[CH];
 #pragma unroll
@@ -290,7 +365,7 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
                 const int e = tid + CG_WG * (q0 + q);
                 if (q0 + q < NPER && (NE % CG_WG == 0 || e < NE)) {
                   int gi, gj;
-                  place(e, gi, gj);
+                  place_rd(rdc, e, gi, gj);
                   r0[q] = rho[gi * Np + gj];
                   a0[q] = stage == 0 ? cmk(0, 0) : acc[gi * Np + gj];
                 }
@@ -300,33 +375,14 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
                 const int e = tid + CG_WG * (q0 + q);
                 if (q0 + q >= NPER || (NE % CG_WG != 0 && e >= NE)) continue;
                 int gi, gj;
-                const c128 k = *place(e, gi, gj);
-                const int id = gi * Np + gj, mid = gj * Np + gi;   // (i, j) and its mirror (j, i)
-                const bool off = gi != gj;
-                if (stage == 0) {
-                  acc[id] = k;
-                  const c128 v = cadd(r0[q], cscale(k, dt2));
-                  rn[id] = v;
-                  if (off) rn[mid] = cconj(v);
-                } else if (stage < 3) {
-                  acc[id] = cadd(a0[q], cscale(k, 2.0));
-                  const c128 v = cadd(r0[q], cscale(k, stage == 1 ? dt2 : dt));
-                  rn[id] = v;
-                  if (off) rn[mid] = cconj(v);
-                } else {
-                  const c128 r1 = cadd(r0[q], cscale(cscale(cadd(a0[q], k), 1.0 / 6.0), dt));
-                  rho[id] = r1;
-                  rn[id] = r1;
-                  if (off) {
-                    rho[mid] = cconj(r1);
-                    rn[mid] = cconj(r1);
-                  }
-                }
+                const c128 k = *place_rd(rdc, e, gi, gj);
+                update(gi, gj, k, r0[q], a0[q]);
               }
             }
           };
           round(std::integral_constant<int, 0>{});
           round(std::integral_constant<int, 1>{});
+#endif
           __syncthreads();
         }
         QD_TMARK(3);
