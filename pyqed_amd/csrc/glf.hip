@@ -125,7 +125,8 @@ __device__ void wg_observables(const c128* rho, const c128* eT, int ne, size_t N
 #define GLF_HERM_X 1   // Hermitian kernel at BT = 128: X GEMM on the CgHermLayout tiles (Lindblad: no Hermitian part below the diagonal; A/B: 0)
 #endif
 #ifndef GLF_EPI_PF
-#define GLF_EPI_PF 4   // Hermitian epilogue: rho / acc loads kept this many update slots ahead (0: chunks of QD_EPI_CH)
+#define GLF_EPI_PF 0   // Hermitian epilogue: rho / acc loads kept this many update slots ahead (0: chunks of QD_EPI_CH;
+                       // 4: 328-332k vs 330-332k DM-steps/s for 0, profiles/r03/lindblad/epi_pf_ab.txt: no gain)
 #endif
 #ifndef GLF_HERM_PIPE
 #define GLF_HERM_PIPE false   // fragment double-buffering in the Hermitian kernel's GEMMs (A/B builds)

@@ -49,7 +49,7 @@ def _worker(rank, world, port, q):
         from pyqed_amd.deom_shard import ShardedDEOM
         sol, rho0 = _model()
         sh = ShardedDEOM(sol, device=torch.device("cuda", 0), exchange="allgather")
-        P1 = np.diag(np.linspace(1, 0, sol.nsys)).astype(complex)
+        P1 = np.diag(np.linspace(1, 0, rho0.shape[0])).astype(complex)
         t, tr = sh.run(rho0, 0.01, 8, P1)
         ados = sh.gather_ados()
         q.put((rank, tr, ados, [len(p.halo) for p in sh.plans]))
@@ -71,7 +71,7 @@ def test_deom_bands_two_processes_hip_stages_match_single():
         p.join(timeout=60)
         assert p.exitcode == 0
     sol, rho0 = _model()
-    P1 = np.diag(np.linspace(1, 0, sol.nsys)).astype(complex)
+    P1 = np.diag(np.linspace(1, 0, rho0.shape[0])).astype(complex)
     t, tr_ref = sol.run(rho0.copy(), 0.01, 8, P1)
     assert res[1][1] is None and res[1][2] is None
     assert all(h > 0 for h in res[0][3])
