@@ -688,9 +688,11 @@ def cpu_baseline_spo2(n=256, dt=0.05, budget_s=5.0):
             "sample": f"{k} Strang steps of the scipy.fftpack restatement of SPO2.run at {n}x{n}x2 in {el:.1f}s"}
 
 
-def _deom_event_rate(dev, sol, bath, H, Q, B, steps, dt=0.002):
+def _deom_event_rate(dev, sol, bath, H, Q, B, steps, dt=0.002, banded=True):
     """RK4 steps/s of B independent hierarchies of `sol` (device-resident state; HIP events on the launch stream
-    around `steps` steps = 4 stage launches each).  B >= 16 runs the ADO-major layout."""
+    around `steps` steps).  B = 1 runs what DEOMSolver.run runs: the persistent tier-banded launch
+    (qd_deom_rk4_banded) where the hierarchy qualifies, else (or banded=False) 4 stage launches per step; B >= 16
+    runs the ADO-major layout."""
     import torch
     from pyqed_amd import _lib
     from pyqed_amd.deom import ado_coefficients
@@ -709,7 +711,16 @@ def _deom_event_rate(dev, sol, bath, H, Q, B, steps, dt=0.002):
     (ados[0] if ado_major else ados[:, 0])[..., 0, 0] = 1
     rho_sys = torch.empty((B, steps + 1, ns, ns), dtype=torch.complex128, device=dev)
 
+    bands = sol.band_tables(dev) if (B == 1 and banded) else None
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+
     def run(n):
+        if bands is not None:
+            rc = lib.qd_deom_rk4_banded(ados.data_ptr(), nmax, K, ns, *bands.args(), *(t.data_ptr() for t in tabs[2:]),
+                                        Qd.shape[0], Hd.data_ptr(), None, Qd.data_ptr(), None, None, None, dt, n,
+                                        rho_sys.data_ptr(), None, 0, None, status.data_ptr(), st)
+            _lib.check(rc, "qd_deom_rk4_banded")
+            return
         rc = fn(ados.data_ptr(), B, nmax, K, ns, *(t.data_ptr() for t in tabs), Qd.shape[0], Hd.data_ptr(), None,
                 Qd.data_ptr(), None, None, None, dt, n, rho_sys.data_ptr(), None, 0, None, st)
         _lib.check(rc, "qd_deom_rk4")
@@ -721,6 +732,7 @@ def _deom_event_rate(dev, sol, bath, H, Q, B, steps, dt=0.002):
     run(steps)
     e1.record()
     torch.cuda.synchronize(dev)
+    assert int(status.item()) == 0, "qd_deom_rk4_banded: a band hand-off timed out"
     tr = torch.diagonal(rho_sys[:, -1], dim1=-2, dim2=-1).sum(-1)
     assert float((tr - 1).abs().max()) < 1e-10
     return steps / (e0.elapsed_time(e1) / 1e3)
@@ -754,6 +766,9 @@ def bench_deom(dev, steps, batch):
     sol5.check_()
     sol5.init_()
     rate5 = _deom_event_rate(dev, sol5, bath5, sz + sx, sx[None], 1, steps, dt=0.001)
+    rate_stage = _deom_event_rate(dev, sol, bath, sz + sx, sx[None], 1, steps, banded=False)
+    rate5_stage = _deom_event_rate(dev, sol5, bath5, sz + sx, sx[None], 1, steps, dt=0.001, banded=False)
+    bt, bt5 = sol.band_tables(dev), sol5.band_tables(dev)
     single = rate[1]
     # per RK4 step ~4.75 MB of ADO traffic per hierarchy = 768 B per ADO-step
     # (4 stages x (read stage input, rho, acc + write next input, acc) of 64-B ADO rows)
@@ -763,6 +778,9 @@ def bench_deom(dev, steps, batch):
     return {
         "value": round(single, 1), "unit": "RK4 steps/s (one hierarchy)",
         "ado_steps_per_s_single": round(single * nmax, 1),
+        "kernel": (f"deom_band_kernel (one persistent launch, {bt.nbands} tier bands)" if bt is not None else
+                   "stage launches"),
+        "steps_per_s_stage_launches": round(rate_stage, 1),
         "run_steps_per_s_end_to_end": round(steps / wall_run, 1),
         "batched": {"hierarchies": batch, "ado_steps_per_s": round(ado_b, 1), "steps_per_s": round(rate[batch], 1),
                     "layout": "ADO-major [nmax][B][2][2], hierarchies dealt to the 8 XCD block classes",
@@ -775,14 +793,19 @@ def bench_deom(dev, steps, batch):
                                  "traffic_unit": "HBM bytes per stage launch (PMC FETCH_SIZE+WRITE_SIZE, calibrated; "
                                                  "profiles/pmc_traffic.json)"}},
         "stretch_npsd5": {"nmax": sol5.nmax, "K": sol5.nind, "L": 12, "dt": 0.001, "steps_per_s": round(rate5, 1),
+                          "bands": bt5.nbands if bt5 is not None else None,
+                          "steps_per_s_stage_launches": round(rate5_stage, 1),
                           "ado_steps_per_s": round(rate5 * sol5.nmax, 1)},
         "roofline": {"bound": "hbm", "achieved": round(bytes_per_step * single / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(bytes_per_step * single / 1e9 / HBM_PEAK_GBS, 4),
                      "bytes_per_step": bytes_per_step,
-                     "note": "latency-bound: 4 dependent stage launches per step on a 396 KB (L2-resident) state"},
+                     "note": "latency-bound: 4 dependent RK4 stages per step on a 396 KB state; the banded launch "
+                             "hands each stage's rows between the bands inside one launch (per-stage hand-off "
+                             "latency, no kernel boundaries)"},
         "config": {"workload": "deom_spin_boson_drude_L12_K5 (BASELINE.json configs[3])", "nmax": nmax, "K": 5,
                    "L": 12, "dt": 0.002, "steps": steps},
-        "note": "value / batched: device-resident state, HIP events over `steps` RK4 steps (4 stage launches each); "
+        "note": "value / batched: device-resident state, HIP events over `steps` RK4 steps (value: the banded "
+                "persistent launch DEOMSolver.run takes for one hierarchy; batched: 4 stage launches per step); "
                 "run_steps_per_s_end_to_end: DEOMSolver.run incl. table setup and transfers",
     }
 

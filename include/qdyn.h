@@ -256,6 +256,35 @@ int qd_deom_rk4_ado_major(qd_c128* ados, int B, int nmax, int K, int ns,
                           int ne, qd_c128* trace, void* stream);
 
 /*
+ * ONE hierarchy (B = 1) of qd_deom_rk4 as one persistent launch over `nbands`
+ * tier bands (DEOMSolver.run, pyqed/heom/deom.py:1072-1114, with rk4 /
+ * rem_cal :641-766).  Workgroup w owns ADO rows [band_lo[w], band_lo[w+1]) and
+ * keeps their stage input plus its halo rows in LDS; the bands hand each RK4
+ * stage's rows to each other inside the launch (write-through stores, one
+ * epoch word per band).  Band tables (device int32, deom_shard.make_plans):
+ * halo_off[nbands+1] / halo_idx (global halo rows per band), src_off[nbands+1]
+ * / src (bands owning them), lminus / lplus [nmax][K] local rows (owned rows
+ * first, then the band's halo rows; -1 absent); max_own / max_loc the largest
+ * owned / owned + halo row counts.  ns in [2, 4], K <= 8,
+ * max_own * (ns == 2 ? 4 : 16) <= 1024, (2 + nmod + max_loc) ns^2 16 B <= 160 KB.
+ * Other arguments and results as qd_deom_rk4 with B = 1 (bit-identical).
+ * status: device int32 set to 1 if a hand-off timed out (bands not
+ * co-resident; results invalid), or null: the call then synchronises the
+ * stream and returns QD_EHIP in that case.
+ */
+int qd_deom_rk4_banded(qd_c128* ados, int nmax, int K, int ns,
+                       const int32_t* lminus, const int32_t* lplus,
+                       const int32_t* band_lo, const int32_t* halo_off,
+                       const int32_t* halo_idx, const int32_t* src_off,
+                       const int32_t* src, int nbands, int max_own, int max_loc,
+                       const qd_c128* coef, const qd_c128* damp, const int32_t* mode,
+                       int nmod, const qd_c128* H, const qd_c128* Hdip,
+                       const qd_c128* Q, const qd_c128* Qdip, const qd_c128* fsys,
+                       const qd_c128* fcoup, double dt, int nsteps, qd_c128* rho_sys,
+                       const qd_c128* E, int ne, qd_c128* trace, int32_t* status,
+                       void* stream);
+
+/*
  * One RK4 stage of a BAND of the ADO hierarchy (tier-banded sharding of one
  * hierarchy over ranks; DEOMSolver.run / rk4 / rem_cal,
  * pyqed/heom/deom.py:641-766, 1072-1114, split across processes).  Rows

@@ -61,6 +61,10 @@ SIGNATURES = {
     "qd_deom_rk4_ado_major": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_double, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "qd_deom_rk4_banded": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_double, c_int,
+                                   c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "qd_deom_stage": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                               c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_double,
                               c_double, c_double, c_double, c_int, c_double, c_void_p, c_int, c_int, c_void_p]),

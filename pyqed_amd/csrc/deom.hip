@@ -20,6 +20,7 @@
 #include "qd_common.hpp"
 
 #include <cstdlib>
+#include <vector>
 
 namespace qd {
 namespace {
@@ -1125,6 +1126,565 @@ extern "C" int qd_heom_chain_euler(qd_c128* ados, int B, int nado, int ns, const
     hipLaunchKernelGGL(deom_trace_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0, st,
                        (const c128*)snap, (const c128*)E, ne, B, ns, nsteps + 1, (c128*)obs);
     QD_HIP(hipGetLastError());
+  }
+  return QD_OK;
+}
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------------------------
+// One hierarchy as ONE persistent launch over a handful of tier bands (qd_deom_rk4_banded).
+//
+// The unbanded path runs one launch per RK4 stage: at the bench hierarchy (6188 ADOs, 396 KB of state) a stage is
+// two dependent memory round trips plus the ~1.5 us kernel boundary, 4.8 us in all.  Here workgroup w owns the
+// contiguous ADO band [band_lo[w], band_lo[w+1]) of the partition deom_shard.make_plans builds (the keys are tier
+// ordered, so a band's outside neighbours sit in tiers l -/+ 1 of it).  Its LDS holds the stage input of its owned
+// rows followed by its halo rows (local rows: lminus / lplus), its registers hold rho and the RK4 accumulator of
+// its owned elements for the whole run.  Per stage a workgroup
+//   1. waits until every band owning one of its halo rows (src) has published the previous stage (ONE wave polls
+//      the sources' epoch words, relaxed agent-scope loads, s_sleep between polls, bounded spin);
+//   2. loads its halo rows of that stage's output with sc1 (L1-bypassing) loads into LDS;
+//   3. evaluates the stencil of the group kernel (same arithmetic, same operand order: bit-identical results) from
+//      LDS and runs the RK4 epilogue in registers;
+//   4. writes the next stage input to its LDS rows and, write-through (sc1 stores), to buf[g & 1]; every wave
+//      drains its stores (s_waitcnt vmcnt(0)), the workgroup meets at a barrier and one lane stores the new epoch.
+// That is the MI355X_MICROARCH.md hand-off form "sc1 payload + drained flag, sc1 loads" (no release / acquire
+// fences).  Reuse of buf[g & 1] is safe: a band overwrites it at stage g only after every source has published
+// stage g - 1, i.e. finished reading it, and the neighbour relation is symmetric (sources == consumers).
+// Stage 0 of step 0 reads the caller's ados (written before the launch); the final rho is buf[1] (the output of
+// the last stage 3), copied to ados behind the launch.  A spin that exceeds its bound (bands not co-resident)
+// sets *status = 1 and every band leaves its loop (results then invalid; the host reports it).
+constexpr int BAND_FLAG_STRIDE = 16;          // 64-B epoch slots
+constexpr unsigned BAND_SPIN_LIMIT = 1u << 21;  // polls (one round trip each): ~1 s
+
+struct BandParams {
+  const c128* ados;      // [nmax][ns2] rho at t = 0 (read at stage 0 of step 0 only)
+  c128* buf;             // [2][nmax][ns2] stage outputs (hand-off buffers)
+  unsigned* flags;       // [nbands][BAND_FLAG_STRIDE] last published epoch (stage g output = g + 1)
+  int* status;           // [1] 0 = ok, 1 = a hand-off timed out
+  const int* band_lo;    // [nbands + 1]
+  const int* halo_off;   // [nbands + 1]
+  const int* halo_idx;   // global ADO rows of each band's halo
+  const int* src_off;    // [nbands + 1]
+  const int* src;        // bands owning each band's halo rows
+  const int* lminus;     // [nmax][K] local rows (owned first, then halo), -1 absent
+  const int* lplus;
+  const c128* coef;      // [nmax][K][3] cL, cR, cP
+  const c128* damp;      // [nmax]
+  const int* mode;       // [K]
+  const c128* H;
+  const c128* Hdip;      // or null
+  const c128* Q;
+  const c128* Qdip;      // or null
+  const c128* fsv;       // [nsteps][3] pulse values (t, t + dt/2, t + dt) or null
+  const c128* fcv;
+  c128* snap;            // [nsteps + 1][ns2] rho_0 after each step, or null
+  unsigned long long* tim;   // QD_PHASE_TIMING builds: [nbands][4] wall-clock ticks per phase
+  int nmax, K, ns, nmod, nsteps, max_loc;
+  double dt;
+};
+
+constexpr int BAND_HM = 8;   // halo elements per thread held as precomputed offsets (one batched load per stage)
+typedef unsigned int band_u4 __attribute__((ext_vector_type(4)));
+
+// 16-B write-through (sc1) buffer load / store of one complex element at byte offset `off`
+__device__ __forceinline__ c128 ld16_sc1(__amdgpu_buffer_rsrc_t r, int off) {
+  const band_u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
+  return cmk(__builtin_bit_cast(double, (unsigned long long)v.x | ((unsigned long long)v.y << 32)),
+             __builtin_bit_cast(double, (unsigned long long)v.z | ((unsigned long long)v.w << 32)));
+}
+__device__ __forceinline__ void st16_sc1(__amdgpu_buffer_rsrc_t r, int off, c128 x) {
+  const unsigned long long a = __builtin_bit_cast(unsigned long long, x.re);
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, x.im);
+  const band_u4 v = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
+}
+
+__device__ __forceinline__ c128 ld_sc1(const c128* q) {
+  return cmk(__hip_atomic_load(&q->re, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+             __hip_atomic_load(&q->im, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1(c128* q, c128 v) {
+  __hip_atomic_store(&q->re, v.re, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&q->im, v.im, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// FAST (ns = 2, K == KMAX, one bath mode): the mode loop, the K bound and H / Q fold to constants and registers.
+template <int G, int KMAX, bool NS2, int TPB, bool FAST>
+__global__ __launch_bounds__(TPB) void deom_band_kernel(BandParams p) {
+  static_assert(!FAST || NS2, "FAST is the ns = 2 specialisation");
+  extern __shared__ c128 deom_lds[];
+  __shared__ int sAbort;
+  const int ns = NS2 ? 2 : p.ns, ns2 = ns * ns, K = FAST ? KMAX : p.K;
+  c128* sH = deom_lds;
+  c128* sQ = deom_lds + ns2;
+  c128* sX = deom_lds + (size_t)(1 + p.nmod) * ns2;   // [n_own + n_halo][ns2], then one zero row (absent neighbours)
+  const int w = blockIdx.x;
+  const int lo = p.band_lo[w], no = p.band_lo[w + 1] - lo;
+  const int hoff = p.halo_off[w], nh = p.halo_off[w + 1] - hoff;
+  const int soff = p.src_off[w], nsrc = p.src_off[w + 1] - soff;
+  const int tid = threadIdx.x;
+  const int a = tid / G, e = tid % G;
+  const bool live = a < no;                  // uniform within a group
+  const bool valid = live && e < ns2;
+  const int ee = e < ns2 ? e : 0;            // padding lanes shadow element 0
+  const int al = live ? a : 0;
+  const int n = lo + al;
+  const int base = (tid & 63) & ~(G - 1);
+  auto shfl = [&](c128 v, int s) { return cmk(__shfl(v.re, base + s, 64), __shfl(v.im, base + s, 64)); };
+  auto bc = [&](c128 v, int s) -> c128 {
+    if constexpr (G == 4) {
+      switch (s) {
+        case 0: return dpp_qc<0x00>(v);
+        case 1: return dpp_qc<0x55>(v);
+        case 2: return dpp_qc<0xAA>(v);
+        default: return dpp_qc<0xFF>(v);
+      }
+    } else {
+      return shfl(v, s);
+    }
+  };
+  auto bci = [&](int v, int s) -> int {
+    if constexpr (G == 4) {
+      switch (s) {
+        case 0: return dpp_qi<0x00>(v);
+        case 1: return dpp_qi<0x55>(v);
+        case 2: return dpp_qi<0xAA>(v);
+        default: return dpp_qi<0xFF>(v);
+      }
+    } else {
+      return __shfl(v, base + s, 64);
+    }
+  };
+
+  // tables of the owned ADO, once per launch: local neighbour rows broadcast into every lane of the group, the
+  // 3K prefactors kept split over the group's lanes (broadcast per stage, as the group kernel)
+  constexpr int NI = (KMAX + G - 1) / G;
+  constexpr int NC = (3 * KMAX + G - 1) / G;
+  int lm[NI], lp[NI];
+  c128 lc[NC];
+#pragma unroll
+  for (int q = 0; q < NI; ++q) {
+    const int k = e + G * q;
+    lm[q] = (live && k < K) ? p.lminus[(size_t)n * K + k] : -1;
+    lp[q] = (live && k < K) ? p.lplus[(size_t)n * K + k] : -1;
+  }
+#pragma unroll
+  for (int q = 0; q < NC; ++q) {
+    const int c = e + G * q;
+    lc[q] = (live && c < 3 * K) ? p.coef[(size_t)n * K * 3 + c] : cmk(0, 0);
+  }
+  const c128 dmp = live ? p.damp[n] : cmk(0, 0);
+  int im[KMAX], ip[KMAX], md[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    im[k] = bci(lm[k / G], k % G);
+    ip[k] = bci(lp[k / G], k % G);
+    md[k] = FAST ? 0 : (k < K ? __builtin_amdgcn_readfirstlane(p.mode[k]) : -1);
+  }
+  // up to 512 threads (<= 2 waves per SIMD, 256 VGPRs) the prefactors are broadcast once into every lane of the
+  // group instead of once per stage
+  constexpr bool FULLC = TPB <= 512;
+  c128 cf[FULLC ? 3 * KMAX : 1];
+  if constexpr (FULLC) {
+#pragma unroll
+    for (int c = 0; c < 3 * KMAX; ++c) cf[c] = bc(lc[c / G], c % G);
+  }
+  const bool pulsed = p.Hdip || p.Qdip;
+  if (!pulsed) {
+    for (int q = tid; q < ns2; q += blockDim.x) sH[q] = p.H[q];
+    for (int q = tid; q < p.nmod * ns2; q += blockDim.x) sQ[q] = p.Q[q];
+  }
+  c128 r0 = valid ? p.ados[(size_t)n * ns2 + e] : cmk(0, 0);
+  c128 acc = cmk(0, 0);
+  if (valid) sX[(size_t)a * ns2 + e] = r0;
+  if (tid == 0) sAbort = 0;
+  // LDS element index of the own and neighbour elements this lane reads every stage; absent neighbours read the
+  // zero row after the band's rows (the host sizes LDS for max_loc + 1 rows; halo writes never reach it)
+  const int zrow = p.max_loc;
+  for (int q = tid; q < ns2; q += blockDim.x) sX[(size_t)zrow * ns2 + q] = cmk(0, 0);
+  const int oown = al * ns2 + ee;
+  int om[KMAX], op[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    om[k] = ((k < K && im[k] >= 0) ? im[k] : zrow) * ns2 + ee;
+    op[k] = ((k < K && ip[k] >= 0) ? ip[k] : zrow) * ns2 + ee;
+  }
+
+  const int i = ee / ns, j = ee % ns;
+  auto colv = [&](c128 v, int l) -> c128 {
+    if constexpr (NS2) return l == 0 ? dpp_qc<0x44>(v) : dpp_qc<0xEE>(v);
+    else return shfl(v, l * ns + j);
+  };
+  auto rowv = [&](c128 v, int l) -> c128 {
+    if constexpr (NS2) return l == 0 ? dpp_qc<0xA0>(v) : dpp_qc<0xF5>(v);
+    else return shfl(v, i * ns + l);
+  };
+  auto for_l = [&](auto&& f) {
+    if constexpr (NS2) {
+      f(0);
+      f(1);
+    } else {
+      for (int l = 0; l < ns; ++l) f(l);
+    }
+  };
+  static constexpr int stage_time[4] = {0, 1, 1, 2};
+  const double dt = p.dt;
+  const size_t slab = (size_t)p.nmax * ns2;
+  const int G4 = 4 * p.nsteps;
+  // this thread's halo elements q = tid + i blockDim (i < BAND_HM): byte offsets in a stage buffer, fixed for the
+  // launch, so a stage issues all its halo loads back to back (one round trip); -1 = none (then element 0 is
+  // loaded and dropped: branch-free).  Elements beyond BAND_HM blockDim take the generic loop below.
+  const int nhe = nh * ns2;
+  int hsrc[BAND_HM];
+#pragma unroll
+  for (int h = 0; h < BAND_HM; ++h) {
+    const int q = tid + h * (int)blockDim.x;
+    hsrc[h] = q < nhe ? (p.halo_idx[hoff + q / ns2] * ns2 + q % ns2) * 16 : -1;
+  }
+  const int slab_bytes = __builtin_amdgcn_readfirstlane((int)(slab * sizeof(c128)));
+  // buffer descriptors from provably wave-uniform inputs (no waterfall loops around the buffer ops)
+  auto uni = [](const void* q) -> void* {
+    const unsigned long long v = (unsigned long long)q;
+    const unsigned l = __builtin_amdgcn_readfirstlane((unsigned)v), h = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return (void*)(((unsigned long long)h << 32) | l);
+  };
+#ifdef QD_PHASE_TIMING
+  unsigned long long tph[4] = {0, 0, 0, 0};
+#endif
+
+  for (int g = 0; g < G4; ++g) {
+    const int step = g >> 2, stage = g & 3;
+    const c128* in = g == 0 ? p.ados : p.buf + (size_t)((g - 1) & 1) * slab;
+    const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(uni(in), (short)0, slab_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rout =
+        __builtin_amdgcn_make_buffer_rsrc(uni(p.buf + (size_t)(g & 1) * slab), (short)0, slab_bytes, 0x00020000);
+#ifdef QD_PHASE_TIMING
+    const unsigned long long t0 = wall_clock64();
+#endif
+    // 1. wait for every source band's stage g - 1 output (one wave polls; the others wait at the barrier)
+    if (g > 0 && tid < 64) {
+      // lane j < nsrc watches source j's epoch word (one poll in flight: several in flight, checked oldest first,
+      // measured slower: 80.0k vs 89.1k steps/s at 128 bands, the extra polls' traffic and the drain of the polls
+      // still in flight)
+      const int f = tid < nsrc ? p.src[soff + tid] : -1;
+      unsigned spins = 0;
+      int fail = 0;
+      for (;;) {
+        const bool ok = f < 0 || __hip_atomic_load(p.flags + (size_t)f * BAND_FLAG_STRIDE, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)g;
+        if (__all(ok)) break;
+        ++spins;
+        if (spins > BAND_SPIN_LIMIT ||
+            ((spins & 255) == 0 && __hip_atomic_load(p.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
+          fail = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (fail && tid == 0) {
+        sAbort = 1;
+        __hip_atomic_store(p.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the loads below the poll (no instruction)
+    // H(t), Q(t) of this stage (driven runs)
+    if (pulsed) {
+      const int ti = step * 3 + stage_time[stage];
+      const c128 fs = p.fsv ? p.fsv[ti] : cmk(0, 0), fc = p.fcv ? p.fcv[ti] : cmk(0, 0);
+      for (int q = tid; q < ns2; q += blockDim.x) sH[q] = p.Hdip ? cadd(p.H[q], cmul(p.Hdip[q], fs)) : p.H[q];
+      for (int q = tid; q < p.nmod * ns2; q += blockDim.x)
+        sQ[q] = p.Qdip ? cadd(p.Q[q], cmul(p.Qdip[q], fc)) : p.Q[q];
+    }
+    __syncthreads();
+    if (sAbort) break;   // uniform: every wave read it behind the barrier
+#ifdef QD_PHASE_TIMING
+    const unsigned long long t1 = wall_clock64();
+#endif
+    // 2. halo rows of the stage input -> LDS (sc1 loads: another workgroup wrote them in this launch)
+    {
+      c128 hv[BAND_HM];
+#pragma unroll
+      for (int h = 0; h < BAND_HM; ++h) hv[h] = ld16_sc1(rin, hsrc[h] < 0 ? 0 : hsrc[h]);
+#pragma unroll
+      for (int h = 0; h < BAND_HM; ++h)
+        if (hsrc[h] >= 0) sX[(size_t)no * ns2 + tid + h * blockDim.x] = hv[h];
+      for (int q = tid + BAND_HM * (int)blockDim.x; q < nhe; q += blockDim.x) {
+        const int r = q / ns2, c = q - r * ns2;
+        sX[(size_t)(no + r) * ns2 + c] = ld16_sc1(rin, (p.halo_idx[hoff + r] * ns2 + c) * 16);
+      }
+    }
+    __syncthreads();
+#ifdef QD_PHASE_TIMING
+    const unsigned long long t2 = wall_clock64();
+#endif
+
+    // 3. stencil (group-kernel arithmetic and order) from LDS
+    const c128 own = sX[oown];
+    c128 ym[KMAX], yp[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      ym[k] = sX[om[k]];
+      yp[k] = sX[op[k]];
+    }
+    // H(t) / Q(t) entries this lane multiplies: H[i][l], H[l][j] (FAST: the two of each, read once per stage)
+    c128 hil[2], hlj[2], qil[2], qlj[2];
+    if constexpr (FAST) {
+#pragma unroll
+      for (int l = 0; l < 2; ++l) {
+        hil[l] = sH[i * 2 + l];
+        hlj[l] = sH[l * 2 + j];
+        qil[l] = sQ[i * 2 + l];
+        qlj[l] = sQ[l * 2 + j];
+      }
+    }
+    c128 d = cmul(dmp, own);
+    c128 comm = cmk(0, 0);
+    for_l([&](int l) {
+      if constexpr (FAST)
+        comm = cadd(comm, csub(cmul(hil[l], colv(own, l)), cmul(rowv(own, l), hlj[l])));
+      else
+        comm = cadd(comm, csub(cmul(sH[i * ns + l], colv(own, l)), cmul(rowv(own, l), sH[l * ns + j])));
+    });
+    d = cadd(d, cmulmi(comm));
+    c128 SL = cmk(0, 0), SR = cmk(0, 0);
+    auto flush = [&](int m) {
+      const c128* Qm = sQ + m * ns2;
+      c128 t = cmk(0, 0);
+      for_l([&](int l) {
+        if constexpr (FAST)
+          t = cadd(t, cadd(cmul(qil[l], colv(SL, l)), cmul(rowv(SR, l), qlj[l])));
+        else
+          t = cadd(t, cadd(cmul(Qm[i * ns + l], colv(SL, l)), cmul(rowv(SR, l), Qm[l * ns + j])));
+      });
+      d = cadd(d, t);
+    };
+    int mcur = md[0];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      if (k >= K) break;
+      const int m = md[k];
+      if (m != mcur) {
+        flush(mcur);
+        SL = SR = cmk(0, 0);
+        mcur = m;
+      }
+      c128 cL, cR, cP;
+      if constexpr (FULLC) {
+        cL = cf[3 * k];
+        cR = cf[3 * k + 1];
+        cP = cf[3 * k + 2];
+      } else {
+        cL = bc(lc[(3 * k) / G], (3 * k) % G);
+        cR = bc(lc[(3 * k + 1) / G], (3 * k + 1) % G);
+        cP = bc(lc[(3 * k + 2) / G], (3 * k + 2) % G);
+      }
+      const c128 py = cmul(cP, yp[k]);
+      SL = cadd(SL, cadd(cmul(cL, ym[k]), py));
+      SR = cadd(SR, csub(cmul(cR, ym[k]), py));
+    }
+    flush(mcur);
+    // RK4 epilogue (deom.py:735-766 order, as the stage kernels)
+    c128 xo;
+    if (stage == 0) {
+      acc = d;
+      xo = cadd(r0, cscale(d, dt / 2));
+    } else if (stage == 1) {
+      acc = cadd(acc, cscale(d, 2.0));
+      xo = cadd(r0, cscale(d, dt / 2));
+    } else if (stage == 2) {
+      acc = cadd(acc, cscale(d, 2.0));
+      xo = cadd(r0, cscale(d, dt));
+    } else {
+      const c128 s = cadd(acc, d);
+      r0 = cadd(r0, cscale(cscale(s, dt), 1.0 / 6.0));
+      xo = r0;
+    }
+    __syncthreads();   // every read of sX done
+#ifdef QD_PHASE_TIMING
+    const unsigned long long t3 = wall_clock64();
+#endif
+    // 4. publish: LDS row, write-through global row, drain, barrier, epoch
+    if (valid) {
+      sX[(size_t)a * ns2 + e] = xo;
+      st16_sc1(rout, (n * ns2 + e) * 16, xo);
+      if (stage == 3 && p.snap && n == 0) p.snap[(size_t)(step + 1) * ns2 + e] = r0;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+      __hip_atomic_store(p.flags + (size_t)w * BAND_FLAG_STRIDE, (unsigned)(g + 1), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+#ifdef QD_PHASE_TIMING
+    const unsigned long long t4 = wall_clock64();
+    tph[0] += t1 - t0;
+    tph[1] += t2 - t1;
+    tph[2] += t3 - t2;
+    tph[3] += t4 - t3;
+#endif
+  }
+#ifdef QD_PHASE_TIMING
+  if (tid == 0 && p.tim)
+    for (int h = 0; h < 4; ++h) p.tim[w * 4 + h] = tph[h];
+#endif
+}
+
+template <int G, int KMAX, bool NS2, bool FAST = false>
+void launch_band(const BandParams& p, int nbands, int tpb, size_t lds, hipStream_t st) {
+  if (tpb <= 256)
+    hipLaunchKernelGGL((deom_band_kernel<G, KMAX, NS2, 256, FAST>), dim3(nbands), dim3(tpb), lds, st, p);
+  else if (tpb <= 512)
+    hipLaunchKernelGGL((deom_band_kernel<G, KMAX, NS2, 512, FAST>), dim3(nbands), dim3(tpb), lds, st, p);
+  else
+    hipLaunchKernelGGL((deom_band_kernel<G, KMAX, NS2, 1024, FAST>), dim3(nbands), dim3(tpb), lds, st, p);
+}
+
+}  // namespace
+
+// One hierarchy (B = 1) as one persistent launch over `nbands` tier bands (see the kernel above).  The band
+// tables come from deom_shard.make_plans: band_lo [nbands + 1], halo_off / halo_idx (global halo rows per band),
+// src_off / src (bands owning them), lminus / lplus [nmax][K] local rows; max_own / max_loc the largest band's
+// owned / owned + halo row counts.  ns^2 <= 16 (ns <= 4), K <= 8, max_own ns'^2 <= 1024 lanes (ns' = 2 or 4),
+// every band's rows in LDS.  status (device int, or null): 1 after the run if a hand-off timed out; with null the
+// call synchronises the stream and returns QD_EHIP in that case.
+extern "C" int qd_deom_rk4_banded(qd_c128* ados, int nmax, int K, int ns, const int32_t* lminus, const int32_t* lplus,
+                                  const int32_t* band_lo, const int32_t* halo_off, const int32_t* halo_idx,
+                                  const int32_t* src_off, const int32_t* src, int nbands, int max_own, int max_loc,
+                                  const qd_c128* coef, const qd_c128* damp, const int32_t* mode, int nmod,
+                                  const qd_c128* H, const qd_c128* Hdip, const qd_c128* Q, const qd_c128* Qdip,
+                                  const qd_c128* fsys, const qd_c128* fcoup, double dt, int nsteps, qd_c128* rho_sys,
+                                  const qd_c128* E, int ne, qd_c128* trace, int32_t* status, void* stream) {
+  WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
+  QD_CHECK_ARG(ados && lminus && lplus && band_lo && halo_off && src_off && coef && damp && mode && H && Q,
+               "qd_deom_rk4_banded: null pointer");
+  QD_CHECK_ARG(nmax >= 1 && K >= 1 && K <= 8 && nsteps >= 0 && nmod >= 1,
+               "qd_deom_rk4_banded: bad sizes nmax=%d K=%d nmod=%d (K <= 8)", nmax, K, nmod);
+  QD_CHECK_ARG(ns >= 2 && ns <= 4, "qd_deom_rk4_banded: ns=%d outside [2, 4]", ns);
+  QD_CHECK_ARG(nbands >= 1 && max_own >= 1 && max_loc >= max_own,
+               "qd_deom_rk4_banded: bad band sizes nbands=%d max_own=%d max_loc=%d", nbands, max_own, max_loc);
+  {  // the bands wait on each other: every band's workgroup must be resident at once (one per CU suffices)
+    int dev = 0, cus = 0;
+    QD_HIP(hipGetDevice(&dev));
+    QD_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    QD_CHECK_ARG(nbands <= cus, "qd_deom_rk4_banded: %d bands exceed the %d CUs (bands must be co-resident)", nbands,
+                 cus);
+  }
+  QD_CHECK_ARG(!Hdip || fsys, "qd_deom_rk4_banded: Hdip given without fsys");
+  QD_CHECK_ARG(!Qdip || fcoup, "qd_deom_rk4_banded: Qdip given without fcoup");
+  QD_CHECK_ARG(!trace || (E && ne >= 1), "qd_deom_rk4_banded: trace requested without observables");
+  const int G = ns == 2 ? 4 : 16;
+  const int tpb = (max_own * G + 63) / 64 * 64;
+  QD_CHECK_ARG(tpb <= 1024, "qd_deom_rk4_banded: %d owned rows x %d lanes exceed one 1024-thread workgroup",
+               max_own, G);
+  const size_t ns2 = (size_t)ns * ns;
+  const size_t lds = ((size_t)(1 + nmod) + (size_t)max_loc + 1) * ns2 * sizeof(c128);   // + the zero row
+  QD_CHECK_ARG(lds <= 160 * 1024, "qd_deom_rk4_banded: %zu B of band rows exceed the 160 KB LDS (more bands)", lds);
+  hipStream_t st = (hipStream_t)stream;
+  const size_t tot = (size_t)nmax * ns2;
+  QD_CHECK_ARG(tot * sizeof(c128) < ((size_t)1 << 31), "qd_deom_rk4_banded: %zu ADO elements exceed 32-bit offsets",
+               tot);
+  const bool need_snap = rho_sys || trace;
+  const size_t snap_elems = need_snap && !rho_sys ? (size_t)(nsteps + 1) * ns2 : 0;
+  const size_t nf = fsys ? (size_t)nsteps * 3 : 0, nc = fcoup ? (size_t)nsteps * 3 : 0;
+  const size_t flag_bytes = ((size_t)nbands * BAND_FLAG_STRIDE + 4) * sizeof(unsigned);   // + status, 16-B padded
+  void* w = nullptr;
+  int rc = workspace(WS_DEOM, (2 * tot + snap_elems + nf + nc) * sizeof(c128) + flag_bytes, &w, st);
+  if (rc) return rc;
+  c128* buf = (c128*)w;
+  c128* snap = rho_sys ? (c128*)rho_sys : (need_snap ? buf + 2 * tot : nullptr);
+  c128* fsv = nf ? buf + 2 * tot + snap_elems : nullptr;
+  c128* fcv = nc ? buf + 2 * tot + snap_elems + nf : nullptr;
+  unsigned* flags = (unsigned*)(buf + 2 * tot + snap_elems + nf + nc);
+  int* stat = status ? (int*)status : (int*)(flags + (size_t)nbands * BAND_FLAG_STRIDE);
+  if (fsv) QD_HIP(hipMemcpyAsync(fsv, fsys, nf * sizeof(c128), hipMemcpyHostToDevice, st));
+  if (fcv) QD_HIP(hipMemcpyAsync(fcv, fcoup, nc * sizeof(c128), hipMemcpyHostToDevice, st));
+  QD_HIP(hipMemsetAsync(flags, 0, flag_bytes, st));
+  if (status) QD_HIP(hipMemsetAsync(status, 0, sizeof(int32_t), st));
+  if (snap) {
+    hipLaunchKernelGGL(deom_snap0_kernel, dim3(1), dim3(64), 0, st, (const c128*)ados, snap, 1, nmax, ns, nsteps, 0);
+    QD_HIP(hipGetLastError());
+  }
+  if (nsteps > 0) {
+    BandParams p;
+    p.ados = (const c128*)ados;
+    p.buf = buf;
+    p.flags = flags;
+    p.status = stat;
+    p.band_lo = band_lo;
+    p.halo_off = halo_off;
+    p.halo_idx = halo_idx;
+    p.src_off = src_off;
+    p.src = src;
+    p.lminus = lminus;
+    p.lplus = lplus;
+    p.coef = (const c128*)coef;
+    p.damp = (const c128*)damp;
+    p.mode = mode;
+    p.H = (const c128*)H;
+    p.Hdip = (const c128*)Hdip;
+    p.Q = (const c128*)Q;
+    p.Qdip = (const c128*)Qdip;
+    p.fsv = fsv;
+    p.fcv = fcv;
+    p.snap = snap;
+    p.tim = nullptr;
+#ifdef QD_PHASE_TIMING
+    void* tw = nullptr;
+    if (int rc2 = workspace(WS_MISC, (size_t)nbands * 4 * sizeof(unsigned long long), &tw, st)) return rc2;
+    p.tim = (unsigned long long*)tw;
+#endif
+    p.nmax = nmax;
+    p.K = K;
+    p.ns = ns;
+    p.nmod = nmod;
+    p.nsteps = nsteps;
+    p.max_loc = max_loc;
+    p.dt = dt;
+    if (G == 4) {
+      const char* fe = getenv("QD_DEOM_BAND_FAST");
+      const bool fast = nmod == 1 && !(fe && fe[0] == '0');
+      if (fast && K == 5) launch_band<4, 5, true, true>(p, nbands, tpb, lds, st);        // the bench bath
+      else if (fast && K == 6) launch_band<4, 6, true, true>(p, nbands, tpb, lds, st);   // its stretch (npsd 5)
+      else if (K <= 5) launch_band<4, 5, true>(p, nbands, tpb, lds, st);
+      else launch_band<4, 8, true>(p, nbands, tpb, lds, st);
+    } else {
+      launch_band<16, 8, false>(p, nbands, tpb, lds, st);
+    }
+    QD_HIP(hipGetLastError());
+#ifdef QD_PHASE_TIMING
+    {   // per-phase wall-clock (100 MHz ticks) summed over the stages: mean and max over bands, per stage, in us
+      std::vector<unsigned long long> h((size_t)nbands * 4);
+      QD_HIP(hipMemcpyAsync(h.data(), p.tim, h.size() * 8, hipMemcpyDeviceToHost, st));
+      QD_HIP(hipStreamSynchronize(st));
+      const char* nm[4] = {"wait", "halo", "compute", "publish"};
+      for (int k = 0; k < 4; ++k) {
+        double sm = 0, mx = 0;
+        for (int b = 0; b < nbands; ++b) {
+          sm += (double)h[(size_t)b * 4 + k];
+          mx = std::max(mx, (double)h[(size_t)b * 4 + k]);
+        }
+        fprintf(stderr, "band phase %-8s mean %.3f us max %.3f us per stage\n", nm[k], sm / nbands / 100.0 / (4.0 * nsteps),
+                mx / 100.0 / (4.0 * nsteps));
+      }
+    }
+#endif
+    // the last stage 3 wrote the final rho to buf[1]
+    QD_HIP(hipMemcpyAsync(ados, buf + tot, tot * sizeof(c128), hipMemcpyDeviceToDevice, st));
+  }
+  if (trace) {
+    const int n = (nsteps + 1) * ne;
+    hipLaunchKernelGGL(deom_trace_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0, st,
+                       (const c128*)snap, (const c128*)E, ne, 1, ns, nsteps + 1, (c128*)trace);
+    QD_HIP(hipGetLastError());
+  }
+  if (!status && nsteps > 0) {
+    int h = 0;
+    QD_HIP(hipMemcpyAsync(&h, stat, sizeof(int), hipMemcpyDeviceToHost, st));
+    QD_HIP(hipStreamSynchronize(st));
+    if (h) {
+      set_error("qd_deom_rk4_banded: a band hand-off timed out (bands not co-resident); results invalid");
+      return QD_EHIP;
+    }
   }
   return QD_OK;
 }

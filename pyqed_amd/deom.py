@@ -293,6 +293,33 @@ def _action_block(A, lcr):
 
 
 # --------------------------------------------------------------------------- solver
+BANDS_MAX = 256   # one workgroup per CU at most (the bands must be co-resident)
+
+
+class _BandTables:
+    """Device copies of the tier-band partition (deom_shard.make_plans) in qd_deom_rk4_banded's layout."""
+
+    def __init__(self, plans, dev, max_own, max_loc):
+        i32 = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=np.int32))).to(dev)
+        self.nbands, self.max_own, self.max_loc = len(plans), max_own, max_loc
+        self.band_lo = i32([p.lo for p in plans] + [plans[-1].hi])
+        self.halo_off = i32(np.concatenate([[0], np.cumsum([len(p.halo) for p in plans])]))
+        halo = np.concatenate([p.halo for p in plans]) if self.halo_off[-1].item() else np.zeros(1)
+        self.halo_idx = i32(halo)
+        srcs = [sorted(p.recv) for p in plans]
+        self.src_off = i32(np.concatenate([[0], np.cumsum([len(s) for s in srcs])]))
+        self.src = i32(np.concatenate([np.asarray(s, dtype=np.int64) for s in srcs]) if sum(map(len, srcs)) else
+                       np.zeros(1))
+        self.lminus = i32(np.concatenate([p.minus for p in plans]))
+        self.lplus = i32(np.concatenate([p.plus for p in plans]))
+
+    def args(self):
+        """lminus, lplus, band_lo, halo_off, halo_idx, src_off, src, nbands, max_own, max_loc."""
+        return (self.lminus.data_ptr(), self.lplus.data_ptr(), self.band_lo.data_ptr(), self.halo_off.data_ptr(),
+                self.halo_idx.data_ptr(), self.src_off.data_ptr(), self.src.data_ptr(), self.nbands, self.max_own,
+                self.max_loc)
+
+
 class DEOMSolver:
     """Drop-in for pyqed.heom.deom.DEOMSolver (heom/deom.py:953-1125)."""
 
@@ -417,14 +444,28 @@ class DEOMSolver:
         p1_t = c128(np.asarray(p1, dtype=complex).reshape(1, ns, ns)) if p1 is not None else None
         trace = torch.empty((B, nt + 1, 1), dtype=torch.complex128, device=dev) if p1 is not None else None
         tabs = (i32(self._minus), i32(self._plus), c128(coef), c128(damp), i32(b.mode))
-        with torch.cuda.device(dev):
-            rc = getattr(_lib.load(), "qd_deom_rk4_ado_major" if ado_major else "qd_deom_rk4")(
-                ados.data_ptr(), B, nmax, K, ns, tabs[0].data_ptr(), tabs[1].data_ptr(), tabs[2].data_ptr(),
-                tabs[3].data_ptr(), tabs[4].data_ptr(), nmod, H.data_ptr(), _lib.ptr(Hdip_t), Q.data_ptr(),
-                _lib.ptr(Qdip_t), fs.ctypes.data if fs is not None else None,
-                fc.ctypes.data if fc is not None else None, float(dt), int(nt), rho_sys.data_ptr(),
-                _lib.ptr(p1_t), 1 if p1 is not None else 0, _lib.ptr(trace), _lib.stream_ptr(dev))
-        _lib.check(rc, "qd_deom_rk4_ado_major" if ado_major else "qd_deom_rk4")
+        bands = self.band_tables(dev) if B == 1 else None
+        if bands is not None:
+            status = torch.zeros(1, dtype=torch.int32, device=dev)
+            with torch.cuda.device(dev):
+                rc = _lib.load().qd_deom_rk4_banded(
+                    ados.data_ptr(), nmax, K, ns, *bands.args(), tabs[2].data_ptr(), tabs[3].data_ptr(),
+                    tabs[4].data_ptr(), nmod, H.data_ptr(), _lib.ptr(Hdip_t), Q.data_ptr(), _lib.ptr(Qdip_t),
+                    fs.ctypes.data if fs is not None else None, fc.ctypes.data if fc is not None else None, float(dt),
+                    int(nt), rho_sys.data_ptr(), _lib.ptr(p1_t), 1 if p1 is not None else 0, _lib.ptr(trace),
+                    status.data_ptr(), _lib.stream_ptr(dev))
+            _lib.check(rc, "qd_deom_rk4_banded")
+            if int(status.item()) != 0:
+                raise RuntimeError("qd_deom_rk4_banded: a band hand-off timed out (bands not co-resident)")
+        else:
+            with torch.cuda.device(dev):
+                rc = getattr(_lib.load(), "qd_deom_rk4_ado_major" if ado_major else "qd_deom_rk4")(
+                    ados.data_ptr(), B, nmax, K, ns, tabs[0].data_ptr(), tabs[1].data_ptr(), tabs[2].data_ptr(),
+                    tabs[3].data_ptr(), tabs[4].data_ptr(), nmod, H.data_ptr(), _lib.ptr(Hdip_t), Q.data_ptr(),
+                    _lib.ptr(Qdip_t), fs.ctypes.data if fs is not None else None,
+                    fc.ctypes.data if fc is not None else None, float(dt), int(nt), rho_sys.data_ptr(),
+                    _lib.ptr(p1_t), 1 if p1 is not None else 0, _lib.ptr(trace), _lib.stream_ptr(dev))
+            _lib.check(rc, "qd_deom_rk4_ado_major" if ado_major else "qd_deom_rk4")
         torch.cuda.synchronize(dev)
         self.ddos = (ados.transpose(0, 1) if ado_major else ados).cpu().numpy()   # [B][nmax][ns][ns]
         t_save = np.arange(nt + 1) * dt
@@ -432,6 +473,47 @@ class DEOMSolver:
         if p1 is not None:
             return t_save, trace[..., 0].cpu().numpy()
         return t_save, rho_sys.cpu().numpy()
+
+    def band_tables(self, dev, nbands=None):
+        """Band tables of qd_deom_rk4_banded (one hierarchy as one persistent launch over tier bands), or None
+        when the hierarchy does not qualify (ns outside [2, 4], K > 8, rows beyond one workgroup's lanes / LDS)
+        or QD_DEOM_BANDED=0.  Default band count: ~32 ADOs per band (ns = 2; 8 for ns = 3, 4), at most one band
+        per CU (the bands must be co-resident); hierarchies that would then need more than 80 (20) rows per band
+        stay on the stage launches.  Measured at 6188 ADOs: 194 bands 92k steps/s against 51.7k for the stage
+        launches; 18,564 ADOs on 256 bands 63k against 41.9k (tools/deom_band_sweep.py,
+        profiles/r03/deom/band_sweep.txt).  QD_DEOM_BANDS overrides.  Cached per (device, count)."""
+        if os.environ.get("QD_DEOM_BANDED") == "0":
+            return None
+        ns, K, nmax = self.nsys, self.nind, self.nmax
+        if not (2 <= ns <= 4) or K > 8:
+            return None
+        G = 4 if ns == 2 else 16
+        per, fat = (32, 80) if G == 4 else (8, 20)
+        cap = min(BANDS_MAX, torch.cuda.get_device_properties(dev).multi_processor_count)
+        if nbands is None:
+            env = os.environ.get("QD_DEOM_BANDS")
+            if env:
+                nbands = int(env)
+            else:
+                nbands = min(cap, max(1, -(-nmax // per)))
+                if -(-nmax // nbands) > fat:   # fat bands lose to the stage launches (146 rows: 0.78x)
+                    return None
+        nbands = max(1, min(int(nbands), nmax, cap))
+        key = (str(dev), nbands, self.lmax, K, nmax)    # the keys are a function of (lmax, K)
+        cache = getattr(self, "_band_cache", None)
+        if cache is not None and cache[0] == key:
+            return cache[1]
+        from .deom_shard import make_plans
+        plans = make_plans(self._minus, self._plus, nbands)
+        own = np.array([p.n_own for p in plans])
+        loc = np.array([p.n_loc for p in plans])
+        nmod = int(np.max(self.bath.mode)) + 1
+        if own.max() * G > 1024 or (2 + nmod + loc.max()) * ns * ns * 16 > 160 * 1024 or \
+                max(len(p.recv) for p in plans) > 64:
+            return None
+        tabs = _BandTables(plans, dev, int(own.max()), int(loc.max()))
+        self._band_cache = (key, tabs)
+        return tabs
 
     # ------------------------------------------------------------------ frequency-domain 2D signal
     def gen_generate_propgator(self):

@@ -1,0 +1,167 @@
+"""qd_deom_rk4_banded (one hierarchy as one persistent launch over tier bands) against the per-stage launch
+sequence (qd_deom_rk4: same arithmetic; bit-identical at ns = 2) and the NumPy restatement (oracle/deom.py)."""
+import numpy as np
+import pytest
+import sympy as sp
+
+from conftest import relerr
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-10
+
+
+def _bath(npsd, nmod=1):
+    from pyqed_amd.deom import Bath
+    w = sp.symbols(r"\omega", real=True)
+    return Bath([2 * 0.5 * 1.0 * w / (1.0 + w ** 2)] * nmod, w, [1.0] * nmod, [npsd] * nmod,
+                [m for m in range(nmod) for _ in range(npsd + 1)])
+
+
+def _run(sol, rho0, dt, nt, nbands, p1=None):
+    """(rho_sys or trace, final ADOs) of one hierarchy: banded with `nbands` bands, or (None) the stage launches."""
+    import torch
+    from pyqed_amd import _lib
+    from pyqed_amd.deom import ado_coefficients
+    from pyqed_amd._util import default_device
+    dev = default_device()
+    sol.check_()
+    sol.init_()
+    ns, K, nmax = sol.nsys, sol.nind, sol.nmax
+    b = sol.bath
+    coef, damp = ado_coefficients(sol.keys, np.asarray(b.etal), np.asarray(b.etar), np.asarray(b.etaa),
+                                  np.asarray(b.expn), sol.lmax)
+    c128 = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=complex))).to(dev)
+    i32 = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=np.int32))).to(dev)
+    ados = torch.zeros((nmax, ns, ns), dtype=torch.complex128, device=dev)
+    ados[0] = c128(rho0)
+    H = c128(sol.system)
+    Q = c128(np.asarray(sol.coupling, dtype=complex).reshape(-1, ns, ns))
+    nmod = Q.shape[0]
+    Hdip, fs = sol._dip_values(sol.system_dipole, sol.pulse_system_func, nt, dt, (ns, ns))
+    Qdip, fc = sol._dip_values(sol.coupling_dipole, sol.pulse_coupling_func, nt, dt, (nmod, ns, ns))
+    Hd = c128(Hdip) if Hdip is not None else None
+    Qd = c128(Qdip) if Qdip is not None else None
+    fs = np.ascontiguousarray(fs) if fs is not None else None
+    fc = np.ascontiguousarray(fc) if fc is not None else None
+    rho_sys = torch.empty((nt + 1, ns, ns), dtype=torch.complex128, device=dev)
+    p1_t = c128(np.asarray(p1, complex).reshape(1, ns, ns)) if p1 is not None else None
+    trace = torch.empty((nt + 1, 1), dtype=torch.complex128, device=dev) if p1 is not None else None
+    coef_t, damp_t, mode_t = c128(coef), c128(damp), i32(b.mode)
+    lib = _lib.load()
+    st = _lib.stream_ptr(dev)
+    fsp = fs.ctypes.data if fs is not None else None
+    fcp = fc.ctypes.data if fc is not None else None
+    if nbands is None:
+        mi, pl = i32(sol._minus), i32(sol._plus)
+        rc = lib.qd_deom_rk4(ados.data_ptr(), 1, nmax, K, ns, mi.data_ptr(), pl.data_ptr(), coef_t.data_ptr(),
+                             damp_t.data_ptr(), mode_t.data_ptr(), nmod, H.data_ptr(), _lib.ptr(Hd), Q.data_ptr(),
+                             _lib.ptr(Qd), fsp, fcp, dt, nt, rho_sys.data_ptr(), _lib.ptr(p1_t),
+                             1 if p1 is not None else 0, _lib.ptr(trace), st)
+        _lib.check(rc, "qd_deom_rk4")
+    else:
+        bt = sol.band_tables(dev, nbands)
+        assert bt is not None and bt.nbands == min(nbands, nmax)
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
+        rc = lib.qd_deom_rk4_banded(ados.data_ptr(), nmax, K, ns, *bt.args(), coef_t.data_ptr(), damp_t.data_ptr(),
+                                    mode_t.data_ptr(), nmod, H.data_ptr(), _lib.ptr(Hd), Q.data_ptr(), _lib.ptr(Qd),
+                                    fsp, fcp, dt, nt, rho_sys.data_ptr(), _lib.ptr(p1_t), 1 if p1 is not None else 0,
+                                    _lib.ptr(trace), status.data_ptr(), st)
+        _lib.check(rc, "qd_deom_rk4_banded")
+        torch.cuda.synchronize(dev)
+        assert int(status.item()) == 0
+    torch.cuda.synchronize(dev)
+    out = trace[:, 0] if p1 is not None else rho_sys
+    return out.cpu().numpy(), ados.cpu().numpy()
+
+
+def _spin_boson(L, npsd=4, pulses=False):
+    from pyqed_amd.deom import DEOMSolver
+    sx = np.array([[0, 1], [1, 0]], complex)
+    sz = np.diag([1.0, -1.0]).astype(complex)
+    if pulses:
+        return DEOMSolver(sz + sx, 0.5 * sx, _bath(npsd), np.array([sx]), np.array([0.2 * sz]),
+                          lambda t: 0.3 * np.sin(2 * t), lambda t: 0.1 * np.cos(t), L)
+    return DEOMSolver(sz + sx, None, _bath(npsd), np.array([sx]), None, None, None, L)
+
+
+@pytest.mark.parametrize("L,nbands", [(5, 1), (5, 2), (5, 7), (12, 65), (12, 128), (12, 194), (12, 256)])
+def test_banded_bit_identical_to_stage_launches(L, nbands):
+    """K = 5 at L = 5 (252 ADOs: one, two and seven bands) and the bench hierarchy (L = 12: 6188 ADOs, 65 to 256
+    bands), 12 RK4 steps."""
+    sol = _spin_boson(L)
+    rho0 = np.array([[1, 0], [0, 0]], complex)
+    ref, ref_ados = _run(sol, rho0, 0.002, 12, None)
+    got, got_ados = _run(sol, rho0, 0.002, 12, nbands)
+    assert np.array_equal(got, ref)
+    assert np.array_equal(got_ados, ref_ados)
+
+
+def test_banded_pulsed_trace_matches_oracle():
+    """Driven H(t) = H + f_s(t) Hdip, Q(t) = Q + f_c(t) Qdip, Tr(p1 rho_0), against the oracle."""
+    from oracle import deom as od
+    sol = _spin_boson(5, npsd=3, pulses=True)
+    rho0 = np.array([[1, 0], [0, 0]], complex)
+    p1 = np.diag([1.0, 0.0]).astype(complex)
+    got, _ = _run(sol, rho0, 0.01, 30, 9, p1=p1)
+    b = sol.bath
+    _, ref_rho, _ = od.run(sol.system, sol.system_dipole, sol.pulse_system_func, np.array(sol.coupling),
+                           np.array(sol.coupling_dipole), sol.pulse_coupling_func,
+                           (b.etal, b.etar, b.etaa, b.expn), 5, rho0, 0.01, 30)
+    ref = np.einsum("ij,tji->t", p1, ref_rho)
+    assert relerr(got, ref) < TOL
+    ref2, _ = _run(sol, rho0, 0.01, 30, None, p1=p1)
+    assert np.array_equal(got, ref2)
+
+
+@pytest.mark.parametrize("ns,nmod", [(3, 1), (4, 2)])
+def test_banded_ns3_ns4_matches_stage_launches_and_oracle(ns, nmod):
+    """16 lanes per ADO (ns = 3, 4), two bath modes (K = 8: the KMAX = 8 instantiation)."""
+    from oracle import deom as od
+    from pyqed_amd.deom import DEOMSolver
+    rng = np.random.default_rng(ns)
+    A = rng.standard_normal((ns, ns)) + 1j * rng.standard_normal((ns, ns))
+    H = (A + A.conj().T) / 4
+    Qs = []
+    for _ in range(nmod):
+        B = rng.standard_normal((ns, ns))
+        Qs.append((B + B.T) / 4)
+    npsd = 3
+    sol = DEOMSolver(H, None, _bath(npsd, nmod), np.array(Qs, dtype=complex), None, None, None, 4)
+    rho0 = np.zeros((ns, ns), complex)
+    rho0[0, 0] = 1
+    got, got_ados = _run(sol, rho0, 0.01, 15, 11)
+    ref, ref_ados = _run(sol, rho0, 0.01, 15, None)
+    # same formula as the 16-lane group kernel; the compilers' FMA contraction may differ in the last bit
+    assert relerr(got, ref) < 1e-14
+    assert relerr(got_ados, ref_ados) < 1e-14
+    b = sol.bath
+    _, orc, _ = od.run(H, np.zeros((ns, ns)), lambda t: 0, np.array(Qs, dtype=complex),
+                       np.zeros((nmod, ns, ns)), lambda t: 0, (b.etal, b.etar, b.etaa, b.expn), 4, rho0, 0.01, 15,
+                       mode=np.asarray(b.mode))
+    assert relerr(got, orc) < TOL
+
+
+def test_solver_run_takes_banded_path_and_env_disables_it(monkeypatch):
+    """DEOMSolver.run (B = 1) runs the banded launch by default; QD_DEOM_BANDED=0 gives the stage launches."""
+    import torch
+    from pyqed_amd._util import default_device
+    sol = _spin_boson(8)
+    rho0 = np.array([[1, 0], [0, 0]], complex)
+    t, a = sol.run(rho0.copy(), 0.005, 20)
+    assert sol.band_tables(default_device()) is not None
+    monkeypatch.setenv("QD_DEOM_BANDED", "0")
+    assert sol.band_tables(default_device()) is None
+    t2, b = sol.run(rho0.copy(), 0.005, 20)
+    assert np.array_equal(np.array(a), np.array(b))
+    torch.cuda.synchronize()
+
+
+def test_banded_stretch_hierarchy_256_bands_matches_stage_launches():
+    """The stretch hierarchy (npsd = 5, K = 6, L = 12: 18,564 ADOs) on 256 bands (the default there; the generic
+    K <= 8 instantiation), 6 steps."""
+    sol = _spin_boson(12, npsd=5)
+    rho0 = np.array([[1, 0], [0, 0]], complex)
+    ref, ref_ados = _run(sol, rho0, 0.001, 6, None)
+    got, got_ados = _run(sol, rho0, 0.001, 6, 256)
+    assert np.array_equal(got, ref)
+    assert np.array_equal(got_ados, ref_ados)
