@@ -477,10 +477,10 @@ class DEOMSolver:
     def band_tables(self, dev, nbands=None):
         """Band tables of qd_deom_rk4_banded (one hierarchy as one persistent launch over tier bands), or None
         when the hierarchy does not qualify (ns outside [2, 4], K > 8, rows beyond one workgroup's lanes / LDS)
-        or QD_DEOM_BANDED=0.  Default band count: ~32 ADOs per band (ns = 2; 8 for ns = 3, 4), at most one band
+        or QD_DEOM_BANDED=0.  Default band count: ~24 ADOs per band (ns = 2; 8 for ns = 3, 4), at most one band
         per CU (the bands must be co-resident); hierarchies that would then need more than 80 (20) rows per band
-        stay on the stage launches.  Measured at 6188 ADOs: 194 bands 92k steps/s against 51.7k for the stage
-        launches; 18,564 ADOs on 256 bands 63k against 41.9k (tools/deom_band_sweep.py,
+        stay on the stage launches.  Measured at 6188 ADOs: 256 bands 94.7k steps/s against 51.7k for the stage
+        launches; 18,564 ADOs on 256 bands 68k against 42.1k (tools/deom_band_sweep.py,
         profiles/r03/deom/band_sweep.txt).  QD_DEOM_BANDS overrides.  Cached per (device, count)."""
         if os.environ.get("QD_DEOM_BANDED") == "0":
             return None
@@ -488,7 +488,7 @@ class DEOMSolver:
         if not (2 <= ns <= 4) or K > 8:
             return None
         G = 4 if ns == 2 else 16
-        per, fat = (32, 80) if G == 4 else (8, 20)
+        per, fat = (24, 80) if G == 4 else (8, 20)
         cap = min(BANDS_MAX, torch.cuda.get_device_properties(dev).multi_processor_count)
         if nbands is None:
             env = os.environ.get("QD_DEOM_BANDS")
