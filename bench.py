@@ -799,6 +799,10 @@ def bench_deom(dev, steps, batch):
         "roofline": {"bound": "hbm", "achieved": round(bytes_per_step * single / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(bytes_per_step * single / 1e9 / HBM_PEAK_GBS, 4),
                      "bytes_per_step": bytes_per_step,
+                     "kernel": "deom_band_kernel<4,5,true,256,true>" if bt is not None else "deom_stage_grp_kernel",
+                     "traffic": measured_traffic("deom_band_kernel<4,5,true,256,true>", 1) if bt is not None else None,
+                     "traffic_unit": "HBM / fabric bytes per RK4 step (PMC FETCH_SIZE+WRITE_SIZE, calibrated; "
+                                     "profiles/pmc_traffic.json): the halo rows every band gathers per stage",
                      "note": "latency-bound: 4 dependent RK4 stages per step on a 396 KB state; the banded launch "
                              "hands each stage's rows between the bands inside one launch (per-stage hand-off "
                              "latency, no kernel boundaries)"},
