@@ -44,10 +44,36 @@ constexpr int MAX_LDS_M = (int)(LDS_MAX / (2 * sizeof(c128)));   // 5120
 
 enum Kind { MIXED = 0, BLUESTEIN = 1, DIRECT = 2 };
 
+// Division by a launch-invariant divisor d >= 1 as a multiply-high (Granlund-Montgomery / Hacker's Delight 10-8,
+// exact for every 32-bit x): l = ceil(log2 d), m = floor(2^32 (2^l - d) / d) + 1, t = umulhi(x, m),
+// x / d = (t + ((x - t) >> 1)) >> (l - 1); d = 1 is x itself.  The element loops of the LDS passes divide their
+// flat index by runtime lengths several times per element; a 32-bit udiv is ~25 VALU instructions, this is 5.
+struct FDiv {
+  unsigned d, m, s;
+};
+inline FDiv make_fdiv(unsigned d) {
+  FDiv r{d, 0u, 0u};
+  if (d > 1) {
+    unsigned l = 0;
+    while ((1ull << l) < d) ++l;
+    r.m = (unsigned)((((unsigned long long)1 << 32) * ((1ull << l) - d)) / d + 1);
+    r.s = l - 1;
+  }
+  return r;
+}
+__host__ __device__ __forceinline__ unsigned fdiv(unsigned x, FDiv D) {
+  if (D.d == 1) return x;
+  const unsigned t = (unsigned)(((unsigned long long)x * D.m) >> 32);
+  return (t + ((x - t) >> 1)) >> D.s;
+}
+
 struct Fft {           // device-side plan of one axis, passed by value
   int L, M, kind, nst;
   int R[MAX_ST];
   int Ns[MAX_ST];
+  FDiv dnb[MAX_ST];    // M / R[s]
+  FDiv dns[MAX_ST];    // Ns[s]
+  FDiv dM;             // M
   const c128* tw;      // exp(-2 pi i m / M), m < M (DIRECT: M = L)
   const c128* chirp;   // BLUESTEIN: exp(-pi i n^2 / L), n < L
   const c128* bhat;    // BLUESTEIN: (1/M) FFT_M(b), b_m = conj(c_|m|) wrapped
@@ -58,6 +84,7 @@ enum Flags { F_INV = 1, F_PT1 = 2, F_SNAP = 4, F_PT2 = 8, F_FWD = 16, F_KY = 32,
 struct AxisArgs {
   c128* psi;
   int O, L, I, C, G, flags, ns;
+  FDiv dLC, dC, dLns, dns;   // L C, C, L ns, ns
   int twl;             // 1: twiddles staged in LDS (M more c128 of dynamic LDS)
   const c128* U1;      // [points][ns][ns] (F_PT1)
   const c128* U2;      // (F_PT2)
@@ -69,18 +96,20 @@ struct AxisArgs {
 // ---------------------------------------------------------------- device FFT
 // One Stockham stage over nl lines of length M: butterfly j of a line reads src[j + r M/R] (r < R) times
 // tw^(r k M/(Ns R)), k = j mod Ns, and writes the R-point DFT to dst[(j / Ns) Ns R + k + q Ns].
-template <bool INV>
-__device__ __forceinline__ void stage(const c128* __restrict__ src, c128* __restrict__ dst, int nl, int M, int R,
-                                      int Ns, const c128* __restrict__ tw) {
+template <bool INV, int R0>   // R0 = 2, 3, 4, 5: closed-form butterflies; 0: any prime R <= GEN_MAXP
+__device__ __forceinline__ void stage(const c128* __restrict__ src, c128* __restrict__ dst, int nl, int M, int Rr,
+                                      int Ns, FDiv dnb, FDiv dns, const c128* __restrict__ tw) {
+  const int R = R0 ? R0 : Rr;
   const int nb = M / R;
   const int tot = nl * nb;
   const int tstep = M / (Ns * R);
   for (int f = threadIdx.x; f < tot; f += blockDim.x) {
-    const int l = f / nb, j = f - l * nb;
+    const int l = (int)fdiv((unsigned)f, dnb), j = f - l * nb;
     const c128* s = src + (size_t)l * M;
     c128* d = dst + (size_t)l * M;
-    const int k = j % Ns;
-    const int db = (j / Ns) * Ns * R + k;
+    const int jq = (int)fdiv((unsigned)j, dns);
+    const int k = j - jq * Ns;
+    const int db = jq * Ns * R + k;
     auto ld = [&](int r) {
       const c128 x = s[j + r * nb];
       if (r == 0 || k == 0) return x;
@@ -88,7 +117,7 @@ __device__ __forceinline__ void stage(const c128* __restrict__ src, c128* __rest
       if (INV) w = cconj(w);
       return cmul(x, w);
     };
-    if (R == 4) {
+    if constexpr (R0 == 4) {
       const c128 x0 = ld(0), x1 = ld(1), x2 = ld(2), x3 = ld(3);
       const c128 a0 = cadd(x0, x2), a1 = csub(x0, x2), b0 = cadd(x1, x3), b1 = csub(x1, x3);
       const c128 ib1 = INV ? cmuli(b1) : cmulmi(b1);
@@ -96,11 +125,11 @@ __device__ __forceinline__ void stage(const c128* __restrict__ src, c128* __rest
       d[db + Ns] = cadd(a1, ib1);
       d[db + 2 * Ns] = csub(a0, b0);
       d[db + 3 * Ns] = csub(a1, ib1);
-    } else if (R == 2) {
+    } else if constexpr (R0 == 2) {
       const c128 x0 = ld(0), x1 = ld(1);
       d[db] = cadd(x0, x1);
       d[db + Ns] = csub(x0, x1);
-    } else if (R == 3) {
+    } else if constexpr (R0 == 3) {
       const double c = -0.5, sn = 0.86602540378443864676;   // cos, sin(2 pi / 3)
       const c128 x0 = ld(0), x1 = ld(1), x2 = ld(2);
       const c128 t = cadd(x1, x2), u = csub(x1, x2);
@@ -109,7 +138,7 @@ __device__ __forceinline__ void stage(const c128* __restrict__ src, c128* __rest
       d[db] = cadd(x0, t);
       d[db + Ns] = cadd(a, b);
       d[db + 2 * Ns] = csub(a, b);
-    } else if (R == 5) {
+    } else if constexpr (R0 == 5) {
       const double c1 = 0.30901699437494742410, c2 = -0.80901699437494742410;   // cos(2 pi/5), cos(4 pi/5)
       const double s1 = 0.95105651629515357212, s2 = 0.58778525229247312917;    // sin(2 pi/5), sin(4 pi/5)
       const c128 x0 = ld(0), x1 = ld(1), x2 = ld(2), x3 = ld(3), x4 = ld(4);
@@ -140,13 +169,18 @@ __device__ __forceinline__ void stage(const c128* __restrict__ src, c128* __rest
     }
   }
 }
-
-// Mixed-radix transform of nl lines (cur -> result in cur; oth is the ping-pong buffer).  Every thread
-// of the workgroup must call it (barriers); it starts and ends behind a barrier.
 template <bool INV>
 __device__ __forceinline__ void stockham(const Fft& p, const c128* tw, c128*& cur, c128*& oth, int nl, int M) {
   for (int s = 0; s < p.nst; ++s) {
-    stage<INV>(cur, oth, nl, M, p.R[s], p.Ns[s], tw);
+    const int R = p.R[s], Ns = p.Ns[s];
+    const FDiv dnb = p.dnb[s], dns = p.dns[s];   // copies: a reference would put the plan in scratch
+    switch (R) {   // wave-uniform: one branch-free element loop per radix
+      case 4: stage<INV, 4>(cur, oth, nl, M, 4, Ns, dnb, dns, tw); break;
+      case 2: stage<INV, 2>(cur, oth, nl, M, 2, Ns, dnb, dns, tw); break;
+      case 3: stage<INV, 3>(cur, oth, nl, M, 3, Ns, dnb, dns, tw); break;
+      case 5: stage<INV, 5>(cur, oth, nl, M, 5, Ns, dnb, dns, tw); break;
+      default: stage<INV, 0>(cur, oth, nl, M, R, Ns, dnb, dns, tw); break;
+    }
     __syncthreads();
     c128* t = cur;
     cur = oth;
@@ -162,7 +196,7 @@ __device__ __forceinline__ void lds_fft(const Fft& p, const c128* tw, c128*& cur
   if (p.kind == BLUESTEIN) {
     const int tot = nl * M;
     for (int f = threadIdx.x; f < tot; f += blockDim.x) {
-      const int n = f % M;
+      const int n = f - (int)fdiv((unsigned)f, p.dM) * M;
       c128 v = cmk(0.0, 0.0);
       if (n < L) {
         c128 ch = p.chirp[n];
@@ -174,14 +208,14 @@ __device__ __forceinline__ void lds_fft(const Fft& p, const c128* tw, c128*& cur
     __syncthreads();
     stockham<false>(p, tw, cur, oth, nl, M);
     for (int f = threadIdx.x; f < tot; f += blockDim.x) {
-      c128 b = p.bhat[f % M];
+      c128 b = p.bhat[f - (int)fdiv((unsigned)f, p.dM) * M];
       if (INV) b = cconj(b);
       cur[f] = cmul(cur[f], b);
     }
     __syncthreads();
     stockham<true>(p, tw, cur, oth, nl, M);
     for (int f = threadIdx.x; f < tot; f += blockDim.x) {
-      const int n = f % M;
+      const int n = f - (int)fdiv((unsigned)f, p.dM) * M;
       if (n < L) {
         c128 ch = p.chirp[n];
         if (INV) ch = cconj(ch);
@@ -212,7 +246,7 @@ __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
   const int gv = min(G, a.O - o0), cv = min(C, I - i0);
   const int tot = G * L * C;
   for (int f = threadIdx.x; f < tot; f += blockDim.x) {
-    const int g = f / (L * C), r = f - g * (L * C), e = r / C, c = r - e * C;
+    const int g = (int)fdiv((unsigned)f, a.dLC), r = f - g * (L * C), e = (int)fdiv((unsigned)r, a.dC), c = r - e * C;
     cur[(g * C + c) * M + e] =
         (g < gv && c < cv) ? a.psi[((size_t)(o0 + g) * L + e) * I + i0 + c] : cmk(0.0, 0.0);
   }
@@ -222,7 +256,8 @@ __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
     const int ns = a.ns;
     const int n = G * L * ns;
     for (int f = threadIdx.x; f < n; f += blockDim.x) {
-      const int g = f / (L * ns), r = f - g * (L * ns), e = r / ns, s = r - e * ns;
+      const int g = (int)fdiv((unsigned)f, a.dLns), r = f - g * (L * ns), e = (int)fdiv((unsigned)r, a.dns),
+                s = r - e * ns;
       if (g >= gv) continue;
       const c128* u = U + (((size_t)(o0 + g) * L + e) * ns + s) * ns;
       c128 acc = cmk(0.0, 0.0);
@@ -237,7 +272,7 @@ __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
   if (a.flags & F_PT1) point_op(a.U1);
   if (a.flags & F_SNAP) {
     for (int f = threadIdx.x; f < tot; f += blockDim.x) {
-      const int g = f / (L * C), r = f - g * (L * C), e = r / C, c = r - e * C;
+      const int g = (int)fdiv((unsigned)f, a.dLC), r = f - g * (L * C), e = (int)fdiv((unsigned)r, a.dC), c = r - e * C;
       if (g < gv && c < cv) a.snap[((size_t)(o0 + g) * L + e) * I + i0 + c] = cur[(g * C + c) * M + e];
     }
   }
@@ -245,7 +280,7 @@ __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
   if (a.flags & F_FWD) lds_fft<false>(p, tw, cur, oth, nl);
   if (a.flags & F_KY) {
     for (int f = threadIdx.x; f < tot; f += blockDim.x) {
-      const int g = f / (L * C), r = f - g * (L * C), e = r / C, c = r - e * C;
+      const int g = (int)fdiv((unsigned)f, a.dLC), r = f - g * (L * C), e = (int)fdiv((unsigned)r, a.dC), c = r - e * C;
       if (g < gv) cur[(g * C + c) * M + e] = cmul(a.Ky[(size_t)(o0 + g) * L + e], cur[(g * C + c) * M + e]);
     }
     __syncthreads();
@@ -254,14 +289,14 @@ __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
     lds_fft<false>(p, tw, cur, oth, nl);
     const int pts = I / a.ns;
     for (int f = threadIdx.x; f < tot; f += blockDim.x) {
-      const int r = f % (L * C), e = r / C, c = r - e * C;
-      if (c < cv) cur[c * M + e] = cmul(cur[c * M + e], a.K[(size_t)e * pts + (i0 + c) / a.ns]);
+      const int r = f - (int)fdiv((unsigned)f, a.dLC) * (L * C), e = (int)fdiv((unsigned)r, a.dC), c = r - e * C;
+      if (c < cv) cur[c * M + e] = cmul(cur[c * M + e], a.K[(size_t)e * pts + (int)fdiv((unsigned)(i0 + c), a.dns)]);
     }
     __syncthreads();
     lds_fft<true>(p, tw, cur, oth, nl);
   }
   for (int f = threadIdx.x; f < tot; f += blockDim.x) {
-    const int g = f / (L * C), r = f - g * (L * C), e = r / C, c = r - e * C;
+    const int g = (int)fdiv((unsigned)f, a.dLC), r = f - g * (L * C), e = (int)fdiv((unsigned)r, a.dC), c = r - e * C;
     if (g < gv && c < cv) a.psi[((size_t)(o0 + g) * L + e) * I + i0 + c] = cur[(g * C + c) * M + e];
   }
 }
@@ -557,9 +592,14 @@ int next_smooth(int n) {  // smallest 2^a 3^b 5^c >= n
 void factor_stages(int M, Fft& f) {
   f.nst = 0;
   int ns = 1, n = M;
+  f.dM = make_fdiv((unsigned)M);
   auto push = [&](int r) {
-    f.R[f.nst] = r;
-    f.Ns[f.nst] = ns;
+    if (f.nst < MAX_ST) {
+      f.R[f.nst] = r;
+      f.Ns[f.nst] = ns;
+      f.dnb[f.nst] = make_fdiv((unsigned)(M / r));
+      f.dns[f.nst] = make_fdiv((unsigned)ns);
+    }
     ++f.nst;
     ns *= r;
     n /= r;
@@ -615,6 +655,7 @@ int plan_axis(int L, c128* tab, Fft& f, hipStream_t st) {
   f.nst = 0;
   hipLaunchKernelGGL(twiddle_table_kernel, dim3((M + 255) / 256), dim3(256), 0, st, M, tab);
   QD_HIP(hipGetLastError());
+  f.dM = make_fdiv((unsigned)M);
   if (kind != DIRECT) factor_stages(M, f);
   if (f.nst > MAX_ST) {
     set_error("spo: FFT plan of length %d needs %d stages (max %d)", M, f.nst, MAX_ST);
@@ -665,6 +706,10 @@ struct Exec {
     a.L = n[d];
     a.I = (int)inner(d);
     a.C = C;
+    a.dLC = make_fdiv((unsigned)(n[d] * C));
+    a.dC = make_fdiv((unsigned)C);
+    a.dLns = make_fdiv((unsigned)(n[d] * ns));
+    a.dns = make_fdiv((unsigned)ns);
     a.G = G;
     a.flags = flags;
     a.ns = ns;

@@ -55,6 +55,8 @@ for n in cases2:
     byts = 4 * n * n * ns * 16 + n * n * ns * ns * 16 + n * n * 16
     print(json.dumps({"case": f"spo2 {n}x{n}x2", "us_per_step": round(sec * 1e6, 2), "steps_per_s": round(1 / sec, 1),
                       "GBps": round(byts / sec / 1e9, 1)}), flush=True)
+if len(sys.argv) > 2 and sys.argv[2] == "2d":
+    sys.exit(0)
 for n in (48, 60, 64, 96, 100, 128):
     ns = 2
     U = t(unit_ops((n, n, n), ns, rng))
