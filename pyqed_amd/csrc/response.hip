@@ -216,7 +216,7 @@ __global__ __launch_bounds__(256) void ens_z_uniform_kernel(const c128* Mt, cons
                                                             int nL, int nz, int G, double t0, double dt, int n1,
                                                             int n1p, c128* Z, const c128* alpha, const c128* lamx,
                                                             int K, int Kp, double t3_0, double dt3, int n3, int n3p,
-                                                            int xbx, c128* X) {
+                                                            int xbx, c128* X, int recur) {
   extern __shared__ c128 zs[];
   const int nMB = (M + G - 1) / G;
   if ((int)blockIdx.y >= nMB) {
@@ -241,17 +241,41 @@ __global__ __launch_bounds__(256) void ens_z_uniform_kernel(const c128* Mt, cons
   __syncthreads();
   // round 2: the exponential tables from LDS operands (no global latency inside the loop)
   const int tab = nz * (16 + nC);
-  for (int e = threadIdx.x; e < g * tab; e += 256) {
-    const int gi = e / tab, r = e % tab;
-    c128 v;
-    if (r < nz * 16) {
-      v = cexp_t(sLam[gi * nz + r / 16], (double)(r % 16) * dt);
-    } else {
-      const int u = r - nz * 16;
-      const int q = u / nC;
-      v = cmul(sBeta[gi * nz + q], cexp_t(sLam[gi * nz + q], t0 + 16.0 * (double)(u % nC) * dt));
+  if (recur) {
+    // one thread per (member, q): fine[j] = e^{lam j dt} as powers of e^{lam dt}, coarse[l] = beta e^{lam t0} times
+    // powers of e^{16 lam dt} (3 exponentials instead of 16 + nC; relative error ~1e-14)
+    for (int e = threadIdx.x; e < g * nz; e += 256) {
+      const int gi = e / nz, q = e - gi * nz;
+      const c128 l = sLam[gi * nz + q];
+      c128* fine = zs + gi * per + nL * nz + q * 16;
+      c128* coarse = zs + gi * per + nL * nz + nz * 16 + q * nC;
+      const c128 e1 = cexp_t(l, dt);
+      c128 f = cmk(1.0, 0.0);
+      fine[0] = f;
+      for (int j = 1; j < 16; ++j) {
+        f = cmul(f, e1);
+        fine[j] = f;
+      }
+      const c128 e16 = cexp_t(l, 16.0 * dt);
+      c128 c = cmul(sBeta[gi * nz + q], cexp_t(l, t0));
+      for (int u = 0; u < nC; ++u) {
+        coarse[u] = c;
+        c = cmul(c, e16);
+      }
     }
-    zs[gi * per + nL * nz + r] = v;
+  } else {
+    for (int e = threadIdx.x; e < g * tab; e += 256) {
+      const int gi = e / tab, r = e % tab;
+      c128 v;
+      if (r < nz * 16) {
+        v = cexp_t(sLam[gi * nz + r / 16], (double)(r % 16) * dt);
+      } else {
+        const int u = r - nz * 16;
+        const int q = u / nC;
+        v = cmul(sBeta[gi * nz + q], cexp_t(sLam[gi * nz + q], t0 + 16.0 * (double)(u % nC) * dt));
+      }
+      zs[gi * per + nL * nz + r] = v;
+    }
   }
   __syncthreads();
   const int k = blockIdx.x * 256 + threadIdx.x;
@@ -272,6 +296,15 @@ __global__ __launch_bounds__(256) void ens_z_uniform_kernel(const c128* Mt, cons
       Z[((size_t)(m0 + gi) * nL + p) * n1p + k] = v;
     }
   }
+}
+
+// Z tables by recurrence (default) or one exponential per entry (QD_Z_RECUR=0, A/B)
+int z_recur() {
+  static const int r = [] {
+    const char* e = std::getenv("QD_Z_RECUR");
+    return e ? std::atoi(e) : 1;
+  }();
+  return r;
 }
 
 // members per block of ens_z_uniform_kernel: tables of <= 32 KB LDS, at most 32 members
@@ -488,7 +521,7 @@ __global__ void ens_reduce_kernel(const c128* slabs, int S, int n3, int n1, int 
   for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
     const int i = (int)(e / n1), k = (int)(e % n1);
     c128 v = accumulate ? out[e] : cmk(0, 0);
-    for (int s = 0; s < S; ++s) v = cadd(v, slabs[((size_t)s * n3p + i) * n1p + k]);
+    v = slab_sum(v, 0, S, [&](int s) { return slabs[((size_t)s * n3p + i) * n1p + k]; });
     out[e] = v;
   }
 }
@@ -502,8 +535,7 @@ __global__ __launch_bounds__(256) void ens_reduce_trans_kernel(const c128* slabs
   {
     const int i = i0 + ty, k = k0 + tx;
     c128 v = cmk(0, 0);
-    if (i < n3 && k < n1)
-      for (int s = 0; s < S; ++s) v = cadd(v, slabs[((size_t)s * n3p + i) * n1p + k]);
+    if (i < n3 && k < n1) v = slab_sum(v, 0, S, [&](int s) { return slabs[((size_t)s * n3p + i) * n1p + k]; });
     tile[ty][tx] = v;
   }
   __syncthreads();
@@ -525,7 +557,7 @@ __global__ void ens_reduce_t2_kernel(const c128* slabs, int S, int n2, int n3, i
     const int i = (int)((e / n1) % n3);
     const int j = (int)(e / ((size_t)n1 * n3));
     c128 v = accumulate ? out[e] : cmk(0, 0);
-    for (int s = 0; s < S; ++s) v = cadd(v, slabs[((size_t)s * n3p + i) * ldz + (size_t)j * n1p + k]);
+    v = slab_sum(v, 0, S, [&](int s) { return slabs[((size_t)s * n3p + i) * ldz + (size_t)j * n1p + k]; });
     out[e] = v;
   }
 }
@@ -791,7 +823,8 @@ int ens_run(const char* fn, const qd_c128* alpha, const qd_c128* Mt, const qd_c1
     const bool xin = !t3 && !xtab;
     hipLaunchKernelGGL(ens_z_uniform_kernel, dim3(zbx, nMB + (xin ? xblocks : 0)), dim3(256),
                        z_lds(G, nL, nz, n1p), st, (const c128*)Mt, (const c128*)beta, lamz, M, nL, nz, G, t1_0,
-                       dt1, n1, n1p, Z, (const c128*)alpha, (const c128*)lam, K, Kp, t3_0, dt3, n3, n3p, xbx, X);
+                       dt1, n1, n1p, Z, (const c128*)alpha, (const c128*)lam, K, Kp, t3_0, dt3, n3, n3p, xbx, X,
+                       z_recur());
     QD_HIP(hipGetLastError());
     if (Kp > K) {
       hipLaunchKernelGGL(ens_z_pad_kernel, dim3(64), dim3(256), 0, st, K, Kp, n1p, Z);
@@ -928,7 +961,7 @@ extern "C" int qd_response2d_t2_operands_rect(const qd_c128* alpha, const qd_c12
   hipLaunchKernelGGL(ens_z_uniform_kernel, dim3(ceil_div(d.n1p, 256), ceil_div(M, G)), dim3(256),
                      z_lds(G, nr, nq, d.n1p), st, (const c128*)Cm,
                      (const c128*)beta, (const c128*)lamq, M, nr, nq, G, t1_0, dt1, n1, d.n1p, Q, (const c128*)nullptr,
-                     (const c128*)nullptr, d.K, d.Kp, 0.0, 0.0, n3, d.n3p, 1, (c128*)nullptr);
+                     (const c128*)nullptr, d.K, d.Kp, 0.0, 0.0, n3, d.n3p, 1, (c128*)nullptr, z_recur());
   QD_HIP(hipGetLastError());
   if (d.Kp > d.K) {
     hipLaunchKernelGGL(ens_z_pad_kernel, dim3(64), dim3(256), 0, st, d.K, d.Kp, d.n1p, Q);

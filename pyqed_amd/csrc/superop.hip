@@ -123,7 +123,7 @@ __global__ void superop_gemm_rk4_kernel(const c128* slabs, int S, size_t tot, c1
                                         double dt, int stage) {
   for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
     c128 k = slabs[e];
-    for (int q = 1; q < S; ++q) k = cadd(k, slabs[(size_t)q * tot + e]);
+    k = slab_sum(k, 1, S, [&](int q) { return slabs[(size_t)q * tot + e]; });
     const c128 p = X[e];
     if (stage == 0) {
       acc[e] = k;
