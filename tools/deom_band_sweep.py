@@ -22,7 +22,7 @@ def main():
     w = sp.symbols(r"\omega", real=True)
     sx = np.array([[0, 1], [1, 0]], complex)
     sz = np.diag([1.0, -1.0]).astype(complex)
-    cases = ((4, 0.002, (65, 96, 128, 160, 192, 256)), (5, 0.001, (128, 192, 256)))
+    cases = ((4, 0.002, (65, 96, 128, 160, 192, 224, 256)), (5, 0.001, (128, 192, 256)))
     if only:
         cases = ((4, 0.002, only),)
     for npsd, dt, counts in cases:
