@@ -17,14 +17,21 @@
 // Kernel layout: one 512-thread workgroup owns one density matrix for the
 // whole run (persistent over nsteps RK4 steps; only workgroup barriers, no
 // inter-workgroup communication).  Per RK4 stage:
-//   phase 1: Y_c = L_c * rs                       (block GEMM, K = N)
-//   phase 2: k   = P rs + rs Q + sum_c Y_c R_c    (one accumulator,
-//            2+nc segments), fused epilogue does the RK4 bookkeeping
-//            (acc += w k ; rs' = rho + c k ; rho update at stage 4).
-// rs (two ping-pong buffers), acc and Y_c live in a per-workgroup scratch
-// slab in HBM (L2/MALL resident in practice).  Matrices are zero-padded to
-// Np = 32, 64 or a multiple of 128 so every GEMM tile is full; the padding
-// stays exactly zero through the propagation.
+//   phase 1: Y_c = L_c * s                        (block GEMM, K = N)
+//   phase 2: k   = P s + s Q + sum_c Y_c R_c      (one accumulator,
+//            2+nc segments), fused epilogue s' = rho + c_m k.
+// RK4 in Horner form: for a generator L that is constant over the step (every
+// path here: H(t) of the driven runs is frozen per step, oqs.py:1780-1786),
+// the classical RK4 update equals the degree-4 Taylor polynomial
+//   rho' = rho + dt L(rho + dt/2 L(rho + dt/3 L(rho + dt/4 L rho)))
+// so stage m reads s_m (s_0 = rho) and writes s_{m+1} = rho + dt/(4-m) L s_m,
+// s_4 = rho'.  No RK4 accumulator: the epilogue reads rho and writes s_{m+1}
+// (round 2 also read and wrote acc).  Equal to phys.rk4 (phys.py:1051-1064)
+// in exact arithmetic; the tests hold it to the oracle's RK4 at 1e-12.
+// s (one buffer for a single GEMM block, else two alternating) and Y_c live
+// in a per-workgroup scratch slab in HBM (L2/MALL resident in practice).
+// Matrices are zero-padded to Np = 32, 64 or a multiple of 128 so every GEMM
+// tile is full; the padding stays exactly zero through the propagation.
 #include "cgemm_block.hpp"
 
 #include <cstdio>
@@ -61,10 +68,15 @@ struct LindbladParams {
   unsigned* ticket;            // [B][1 + nc][nb^2] arrival counters (zero between launches)
 };
 
-// Per-matrix scratch slots of Np x Np: stage buffer(s), RK4 accumulator, Y_c.
+// Per-matrix scratch slots of Np x Np: stage buffer(s), Y_c.
 __host__ __device__ inline int glf_slots(int Np, int nc, int herm) {
   (void)herm;
-  return (Np <= 128 ? 1 : 2) + 1 + nc;
+  return (Np <= 128 ? 1 : 2) + nc;
+}
+
+// Horner coefficient of RK4 stage m (0..3): s_{m+1} = rho + dt / (4 - m) L s_m  (see the file header)
+__device__ __forceinline__ double glf_horner_coef(double dt, int stage) {
+  return stage == 0 ? dt * 0.25 : stage == 1 ? dt / 3.0 : stage == 2 ? dt * 0.5 : dt;
 }
 
 #ifdef QD_PHASE_TIMING
@@ -124,10 +136,6 @@ __device__ void wg_observables(const c128* rho, const c128* eT, int ne, size_t N
 #ifndef GLF_HERM_X
 #define GLF_HERM_X 1   // Hermitian kernel at BT = 128: X GEMM on the CgHermLayout tiles (Lindblad: no Hermitian part below the diagonal; A/B: 0)
 #endif
-#ifndef GLF_EPI_PF
-#define GLF_EPI_PF 0   // Hermitian epilogue: rho / acc loads kept this many update slots ahead (0: chunks of QD_EPI_CH;
-                       // 4: 328-332k vs 330-332k DM-steps/s for 0, profiles/r03/lindblad/epi_pf_ab.txt: no gain)
-#endif
 #ifndef GLF_HERM_PIPE
 #define GLF_HERM_PIPE false   // fragment double-buffering in the Hermitian kernel's GEMMs (A/B builds)
 #endif
@@ -149,17 +157,14 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
   const bool single = (Np / BT) == 1;
   c128* ws = p.ws + (size_t)b * glf_slots(Np, nc, HERM) * NN;
   c128* rbuf1 = single ? ws : ws + NN;
-  c128* acc = single ? ws + NN : ws + 2 * NN;
-  c128* Y = acc + NN;
+  c128* Y = single ? ws + NN : ws + 2 * NN;
   c128* obs = p.obs ? p.obs + (size_t)b * (p.total_steps + 1) * p.ne : nullptr;
 
-  for (size_t i = threadIdx.x; i < NN; i += CG_WG) ws[i] = rho[i];
   if (p.ne > 0 && p.step0 == 0) wg_observables(rho, p.eT, p.ne, NN, obs, sred);
   __syncthreads();
 
   const int nb = Np / BT;
-  const double dt = p.dt, dt2 = p.dt / 2.0;
-  int cur = 0;
+  const double dt = p.dt;
   CgAcc<BT> A;
   // Phase offset: the workgroups run identical schedules, so without an offset every CU reaches its
   // memory-bound RK4 epilogue at the same moment.  Delaying every other workgroup of each XCD
@@ -172,26 +177,11 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
 
   for (int step = 0; step < p.nsteps; ++step) {
     for (int stage = 0; stage < 4; ++stage) {
-      const c128* r = cur ? rbuf1 : ws;
-      c128* rn = cur ? ws : rbuf1;
-      auto rk4_update = [&](size_t idx, c128 k) {
-        const c128 r0 = rho[idx];
-        if (stage == 0) {
-          acc[idx] = k;
-          rn[idx] = cadd(r0, cscale(k, dt2));
-        } else if (stage == 1) {
-          acc[idx] = cadd(acc[idx], cscale(k, 2.0));
-          rn[idx] = cadd(r0, cscale(k, dt2));
-        } else if (stage == 2) {
-          acc[idx] = cadd(acc[idx], cscale(k, 2.0));
-          rn[idx] = cadd(r0, cscale(k, dt));
-        } else {
-          const c128 a = cadd(acc[idx], k);
-          const c128 r1 = cadd(r0, cscale(cscale(a, 1.0 / 6.0), dt));
-          rho[idx] = r1;
-          rn[idx] = r1;
-        }
-      };
+      // Horner stages (glf_horner_coef): rho -> s1 -> s2 -> s3 -> rho; single block: s_m in place in ws
+      const c128* r = stage == 0 ? rho : ((stage - 1) & 1) ? rbuf1 : ws;
+      c128* rn = stage == 3 ? rho : (stage & 1) ? rbuf1 : ws;
+      const double hc = glf_horner_coef(dt, stage);
+      auto rk4_update = [&](size_t idx, c128 k) { rn[idx] = cadd(rho[idx], cscale(k, hc)); };
       if constexpr (HERM) {
         // Hermitian rho: L[rho] = X + X^+ with X = (-iK) r + sum_c (C_c r)(C_c^+ / 2)   (single block, nb == 1;
         // p.Cd holds C_c^+ / 2 on this path).  phase 1: Y_c = C_c r
@@ -235,9 +225,9 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
         // the conjugate.  Pass A stores the accumulator's upper elements: tile (0, 1) into T01 [TS][TS + 1] and the
         // diagonal tiles' upper triangles into Tt (packed, folded: rows u and TS - 1 - u of a tile share one run of
         // TS + 1 slots); pass B adds the conjugate of every lower element at its mirror slot.  The accumulator
-        // stays in registers through both passes (no global round trip of the diagonal tiles).  The RK4 update then
-        // reads rho and acc on the upper triangle only, keeps acc there only (the epilogue is its only reader) and
-        // writes rn and rho in full (the GEMMs, observables and the caller read them).
+        // stays in registers through both passes (no global round trip of the diagonal tiles).  The Horner update then
+        // reads rho on the upper triangle only and writes the next stage input (rho at stage 3) in full (the GEMMs,
+        // observables and the caller read it).
         {
           constexpr int TS = BT / 2, LD = TS + 1, TRI = TS * (TS + 1) / 2;
           static_assert((TS * LD + 2 * TRI) * sizeof(c128) <= sizeof(CgLds<BT>), "LDS k buffers");
@@ -283,84 +273,20 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
             gj = ts * TS + (lo ? u + v : ra + v - (TS - u));
             return &Tt[e];
           };
-          // RK4 update of one upper element (i, j) with k, writing the mirror (j, i) as the conjugate
-          auto update = [&](int gi, int gj, c128 k, c128 r0v, c128 a0v) {
+          // Horner update of one upper element (i, j) with k, writing the mirror (j, i) as the conjugate
+          auto update = [&](int gi, int gj, c128 k, c128 r0v) {
             const int id = gi * Np + gj, mid = gj * Np + gi;
-            const bool off = gi != gj;
-            if (stage == 0) {
-              acc[id] = k;
-              const c128 v = cadd(r0v, cscale(k, dt2));
-              rn[id] = v;
-              if (off) rn[mid] = cconj(v);
-            } else if (stage < 3) {
-              acc[id] = cadd(a0v, cscale(k, 2.0));
-              const c128 v = cadd(r0v, cscale(k, stage == 1 ? dt2 : dt));
-              rn[id] = v;
-              if (off) rn[mid] = cconj(v);
-            } else {
-              const c128 r1 = cadd(r0v, cscale(cscale(cadd(a0v, k), 1.0 / 6.0), dt));
-              rho[id] = r1;
-              rn[id] = r1;
-              if (off) {
-                rho[mid] = cconj(r1);
-                rn[mid] = cconj(r1);
-              }
-            }
+            const c128 v = cadd(r0v, cscale(k, hc));
+            rn[id] = v;
+            if (gi != gj) rn[mid] = cconj(v);
           };
-#if GLF_EPI_PF
-          // Software-pipelined update over both rounds (NP0 + NP1 slots per thread): the rho / acc loads of slot
-          // q + GLF_EPI_PF are issued before slot q is updated, so the chain of load round trips (one per chunk)
-          // overlaps.  Loads and stores touch disjoint elements across slots (reads: the upper triangle; each slot
-          // writes its own element and its mirror).
-          {
-            constexpr int NE0 = TS * TS, NE1 = 2 * TRI;
-            constexpr int NP0 = (NE0 + CG_WG - 1) / CG_WG, NP1 = (NE1 + CG_WG - 1) / CG_WG;
-            constexpr int NS = NP0 + NP1;
-            c128 r0[1], a0[1];
-            auto slot_ok = [&](int q, int& e) {
-              e = tid + CG_WG * (q < NP0 ? q : q - NP0);
-              return q < NP0 ? (NE0 % CG_WG == 0 || e < NE0) : (NE1 % CG_WG == 0 || e < NE1);
-            };
-            // a window of W = GLF_EPI_PF slots of loads in flight ahead of the slot being updated: a runtime loop over
-            // chunks of W slots, buffer j of the window reloaded with slot q + W right after slot q is updated
-            constexpr int W = GLF_EPI_PF;
-            (void)r0;
-            (void)a0;
-            c128 rb[W], ab[W];
-            auto issue_to = [&](int q, c128& rv, c128& av) {
-              int e;
-              if (q >= NS || !slot_ok(q, e)) return;
-              int gi, gj;
-              if (q < NP0) place_rd(std::integral_constant<int, 0>{}, e, gi, gj);
-              else place_rd(std::integral_constant<int, 1>{}, e, gi, gj);
-              rv = rho[gi * Np + gj];
-              av = stage == 0 ? cmk(0, 0) : acc[gi * Np + gj];
-            };
-#pragma unroll
-            for (int j = 0; j < W; ++j) issue_to(j, rb[j], ab[j]);
-            for (int q0 = 0; q0 < NS; q0 += W) {
-#pragma unroll
-              for (int j = 0; j < W; ++j) {
-                const int q = q0 + j;
-                int e;
-                if (q < NS && slot_ok(q, e)) {
-                  int gi, gj;
-                  const c128 k = q < NP0 ? *place_rd(std::integral_constant<int, 0>{}, e, gi, gj)
-                                         : *place_rd(std::integral_constant<int, 1>{}, e, gi, gj);
-                  update(gi, gj, k, rb[j], ab[j]);
-                }
-                issue_to(q + W, rb[j], ab[j]);
-              }
-            }
-          }
-#else
           auto round = [&](auto rdc) {
             constexpr int rd = decltype(rdc)::value;
             constexpr int NE = rd == 0 ? TS * TS : 2 * TRI;
             constexpr int NPER = (NE + CG_WG - 1) / CG_WG;
             constexpr int CH = NPER < QD_EPI_CH ? NPER : QD_EPI_CH;
             for (int q0 = 0; q0 < NPER; q0 += CH) {
-              c128 r0[CH], a0[CH];
+              c128 r0[CH];
 #pragma unroll
               for (int q = 0; q < CH; ++q) {
                 const int e = tid + CG_WG * (q0 + q);
@@ -368,7 +294,6 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
                   int gi, gj;
                   place_rd(rdc, e, gi, gj);
                   r0[q] = rho[gi * Np + gj];
-                  a0[q] = stage == 0 ? cmk(0, 0) : acc[gi * Np + gj];
                 }
               }
 #pragma unroll
@@ -377,17 +302,15 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
                 if (q0 + q >= NPER || (NE % CG_WG != 0 && e >= NE)) continue;
                 int gi, gj;
                 const c128 k = *place_rd(rdc, e, gi, gj);
-                update(gi, gj, k, r0[q], a0[q]);
+                update(gi, gj, k, r0[q]);
               }
             }
           };
           round(std::integral_constant<int, 0>{});
           round(std::integral_constant<int, 1>{});
-#endif
           __syncthreads();
         }
         QD_TMARK(3);
-        cur ^= 1;
         continue;
       } else {
       // ---- phase 1: Y_c = C_c r
@@ -431,7 +354,6 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
           QD_TMARK(3);
         }
       __syncthreads();
-      cur ^= 1;
       }
     }
     const int gs = p.step0 + step + 1;  // global step count after this step
@@ -596,11 +518,11 @@ __global__ void sandwich_prep_kernel(const c128* Lm, const c128* Rm, int N, int 
 //                                            fused RK4 epilogue of the block (same order as the
 //                                            persistent kernel's rk4_update)
 // Stage buffers: stage 0 reads rho, then scratch 0 / 1 alternate; stage 3 writes rho only, which is the
-// next step's stage-0 input.  Scratch per matrix: [buf0, buf1, acc, Y_0 .. Y_nc-1].
+// next step's stage-0 input (Horner stages, see the file header).  Scratch per matrix: [buf0, buf1, Y_0 .. Y_nc-1].
 __device__ __forceinline__ c128* split_buf(const LindbladParams& p, int b, int which) {
   const size_t NN = (size_t)p.Np * p.Np;
   if (which == 0) return p.rho + (size_t)b * NN;
-  return p.ws + (size_t)b * (3 + p.nc) * NN + (size_t)(which - 1) * NN;
+  return p.ws + (size_t)b * (2 + p.nc) * NN + (size_t)(which - 1) * NN;
 }
 
 // Split-K (small batches): the k-phase (2 + nc segments) and Y-phase K-tiles of one output block are dealt
@@ -678,7 +600,7 @@ __global__ __launch_bounds__(CG_WG) void glf_split_y_kernel(LindbladParams p) {
   const int Np = p.Np;
   const size_t NN = (size_t)Np * Np;
   const c128* r = split_buf(p, b, p.rin);
-  c128* Yc = p.ws + (size_t)b * (3 + p.nc) * NN + (size_t)(3 + c) * NN;
+  c128* Yc = p.ws + (size_t)b * (2 + p.nc) * NN + (size_t)(2 + c) * NN;
   if (threadIdx.x == 0) {
     segs[0].A = p.Cop + (size_t)c * NN + (size_t)bm * BT * Np;
     segs[0].B = r + bn * BT;
@@ -702,24 +624,10 @@ __global__ __launch_bounds__(CG_WG) void glf_split_y_kernel(LindbladParams p) {
   }
 }
 
-// RK4 epilogue of one element of the block (same order as the persistent kernel's rk4_update)
-__device__ __forceinline__ void split_rk4(const LindbladParams& p, c128* rho, c128* acc, c128* rn, size_t idx, c128 k) {
-  const int stage = p.stage;
-  const double dt = p.dt, dt2 = p.dt / 2.0;
-  const c128 r0 = rho[idx];
-  if (stage == 0) {
-    acc[idx] = k;
-    rn[idx] = cadd(r0, cscale(k, dt2));
-  } else if (stage == 1) {
-    acc[idx] = cadd(acc[idx], cscale(k, 2.0));
-    rn[idx] = cadd(r0, cscale(k, dt2));
-  } else if (stage == 2) {
-    acc[idx] = cadd(acc[idx], cscale(k, 2.0));
-    rn[idx] = cadd(r0, cscale(k, dt));
-  } else {
-    const c128 a = cadd(acc[idx], k);
-    rho[idx] = cadd(r0, cscale(cscale(a, 1.0 / 6.0), dt));
-  }
+// Horner epilogue of one element of the block (the persistent kernel's rk4_update): rn = rho + dt / (4 - stage) k,
+// rn = rho at stage 3
+__device__ __forceinline__ void split_rk4(const LindbladParams& p, c128* rho, c128* rn, size_t idx, c128 k) {
+  (p.stage == 3 ? rho : rn)[idx] = cadd(rho[idx], cscale(k, glf_horner_coef(p.dt, p.stage)));
 }
 
 template <int BT>
@@ -733,9 +641,7 @@ __global__ __launch_bounds__(CG_WG) void glf_split_k_kernel(LindbladParams p) {
   const c128* r = split_buf(p, b, p.rin);
   c128* rn = p.rout ? split_buf(p, b, p.rout) : nullptr;
   c128* rho = p.rho + (size_t)b * NN;
-  c128* ws = p.ws + (size_t)b * (3 + nc) * NN;
-  c128* acc = ws + 2 * NN;
-  const c128* Y = ws + 3 * NN;
+  const c128* Y = p.ws + (size_t)b * (2 + nc) * NN + 2 * NN;
   if (threadIdx.x == 0) {
     segs[0].A = p.mK + (size_t)bm * BT * Np;
     segs[0].B = r + bn * BT;
@@ -751,7 +657,7 @@ __global__ __launch_bounds__(CG_WG) void glf_split_k_kernel(LindbladParams p) {
   if (S == 1) {
     cg_block_gemm<BT>(segs, 2 + nc, Np, Np, Np, L, A);
     cg_epilogue<BT>(A, [&](int row, int col, c128 k) {
-      split_rk4(p, rho, acc, rn, (size_t)(bm * BT + row) * Np + bn * BT + col, k);
+      split_rk4(p, rho, rn, (size_t)(bm * BT + row) * Np + bn * BT + col, k);
     });
     return;
   }
@@ -762,7 +668,7 @@ __global__ __launch_bounds__(CG_WG) void glf_split_k_kernel(LindbladParams p) {
   for (int e = threadIdx.x; e < BT * BT; e += CG_WG) {
     c128 k = slab_ld(slab + e);
     for (int q = 1; q < S; ++q) k = cadd(k, slab_ld(slab + (size_t)q * BT * BT + e));
-    split_rk4(p, rho, acc, rn, (size_t)(bm * BT + e / BT) * Np + bn * BT + e % BT, k);
+    split_rk4(p, rho, rn, (size_t)(bm * BT + e / BT) * Np + bn * BT + e % BT, k);
   }
 }
 
@@ -772,8 +678,7 @@ __global__ __launch_bounds__(CG_WG) void glf_split_k_kernel(LindbladParams p) {
 //   X(bm, bn) with the Hermitian part C r C^+ in full (A operand Y doubled in the staging, exact), and
 //   X(bn, bm) = (P r)(bn, bm) only (C r C^+ is Hermitian, so its lower block is redundant),
 // and forms k on the upper block, k_ij = X_ij + conj(X_ji), through an LDS transpose; a diagonal block takes the
-// half-weighted X and its own transpose.  The RK4 update runs on the upper elements (rho / acc read there, acc kept
-// there only) and writes each mirror as the conjugate.  Work per stage at n_c = 1 and nb x nb blocks: nb^2 Y blocks
+// half-weighted X and its own transpose.  The Horner update runs on the upper elements (rho read there) and writes each mirror as the conjugate.  Work per stage at n_c = 1 and nb x nb blocks: nb^2 Y blocks
 // + nb(nb-1)/2 x 3 + nb x 2 X segment-blocks, against nb^2 x 4 for the general split path (nb = 4: 42 vs 64).
 template <int BT>
 struct CgSegAScaled {   // CgSegA with the segments >= 1 multiplied by `scale` as they are staged
@@ -790,23 +695,13 @@ struct CgSegAScaled {   // CgSegA with the segments >= 1 multiplied by `scale` a
   }
 };
 
-__device__ __forceinline__ void split_herm_rk4(const LindbladParams& p, c128* rho, c128* acc, c128* rn, int gi, int gj,
-                                               c128 k) {
-  const int stage = p.stage, Np = p.Np;
-  const double dt = p.dt, dt2 = p.dt / 2.0;
+__device__ __forceinline__ void split_herm_rk4(const LindbladParams& p, c128* rho, c128* rn, int gi, int gj, c128 k) {
+  const int Np = p.Np;
   const size_t id = (size_t)gi * Np + gj, mid = (size_t)gj * Np + gi;
-  const bool off = gi != gj;
-  const c128 r0 = rho[id];
-  if (stage < 3) {
-    acc[id] = stage == 0 ? k : cadd(acc[id], cscale(k, 2.0));
-    const c128 v = cadd(r0, cscale(k, stage == 2 ? dt : dt2));
-    rn[id] = v;
-    if (off) rn[mid] = cconj(v);
-  } else {
-    const c128 r1 = cadd(r0, cscale(cscale(cadd(acc[id], k), 1.0 / 6.0), dt));
-    rho[id] = r1;
-    if (off) rho[mid] = cconj(r1);
-  }
+  c128* out = p.stage == 3 ? rho : rn;
+  const c128 v = cadd(rho[id], cscale(k, glf_horner_coef(p.dt, p.stage)));
+  out[id] = v;
+  if (gi != gj) out[mid] = cconj(v);
 }
 
 template <int BT>
@@ -825,9 +720,7 @@ __global__ __launch_bounds__(CG_WG) void glf_split_hk_kernel(LindbladParams p) {
   const c128* r = split_buf(p, b, p.rin);
   c128* rn = p.rout ? split_buf(p, b, p.rout) : nullptr;
   c128* rho = p.rho + (size_t)b * NN;
-  c128* ws = p.ws + (size_t)b * (3 + nc) * NN;
-  c128* acc = ws + 2 * NN;
-  const c128* Y = ws + 3 * NN;
+  const c128* Y = p.ws + (size_t)b * (2 + nc) * NN + 2 * NN;
   const int tps = Np / CG_KT;
   if (threadIdx.x == 0) {
     segs[0].A = p.mK + (size_t)bm * BT * Np;
@@ -863,7 +756,7 @@ __global__ __launch_bounds__(CG_WG) void glf_split_hk_kernel(LindbladParams p) {
   __syncthreads();
   cg_epilogue<BT>(XU, [&](int row, int col, c128 v) {
     if (bm == bn && row > col) return;
-    split_herm_rk4(p, rho, acc, rn, bm * BT + row, bn * BT + col, cadd(v, cconj(T[col * LD + row])));
+    split_herm_rk4(p, rho, rn, bm * BT + row, bn * BT + col, cadd(v, cconj(T[col * LD + row])));
   });
 }
 
@@ -1008,7 +901,7 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
     if (const char* e = std::getenv("QD_GLF_KS")) ks = std::max(1, std::min(Tk, std::atoi(e)));  // A/B overrides
     if (const char* e = std::getenv("QD_GLF_YS")) ys = nc ? std::max(1, std::min(Ty, std::atoi(e))) : 1;
   }
-  const size_t per = (size_t)(split_bt ? 3 + nc + (ks > 1 ? ks : 0) + (ys > 1 ? nc * ys : 0)
+  const size_t per = (size_t)(split_bt ? 2 + nc + (ks > 1 ? ks : 0) + (ys > 1 ? nc * ys : 0)
                                        : glf_slots(Np, nc, herm)) * NN;
   const size_t nticket = split_bt ? (size_t)B * (1 + nc) * (Np / split_bt) * (Np / split_bt) : 0;
   const size_t st_elems = (size_t)B * per + (pad ? (size_t)B * NN : 0) + (nticket + 3) / 4;
@@ -1073,7 +966,7 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   p.ks = ks;
   p.ys = ys;
   // split-K slabs after the per-matrix scratch of all B matrices; tickets after the padded copy
-  p.kslab = split_bt ? scratch + (size_t)B * (3 + nc) * NN : nullptr;
+  p.kslab = split_bt ? scratch + (size_t)B * (2 + nc) * NN : nullptr;
   p.yslab = split_bt ? p.kslab + (size_t)B * (ks > 1 ? ks : 0) * NN : nullptr;
   p.ticket = split_bt ? (unsigned*)(scratch + (size_t)B * per + (pad ? (size_t)B * NN : 0)) : nullptr;
   if (split_bt && (ks > 1 || ys > 1)) QD_HIP(hipMemsetAsync(p.ticket, 0, nticket * sizeof(unsigned), st));
