@@ -294,7 +294,11 @@ int qd_deom_rk4_banded(qd_c128* ados, int nmax, int K, int ns,
  * slices of qd_deom_rk4's tables.  stage 0..3 (RK4 order of deom.py:725-766;
  * stage 0 reads xin = rho); fs / fc the pulse values at the stage's time.  snap
  * [nsteps+1][ns][ns] (band owning ADO 0 only, else NULL) gets rho_0 after step
- * `step` at stage 3.  ns <= 16; ns <= 8 group kernel, 9..16 MFMA tiles.
+ * `step` at stage 3.  Any ns (group kernel ns <= 8, MFMA tiles above).
+ * acc [n_own][ns][ns]: the classic RK4 accumulator (required when Hdip / Qdip
+ * drive the stage); acc = NULL selects the accumulator-free Horner form that
+ * qd_deom_rk4 runs for undriven hierarchies (stage s writes rho + dt/(4-s) L x;
+ * identical to RK4 for a generator constant over the step).
  */
 int qd_deom_stage(qd_c128* rho, const qd_c128* xin, qd_c128* xout, qd_c128* acc,
                   int n_own, int K, int ns, const int32_t* minus,

@@ -15,8 +15,9 @@
 // One launch per RK4 stage (the stage needs every ADO of the previous stage);
 // one thread per matrix element (b, n, i, j); H(t)/Q(t) are assembled in LDS
 // per workgroup from H + f_sys(t) Hdip, Q + f_coup(t) Qdip.  The fused
-// epilogue does the RK4 bookkeeping (acc, next-stage state, final update) and
-// records rho_0 (the system density matrix) after every step.
+// epilogue does the RK4 bookkeeping (deom_rk4_next: the classic acc form for
+// driven runs, the accumulator-free Horner form when the generator is constant
+// over the step) and records rho_0 (the system density matrix) after every step.
 #include "qd_common.hpp"
 
 #include <cstdlib>
@@ -52,7 +53,28 @@ struct DeomParams {
   int xsplit;  // group kernel: 0 = flat lane numbering; X in {1, 2, 4, 8} = hierarchies dealt to X block classes
   int ntst;    // group kernel: non-temporal rho / acc accesses (host: state beyond the Infinity Cache's share)
   int bchunk;  // group kernel, ADO-major: hierarchies of a class walked in chunks of bchunk (0 = all at once)
+  int horner;  // RK4 in Horner form (no pulse: the generator is constant over the step; acc unused)
 };
+
+// RK4 stage epilogue: returns the next stage input (stage < 3) or the new rho (stage 3); `acc` is the lane's RK4
+// accumulator (in: its value after the previous stage, out: after this one).
+//   classic (driven runs, H(t) / Q(t) at t, t + dt/2, t + dt): deom.py:735-766's order, ddos1 = k1; += 2 k2;
+//     += 2 k3; += k4; ddos += ddos1 dt / 6, each stage input rho + c k;
+//   Horner (no pulse): for a generator L constant over the step RK4 is exactly the degree-4 Taylor polynomial,
+//     rho' = rho + dt L(rho + dt/2 L(rho + dt/3 L(rho + dt/4 L rho))), so stage m writes rho + dt / (4 - m) L s_m
+//     and needs no accumulator (glf.hip header): one state row less read and written per stage.
+__device__ __forceinline__ c128 deom_rk4_next(int stage, bool horner, double dt, c128 r0, c128& acc, c128 d) {
+  if (horner) return cadd(r0, cscale(d, stage == 0 ? dt * 0.25 : stage == 1 ? dt / 3.0 : stage == 2 ? dt * 0.5 : dt));
+  if (stage == 0) {
+    acc = d;
+    return cadd(r0, cscale(d, dt / 2));
+  }
+  if (stage < 3) {
+    acc = cadd(acc, cscale(d, 2.0));
+    return cadd(r0, cscale(d, stage == 1 ? dt / 2 : dt));
+  }
+  return cadd(r0, cscale(cscale(cadd(acc, d), dt), 1.0 / 6.0));
+}
 
 
 __global__ __launch_bounds__(DEOM_TPB) void deom_stage_kernel(DeomParams p) {
@@ -107,25 +129,18 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_kernel(DeomParams p) {
     }
   }
 
-  // RK4 bookkeeping (deom.py:735-766 order: ddos1 = k1; ddos1 += 2 k2; += 2 k3; += k4; ddos += ddos1*dt/6)
-  const double dt = p.dt;
+  // RK4 bookkeeping (deom_rk4_next)
   const c128 r0 = p.rho[e];
-  if (p.stage == 0) {
-    p.acc[e] = d;
-    p.xout[e] = cadd(r0, cscale(d, dt / 2));
-  } else if (p.stage == 1) {
-    p.acc[e] = cadd(p.acc[e], cscale(d, 2.0));
-    p.xout[e] = cadd(r0, cscale(d, dt / 2));
-  } else if (p.stage == 2) {
-    p.acc[e] = cadd(p.acc[e], cscale(d, 2.0));
-    p.xout[e] = cadd(r0, cscale(d, dt));
+  c128 a = (p.stage > 0 && !p.horner) ? p.acc[e] : cmk(0, 0);
+  const c128 v = deom_rk4_next(p.stage, p.horner, p.dt, r0, a, d);
+  if (p.stage < 3) {
+    if (!p.horner) p.acc[e] = a;
+    p.xout[e] = v;
   } else {
-    const c128 a = cadd(p.acc[e], d);
-    const c128 r1 = cadd(r0, cscale(cscale(a, dt), 1.0 / 6.0));
-    p.rho_out[e] = r1;
+    p.rho_out[e] = v;
     if (p.snap && n == 0) {
       const size_t b = bn / p.nmax;
-      p.snap[(b * (p.nsteps + 1) + p.step + 1) * ns2 + i * ns + j] = r1;
+      p.snap[(b * (p.nsteps + 1) + p.step + 1) * ns2 + i * ns + j] = v;
     }
   }
 }
@@ -265,8 +280,9 @@ __device__ __forceinline__ void deom_stage_grp_body(const DeomParams& p) {
   const c128 own = live ? X[(size_t)n * rs + ee] : cmk(0, 0);
   const c128 dmp = UNI ? ld_uniform(p.damp + nu) : (live ? p.damp[n] : cmk(0, 0));
   const size_t idx = grp * ns2 + e;
-  const c128 r0 = valid ? ld_once(p.rho + idx, p.ntst) : cmk(0, 0);
-  const c128 a0 = (valid && p.stage > 0) ? ld_once(p.acc + idx, p.ntst) : cmk(0, 0);
+  // stage 0 of the Horner form: the stage input is rho itself (own == rho[idx] for a valid lane)
+  const c128 r0 = !valid ? cmk(0, 0) : (p.horner && p.stage == 0) ? own : ld_once(p.rho + idx, p.ntst);
+  c128 a0 = (valid && p.stage > 0 && !p.horner) ? ld_once(p.acc + idx, p.ntst) : cmk(0, 0);
   for (int q = threadIdx.x; q < ns2; q += blockDim.x)
     sH[q] = p.Hdip ? cadd(p.H[q], cmul(p.Hdip[q], p.fs)) : p.H[q];
   for (int q = threadIdx.x; q < p.nmod * ns2; q += blockDim.x)
@@ -358,21 +374,13 @@ __device__ __forceinline__ void deom_stage_grp_body(const DeomParams& p) {
   flush(mcur);
   if (!valid) return;
 
-  const double dt = p.dt;
-  if (p.stage == 0) {
-    st_once(p.acc + idx, d, p.ntst);
-    p.xout[idx] = cadd(r0, cscale(d, dt / 2));
-  } else if (p.stage == 1) {
-    st_once(p.acc + idx, cadd(a0, cscale(d, 2.0)), p.ntst);
-    p.xout[idx] = cadd(r0, cscale(d, dt / 2));
-  } else if (p.stage == 2) {
-    st_once(p.acc + idx, cadd(a0, cscale(d, 2.0)), p.ntst);
-    p.xout[idx] = cadd(r0, cscale(d, dt));
+  const c128 v = deom_rk4_next(p.stage, p.horner, p.dt, r0, a0, d);
+  if (p.stage < 3) {
+    if (!p.horner) st_once(p.acc + idx, a0, p.ntst);
+    p.xout[idx] = v;
   } else {
-    const c128 a = cadd(a0, d);
-    const c128 r1 = cadd(r0, cscale(cscale(a, dt), 1.0 / 6.0));
-    p.rho_out[idx] = r1;
-    if (p.snap && n == 0) p.snap[(hb * (p.nsteps + 1) + p.step + 1) * ns2 + e] = r1;
+    p.rho_out[idx] = v;
+    if (p.snap && n == 0) p.snap[(hb * (p.nsteps + 1) + p.step + 1) * ns2 + e] = v;
   }
 }
 
@@ -431,7 +439,7 @@ __global__ __launch_bounds__(256) void deom_stage_mfma16_kernel(DeomParams p) {
   for (int r = 0; r < 4; ++r) {
     x[r] = ld(X + (size_t)n * ns2, r);
     r0[r] = ld(p.rho + own, r);
-    a0[r] = p.stage > 0 ? ld(p.acc + own, r) : cmk(0, 0);
+    a0[r] = (p.stage > 0 && !p.horner) ? ld(p.acc + own, r) : cmk(0, 0);
   }
   const c128 dmp = p.damp[n];
   c128 SL[NM][4], SR[NM][4];
@@ -506,20 +514,14 @@ __global__ __launch_bounds__(256) void deom_stage_mfma16_kernel(DeomParams p) {
     if (!(valid && colv && i < ns)) continue;
     const c128 d = cadd(cmk(Dre[r], Dim[r]), cmul(dmp, x[r]));
     const size_t idx = own + (size_t)i * ns + col;
-    if (p.stage == 0) {
-      p.acc[idx] = d;
-      p.xout[idx] = cadd(r0[r], cscale(d, dt / 2));
-    } else if (p.stage == 1) {
-      p.acc[idx] = cadd(a0[r], cscale(d, 2.0));
-      p.xout[idx] = cadd(r0[r], cscale(d, dt / 2));
-    } else if (p.stage == 2) {
-      p.acc[idx] = cadd(a0[r], cscale(d, 2.0));
-      p.xout[idx] = cadd(r0[r], cscale(d, dt));
+    c128 a = a0[r];
+    const c128 v = deom_rk4_next(p.stage, p.horner, dt, r0[r], a, d);
+    if (p.stage < 3) {
+      if (!p.horner) p.acc[idx] = a;
+      p.xout[idx] = v;
     } else {
-      const c128 a = cadd(a0[r], d);
-      const c128 r1 = cadd(r0[r], cscale(cscale(a, dt), 1.0 / 6.0));
-      p.rho_out[idx] = r1;
-      if (p.snap && n == 0) p.snap[(hb * (p.nsteps + 1) + p.step + 1) * ns2 + (size_t)i * ns + col] = r1;
+      p.rho_out[idx] = v;
+      if (p.snap && n == 0) p.snap[(hb * (p.nsteps + 1) + p.step + 1) * ns2 + (size_t)i * ns + col] = v;
     }
   }
 }
@@ -683,22 +685,16 @@ __global__ __launch_bounds__(256) void deom_stage_tile_kernel(DeomParams p) {
     const size_t e = bbase + (size_t)n * ns2 + (size_t)i * ns + j;
     const c128 d = cadd(sacc[f], cmul(p.damp[n], xn[i * ns + j]));
     const c128 r0 = p.rho[e];
-    if (p.stage == 0) {
-      p.acc[e] = d;
-      p.xout[e] = cadd(r0, cscale(d, dt / 2));
-    } else if (p.stage == 1) {
-      p.acc[e] = cadd(p.acc[e], cscale(d, 2.0));
-      p.xout[e] = cadd(r0, cscale(d, dt / 2));
-    } else if (p.stage == 2) {
-      p.acc[e] = cadd(p.acc[e], cscale(d, 2.0));
-      p.xout[e] = cadd(r0, cscale(d, dt));
+    c128 a = (p.stage > 0 && !p.horner) ? p.acc[e] : cmk(0, 0);
+    const c128 v = deom_rk4_next(p.stage, p.horner, dt, r0, a, d);
+    if (p.stage < 3) {
+      if (!p.horner) p.acc[e] = a;
+      p.xout[e] = v;
     } else {
-      const c128 a = cadd(p.acc[e], d);
-      const c128 r1 = cadd(r0, cscale(cscale(a, dt), 1.0 / 6.0));
-      p.rho_out[e] = r1;
+      p.rho_out[e] = v;
       if (p.snap && n == 0) {
         const size_t b = bn / p.nmax;
-        p.snap[(b * (p.nsteps + 1) + p.step + 1) * ns2 + i * ns + j] = r1;
+        p.snap[(b * (p.nsteps + 1) + p.step + 1) * ns2 + i * ns + j] = v;
       }
     }
   }
@@ -786,22 +782,16 @@ __global__ __launch_bounds__(256) void deom_stage_tmfma_kernel(DeomParams p) {
     const size_t e = bbase + (size_t)n * ns2 + (size_t)i * ns + j;
     const c128 d = cadd(cmk(Dre[r], Dim[r]), cmul(dmp, xn[i * ns + j]));
     const c128 r0 = p.rho[e];
-    if (p.stage == 0) {
-      p.acc[e] = d;
-      p.xout[e] = cadd(r0, cscale(d, dt / 2));
-    } else if (p.stage == 1) {
-      p.acc[e] = cadd(p.acc[e], cscale(d, 2.0));
-      p.xout[e] = cadd(r0, cscale(d, dt / 2));
-    } else if (p.stage == 2) {
-      p.acc[e] = cadd(p.acc[e], cscale(d, 2.0));
-      p.xout[e] = cadd(r0, cscale(d, dt));
+    c128 a = (p.stage > 0 && !p.horner) ? p.acc[e] : cmk(0, 0);
+    const c128 v = deom_rk4_next(p.stage, p.horner, dt, r0, a, d);
+    if (p.stage < 3) {
+      if (!p.horner) p.acc[e] = a;
+      p.xout[e] = v;
     } else {
-      const c128 a = cadd(p.acc[e], d);
-      const c128 r1 = cadd(r0, cscale(cscale(a, dt), 1.0 / 6.0));
-      p.rho_out[e] = r1;
+      p.rho_out[e] = v;
       if (p.snap && n == 0) {
         const size_t b = bn / p.nmax;
-        p.snap[(b * (p.nsteps + 1) + p.step + 1) * ns2 + i * ns + j] = r1;
+        p.snap[(b * (p.nsteps + 1) + p.step + 1) * ns2 + i * ns + j] = v;
       }
     }
   }
@@ -980,6 +970,9 @@ int deom_run(qd_c128* ados, int B, int nmax, int K, int ns, const int32_t* minus
   p.nsteps = nsteps;
   p.dt = dt;
   p.bminor = bminor;
+  // Horner-form RK4 unless the run is driven (QD_DEOM_HORNER=0 keeps the classic form, for A/B runs)
+  const char* he = getenv("QD_DEOM_HORNER");
+  p.horner = !Hdip && !Qdip && !(he && he[0] == '0');
   static const int stage_time[4] = {0, 1, 1, 2};
   for (int s = 0; s < nsteps; ++s) {
     p.step = s;
@@ -1027,13 +1020,16 @@ extern "C" int qd_deom_rk4_ado_major(qd_c128* ados, int B, int nmax, int K, int 
 // rho / xin / xout are this band's ADOs, rows [n_own, n_loc) of xin the halo copies of the neighbours other bands
 // own; minus / plus [n_own][K] hold LOCAL row indices (-1 = absent).  Stage s reads xin (s = 0: rho), writes the
 // owned rows of xout (s < 3) and acc, and at s = 3 the owned rows of rho; snap (band owning ADO 0 only) receives
-// rho_0 after the step.  Same kernels and arithmetic as qd_deom_rk4.
+// rho_0 after the step.  Same kernels and arithmetic as qd_deom_rk4: acc = null selects the Horner-form stages
+// (what qd_deom_rk4 runs without a pulse; then stage s writes rho + dt / (4 - s) L x), a non-null acc the classic
+// RK4 bookkeeping (required for driven stages).
 extern "C" int qd_deom_stage(qd_c128* rho, const qd_c128* xin, qd_c128* xout, qd_c128* acc, int n_own, int K, int ns,
                              const int32_t* minus, const int32_t* plus, const qd_c128* coef, const qd_c128* damp,
                              const int32_t* mode, int nmod, const qd_c128* H, const qd_c128* Hdip, const qd_c128* Q,
                              const qd_c128* Qdip, double fs_re, double fs_im, double fc_re, double fc_im, int stage,
                              double dt, qd_c128* snap, int step, int nsteps, void* stream) {
-  QD_CHECK_ARG(rho && xin && acc && minus && plus && coef && damp && mode && H && Q, "qd_deom_stage: null pointer");
+  QD_CHECK_ARG(rho && xin && minus && plus && coef && damp && mode && H && Q, "qd_deom_stage: null pointer");
+  QD_CHECK_ARG(acc || (!Hdip && !Qdip), "qd_deom_stage: a driven stage needs the RK4 accumulator acc");
   QD_CHECK_ARG(stage >= 0 && stage <= 3 && (stage == 3 || xout), "qd_deom_stage: bad stage %d / null xout", stage);
   QD_CHECK_ARG(n_own >= 1 && K >= 1, "qd_deom_stage: bad sizes n_own=%d K=%d", n_own, K);
   QD_CHECK_ARG(ns >= 1 && nmod >= 1, "qd_deom_stage: ns=%d nmod=%d", ns, nmod);
@@ -1066,6 +1062,7 @@ extern "C" int qd_deom_stage(qd_c128* rho, const qd_c128* xin, qd_c128* xout, qd
   p.nsteps = nsteps;
   p.dt = dt;
   p.bminor = 0;
+  p.horner = acc == nullptr;   // no accumulator: Horner-form stages (constant generator over the step)
   return deom_launch_stage(p, (hipStream_t)stream);
 }
 
@@ -1484,22 +1481,9 @@ __global__ __launch_bounds__(TPB) void deom_band_kernel(BandParams p) {
       SR = cadd(SR, csub(cmul(cR, ym[k]), py));
     }
     flush(mcur);
-    // RK4 epilogue (deom.py:735-766 order, as the stage kernels)
-    c128 xo;
-    if (stage == 0) {
-      acc = d;
-      xo = cadd(r0, cscale(d, dt / 2));
-    } else if (stage == 1) {
-      acc = cadd(acc, cscale(d, 2.0));
-      xo = cadd(r0, cscale(d, dt / 2));
-    } else if (stage == 2) {
-      acc = cadd(acc, cscale(d, 2.0));
-      xo = cadd(r0, cscale(d, dt));
-    } else {
-      const c128 s = cadd(acc, d);
-      r0 = cadd(r0, cscale(cscale(s, dt), 1.0 / 6.0));
-      xo = r0;
-    }
+    // RK4 epilogue (deom_rk4_next, as the stage kernels: Horner form unless driven)
+    const c128 xo = deom_rk4_next(stage, !pulsed, dt, r0, acc, d);
+    if (stage == 3) r0 = xo;
     __syncthreads();   // every read of sX done
 #ifdef QD_PHASE_TIMING
     const unsigned long long t3 = wall_clock64();

@@ -108,7 +108,9 @@ class DeomBand:
         self.Qdip = c128(Qdip) if Qdip is not None else None
         z = lambda n: torch.zeros((n, ns, ns), dtype=torch.complex128, device=self.dev)
         self.bufs = {"rho": z(plan.n_loc), "x0": z(plan.n_loc), "x1": z(plan.n_loc)}
-        self.acc = z(plan.n_own)
+        # RK4 accumulator only for driven stages; undriven bands run the accumulator-free Horner form (qd_deom_stage
+        # with acc = NULL, as qd_deom_rk4 does)
+        self.acc = z(plan.n_own) if (Hdip is not None or Qdip is not None) else None
         self.snap = z(nt + 1) if lo == 0 else None
         self.send_idx = {q: i32(v) for q, v in plan.send.items()}
         self.send_buf = {q: z(len(v)) for q, v in plan.send.items()}
@@ -129,7 +131,7 @@ class DeomBand:
         p = self.plan
         with torch.cuda.device(self.dev):
             rc = _lib.load().qd_deom_stage(
-                self.bufs["rho"].data_ptr(), xin.data_ptr(), xout.data_ptr(), self.acc.data_ptr(), p.n_own, self.K,
+                self.bufs["rho"].data_ptr(), xin.data_ptr(), xout.data_ptr(), _lib.ptr(self.acc), p.n_own, self.K,
                 self.ns, self.minus.data_ptr(), self.plus.data_ptr(), self.coef.data_ptr(), self.damp.data_ptr(),
                 self.mode.data_ptr(), self.nmod, self.H.data_ptr(), _lib.ptr(self.Hdip), self.Q.data_ptr(),
                 _lib.ptr(self.Qdip), float(fs.real), float(fs.imag), float(fc.real), float(fc.imag), int(stage),

@@ -243,6 +243,13 @@ def _host_stage(band, stage, step, dt, fs, fc, xin, xout):
     d = od.band_rhs(xin.numpy(), p.n_own, p.minus, p.plus, band.coef.numpy(), band.damp.numpy(), band.mode.numpy(),
                     H, Q)
     r0 = band.bufs["rho"][:p.n_own].numpy()
+    if band.acc is None:   # undriven band: the kernel's Horner-form stages (deom_rk4_next)
+        v = torch.from_numpy(r0 + d * (dt / (4 - stage)))
+        if stage < 3:
+            xout[:p.n_own] = v
+        else:
+            band.bufs["rho"][:p.n_own] = v
+        return
     acc = band.acc.numpy()
     if stage == 0:
         acc[...] = d
