@@ -823,8 +823,17 @@ def time_reduce_one_rank(dev, reps=50):
     from pyqed_amd import _lib
     lib = _lib.load()
     uid = ctypes.create_string_buffer(128)
-    _lib.check(lib.qd_comm_unique_id(uid), "qd_comm_unique_id")
-    _lib.check(lib.qd_comm_init(1, 0, uid), "qd_comm_init")
+    # RCCL prints its version banner to stdout at communicator init: send fd 1 to stderr meanwhile, so that stdout
+    # carries only the bench's JSON line
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        _lib.check(lib.qd_comm_unique_id(uid), "qd_comm_unique_id")
+        _lib.check(lib.qd_comm_init(1, 0, uid), "qd_comm_init")
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
     try:
         x = torch.zeros(256 * 256, dtype=torch.complex128, device=dev)
         st = _lib.stream_ptr(dev)
