@@ -91,13 +91,13 @@ __device__ __forceinline__ double glf_horner_coef(double dt, int stage) {
     }                                                    \
   }
 #define QD_TIMING_DECL                                                                \
-  unsigned long long tacc[5] = {0, 0, 0, 0, 0}, tlast = p.tbuf ? wall_clock64() : 0; \
+  unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = p.tbuf ? wall_clock64() : 0; \
   const unsigned long long t0w_ = tlast, t0c_ = clock64();
 #define QD_TIMING_FLUSH                                                     \
   if (p.tbuf && threadIdx.x == 0) {                                         \
-    for (int q = 0; q < 5; ++q) p.tbuf[(size_t)b * 8 + q] += tacc[q];      \
-    p.tbuf[(size_t)b * 8 + 5] += clock64() - t0c_;                          \
-    p.tbuf[(size_t)b * 8 + 6] += wall_clock64() - t0w_;                     \
+    for (int q = 0; q < 6; ++q) p.tbuf[(size_t)b * 8 + q] += tacc[q];      \
+    p.tbuf[(size_t)b * 8 + 6] += clock64() - t0c_;                          \
+    p.tbuf[(size_t)b * 8 + 7] += wall_clock64() - t0w_;                     \
   }
 #else
 #define QD_TMARK(slot)
@@ -136,9 +136,60 @@ __device__ void wg_observables(const c128* rho, const c128* eT, int ne, size_t N
 #ifndef GLF_HERM_X
 #define GLF_HERM_X 1   // Hermitian kernel at BT = 128: X GEMM on the CgHermLayout tiles (Lindblad: no Hermitian part below the diagonal; A/B: 0)
 #endif
+#ifndef GLF_EPI_PRE
+#define GLF_EPI_PRE 0   // Hermitian epilogue: this many rho loads of round 0's first chunk issued before the LDS passes (A/B)
+#endif
 #ifndef GLF_HERM_PIPE
 #define GLF_HERM_PIPE false   // fragment double-buffering in the Hermitian kernel's GEMMs (A/B builds)
 #endif
+
+#ifndef GLF_KW
+#define GLF_KW 1   // Hermitian kernel (HSEG): k = X + X^+ passes with the wave's tile roles as compile-time constants
+#endif
+
+// Pass A (PB = false) / pass B (PB = true) of k = X + X^+ into the LDS k buffers (see the kernel) for wave W of the
+// CgHermLayout tiles.  Tile (R, C) of 16 x 16 lies in 64 x 64 quadrant (R / 4, C / 4); only the diagonal 16 x 16 tiles
+// need per-element tests, every other tile is wholly upper (pass A stores), wholly lower (pass B adds the conjugate
+// at the mirror slot) or in the lower-left quadrant (pass B into T01 transposed).  Same stores / adds as the generic
+// visitor, without its per-element index arithmetic and branches.
+template <int W, bool PB, typename Slot>
+__device__ __forceinline__ void herm_k_pass(const CgAcc<128>& A, c128* T01, c128* Tt, int lane, Slot&& slot) {
+  constexpr int TS = 64, LD = TS + 1, TRI = TS * (TS + 1) / 2;
+  const int lr = lane >> 4, lc = lane & 15;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int nj = 0; nj < 4; ++nj) {
+      const int R = mi == 0 ? (W >> 1) : 7 - (W >> 1), C = cg_herm_ctile(W, nj);   // constants after unrolling
+      const int QR = R >> 2, QC = C >> 2, rr = (R & 3) * 16, c0 = (C & 3) * 16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const c128 v = cmk(A.re[mi][nj][r], A.im[mi][nj][r]);
+        const int ra = rr + lr + 4 * r, cc = c0 + lc;
+        if (QR < QC) {
+          if (!PB) T01[ra * LD + cc] = v;
+        } else if (QR > QC) {
+          if (PB) {
+            c128* t = &T01[cc * LD + ra];
+            *t = cadd(*t, cconj(v));
+          }
+        } else if ((R & 3) < (C & 3)) {
+          if (!PB) Tt[QR * TRI + slot(ra, cc)] = v;
+        } else if ((R & 3) > (C & 3)) {
+          if (PB) {
+            c128* t = &Tt[QR * TRI + slot(cc, ra)];
+            *t = cadd(*t, cconj(v));
+          }
+        } else if (!PB) {
+          if (ra < cc) Tt[QR * TRI + slot(ra, cc)] = v;
+          else if (ra == cc) Tt[QR * TRI + slot(ra, cc)] = cadd(v, cconj(v));
+        } else if (ra > cc) {
+          c128* t = &Tt[QR * TRI + slot(cc, ra)];
+          *t = cadd(*t, cconj(v));
+        }
+      }
+    }
+}
 
 // HSEG (Hermitian kernel only): sum_c L_c r W_c is itself Hermitian (Lindblad C r C^+ / 2), so the X GEMM skips its
 // tiles below the diagonal (cg_herm_x_gemm); without it (Redfield's GLF operands) the plain X GEMM (cg_herm_x_gemm_q).
@@ -244,6 +295,31 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
             const int u = top ? ra : TS - 1 - ra;
             return u * (TS + 1) + (top ? 0 : TS - u) + (cc - ra);
           };
+          constexpr int NPER0 = (TS * TS + CG_WG - 1) / CG_WG;
+          constexpr int CH0 = NPER0 < QD_EPI_CH ? NPER0 : QD_EPI_CH;
+          constexpr int NPRE = GLF_EPI_PRE < CH0 ? GLF_EPI_PRE : CH0;   // prefetched elements per thread
+          c128 pre[NPRE ? NPRE : 1];
+          if constexpr (GLF_EPI_PRE) {   // round 0's first chunk (tile (0, 1): e -> (e / TS, TS + e % TS))
+#pragma unroll
+            for (int q = 0; q < NPRE; ++q) {
+              const int e = tid + CG_WG * q;
+              if (e < TS * TS) pre[q] = rho[(e / TS) * Np + TS + e % TS];
+            }
+          }
+          if constexpr (HX && HSEG && GLF_KW) {
+            const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = tid & 63;
+            auto pass = [&](auto pbc) {
+              constexpr bool PB = decltype(pbc)::value;
+#define QD_KW(w) \
+  case w: herm_k_pass<w, PB>(A, T01, Tt, lane, slot); break;
+              switch (wave) { QD_KW(0) QD_KW(1) QD_KW(2) QD_KW(3) QD_KW(4) QD_KW(5) QD_KW(6) default: QD_KW(7) }
+#undef QD_KW
+            };
+            pass(std::false_type{});
+            __syncthreads();
+            pass(std::true_type{});
+            __syncthreads();
+          } else {
           visit([&](int row, int col, c128 v) {
             const int ti = row / TS, tj = col / TS, ra = row - ti * TS, cc = col - tj * TS;
             if (ti < tj) T01[ra * LD + cc] = v;
@@ -257,6 +333,8 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
             if (t) *t = cadd(*t, cconj(v));
           });
           __syncthreads();
+          }
+          QD_TMARK(5);
           // round 0: tile (0, 1), element e -> (e / TS, TS + e % TS), k at T01; round 1: the two folded diagonal
           // triangles, element e -> k at Tt[e]
           auto place_rd = [&](auto rdc, int e, int& gi, int& gj) -> const c128* {
@@ -293,7 +371,8 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
                 if (q0 + q < NPER && (NE % CG_WG == 0 || e < NE)) {
                   int gi, gj;
                   place_rd(rdc, e, gi, gj);
-                  r0[q] = rho[gi * Np + gj];
+                  if (NPRE && rd == 0 && q0 == 0 && q < NPRE) r0[q] = pre[q < NPRE ? q : 0];
+                  else r0[q] = rho[gi * Np + gj];
                 }
               }
 #pragma unroll
@@ -1065,18 +1144,18 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
     int dev = 0, khz = 100000;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
-    const char* names[5] = {"gemm1", "epi1", "gemm2", "epi2", "obs/snap"};
+    const char* names[6] = {"gemm1", "epi1", "gemm2", "epi2", "obs/snap", "epi2-lds"};
     std::fprintf(stderr, "[qd phase timing] N=%d B=%d herm=%d nsteps=%d, us per step (mean over workgroups):", N, B,
                  herm, nsteps);
-    for (int q = 0; q < 5; ++q) {
+    for (int q = 0; q < 6; ++q) {
       double s = 0;
       for (int b = 0; b < B; ++b) s += (double)t[(size_t)b * 8 + q];
       std::fprintf(stderr, " %s %.2f", names[q], s / B / (khz * 1e-3) / std::max(1, nsteps));
     }
     double cyc = 0, wt = 0;
     for (int b = 0; b < B; ++b) {
-      cyc += (double)t[(size_t)b * 8 + 5];
-      wt += (double)t[(size_t)b * 8 + 6];
+      cyc += (double)t[(size_t)b * 8 + 6];
+      wt += (double)t[(size_t)b * 8 + 7];
     }
     std::fprintf(stderr, " | shader clock %.0f MHz\n", wt > 0 ? cyc / (wt / (khz * 1e3)) / 1e6 : 0.0);
   }
