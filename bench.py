@@ -973,6 +973,9 @@ def main():
     ap.add_argument("--no-deom", action="store_true")
     ap.add_argument("--no-deom-banded", action="store_true", help="skip the tier-banded DEOM leg")
     ap.add_argument("--no-redfield", action="store_true")
+    ap.add_argument("--no-reduce", action="store_true",
+                    help="skip the one-rank RCCL reduce timing of the 2DES projection (its communicator init crashes "
+                         "under rocprofv3 --pmc)")
     ap.add_argument("--no-superop", action="store_true")
     args = ap.parse_args()
 
@@ -1068,6 +1071,8 @@ def main():
                 "event_ms_per_grid": shard["event_ms_per_grid"], "roofline": shard["roofline"],
                 "projected_8gpu_speedup_compute_only": round(twodes["ms_per_grid"] / shard["ms_per_grid"], 3)}
             try:
+                if args.no_reduce:
+                    raise RuntimeError("skipped (--no-reduce)")
                 red = time_reduce_one_rank(dev)
                 sh8 = twodes["shard_1of8"]
                 sh8["reduce_1mib_one_rank_ms"] = round(red, 4)

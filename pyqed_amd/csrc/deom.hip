@@ -64,7 +64,7 @@ struct DeomParams {
 //     rho' = rho + dt L(rho + dt/2 L(rho + dt/3 L(rho + dt/4 L rho))), so stage m writes rho + dt / (4 - m) L s_m
 //     and needs no accumulator (glf.hip header): one state row less read and written per stage.
 __device__ __forceinline__ c128 deom_rk4_next(int stage, bool horner, double dt, c128 r0, c128& acc, c128 d) {
-  if (horner) return cadd(r0, cscale(d, stage == 0 ? dt * 0.25 : stage == 1 ? dt / 3.0 : stage == 2 ? dt * 0.5 : dt));
+  if (horner) return cadd(r0, cscale(d, rk4_horner_coef(dt, stage)));
   if (stage == 0) {
     acc = d;
     return cadd(r0, cscale(d, dt / 2));

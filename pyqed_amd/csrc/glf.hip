@@ -75,9 +75,7 @@ __host__ __device__ inline int glf_slots(int Np, int nc, int herm) {
 }
 
 // Horner coefficient of RK4 stage m (0..3): s_{m+1} = rho + dt / (4 - m) L s_m  (see the file header)
-__device__ __forceinline__ double glf_horner_coef(double dt, int stage) {
-  return stage == 0 ? dt * 0.25 : stage == 1 ? dt / 3.0 : stage == 2 ? dt * 0.5 : dt;
-}
+__device__ __forceinline__ double glf_horner_coef(double dt, int stage) { return rk4_horner_coef(dt, stage); }
 
 #ifdef QD_PHASE_TIMING
 // Diagnostics only (p.tbuf != null): barrier, then thread 0 charges the ticks since the last mark to `slot`.

@@ -109,6 +109,15 @@ __device__ __forceinline__ c128 slab_sum(c128 v, int s0, int S, F&& at) {
   return v;
 }
 
+// RK4 in Horner form for a linear generator L that is constant over the step (every propagator here except the
+// driven DEOM stages): classical RK4 is then exactly the degree-4 Taylor polynomial
+//   rho' = rho + dt L(rho + dt/2 L(rho + dt/3 L(rho + dt/4 L rho))),
+// so stage m (0..3) reads s_m (s_0 = rho) and writes s_{m+1} = rho + c_m L s_m with c_m = dt / (4 - m), s_4 = rho'.
+// No accumulator is read or written (phys.rk4, phys.py:1051-1064, up to rounding).
+__device__ __forceinline__ double rk4_horner_coef(double dt, int stage) {
+  return stage == 0 ? dt * 0.25 : stage == 1 ? dt / 3.0 : stage == 2 ? dt * 0.5 : dt;
+}
+
 inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
 // Split-K complex fp64 MFMA GEMM (response.hip): slabs[s] = A [Mp][Kp] x B [Kp][Np] over K slice s, S <= max_S

@@ -80,19 +80,8 @@ __global__ __launch_bounds__(SO_TPB) void superop_rows_kernel(const c128* __rest
     if (row < N2) {
       const c128 k = cmk(kr, ki);
       const long idx = (long)b * vstride + row;
-      const c128 rv = v[idx];
-      if (stage == 0) {
-        acc[idx] = k;
-        xout[idx] = cadd(rv, cscale(k, dt / 2.0));
-      } else if (stage == 1) {
-        acc[idx] = cadd(acc[idx], cscale(k, 2.0));
-        xout[idx] = cadd(rv, cscale(k, dt / 2.0));
-      } else if (stage == 2) {
-        acc[idx] = cadd(acc[idx], cscale(k, 2.0));
-        xout[idx] = cadd(rv, cscale(k, dt));
-      } else {
-        v[idx] = cadd(rv, cscale(cscale(cadd(acc[idx], k), 1.0 / 6.0), dt));
-      }
+      // Horner-form RK4 (rk4_horner_coef): L is constant over the step; no accumulator
+      (stage == 3 ? v : xout)[idx] = cadd(v[idx], cscale(k, rk4_horner_coef(dt, stage)));
     }
   }
 }
@@ -118,25 +107,14 @@ __global__ void superop_pad_l_kernel(const c128* L, int N2, int N2p, c128* Lp) {
   }
 }
 
-// k = sum_s slabs[s] (fixed order: deterministic), then the RK4 update of every element (phys.rk4 order)
+// k = sum_s slabs[s] (fixed order: deterministic), then the Horner-form RK4 update of every element (rk4_horner_coef)
 __global__ void superop_gemm_rk4_kernel(const c128* slabs, int S, size_t tot, c128* X, c128* x0, c128* x1, c128* acc,
                                         double dt, int stage) {
   for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
     c128 k = slabs[e];
     k = slab_sum(k, 1, S, [&](int q) { return slabs[(size_t)q * tot + e]; });
-    const c128 p = X[e];
-    if (stage == 0) {
-      acc[e] = k;
-      x0[e] = cadd(p, cscale(k, dt / 2.0));
-    } else if (stage == 1) {
-      acc[e] = cadd(acc[e], cscale(k, 2.0));
-      x1[e] = cadd(p, cscale(k, dt / 2.0));
-    } else if (stage == 2) {
-      acc[e] = cadd(acc[e], cscale(k, 2.0));
-      x0[e] = cadd(p, cscale(k, dt));
-    } else {
-      X[e] = cadd(p, cscale(cscale(cadd(acc[e], k), 1.0 / 6.0), dt));
-    }
+    // Horner-form RK4: stage 0 -> x0, 1 -> x1, 2 -> x0, 3 -> X
+    (stage == 3 ? X : (stage & 1) ? x1 : x0)[e] = cadd(X[e], cscale(k, rk4_horner_coef(dt, stage)));
   }
 }
 

@@ -105,7 +105,6 @@ __global__ __launch_bounds__(TD_TPB) void tdse_rk4_kernel(const c128* mHT, c128*
   __syncthreads();
   c128* ob = obs ? obs + (size_t)b * (nsave + 1) * ne : nullptr;
   if (ob && save0 == 0) td_expect(psi, ET, ne, N, ob, red);
-  const double dt2 = dt / 2.0;
   for (int s = 0; s < nsteps; ++s) {
     for (int stage = 0; stage < 4; ++stage) {
       // k = (-iH) xs ; each thread owns rows r
@@ -124,21 +123,10 @@ __global__ __launch_bounds__(TD_TPB) void tdse_rk4_kernel(const c128* mHT, c128*
       for (int q = 0; q < QMAX; ++q) {
         const int r = threadIdx.x + q * TD_TPB;
         if (r >= N) break;
-        const c128 k = kreg[q];
-        if (stage == 0) {
-          acc[r] = k;
-          xs[r] = cadd(psi[r], cscale(k, dt2));
-        } else if (stage == 1) {
-          acc[r] = cadd(acc[r], cscale(k, 2.0));
-          xs[r] = cadd(psi[r], cscale(k, dt2));
-        } else if (stage == 2) {
-          acc[r] = cadd(acc[r], cscale(k, 2.0));
-          xs[r] = cadd(psi[r], cscale(k, dt));
-        } else {
-          const c128 a = cadd(acc[r], k);
-          psi[r] = cadd(psi[r], cscale(cscale(a, 1.0 / 6.0), dt));
-          xs[r] = psi[r];
-        }
+        // Horner-form RK4 (rk4_horner_coef): H is constant over the step
+        const c128 v = cadd(psi[r], cscale(kreg[q], rk4_horner_coef(dt, stage)));
+        if (stage == 3) psi[r] = v;
+        xs[r] = v;
       }
       __syncthreads();
     }
@@ -215,30 +203,15 @@ __global__ __launch_bounds__(256) void tdse_row_stage_kernel(const c128* H, c128
     }
   }
   if (lane != 0) return;
-  const double dt2 = dt / 2.0;
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
     if (q >= nb) break;
     const size_t b = b0 + q;
     c128* psi = psi_g + b * N;
     c128* x0 = ws + b * 3 * N;
-    c128* acc = x0 + 2 * N;
-    c128* xout = (stage & 1) ? x0 + N : x0;   // stage 0: x0, stage 1: x1, stage 2: x0
+    c128* xout = stage == 3 ? psi : (stage & 1) ? x0 + N : x0;   // stage 0: x0, 1: x1, 2: x0, 3: psi
     const c128 k = cmulmi(cmk(sr[q], si[q]));
-    const c128 p = psi[r];
-    if (stage == 0) {
-      acc[r] = k;
-      xout[r] = cadd(p, cscale(k, dt2));
-    } else if (stage == 1) {
-      acc[r] = cadd(acc[r], cscale(k, 2.0));
-      xout[r] = cadd(p, cscale(k, dt2));
-    } else if (stage == 2) {
-      acc[r] = cadd(acc[r], cscale(k, 2.0));
-      xout[r] = cadd(p, cscale(k, dt));
-    } else {
-      const c128 a = cadd(acc[r], k);
-      psi[r] = cadd(p, cscale(cscale(a, 1.0 / 6.0), dt));
-    }
+    xout[r] = cadd(psi[r], cscale(k, rk4_horner_coef(dt, stage)));   // Horner-form RK4
   }
 }
 
@@ -302,27 +275,16 @@ __global__ void tdse_pad_psi_kernel(c128* psi, int B, int N, int Bp, int Np, c12
   }
 }
 
-// k = sum_s slabs[s] (fixed order), then the RK4 update of every padded element
+// k = sum_s slabs[s] (fixed order), then the (Horner-form) RK4 update of every padded element
 __global__ void tdse_gemm_rk4_kernel(const c128* slabs, int S, size_t tot, c128* P, c128* x0, c128* x1, c128* acc,
                                      double dt, int stage) {
-  const double dt2 = dt / 2.0;
+  (void)acc;   // Horner-form RK4: no accumulator
+  c128* out = stage == 3 ? P : (stage & 1) ? x1 : x0;   // stage 0: x0, 1: x1, 2: x0, 3: P
+  const double hc = rk4_horner_coef(dt, stage);
   for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
     c128 k = slabs[e];
     k = slab_sum(k, 1, S, [&](int q) { return slabs[(size_t)q * tot + e]; });
-    const c128 p = P[e];
-    if (stage == 0) {
-      acc[e] = k;
-      x0[e] = cadd(p, cscale(k, dt2));
-    } else if (stage == 1) {
-      acc[e] = cadd(acc[e], cscale(k, 2.0));
-      x1[e] = cadd(p, cscale(k, dt2));
-    } else if (stage == 2) {
-      acc[e] = cadd(acc[e], cscale(k, 2.0));
-      x0[e] = cadd(p, cscale(k, dt));
-    } else {
-      const c128 a = cadd(acc[e], k);
-      P[e] = cadd(p, cscale(cscale(a, 1.0 / 6.0), dt));
-    }
+    out[e] = cadd(P[e], cscale(k, hc));
   }
 }
 
