@@ -770,8 +770,8 @@ def bench_deom(dev, steps, batch):
     rate5_stage = _deom_event_rate(dev, sol5, bath5, sz + sx, sx[None], 1, steps, dt=0.001, banded=False)
     bt, bt5 = sol.band_tables(dev), sol5.band_tables(dev)
     single = rate[1]
-    # per RK4 step ~4.75 MB of ADO traffic per hierarchy = 768 B per ADO-step
-    # (4 stages x (read stage input, rho, acc + write next input, acc) of 64-B ADO rows)
+    # per RK4 step ~4.75 MB of ADO traffic per hierarchy = 768 B per ADO-step (the survey's figure,
+    # kept as the denominator; the Horner-form stages move 11 rows of 64 B = 704 B per ADO-step)
     bytes_per_step = 4.75e6
     bytes_per_ado_step = 768.0
     ado_b = rate[batch] * nmax * batch
@@ -784,11 +784,11 @@ def bench_deom(dev, steps, batch):
         "run_steps_per_s_end_to_end": round(steps / wall_run, 1),
         "batched": {"hierarchies": batch, "ado_steps_per_s": round(ado_b, 1), "steps_per_s": round(rate[batch], 1),
                     "layout": "ADO-major [nmax][B][2][2], hierarchies dealt to the 8 XCD block classes",
-                    "roofline": {"bound": "hbm", "kernel": "deom_stage_grp_kernel<4,6,true>",
+                    "roofline": {"bound": "hbm", "kernel": "deom_stage_grp_kernel<4,5,true>",
                                  "achieved": round(ado_b * bytes_per_ado_step / 1e9, 1), "peak": HBM_PEAK_GBS,
                                  "unit": "GB/s", "frac": round(ado_b * bytes_per_ado_step / 1e9 / HBM_PEAK_GBS, 4),
                                  "bytes_per_ado_step": bytes_per_ado_step,
-                                 "traffic": measured_traffic("deom_stage_grp_kernel<4,6,true>_64h", nmax * batch / 4)
+                                 "traffic": measured_traffic("deom_stage_grp_kernel<4,5,true>_64h", nmax * batch / 4)
                                  if batch == 64 else None,
                                  "traffic_unit": "HBM bytes per stage launch (PMC FETCH_SIZE+WRITE_SIZE, calibrated; "
                                                  "profiles/pmc_traffic.json)"}},
