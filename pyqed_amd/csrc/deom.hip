@@ -64,7 +64,10 @@ struct DeomParams {
 //     rho' = rho + dt L(rho + dt/2 L(rho + dt/3 L(rho + dt/4 L rho))), so stage m writes rho + dt / (4 - m) L s_m
 //     and needs no accumulator (glf.hip header): one state row less read and written per stage.
 __device__ __forceinline__ c128 deom_rk4_next(int stage, bool horner, double dt, c128 r0, c128& acc, c128 d) {
-  if (horner) return cadd(r0, cscale(d, rk4_horner_coef(dt, stage)));
+  if (horner) {   // explicit fma: the same rounding in every kernel whatever the compiler contracts around it
+    const double c = rk4_horner_coef(dt, stage);
+    return cmk(__builtin_fma(d.re, c, r0.re), __builtin_fma(d.im, c, r0.im));
+  }
   if (stage == 0) {
     acc = d;
     return cadd(r0, cscale(d, dt / 2));
@@ -185,8 +188,11 @@ __device__ __forceinline__ T ld_uniform(const T* q) {
 // UNI: every wave holds lanes of ONE ADO (ADO-major layout, B / xsplit a multiple of 64 / G), so the ADO's
 // neighbour indices, prefactors and damping are wave-uniform scalar loads instead of per-group vector loads
 // broadcast by DPP moves.
-template <int G, int KMAX, bool NS2, bool UNI = false>
+// HM: 1 = Horner-form stages fixed at compile time (no accumulator registers or code; the undriven ns = 2 launches),
+// 0 = p.horner at run time.
+template <int G, int KMAX, bool NS2, bool UNI = false, int HM = 0>
 __device__ __forceinline__ void deom_stage_grp_body(const DeomParams& p) {
+  const bool horner = HM ? true : (bool)p.horner;
   extern __shared__ c128 deom_lds[];
   c128* sH = deom_lds;
   c128* sQ = deom_lds + p.ns * p.ns;
@@ -281,8 +287,8 @@ __device__ __forceinline__ void deom_stage_grp_body(const DeomParams& p) {
   const c128 dmp = UNI ? ld_uniform(p.damp + nu) : (live ? p.damp[n] : cmk(0, 0));
   const size_t idx = grp * ns2 + e;
   // stage 0 of the Horner form: the stage input is rho itself (own == rho[idx] for a valid lane)
-  const c128 r0 = !valid ? cmk(0, 0) : (p.horner && p.stage == 0) ? own : ld_once(p.rho + idx, p.ntst);
-  c128 a0 = (valid && p.stage > 0 && !p.horner) ? ld_once(p.acc + idx, p.ntst) : cmk(0, 0);
+  const c128 r0 = !valid ? cmk(0, 0) : (horner && p.stage == 0) ? own : ld_once(p.rho + idx, p.ntst);
+  c128 a0 = (valid && p.stage > 0 && !horner) ? ld_once(p.acc + idx, p.ntst) : cmk(0, 0);
   for (int q = threadIdx.x; q < ns2; q += blockDim.x)
     sH[q] = p.Hdip ? cadd(p.H[q], cmul(p.Hdip[q], p.fs)) : p.H[q];
   for (int q = threadIdx.x; q < p.nmod * ns2; q += blockDim.x)
@@ -374,9 +380,9 @@ __device__ __forceinline__ void deom_stage_grp_body(const DeomParams& p) {
   flush(mcur);
   if (!valid) return;
 
-  const c128 v = deom_rk4_next(p.stage, p.horner, p.dt, r0, a0, d);
+  const c128 v = deom_rk4_next(p.stage, horner, p.dt, r0, a0, d);
   if (p.stage < 3) {
-    if (!p.horner) st_once(p.acc + idx, a0, p.ntst);
+    if (!horner) st_once(p.acc + idx, a0, p.ntst);
     p.xout[idx] = v;
   } else {
     p.rho_out[idx] = v;
@@ -384,9 +390,16 @@ __device__ __forceinline__ void deom_stage_grp_body(const DeomParams& p) {
   }
 }
 
-template <int G, int KMAX, bool NS2, bool UNI = false>
-__global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) {
-  deom_stage_grp_body<G, KMAX, NS2, UNI>(p);
+#ifndef DEOM_HM_WAVES
+#define DEOM_HM_WAVES 0   // waves-per-SIMD floor of the compile-time Horner ns = 2 kernels (0: none; A/B)
+#endif
+template <int G, int KMAX, bool NS2, bool UNI = false, int HM = 0>
+__global__ __launch_bounds__(DEOM_TPB)
+#if DEOM_HM_WAVES
+__attribute__((amdgpu_waves_per_eu(HM ? DEOM_HM_WAVES : 1)))
+#endif
+void deom_stage_grp_kernel(DeomParams p) {
+  deom_stage_grp_body<G, KMAX, NS2, UNI, HM>(p);
 }
 
 // MFMA tile kernel for 9 <= ns <= 16 (zero-padded to 16 in registers), NM <= 2 bath modes, K <= 21: one wave per
@@ -891,21 +904,27 @@ int deom_launch_stage(const DeomParams& p, hipStream_t st) {
       hipLaunchKernelGGL(deom_stage_kernel, dim3(grid), dim3(tpb), 0, st, q);
       return;
     }
+    auto launch_g4 = [&](auto hmc) {
+      constexpr int HM = decltype(hmc)::value;
+      if (uni) {
+        if (K <= 4) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 4, true, true, HM>), dim3(grid), dim3(tpb), lds, st, q);
+        else if (K == 5) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 5, true, true, HM>), dim3(grid), dim3(tpb), lds, st, q);
+        else if (K <= 6) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 6, true, true, HM>), dim3(grid), dim3(tpb), lds, st, q);
+        else hipLaunchKernelGGL((deom_stage_grp_kernel<4, 8, true, true, HM>), dim3(grid), dim3(tpb), lds, st, q);
+      } else {
+        if (K <= 4) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 4, true, false, HM>), dim3(grid), dim3(tpb), lds, st, q);
+        else if (K == 5) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 5, true, false, HM>), dim3(grid), dim3(tpb), lds, st, q);
+        else if (K <= 6) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 6, true, false, HM>), dim3(grid), dim3(tpb), lds, st, q);
+        else hipLaunchKernelGGL((deom_stage_grp_kernel<4, 8, true, false, HM>), dim3(grid), dim3(tpb), lds, st, q);
+      }
+    };
     switch (G) {
       case 1: hipLaunchKernelGGL((deom_stage_grp_kernel<1, 8, false>), dim3(grid), dim3(tpb), lds, st, q); break;
       case 4:  // ns = 2; registers sized to K (ym/yp/indices scale with KMAX); K = 5 (the bench bath, Pade npsd = 4):
-               // 104 instead of 116 VGPRs, same speed (profiles/r02/deom/kmax5_ab.txt)
-        if (uni) {
-          if (K <= 4) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 4, true, true>), dim3(grid), dim3(tpb), lds, st, q);
-          else if (K == 5) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 5, true, true>), dim3(grid), dim3(tpb), lds, st, q);
-          else if (K <= 6) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 6, true, true>), dim3(grid), dim3(tpb), lds, st, q);
-          else hipLaunchKernelGGL((deom_stage_grp_kernel<4, 8, true, true>), dim3(grid), dim3(tpb), lds, st, q);
-        } else {
-          if (K <= 4) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 4, true>), dim3(grid), dim3(tpb), lds, st, q);
-          else if (K == 5) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 5, true>), dim3(grid), dim3(tpb), lds, st, q);
-          else if (K <= 6) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 6, true>), dim3(grid), dim3(tpb), lds, st, q);
-          else hipLaunchKernelGGL((deom_stage_grp_kernel<4, 8, true>), dim3(grid), dim3(tpb), lds, st, q);
-        }
+               // 104 instead of 116 VGPRs, same speed (profiles/r02/deom/kmax5_ab.txt); undriven runs take the
+               // compile-time Horner instantiations (HM = 1)
+        if (q.horner) launch_g4(std::integral_constant<int, 1>{});
+        else launch_g4(std::integral_constant<int, 0>{});
         break;
       case 16: hipLaunchKernelGGL((deom_stage_grp_kernel<16, 8, false>), dim3(grid), dim3(tpb), lds, st, q); break;
       case 32: hipLaunchKernelGGL((deom_stage_grp_kernel<32, 8, false>), dim3(grid), dim3(tpb), lds, st, q); break;
