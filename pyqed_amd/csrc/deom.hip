@@ -1201,6 +1201,9 @@ struct BandParams {
 };
 
 constexpr int BAND_HM = 8;   // halo elements per thread held as precomputed offsets (one batched load per stage)
+#ifndef DEOM_BAND_EARLY
+#define DEOM_BAND_EARLY 1   // undriven runs: the next stage's damping + coherent part computed before the poll (A/B: 0)
+#endif
 typedef unsigned int band_u4 __attribute__((ext_vector_type(4)));
 
 // 16-B write-through (sc1) buffer load / store of one complex element at byte offset `off`
@@ -1344,6 +1347,39 @@ __global__ __launch_bounds__(TPB) void deom_band_kernel(BandParams p) {
       for (int l = 0; l < ns; ++l) f(l);
     }
   };
+  // H(t) / Q(t) entries this lane multiplies: H[i][l], H[l][j] (FAST: the two of each; read once for the run when
+  // undriven, per stage when driven)
+  c128 hil[2], hlj[2], qil[2], qlj[2];
+  auto read_hq = [&]() {
+    if constexpr (FAST) {
+#pragma unroll
+      for (int l = 0; l < 2; ++l) {
+        hil[l] = sH[i * 2 + l];
+        hlj[l] = sH[l * 2 + j];
+        qil[l] = sQ[i * 2 + l];
+        qlj[l] = sQ[l * 2 + j];
+      }
+    }
+  };
+  // damping + coherent part of the stencil, damp_n x - i[H, x], from the lane group's own elements only
+  auto dlocal = [&](c128 own) -> c128 {
+    c128 d = cmul(dmp, own);
+    c128 comm = cmk(0, 0);
+    for_l([&](int l) {
+      if constexpr (FAST)
+        comm = cadd(comm, csub(cmul(hil[l], colv(own, l)), cmul(rowv(own, l), hlj[l])));
+      else
+        comm = cadd(comm, csub(cmul(sH[i * ns + l], colv(own, l)), cmul(rowv(own, l), sH[l * ns + j])));
+    });
+    return cadd(d, cmulmi(comm));
+  };
+  // Undriven runs (H fixed): that part of stage g + 1 depends on the lane group's own rows only, so it is evaluated
+  // right after stage g is published, while the source bands publish theirs (the same operations in the same
+  // order: bit-identical to the stage launches)
+  const bool early = DEOM_BAND_EARLY && !pulsed;
+  __syncthreads();   // sH / sQ and the band's rows written above
+  if (!pulsed) read_hq();
+  c128 dpre = early ? dlocal(sX[oown]) : cmk(0, 0);
   static constexpr int stage_time[4] = {0, 1, 1, 2};
   const double dt = p.dt;
   const size_t slab = (size_t)p.nmax * ns2;
@@ -1443,26 +1479,8 @@ __global__ __launch_bounds__(TPB) void deom_band_kernel(BandParams p) {
       ym[k] = sX[om[k]];
       yp[k] = sX[op[k]];
     }
-    // H(t) / Q(t) entries this lane multiplies: H[i][l], H[l][j] (FAST: the two of each, read once per stage)
-    c128 hil[2], hlj[2], qil[2], qlj[2];
-    if constexpr (FAST) {
-#pragma unroll
-      for (int l = 0; l < 2; ++l) {
-        hil[l] = sH[i * 2 + l];
-        hlj[l] = sH[l * 2 + j];
-        qil[l] = sQ[i * 2 + l];
-        qlj[l] = sQ[l * 2 + j];
-      }
-    }
-    c128 d = cmul(dmp, own);
-    c128 comm = cmk(0, 0);
-    for_l([&](int l) {
-      if constexpr (FAST)
-        comm = cadd(comm, csub(cmul(hil[l], colv(own, l)), cmul(rowv(own, l), hlj[l])));
-      else
-        comm = cadd(comm, csub(cmul(sH[i * ns + l], colv(own, l)), cmul(rowv(own, l), sH[l * ns + j])));
-    });
-    d = cadd(d, cmulmi(comm));
+    if (pulsed) read_hq();
+    c128 d = early ? dpre : dlocal(own);
     c128 SL = cmk(0, 0), SR = cmk(0, 0);
     auto flush = [&](int m) {
       const c128* Qm = sQ + m * ns2;
@@ -1518,6 +1536,7 @@ __global__ __launch_bounds__(TPB) void deom_band_kernel(BandParams p) {
     if (tid == 0)
       __hip_atomic_store(p.flags + (size_t)w * BAND_FLAG_STRIDE, (unsigned)(g + 1), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
+    if (early) dpre = dlocal(xo);   // next stage's own element is xo (a padding lane's is never read)
 #ifdef QD_PHASE_TIMING
     const unsigned long long t4 = wall_clock64();
     tph[0] += t1 - t0;
