@@ -137,6 +137,26 @@ __device__ void wg_observables(const c128* rho, const c128* eT, int ne, size_t N
 #ifndef GLF_EPI_PRE
 #define GLF_EPI_PRE 0   // Hermitian epilogue: this many rho loads of round 0's first chunk issued before the LDS passes (A/B)
 #endif
+#ifndef GLF_SPLIT_DEPTH
+#define GLF_SPLIT_DEPTH 2   // split-path GEMMs: K-tiles of global loads in flight ahead of the MFMAs (1 or 2)
+#endif
+// the split-path GEMM engine: tile loads one (cg_block_gemm_gen) or two (cg_block_gemm_gen2) K-tiles ahead; same
+// MFMA order, bit-identical results
+// (measured and rejected: 32-blocks with the even / odd K-tiles on the two wave halves of a single-buffered K-tile
+// pair, all eight waves issuing MFMAs: 64 matrices 204k vs 218-223k DM-steps/s, profiles/r03/lindblad/split_halves_ab.txt)
+template <int BT, typename APol, typename BPol>
+__device__ __forceinline__ void split_gemm(int T, APol& pa, BPol& pb, CgLds<BT>& L, CgAcc<BT>& acc) {
+  if constexpr (GLF_SPLIT_DEPTH >= 2) cg_block_gemm_gen2<BT>(T, pa, pb, L, acc);
+  else cg_block_gemm_gen<BT>(T, pa, pb, L, acc);
+}
+template <int BT>
+__device__ __forceinline__ void split_block_gemm(const CgSeg* segs, int nseg, int K, int lda, int ldb, CgLds<BT>& L,
+                                                 CgAcc<BT>& acc) {
+  const int tps = K / CG_KT;
+  CgSegA<BT> pa{segs, tps, lda};
+  CgSegB<BT> pb{segs, tps, ldb};
+  split_gemm<BT>(nseg * tps, pa, pb, L, acc);
+}
 #ifndef GLF_HERM_PIPE
 #define GLF_HERM_PIPE false   // fragment double-buffering in the Hermitian kernel's GEMMs (A/B builds)
 #endif
@@ -649,7 +669,7 @@ __device__ __forceinline__ void split_gemm_range(const CgSeg* segs, int tps, int
   const int t0 = (int)((long)T * s / S), t1 = (int)((long)T * (s + 1) / S);
   CgOffset<CgSegA<BT>> pa{CgSegA<BT>{segs, tps, ld}, t0};
   CgOffset<CgSegB<BT>> pb{CgSegB<BT>{segs, tps, ld}, t0};
-  cg_block_gemm_gen<BT>(t1 - t0, pa, pb, L, A);
+  split_gemm<BT>(t1 - t0, pa, pb, L, A);
 }
 
 // Publish this workgroup's partial block and return true in the last arriver (all threads agree).
@@ -686,7 +706,7 @@ __global__ __launch_bounds__(CG_WG) void glf_split_y_kernel(LindbladParams p) {
   CgAcc<BT> A;
   auto store = [&](int row, int col, c128 v) { Yc[(size_t)(bm * BT + row) * Np + bn * BT + col] = v; };
   if (S == 1) {
-    cg_block_gemm<BT>(segs, 1, Np, Np, Np, L, A);
+    split_block_gemm<BT>(segs, 1, Np, Np, Np, L, A);
     cg_epilogue<BT>(A, store);
     return;
   }
@@ -732,7 +752,7 @@ __global__ __launch_bounds__(CG_WG) void glf_split_k_kernel(LindbladParams p) {
   __syncthreads();
   CgAcc<BT> A;
   if (S == 1) {
-    cg_block_gemm<BT>(segs, 2 + nc, Np, Np, Np, L, A);
+    split_block_gemm<BT>(segs, 2 + nc, Np, Np, Np, L, A);
     cg_epilogue<BT>(A, [&](int row, int col, c128 k) {
       split_rk4(p, rho, rn, (size_t)(bm * BT + row) * Np + bn * BT + col, k);
     });
@@ -812,7 +832,7 @@ __global__ __launch_bounds__(CG_WG) void glf_split_hk_kernel(LindbladParams p) {
   {
     CgSegAScaled<BT> pa{segs, tps, Np, bm < bn ? 2.0 : 1.0};
     CgSegB<BT> pb{segs, tps, Np};
-    cg_block_gemm_gen<BT>((1 + nc) * tps, pa, pb, L, XU);
+    split_gemm<BT>((1 + nc) * tps, pa, pb, L, XU);
   }
   if (bm < bn) {
     if (threadIdx.x == 0) {
@@ -822,7 +842,7 @@ __global__ __launch_bounds__(CG_WG) void glf_split_hk_kernel(LindbladParams p) {
     __syncthreads();
     CgSegA<BT> pa{segs, tps, Np};
     CgSegB<BT> pb{segs, tps, Np};
-    cg_block_gemm_gen<BT>(tps, pa, pb, L, XL);
+    split_gemm<BT>(tps, pa, pb, L, XL);
   }
   constexpr int LD = BT + 1;
   static_assert(BT * LD * sizeof(c128) <= sizeof(CgLds<BT>), "LDS transpose buffer");
