@@ -857,6 +857,93 @@ __global__ __launch_bounds__(CG_WG) void glf_split_hk_kernel(LindbladParams p) {
   });
 }
 
+// The same stage with each off-diagonal pair's two GEMMs on two workgroups (glf_split_hk2_kernel, grid x = pairs +
+// off-diagonal pairs): the pair's workgroup computes XU (16 K-tiles at N_p = 128, n_c = 1), an extra workgroup XL
+// (8 K-tiles), so the longest workgroup no longer runs all 24.  Both publish their block to a slab (write-through)
+// and take the pair's arrival ticket (split_arrive, the split-K hand-off); the last arriver forms k from its own
+// accumulator and the other's slab and runs the update.  The same GEMMs and sums as glf_split_hk_kernel: bit-identical.
+template <int BT>
+__global__ __launch_bounds__(CG_WG) void glf_split_hk2_kernel(LindbladParams p) {
+  __shared__ CgLds<BT> L;
+  __shared__ CgSeg segs[1 + MAX_NC];
+  const int nb = p.Np / BT, npairs = nb * (nb + 1) / 2, noff = nb * (nb - 1) / 2;
+  const bool xl_role = (int)blockIdx.x >= npairs;
+  int bm = 0, bn, oj = -1;   // (bm, bn) block pair; oj = its index among the off-diagonal pairs (row-major)
+  if (!xl_role) {
+    int pi = blockIdx.x;
+    while (pi >= nb - bm) {
+      pi -= nb - bm;
+      ++bm;
+    }
+    bn = bm + pi;
+    if (bm < bn) oj = bm * (nb - 1) - bm * (bm - 1) / 2 + (bn - bm - 1);
+  } else {
+    oj = blockIdx.x - npairs;
+    int j = oj;
+    while (j >= nb - 1 - bm) {
+      j -= nb - 1 - bm;
+      ++bm;
+    }
+    bn = bm + 1 + j;
+  }
+  const int b = blockIdx.y;
+  const int Np = p.Np, nc = p.nc;
+  const size_t NN = (size_t)Np * Np;
+  const c128* r = split_buf(p, b, p.rin);
+  c128* rn = p.rout ? split_buf(p, b, p.rout) : nullptr;
+  c128* rho = p.rho + (size_t)b * NN;
+  const c128* Y = p.ws + (size_t)b * (2 + nc) * NN + 2 * NN;
+  const int tps = Np / CG_KT;
+  constexpr int LD = BT + 1;
+  static_assert(BT * LD * sizeof(c128) <= sizeof(CgLds<BT>), "LDS transpose buffer");
+  c128* T = reinterpret_cast<c128*>(&L);
+  auto put = [&](int row, int col, c128 v) { T[row * LD + col] = v; };
+  auto update = [&](int row, int col, c128 v) {
+    if (bm == bn && row > col) return;
+    split_herm_rk4(p, rho, rn, bm * BT + row, bn * BT + col, cadd(v, cconj(T[col * LD + row])));
+  };
+  c128* slab = oj >= 0 ? p.kslab + ((size_t)b * (noff > 0 ? noff : 1) + oj) * 2 * BT * BT : nullptr;   // [XU, XL]
+  unsigned* ticket = p.ticket + (size_t)b * nb * nb + (oj >= 0 ? oj : 0);
+  CgAcc<BT> X;
+  if (!xl_role) {
+    if (threadIdx.x == 0) {
+      segs[0].A = p.mK + (size_t)bm * BT * Np;
+      segs[0].B = r + bn * BT;
+      for (int c = 0; c < nc; ++c) {
+        segs[1 + c].A = Y + (size_t)c * NN + (size_t)bm * BT * Np;
+        segs[1 + c].B = p.Cd + (size_t)c * NN + bn * BT;
+      }
+    }
+    __syncthreads();
+    CgSegAScaled<BT> pa{segs, tps, Np, bm < bn ? 2.0 : 1.0};
+    CgSegB<BT> pb{segs, tps, Np};
+    split_gemm<BT>((1 + nc) * tps, pa, pb, L, X);
+    if (bm == bn) {   // diagonal block: its own transpose
+      cg_epilogue<BT>(X, put);
+      __syncthreads();
+      cg_epilogue<BT>(X, update);
+      return;
+    }
+    if (!split_arrive<BT>(X, slab, ticket, 2)) return;
+    for (int e = threadIdx.x; e < BT * BT; e += CG_WG) T[(e / BT) * LD + e % BT] = slab_ld(slab + BT * BT + e);
+    __syncthreads();
+    cg_epilogue<BT>(X, update);
+    return;
+  }
+  if (threadIdx.x == 0) {
+    segs[0].A = p.mK + (size_t)bn * BT * Np;
+    segs[0].B = r + bm * BT;
+  }
+  __syncthreads();
+  CgSegA<BT> pa{segs, tps, Np};
+  CgSegB<BT> pb{segs, tps, Np};
+  split_gemm<BT>(tps, pa, pb, L, X);
+  if (!split_arrive<BT>(X, slab + BT * BT, ticket, 2)) return;
+  cg_epilogue<BT>(X, put);
+  __syncthreads();
+  for (int e = threadIdx.x; e < BT * BT; e += CG_WG) update(e / BT, e % BT, slab_ld(slab + e));
+}
+
 // Observables / snapshot of global step gs (after it; gs = 0: the initial state), one workgroup per matrix.
 __global__ __launch_bounds__(CG_WG) void glf_split_obs_kernel(LindbladParams p, int gs) {
   __shared__ c128 sred[CG_WG / 64];
@@ -998,7 +1085,12 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
     if (const char* e = std::getenv("QD_GLF_KS")) ks = std::max(1, std::min(Tk, std::atoi(e)));  // A/B overrides
     if (const char* e = std::getenv("QD_GLF_YS")) ys = nc ? std::max(1, std::min(Ty, std::atoi(e))) : 1;
   }
-  const size_t per = (size_t)(split_bt ? 2 + nc + (ks > 1 ? ks : 0) + (ys > 1 ? nc * ys : 0)
+  // two-workgroup Hermitian pairs (glf_split_hk2_kernel; QD_GLF_HK2=0 keeps one workgroup per pair): one N_p^2
+  // slab slot per matrix holds the off-diagonal pairs' XU / XL blocks
+  const char* hk2e = std::getenv("QD_GLF_HK2");
+  const bool hk2 = hsplit && !(hk2e && hk2e[0] == '0');
+  const int kslots = (ks > 1 ? ks : 0) + (hk2 ? 1 : 0);
+  const size_t per = (size_t)(split_bt ? 2 + nc + kslots + (ys > 1 ? nc * ys : 0)
                                        : glf_slots(Np, nc, herm)) * NN;
   const size_t nticket = split_bt ? (size_t)B * (1 + nc) * (Np / split_bt) * (Np / split_bt) : 0;
   const size_t st_elems = (size_t)B * per + (pad ? (size_t)B * NN : 0) + (nticket + 3) / 4;
@@ -1064,9 +1156,9 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   p.ys = ys;
   // split-K slabs after the per-matrix scratch of all B matrices; tickets after the padded copy
   p.kslab = split_bt ? scratch + (size_t)B * (2 + nc) * NN : nullptr;
-  p.yslab = split_bt ? p.kslab + (size_t)B * (ks > 1 ? ks : 0) * NN : nullptr;
+  p.yslab = split_bt ? p.kslab + (size_t)B * kslots * NN : nullptr;
   p.ticket = split_bt ? (unsigned*)(scratch + (size_t)B * per + (pad ? (size_t)B * NN : 0)) : nullptr;
-  if (split_bt && (ks > 1 || ys > 1)) QD_HIP(hipMemsetAsync(p.ticket, 0, nticket * sizeof(unsigned), st));
+  if (split_bt && (ks > 1 || ys > 1 || hk2)) QD_HIP(hipMemsetAsync(p.ticket, 0, nticket * sizeof(unsigned), st));
   if (const char* e = std::getenv("QD_STAGGER_US")) p.stagger = (unsigned long long)(std::atof(e) * 100.0);  // 100 MHz
 #ifdef QD_PHASE_TIMING
   const bool timing = true;  // diagnostics build: per-phase clocks to stderr
@@ -1102,7 +1194,13 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
           QD_SPLIT(glf_split_y_kernel, dim3(nb * nb, nc, B * ys));
           QD_HIP(hipGetLastError());
         }
-        if (hsplit) {   // split_bt is 32 or 64 here
+        if (hk2) {   // split_bt is 32 or 64 here
+          const unsigned np2 = nb * (nb + 1) / 2 + nb * (nb - 1) / 2;
+          if (split_bt == 64)
+            hipLaunchKernelGGL(glf_split_hk2_kernel<64>, dim3(np2, B), dim3(CG_WG), 0, st, p);
+          else
+            hipLaunchKernelGGL(glf_split_hk2_kernel<32>, dim3(np2, B), dim3(CG_WG), 0, st, p);
+        } else if (hsplit) {
           if (split_bt == 64)
             hipLaunchKernelGGL(glf_split_hk_kernel<64>, dim3(nb * (nb + 1) / 2, B), dim3(CG_WG), 0, st, p);
           else

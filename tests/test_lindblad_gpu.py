@@ -201,8 +201,8 @@ def test_lindblad_hermitian_kernel_matches_general(N, nc, B):
                                        (128, 1, 40, "64"), (64, 1, 24, None), (100, 1, 17, None),
                                        (128, 0, 16, None), (64, 3, 18, "64")])
 def test_lindblad_hermitian_split_path(N, nc, B, bt, monkeypatch):
-    """Hermitian batches below the persistent kernel's range run the pair-block split path (glf_split_hk_kernel:
-    one workgroup per upper block pair, the Hermitian part C r C^+ only on the upper block; 32-blocks, 64-blocks
+    """Hermitian batches below the persistent kernel's range run the pair-block split path (glf_split_hk2_kernel, or
+    glf_split_hk_kernel with QD_GLF_HK2=0: one workgroup per upper block pair, the Hermitian part C r C^+ only on the upper block; 32-blocks, 64-blocks
     forced by QD_GLF_HSPLIT_BT; N = 100 is zero-padded to 128; no collapse operators, three): vs the oracle, the persistent Hermitian kernel
     (QD_GLF_HSPLIT=0) and the general kernel, exactly Hermitian, with observables and snapshots."""
     if bt is not None:
@@ -222,11 +222,16 @@ def test_lindblad_hermitian_split_path(N, nc, B, bt, monkeypatch):
     Ct = torch.from_numpy(np.array(cs)).to(dev) if nc else None
     E = torch.eye(N, dtype=torch.complex128, device=dev).unsqueeze(0)
     out = {}
-    for tag, herm, env in (("split", None, None), ("persistent", True, "0"), ("general", False, None)):
+    for tag, herm, env, hk2 in (("split", None, None, None), ("split1", None, None, "0"), ("persistent", True, "0", None),
+                                ("general", False, None, None)):
         if env is None:
             monkeypatch.delenv("QD_GLF_HSPLIT", raising=False)
         else:
             monkeypatch.setenv("QD_GLF_HSPLIT", env)
+        if hk2 is None:
+            monkeypatch.delenv("QD_GLF_HK2", raising=False)
+        else:
+            monkeypatch.setenv("QD_GLF_HK2", hk2)
         rho = torch.from_numpy(rho0.copy()).to(dev)
         obs, snap = lindblad_rk4(Ht, Ct, rho, dt, steps, e_ops=E, save_every=3, hermitian=herm)
         torch.cuda.synchronize()
@@ -234,6 +239,10 @@ def test_lindblad_hermitian_split_path(N, nc, B, bt, monkeypatch):
     r = out["split"][0]
     assert relerr(r, ref) < TOL
     assert np.array_equal(r, np.conj(np.swapaxes(r, 1, 2)))
+    # two workgroups per off-diagonal pair (glf_split_hk2_kernel, default) vs one (QD_GLF_HK2=0): the same GEMMs and
+    # sums, so bit-identical
+    for a, b in zip(out["split"], out["split1"]):
+        assert np.array_equal(a, b)
     for other in ("persistent", "general"):
         for a, b in zip(out["split"], out[other]):
             assert relerr(a, b) < TOL
