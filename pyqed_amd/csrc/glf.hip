@@ -41,7 +41,7 @@
 namespace qd {
 namespace {
 
-constexpr int MAX_NC = 64;   // collapse-operator / GLF pair segments held in the kernels' LDS segment tables
+constexpr int MAX_NC = 256;  // collapse-operator / GLF pair segments held in the kernels' LDS segment tables (4 KB)
 
 struct LindbladParams {
   const c128* Cop;  // [nc][Np][Np]  L_c   (Lindblad: C_c)

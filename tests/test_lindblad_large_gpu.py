@@ -47,20 +47,23 @@ def test_lindblad_many_collapse_ops_and_observables_match_oracle():
     assert relerr(last.toarray() if hasattr(last, "toarray") else np.asarray(last), rho_ref) < TOL
 
 
-def test_glf_many_pairs_batch_matches_oracle():
-    """qd_lindblad_rk4 on a batch of 4 with 40 collapse operators (the persistent / split kernels' segment tables),
-    N = 64."""
+@pytest.mark.parametrize("N,nc,B,herm", [(64, 40, 4, None), (24, 256, 2, None), (24, 256, 2, False),
+                                         (100, 120, 2, None), (100, 120, 20, True)])
+def test_glf_many_pairs_batch_matches_oracle(N, nc, B, herm):
+    """qd_lindblad_rk4 with up to 256 collapse operators (the kernels' LDS segment tables; round 2 capped them at 16,
+    early round 3 at 64): the persistent kernels (N = 24, Hermitian and general), the split-K path (N = 100, B = 2)
+    and the Hermitian pair-block split path (N = 100, B = 20) against the oracle."""
     import torch
     from oracle import lindblad as olb
     from pyqed_amd import lindblad_rk4
-    N, nc, B, steps, dt = 64, 40, 4, 4, 5e-3
+    steps, dt = 4, 5e-3
     rng = np.random.default_rng(40)
     H, _ = olb.synthetic_lindblad(N, nc=1)
-    cs = np.array([0.03 * (rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N))) / np.sqrt(N)
+    cs = np.array([0.3 / np.sqrt(nc) * (rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N))) / np.sqrt(N)
                    for _ in range(nc)])
     rho0 = olb.random_pure_states(B, N, seed=5)
     ref = olb.lindblad_batch(H, list(cs), rho0, dt, steps)
     dev = torch.device("cuda", 0)
     rho = torch.from_numpy(rho0.copy()).to(dev)
-    lindblad_rk4(torch.from_numpy(H).to(dev), torch.from_numpy(cs).to(dev), rho, dt, steps)
+    lindblad_rk4(torch.from_numpy(H).to(dev), torch.from_numpy(cs).to(dev), rho, dt, steps, hermitian=herm)
     assert relerr(rho.cpu().numpy(), ref) < TOL
