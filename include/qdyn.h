@@ -72,7 +72,8 @@ int qd_workspace_stats(size_t* reserved, size_t* used);
  *                         oqs.py:1680), NULL when ne == 0
  *   snap  [B][nsteps/save_every][N][N]  rho after steps save_every, 2*save_every, ...
  *                         (NULL or save_every <= 0: no snapshots)
- * Constraints: 1 <= N <= 1024, 0 <= nc <= 16, 0 <= ne <= 16, B >= 1.
+ * Constraints: 1 <= N <= 16384, 0 <= nc <= 256, ne >= 0, B >= 1.  RK4 is evaluated
+ * in Horner form (phys.rk4 in exact arithmetic; no accumulator buffer).
  */
 int qd_lindblad_rk4(const qd_c128* H, const qd_c128* C, int nc, qd_c128* rho,
                     int B, int N, double dt, int nsteps, const qd_c128* E,
@@ -110,7 +111,7 @@ int qd_lindblad_driven_rk4(const qd_c128* H0, const qd_c128* Hd, int nd,
  * Used for Redfield dynamics in the H eigenbasis: replaces the csr R.vec(rho)
  * RK4 loop of pyqed/oqs.py:436-459 (_redfield) + rhs (oqs.py:462-463); the
  * pyqed_amd host builds P, Q, L_c, R_c from redfield_tensor's ingredients
- * (oqs.py:519-570).  Constraints: 0 <= npairs <= 16.
+ * (oqs.py:519-570).  Constraints: 0 <= npairs <= 256.
  */
 int qd_glf_rk4(const qd_c128* P, const qd_c128* Q, const qd_c128* L,
                const qd_c128* R, int npairs, qd_c128* rho, int B, int N,
@@ -230,7 +231,9 @@ int qd_spo1d_run(qd_c128* psi, const qd_c128* expV, const qd_c128* expVh,
  *                deom.py:1100,1113; e_ops of HEOM/heom.py:339-343), or NULL
  * Also runs the single-exponential HEOM chain of pyqed/HEOM/heom.py:275-347
  * (_heom, RK4) with chain tables (K = 1) built by the host.
- * Constraints: ns <= 16, nmod <= 8.
+ * Any ns and nmod: lane-group kernel (ns^2 <= 64, K <= 8), MFMA 16 x 16 tiles
+ * (9 <= ns <= 16, <= 2 modes), tiled GEMM-form kernels otherwise.  Undriven runs
+ * use Horner-form RK4 stages (no accumulator), driven ones the classic form.
  */
 int qd_deom_rk4(qd_c128* ados, int B, int nmax, int K, int ns,
                 const int32_t* minus, const int32_t* plus, const qd_c128* coef,
