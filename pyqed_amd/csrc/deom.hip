@@ -390,15 +390,15 @@ __device__ __forceinline__ void deom_stage_grp_body(const DeomParams& p) {
   }
 }
 
-#ifndef DEOM_HM_WAVES
-#define DEOM_HM_WAVES 0   // waves-per-SIMD floor of the compile-time Horner ns = 2 kernels (0: none; A/B)
-#endif
 template <int G, int KMAX, bool NS2, bool UNI = false, int HM = 0>
-__global__ __launch_bounds__(DEOM_TPB)
-#if DEOM_HM_WAVES
-__attribute__((amdgpu_waves_per_eu(HM ? DEOM_HM_WAVES : 1)))
-#endif
-void deom_stage_grp_kernel(DeomParams p) {
+__global__ __launch_bounds__(DEOM_TPB) void deom_stage_grp_kernel(DeomParams p) {
+  deom_stage_grp_body<G, KMAX, NS2, UNI, HM>(p);
+}
+// The same body held to five waves per SIMD (96 VGPRs, 12 B of spill at K = 5): the undriven ns = 2 batches of >= 64
+// hierarchies whose XCD classes are not wave-uniform (64 hierarchies: 30.5 -> 29.8 us per stage; at 16 hierarchies
+// it is slower, 11.2 vs 10.3: profiles/r03/deom/horner_compile_time_ab.txt)
+template <int G, int KMAX, bool NS2, bool UNI, int HM>
+__global__ __launch_bounds__(DEOM_TPB) __attribute__((amdgpu_waves_per_eu(5))) void deom_stage_grp_w5_kernel(DeomParams p) {
   deom_stage_grp_body<G, KMAX, NS2, UNI, HM>(p);
 }
 
@@ -904,6 +904,7 @@ int deom_launch_stage(const DeomParams& p, hipStream_t st) {
       hipLaunchKernelGGL(deom_stage_kernel, dim3(grid), dim3(tpb), 0, st, q);
       return;
     }
+    const char* w5e = getenv("QD_DEOM_W5");   // 0: keep the unconstrained kernel for >= 64 hierarchies (A/B)
     auto launch_g4 = [&](auto hmc) {
       constexpr int HM = decltype(hmc)::value;
       if (uni) {
@@ -913,6 +914,8 @@ int deom_launch_stage(const DeomParams& p, hipStream_t st) {
         else hipLaunchKernelGGL((deom_stage_grp_kernel<4, 8, true, true, HM>), dim3(grid), dim3(tpb), lds, st, q);
       } else {
         if (K <= 4) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 4, true, false, HM>), dim3(grid), dim3(tpb), lds, st, q);
+        else if (K == 5 && HM && B >= 64 && !(w5e && w5e[0] == '0'))
+          hipLaunchKernelGGL((deom_stage_grp_w5_kernel<4, 5, true, false, 1>), dim3(grid), dim3(tpb), lds, st, q);
         else if (K == 5) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 5, true, false, HM>), dim3(grid), dim3(tpb), lds, st, q);
         else if (K <= 6) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 6, true, false, HM>), dim3(grid), dim3(tpb), lds, st, q);
         else hipLaunchKernelGGL((deom_stage_grp_kernel<4, 8, true, false, HM>), dim3(grid), dim3(tpb), lds, st, q);
