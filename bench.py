@@ -784,7 +784,7 @@ def bench_deom(dev, steps, batch):
         "run_steps_per_s_end_to_end": round(steps / wall_run, 1),
         "batched": {"hierarchies": batch, "ado_steps_per_s": round(ado_b, 1), "steps_per_s": round(rate[batch], 1),
                     "layout": "ADO-major [nmax][B][2][2], hierarchies dealt to the 8 XCD block classes",
-                    "roofline": {"bound": "hbm", "kernel": "deom_stage_grp_kernel<4,5,true>",
+                    "roofline": {"bound": "hbm", "kernel": "deom_stage_grp_w5_kernel<4,5,true,false,1>",
                                  "achieved": round(ado_b * bytes_per_ado_step / 1e9, 1), "peak": HBM_PEAK_GBS,
                                  "unit": "GB/s", "frac": round(ado_b * bytes_per_ado_step / 1e9 / HBM_PEAK_GBS, 4),
                                  "bytes_per_ado_step": bytes_per_ado_step,
