@@ -788,7 +788,7 @@ def bench_deom(dev, steps, batch):
                                  "achieved": round(ado_b * bytes_per_ado_step / 1e9, 1), "peak": HBM_PEAK_GBS,
                                  "unit": "GB/s", "frac": round(ado_b * bytes_per_ado_step / 1e9 / HBM_PEAK_GBS, 4),
                                  "bytes_per_ado_step": bytes_per_ado_step,
-                                 "traffic": measured_traffic("deom_stage_grp_kernel<4,5,true>_64h", nmax * batch / 4)
+                                 "traffic": measured_traffic("deom_stage_grp_w5_kernel<4,5,true>_64h", nmax * batch / 4)
                                  if batch == 64 else None,
                                  "traffic_unit": "HBM bytes per stage launch (PMC FETCH_SIZE+WRITE_SIZE, calibrated; "
                                                  "profiles/pmc_traffic.json)"}},

@@ -18,8 +18,8 @@ if [ "$PART" = stats ]; then
   timeout -k 10 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/calib_fetch -o run -- $R/tools/pmc_calib > $OUT/calib_fetch.log 2>&1
   timeout -k 10 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/calib_write -o run -- $R/tools/pmc_calib > $OUT/calib_write.log 2>&1
 else
-  timeout -k 10 250 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu --no-reduce > $OUT/fetch.log 2>&1
-  timeout -k 10 250 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu --no-reduce > $OUT/write.log 2>&1
-  timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/gfetch -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu --no-reduce --general --no-2des --no-spo --no-deom --no-redfield > $OUT/gfetch.log 2>&1
-  timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/gwrite -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu --no-reduce --general --no-2des --no-spo --no-deom --no-redfield > $OUT/gwrite.log 2>&1
+  timeout -k 10 250 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu --no-reduce --no-deom-banded > $OUT/fetch.log 2>&1
+  timeout -k 10 250 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu --no-reduce --no-deom-banded > $OUT/write.log 2>&1
+  timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/gfetch -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu --no-reduce --no-deom-banded --general --no-2des --no-spo --no-deom --no-redfield > $OUT/gfetch.log 2>&1
+  timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/gwrite -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu --no-reduce --no-deom-banded --general --no-2des --no-spo --no-deom --no-redfield > $OUT/gwrite.log 2>&1
 fi
