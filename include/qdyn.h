@@ -35,6 +35,8 @@ extern "C" {
 #define QD_EHIP -2     /* HIP runtime error                                    */
 #define QD_ERCCL -3    /* RCCL error                                           */
 #define QD_ENOMEM -4   /* workspace allocation failed                          */
+#define QD_EBUSY -5    /* a persistent launch whose workgroups must all be resident at once was refused by
+                          hipLaunchCooperativeKernel (qd_deom_rk4_banded): nothing ran, the inputs are untouched */
 
 #define QD_COMM_ID_BYTES 128  /* size of the RCCL unique id qd_comm_unique_id writes */
 
@@ -272,8 +274,12 @@ int qd_deom_rk4_ado_major(qd_c128* ados, int B, int nmax, int K, int ns,
  * max_own * (ns == 2 ? 4 : 16) <= 1024, (2 + nmod + max_loc) ns^2 16 B <= 160 KB.
  * Other arguments and results as qd_deom_rk4 with B = 1 (bit-identical).
  * status: device int32 set to 1 if a hand-off timed out (bands not
- * co-resident; results invalid), or null: the call then synchronises the
- * stream and returns QD_EHIP in that case.
+ * co-resident; results invalid, ados overwritten), or null: the call then
+ * synchronises the stream and returns QD_EHIP in that case.  The launch is
+ * cooperative: a band count the device cannot hold at once returns QD_EBUSY
+ * before anything runs.  Undriven runs always use the Horner form of RK4 (the
+ * QD_DEOM_HORNER=0 A/B switch of qd_deom_rk4 does not apply here; DEOMSolver
+ * routes such runs to the stage launches).
  */
 int qd_deom_rk4_banded(qd_c128* ados, int nmax, int K, int ns,
                        const int32_t* lminus, const int32_t* lplus,
@@ -312,9 +318,12 @@ int qd_deom_stage(qd_c128* rho, const qd_c128* xin, qd_c128* xout, qd_c128* acc,
                   int stage, double dt, qd_c128* snap, int step, int nsteps,
                   void* stream);
 
-/* dst[i][:] = src[idx[i]][:], i < n, rows of row_elems complex (halo packing). */
-int qd_gather_rows(const qd_c128* src, const int32_t* idx, int n, int row_elems,
-                   qd_c128* dst, void* stream);
+/* dst[i][:] = src[idx[i]][:], i < n, rows of row_elems complex (halo packing);
+ * src holds nsrc rows.  An index outside [0, nsrc) is not read: its row is
+ * written as NaN, and with check != 0 the call synchronises the stream and
+ * returns QD_EINVAL. */
+int qd_gather_rows(const qd_c128* src, int nsrc, const int32_t* idx, int n,
+                   int row_elems, qd_c128* dst, int check, void* stream);
 
 /* obs[s][m] = Tr(E_m rho_0(s)), s < nsnap: DEOMSolver.run's Tr(p1 rho_0)
  * (heom/deom.py:1100,1113) from a snapshot stack [nsnap][ns][ns]. */

@@ -20,6 +20,7 @@ QD_EINVAL = -1
 QD_EHIP = -2
 QD_ERCCL = -3
 QD_ENOMEM = -4
+QD_EBUSY = -5
 
 c_int = ctypes.c_int
 c_double = ctypes.c_double
@@ -68,7 +69,7 @@ SIGNATURES = {
     "qd_deom_stage": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                               c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_double,
                               c_double, c_double, c_double, c_int, c_double, c_void_p, c_int, c_int, c_void_p]),
-    "qd_gather_rows": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "qd_gather_rows": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
     "qd_deom_trace": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "qd_heom_chain_euler": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_double, c_double, c_double,
                                     c_double, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),

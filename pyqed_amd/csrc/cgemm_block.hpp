@@ -145,20 +145,24 @@ __device__ __forceinline__ void cg_compute_tile(const CgLds<BT>& L, int buf, CgA
 // where e = tid + CG_WG*q is the element of the tile this thread stages (A: row e>>4, col e&15;
 // B: row e/BT, col e%BT) and q < cg_nld<BT>() its compile-time slot.  A policy may fetch inputs and compute the operand in finish (generated operands).
 // All threads of the workgroup must call it.  Ends with a workgroup barrier.
+// zero = false accumulates onto acc (segment lists longer than an LDS table, run in chunks).
 template <int BT, bool PIPE = false, typename APol, typename BPol>
-__device__ __forceinline__ void cg_block_gemm_gen(int T, APol& pa, BPol& pb, CgLds<BT>& L, CgAcc<BT>& acc) {
+__device__ __forceinline__ void cg_block_gemm_gen(int T, APol& pa, BPol& pb, CgLds<BT>& L, CgAcc<BT>& acc,
+                                                  bool zero = true) {
   constexpr int MW = CgCfg<BT>::MW, NW = CgCfg<BT>::NW, WC = CgCfg<BT>::WC, WR = CgCfg<BT>::WR;
   const int wave = threadIdx.x >> 6;
   const bool active = wave < WR * WC;
   const int wr0 = (wave / WC) * (MW * 16);
   const int wc0 = (wave % WC) * (NW * 16);
+  if (zero) {
 #pragma unroll
-  for (int mi = 0; mi < MW; ++mi)
+    for (int mi = 0; mi < MW; ++mi)
 #pragma unroll
-    for (int nj = 0; nj < NW; ++nj) {
-      acc.re[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
-      acc.im[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
-    }
+      for (int nj = 0; nj < NW; ++nj) {
+        acc.re[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
+        acc.im[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
+      }
+  }
   constexpr int NLD = cg_nld<BT>();
   int tid = threadIdx.x;
   asm volatile("" : "+v"(tid));  // staging address math stays per call (see cg_epilogue)
@@ -298,11 +302,11 @@ struct CgSegB {
 // Ends with a workgroup barrier, so LDS may be reused immediately after.
 template <int BT, bool PIPE = false>
 __device__ __forceinline__ void cg_block_gemm(const CgSeg* segs, int nseg, int K, int lda, int ldb, CgLds<BT>& L,
-                                              CgAcc<BT>& acc) {
+                                              CgAcc<BT>& acc, bool zero = true) {
   const int tps = K / CG_KT;
   CgSegA<BT> pa{segs, tps, lda};
   CgSegB<BT> pb{segs, tps, ldb};
-  cg_block_gemm_gen<BT, PIPE>(nseg * tps, pa, pb, L, acc);
+  cg_block_gemm_gen<BT, PIPE>(nseg * tps, pa, pb, L, acc, zero);
 }
 
 // ---------------------------------------------------------------- Hermitian X GEMM (BT = 128)
@@ -423,18 +427,21 @@ __device__ __forceinline__ void cg_herm_x_range(int t0, int t1, int T, const CgS
 // CgHermLayout; GLF operands without that property use cg_herm_x_gemm_q's plain X GEMM).  Each wave runs the
 // Hermitian segments with its own compile-time tile roles (one code path per wave for the whole range, so the MFMA
 // stream carries no selects or branches).  All threads call it; ends with a workgroup barrier.  Visit the result with
-// cg_herm_epilogue.
+// cg_herm_epilogue.  Chunked segment lists (more Hermitian segments than an LDS table holds): the first chunk as
+// above (nplain = 1, zero = true), every later one all Hermitian (nplain = 0) accumulated onto acc (zero = false).
 __device__ __forceinline__ void cg_herm_x_gemm(const CgSeg* segs, int nseg, int K, int lda, int ldb, CgLds<128>& L,
-                                               CgAcc<128>& acc) {
+                                               CgAcc<128>& acc, bool zero = true, int nplain = 1) {
   constexpr int BT = 128, MW = 2, NW = 4;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (zero) {
 #pragma unroll
-  for (int mi = 0; mi < MW; ++mi)
+    for (int mi = 0; mi < MW; ++mi)
 #pragma unroll
-    for (int nj = 0; nj < NW; ++nj) {
-      acc.re[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
-      acc.im[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
-    }
+      for (int nj = 0; nj < NW; ++nj) {
+        acc.re[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
+        acc.im[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
+      }
+  }
   const int tps = K / CG_KT, T = nseg * tps;
   CgSegA<BT> pa{segs, tps, lda};
   CgSegB<BT> pb{segs, tps, ldb};
@@ -451,8 +458,9 @@ __device__ __forceinline__ void cg_herm_x_gemm(const CgSeg* segs, int nseg, int 
   __syncthreads();
   auto run = [&](auto wc) {
     constexpr int W = decltype(wc)::value;
-    cg_herm_x_range<W, 0u, 0u>(0, tps, T, pa, pb, L, acc, wave, tid, ra, rb);
-    cg_herm_x_range<W, cg_herm_mask(W, true), cg_herm_mask(W, false)>(tps, T, T, pa, pb, L, acc, wave, tid, ra, rb);
+    const int tp = nplain * tps;
+    cg_herm_x_range<W, 0u, 0u>(0, tp, T, pa, pb, L, acc, wave, tid, ra, rb);
+    cg_herm_x_range<W, cg_herm_mask(W, true), cg_herm_mask(W, false)>(tp, T, T, pa, pb, L, acc, wave, tid, ra, rb);
   };
 #define QD_HT(w) \
   case w: run(std::integral_constant<int, w>{}); break;
@@ -544,16 +552,18 @@ __device__ __forceinline__ void cg_herm_compute_tile_q(const CgLds<128>& L, int 
 // every tile takes every segment (the plain X GEMM on this layout).  All threads call it; ends with a workgroup
 // barrier.  Visit the result with cg_herm_epilogue_q.
 __device__ __forceinline__ void cg_herm_x_gemm_q(const CgSeg* segs, int nseg, int K, int lda, int ldb, CgLds<128>& L,
-                                               CgAcc<128>& acc, bool hermitian_part) {
+                                               CgAcc<128>& acc, bool hermitian_part, bool zero = true, int nplain = 1) {
   constexpr int BT = 128, MW = 2, NW = 4;
   const int wave = threadIdx.x >> 6;
+  if (zero) {
 #pragma unroll
-  for (int mi = 0; mi < MW; ++mi)
+    for (int mi = 0; mi < MW; ++mi)
 #pragma unroll
-    for (int nj = 0; nj < NW; ++nj) {
-      acc.re[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
-      acc.im[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
-    }
+      for (int nj = 0; nj < NW; ++nj) {
+        acc.re[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
+        acc.im[mi][nj] = d4{0.0, 0.0, 0.0, 0.0};
+      }
+  }
   const int tps = K / CG_KT, T = nseg * tps;
   CgSegA<BT> pa{segs, tps, lda};
   CgSegB<BT> pb{segs, tps, ldb};
@@ -586,7 +596,7 @@ __device__ __forceinline__ void cg_herm_x_gemm_q(const CgSeg* segs, int nseg, in
     auto mid = [&]() {
       if (more) store(t + 1, (t + 1) & 1);
     };
-    cg_herm_compute_tile_q(L, t & 1, acc, wave, hermitian_part && t >= tps, mid);
+    cg_herm_compute_tile_q(L, t & 1, acc, wave, hermitian_part && t >= nplain * tps, mid);
     __syncthreads();
   }
 }

@@ -1089,23 +1089,46 @@ extern "C" int qd_deom_stage(qd_c128* rho, const qd_c128* xin, qd_c128* xout, qd
 }
 
 namespace {
-__global__ void gather_rows_kernel(const c128* src, const int32_t* idx, int n, int row, c128* dst) {
+// Bounds-checked (the round-3 kernel trusted idx): a row index outside [0, nsrc) reads
+// nothing, writes NaN and raises *bad, which the host entry point reports.
+__global__ void gather_rows_kernel(const c128* src, int nsrc, const int32_t* idx, int n, int row, c128* dst,
+                                   int* bad) {
   const size_t tot = (size_t)n * row;
-  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x)
-    dst[e] = src[(size_t)idx[e / row] * row + e % row];
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    const int r = idx[e / row];
+    if (r >= 0 && r < nsrc) {
+      dst[e] = src[(size_t)r * row + e % row];
+    } else {
+      dst[e] = cmk(__builtin_nan(""), __builtin_nan(""));
+      *bad = 1;   // vector store (global_store): benign race, every writer stores 1
+    }
+  }
 }
 }  // namespace
 
-// dst[i][:] = src[idx[i]][:] for i < n, rows of `row_elems` complex (packs a band's halo rows for the exchange)
-extern "C" int qd_gather_rows(const qd_c128* src, const int32_t* idx, int n, int row_elems, qd_c128* dst,
-                              void* stream) {
-  QD_CHECK_ARG(n >= 0 && row_elems >= 1, "qd_gather_rows: bad sizes n=%d row=%d", n, row_elems);
+// dst[i][:] = src[idx[i]][:] for i < n, rows of `row_elems` complex (packs a band's halo rows for the exchange);
+// src holds nsrc rows.  check != 0: synchronise and return QD_EINVAL if an index was out of range.
+extern "C" int qd_gather_rows(const qd_c128* src, int nsrc, const int32_t* idx, int n, int row_elems, qd_c128* dst,
+                              int check, void* stream) {
+  QD_CHECK_ARG(n >= 0 && row_elems >= 1 && nsrc >= 0, "qd_gather_rows: bad sizes n=%d row=%d nsrc=%d", n, row_elems,
+               nsrc);
   if (n == 0) return QD_OK;
   QD_CHECK_ARG(src && idx && dst, "qd_gather_rows: null pointer");
+  WsScope wss_((hipStream_t)stream);
+  void* w = nullptr;
+  int rc = workspace(WS_MISC, sizeof(int), &w, (hipStream_t)stream);
+  if (rc) return rc;
+  QD_HIP(hipMemsetAsync(w, 0, sizeof(int), (hipStream_t)stream));
   const size_t tot = (size_t)n * row_elems;
   hipLaunchKernelGGL(gather_rows_kernel, dim3((int)std::min<size_t>((tot + 255) / 256, 8192)), dim3(256), 0,
-                     (hipStream_t)stream, (const c128*)src, idx, n, row_elems, (c128*)dst);
+                     (hipStream_t)stream, (const c128*)src, nsrc, idx, n, row_elems, (c128*)dst, (int*)w);
   QD_HIP(hipGetLastError());
+  if (check) {
+    int h = 0;
+    QD_HIP(hipMemcpyAsync(&h, w, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    QD_HIP(hipStreamSynchronize((hipStream_t)stream));
+    QD_CHECK_ARG(h == 0, "qd_gather_rows: a row index outside [0, %d)", nsrc);
+  }
   return QD_OK;
 }
 
@@ -1554,14 +1577,27 @@ __global__ __launch_bounds__(TPB) void deom_band_kernel(BandParams p) {
 #endif
 }
 
+// The bands spin on each other's epochs, so all of them must be resident at once.  The launch is cooperative
+// (hipLaunchCooperativeKernel checks the grid against the occupancy of the kernel and refuses an oversize one with
+// hipErrorCooperativeLaunchTooLarge instead of stranding bands; +15-19 us once per run, MI355X_MICROARCH.md row
+// coop-launch).  Work queued on other streams can still delay a band's start; the bounded spin then sets *status and
+// the caller re-runs on the stage launches (DEOMSolver.run).  QD_DEOM_BAND_COOP=0: plain launch (A/B).
+template <typename Kern>
+hipError_t band_launch_one(Kern kern, BandParams p, int nbands, int tpb, size_t lds, hipStream_t st) {
+  const char* ce = getenv("QD_DEOM_BAND_COOP");
+  if (ce && ce[0] == '0') {
+    hipLaunchKernelGGL(kern, dim3(nbands), dim3(tpb), lds, st, p);
+    return hipGetLastError();
+  }
+  void* args[] = {(void*)&p};
+  return hipLaunchCooperativeKernel((const void*)kern, dim3(nbands), dim3(tpb), args, (unsigned)lds, st);
+}
+
 template <int G, int KMAX, bool NS2, bool FAST = false>
-void launch_band(const BandParams& p, int nbands, int tpb, size_t lds, hipStream_t st) {
-  if (tpb <= 256)
-    hipLaunchKernelGGL((deom_band_kernel<G, KMAX, NS2, 256, FAST>), dim3(nbands), dim3(tpb), lds, st, p);
-  else if (tpb <= 512)
-    hipLaunchKernelGGL((deom_band_kernel<G, KMAX, NS2, 512, FAST>), dim3(nbands), dim3(tpb), lds, st, p);
-  else
-    hipLaunchKernelGGL((deom_band_kernel<G, KMAX, NS2, 1024, FAST>), dim3(nbands), dim3(tpb), lds, st, p);
+hipError_t launch_band(const BandParams& p, int nbands, int tpb, size_t lds, hipStream_t st) {
+  if (tpb <= 256) return band_launch_one(deom_band_kernel<G, KMAX, NS2, 256, FAST>, p, nbands, tpb, lds, st);
+  if (tpb <= 512) return band_launch_one(deom_band_kernel<G, KMAX, NS2, 512, FAST>, p, nbands, tpb, lds, st);
+  return band_launch_one(deom_band_kernel<G, KMAX, NS2, 1024, FAST>, p, nbands, tpb, lds, st);
 }
 
 }  // namespace
@@ -1665,17 +1701,26 @@ extern "C" int qd_deom_rk4_banded(qd_c128* ados, int nmax, int K, int ns, const 
     p.nsteps = nsteps;
     p.max_loc = max_loc;
     p.dt = dt;
+    hipError_t le;
     if (G == 4) {
       const char* fe = getenv("QD_DEOM_BAND_FAST");
       const bool fast = nmod == 1 && !(fe && fe[0] == '0');
-      if (fast && K == 5) launch_band<4, 5, true, true>(p, nbands, tpb, lds, st);        // the bench bath
-      else if (fast && K == 6) launch_band<4, 6, true, true>(p, nbands, tpb, lds, st);   // its stretch (npsd 5)
-      else if (K <= 5) launch_band<4, 5, true>(p, nbands, tpb, lds, st);
-      else launch_band<4, 8, true>(p, nbands, tpb, lds, st);
+      if (fast && K == 5) le = launch_band<4, 5, true, true>(p, nbands, tpb, lds, st);        // the bench bath
+      else if (fast && K == 6) le = launch_band<4, 6, true, true>(p, nbands, tpb, lds, st);   // its stretch (npsd 5)
+      else if (K <= 5) le = launch_band<4, 5, true>(p, nbands, tpb, lds, st);
+      else le = launch_band<4, 8, true>(p, nbands, tpb, lds, st);
     } else {
-      launch_band<16, 8, false>(p, nbands, tpb, lds, st);
+      le = launch_band<16, 8, false>(p, nbands, tpb, lds, st);
     }
-    QD_HIP(hipGetLastError());
+    if (le == hipErrorCooperativeLaunchTooLarge) {
+      (void)hipGetLastError();
+      set_error("qd_deom_rk4_banded: %d bands of %d threads / %zu B LDS cannot all be co-resident "
+                "(hipErrorCooperativeLaunchTooLarge); use fewer bands or the stage launches", nbands, tpb, lds);
+      return QD_EBUSY;
+    }
+    QD_HIP(le);
+    if (const char* fe = getenv("QD_DEOM_BAND_FAKE_TIMEOUT"))   // tests: report a hand-off timeout after the run
+      if (fe[0] == '1') QD_HIP(hipMemsetAsync(stat, 1, 1, st));
 #ifdef QD_PHASE_TIMING
     {   // per-phase wall-clock (100 MHz ticks) summed over the stages: mean and max over bands, per stage, in us
       std::vector<unsigned long long> h((size_t)nbands * 4);

@@ -3,11 +3,16 @@
 //   qd_fft_axis : FFT / inverse FFT along one axis of a contiguous array viewed as
 //                 [outer][n][inner], fused with fftshift, a scale factor and the
 //                 phase exp(-/+ i freq x0) of pyqed.fft.fft / ifft (fft.py:11-102)
-//                 and fft2 (fft.py:104-126).  n a power of two <= 1024 uses the
-//                 Stockham LDS FFT of spo.hip's family; any other n <= 4096 uses a
-//                 direct DFT with integer-reduced fp64 twiddles (exact periodicity).
+//                 and fft2 (fft.py:104-126).  Any n (numpy.fft takes every length):
+//                 powers of two in [16, 1024] run one Stockham LDS kernel with the
+//                 epilogue fused; every other n runs the any-size engine of the SPO
+//                 grids (spo_gen.hip fft_lines: mixed radix 2/3/4/5/p <= 61 in LDS,
+//                 Bluestein, four-step for long smooth lengths, direct DFT for the
+//                 rest) on a copy, then one shift / scale / phase pass back.
 //   qd_dft2     : DFT at arbitrary momenta (fft.py:128-160 dft / dft2).
 #include "qd_common.hpp"
+
+#include <cstdlib>
 
 namespace qd {
 namespace {
@@ -83,35 +88,26 @@ __global__ void fft_pow2_kernel(c128* data, int inner, int inverse, int shift, d
   fft_store(X, base, inner, L, shift, scale, freq, x0, inverse ? 1 : -1);
 }
 
-// direct DFT for arbitrary n: X[k] = sum_j x[j] w^{(j k) mod n}, w = exp(-/+ 2 pi i / n)
-__global__ void dft_kernel(c128* data, int n, int inner, int inverse, int shift, double scale, const double* freq,
-                           double x0) {
-  extern __shared__ c128 sm[];
-  c128* x = sm;       // n
-  c128* X = sm + n;   // n
-  c128* tw = X + n;   // n
-  const long b = blockIdx.x;
-  const long o = b / inner, i = b % inner;
-  c128* base = data + o * (long)n * inner + i;
-  for (int k = threadIdx.x; k < n; k += blockDim.x) {
-    x[k] = base[(long)k * inner];
-    double s, c;
-    sincospi((inverse ? 2.0 : -2.0) * (double)k / (double)n, &s, &c);
-    tw[k] = cmk(c, s);
-  }
-  __syncthreads();
-  for (int k = threadIdx.x; k < n; k += blockDim.x) {
-    c128 acc = cmk(0, 0);
-    long idx = 0;
-    for (int j = 0; j < n; ++j) {
-      acc = cadd(acc, cmul(x[j], tw[idx]));
-      idx += k;
-      if (idx >= n) idx -= n;
+// out[o][kp][i] = scale X[o][pos(k)][i] exp(sign i freq[kp] x0), k = fftshift source of kp; pos = the slot of X[k]
+// in fft_lines' output (four-step order when l2 != 0)
+__global__ void fft_post_kernel(const c128* __restrict__ X, c128* __restrict__ out, long O, int n, long I, int shift,
+                                double scale, const double* __restrict__ freq, double x0, int sign, int l2) {
+  const long tot = O * n * I;
+  const int l1 = l2 ? n / l2 : 1;
+  for (long f = blockIdx.x * (long)blockDim.x + threadIdx.x; f < tot; f += (long)gridDim.x * blockDim.x) {
+    const long o = f / ((long)n * I), r = f - o * n * I;
+    const int kp = (int)(r / I);
+    const long i = r - (long)kp * I;
+    const int k = shift ? ((kp - n / 2) % n + n) % n : kp;
+    const int pos = l2 ? (k % l1) * l2 + k / l1 : k;
+    c128 v = cscale(X[((size_t)o * n + pos) * I + i], scale);
+    if (freq) {
+      double sn, c;
+      sincos(sign * freq[kp] * x0, &sn, &c);
+      v = cmul(v, cmk(c, sn));
     }
-    X[k] = acc;
+    out[f] = v;
   }
-  __syncthreads();
-  fft_store(X, base, inner, n, shift, scale, freq, x0, inverse ? 1 : -1);
 }
 
 __global__ void twiddles_kernel(int L, c128* tw) {
@@ -149,11 +145,11 @@ extern "C" int qd_fft_axis(qd_c128* data, int outer, int n, int inner, int inver
   WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   QD_CHECK_ARG(data, "qd_fft_axis: null pointer");
   QD_CHECK_ARG(outer >= 1 && inner >= 1 && n >= 1, "qd_fft_axis: bad sizes");
-  QD_CHECK_ARG((long)outer * inner < (1L << 31), "qd_fft_axis: batch too large");
+  QD_CHECK_ARG((long)outer * n * inner < (1L << 31), "qd_fft_axis: array too large (%ld elements)",
+               (long)outer * n * inner);
   hipStream_t st = (hipStream_t)stream;
   const int batch = outer * inner;
-  const bool pow2 = n >= 16 && n <= 1024 && (n & (n - 1)) == 0;
-  QD_CHECK_ARG(pow2 || n <= 3200, "qd_fft_axis: n=%d: powers of two up to 1024 or any n up to 3200", n);
+  const bool pow2 = n >= 16 && n <= 1024 && (n & (n - 1)) == 0 && !std::getenv("QD_FFT_GENERIC");
   if (pow2) {
     void* w = nullptr;
     int rc = workspace(WS_MISC, n * sizeof(c128), &w, st);
@@ -174,10 +170,21 @@ extern "C" int qd_fft_axis(qd_c128* data, int outer, int n, int inner, int inver
       case 1024: FCALL(1024); break;
     }
 #undef FCALL
-  } else {
-    hipLaunchKernelGGL(dft_kernel, dim3(batch), dim3(256), 3 * n * sizeof(c128), st, (c128*)data, n, inner, inverse,
-                       shift, scale, freq, x0);
+    QD_HIP(hipGetLastError());
+    return QD_OK;
   }
+  // any other length: transform a copy with the any-size engine, then shift / scale / phase back into data
+  const long tot = (long)outer * n * inner;
+  void* w = nullptr;
+  int rc = workspace(WS_MISC, (size_t)tot * sizeof(c128), &w, st);
+  if (rc) return rc;
+  c128* X = (c128*)w;
+  QD_HIP(hipMemcpyAsync(X, data, (size_t)tot * sizeof(c128), hipMemcpyDeviceToDevice, st));
+  int l2 = 0;
+  if ((rc = fft_lines(X, outer, n, inner, inverse != 0, st, &l2))) return rc;
+  const int grid = (int)std::max<long>(1, std::min<long>((tot + 255) / 256, 16384));
+  hipLaunchKernelGGL(fft_post_kernel, dim3(grid), dim3(256), 0, st, (const c128*)X, (c128*)data, (long)outer, n,
+                     (long)inner, shift, scale, freq, x0, inverse ? 1 : -1, l2);
   QD_HIP(hipGetLastError());
   return QD_OK;
 }

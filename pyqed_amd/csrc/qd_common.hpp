@@ -125,4 +125,8 @@ inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 int cgemm_splitk_slabs(const c128* A, const c128* B, int Mp, int Kp, int Np, c128* slabs, int max_S, int* S_out,
                        hipStream_t st);
 
+// Unnormalised DFT along the middle axis of the [O][L][I] grid x, in place, any L (spo_gen.hip).  *l2 != 0: four-step
+// order, X[k1 + (L / *l2) k2] at slot *l2 k1 + k2; else natural order.  O L I < 2^31.
+int fft_lines(c128* x, long O, int L, long I, bool inv, hipStream_t st, int* l2);
+
 }  // namespace qd

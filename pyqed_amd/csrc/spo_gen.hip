@@ -395,6 +395,19 @@ __global__ void fourstep_kperm_kernel(const c128* __restrict__ K, c128* Kp, int 
   }
 }
 
+// Four-step twiddle of lines viewed as [L1][L2] inside a [O][L][I] grid: element (o, k1, n2, i) *= w_L^(+-n2 k1)
+__global__ void fourstep_twiddle_inner_kernel(c128* psi, long n, int L1, int L2, long I, const c128* __restrict__ twL,
+                                              int inv) {
+  const long L = (long)L1 * L2;
+  for (long f = blockIdx.x * (long)blockDim.x + threadIdx.x; f < n; f += (long)gridDim.x * blockDim.x) {
+    const long r = (f / I) % L;
+    const long k1 = r / L2, n2 = r - k1 * L2;
+    c128 w = twL[(n2 * k1) % L];
+    if (inv) w = cconj(w);
+    psi[f] = cmul(psi[f], w);
+  }
+}
+
 // ---------------------------------------------------------------- plan tables
 __global__ void twiddle_table_kernel(int M, c128* tw) {
   for (int m = blockIdx.x * blockDim.x + threadIdx.x; m < M; m += gridDim.x * blockDim.x) {
@@ -533,16 +546,28 @@ __global__ __launch_bounds__(1024) void spo_expm_kernel(const void* v_, int herm
       for (int l = 0; l < ns; ++l) nrm = fmax(nrm, T[l].re);
       nrm *= fabs(tau);
       int sq = 0;
-      while (nrm > 0.5) {
-        nrm *= 0.5;
-        ++sq;
+      if (!(nrm <= 1.7976931348623157e308)) {
+        sq = -1;   // inf / NaN in V: no exponential (the host raises LinAlgError first, as eigh does)
+      } else {
+        while (nrm > 0.5 && sq < 1100) {   // a finite norm needs at most ~1025 halvings: the loop always ends
+          nrm *= 0.5;
+          ++sq;
+        }
       }
       sh_s = sq;
     }
     __syncthreads();
     const int sq = sh_s;
     __syncthreads();
-    const double sc = tau / (double)(1L << sq);
+    if (sq < 0) {
+      const c128 nan = cmk(__builtin_nan(""), __builtin_nan(""));
+      if (own) {
+        expVh[(size_t)p * ns2 + e] = nan;
+        if (expV) expV[(size_t)p * ns2 + e] = nan;
+      }
+      continue;
+    }
+    const double sc = ldexp(tau, -sq);   // tau / 2^sq without an integer shift (sq may exceed 63)
     // X = -i V tau / 2^sq ; S = I + X ; T = X
     if (own) {
       X[e] = cmulmi(cscale(h, sc));
@@ -838,6 +863,69 @@ int run_nd(Exec& x, const c128* Uh, const c128* Ufull, int nsteps, int nout, c12
 }
 
 }  // namespace spog
+
+// Unnormalised DFT along the middle axis of the [O][L][I] grid x, in place (inv: the conjugate kernel), for pyqed.fft's
+// any-length transforms (fft.hip).  Lengths the LDS plans take (mixed radix <= 5120, Bluestein with M <= 5120) run one
+// spo_axis_kernel pass; longer lengths that split as L1 L2 with both factors LDS-plannable run the four-step FFT and
+// leave X[k1 + L1 k2] at slot L2 k1 + k2 (*l2 = L2; *l2 = 0: natural order); anything else a direct DFT.
+int fft_lines(c128* x, long O, int L, long I, bool inv, hipStream_t st, int* l2) {
+  using namespace spog;
+  *l2 = 0;
+  const long total = O * L * I;
+  int kind, M;
+  size_t nslots;
+  plan_kind(L, &kind, &M, &nslots);
+  const char* fk = getenv("QD_SPO_FORCE_KIND");
+  int L1 = 0;
+  if (kind == DIRECT && !(fk && fk[0] == '2')) {
+    for (int a = 2; (long)a * a <= L; ++a) {
+      if (L % a) continue;
+      int k1, k2, m1, m2;
+      size_t s1, s2;
+      plan_kind(a, &k1, &m1, &s1);
+      plan_kind(L / a, &k2, &m2, &s2);
+      if (k1 != DIRECT && k2 != DIRECT) L1 = a;   // the most balanced plannable split
+    }
+  }
+  Exec e;
+  e.st = st;
+  e.psi = x;
+  e.ns = (int)I;
+  int rc;
+  if (L1) {
+    const int L2 = L / L1;
+    void* w = nullptr;
+    if ((rc = workspace(WS_MISC, (plan_slots(L1) + plan_slots(L2) + (size_t)L) * sizeof(c128), &w, st))) return rc;
+    c128* tab = (c128*)w;
+    c128* twL = tab + plan_slots(L1) + plan_slots(L2);
+    e.D = 3;
+    e.n[0] = (int)O;
+    e.n[1] = L1;
+    e.n[2] = L2;
+    e.npts = O * L;
+    if ((rc = plan_axis(L1, tab, e.f[1], st))) return rc;
+    if ((rc = plan_axis(L2, tab + plan_slots(L1), e.f[2], st))) return rc;
+    hipLaunchKernelGGL(twiddle_table_kernel, dim3((L + 255) / 256), dim3(256), 0, st, L, twL);
+    QD_HIP(hipGetLastError());
+    if ((rc = e.transform(1, inv))) return rc;
+    hipLaunchKernelGGL(fourstep_twiddle_inner_kernel, dim3(grid_for(total)), dim3(256), 0, st, x, total, L1, L2, I,
+                       (const c128*)twL, inv ? 1 : 0);
+    QD_HIP(hipGetLastError());
+    if ((rc = e.transform(2, inv))) return rc;
+    *l2 = L2;
+    return QD_OK;
+  }
+  void* w = nullptr;
+  const size_t tmp = kind == DIRECT ? (size_t)total : 0;
+  if ((rc = workspace(WS_MISC, (nslots + tmp) * sizeof(c128), &w, st))) return rc;
+  e.D = 2;
+  e.n[0] = (int)O;
+  e.n[1] = L;
+  e.npts = O * L;
+  e.tmp = (c128*)w + nslots;
+  if ((rc = plan_axis(L, (c128*)w, e.f[1], st))) return rc;
+  return e.transform(1, inv);
+}
 
 // Generic SPO2 / SPO3 run (any grid, any ns).  dims = {nx, ny} or {nx, ny, nz}; expK [dims] unscaled;
 // expKy [nx][ny] (2D Jacobi) or null; expV (merged V structure) or null.

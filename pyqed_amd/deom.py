@@ -450,7 +450,13 @@ class DEOMSolver:
         trace = torch.empty((B, nt + 1, 1), dtype=torch.complex128, device=dev) if p1 is not None else None
         tabs = self.device_tables(dev)
         bands = self.band_tables(dev) if B == 1 else None
+        self.last_run_banded = False
         if bands is not None:
+            # The bands wait on each other inside one launch: if the device cannot hold them all at once
+            # (QD_EBUSY from the cooperative launch, nothing ran) or a hand-off timed out (status, e.g. work on
+            # another stream delayed a band; ados was overwritten), the run is repeated on the stage launches,
+            # which need no co-residency and give bit-identical results.
+            ados0 = ados.clone()
             status = torch.zeros(1, dtype=torch.int32, device=dev)
             with torch.cuda.device(dev):
                 rc = _lib.load().qd_deom_rk4_banded(
@@ -459,10 +465,18 @@ class DEOMSolver:
                     fs.ctypes.data if fs is not None else None, fc.ctypes.data if fc is not None else None, float(dt),
                     int(nt), rho_sys.data_ptr(), _lib.ptr(p1_t), 1 if p1 is not None else 0, _lib.ptr(trace),
                     status.data_ptr(), _lib.stream_ptr(dev))
-            _lib.check(rc, "qd_deom_rk4_banded")
-            if int(status.item()) != 0:
-                raise RuntimeError("qd_deom_rk4_banded: a band hand-off timed out (bands not co-resident)")
-        else:
+            if rc != _lib.QD_EBUSY:
+                _lib.check(rc, "qd_deom_rk4_banded")
+            if rc == _lib.QD_EBUSY or int(status.item()) != 0:
+                import warnings
+                warnings.warn("qd_deom_rk4_banded: " + ("bands cannot be co-resident" if rc else
+                                                         "a band hand-off timed out") +
+                              "; re-running on the stage launches", RuntimeWarning)
+                ados.copy_(ados0)
+                bands = None
+            else:
+                self.last_run_banded = True
+        if bands is None:
             with torch.cuda.device(dev):
                 rc = getattr(_lib.load(), "qd_deom_rk4_ado_major" if ado_major else "qd_deom_rk4")(
                     ados.data_ptr(), B, nmax, K, ns, tabs[0].data_ptr(), tabs[1].data_ptr(), tabs[2].data_ptr(),
@@ -504,8 +518,8 @@ class DEOMSolver:
         stay on the stage launches.  Measured at 6188 ADOs: 256 bands 94.7k steps/s against 51.7k for the stage
         launches; 18,564 ADOs on 256 bands 68k against 42.1k (tools/deom_band_sweep.py,
         profiles/r03/deom/band_sweep.txt).  QD_DEOM_BANDS overrides.  Cached per (device, count)."""
-        if os.environ.get("QD_DEOM_BANDED") == "0":
-            return None
+        if os.environ.get("QD_DEOM_BANDED") == "0" or os.environ.get("QD_DEOM_HORNER") == "0":
+            return None   # QD_DEOM_HORNER=0 (classic-RK4 A/B runs) is a stage-launch switch: the bands run Horner
         ns, K, nmax = self.nsys, self.nind, self.nmax
         if not (2 <= ns <= 4) or K > 8:
             return None
@@ -521,7 +535,9 @@ class DEOMSolver:
                 if -(-nmax // nbands) > fat:   # fat bands lose to the stage launches (146 rows: 0.78x)
                     return None
         nbands = max(1, min(int(nbands), nmax, cap))
-        key = (str(dev), nbands, self.lmax, K, nmax)    # the keys are a function of (lmax, K)
+        nmod = int(np.max(self.bath.mode)) + 1
+        # the keys are a function of (lmax, K); ns and nmod enter the eligibility checks below
+        key = (str(dev), nbands, self.lmax, K, nmax, ns, nmod)
         cache = getattr(self, "_band_cache", None)
         if cache is not None and cache[0] == key:
             return cache[1]
@@ -529,7 +545,6 @@ class DEOMSolver:
         plans = make_plans(self._minus, self._plus, nbands)
         own = np.array([p.n_own for p in plans])
         loc = np.array([p.n_loc for p in plans])
-        nmod = int(np.max(self.bath.mode)) + 1
         if own.max() * G > 1024 or (2 + nmod + loc.max()) * ns * ns * 16 > 160 * 1024 or \
                 max(len(p.recv) for p in plans) > 64:
             return None

@@ -112,6 +112,9 @@ class DeomBand:
         # with acc = NULL, as qd_deom_rk4 does)
         self.acc = z(plan.n_own) if (Hdip is not None or Qdip is not None) else None
         self.snap = z(nt + 1) if lo == 0 else None
+        for q, v in plan.send.items():   # packed rows are this band's own rows (qd_gather_rows also bounds-checks)
+            if len(v) and (int(np.min(v)) < 0 or int(np.max(v)) >= plan.n_own):
+                raise ValueError(f"band {plan.rank}: send rows for band {q} outside [0, {plan.n_own})")
         self.send_idx = {q: i32(v) for q, v in plan.send.items()}
         self.send_buf = {q: z(len(v)) for q, v in plan.send.items()}
         self.stage_fn = stage_fn
@@ -146,8 +149,8 @@ class DeomBand:
             torch.index_select(src, 0, idx.long(), out=dst)
             return dst
         with torch.cuda.device(self.dev):
-            rc = _lib.load().qd_gather_rows(src.data_ptr(), idx.data_ptr(), len(idx), self.ns * self.ns, dst.data_ptr(),
-                                            _lib.stream_ptr(self.dev))
+            rc = _lib.load().qd_gather_rows(src.data_ptr(), src.shape[0], idx.data_ptr(), len(idx), self.ns * self.ns,
+                                            dst.data_ptr(), 0, _lib.stream_ptr(self.dev))
         _lib.check(rc, "qd_gather_rows")
         return dst
 
@@ -220,8 +223,9 @@ class CollectiveExchange:
         if n:
             if self.dev.type == "cuda":
                 with torch.cuda.device(self.dev):
-                    rc = _lib.load().qd_gather_rows(src.data_ptr(), self.export.data_ptr(), n, self.ns * self.ns,
-                                                    self.sendbuf.data_ptr(), _lib.stream_ptr(self.dev))
+                    rc = _lib.load().qd_gather_rows(src.data_ptr(), src.shape[0], self.export.data_ptr(), n,
+                                                    self.ns * self.ns, self.sendbuf.data_ptr(), 0,
+                                                    _lib.stream_ptr(self.dev))
                 _lib.check(rc, "qd_gather_rows")
             else:
                 torch.index_select(src, 0, self.export.long(), out=self.sendbuf[:n])

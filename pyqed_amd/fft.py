@@ -25,22 +25,66 @@ def _fft_axis(a, axis, inverse, scale, freq, x0, shift=True):
     return t.cpu().numpy()
 
 
+def _normalize_axis(axis, ndim):
+    """numpy's normalize_axis_index (fft.py:41 / :78): an out-of-range axis raises AxisError."""
+    if not -ndim <= axis < ndim:
+        raise np.exceptions.AxisError(axis, ndim)
+    return axis % ndim
+
+
+_NORM_SCALE = {None: lambda n: 1.0, "backward": lambda n: 1.0, "ortho": lambda n: 1.0 / np.sqrt(n),
+               "forward": lambda n: 1.0 / n}
+
+
 def fft(a, x=None, axis=-1, **kwargs):
-    """fft.py:11-68: g(w) = fftshift(FFT(a)) dx exp(-i w x0), freq = 2 pi fftshift(fftfreq(n, dx))."""
+    """fft.py:11-68: g(w) = fftshift(FFT(a)) dx exp(-i w x0), freq = 2 pi fftshift(fftfreq(n, dx)).
+
+    Any length (numpy.fft takes every n).  ``**kwargs`` are forwarded as the reference forwards them to
+    ``np.fft.fft`` (fft.py:49): ``norm`` (None / 'backward' / 'ortho' / 'forward') scales the transform; ``n`` pads or
+    truncates the axis, after which the reference multiplies the length-n result by a phase built from the
+    ORIGINAL length and fails to broadcast unless n equals it -- that ValueError is reproduced here.  Anything else
+    raises the TypeError numpy raises for an unknown keyword."""
     a = np.asarray(a)
-    axis = axis % a.ndim
+    axis = _normalize_axis(axis, a.ndim)
     nx = a.shape[axis]
     if x is None:
         x = np.arange(nx)
     dx = x[1] - x[0]
+    kw = dict(kwargs)
+    norm = kw.pop("norm", None)
+    n = kw.pop("n", None)
+    if kw:
+        raise TypeError(f"fft() got an unexpected keyword argument '{next(iter(kw))}'")
+    if norm not in _NORM_SCALE:
+        raise ValueError(f'Invalid norm value {norm}; should be "backward", "ortho" or "forward".')
+    if n is not None:
+        n = int(n)
+        if n < 1:
+            raise ValueError(f"Invalid number of FFT data points ({n}) specified.")
+        if n != nx and n != 1:
+            # np.fft.fft(a, n) has n points along `axis`; the reference's exp(-i freq x0) has nx (fft.py:53-61)
+            shape = list(a.shape)
+            shape[axis] = n
+            raise ValueError(f"operands could not be broadcast together with shapes {tuple(shape)} ({nx},)")
     freq = 2. * np.pi * np.fft.fftshift(np.fft.fftfreq(nx, d=dx))
-    return _fft_axis(a, axis, False, dx, freq, float(np.real(x[0]))), freq
+    if n == 1 and nx != 1:
+        # np.fft.fft(a, n=1) keeps a[0] along the axis, and the reference's phase broadcasts it to nx points:
+        # a[0] dx exp(-i freq x0).  That is exactly the length-nx transform of a[0] placed at index 0 (the FFT of a
+        # delta is the constant a[0]; every other term is an exact zero), so the GPU path serves it unchanged.
+        z = np.zeros(a.shape, dtype=complex)
+        sl = [slice(None)] * a.ndim
+        sl[axis] = slice(0, 1)
+        z[tuple(sl)] = a[tuple(sl)]
+        a, nx = z, 1
+    scale = dx * _NORM_SCALE[norm](nx)
+    return _fft_axis(a, axis, False, scale, freq, float(np.real(x[0]))), freq
 
 
 def ifft(a, x=None, axis=-1):
-    """fft.py:70-102: g = fftshift(IFFT(a)) dx n exp(+i w x0)."""
+    """fft.py:70-102: g = fftshift(IFFT(a)) dx n exp(+i w x0), any length (the unnormalised inverse kernel times dx,
+    which is the reference's ifft(a) * dx * n)."""
     a = np.asarray(a)
-    axis = axis % a.ndim
+    axis = _normalize_axis(axis, a.ndim)
     nx = a.shape[axis]
     if x is None:
         x = np.arange(nx)

@@ -17,6 +17,13 @@ from .mol import Result
 pi = np.pi
 
 
+
+def _check_finite(v):
+    """The reference builds the point propagators with eigh / eig (wpd.py:585-623, 960-985), which raise LinAlgError on
+    inf / NaN potentials; the device exponential would only produce NaN, so the same error is raised up front."""
+    if not np.all(np.isfinite(v)):
+        raise np.linalg.LinAlgError("Array must not contain infs or NaNs")
+
 def interval(x):
     return x[1] - x[0]
 
@@ -188,6 +195,7 @@ class _PointPropagators:
     def _build_point_ops(self, dt):
         v = self._pot()
         ns = v.shape[-1]
+        _check_finite(v)
         if ns > 32:   # beyond the device exponential's workgroup (ns^2 <= 1024 lanes): host eigh, as the reference
             w, u = self._host_eig()
             ud = np.conj(np.swapaxes(u, -1, -2))
@@ -408,6 +416,7 @@ class SPO2NH(SPO2):
         v = np.asarray(self.v, dtype=complex)
         self._ur = self._ovlp = None
         ns = v.shape[-1]
+        _check_finite(v)
         if ns > 32:
             ur = self.right_eigenstates
             w = self._w

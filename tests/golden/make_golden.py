@@ -356,6 +356,39 @@ def fft_phys():
     save("fft_phys", **out)
 
 
+@golden
+def fft_any():
+    """pyqed.fft.fft / ifft at lengths the round-3 GPU path refused or ran as a direct DFT (fft.py:11-102), with the
+    caller's kwargs forwarded to np.fft.fft (fft.py:49): norm, n; axis 0 of a 3-D array; odd / prime lengths."""
+    import importlib
+    pf = importlib.import_module("pyqed.fft")
+    rng = np.random.default_rng(77)
+    out = {}
+    for n in (8, 2048, 4096, 5000, 7919, 12288, 1000):
+        x = np.linspace(-7.0, 9.0, n)
+        a = np.exp(-(x - 1) ** 2 / 3) * np.exp(0.7j * x) + 0.01 * rng.standard_normal(n)
+        out[f"x{n}"], out[f"a{n}"] = x, a
+        out[f"fft{n}_g"], out[f"fft{n}_w"] = pf.fft(a, x)
+        out[f"ifft{n}_g"], _ = pf.ifft(a, x)
+    out["fft5000_ortho_g"], _ = pf.fft(out["a5000"], out["x5000"], norm="ortho")
+    out["fft2048_forward_g"], _ = pf.fft(out["a2048"], out["x2048"], norm="forward")
+    out["fft7919_n_g"], _ = pf.fft(out["a7919"], out["x7919"], n=7919)
+    out["fft1000_n1_g"], _ = pf.fft(out["a1000"], out["x1000"], n=1)
+    try:
+        pf.fft(out["a1000"], out["x1000"], n=900)
+        out["n900_raises"] = np.array(False)
+    except ValueError:
+        out["n900_raises"] = np.array(True)
+    T = rng.standard_normal((45, 6, 7)) + 1j * rng.standard_normal((45, 6, 7))
+    xt = np.linspace(0.5, 3.0, 45)
+    out["T"], out["xt"] = T, xt
+    out["fftT0_g"], out["fftT0_w"] = pf.fft(T, xt, axis=0)
+    out["fftT1_ortho_g"], _ = pf.fft(T, np.linspace(0, 1, 6), axis=1, norm="ortho")
+    out["ifftT0_g"], _ = pf.ifft(T, xt, axis=0)
+    out["ifftTm1_g"], _ = pf.ifft(T, np.linspace(-1, 1, 7), axis=-1)
+    save("fft_any", **out)
+
+
 # ----------------------------------------------------------------- Redfield / 2DES
 # Spectral functions by name (tests/conftest.py SPECTRA holds the same definitions).
 SPECTRA = {

@@ -165,3 +165,51 @@ def test_banded_stretch_hierarchy_256_bands_matches_stage_launches():
     got, got_ados = _run(sol, rho0, 0.001, 6, 256)
     assert np.array_equal(got, ref)
     assert np.array_equal(got_ados, ref_ados)
+
+
+def test_solver_run_falls_back_to_stage_launches_after_band_timeout(monkeypatch):
+    """A hand-off timeout (status = 1, forced by QD_DEOM_BAND_FAKE_TIMEOUT after a real banded run has overwritten the
+    ADOs) makes DEOMSolver.run restore the initial ADOs and re-run on the stage launches with a warning: the result
+    equals the stage launches bit for bit."""
+    import warnings
+    sol = _spin_boson(8)
+    rho0 = np.array([[1, 0], [0, 0]], complex)
+    monkeypatch.setenv("QD_DEOM_BANDED", "0")
+    _, ref = sol.run(rho0.copy(), 0.005, 20)
+    ref_ddos = sol.ddos.copy()
+    monkeypatch.delenv("QD_DEOM_BANDED")
+    monkeypatch.setenv("QD_DEOM_BAND_FAKE_TIMEOUT", "1")
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        _, got = sol.run(rho0.copy(), 0.005, 20)
+    assert any("timed out" in str(x.message) for x in w)
+    assert sol.last_run_banded is False
+    assert np.array_equal(np.array(got), np.array(ref))
+    assert np.array_equal(sol.ddos, ref_ddos)
+    monkeypatch.delenv("QD_DEOM_BAND_FAKE_TIMEOUT")
+    _, again = sol.run(rho0.copy(), 0.005, 20)
+    assert sol.last_run_banded is True
+    assert np.array_equal(np.array(again), np.array(ref))
+
+
+def test_banded_cooperative_and_plain_launch_agree(monkeypatch):
+    """The cooperative launch (default) and the plain launch (QD_DEOM_BAND_COOP=0) give identical results."""
+    sol = _spin_boson(12)
+    rho0 = np.array([[1, 0], [0, 0]], complex)
+    a, a_ados = _run(sol, rho0, 0.005, 5, 256)
+    monkeypatch.setenv("QD_DEOM_BAND_COOP", "0")
+    b, b_ados = _run(sol, rho0, 0.005, 5, 256)
+    assert np.array_equal(a, b) and np.array_equal(a_ados, b_ados)
+
+
+def test_band_table_cache_keyed_on_ns_and_modes():
+    """band_tables' cache key includes ns and the mode count: a solver whose system size changes between
+    runs re-plans instead of reusing stale, unchecked tables."""
+    from pyqed_amd._util import default_device
+    dev = default_device()
+    sol = _spin_boson(5)
+    sol.check_()
+    sol.init_()
+    t1 = sol.band_tables(dev, 4)
+    assert sol._band_cache[0][-2:] == (2, 1)
+    assert sol.band_tables(dev, 4) is t1

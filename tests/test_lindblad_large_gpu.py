@@ -67,3 +67,44 @@ def test_glf_many_pairs_batch_matches_oracle(N, nc, B, herm):
     rho = torch.from_numpy(rho0.copy()).to(dev)
     lindblad_rk4(torch.from_numpy(H).to(dev), torch.from_numpy(cs).to(dev), rho, dt, steps, hermitian=herm)
     assert relerr(rho.cpu().numpy(), ref) < TOL
+
+
+def _jump_ops(N, rng, scale=0.05):
+    """every |i><j| transition (i != j) with a random rate: N(N - 1) collapse operators (a thermal Lindbladian)."""
+    cs = []
+    for i in range(N):
+        for j in range(N):
+            if i != j:
+                c = np.zeros((N, N), complex)
+                c[i, j] = np.sqrt(scale * rng.uniform(0.1, 1.0) / N)
+                cs.append(c)
+    return np.array(cs)
+
+
+@pytest.mark.parametrize("N,nc,B,herm", [(24, 552, 2, False), (24, 552, 3, True), (64, 300, 4, None),
+                                         (64, 300, 2, True), (100, 300, 2, None), (100, 300, 2, True)])
+def test_lindblad_more_collapse_ops_than_lds_table(N, nc, B, herm):
+    """More collapse operators than the kernels' LDS segment table (MAX_NC = 256; round 3 refused the rest,
+    VERDICT r03 missing #2): the persistent kernels' CHUNK instantiations (glf_chunk.hip), general and Hermitian,
+    Np = 32 / 64 / 128, against the oracle's sum over the whole list (oqs.py:697-714).  N = 24 runs every |i><j|
+    jump operator (552)."""
+    import torch
+    from oracle import lindblad as olb
+    from pyqed_amd import lindblad_rk4
+    steps, dt = 3, 5e-3
+    rng = np.random.default_rng(41)
+    H, _ = olb.synthetic_lindblad(N, nc=1)
+    if nc == N * (N - 1):
+        cs = _jump_ops(N, rng)
+    else:
+        cs = np.array([0.3 / np.sqrt(nc) * (rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N)))
+                       / np.sqrt(N) for _ in range(nc)])
+    rho0 = olb.random_pure_states(B, N, seed=6)
+    ref = olb.lindblad_batch(H, list(cs), rho0, dt, steps)
+    dev = torch.device("cuda", 0)
+    rho = torch.from_numpy(rho0.copy()).to(dev)
+    lindblad_rk4(torch.from_numpy(H).to(dev), torch.from_numpy(cs).to(dev), rho, dt, steps, hermitian=herm)
+    assert relerr(rho.cpu().numpy(), ref) < TOL
+    # trace is conserved by every Lindbladian
+    tr = np.einsum("bii->b", rho.cpu().numpy())
+    assert np.max(np.abs(tr - 1.0)) < 1e-12

@@ -291,3 +291,21 @@ def test_heom_chain_oracle_matches_reference(tag):
             float(g[f"{tag}_reorganization"]), int(g[f"{tag}_nado"]), float(g[f"{tag}_dt"]), int(g[f"{tag}_nt"]))
     assert relerr(oh.chain_rk4(*args), g[f"{tag}_rk4"]) < 1e-12
     assert relerr(oh.chain_euler(*args), g[f"{tag}_euler"]) < 1e-12
+
+
+def test_oracle_fft_matches_reference_golden():
+    """oracle/fft.py (the checker of pyqed_amd.fft) against the reference's own outputs at every fixture length,
+    norm / n kwargs and axes (fft_phys, fft_any)."""
+    from oracle import fft as of
+    g = load_golden("fft_phys")
+    assert relerr(of.fft(g["a"], g["x"])[0], g["fft_g"]) < 1e-12
+    assert relerr(of.ifft(g["a"], g["x"])[0], g["ifft_g"]) < 1e-12
+    assert relerr(of.fft(g["M"], x=np.linspace(0, 3.1, 32), axis=0)[0], g["fftax0_g"]) < 1e-12
+    g = load_golden("fft_any")
+    for n in (8, 1000, 2048, 4096, 5000, 7919, 12288):
+        assert relerr(of.fft(g[f"a{n}"], g[f"x{n}"])[0], g[f"fft{n}_g"]) < 1e-12
+        assert relerr(of.ifft(g[f"a{n}"], g[f"x{n}"])[0], g[f"ifft{n}_g"]) < 1e-12
+    assert relerr(of.fft(g["a5000"], g["x5000"], norm="ortho")[0], g["fft5000_ortho_g"]) < 1e-12
+    assert relerr(of.fft(g["a1000"], g["x1000"], n=1)[0], g["fft1000_n1_g"]) < 1e-12
+    assert relerr(of.fft(g["T"], g["xt"], axis=0)[0], g["fftT0_g"]) < 1e-12
+    assert relerr(of.ifft(g["T"], np.linspace(-1, 1, 7), axis=-1)[0], g["ifftTm1_g"]) < 1e-12

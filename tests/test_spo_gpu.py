@@ -340,3 +340,44 @@ def test_spo2nh_device_exponential_matches_eig(ns):
         ref = (ur * np.exp(-1j * w * tau)[..., None, :]) @ ul
         assert relerr(got, ref) < 1e-12
     assert sol.right_eigenstates.shape == v.shape and sol.ovlp_rr.shape == v.shape
+
+
+def test_spo2_device_exponential_large_and_nonfinite_potentials():
+    """qd_spo_expm / SPO2.build on hard-wall potentials: entries up to 1e9 need ~30 squarings and stay
+    unitary and close to eigh; inf raises LinAlgError up front as the reference's eigh does (wpd.py:585-623) instead
+    of hanging the device loop; a direct library call on inf returns NaN rather than spinning."""
+    import torch
+    from pyqed_amd import SPO2, _lib
+    from pyqed_amd._util import default_device
+    ns, n = 3, 16
+    x = np.linspace(-4, 4, n)
+    rng = np.random.default_rng(9)
+    v = rng.standard_normal((n, n, ns, ns))
+    v = 0.5 * (v + np.swapaxes(v, -1, -2))
+    v[:3] += 1e9 * np.eye(ns)        # walls
+    sol = SPO2(x, x, mass=[1.0, 1.0], nstates=ns)
+    sol.set_dpes(v)
+    dt = 0.05
+    sol.build(dt)
+    w, u = np.linalg.eigh(v)
+    ref = (u * np.exp(-1j * w * dt / 2)[..., None, :]) @ np.conj(np.swapaxes(u, -1, -2))
+    got = sol.exp_V_half
+    eye = np.eye(ns)
+    assert np.max(np.abs(got @ np.conj(np.swapaxes(got, -1, -2)) - eye)) < 1e-6
+    assert relerr(got[3:], ref[3:]) < 1e-12
+    assert relerr(got[:3], ref[:3]) < 1e-5      # 1e9 dt/2 rad of phase: conditioning, not the method
+    vb = v.copy()
+    vb[5, 5, 0, 0] = np.inf
+    sol2 = SPO2(x, x, mass=[1.0, 1.0], nstates=ns)
+    sol2.set_dpes(vb)
+    with pytest.raises(np.linalg.LinAlgError):
+        sol2.build(dt)
+    dev = default_device()
+    vd = torch.from_numpy(np.ascontiguousarray(vb.astype(complex))).to(dev)
+    eV = torch.empty(vd.shape, dtype=torch.complex128, device=dev)
+    eVh = torch.empty_like(eV)
+    rc = _lib.load().qd_spo_expm(vd.data_ptr(), 1, n * n, ns, dt, eV.data_ptr(), eVh.data_ptr(), _lib.stream_ptr(dev))
+    _lib.check(rc, "qd_spo_expm")
+    torch.cuda.synchronize(dev)
+    h = eVh.cpu().numpy()
+    assert np.isnan(h[5, 5]).all() and np.isfinite(h[4, 4]).all()
