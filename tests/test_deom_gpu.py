@@ -323,8 +323,8 @@ def test_deom_batched_w5_kernel_matches_oracle_and_unconstrained(B, monkeypatch)
     for w5 in ("1", "0"):
         monkeypatch.setenv("QD_DEOM_W5", w5)
         sol = DEOMSolver(sz + sx, None, bath, np.array([sx]), None, None, None, L)
-        assert sol.nind == 5
         _, saved = sol.run_batch(rho0, dt, nt)
+        assert sol.nind == 5
         out[w5] = (np.array(saved), sol.ddos.copy())
     assert np.array_equal(out["1"][0], out["0"][0]) and np.array_equal(out["1"][1], out["0"][1])
     for b in (0, B // 2, B - 1):
