@@ -5,6 +5,8 @@ output and finalised.  This runs only the 8-band loopback run (ShardedDEOM) and 
     python tools/band_exit_probe.py plain       return from main (normal exit)
     python tools/band_exit_probe.py shutdown    qd_shutdown() (trims libqdyn's stream-ordered memory pool) first
     python tools/band_exit_probe.py launches N  no DEOM: N tiny qd_gather_rows launches (dispatch-count probe)
+    python tools/band_exit_probe.py persist     DEOMSolver.run only (the persistent banded kernel, qd_deom_rk4_banded)
+    python tools/band_exit_probe.py both        DEOMSolver.run, then the 8-band loopback run
 """
 import os
 import sys
@@ -40,9 +42,13 @@ else:
     sol = DEOMSolver(sz + sx, None, bath, np.array([sx]), None, None, None, 12)
     r0 = np.zeros((2, 2), complex)
     r0[0, 0] = 1
-    sh = ShardedDEOM(sol, nbands=8, loopback=True, device=dev, exchange="allgather")
-    t, rs = sh.run(r0, 0.002, 40)
-    print("trace", float(np.trace(rs[-1]).real), flush=True)
+    if mode in ("persist", "both"):
+        _, rs = sol.run(r0.copy(), 0.002, 100)
+        print("persistent banded: trace", float(np.trace(rs[-1]).real), "banded", sol.last_run_banded, flush=True)
+    if mode != "persist":
+        sh = ShardedDEOM(sol, nbands=8, loopback=True, device=dev, exchange="allgather")
+        t, rs = sh.run(r0, 0.002, 40)
+        print("loopback: trace", float(np.trace(rs[-1]).real), flush=True)
 torch.cuda.synchronize(dev)
 if mode == "shutdown":
     _lib.check(_lib.load().qd_shutdown(), "qd_shutdown")
