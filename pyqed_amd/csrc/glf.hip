@@ -693,6 +693,37 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
     QD_HIP(hipGetLastError());
   }
 
+  // Few undriven matrices: one persistent launch with a workgroup per 16 x 16 output tile (glf_single.hip; the split
+  // path takes eight dependent launches per step).  A refused cooperative launch or a hand-off timeout re-runs the
+  // batch below from a saved copy.  QD_GLF_SINGLE=0 / 1 turns it off / keeps it on wherever it applies.
+  {
+    const char* sge = std::getenv("QD_GLF_SINGLE");
+    const bool forced_split = std::getenv("QD_GLF_SPLIT") != nullptr;   // A/B runs and tests of the split path
+    const bool single = !herm && !nd && B <= glf_single_max_batch(Np, nc) && !(sge && sge[0] == '0') &&
+                        !(forced_split && !(sge && sge[0] == '1'));
+    if (single) {
+      void* wsave = nullptr;
+      if ((rc = workspace(WS_MISC, (size_t)B * NN * sizeof(c128), &wsave, st))) return rc;
+      QD_HIP(hipMemcpyAsync(wsave, rho_p, (size_t)B * NN * sizeof(c128), hipMemcpyDeviceToDevice, st));
+      int timed_out = 0;
+      rc = glf_single_run(mK, iKd, Cop, Cd, nc, eT, ne, rho_p, B, N, Np, dt, nsteps, obs,
+                          save_every > 0 ? snap : nullptr, save_every, &timed_out, st);
+      if (rc == QD_OK && !timed_out) {
+        if (pad) {
+          const size_t tot = (size_t)B * N * N;
+          hipLaunchKernelGGL(unpad_kernel, dim3((int)std::min<size_t>((tot + threads - 1) / threads, 65535)),
+                             dim3(threads), 0, st, rho_p, rho, B, N, Np);
+          QD_HIP(hipGetLastError());
+        }
+        return QD_OK;
+      }
+      if (rc != QD_OK && rc != QD_EBUSY) return rc;
+      std::fprintf(stderr, "[libqdyn] glf single-trajectory launch %s; re-running on the split path\n",
+                   timed_out ? "timed out" : "refused");
+      QD_HIP(hipMemcpyAsync(rho_p, wsave, (size_t)B * NN * sizeof(c128), hipMemcpyDeviceToDevice, st));
+    }
+  }
+
   LindbladParams p;
   p.Cop = Cop;
   p.mK = mK;

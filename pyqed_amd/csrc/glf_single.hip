@@ -1,0 +1,361 @@
+// glf_single.hip — a few density matrices (one trajectory: LindbladSolver.run, oqs.py:1596-1696) as ONE persistent
+// launch.
+//
+// The batch kernels give one CU per density matrix, and the split path (glf.hip) spreads one matrix over many
+// workgroups but pays eight dependent launches per RK4 step, each a chain of operand-load / slab / ticket round trips
+// (~10 us per launch, 12.3k steps/s at N = 128).  Here every 16 x 16 output tile of every matrix is a workgroup
+// (T = Np / 16, T^2 workgroups per matrix, B T^2 <= 256) that lives for the whole run:
+//   - its slices of the constant operators (P rows, Q columns, L_c rows, R_c columns of the GLF form
+//     d rho/dt = P rho + rho Q + sum_c L_c rho R_c) are loaded ONCE into registers in the MFMA fragment layout;
+//   - its tile of rho stays in registers (threads 0..255, one element each);
+//   - the 8 waves split K = Np into 8 chunks (KS k-steps of 4 each) and the partial tiles are summed in LDS in the
+//     fixed wave order (deterministic);
+//   - per RK4 stage two hand-offs inside the launch: Y_c(bm, bn) = L_c[bm, :] r[:, bn] is published, then
+//     k(bm, bn) = P[bm, :] r[:, bn] + r[bm, :] Q[:, bn] + sum_c Y_c[bm, :] R_c[:, bn] needs the Y_c row block bm;
+//     the Horner update s' = rho + dt / (4 - m) k (glf.hip header) is published as the next stage input, whose row
+//     block bm and column block bn the next stage reads.
+// Hand-off form (MI355X_MICROARCH.md "Valid forms", table row 1, as deom.hip's banded kernel): 16-B write-through
+// (sc1) buffer stores of the payload, every wave drains (s_waitcnt vmcnt(0)), workgroup barrier, one lane stores the
+// epoch (relaxed agent atomic); consumers poll the producers' epochs with relaxed agent loads from one wave and load
+// the payload with 16-B sc1 buffer loads only (never a plain or flat load of handed-off bytes).
+// Buffer reuse: stage outputs and Y_c alternate between two buffers.  A workgroup overwrites r_{g-1} (buffer
+// (g+1) & 1) at the end of stage g only after it has seen stage g's Y_c of every workgroup of its row and stage g's
+// input from every workgroup of its row and column, i.e. after every reader of its r_{g-1} tile (the workgroups of
+// its row and column) finished stage g - 1; likewise Y_{g-2} (buffer g & 1) is overwritten in stage g after every
+// reader of it (its row) published stage g - 1's output, seen at the start of stage g.  Every spin is bounded; a
+// timeout sets *status (the host re-runs the batch on the split path).
+// Observables: each workgroup sums Tr(E rho) over its tile after every step into a partial slot, and one small
+// kernel adds the T^2 partials in fixed order after the launch.
+#include "glf_kernel.hpp"
+
+namespace qd {
+namespace {
+
+constexpr int SG_WG = 512;
+constexpr int SG_FLAG_STRIDE = 16;              // 64-B epoch slots
+constexpr unsigned SG_SPIN_LIMIT = 1u << 22;    // polls (one round trip each, s_sleep between): ~2 s
+
+struct SingleParams {
+  const c128* P;       // [Np][Np] padded GLF operators (glf_run's operator workspace)
+  const c128* Q;
+  const c128* Lop;     // [nc][Np][Np]
+  const c128* Rop;     // [nc][Np][Np]
+  const c128* eT;      // [ne][Np][Np] E_m^T
+  c128* rho;           // [B][Np][Np] state (in / out)
+  c128* rbuf;          // [2][B][Np][Np] stage outputs
+  c128* ybuf;          // [2][nc][B][Np][Np]
+  unsigned* flags;     // [B T^2][2][SG_FLAG_STRIDE]: 0 = stage output epoch, 1 = Y epoch
+  c128* obs_part;      // [B][total_steps + 1][ne][T^2]
+  c128* snap;          // [B][nsave][N][N] or null
+  int* status;
+  int N, ne, nsteps, step0, total_steps, save_every, nsave;
+  double dt;
+};
+
+typedef unsigned int sg_u4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ c128 sg_ld(__amdgpu_buffer_rsrc_t r, int off) {   // 16-B sc1 load
+  const sg_u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
+  return cmk(__builtin_bit_cast(double, (unsigned long long)v.x | ((unsigned long long)v.y << 32)),
+             __builtin_bit_cast(double, (unsigned long long)v.z | ((unsigned long long)v.w << 32)));
+}
+__device__ __forceinline__ void sg_st(__amdgpu_buffer_rsrc_t r, int off, c128 x) {   // 16-B write-through store
+  const unsigned long long a = __builtin_bit_cast(unsigned long long, x.re);
+  const unsigned long long c = __builtin_bit_cast(unsigned long long, x.im);
+  const sg_u4 v = {(unsigned)a, (unsigned)(a >> 32), (unsigned)c, (unsigned)(c >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
+}
+__device__ __forceinline__ void* sg_uni(const void* q) {   // provably wave-uniform pointer for a buffer descriptor
+  const unsigned long long v = (unsigned long long)q;
+  const unsigned l = __builtin_amdgcn_readfirstlane((unsigned)v), h = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return (void*)(((unsigned long long)h << 32) | l);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sg_rsrc(const void* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(sg_uni(base), (short)0, bytes, 0x00020000);
+}
+
+// one complex k-step of a 16 x 16 tile: acc += a b (a: A fragment, b: B fragment of v_mfma_f64_16x16x4_f64)
+__device__ __forceinline__ void sg_mac(d4& re, d4& im, c128 a, c128 b) {
+  re = __builtin_amdgcn_mfma_f64_16x16x4f64(a.re, b.re, re, 0, 0, 0);
+  im = __builtin_amdgcn_mfma_f64_16x16x4f64(a.re, b.im, im, 0, 0, 0);
+  re = __builtin_amdgcn_mfma_f64_16x16x4f64(-a.im, b.im, re, 0, 0, 0);
+  im = __builtin_amdgcn_mfma_f64_16x16x4f64(a.im, b.re, im, 0, 0, 0);
+}
+
+// KS: k-steps of 4 per wave (Np = 32 KS), NC collapse operators / GLF pairs
+template <int KS, int NC>
+__global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
+  constexpr int T = 2 * KS, Np = 32 * KS, NN = Np * Np;
+  __shared__ c128 red[8][256];
+  __shared__ int sAbort;
+  const int w = blockIdx.x, b = w / (T * T), tile = w - b * (T * T), bm = tile / T, bn = tile - bm * T;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lk = lane >> 4;
+  const int kb = wave * 4 * KS;
+  // constant operator fragments, loaded once: A rows bm (P, L_c), B columns bn (Q, R_c)
+  c128 aP[KS], bQ[KS], aL[NC > 0 ? NC : 1][KS], bR[NC > 0 ? NC : 1][KS];
+#pragma unroll
+  for (int q = 0; q < KS; ++q) {
+    const int k = kb + 4 * q + lk;
+    aP[q] = p.P[(bm * 16 + lr) * Np + k];
+    bQ[q] = p.Q[k * Np + bn * 16 + lr];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      aL[c][q] = p.Lop[(size_t)c * NN + (bm * 16 + lr) * Np + k];
+      bR[c][q] = p.Rop[(size_t)c * NN + k * Np + bn * 16 + lr];
+    }
+  }
+  const bool owner = tid < 256;
+  const int orow = bm * 16 + ((tid >> 4) & 15), ocol = bn * 16 + (tid & 15);
+  c128* rhob = p.rho + (size_t)b * NN;
+  c128 rh = owner ? rhob[orow * Np + ocol] : cmk(0, 0);
+  if (tid == 0) sAbort = 0;
+  const int mats = gridDim.x / (T * T);
+  const int slab = mats * NN * (int)sizeof(c128);   // bytes of one [B][Np][Np] buffer
+  unsigned* fl = p.flags;
+  auto flag_at = [&](int wg, int kind) { return fl + ((size_t)wg * 2 + kind) * SG_FLAG_STRIDE; };
+
+  // Tr(E_m rho) partial over this tile -> obs_part (fixed-order sums: lanes of a wave, then the 4 owner waves)
+  auto observe = [&](int gs) {
+    for (int m = 0; m < p.ne; ++m) {
+      c128 v = cmk(0, 0);
+      if (owner) v = cmul(rh, p.eT[(size_t)m * NN + orow * Np + ocol]);
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        v.re += __shfl_xor(v.re, off, 64);
+        v.im += __shfl_xor(v.im, off, 64);
+      }
+      __syncthreads();
+      if (lane == 0) red[0][wave] = v;
+      __syncthreads();
+      if (tid == 0) {
+        c128 s = red[0][0];
+        for (int q = 1; q < 4; ++q) s = cadd(s, red[0][q]);
+        p.obs_part[(((size_t)b * (p.total_steps + 1) + gs) * p.ne + m) * (T * T) + tile] = s;
+      }
+    }
+  };
+  if (p.ne > 0 && p.step0 == 0) observe(0);
+
+  // fixed-order sum of the 8 waves' partial tiles; returns element tid (tid < 256) of the tile
+  auto reduce = [&](const d4& re, const d4& im) -> c128 {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wave][(lk + 4 * r) * 16 + lr] = cmk(re[r], im[r]);
+    __syncthreads();
+    c128 v = cmk(0, 0);
+    if (owner) {
+      v = red[0][tid];
+#pragma unroll
+      for (int q = 1; q < 8; ++q) v = cadd(v, red[q][tid]);
+    }
+    return v;
+  };
+  // wave 0 waits until every listed workgroup's epoch word `kind` reaches `target`; the other waves wait at the barrier
+  auto wait_for = [&](int nsrc, int kind, unsigned target, auto&& src_of) {
+    if (wave == 0) {
+      const unsigned* f = lane < nsrc ? flag_at(src_of(lane), kind) : nullptr;
+      unsigned spins = 0;
+      for (;;) {
+        const bool ok = !f || __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target;
+        if (__all(ok)) break;
+        ++spins;
+        if (spins > SG_SPIN_LIMIT ||
+            ((spins & 255) == 0 && __hip_atomic_load(p.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
+          if (lane == 0) {
+            sAbort = 1;
+            __hip_atomic_store(p.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the payload loads below the poll
+    __syncthreads();
+    return sAbort == 0;
+  };
+  auto publish = [&](int kind, unsigned epoch) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's write-through stores are complete
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(flag_at(w, kind), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+
+  const int G4 = 4 * p.nsteps;
+  for (int g = 0; g < G4; ++g) {
+    const int s = g >> 2, m = g & 3;
+    // ---- stage input r_g: the caller's rho at g = 0, else the previous stage's output in rbuf[g & 1]
+    const c128* rin = g == 0 ? p.rho : p.rbuf + (size_t)(g & 1) * mats * NN;
+    if (g > 0 && !wait_for(2 * T, 0, (unsigned)g, [&](int l) {   // column bn and row bm of r_g
+          return b * T * T + (l < T ? l * T + bn : bm * T + (l - T));
+        }))
+      break;
+    const __amdgpu_buffer_rsrc_t rr = sg_rsrc(rin, slab);
+    c128 rcol[KS], rrow[KS];
+#pragma unroll
+    for (int q = 0; q < KS; ++q) {
+      const int k = kb + 4 * q + lk;
+      rcol[q] = sg_ld(rr, ((b * Np + k) * Np + bn * 16 + lr) * 16);
+      rrow[q] = sg_ld(rr, ((b * Np + bm * 16 + lr) * Np + k) * 16);
+    }
+    // ---- Y_c(bm, bn) = L_c[bm, :] r[:, bn], published for the k phase of the row
+    c128* ybase = p.ybuf + (size_t)(g & 1) * NC * mats * NN;
+    if constexpr (NC > 0) {
+      const __amdgpu_buffer_rsrc_t ry = sg_rsrc(ybase, NC * slab);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        d4 re = {0, 0, 0, 0}, im = {0, 0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < KS; ++q) sg_mac(re, im, aL[c][q], rcol[q]);
+        const c128 y = reduce(re, im);
+        if (owner) sg_st(ry, (((c * mats + b) * Np + orow) * Np + ocol) * 16, y);
+        __syncthreads();   // red is reused by the next reduction
+      }
+      publish(1, (unsigned)(g + 1));
+    }
+    // ---- k(bm, bn) = P r + r Q + sum_c Y_c R_c; the P r + r Q part runs while the row's Y_c are handed over
+    d4 re = {0, 0, 0, 0}, im = {0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < KS; ++q) sg_mac(re, im, aP[q], rcol[q]);
+#pragma unroll
+    for (int q = 0; q < KS; ++q) sg_mac(re, im, rrow[q], bQ[q]);
+    if constexpr (NC > 0) {
+      if (!wait_for(T, 1, (unsigned)(g + 1), [&](int l) { return b * T * T + bm * T + l; })) break;
+      const __amdgpu_buffer_rsrc_t ry = sg_rsrc(ybase, NC * slab);
+      c128 yrow[NC][KS];
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int q = 0; q < KS; ++q)
+          yrow[c][q] = sg_ld(ry, (((c * mats + b) * Np + bm * 16 + lr) * Np + kb + 4 * q + lk) * 16);
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int q = 0; q < KS; ++q) sg_mac(re, im, yrow[c][q], bR[c][q]);
+    }
+    const c128 kv = reduce(re, im);
+    const double hc = rk4_horner_coef(p.dt, m);
+    const c128 v = cadd(rh, cscale(kv, hc));
+    if (m == 3) rh = v;
+    if (owner && g + 1 < G4) sg_st(sg_rsrc(p.rbuf + (size_t)((g + 1) & 1) * mats * NN, slab),
+                                   ((b * Np + orow) * Np + ocol) * 16, v);
+    if (m == 3) {
+      const int gs = p.step0 + s + 1;
+      if (p.snap && p.save_every > 0 && gs % p.save_every == 0) {
+        const int si = gs / p.save_every - 1;
+        if (owner && si < p.nsave && orow < p.N && ocol < p.N)
+          p.snap[(((size_t)b * p.nsave + si) * p.N + orow) * p.N + ocol] = v;
+      }
+      if (p.ne > 0) observe(gs);
+    }
+    if (g + 1 < G4) publish(0, (unsigned)(g + 1));
+    else __syncthreads();
+  }
+  if (owner) rhob[orow * Np + ocol] = rh;
+}
+
+// obs[b][gs][m] = sum over the T^2 tiles of obs_part, fixed order
+__global__ void glf_single_obs_kernel(const c128* part, int T2, long n, c128* obs) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const c128* s = part + e * T2;
+    c128 v = s[0];
+    for (int q = 1; q < T2; ++q) v = cadd(v, s[q]);
+    obs[e] = v;
+  }
+}
+
+template <int KS, int NC>
+hipError_t sg_launch(SingleParams p, int grid, bool coop, hipStream_t st) {
+  if (!coop) {
+    hipLaunchKernelGGL((glf_single_kernel<KS, NC>), dim3(grid), dim3(SG_WG), 0, st, p);
+    return hipGetLastError();
+  }
+  void* args[] = {(void*)&p};
+  return hipLaunchCooperativeKernel((const void*)glf_single_kernel<KS, NC>, dim3(grid), dim3(SG_WG), args, 0, st);
+}
+
+}  // namespace
+
+int glf_single_max_batch(int Np, int nc) {
+  if (nc > 2 || (Np != 32 && Np != 64 && Np != 128)) return 0;
+  const int T = Np / 16;
+  return 256 / (T * T);
+}
+
+// One persistent launch for B matrices (B <= glf_single_max_batch), undriven GLF operators already padded.  Returns
+// QD_OK with *timed_out = 1 if a hand-off spin expired (the state is then invalid: the caller re-runs it), QD_EBUSY
+// when the cooperative launch is refused (nothing ran).
+int glf_single_run(const c128* P, const c128* Q, const c128* Lop, const c128* Rop, int nc, const c128* eT, int ne,
+                   c128* rho, int B, int N, int Np, double dt, int nsteps, c128* obs, c128* snap, int save_every,
+                   int* timed_out, hipStream_t st) {
+  *timed_out = 0;
+  if (nsteps <= 0 && ne == 0) return QD_OK;
+  const int T = Np / 16, T2 = T * T;
+  const size_t NN = (size_t)Np * Np;
+  const size_t flag_bytes = ((size_t)B * T2 * 2 * SG_FLAG_STRIDE + 4) * sizeof(unsigned);
+  const size_t obs_elems = ne ? (size_t)B * (nsteps + 1) * ne * T2 : 0;
+  const size_t elems = 2 * (size_t)B * NN + 2 * (size_t)(nc > 0 ? nc : 0) * B * NN + obs_elems;
+  void* w = nullptr;
+  int rc = workspace(WS_LINDBLAD, elems * sizeof(c128) + flag_bytes, &w, st);
+  if (rc) return rc;
+  SingleParams p;
+  p.P = P;
+  p.Q = Q;
+  p.Lop = Lop;
+  p.Rop = Rop;
+  p.eT = eT;
+  p.rho = rho;
+  p.rbuf = (c128*)w;
+  p.ybuf = p.rbuf + 2 * (size_t)B * NN;
+  p.obs_part = ne ? p.ybuf + 2 * (size_t)nc * B * NN : nullptr;
+  p.flags = (unsigned*)((c128*)w + elems);
+  p.status = (int*)(p.flags + (size_t)B * T2 * 2 * SG_FLAG_STRIDE);
+  p.N = N;
+  p.ne = ne;
+  p.nsteps = nsteps;
+  p.step0 = 0;
+  p.total_steps = nsteps;
+  p.save_every = save_every;
+  p.nsave = save_every > 0 ? nsteps / save_every : 0;
+  p.snap = p.nsave > 0 ? snap : nullptr;
+  p.dt = dt;
+  QD_HIP(hipMemsetAsync(p.flags, 0, flag_bytes, st));
+  const char* ce = getenv("QD_GLF_SINGLE_COOP");
+  const bool coop = !(ce && ce[0] == '0');
+  const int grid = B * T2;
+  hipError_t e = hipErrorInvalidValue;
+#define SG_CASE(KS_)                                                    \
+  switch (nc) {                                                         \
+    case 0: e = sg_launch<KS_, 0>(p, grid, coop, st); break;            \
+    case 1: e = sg_launch<KS_, 1>(p, grid, coop, st); break;            \
+    default: e = sg_launch<KS_, 2>(p, grid, coop, st); break;           \
+  }
+  switch (Np) {
+    case 32: SG_CASE(1) break;
+    case 64: SG_CASE(2) break;
+    default: SG_CASE(4) break;
+  }
+#undef SG_CASE
+  if (e == hipErrorCooperativeLaunchTooLarge) {
+    (void)hipGetLastError();
+    set_error("glf single-trajectory launch: %d workgroups cannot be co-resident", grid);
+    return QD_EBUSY;
+  }
+  QD_HIP(e);
+  if (const char* fe = getenv("QD_GLF_SINGLE_FAKE_TIMEOUT"))   // tests: report a hand-off timeout after the run
+    if (fe[0] == '1') QD_HIP(hipMemsetAsync(p.status, 1, 1, st));
+  int h = 0;
+  QD_HIP(hipMemcpyAsync(&h, p.status, sizeof(int), hipMemcpyDeviceToHost, st));
+  QD_HIP(hipStreamSynchronize(st));
+  if (h) {
+    *timed_out = 1;
+    return QD_OK;
+  }
+  if (ne) {
+    const long n = (long)B * (nsteps + 1) * ne;
+    hipLaunchKernelGGL(glf_single_obs_kernel, dim3((int)std::min<long>((n + 255) / 256, 1024)), dim3(256), 0, st,
+                       (const c128*)p.obs_part, T2, n, obs);
+    QD_HIP(hipGetLastError());
+  }
+  return QD_OK;
+}
+
+}  // namespace qd

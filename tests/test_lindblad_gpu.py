@@ -462,3 +462,60 @@ def test_lindblad_np64_hermitian_dispatch_matches_oracle(N, B):
     rho = torch.from_numpy(rho0.copy()).to(dev)
     lindblad_rk4(torch.from_numpy(H).to(dev), torch.from_numpy(np.array(cs)).to(dev), rho, 1e-2, 5)
     assert relerr(rho.cpu().numpy()[:3], ref) < TOL
+
+
+@pytest.mark.parametrize("N,nc,B", [(128, 1, 1), (128, 2, 1), (100, 1, 4), (64, 1, 3), (40, 2, 2), (20, 0, 5),
+                                    (32, 1, 64)])
+def test_lindblad_single_launch_matches_split_path_and_oracle(N, nc, B, monkeypatch):
+    """Few density matrices as ONE persistent launch (glf_single.hip: a workgroup per 16 x 16 output tile, operator
+    fragments in registers, Y_c and stage outputs handed over inside the launch): final state, observables after every
+    step and snapshots against the split path (QD_GLF_SINGLE=0) and the oracle's RK4 (oqs.py:697-714, 1596-1696);
+    Np = 128 / 64 / 32, nc = 0 / 1 / 2, up to the 256-workgroup cap (B = 4 at Np = 128, 64 at Np = 32)."""
+    import torch
+    from oracle import lindblad as olb
+    from pyqed_amd import lindblad_rk4
+    H, cs = olb.synthetic_lindblad(N, nc=max(nc, 1))
+    cs = cs[:nc]
+    rho0 = olb.random_pure_states(B, N, seed=9)
+    E = np.array([np.diag(np.arange(N, dtype=float)).astype(complex), H])
+    steps, dt = 7, 1e-2
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    Ct = t(np.array(cs)) if nc else None
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("QD_GLF_SINGLE", mode)
+        rho = t(rho0.copy())
+        obs, snap = lindblad_rk4(t(H), Ct, rho, dt, steps, t(E), save_every=1, hermitian=False)
+        torch.cuda.synchronize()
+        out[mode] = (rho.cpu().numpy(), obs.cpu().numpy(), snap.cpu().numpy())
+    ref = olb.lindblad_batch(H, cs, rho0, dt, steps)
+    assert relerr(out["1"][0], ref) < TOL
+    for a, b in zip(out["1"], out["0"]):
+        assert relerr(a, b) < 1e-12
+    assert relerr(out["1"][2][:, -1], out["1"][0]) == 0.0
+    obs_ref = np.einsum("bij,mji->bm", rho0, E)
+    assert relerr(out["1"][1][:, 0], obs_ref) < 1e-13
+
+
+def test_lindblad_single_launch_timeout_falls_back(monkeypatch, capfd):
+    """A hand-off timeout of the single-trajectory launch (forced after a real run by QD_GLF_SINGLE_FAKE_TIMEOUT) makes
+    libqdyn restore the initial state and re-run on the split path: same result as the split path."""
+    import torch
+    from oracle import lindblad as olb
+    from pyqed_amd import lindblad_rk4
+    N, steps, dt = 128, 4, 1e-2
+    H, cs = olb.synthetic_lindblad(N, nc=1)
+    rho0 = olb.random_pure_states(1, N, seed=4)
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    monkeypatch.setenv("QD_GLF_SINGLE", "0")
+    r_split = t(rho0.copy())
+    lindblad_rk4(t(H), t(np.array(cs)), r_split, dt, steps, hermitian=False)
+    monkeypatch.setenv("QD_GLF_SINGLE", "1")
+    monkeypatch.setenv("QD_GLF_SINGLE_FAKE_TIMEOUT", "1")
+    r = t(rho0.copy())
+    lindblad_rk4(t(H), t(np.array(cs)), r, dt, steps, hermitian=False)
+    torch.cuda.synchronize()
+    assert "timed out" in capfd.readouterr().err
+    assert torch.equal(r, r_split)
