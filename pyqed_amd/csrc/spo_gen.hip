@@ -86,6 +86,9 @@ struct AxisArgs {
   int O, L, I, C, G, flags, ns;
   FDiv dLC, dC, dLns, dns;   // L C, C, L ns, ns
   int twl;             // 1: twiddles staged in LDS (M more c128 of dynamic LDS)
+  int aux;             // operators staged in LDS with the tile (one load round trip per pass): 1 = U1 (and U2 when it
+                       // differs) rows [G][L][ns][ns]; 2 = the tile's exp_K / N factors [L][C]; 0 = read from HBM/L2
+  int u2same;          // U2 == U1 (the Strang row pass applies exp(-i V dt/2) twice)
   const c128* U1;      // [points][ns][ns] (F_PT1)
   const c128* U2;      // (F_PT2)
   c128* snap;          // (F_SNAP) same layout as psi
@@ -245,6 +248,22 @@ __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
   const int o0 = blockIdx.x * G, i0 = blockIdx.y * C;
   const int gv = min(G, a.O - o0), cv = min(C, I - i0);
   const int tot = G * L * C;
+  // operators of this tile, staged in LDS by the same load phase as the tile (no dependent HBM round trip later)
+  c128* aux = (a.twl ? oth + (size_t)nl * M + M : oth + (size_t)nl * M);
+  const int ns = a.ns, nsq = ns * ns;
+  const int nU = a.aux == 1 ? gv * L * nsq : 0;            // U1 rows of the tile's valid rows (contiguous)
+  const c128* U1 = a.aux == 1 ? aux : a.U1;
+  const c128* U2 = a.aux == 1 ? (a.u2same ? aux : aux + (size_t)G * L * nsq) : a.U2;
+  const int pts = I / ns;
+  for (int q = threadIdx.x; q < nU; q += blockDim.x) {
+    aux[q] = a.U1[(size_t)o0 * L * nsq + q];
+    if (!a.u2same && (a.flags & F_PT2)) aux[(size_t)G * L * nsq + q] = a.U2[(size_t)o0 * L * nsq + q];
+  }
+  if (a.aux == 2)
+    for (int q = threadIdx.x; q < L * C; q += blockDim.x) {
+      const int e = (int)fdiv((unsigned)q, a.dC), c = q - e * C;
+      aux[q] = c < cv ? a.K[(size_t)e * pts + (int)fdiv((unsigned)(i0 + c), a.dns)] : cmk(0.0, 0.0);
+    }
   for (int f = threadIdx.x; f < tot; f += blockDim.x) {
     const int g = (int)fdiv((unsigned)f, a.dLC), r = f - g * (L * C), e = (int)fdiv((unsigned)r, a.dC), c = r - e * C;
     cur[(g * C + c) * M + e] =
@@ -253,13 +272,13 @@ __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
   __syncthreads();
   if (a.flags & F_INV) lds_fft<true>(p, tw, cur, oth, nl);
   auto point_op = [&](const c128* U) {   // C == I == ns: line g * ns + s holds state s of row g
-    const int ns = a.ns;
     const int n = G * L * ns;
+    const int row0 = a.aux == 1 ? 0 : o0;   // staged rows start at the tile's first row
     for (int f = threadIdx.x; f < n; f += blockDim.x) {
       const int g = (int)fdiv((unsigned)f, a.dLns), r = f - g * (L * ns), e = (int)fdiv((unsigned)r, a.dns),
                 s = r - e * ns;
       if (g >= gv) continue;
-      const c128* u = U + (((size_t)(o0 + g) * L + e) * ns + s) * ns;
+      const c128* u = U + (((size_t)(row0 + g) * L + e) * ns + s) * ns;
       c128 acc = cmk(0.0, 0.0);
       for (int b = 0; b < ns; ++b) acc = cadd(acc, cmul(u[b], cur[(g * ns + b) * M + e]));
       oth[(g * ns + s) * M + e] = acc;
@@ -269,14 +288,14 @@ __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
     cur = oth;
     oth = t;
   };
-  if (a.flags & F_PT1) point_op(a.U1);
+  if (a.flags & F_PT1) point_op(U1);
   if (a.flags & F_SNAP) {
     for (int f = threadIdx.x; f < tot; f += blockDim.x) {
       const int g = (int)fdiv((unsigned)f, a.dLC), r = f - g * (L * C), e = (int)fdiv((unsigned)r, a.dC), c = r - e * C;
       if (g < gv && c < cv) a.snap[((size_t)(o0 + g) * L + e) * I + i0 + c] = cur[(g * C + c) * M + e];
     }
   }
-  if (a.flags & F_PT2) point_op(a.U2);
+  if (a.flags & F_PT2) point_op(U2);
   if (a.flags & F_FWD) lds_fft<false>(p, tw, cur, oth, nl);
   if (a.flags & F_KY) {
     for (int f = threadIdx.x; f < tot; f += blockDim.x) {
@@ -287,10 +306,11 @@ __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
   }
   if (a.flags & F_KMUL) {   // outermost axis (O == 1): FFT -> * exp_K / N -> IFFT
     lds_fft<false>(p, tw, cur, oth, nl);
-    const int pts = I / a.ns;
     for (int f = threadIdx.x; f < tot; f += blockDim.x) {
       const int r = f - (int)fdiv((unsigned)f, a.dLC) * (L * C), e = (int)fdiv((unsigned)r, a.dC), c = r - e * C;
-      if (c < cv) cur[c * M + e] = cmul(cur[c * M + e], a.K[(size_t)e * pts + (int)fdiv((unsigned)(i0 + c), a.dns)]);
+      if (c < cv)
+        cur[c * M + e] = cmul(cur[c * M + e], a.aux == 2 ? aux[e * C + c]
+                                                          : a.K[(size_t)e * pts + (int)fdiv((unsigned)(i0 + c), a.dns)]);
     }
     __syncthreads();
     lds_fft<true>(p, tw, cur, oth, nl);
@@ -746,6 +766,22 @@ struct Exec {
     size_t lds = (size_t)2 * G * C * f[d].M * sizeof(c128);
     a.twl = lds + (size_t)f[d].M * sizeof(c128) <= LDS_MAX;
     if (a.twl) lds += (size_t)f[d].M * sizeof(c128);
+    // stage the pass's operators with the tile when they fit (QD_SPO_AUX=0: read them from HBM/L2, A/B)
+    a.u2same = U1 == U2;
+    a.aux = 0;
+    const char* xe = getenv("QD_SPO_AUX");
+    if (!(xe && xe[0] == '0')) {
+      const size_t ub = (size_t)G * n[d] * ns * ns * sizeof(c128) * ((flags & F_PT2) && !a.u2same ? 2 : 1);
+      const size_t kb = (size_t)n[d] * C * sizeof(c128);
+      if ((flags & (F_PT1 | F_PT2)) && lds + ub <= LDS_MAX) {
+        a.aux = 1;
+        lds += ub;
+      } else if ((flags & F_KMUL) && lds + kb <= LDS_MAX) {
+        a.aux = 2;
+        lds += kb;
+      }
+    }
+    if ((flags & F_PT2) && !(flags & F_PT1) && a.aux == 1) a.aux = 0;   // (the staging loop keys on U1)
     (void)hipFuncSetAttribute((const void*)spo_axis_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
     hipLaunchKernelGGL(spo_axis_kernel, dim3((a.O + G - 1) / G, (a.I + C - 1) / C), dim3(256), lds, st, f[d], a);
     QD_HIP(hipGetLastError());

@@ -20,7 +20,7 @@ if [ "$PART" = stats ]; then
 else
   # a cooperative launch makes rocprofv3 --pmc segfault at process exit (profiles/r04/pmc_crash/SUMMARY.md): the
   # counter passes take the plain launch of the banded DEOM kernel (same kernel, same residency)
-  export QD_DEOM_BAND_COOP=0
+  export QD_DEOM_BAND_COOP=0 QD_GLF_SINGLE_COOP=0
   timeout -k 10 250 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu > $OUT/fetch.log 2>&1
   timeout -k 10 250 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu > $OUT/write.log 2>&1
   timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/gfetch -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu --general --no-2des --no-spo --no-deom --no-redfield > $OUT/gfetch.log 2>&1
