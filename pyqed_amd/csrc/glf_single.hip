@@ -82,8 +82,34 @@ __device__ __forceinline__ void sg_mac(d4& re, d4& im, c128 a, c128 b) {
   im = __builtin_amdgcn_mfma_f64_16x16x4f64(a.im, b.re, im, 0, 0, 0);
 }
 
-// KS: k-steps of 4 per wave (Np = 32 KS), NC collapse operators / GLF pairs
-template <int KS, int NC>
+// A 16 x 16 complex accumulator.  M3 = false: 4 real MFMAs per complex k-step (re += ar br - ai bi, im += ar bi + ai br).
+// M3 = true: the 3-product form, P1 += ar br, P2 += ai bi, P3 += (ar + ai)(br + bi), re = P1 - P2, im = P3 - P1 - P2
+// (3 MFMAs per k-step; the two operand sums are VALU adds beside the MFMAs; one accumulator set more).
+template <bool M3>
+struct SgAcc {
+  d4 a0 = {0, 0, 0, 0}, a1 = {0, 0, 0, 0}, a2 = {0, 0, 0, 0};
+  __device__ __forceinline__ void mac(c128 a, c128 b) {
+    if constexpr (M3) {
+      a0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a.re, b.re, a0, 0, 0, 0);
+      a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a.im, b.im, a1, 0, 0, 0);
+      a2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a.re + a.im, b.re + b.im, a2, 0, 0, 0);
+    } else {
+      sg_mac(a0, a1, a, b);
+    }
+  }
+  __device__ __forceinline__ void result(d4& re, d4& im) const {
+    if constexpr (M3) {
+      re = a0 - a1;
+      im = a2 - a0 - a1;
+    } else {
+      re = a0;
+      im = a1;
+    }
+  }
+};
+
+// KS: k-steps of 4 per wave (Np = 32 KS), NC collapse operators / GLF pairs, M3: SgAcc form
+template <int KS, int NC, bool M3>
 __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
   constexpr int T = 2 * KS, Np = 32 * KS, NN = Np * Np;
   __shared__ c128 red[8][256];
@@ -137,7 +163,9 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
   if (p.ne > 0 && p.step0 == 0) observe(0);
 
   // fixed-order sum of the 8 waves' partial tiles; returns element tid (tid < 256) of the tile
-  auto reduce = [&](const d4& re, const d4& im) -> c128 {
+  auto reduce = [&](const SgAcc<M3>& acc) -> c128 {
+    d4 re, im;
+    acc.result(re, im);
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[wave][(lk + 4 * r) * 16 + lr] = cmk(re[r], im[r]);
     __syncthreads();
@@ -202,21 +230,21 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
       const __amdgpu_buffer_rsrc_t ry = sg_rsrc(ybase, NC * slab);
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        d4 re = {0, 0, 0, 0}, im = {0, 0, 0, 0};
+        SgAcc<M3> acc;
 #pragma unroll
-        for (int q = 0; q < KS; ++q) sg_mac(re, im, aL[c][q], rcol[q]);
-        const c128 y = reduce(re, im);
+        for (int q = 0; q < KS; ++q) acc.mac(aL[c][q], rcol[q]);
+        const c128 y = reduce(acc);
         if (owner) sg_st(ry, (((c * mats + b) * Np + orow) * Np + ocol) * 16, y);
         __syncthreads();   // red is reused by the next reduction
       }
       publish(1, (unsigned)(g + 1));
     }
     // ---- k(bm, bn) = P r + r Q + sum_c Y_c R_c; the P r + r Q part runs while the row's Y_c are handed over
-    d4 re = {0, 0, 0, 0}, im = {0, 0, 0, 0};
+    SgAcc<M3> acc;
 #pragma unroll
-    for (int q = 0; q < KS; ++q) sg_mac(re, im, aP[q], rcol[q]);
+    for (int q = 0; q < KS; ++q) acc.mac(aP[q], rcol[q]);
 #pragma unroll
-    for (int q = 0; q < KS; ++q) sg_mac(re, im, rrow[q], bQ[q]);
+    for (int q = 0; q < KS; ++q) acc.mac(rrow[q], bQ[q]);
     if constexpr (NC > 0) {
       if (!wait_for(T, 1, (unsigned)(g + 1), [&](int l) { return b * T * T + bm * T + l; })) break;
       const __amdgpu_buffer_rsrc_t ry = sg_rsrc(ybase, NC * slab);
@@ -229,9 +257,9 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
 #pragma unroll
       for (int c = 0; c < NC; ++c)
 #pragma unroll
-        for (int q = 0; q < KS; ++q) sg_mac(re, im, yrow[c][q], bR[c][q]);
+        for (int q = 0; q < KS; ++q) acc.mac(yrow[c][q], bR[c][q]);
     }
-    const c128 kv = reduce(re, im);
+    const c128 kv = reduce(acc);
     const double hc = rk4_horner_coef(p.dt, m);
     const c128 v = cadd(rh, cscale(kv, hc));
     if (m == 3) rh = v;
@@ -262,14 +290,21 @@ __global__ void glf_single_obs_kernel(const c128* part, int T2, long n, c128* ob
   }
 }
 
-template <int KS, int NC>
-hipError_t sg_launch(SingleParams p, int grid, bool coop, hipStream_t st) {
+template <int KS, int NC, bool M3>
+hipError_t sg_launch3(SingleParams p, int grid, bool coop, hipStream_t st) {
   if (!coop) {
-    hipLaunchKernelGGL((glf_single_kernel<KS, NC>), dim3(grid), dim3(SG_WG), 0, st, p);
+    hipLaunchKernelGGL((glf_single_kernel<KS, NC, M3>), dim3(grid), dim3(SG_WG), 0, st, p);
     return hipGetLastError();
   }
   void* args[] = {(void*)&p};
-  return hipLaunchCooperativeKernel((const void*)glf_single_kernel<KS, NC>, dim3(grid), dim3(SG_WG), args, 0, st);
+  return hipLaunchCooperativeKernel((const void*)glf_single_kernel<KS, NC, M3>, dim3(grid), dim3(SG_WG), args, 0, st);
+}
+// QD_GLF_SINGLE_3M=1: the 3-product complex MACs (A/B)
+template <int KS, int NC>
+hipError_t sg_launch(SingleParams p, int grid, bool coop, hipStream_t st) {
+  const char* me = getenv("QD_GLF_SINGLE_3M");
+  if (me && me[0] == '1') return sg_launch3<KS, NC, true>(p, grid, coop, st);
+  return sg_launch3<KS, NC, false>(p, grid, coop, st);
 }
 
 }  // namespace
