@@ -518,6 +518,8 @@ __global__ __launch_bounds__(256) void spo1d_gen_kernel(Fft p, c128* psi, const 
 template <bool CPLX>
 __global__ __launch_bounds__(1024) void spo_expm_kernel(const void* v_, int herm, long npts, int ns, double dt,
                                                         c128* expV, c128* expVh) {
+  // ns <= 50: four ns x ns matrices in LDS (160 KB at ns = 50); thread t owns elements t, t + blockDim, ... (one each up
+  // to ns = 32, where blockDim = ns^2 rounded up to 64)
   extern __shared__ c128 sm[];
   const int ns2 = ns * ns;
   c128* X = sm;
@@ -525,43 +527,55 @@ __global__ __launch_bounds__(1024) void spo_expm_kernel(const void* v_, int herm
   c128* S = T + ns2;
   c128* W = S + ns2;
   __shared__ int sh_s;
-  const int e = threadIdx.x;
-  const bool own = e < ns2;
-  const int i = own ? e / ns : 0, j = own ? e % ns : 0;
+  const int t0 = threadIdx.x, nt = blockDim.x;
   auto vat = [&](long p, int r, int c) {
     const size_t o = (size_t)p * ns2 + (size_t)r * ns + c;
     return CPLX ? ((const c128*)v_)[o] : cmk(((const double*)v_)[o], 0.0);
   };
   auto matmul = [&](const c128* A, const c128* B, c128* C, double scale) {   // C = scale A B
     __syncthreads();
-    c128 acc = cmk(0.0, 0.0);
-    if (own)
-      for (int l = 0; l < ns; ++l) acc = cadd(acc, cmul(A[i * ns + l], B[l * ns + j]));
+    constexpr int PER = 3;   // elements per thread: ceil(2500 / 1024)
+    c128 acc[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int e = t0 + q * nt;
+      acc[q] = cmk(0.0, 0.0);
+      if (e < ns2) {
+        const int i = e / ns, j = e - i * ns;
+        for (int l = 0; l < ns; ++l) acc[q] = cadd(acc[q], cmul(A[i * ns + l], B[l * ns + j]));
+      }
+    }
     __syncthreads();
-    if (own) C[e] = cscale(acc, scale);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int e = t0 + q * nt;
+      if (e < ns2) C[e] = cscale(acc[q], scale);
+    }
     __syncthreads();
   };
   for (long p = blockIdx.x; p < npts; p += gridDim.x) {
-    c128 h = cmk(0.0, 0.0);
-    if (own) {
+    // ||V tau||_inf (max row sum), tau = dt / 2; H (the matrix eigh / eig would see) staged in X
+    const double tau = 0.5 * dt;
+    for (int e = t0; e < ns2; e += nt) {
+      const int i = e / ns, j = e - i * ns;
+      c128 h;
       if (herm) {
         if (i == j) h = cmk(vat(p, i, i).re, 0.0);
         else h = i > j ? vat(p, i, j) : cconj(vat(p, j, i));
       } else {
         h = vat(p, i, j);
       }
+      X[e] = h;
+      W[e] = cmk(sqrt(h.re * h.re + h.im * h.im), 0.0);
     }
-    // ||V tau||_inf (max row sum), tau = dt / 2
-    const double tau = 0.5 * dt;
-    if (own) W[e] = cmk(sqrt(h.re * h.re + h.im * h.im), 0.0);
     __syncthreads();
-    if (e < ns) {
+    for (int e = t0; e < ns; e += nt) {
       double r = 0.0;
       for (int l = 0; l < ns; ++l) r += W[e * ns + l].re;
       T[e] = cmk(r, 0.0);
     }
     __syncthreads();
-    if (e == 0) {
+    if (t0 == 0) {
       double nrm = 0.0;
       for (int l = 0; l < ns; ++l) nrm = fmax(nrm, T[l].re);
       nrm *= fabs(tau);
@@ -578,38 +592,40 @@ __global__ __launch_bounds__(1024) void spo_expm_kernel(const void* v_, int herm
     }
     __syncthreads();
     const int sq = sh_s;
-    __syncthreads();
     if (sq < 0) {
       const c128 nan = cmk(__builtin_nan(""), __builtin_nan(""));
-      if (own) {
+      for (int e = t0; e < ns2; e += nt) {
         expVh[(size_t)p * ns2 + e] = nan;
         if (expV) expV[(size_t)p * ns2 + e] = nan;
       }
+      __syncthreads();
       continue;
     }
     const double sc = ldexp(tau, -sq);   // tau / 2^sq without an integer shift (sq may exceed 63)
     // X = -i V tau / 2^sq ; S = I + X ; T = X
-    if (own) {
-      X[e] = cmulmi(cscale(h, sc));
-      T[e] = X[e];
-      S[e] = cadd(X[e], cmk(i == j ? 1.0 : 0.0, 0.0));
+    for (int e = t0; e < ns2; e += nt) {
+      const int i = e / ns, j = e - i * ns;
+      const c128 x = cmulmi(cscale(X[e], sc));
+      X[e] = x;
+      T[e] = x;
+      S[e] = cadd(x, cmk(i == j ? 1.0 : 0.0, 0.0));
     }
     for (int k = 2; k <= 18; ++k) {
       matmul(T, X, W, 1.0 / k);   // W = T X / k
-      if (own) {
+      for (int e = t0; e < ns2; e += nt) {
         T[e] = W[e];
         S[e] = cadd(S[e], W[e]);
       }
     }
     for (int q = 0; q < sq; ++q) {
       matmul(S, S, W, 1.0);
-      if (own) S[e] = W[e];
+      for (int e = t0; e < ns2; e += nt) S[e] = W[e];
     }
     __syncthreads();
-    if (own) expVh[(size_t)p * ns2 + e] = S[e];
+    for (int e = t0; e < ns2; e += nt) expVh[(size_t)p * ns2 + e] = S[e];
     if (expV) {
       matmul(S, S, W, 1.0);
-      if (own) expV[(size_t)p * ns2 + e] = W[e];
+      for (int e = t0; e < ns2; e += nt) expV[(size_t)p * ns2 + e] = W[e];
     }
     __syncthreads();
   }
@@ -999,12 +1015,16 @@ int spo_generic_run(c128* psi, const c128* expVh, const c128* expV, const c128* 
   return run_nd(x, expVh, expV, nsteps, nout, snap, expKy != nullptr);
 }
 
-// exp(-i V dt/2), exp(-i V dt) per point for any ns <= 32 (spo_expm_kernel).
+// exp(-i V dt/2), exp(-i V dt) per point for any ns <= 50 (spo_expm_kernel).
 int spo_expm_run(const void* v, int v_complex, int herm, long npts, int ns, double dt, c128* expV, c128* expVh,
                  hipStream_t st) {
   using namespace spog;
-  const int threads = std::max(64, ((ns * ns + 63) / 64) * 64);
+  const int threads = std::min(1024, std::max(64, ((ns * ns + 63) / 64) * 64));
   const size_t lds = (size_t)4 * ns * ns * sizeof(c128);
+  (void)hipFuncSetAttribute((const void*)spo_expm_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(LDS_MAX - 64));
+  (void)hipFuncSetAttribute((const void*)spo_expm_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(LDS_MAX - 64));
   const int grid = (int)std::min<long>(npts, 16384);
   if (v_complex)
     hipLaunchKernelGGL(spo_expm_kernel<true>, dim3(grid), dim3(threads), lds, st, v, herm, npts, ns, dt, expV, expVh);

@@ -135,9 +135,9 @@ class _PointPropagators:
     The reference's build (wpd.py:585-623, SPO3 :1290-1330) loops over grid points calling eigh and
     forming U e^{-i w tau} U^+.  qd_spo_expv evaluates the same point propagators on the GPU (LAPACK
     conventions: lower triangle, real diagonal): in closed form for ns <= 2, as a scaling-and-squaring
-    matrix exponential for 2 < ns <= 32; they stay on the device for the run and are copied to the
+    matrix exponential for 2 < ns <= 50; they stay on the device for the run and are copied to the
     host only when exp_V / exp_V_half are read.  The eigen data (d2a = U, apes = w) are host eigh
-    results computed on first access.  ns > 32 builds on the host with a vectorised eigh.
+    results computed on first access.  ns > 50 builds on the host with a vectorised eigh.
     """
     _eV_dev = _eVh_dev = None
     _exp_V_host = _exp_V_half_host = None
@@ -196,7 +196,7 @@ class _PointPropagators:
         v = self._pot()
         ns = v.shape[-1]
         _check_finite(v)
-        if ns > 32:   # beyond the device exponential's workgroup (ns^2 <= 1024 lanes): host eigh, as the reference
+        if ns > 50:   # beyond the device exponential's LDS (four ns x ns matrices, 160 KB): host eigh, as the reference
             w, u = self._host_eig()
             ud = np.conj(np.swapaxes(u, -1, -2))
             self.exp_V = (u * np.exp(-1j * w * dt)[..., None, :]) @ ud
@@ -406,7 +406,7 @@ class SPO2NH(SPO2):
 
     def build(self, dt):
         """wpd.py:960-985.  exp_V = U_R e^{-i w dt} U_R^-1 is the matrix exponential exp(-i V dt); it is evaluated on
-        the GPU (qd_spo_expm, scaling and squaring, no eigenvectors) for ns <= 32.  The right eigenvectors and their
+        the GPU (qd_spo_expm, scaling and squaring, no eigenvectors) for ns <= 50.  The right eigenvectors and their
         overlap (right_eigenstates, ovlp_rr; nonherm.eig order, eigenvalues by argsort) are host eig results made
         on first access (position() reads ovlp_rr)."""
         nx, ny = self.nx, self.ny
@@ -417,7 +417,7 @@ class SPO2NH(SPO2):
         self._ur = self._ovlp = None
         ns = v.shape[-1]
         _check_finite(v)
-        if ns > 32:
+        if ns > 50:
             ur = self.right_eigenstates
             w = self._w
             ul = np.linalg.inv(ur)
