@@ -48,9 +48,21 @@ struct SingleParams {
   c128* obs_part;      // [B][total_steps + 1][ne][T^2]
   c128* snap;          // [B][nsave][N][N] or null
   int* status;
+  unsigned long long* tim;   // QD_PHASE_TIMING builds: [grid][8] wall-clock ticks per phase (thread 0's view)
   int N, ne, nsteps, step0, total_steps, save_every, nsave;
   double dt;
 };
+
+#ifdef QD_PHASE_TIMING
+#define SG_MARK(k)                                 \
+  if (tid == 0) {                                  \
+    const unsigned long long now_ = wall_clock64(); \
+    tacc[k] += now_ - tlast;                       \
+    tlast = now_;                                  \
+  }
+#else
+#define SG_MARK(k)
+#endif
 
 typedef unsigned int sg_u4 __attribute__((ext_vector_type(4)));
 
@@ -207,6 +219,9 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
     if (tid == 0) __hip_atomic_store(flag_at(w, kind), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
 
+#ifdef QD_PHASE_TIMING
+  unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = wall_clock64();
+#endif
   const int G4 = 4 * p.nsteps;
   for (int g = 0; g < G4; ++g) {
     const int s = g >> 2, m = g & 3;
@@ -216,6 +231,7 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
           return b * T * T + (l < T ? l * T + bn : bm * T + (l - T));
         }))
       break;
+    SG_MARK(0)
     const __amdgpu_buffer_rsrc_t rr = sg_rsrc(rin, slab);
     c128 rcol[KS], rrow[KS];
 #pragma unroll
@@ -239,14 +255,17 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
       }
       publish(1, (unsigned)(g + 1));
     }
+    SG_MARK(1)
     // ---- k(bm, bn) = P r + r Q + sum_c Y_c R_c; the P r + r Q part runs while the row's Y_c are handed over
     SgAcc<M3> acc;
 #pragma unroll
     for (int q = 0; q < KS; ++q) acc.mac(aP[q], rcol[q]);
 #pragma unroll
     for (int q = 0; q < KS; ++q) acc.mac(rrow[q], bQ[q]);
+    SG_MARK(2)
     if constexpr (NC > 0) {
       if (!wait_for(T, 1, (unsigned)(g + 1), [&](int l) { return b * T * T + bm * T + l; })) break;
+      SG_MARK(3)
       const __amdgpu_buffer_rsrc_t ry = sg_rsrc(ybase, NC * slab);
       c128 yrow[NC][KS];
 #pragma unroll
@@ -260,6 +279,7 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
         for (int q = 0; q < KS; ++q) acc.mac(yrow[c][q], bR[c][q]);
     }
     const c128 kv = reduce(acc);
+    SG_MARK(4)
     const double hc = rk4_horner_coef(p.dt, m);
     const c128 v = cadd(rh, cscale(kv, hc));
     if (m == 3) rh = v;
@@ -276,8 +296,13 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
     }
     if (g + 1 < G4) publish(0, (unsigned)(g + 1));
     else __syncthreads();
+    SG_MARK(5)
   }
   if (owner) rhob[orow * Np + ocol] = rh;
+#ifdef QD_PHASE_TIMING
+  if (tid == 0 && p.tim)
+    for (int k = 0; k < 6; ++k) p.tim[(size_t)w * 8 + k] = tacc[k];
+#endif
 }
 
 // obs[b][gs][m] = sum over the T^2 tiles of obs_part, fixed order
@@ -353,6 +378,13 @@ int glf_single_run(const c128* P, const c128* Q, const c128* Lop, const c128* Ro
   p.snap = p.nsave > 0 ? snap : nullptr;
   p.dt = dt;
   QD_HIP(hipMemsetAsync(p.flags, 0, flag_bytes, st));
+  p.tim = nullptr;
+#ifdef QD_PHASE_TIMING
+  void* tw = nullptr;
+  if ((rc = workspace(WS_MISC, (size_t)B * T2 * 8 * sizeof(unsigned long long), &tw, st))) return rc;
+  QD_HIP(hipMemsetAsync(tw, 0, (size_t)B * T2 * 8 * sizeof(unsigned long long), st));
+  p.tim = (unsigned long long*)tw;
+#endif
   const char* ce = getenv("QD_GLF_SINGLE_COOP");
   const bool coop = !(ce && ce[0] == '0');
   const int grid = B * T2;
@@ -384,6 +416,20 @@ int glf_single_run(const c128* P, const c128* Q, const c128* Lop, const c128* Ro
     *timed_out = 1;
     return QD_OK;
   }
+#ifdef QD_PHASE_TIMING
+  {   // per-phase wall clock (100 MHz ticks, workgroup thread 0), mean over workgroups, per stage, in us
+    std::vector<unsigned long long> hv((size_t)B * T2 * 8);
+    QD_HIP(hipMemcpy(hv.data(), p.tim, hv.size() * 8, hipMemcpyDeviceToHost));
+    const char* nm[6] = {"wait_r", "y_publish", "pr_rq_mfma", "wait_y", "y_mfma_reduce", "update_publish"};
+    fprintf(stderr, "[glf single phase timing] N=%d B=%d nsteps=%d, us per stage:", N, B, nsteps);
+    for (int k = 0; k < 6; ++k) {
+      double sm = 0;
+      for (int q = 0; q < B * T2; ++q) sm += (double)hv[(size_t)q * 8 + k];
+      fprintf(stderr, " %s %.3f", nm[k], sm / (B * T2) / 100.0 / (4.0 * nsteps));
+    }
+    fprintf(stderr, "\n");
+  }
+#endif
   if (ne) {
     const long n = (long)B * (nsteps + 1) * ne;
     hipLaunchKernelGGL(glf_single_obs_kernel, dim3((int)std::min<long>((n + 255) / 256, 1024)), dim3(256), 0, st,
