@@ -324,11 +324,14 @@ hipError_t sg_launch3(SingleParams p, int grid, bool coop, hipStream_t st) {
   void* args[] = {(void*)&p};
   return hipLaunchCooperativeKernel((const void*)glf_single_kernel<KS, NC, M3>, dim3(grid), dim3(SG_WG), args, 0, st);
 }
-// QD_GLF_SINGLE_3M=1: the 3-product complex MACs (A/B)
+// The 3-product complex MACs on a half-filled chip (<= 128 workgroups), the 4-product ones above: N = 128, one matrix
+// 29.7k -> 34.9k steps/s and two 61.7k -> 69.4k with 3 products, four (256 workgroups) 117k -> 103k; N = 32, 64
+// matrices 2.91M -> 2.61M (profiles/r04/lindblad/glf_single_bench.txt).  QD_GLF_SINGLE_3M=0 / 1 forces either (A/B).
 template <int KS, int NC>
 hipError_t sg_launch(SingleParams p, int grid, bool coop, hipStream_t st) {
   const char* me = getenv("QD_GLF_SINGLE_3M");
-  if (me && me[0] == '1') return sg_launch3<KS, NC, true>(p, grid, coop, st);
+  const bool m3 = me ? me[0] == '1' : (grid <= 128 && NC < 2);   // (NC = 2 with 3 products spills)
+  if (m3) return sg_launch3<KS, NC, true>(p, grid, coop, st);
   return sg_launch3<KS, NC, false>(p, grid, coop, st);
 }
 

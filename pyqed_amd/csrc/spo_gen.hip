@@ -782,11 +782,13 @@ struct Exec {
     size_t lds = (size_t)2 * G * C * f[d].M * sizeof(c128);
     a.twl = lds + (size_t)f[d].M * sizeof(c128) <= LDS_MAX;
     if (a.twl) lds += (size_t)f[d].M * sizeof(c128);
-    // stage the pass's operators with the tile when they fit (QD_SPO_AUX=0: read them from HBM/L2, A/B)
+    // QD_SPO_AUX=1: stage the pass's operators with the tile (one load round trip per pass).  Off by default: same-box
+    // A/B (profiles/r04/spo/spo_any_aux_*.txt) 200^2 x 2 25.3 vs 24.8 us per step, 500^2 x 2 50.3 vs 43.8 (the larger
+    // tile lowers the workgroups per CU), so the operator loads are not what bounds these passes.
     a.u2same = U1 == U2;
     a.aux = 0;
     const char* xe = getenv("QD_SPO_AUX");
-    if (!(xe && xe[0] == '0')) {
+    if (xe && xe[0] == '1') {
       const size_t ub = (size_t)G * n[d] * ns * ns * sizeof(c128) * ((flags & F_PT2) && !a.u2same ? 2 : 1);
       const size_t kb = (size_t)n[d] * C * sizeof(c128);
       if ((flags & (F_PT1 | F_PT2)) && lds + ub <= LDS_MAX) {

@@ -464,14 +464,18 @@ def test_lindblad_np64_hermitian_dispatch_matches_oracle(N, B):
     assert relerr(rho.cpu().numpy()[:3], ref) < TOL
 
 
-@pytest.mark.parametrize("N,nc,B", [(128, 1, 1), (128, 2, 1), (100, 1, 4), (64, 1, 3), (40, 2, 2), (20, 0, 5),
-                                    (32, 1, 64)])
-def test_lindblad_single_launch_matches_split_path_and_oracle(N, nc, B, monkeypatch):
+@pytest.mark.parametrize("N,nc,B,m3", [(128, 1, 1, None), (128, 1, 1, "0"), (128, 2, 1, None), (100, 1, 4, None),
+                                       (100, 1, 4, "1"), (64, 1, 3, None), (40, 2, 2, None), (20, 0, 5, None),
+                                       (32, 1, 64, None)])
+def test_lindblad_single_launch_matches_split_path_and_oracle(N, nc, B, m3, monkeypatch):
     """Few density matrices as ONE persistent launch (glf_single.hip: a workgroup per 16 x 16 output tile, operator
     fragments in registers, Y_c and stage outputs handed over inside the launch): final state, observables after every
     step and snapshots against the split path (QD_GLF_SINGLE=0) and the oracle's RK4 (oqs.py:697-714, 1596-1696);
-    Np = 128 / 64 / 32, nc = 0 / 1 / 2, up to the 256-workgroup cap (B = 4 at Np = 128, 64 at Np = 32)."""
+    Np = 128 / 64 / 32, nc = 0 / 1 / 2, up to the 256-workgroup cap (B = 4 at Np = 128, 64 at Np = 32); the 3- and
+    4-product complex MACs (QD_GLF_SINGLE_3M; default: 3 products up to 128 workgroups)."""
     import torch
+    if m3 is not None:
+        monkeypatch.setenv("QD_GLF_SINGLE_3M", m3)
     from oracle import lindblad as olb
     from pyqed_amd import lindblad_rk4
     H, cs = olb.synthetic_lindblad(N, nc=max(nc, 1))
