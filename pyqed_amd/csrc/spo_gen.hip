@@ -232,8 +232,25 @@ __device__ __forceinline__ void lds_fft(const Fft& p, const c128* tw, c128*& cur
 }
 
 // ---------------------------------------------------------------- fused axis pass
+#ifdef QD_PHASE_TIMING
+// diagnostics build: per-pass phase wall clock summed over blocks (thread 0's view after each barrier)
+// [0] load, [1] inverse FFT, [2] point ops / snapshot / k_y, [3] forward FFT / kinetic step, [4] store, [5] blocks
+__device__ unsigned long long g_spo_tim[2][6];
+#define SPO_MARK(k)                                   \
+  if (threadIdx.x == 0) {                             \
+    const unsigned long long now_ = wall_clock64();   \
+    atomicAdd(&g_spo_tim[a.flags & F_KMUL ? 1 : 0][k], now_ - tl_); \
+    tl_ = now_;                                       \
+  }
+#else
+#define SPO_MARK(k)
+#endif
 __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
   extern __shared__ c128 sm[];
+#ifdef QD_PHASE_TIMING
+  unsigned long long tl_ = wall_clock64();
+  if (threadIdx.x == 0) atomicAdd(&g_spo_tim[a.flags & F_KMUL ? 1 : 0][5], 1ull);
+#endif
   const int M = p.M, L = a.L, C = a.C, G = a.G, I = a.I;
   const int nl = G * C;
   c128* cur = sm;
@@ -270,7 +287,9 @@ __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
         (g < gv && c < cv) ? a.psi[((size_t)(o0 + g) * L + e) * I + i0 + c] : cmk(0.0, 0.0);
   }
   __syncthreads();
+  SPO_MARK(0)
   if (a.flags & F_INV) lds_fft<true>(p, tw, cur, oth, nl);
+  SPO_MARK(1)
   auto point_op = [&](const c128* U) {   // C == I == ns: line g * ns + s holds state s of row g
     const int n = G * L * ns;
     const int row0 = a.aux == 1 ? 0 : o0;   // staged rows start at the tile's first row
@@ -296,6 +315,7 @@ __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
     }
   }
   if (a.flags & F_PT2) point_op(U2);
+  SPO_MARK(2)
   if (a.flags & F_FWD) lds_fft<false>(p, tw, cur, oth, nl);
   if (a.flags & F_KY) {
     for (int f = threadIdx.x; f < tot; f += blockDim.x) {
@@ -315,10 +335,15 @@ __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
     __syncthreads();
     lds_fft<true>(p, tw, cur, oth, nl);
   }
+  SPO_MARK(3)
   for (int f = threadIdx.x; f < tot; f += blockDim.x) {
     const int g = (int)fdiv((unsigned)f, a.dLC), r = f - g * (L * C), e = (int)fdiv((unsigned)r, a.dC), c = r - e * C;
     if (g < gv && c < cv) a.psi[((size_t)(o0 + g) * L + e) * I + i0 + c] = cur[(g * C + c) * M + e];
   }
+#ifdef QD_PHASE_TIMING
+  __syncthreads();
+#endif
+  SPO_MARK(4)
 }
 
 // ---------------------------------------------------------------- unfused kernels
@@ -1014,7 +1039,25 @@ int spo_generic_run(c128* psi, const c128* expVh, const c128* expV, const c128* 
   QD_HIP(hipGetLastError());
   x.Ks = ks;
   x.Ky = expKy;
+#ifdef QD_PHASE_TIMING
+  {
+    unsigned long long z[2][6] = {};
+    QD_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_spo_tim), z, sizeof(z), 0, hipMemcpyHostToDevice, st));
+    rc = run_nd(x, expVh, expV, nsteps, nout, snap, expKy != nullptr);
+    QD_HIP(hipStreamSynchronize(st));
+    QD_HIP(hipMemcpyFromSymbol(z, HIP_SYMBOL(g_spo_tim), sizeof(z)));
+    const char* nm[5] = {"load", "inv_fft", "point_ops", "fwd_fft_or_kin", "store"};
+    for (int k = 0; k < 2; ++k) {
+      if (!z[k][5]) continue;
+      fprintf(stderr, "[spo_axis phase timing] %s pass, us per block:", k ? "kinetic" : "row");
+      for (int q = 0; q < 5; ++q) fprintf(stderr, " %s %.3f", nm[q], (double)z[k][q] / z[k][5] / 100.0);
+      fprintf(stderr, " (%llu blocks)\n", z[k][5]);
+    }
+    return rc;
+  }
+#else
   return run_nd(x, expVh, expV, nsteps, nout, snap, expKy != nullptr);
+#endif
 }
 
 // exp(-i V dt/2), exp(-i V dt) per point for any ns <= 50 (spo_expm_kernel).
