@@ -812,8 +812,8 @@ struct Exec {
     // tile lowers the workgroups per CU), so the operator loads are not what bounds these passes.
     a.u2same = U1 == U2;
     a.aux = 0;
-    const char* xe = getenv("QD_SPO_AUX");
-    if (xe && xe[0] == '1') {
+    const char* xe = getenv("QD_SPO_AUX");   // 1: both kinds of pass, 2: kinetic passes only
+    if (xe && (xe[0] == '1' || (xe[0] == '2' && (flags & F_KMUL)))) {
       const size_t ub = (size_t)G * n[d] * ns * ns * sizeof(c128) * ((flags & F_PT2) && !a.u2same ? 2 : 1);
       const size_t kb = (size_t)n[d] * C * sizeof(c128);
       if ((flags & (F_PT1 | F_PT2)) && lds + ub <= LDS_MAX) {
@@ -840,7 +840,9 @@ struct Exec {
       c = (int)I;
     } else {   // 8 consecutive columns (128-B rows) when that still leaves >= 256 tiles, else fewer
       c = (int)std::min<long>(I, 8);
-      while (c > 1 && ((size_t)c * line > LDS_SOFT || ((I + c - 1) / c) * O < 256)) c >>= 1;
+      int minc = 1;   // QD_SPO_GEN_MINC: never fewer columns per tile than this (A/B of coalescing vs tile count)
+      if (const char* e = getenv("QD_SPO_GEN_MINC")) minc = std::max(1, std::min(8, atoi(e)));
+      while (c > minc && ((size_t)c * line > LDS_SOFT || ((I + c - 1) / c) * O < 256)) c >>= 1;
     }
     if ((size_t)c * line > LDS_MAX) return false;
     int g = 1;
