@@ -946,6 +946,14 @@ def cpu_baseline_deom(budget_s=8.0):
             "sample": f"1 RK4 step of the NumPy restatement of DEOMSolver.run at L=12, K=5 in {el:.1f}s"}
 
 
+_T0 = time.perf_counter()
+
+
+def progress(msg):
+    """One line per leg on stderr (stdout carries only the JSON line): long runs under a profiler show activity."""
+    print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def write_detail(out, path):
     """Every leg's full record (per-leg configs, notes, PMC traffic, cpu_baseline samples) goes to a side file; the
     stdout line carries the compact summary (the driver keeps only the tail of stdout)."""
@@ -1125,6 +1133,7 @@ def main():
     # runs B = 64 (Hermitian states, 16 <= B < 192) on the Hermitian pair-block split path and B = 1 on the
     # general kernel's split-K path; each entry's flops are its own path's (Hermitian GLF form / general kernel)
     from pyqed_amd.oqs import HERM_SPLIT_MIN_BATCH
+    progress("lindblad headline leg done")
     batch_sweep = {}
     for Bs in (1, 64):
         rs = rho[:Bs].clone()
@@ -1147,6 +1156,7 @@ def main():
                          "frac": round(tf / FP64_MFMA_PEAK_TFLOPS, 4), "flop_per_dm_step": fl}}
     single_rate = batch_sweep["1"]["dm_steps_per_s"]
 
+    progress("lindblad batch sweep done")
     twodes = None
     if not args.no_2des:
         twodes, sig, ens_in = bench_2des(dev, world, rank, args.ens, args.ens_reps)
@@ -1185,22 +1195,27 @@ def main():
     def pair(r):
         return r if isinstance(r, tuple) else (r, None)
 
+    progress("2des legs done")
     redfield = None
     if not args.no_redfield:
         redfield, rf_sol = pair(guarded(bench_redfield, dev, args.steps, B))
 
+    progress("redfield leg done")
     superop = None
     if not args.no_superop:
         superop, so_in = pair(guarded(bench_superop, dev))
 
+    progress("superop leg done")
     spo = None
     if not args.no_spo:
         spo = guarded(bench_spo2, dev, args.spo_steps)
 
+    progress("spo2 leg done")
     spo3 = None
     if not args.no_spo3:
         spo3 = guarded(bench_spo3, dev)
 
+    progress("spo3 leg done")
     deom = None
     if not args.no_deom:
         deom = guarded(bench_deom, dev, args.deom_steps, args.deom_batch)
@@ -1209,6 +1224,7 @@ def main():
     # At world > 1 it is opt-in (--deom-banded-ranks): a collective leg cannot be guarded per rank (one rank's
     # exception would leave the others waiting in the all-gather), and the halo is 2.5x the owned rows at 8 bands, so
     # it is a capacity tool, not a speed-up, for the bench hierarchy.  World 1 runs the 8-band loopback.
+    progress("deom leg done")
     deom_banded = None
     if not args.no_deom and not args.no_deom_banded:
         if world > 1:
