@@ -99,7 +99,7 @@ struct AxisArgs {
 // ---------------------------------------------------------------- device FFT
 // One Stockham stage over nl lines of length M: butterfly j of a line reads src[j + r M/R] (r < R) times
 // tw^(r k M/(Ns R)), k = j mod Ns, and writes the R-point DFT to dst[(j / Ns) Ns R + k + q Ns].
-template <bool INV, int R0>   // R0 = 2, 3, 4, 5: closed-form butterflies; 0: any prime R <= GEN_MAXP
+template <bool INV, int R0>   // R0 = 2, 3, 4, 5, 8: closed-form butterflies; 0: any prime R <= GEN_MAXP
 __device__ __forceinline__ void stage(const c128* __restrict__ src, c128* __restrict__ dst, int nl, int M, int Rr,
                                       int Ns, FDiv dnb, FDiv dns, const c128* __restrict__ tw) {
   const int R = R0 ? R0 : Rr;
@@ -120,7 +120,27 @@ __device__ __forceinline__ void stage(const c128* __restrict__ src, c128* __rest
       if (INV) w = cconj(w);
       return cmul(x, w);
     };
-    if constexpr (R0 == 4) {
+    if constexpr (R0 == 8) {   // DFT8 = DFT4 of the even and of the odd inputs, combined with w8^k
+      const c128 x0 = ld(0), x1 = ld(1), x2 = ld(2), x3 = ld(3), x4 = ld(4), x5 = ld(5), x6 = ld(6), x7 = ld(7);
+      auto mj = [](c128 v) { return INV ? cmuli(v) : cmulmi(v); };   // times -+ i
+      const c128 a0 = cadd(x0, x4), a1 = csub(x0, x4), a2 = cadd(x2, x6), a3 = mj(csub(x2, x6));
+      const c128 b0 = cadd(x1, x5), b1 = csub(x1, x5), b2 = cadd(x3, x7), b3 = mj(csub(x3, x7));
+      const c128 e0 = cadd(a0, a2), e2 = csub(a0, a2), e1 = cadd(a1, a3), e3 = csub(a1, a3);
+      c128 o0 = cadd(b0, b2), o2 = csub(b0, b2), o1 = cadd(b1, b3), o3 = csub(b1, b3);
+      const double h = 0.70710678118654752440;   // 1 / sqrt(2)
+      // o1 w8, o2 w8^2 = -+ i, o3 w8^3 with w8 = (1 -+ i) / sqrt(2)
+      o1 = INV ? cmk((o1.re - o1.im) * h, (o1.re + o1.im) * h) : cmk((o1.re + o1.im) * h, (o1.im - o1.re) * h);
+      o2 = mj(o2);
+      o3 = INV ? cmk(-(o3.re + o3.im) * h, (o3.re - o3.im) * h) : cmk((o3.im - o3.re) * h, -(o3.re + o3.im) * h);
+      d[db] = cadd(e0, o0);
+      d[db + Ns] = cadd(e1, o1);
+      d[db + 2 * Ns] = cadd(e2, o2);
+      d[db + 3 * Ns] = cadd(e3, o3);
+      d[db + 4 * Ns] = csub(e0, o0);
+      d[db + 5 * Ns] = csub(e1, o1);
+      d[db + 6 * Ns] = csub(e2, o2);
+      d[db + 7 * Ns] = csub(e3, o3);
+    } else if constexpr (R0 == 4) {
       const c128 x0 = ld(0), x1 = ld(1), x2 = ld(2), x3 = ld(3);
       const c128 a0 = cadd(x0, x2), a1 = csub(x0, x2), b0 = cadd(x1, x3), b1 = csub(x1, x3);
       const c128 ib1 = INV ? cmuli(b1) : cmulmi(b1);
@@ -178,6 +198,7 @@ __device__ __forceinline__ void stockham(const Fft& p, const c128* tw, c128*& cu
     const int R = p.R[s], Ns = p.Ns[s];
     const FDiv dnb = p.dnb[s], dns = p.dns[s];   // copies: a reference would put the plan in scratch
     switch (R) {   // wave-uniform: one branch-free element loop per radix
+      case 8: stage<INV, 8>(cur, oth, nl, M, 8, Ns, dnb, dns, tw); break;
       case 4: stage<INV, 4>(cur, oth, nl, M, 4, Ns, dnb, dns, tw); break;
       case 2: stage<INV, 2>(cur, oth, nl, M, 2, Ns, dnb, dns, tw); break;
       case 3: stage<INV, 3>(cur, oth, nl, M, 3, Ns, dnb, dns, tw); break;
@@ -690,6 +711,21 @@ void factor_stages(int M, Fft& f) {
     ns *= r;
     n /= r;
   };
+  // radix 8 first (one LDS stage and barrier instead of a radix-4 and a radix-2 one: 200 = 8 5 5 in three stages
+  // instead of four); QD_SPO_RADIX8=0 keeps radix 4 / 2 (A/B)
+  static const bool r8 = [] {
+    const char* e = getenv("QD_SPO_RADIX8");
+    return !(e && e[0] == '0');
+  }();
+  if (r8) {
+    // 8s as long as no single 2 would be left over unpaired with a 4 (16 = 8 2 would take as many stages as 4 4)
+    int twos = 0;
+    for (int m = n; m % 2 == 0; m /= 2) ++twos;
+    for (int k = 0; k < twos / 3 && twos % 3 != 1; ++k) push(8);
+    if (twos % 3 == 1 && twos >= 4) {   // 2^(3j+1): 8^(j-1) 4 4 is as short as 8^j 2 and has no radix-2 stage
+      for (int k = 0; k < (twos - 4) / 3; ++k) push(8);
+    }
+  }
   while (n % 4 == 0) push(4);
   while (n % 2 == 0) push(2);
   while (n % 3 == 0) push(3);

@@ -12,15 +12,16 @@ R=$PWD
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
+# a cooperative launch makes rocprofv3 segfault at process exit, with --pmc and (seen in r04) with --kernel-trace
+# too, after the output is written (profiles/r04/pmc_crash/SUMMARY.md): every profiled run takes the plain launch
+# of the banded DEOM and single-trajectory Lindblad kernels (same kernels, same residency)
+export QD_DEOM_BAND_COOP=0 QD_GLF_SINGLE_COOP=0
 if [ "$PART" = stats ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- python3 $R/bench.py --steps 50 --warmup 5 --no-cpu > $OUT/stats.log 2>&1
   timeout -k 10 60 $R/tools/mfma_f64_peak > $OUT/mfma_f64_peak.log 2>&1
   timeout -k 10 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/calib_fetch -o run -- $R/tools/pmc_calib > $OUT/calib_fetch.log 2>&1
   timeout -k 10 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/calib_write -o run -- $R/tools/pmc_calib > $OUT/calib_write.log 2>&1
 else
-  # a cooperative launch makes rocprofv3 --pmc segfault at process exit (profiles/r04/pmc_crash/SUMMARY.md): the
-  # counter passes take the plain launch of the banded DEOM kernel (same kernel, same residency)
-  export QD_DEOM_BAND_COOP=0 QD_GLF_SINGLE_COOP=0
   timeout -k 10 250 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu > $OUT/fetch.log 2>&1
   timeout -k 10 250 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu > $OUT/write.log 2>&1
   timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/gfetch -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu --general --no-2des --no-spo --no-deom --no-redfield > $OUT/gfetch.log 2>&1
