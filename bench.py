@@ -1151,9 +1151,13 @@ def main():
         tf = fl * Bs * ss / sec / 1e12
         batch_sweep[str(Bs)] = {
             "dm_steps_per_s": round(Bs * ss / sec, 1), "us_per_step": round(sec / ss * 1e6, 2),
-            "path": "Hermitian pair-block split (glf_split_hk)" if hs else "glf split-K (general kernel)",
+            "path": ("Hermitian pair-block split (glf_split_hk)" if hs else
+                     "single-trajectory tile launch (glf_single_kernel)" if Bs == 1 and N in (32, 64, 128) and nc <= 2
+                     else "glf split-K (general kernel)"),
             "roofline": {"bound": "mfma", "achieved": round(tf, 3), "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(tf / FP64_MFMA_PEAK_TFLOPS, 4), "flop_per_dm_step": fl}}
+                         "frac": round(tf / FP64_MFMA_PEAK_TFLOPS, 4), "flop_per_dm_step": fl,
+                         "traffic": (measured_traffic("glf_single_kernel<4,1,true>_b1", ss)
+                                     if (Bs, N, nc) == (1, 128, 1) else None)}}
     single_rate = batch_sweep["1"]["dm_steps_per_s"]
 
     progress("lindblad batch sweep done")
