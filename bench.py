@@ -784,11 +784,11 @@ def bench_deom(dev, steps, batch):
         "run_steps_per_s_end_to_end": round(steps / wall_run, 1),
         "batched": {"hierarchies": batch, "ado_steps_per_s": round(ado_b, 1), "steps_per_s": round(rate[batch], 1),
                     "layout": "ADO-major [nmax][B][2][2], hierarchies dealt to the 8 XCD block classes",
-                    "roofline": {"bound": "hbm", "kernel": "deom_stage_grp_w5_kernel<4,5,true,false,1>",
+                    "roofline": {"bound": "hbm", "kernel": "deom_stage_pipe_kernel<5>",
                                  "achieved": round(ado_b * bytes_per_ado_step / 1e9, 1), "peak": HBM_PEAK_GBS,
                                  "unit": "GB/s", "frac": round(ado_b * bytes_per_ado_step / 1e9 / HBM_PEAK_GBS, 4),
                                  "bytes_per_ado_step": bytes_per_ado_step,
-                                 "traffic": measured_traffic("deom_stage_grp_w5_kernel<4,5,true>_64h", nmax * batch / 4)
+                                 "traffic": measured_traffic("deom_stage_pipe_kernel<5>_64h", nmax * batch / 4)
                                  if batch == 64 else None,
                                  "traffic_unit": "HBM bytes per stage launch (PMC FETCH_SIZE+WRITE_SIZE, calibrated; "
                                                  "profiles/pmc_traffic.json)"}},

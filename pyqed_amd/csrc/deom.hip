@@ -402,6 +402,147 @@ __global__ __launch_bounds__(DEOM_TPB) __attribute__((amdgpu_waves_per_eu(5))) v
   deom_stage_grp_body<G, KMAX, NS2, UNI, HM>(p);
 }
 
+// Software-pipelined persistent form of the ns = 2 group kernel for undriven ADO-major batches (Horner stages, XCD
+// classes of B / 8 hierarchies, no hierarchy chunks): a fixed grid whose waves walk the class's lane groups with a
+// stride, and while one group's neighbour rows are in flight the NEXT group's neighbour indices, own element and
+// stage state are loaded.  The stage kernels above spend two dependent memory round trips per wave (tables + own
+// rows, then the neighbour rows the tables point at), once per wave generation; here a wave pays about one per group
+// after the first.  Same per-element arithmetic in the same order as deom_stage_grp_body<4, KMAX, true, false, 1>,
+// so the result is bit-identical (tests/test_deom_gpu.py); H / Q go to LDS once per workgroup.
+template <int KMAX>
+__global__ __launch_bounds__(DEOM_TPB) void deom_stage_pipe_kernel(DeomParams p) {
+  constexpr int G = 4, NI = (KMAX + G - 1) / G, NC = (3 * KMAX + G - 1) / G;
+  extern __shared__ c128 deom_lds[];
+  c128* sH = deom_lds;
+  c128* sQ = deom_lds + 4;
+  for (int q = threadIdx.x; q < 4; q += blockDim.x) sH[q] = p.H[q];
+  for (int q = threadIdx.x; q < p.nmod * 4; q += blockDim.x) sQ[q] = p.Q[q];
+  __syncthreads();
+  const int K = p.K;
+  const unsigned cls = blockIdx.x & 7;
+  const unsigned Bx = (unsigned)(p.B / p.xsplit);
+  const unsigned per = Bx * (unsigned)p.nmax * G;            // lanes of this class
+  const unsigned stride = (gridDim.x >> 3) * blockDim.x;
+  const unsigned lane = threadIdx.x & 63;
+  const int e = (int)(threadIdx.x & 3);
+  const int base = (int)lane & ~(G - 1);
+  const size_t rs = (size_t)p.B * 4;                        // ADO row stride
+  const int i = e >> 1, j = e & 1;
+  auto bc = [&](c128 v, int src) -> c128 {
+    switch (src) {
+      case 0: return dpp_qc<0x00>(v);
+      case 1: return dpp_qc<0x55>(v);
+      case 2: return dpp_qc<0xAA>(v);
+      default: return dpp_qc<0xFF>(v);
+    }
+  };
+  auto bci = [&](int v, int src) -> int {
+    switch (src) {
+      case 0: return dpp_qi<0x00>(v);
+      case 1: return dpp_qi<0x55>(v);
+      case 2: return dpp_qi<0xAA>(v);
+      default: return dpp_qi<0xFF>(v);
+    }
+  };
+  auto colv = [&](c128 v, int l) -> c128 { return l == 0 ? dpp_qc<0x44>(v) : dpp_qc<0xEE>(v); };
+  auto rowv = [&](c128 v, int l) -> c128 { return l == 0 ? dpp_qc<0xA0>(v) : dpp_qc<0xF5>(v); };
+  // the part of a group's inputs that addresses nothing else: its neighbour indices and own element
+  struct Head {
+    int lm[NI], lp[NI];
+    c128 own;
+    int n;
+    unsigned hb;
+    bool live;
+  };
+  auto head = [&](unsigned uu, Head& h) {
+    const unsigned lgrp = uu / G;
+    h.live = uu < per;
+    const unsigned hi = lgrp / Bx, lo = lgrp - hi * Bx;
+    h.n = h.live ? (int)hi : 0;
+    h.hb = cls * Bx + (h.live ? lo : 0);
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      const int k = e + G * q;
+      h.lm[q] = (h.live && k < K) ? p.minus[(size_t)h.n * K + k] : -1;
+      h.lp[q] = (h.live && k < K) ? p.plus[(size_t)h.n * K + k] : -1;
+    }
+    const c128* X = p.xin + (size_t)h.hb * 4;
+    h.own = h.live ? X[(size_t)h.n * rs + e] : cmk(0, 0);
+  };
+  unsigned u = (blockIdx.x >> 3) * blockDim.x + threadIdx.x;
+  Head cur;
+  head(u, cur);
+  while (__builtin_amdgcn_readfirstlane(u - lane) < per) {   // wave-uniform trip count (DPP needs whole quads)
+    // this group's prefactors, damping and neighbour rows
+    c128 lc[NC];
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      const int c = e + G * q;
+      lc[q] = (cur.live && c < 3 * K) ? p.coef[(size_t)cur.n * K * 3 + c] : cmk(0, 0);
+    }
+    const c128 dmp = cur.live ? p.damp[cur.n] : cmk(0, 0);
+    const size_t idx = ((size_t)cur.n * p.B + cur.hb) * 4 + e;
+    const c128 r0 = !cur.live ? cmk(0, 0) : p.stage == 0 ? cur.own : ld_once(p.rho + idx, p.ntst);
+    const c128* X = p.xin + (size_t)cur.hb * 4;
+    c128 ym[KMAX], yp[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int im = bci(cur.lm[k / G], k % G), ip = bci(cur.lp[k / G], k % G);
+      ym[k] = (k < K && im >= 0) ? X[(size_t)im * rs + e] : cmk(0, 0);
+      yp[k] = (k < K && ip >= 0) ? X[(size_t)ip * rs + e] : cmk(0, 0);
+    }
+    // the next group's head, in flight with the rows above
+    const unsigned un = u + stride;
+    Head nxt;
+    head(un, nxt);
+    // stencil: deom_stage_grp_body's ns = 2 arithmetic, operation for operation
+    c128 d = cmul(dmp, cur.own);
+    c128 comm = cmk(0, 0);
+#pragma unroll
+    for (int l = 0; l < 2; ++l)
+      comm = cadd(comm, csub(cmul(sH[i * 2 + l], colv(cur.own, l)), cmul(rowv(cur.own, l), sH[l * 2 + j])));
+    d = cadd(d, cmulmi(comm));
+    c128 SL = cmk(0, 0), SR = cmk(0, 0);
+    auto flush = [&](int m) {
+      const c128* Qm = sQ + m * 4;
+      c128 t = cmk(0, 0);
+#pragma unroll
+      for (int l = 0; l < 2; ++l) t = cadd(t, cadd(cmul(Qm[i * 2 + l], colv(SL, l)), cmul(rowv(SR, l), Qm[l * 2 + j])));
+      d = cadd(d, t);
+    };
+    int mcur = p.mode[0];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      if (k >= K) break;
+      const int m = p.mode[k];
+      if (m != mcur) {
+        flush(mcur);
+        SL = SR = cmk(0, 0);
+        mcur = m;
+      }
+      const c128 cL = bc(lc[(3 * k) / G], (3 * k) % G);
+      const c128 cR = bc(lc[(3 * k + 1) / G], (3 * k + 1) % G);
+      const c128 cP = bc(lc[(3 * k + 2) / G], (3 * k + 2) % G);
+      const c128 py = cmul(cP, yp[k]);
+      SL = cadd(SL, cadd(cmul(cL, ym[k]), py));
+      SR = cadd(SR, csub(cmul(cR, ym[k]), py));
+    }
+    flush(mcur);
+    if (cur.live) {
+      c128 a0 = cmk(0, 0);
+      const c128 v = deom_rk4_next(p.stage, true, p.dt, r0, a0, d);
+      if (p.stage < 3) {
+        p.xout[idx] = v;
+      } else {
+        p.rho_out[idx] = v;
+        if (p.snap && cur.n == 0) p.snap[((size_t)cur.hb * (p.nsteps + 1) + p.step + 1) * 4 + e] = v;
+      }
+    }
+    cur = nxt;
+    u = un;
+  }
+}
+
 // MFMA tile kernel for 9 <= ns <= 16 (zero-padded to 16 in registers), NM <= 2 bath modes, K <= 21: one wave per
 // ADO.  The stencil regrouped by mode m:
 //   d rho_n = damp_n x - iH x + x iH + sum_m (Q_m SL_m + SR_m Q_m),
@@ -902,6 +1043,36 @@ int deom_launch_stage(const DeomParams& p, hipStream_t st) {
     }
     if (!grp) {
       hipLaunchKernelGGL(deom_stage_kernel, dim3(grid), dim3(tpb), 0, st, q);
+      return;
+    }
+    // the software-pipelined persistent form (undriven ns = 2 ADO-major batches of >= 64 hierarchies in 8 XCD classes,
+    // no hierarchy chunks); QD_DEOM_PIPE=0 keeps the stage kernels, QD_DEOM_PIPE_BPC sets the workgroups per class
+    const char* pe = getenv("QD_DEOM_PIPE");
+    if (G == 4 && q.horner && bminor && q.xsplit == 8 && q.bchunk == 0 && B >= 64 && K <= 6 && !(pe && pe[0] == '0') &&
+        tpb == DEOM_TPB) {
+      auto go = [&](const void* fn, auto kern) {
+        // workgroups per class: what one XCD's CUs hold at once (every wave persistent, no tail generation)
+        static thread_local const void* last_fn = nullptr;   // one lookup per kernel / LDS size / device
+        static thread_local size_t last_lds = 0;
+        static thread_local int last_dev = -1, last_bpc = 1;
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (fn != last_fn || lds != last_lds || dev != last_dev) {
+          int per_cu = 0, cus = 0;
+          (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+          (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, DEOM_TPB, lds);
+          last_fn = fn;
+          last_lds = lds;
+          last_dev = dev;
+          last_bpc = std::max(1, per_cu) * std::max(1, cus / 8);
+        }
+        int bpc = last_bpc;
+        if (const char* s = getenv("QD_DEOM_PIPE_BPC")) bpc = std::max(1, atoi(s));
+        hipLaunchKernelGGL(kern, dim3((unsigned)(8 * bpc)), dim3(DEOM_TPB), lds, st, q);
+      };
+      if (K == 5) go((const void*)deom_stage_pipe_kernel<5>, deom_stage_pipe_kernel<5>);
+      else if (K <= 4) go((const void*)deom_stage_pipe_kernel<4>, deom_stage_pipe_kernel<4>);
+      else go((const void*)deom_stage_pipe_kernel<6>, deom_stage_pipe_kernel<6>);
       return;
     }
     const char* w5e = getenv("QD_DEOM_W5");   // 0: keep the unconstrained kernel for >= 64 hierarchies (A/B)

@@ -5,7 +5,7 @@
 // powers of two in [16, 1024]; this file serves every other grid with the same pass structure:
 //
 //   axis plan per grid axis of length L (plan_axis):
-//     MIXED      mixed-radix Stockham autosort in LDS: radix 4, 2, 3, 5 butterflies in closed form, any
+//     MIXED      mixed-radix Stockham autosort in LDS: radix 8, 4, 2, 3, 5 butterflies in closed form, any
 //                other prime p <= 61 as a direct p-point DFT stage; natural-order output, fp64 twiddles
 //                exp(-2 pi i m / L) from sincospi, L <= 5120 (two LDS lines of L complex values)
 //     BLUESTEIN  lengths with a prime factor > 61: chirp-z, X_k = c_k sum_n (x_n c_n) conj(c_{k-n}),
@@ -24,6 +24,12 @@
 //   A pass that does not fit the LDS budget (DIRECT axes, ns * M too large for a fused row) runs
 //   unfused: axis transforms, a point-operator kernel (thread per (point, state), any ns) and a
 //   k-space multiply, with one grid-sized scratch buffer.
+//
+//   2D grids alternate two layouts between the passes (Exec::xpose): the row pass reads [x][y][s] rows and writes
+//   [y][x][s], the kinetic pass reads those x lines contiguously (exp_K / N transposed to match) and writes [x][y][s]
+//   back, so every pass loads whole contiguous lines and only the stores are strided (fire-and-forget, off the
+//   dependent chain): 200^2 x 2 24.3 -> 22.5 us per step, 1000^2 x 2 143 -> 134 (profiles/r04/spo/spo_xpose_ab.txt).
+//   3D grids can rotate their layouts the same way (QD_SPO_XPOSE3=1) but lose at 96^3 and above (see Exec).
 //
 //   SPO (1D, wpd.py:225-273): one persistent workgroup per wavepacket, all steps in LDS when the line
 //   fits; otherwise one launch sequence per step.
@@ -79,10 +85,16 @@ struct Fft {           // device-side plan of one axis, passed by value
   const c128* bhat;    // BLUESTEIN: (1/M) FFT_M(b), b_m = conj(c_|m|) wrapped
 };
 
-enum Flags { F_INV = 1, F_PT1 = 2, F_SNAP = 4, F_PT2 = 8, F_FWD = 16, F_KY = 32, F_KMUL = 64 };
+enum Flags { F_INV = 1, F_PT1 = 2, F_SNAP = 4, F_PT2 = 8, F_FWD = 16, F_KY = 32, F_KMUL = 64,
+             F_XOUT = 128,    // store into another layout: element (o, e, i) of [O][L][I], o = hi nlo + lo, to
+                              // out[hi sh + lo sl + e se + i] (2D: [L][O][I])
+             F_KROW = 256 };  // KMUL on whole rows (C == I == ns): factor K[o][e] of the [O][L] table
 
 struct AxisArgs {
-  c128* psi;
+  c128* psi;           // tile source
+  c128* out;           // tile destination (psi: in place; F_XOUT: the other layout's buffer)
+  long sh, sl, se;     // F_XOUT strides of hi, lo, e
+  FDiv dlo;            // F_XOUT: division by nlo
   int O, L, I, C, G, flags, ns;
   FDiv dLC, dC, dLns, dns;   // L C, C, L ns, ns
   int twl;             // 1: twiddles staged in LDS (M more c128 of dynamic LDS)
@@ -349,9 +361,13 @@ __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
     lds_fft<false>(p, tw, cur, oth, nl);
     for (int f = threadIdx.x; f < tot; f += blockDim.x) {
       const int r = f - (int)fdiv((unsigned)f, a.dLC) * (L * C), e = (int)fdiv((unsigned)r, a.dC), c = r - e * C;
-      if (c < cv)
+        if (a.flags & F_KROW) {
+        const int g = (int)fdiv((unsigned)f, a.dLC);
+        if (g < gv) cur[(g * C + c) * M + e] = cmul(cur[(g * C + c) * M + e], a.K[(size_t)(o0 + g) * L + e]);
+      } else if (c < cv) {
         cur[c * M + e] = cmul(cur[c * M + e], a.aux == 2 ? aux[e * C + c]
                                                           : a.K[(size_t)e * pts + (int)fdiv((unsigned)(i0 + c), a.dns)]);
+      }
     }
     __syncthreads();
     lds_fft<true>(p, tw, cur, oth, nl);
@@ -359,7 +375,16 @@ __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
   SPO_MARK(3)
   for (int f = threadIdx.x; f < tot; f += blockDim.x) {
     const int g = (int)fdiv((unsigned)f, a.dLC), r = f - g * (L * C), e = (int)fdiv((unsigned)r, a.dC), c = r - e * C;
-    if (g < gv && c < cv) a.psi[((size_t)(o0 + g) * L + e) * I + i0 + c] = cur[(g * C + c) * M + e];
+    if (g < gv && c < cv) {
+      size_t o;
+      if (a.flags & F_XOUT) {
+        const unsigned og = (unsigned)(o0 + g), hi = fdiv(og, a.dlo), lo = og - hi * a.dlo.d;
+        o = (size_t)hi * a.sh + (size_t)lo * a.sl + (size_t)e * a.se + i0 + c;
+      } else {
+        o = ((size_t)(o0 + g) * L + e) * I + i0 + c;
+      }
+      a.out[o] = cur[(g * C + c) * M + e];
+    }
   }
 #ifdef QD_PHASE_TIMING
   __syncthreads();
@@ -429,6 +454,23 @@ __global__ void kmul_kernel(c128* psi, const c128* __restrict__ K, long n, int n
     psi[f] = cmul(psi[f], K[f / ns]);
 }
 
+// dst[z][y][x] = s src[x][y][z] (src [n0][n1][n2]): the kinetic table of the 3D rotated passes
+__global__ void scale_permute3_kernel(const c128* __restrict__ src, c128* __restrict__ dst, int n0, int n1, int n2,
+                                      double s) {
+  const long n = (long)n0 * n1 * n2;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const int z = (int)(e % n2), y = (int)((e / n2) % n1), x = (int)(e / ((long)n1 * n2));
+    dst[((size_t)z * n1 + y) * n0 + x] = cscale(src[e], s);
+  }
+}
+// dst[j][i] = s src[i][j] (src [r][c]): the kinetic table of the xpose passes
+__global__ void scale_transpose_kernel(const c128* __restrict__ src, c128* __restrict__ dst, int r, int c, double s) {
+  const long n = (long)r * c;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const int i = (int)(e / c), j = (int)(e % c);
+    dst[(size_t)j * r + i] = cscale(src[e], s);
+  }
+}
 __global__ void scale_copy_kernel(const c128* __restrict__ src, c128* __restrict__ dst, long n, double s) {
   for (long f = blockIdx.x * (long)blockDim.x + threadIdx.x; f < n; f += (long)gridDim.x * blockDim.x)
     dst[f] = cscale(src[f], s);
@@ -816,21 +858,38 @@ struct Exec {
   c128* psi = nullptr;
   c128* tmp = nullptr;     // grid-sized scratch (unfused passes)
   const c128* Ks = nullptr;   // exp_K / N
+  const c128* KsT = nullptr;  // exp_K / N in the kinetic pass's input layout (xpose): [n1][n0] / [n2][n1][n0]
   const c128* Ky = nullptr;   // Jacobi k_y phase [n0][n1] (D == 2)
+  bool xpose = false;         // 2D: alternating layouts (file header); psi [n0][n1][ns] <-> tmp [n1][n0][ns]
+  int kin_g = 1;              // xpose: rows per tile of the kinetic pass
 
   long outer(int d) const { long o = 1; for (int k = 0; k < d; ++k) o *= n[k]; return o; }
   long inner(int d) const { long i = ns; for (int k = d + 1; k < D; ++k) i *= n[k]; return i; }
 
   int launch_axis(int d, int flags, int C, int G, const c128* U1, const c128* U2, c128* snap) {
+    return launch_tile(f[d], outer(d), inner(d), flags, C, G, U1, U2, snap, psi, psi, Ks);
+  }
+  struct Store {   // F_XOUT map (see Flags)
+    long nlo, sh, sl, se;
+  };
+  // one spo_axis_kernel pass with plan p over the [O][p.L][I] grid at src, stored to dst ([p.L][O][I] with F_XOUT)
+  int launch_tile(const Fft& p, long O, long I, int flags, int C, int G, const c128* U1, const c128* U2, c128* snap,
+                  c128* src, c128* dst, const c128* K, Store sm = {1, 0, 0, 0}) {
+    const int L = p.L;
     AxisArgs a;
-    a.psi = psi;
-    a.O = (int)outer(d);
-    a.L = n[d];
-    a.I = (int)inner(d);
+    a.psi = src;
+    a.out = dst;
+    a.sh = sm.sh;
+    a.sl = sm.sl;
+    a.se = sm.se;
+    a.dlo = make_fdiv((unsigned)sm.nlo);
+    a.O = (int)O;
+    a.L = L;
+    a.I = (int)I;
     a.C = C;
-    a.dLC = make_fdiv((unsigned)(n[d] * C));
+    a.dLC = make_fdiv((unsigned)(L * C));
     a.dC = make_fdiv((unsigned)C);
-    a.dLns = make_fdiv((unsigned)(n[d] * ns));
+    a.dLns = make_fdiv((unsigned)(L * ns));
     a.dns = make_fdiv((unsigned)ns);
     a.G = G;
     a.flags = flags;
@@ -838,20 +897,20 @@ struct Exec {
     a.U1 = U1;
     a.U2 = U2;
     a.snap = snap;
-    a.K = Ks;
+    a.K = K;
     a.Ky = Ky;
-    size_t lds = (size_t)2 * G * C * f[d].M * sizeof(c128);
-    a.twl = lds + (size_t)f[d].M * sizeof(c128) <= LDS_MAX;
-    if (a.twl) lds += (size_t)f[d].M * sizeof(c128);
+    size_t lds = (size_t)2 * G * C * p.M * sizeof(c128);
+    a.twl = lds + (size_t)p.M * sizeof(c128) <= LDS_MAX;
+    if (a.twl) lds += (size_t)p.M * sizeof(c128);
     // QD_SPO_AUX=1: stage the pass's operators with the tile (one load round trip per pass).  Off by default: same-box
     // A/B (profiles/r04/spo/spo_any_aux_*.txt) 200^2 x 2 25.3 vs 24.8 us per step, 500^2 x 2 50.3 vs 43.8 (the larger
     // tile lowers the workgroups per CU), so the operator loads are not what bounds these passes.
     a.u2same = U1 == U2;
     a.aux = 0;
     const char* xe = getenv("QD_SPO_AUX");   // 1: both kinds of pass, 2: kinetic passes only
-    if (xe && (xe[0] == '1' || (xe[0] == '2' && (flags & F_KMUL)))) {
-      const size_t ub = (size_t)G * n[d] * ns * ns * sizeof(c128) * ((flags & F_PT2) && !a.u2same ? 2 : 1);
-      const size_t kb = (size_t)n[d] * C * sizeof(c128);
+    if (xe && !(flags & F_KROW) && (xe[0] == '1' || (xe[0] == '2' && (flags & F_KMUL)))) {
+      const size_t ub = (size_t)G * L * ns * ns * sizeof(c128) * ((flags & F_PT2) && !a.u2same ? 2 : 1);
+      const size_t kb = (size_t)L * C * sizeof(c128);
       if ((flags & (F_PT1 | F_PT2)) && lds + ub <= LDS_MAX) {
         a.aux = 1;
         lds += ub;
@@ -862,9 +921,55 @@ struct Exec {
     }
     if ((flags & F_PT2) && !(flags & F_PT1) && a.aux == 1) a.aux = 0;   // (the staging loop keys on U1)
     (void)hipFuncSetAttribute((const void*)spo_axis_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
-    hipLaunchKernelGGL(spo_axis_kernel, dim3((a.O + G - 1) / G, (a.I + C - 1) / C), dim3(256), lds, st, f[d], a);
+    hipLaunchKernelGGL(spo_axis_kernel, dim3((a.O + G - 1) / G, (a.I + C - 1) / C), dim3(256), lds, st, p, a);
     QD_HIP(hipGetLastError());
     return QD_OK;
+  }
+
+  // rows per tile of a whole-row pass (C == I) over O rows of length L: stack short rows (< 256 elements per
+  // tile) while >= 256 tiles remain
+  int stack_rows(long O, int L, int c, int M) const {
+    const size_t line = (size_t)2 * M * sizeof(c128);
+    int g = 1;
+    while (g < O && (long)g * c * L < 256 && O / (2 * g) >= 256 && (size_t)(2 * g) * c * line <= LDS_SOFT) g *= 2;
+    return (int)std::min<long>(g, O);
+  }
+  // xpose passes (D == 2): the row pass over psi ([n0][n1][ns] rows), stored transposed into tmp when xout; the
+  // kinetic pass over tmp's x lines ([n1][n0][ns]) with exp_K / N transposed, stored transposed back into psi
+  int row_pass(int flags, const c128* U1, const c128* U2, c128* snap, bool xout) {
+    const int G = stack_rows(n[0], n[1], ns, f[1].M);
+    return launch_tile(f[1], n[0], ns, flags | (xout ? F_XOUT : 0), ns, G, U1, U2, snap, psi, xout ? tmp : psi, Ks,
+                       Store{n[0], 0, ns, (long)n[0] * ns});
+  }
+  int kin_pass() {
+    return launch_tile(f[0], n[1], ns, F_KMUL | F_KROW | F_XOUT, ns, kin_g, nullptr, nullptr, nullptr, tmp, psi, KsT,
+                       Store{n[1], 0, ns, (long)n[1] * ns});
+  }
+  // D == 3 rotation (n0, n1, n2 = x, y, z; canonical C = [x][y][z] in psi):
+  //   z pass   reads C (psi), FWD: stores [x][z][y] into tmp (else in place)
+  //   y FWD    reads [x][z][y] (tmp), stores [z][y][x] into psi
+  //   x KMUL   reads [z][y][x] (psi, exp_K / N permuted to match), stores [x][z][y] into tmp
+  //   y INV    reads [x][z][y] (tmp), stores C into psi
+  int z3_pass(int flags, const c128* U1, const c128* U2, c128* snap) {
+    const bool xo = flags & F_FWD;
+    const long O = (long)n[0] * n[1];
+    const int G = stack_rows(O, n[2], ns, f[2].M);
+    return launch_tile(f[2], O, ns, flags | (xo ? F_XOUT : 0), ns, G, U1, U2, snap, psi, xo ? tmp : psi, Ks,
+                       Store{n[1], (long)n[2] * n[1] * ns, ns, (long)n[1] * ns});
+  }
+  int y3_pass(bool inv) {
+    const long O = (long)n[0] * n[2];
+    const int G = stack_rows(O, n[1], ns, f[1].M);
+    if (!inv)
+      return launch_tile(f[1], O, ns, F_FWD | F_XOUT, ns, G, nullptr, nullptr, nullptr, tmp, psi, Ks,
+                         Store{n[2], ns, (long)n[1] * n[0] * ns, (long)n[0] * ns});
+    return launch_tile(f[1], O, ns, F_INV | F_XOUT, ns, G, nullptr, nullptr, nullptr, tmp, psi, Ks,
+                       Store{n[2], (long)n[1] * n[2] * ns, ns, (long)n[2] * ns});
+  }
+  int x3_pass() {
+    const long O = (long)n[2] * n[1];
+    return launch_tile(f[0], O, ns, F_KMUL | F_KROW | F_XOUT, ns, kin_g, nullptr, nullptr, nullptr, psi, tmp, KsT,
+                       Store{n[1], (long)n[1] * ns, ns, (long)n[2] * n[1] * ns});
   }
 
   // lines-per-tile choice for an LDS pass over axis d; C == I (whole rows) required for point ops
@@ -882,10 +987,7 @@ struct Exec {
     }
     if ((size_t)c * line > LDS_MAX) return false;
     int g = 1;
-    if (c == I) {   // whole rows: stack short rows (< 256 elements per tile) while >= 256 tiles remain
-      while (g < O && (long)g * c * n[d] < 256 && O / (2 * g) >= 256 && (size_t)(2 * g) * c * line <= LDS_SOFT) g *= 2;
-      g = (int)std::min<long>(g, O);
-    }
+    if (c == I) g = stack_rows(O, n[d], c, f[d].M);   // whole rows
     *C = c;
     *G = g;
     return true;
@@ -953,6 +1055,44 @@ int run_nd(Exec& x, const c128* Uh, const c128* Ufull, int nsteps, int nout, c12
   const int kyf = ky ? F_KY : 0;
   const size_t grid_elems = (size_t)x.npts * x.ns;
   int rc;
+  if (x.xpose && D == 3) {   // the same pass sequence over the rotated layouts (Exec::z3_pass)
+    if ((rc = x.z3_pass(F_PT1 | F_FWD, Uh, nullptr, nullptr))) return rc;
+    if ((rc = x.y3_pass(false))) return rc;
+    for (int s = 1; s <= nsteps; ++s) {
+      if ((rc = x.x3_pass())) return rc;
+      if ((rc = x.y3_pass(true))) return rc;
+      const bool take = snap && (s % nout == 0);
+      c128* sp = take ? snap + (size_t)(s / nout - 1) * grid_elems : nullptr;
+      int flags = F_INV | F_PT1 | (take ? F_SNAP : 0);
+      if (Ufull) flags |= F_FWD;
+      else if (s < nsteps) flags |= F_PT2 | F_FWD;
+      if ((rc = x.z3_pass(flags, Ufull ? Ufull : Uh, Uh, sp))) return rc;
+      if ((flags & F_FWD) && (rc = x.y3_pass(false))) return rc;
+    }
+    if (Ufull) {
+      if ((rc = x.x3_pass())) return rc;
+      if ((rc = x.y3_pass(true))) return rc;
+      if ((rc = x.z3_pass(F_INV | F_PT1, Uh, nullptr, nullptr))) return rc;
+    }
+    return QD_OK;
+  }
+  if (x.xpose) {   // D == 2, nsteps >= 1: the same pass sequence with the row pass storing into the other layout
+    if ((rc = x.row_pass(F_PT1 | F_FWD | kyf, Uh, nullptr, nullptr, true))) return rc;
+    for (int s = 1; s <= nsteps; ++s) {
+      if ((rc = x.kin_pass())) return rc;
+      const bool take = snap && (s % nout == 0);
+      c128* sp = take ? snap + (size_t)(s / nout - 1) * grid_elems : nullptr;
+      int flags = F_INV | F_PT1 | (take ? F_SNAP : 0);
+      if (Ufull) flags |= F_FWD | kyf;
+      else if (s < nsteps) flags |= F_PT2 | F_FWD | kyf;
+      if ((rc = x.row_pass(flags, Ufull ? Ufull : Uh, Uh, sp, (flags & F_FWD) != 0))) return rc;
+    }
+    if (Ufull) {
+      if ((rc = x.kin_pass())) return rc;
+      if ((rc = x.row_pass(F_INV | F_PT1, Uh, nullptr, nullptr, false))) return rc;
+    }
+    return QD_OK;
+  }
   if ((rc = x.pass(last, F_PT1 | F_FWD | kyf, Uh, nullptr, nullptr))) return rc;
   for (int d = last - 1; d >= 1; --d)
     if ((rc = x.pass(d, F_FWD, nullptr, nullptr, nullptr))) return rc;
@@ -1060,7 +1200,7 @@ int spo_generic_run(c128* psi, const c128* expVh, const c128* expV, const c128* 
     x.n[d] = dims[d];
     x.npts *= dims[d];
   }
-  size_t slots = (size_t)x.npts * ns + x.npts;   // tmp grid + exp_K / N
+  size_t slots = (size_t)x.npts * ns + 2 * x.npts;   // tmp grid + exp_K / N (+ transposed)
   for (int d = 0; d < D; ++d) slots += plan_slots(dims[d]);
   void* w = nullptr;
   int rc = workspace(WS_SPO, slots * sizeof(c128), &w, st);
@@ -1077,6 +1217,32 @@ int spo_generic_run(c128* psi, const c128* expVh, const c128* expV, const c128* 
   QD_HIP(hipGetLastError());
   x.Ks = ks;
   x.Ky = expKy;
+  // alternating layouts (2D, every axis an LDS plan whose whole-row tile fits; QD_SPO_XPOSE=0: in-place passes)
+  {
+    const char* xev = getenv("QD_SPO_XPOSE");   // read per run (tests switch it)
+    const bool xe = !(xev && xev[0] == '0');
+    // 3D rotation: opt-in (QD_SPO_XPOSE3=1).  Same-box A/B (profiles/r04/spo/spo_xpose_ab.txt): 60^3 x 2 55.4 -> 54.4 us
+    // per step, but 96^3 126.5 -> 143.4 and 100^3 140.7 -> 161.7: three of the four 3D passes then store scattered
+    // 32-B pieces at large strides, which costs more than the strided loads they remove
+    const char* x3v = getenv("QD_SPO_XPOSE3");
+    const bool x3 = x3v && x3v[0] == '1';
+    bool fit = nsteps >= 1 && (D == 2 || (D == 3 && x3));
+    for (int d = 0; d < D && fit; ++d)   // every axis a whole-row LDS pass (C == ns)
+      fit = x.f[d].kind != DIRECT && (size_t)2 * ns * x.f[d].M * sizeof(c128) <= LDS_MAX;
+    x.xpose = xe && fit;
+    if (x.xpose) {
+      c128* kt = tab;   // behind the plan tables
+      if (D == 2)
+        hipLaunchKernelGGL(scale_transpose_kernel, dim3(grid_for(x.npts)), dim3(256), 0, st, expK, kt, dims[0], dims[1],
+                           1.0 / (double)x.npts);
+      else
+        hipLaunchKernelGGL(scale_permute3_kernel, dim3(grid_for(x.npts)), dim3(256), 0, st, expK, kt, dims[0], dims[1],
+                           dims[2], 1.0 / (double)x.npts);
+      QD_HIP(hipGetLastError());
+      x.KsT = kt;
+      x.kin_g = x.stack_rows(x.npts / dims[0], dims[0], ns, x.f[0].M);
+    }
+  }
 #ifdef QD_PHASE_TIMING
   {
     unsigned long long z[2][6] = {};

@@ -302,12 +302,18 @@ def test_deom_tier_bands_loopback_matches_single(ns, npsd, L, nbands):
     assert relerr(ados, sol.ddos[0]) < 1e-13
 
 
+# the batched bench line's stage kernels: the software-pipelined persistent kernel (default, round 4), the five-waves
+# instantiation (QD_DEOM_PIPE=0) and the unconstrained one (QD_DEOM_PIPE=0 QD_DEOM_W5=0)
+_BATCH_KERNELS = {"pipe": {"QD_DEOM_PIPE": "1"}, "w5": {"QD_DEOM_PIPE": "0", "QD_DEOM_W5": "1"},
+                  "plain": {"QD_DEOM_PIPE": "0", "QD_DEOM_W5": "0"}}
+
+
 @pytest.mark.parametrize("B", [64, 72])
 def test_deom_batched_w5_kernel_matches_oracle_and_unconstrained(B, monkeypatch):
-    """The batched bench line's stage kernel (deom_stage_grp_w5_kernel: K = 5, Horner form, >= 64 hierarchies,
-    ADO-major with the default 8 XCD block classes): B = 64 (the bench) and 72 (ragged classes of
-    9), L = 6, 6 steps.  Bit-identical to the unconstrained instantiation (QD_DEOM_W5=0) and to the oracle's RK4
-    (heom/deom.py:641-766, 1072-1114) at 1e-10 for the first, a middle and the last member."""
+    """The batched bench line's stage kernels (K = 5, Horner form, >= 64 hierarchies, ADO-major with the default 8 XCD
+    block classes): B = 64 (the bench) and 72 (ragged classes of 9), L = 6, 6 steps.  The
+    pipelined persistent kernel, deom_stage_grp_w5_kernel and the unconstrained instantiation agree bit for bit, and
+    match the oracle's RK4 (heom/deom.py:641-766, 1072-1114) at 1e-10 for the first, a middle and the last member."""
     from oracle import deom as od
     from pyqed_amd.deom import Bath, DEOMSolver
     w = sp.symbols(r"\omega", real=True)
@@ -320,24 +326,26 @@ def test_deom_batched_w5_kernel_matches_oracle_and_unconstrained(B, monkeypatch)
     rho0 = np.einsum("bi,bj->bij", psi, psi.conj())
     dt, nt, L = 0.005, 6, 6
     out = {}
-    for w5 in ("1", "0"):
-        monkeypatch.setenv("QD_DEOM_W5", w5)
+    for name, env in _BATCH_KERNELS.items():
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
         sol = DEOMSolver(sz + sx, None, bath, np.array([sx]), None, None, None, L)
         _, saved = sol.run_batch(rho0, dt, nt)
         assert sol.nind == 5
-        out[w5] = (np.array(saved), sol.ddos.copy())
-    assert np.array_equal(out["1"][0], out["0"][0]) and np.array_equal(out["1"][1], out["0"][1])
+        out[name] = (np.array(saved), sol.ddos.copy())
+    for name in ("w5", "plain"):
+        assert np.array_equal(out["pipe"][0], out[name][0]) and np.array_equal(out["pipe"][1], out[name][1]), name
     for b in (0, B // 2, B - 1):
         _, ref, _ = od.run(sz + sx, np.zeros((2, 2)), lambda t: 0, np.array([sx]), np.zeros((1, 2, 2)),
                            lambda t: 0, (bath.etal, bath.etar, bath.etaa, bath.expn), L, rho0[b], dt, nt)
-        assert relerr(out["1"][0][b], ref) < TOL, b
+        assert relerr(out["pipe"][0][b], ref) < TOL, b
 
 
 def test_deom_batched_w5_kernel_bench_hierarchy_matches_reference(monkeypatch):
     """64 hierarchies of the bench hierarchy (L = 12, K = 5: 6188 ADOs each, the bench's [nmax][B][2][2] layout and
     XCD dealing) for the reference fixture's 3 steps: member 0 starts from the fixture's |0><0| and its Tr(p1 rho_0)
-    equals deom_run_bench (the reference's own run) at 1e-10; every member equals the QD_DEOM_W5=0 kernel bit for
-    bit."""
+    equals deom_run_bench (the reference's own run) at 1e-10; every member is bit-identical across the pipelined,
+    five-waves and unconstrained kernels."""
     g = load_golden("deom_run_bench")
     B = 64
     rng = np.random.default_rng(64)
@@ -350,17 +358,19 @@ def test_deom_batched_w5_kernel_bench_hierarchy_matches_reference(monkeypatch):
     w = sp.symbols(r"\omega", real=True)
     lam, gam, beta = float(g["lam"]), float(g["gam"]), float(g["beta"])
     out = {}
-    for w5 in ("1", "0"):
-        monkeypatch.setenv("QD_DEOM_W5", w5)
+    for name, env in _BATCH_KERNELS.items():
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
         # the fixture's pulses are zero, so the undriven solver (Horner-form stages, the w5 kernel) runs the same
         # equations of motion as the reference's H + 0 * sdip
         bath = Bath([2 * lam * gam * w / (gam ** 2 + w ** 2)], w, [beta], [int(g["npsd"])], [0] * (1 + int(g["npsd"])))
         sol = DEOMSolver(g["H"], None, bath, g["Q"], None, None, None, int(g["lmax"]))
         t, tr = sol.run_batch(rho0, float(g["dt"]), int(g["nt"]), p1)
-        out[w5] = (np.array(tr), sol.ddos.copy())
+        out[name] = (np.array(tr), sol.ddos.copy())
     assert sol.nmax == 6188
-    assert relerr(out["1"][0][0], g["trace_p1"]) < TOL
-    assert np.array_equal(out["1"][0], out["0"][0]) and np.array_equal(out["1"][1], out["0"][1])
+    assert relerr(out["pipe"][0][0], g["trace_p1"]) < TOL
+    for name in ("w5", "plain"):
+        assert np.array_equal(out["pipe"][0], out[name][0]) and np.array_equal(out["pipe"][1], out[name][1]), name
 
 
 def test_gather_rows_bounds_checked():

@@ -133,3 +133,45 @@ def test_spo1d_long_line_direct_dft_matches_reference(monkeypatch):
     sol.set_potential(lambda q: q ** 2 / 2)
     r = sol.run(psi0, dt=0.01, nt=int(g[f"n{n}_nt"]), nout=int(g[f"n{n}_nout"]))
     assert relerr(r.psi, g[f"n{n}_psi"]) < TOL
+
+
+@pytest.mark.parametrize("name", ["spo2_96x80", "spo2_67x45_ns3"])
+def test_spo2_alternating_layouts_bit_identical_to_in_place_passes(name, monkeypatch):
+    """The 2D generic passes alternate [x][y][s] / [y][x][s] layouts (spo_gen.hip Exec::xpose): same FFT plans, same
+    operations on the same line values, so the result equals the in-place passes (QD_SPO_XPOSE=0) bit for bit —
+    Strang, merged-V and Jacobi step sequences — and the reference fixture."""
+    from pyqed_amd import SPO2
+    g, r1, x, y = _spo2(name)
+    _, r0, _, _ = _spo2(name, env={"QD_SPO_XPOSE": "0"})
+    assert np.array_equal(np.array(r1.psilist), np.array(r0.psilist))
+    assert relerr(np.array(r1.psilist), g["psilist"]) < TOL
+    xs, ys, surfaces, couplings, psi0 = spo2_model_rect(30, 22, 2)
+    for kw, coords in (({"return_states": False}, "linear"), ({}, "jacobi")):
+        mass = [1.0, 1.3] if coords == "linear" else [1.0, lambda q: 1.5 + 0.2 * q ** 2]
+        out = []
+        for xp in ("1", "0"):
+            monkeypatch.setenv("QD_SPO_XPOSE", xp)
+            sol = SPO2(xs, ys, mass=mass, nstates=2, coords=coords)
+            sol.set_DPES(surfaces, couplings)
+            out.append(sol.run(psi0, dt=0.05, nt=5, nout=2, **kw).psi)
+        assert np.array_equal(out[0], out[1]), coords
+
+
+def test_spo3_rotated_layouts_bit_identical_to_in_place_passes(monkeypatch):
+    """3D grids can rotate their layouts (QD_SPO_XPOSE3=1, opt-in): [x][y][z] -> [x][z][y] -> [z][y][x] -> [x][z][y]
+    -> [x][y][z] over a step's four passes (spo_gen.hip Exec::z3_pass), equal bit for bit to the in-place passes
+    (QD_SPO_XPOSE3=0), Strang and merged V."""
+    from pyqed_amd import SPO3
+    g = load_golden("spo3_24x20x18")
+    (x, y, z), masses, surfaces, couplings, psi0 = spo3_model()
+    out = {}
+    for xp in ("1", "0"):
+        monkeypatch.setenv("QD_SPO_XPOSE3", xp)
+        sol = SPO3(x, y, z, masses=masses, nstates=2)
+        sol.set_DPES(surfaces, couplings)
+        r = sol.run(psi0=psi0, dt=float(g["dt"]), nt=int(g["nt"]), nout=int(g["nout"]))
+        rm = sol.run(psi0=psi0, dt=float(g["dt"]), nt=3, nout=1, return_states=False)
+        out[xp] = (np.array(r.psilist), r.psi, rm.psi)
+    for a, b in zip(out["1"], out["0"]):
+        assert np.array_equal(a, b)
+    assert relerr(out["1"][0], g["psilist"]) < TOL

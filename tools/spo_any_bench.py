@@ -40,7 +40,10 @@ def timed(fn, steps):
 
 
 rng = np.random.default_rng(0)
+mode = sys.argv[2] if len(sys.argv) > 2 else "all"   # "2d": SPO2 cases only; "3d": SPO3 cases only
 cases2 = [int(x) for x in (sys.argv[1].split(",") if len(sys.argv) > 1 else "200,256,500,512,1000,1024".split(","))]
+if mode == "3d":
+    cases2 = []
 for n in cases2:
     ns = 2
     U = t(unit_ops((n, n), ns, rng))
@@ -71,7 +74,7 @@ for n in (48, 60, 64, 96, 100, 128):
     byts = 8 * n ** 3 * ns * 16 + n ** 3 * ns * ns * 16 + n ** 3 * 16
     print(json.dumps({"case": f"spo3 {n}^3x2", "us_per_step": round(sec * 1e6, 2), "steps_per_s": round(1 / sec, 1),
                       "GBps_4pass": round(byts / sec / 1e9, 1)}), flush=True)
-for n in (1000, 1024, 2048, 2053, 4096, 6000):
+for n in (() if mode == "3d" else (1000, 1024, 2048, 2053, 4096, 6000)):
     x = np.linspace(-8, 8, n)
     eV = t(np.exp(-1j * 0.01 * x ** 2 / 2))
     eVh = t(np.exp(-0.5j * 0.01 * x ** 2 / 2))
