@@ -35,6 +35,25 @@ HERM_NP64_MIN_BATCH = 160   # 33 <= N <= 64 (padded to 64): the general split-K 
                             # Hermitian DM-steps/s; B = 192 1.18M vs 1.40M)
 
 
+_HERM_CHECKED = {}   # id(H) -> (weakref to H, H._version, result)
+
+
+def _is_hermitian_cached(H: torch.Tensor) -> bool:
+    """H == H^+ bit for bit.  The check is a device reduction plus a host synchronisation, so its result is kept per
+    tensor object and version (a weak reference guards against a new tensor at a recycled id; an in-place update
+    bumps _version): repeated calls on the same Hamiltonian skip it."""
+    import weakref
+    key = id(H)
+    hit = _HERM_CHECKED.get(key)
+    if hit is not None and hit[0]() is H and hit[1] == H._version:
+        return hit[2]
+    res = bool(torch.equal(H, H.transpose(-1, -2).conj()))
+    if len(_HERM_CHECKED) > 64:
+        _HERM_CHECKED.clear()
+    _HERM_CHECKED[key] = (weakref.ref(H), H._version, res)
+    return res
+
+
 def lindblad_rk4(H: torch.Tensor, c_ops: torch.Tensor | None, rho: torch.Tensor, dt: float, nsteps: int,
                  e_ops: torch.Tensor | None = None, save_every: int = 0, stream=None,
                  hermitian: bool | None = None):
@@ -78,7 +97,7 @@ def lindblad_rk4(H: torch.Tensor, c_ops: torch.Tensor | None, rho: torch.Tensor,
     st = stream if stream is not None else _lib.stream_ptr(dev)
     # X + X^+ equals the reference's -i[H, rho] + D[rho] only for Hermitian H and rho (oqs.py:697-714 uses
     # rho H, not rho H^+), so the Hermitian kernel is gated on both, bit for bit.
-    h_herm = bool(torch.equal(H, H.transpose(-1, -2).conj()))
+    h_herm = _is_hermitian_cached(H)
     if hermitian is None:
         np64 = 32 < N <= 64 and os.environ.get("QD_GLF_HSPLIT_NP64") != "1"   # =1: the pair-block path (tests)
         min_b = HERM_NP64_MIN_BATCH if np64 else HERM_SPLIT_MIN_BATCH
