@@ -41,25 +41,36 @@ def measured_traffic(kernel: str, units: float):
     return (d["read_bytes_per_unit"] + d["write_bytes_per_unit"]) * units
 
 
-def ramp_warmup(fn, dev, min_ms=60.0, max_calls=10000):
-    """Untimed calls of a leg's own work until >= min_ms of it has run.  A leg whose inputs were just built on the host
+def ramp_warmup(fn, dev, min_ms=60.0, max_calls=10000, agree=False):
+    """Untimed calls of a leg's own work for >= min_ms of steady calls.  A leg whose inputs were just built on the host
     starts on an idle GPU, whose clocks take tens of ms to come up (profiles/r04/lindblad/launch_overhead.txt: a
-    20-step Lindblad launch after 20 ms idle runs 0.825 ms per step against 0.726 behind other work); the timed region
-    then measures the leg at the clocks a running job has, not the ramp."""
+    20-step Lindblad launch after 20 ms idle runs 0.825 ms per step against 0.726 behind other work;
+    tools/ramp_probe*.py: a 2DES grid needs ~25 ms of sustained load); the timed region then measures the leg at the
+    clocks a running job has, not the ramp.  The number of calls is fixed from the second call's time, so that with
+    agree=True (legs whose calls issue collectives, world > 1) every rank makes the same number of calls: the ranks
+    take the largest count (one all-reduce before the loop)."""
     import torch
+    dev = torch.device(dev)
+    sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
     fn()                                  # first call: one-time setup (code objects, pool growth, cached operands)
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()              # the min_ms budget counts steady calls only
+    sync()
+    t0 = time.perf_counter()              # the budget counts steady calls only
     fn()
-    torch.cuda.synchronize(dev)
+    sync()
     one = max(time.perf_counter() - t0, 1e-6)
+    n = int(min(max_calls, max(0, np.ceil(min_ms / 1e3 / one) - 1)))
+    if agree:
+        import torch.distributed as dist
+        c = torch.tensor([n], dtype=torch.int64, device=dev)
+        dist.all_reduce(c, op=dist.ReduceOp.MAX)
+        n = int(c.item())
     per_sync = max(1, int(0.005 / one))   # short calls are queued back to back, ~5 ms of work per synchronisation
-    calls = 2
-    while (time.perf_counter() - t0) * 1e3 < min_ms and calls < max_calls:
-        for _ in range(per_sync):
+    done = 0
+    while done < n:
+        for _ in range(min(per_sync, n - done)):
             fn()
-        calls += per_sync
-        torch.cuda.synchronize(dev)
+        done += min(per_sync, n - done)
+        sync()
 
 
 def synthetic_lindblad(N, seed_h=0, seed_c=1, nc=1, gamma=0.1):
@@ -337,7 +348,7 @@ def bench_2des(dev, world, rank, M_total, reps, n=256):
         once()
         pipe.finish()
 
-    ramp_warmup(warm, dev)
+    ramp_warmup(warm, dev, agree=world > 1)   # its calls issue the RCCL reduce at world > 1
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -440,7 +451,7 @@ def bench_2des_t2scan(dev, world, rank, M_total, n2, reps, n=256):
         scan[0] = T2Scan(lam_t, alpha_t, B_t, C_t, beta_t, t, t)
         sharded_sum_buckets(local, M_total, out, buckets, dst=0)
 
-    ramp_warmup(once, dev)
+    ramp_warmup(once, dev, agree=world > 1)   # its calls issue the bucket reduces at world > 1
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)

@@ -409,3 +409,43 @@ def test_deom_tier_bands_allgather_gloo():
     assert np.allclose(res[0][1], tr_ref, rtol=1e-12, atol=1e-13)
     assert np.allclose(res[0][2], ados_ref, rtol=1e-11, atol=1e-13)
     assert all(r[4] > 0 for r in res)          # every band has halo rows
+
+
+# ---------------------------------------------------------------- bench warm-up under collectives
+def _worker_ramp(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    import time
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    calls = [0]
+    x = torch.ones(4)
+
+    def fn():                           # a leg call that issues a collective, slower on rank 1
+        time.sleep(0.002 * (1 + 2 * rank))
+        dist.all_reduce(x)
+        calls[0] += 1
+
+    bench.ramp_warmup(fn, "cpu", min_ms=40.0, agree=True)
+    q.put((rank, calls[0]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ramp_warmup_agrees_on_call_count_gloo():
+    """bench.ramp_warmup(agree=True) (the 2DES legs, whose calls issue the reduce at world > 1): ranks whose calls take
+    different times still make the same number of calls, so no collective is left unmatched."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_ramp, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][1] == res[1][1] >= 3, res
