@@ -1090,7 +1090,7 @@ def main():
     ap.add_argument("--ens", type=int, default=65536,
                     help="2DES disorder-ensemble members (total; strong scaling: enough work to split 8 ways; "
                          "65,536 leaves each of 8 ranks 8,192 members, 0.2 ms per grid)")
-    ap.add_argument("--ens-reps", type=int, default=20)
+    ap.add_argument("--ens-reps", type=int, default=50)   # >= 8 ms timed even for an 8-way shard
     ap.add_argument("--no-2des", action="store_true")
     ap.add_argument("--t2", type=int, default=16, help="2DES waiting times per scan (0 = skip the scan leg)")
     ap.add_argument("--t2-reps", type=int, default=3)
