@@ -18,6 +18,7 @@
 // epilogue does the RK4 bookkeeping (deom_rk4_next: the classic acc form for
 // driven runs, the accumulator-free Horner form when the generator is constant
 // over the step) and records rho_0 (the system density matrix) after every step.
+#include "handoff.hpp"
 #include "qd_common.hpp"
 
 #include <cstdlib>
@@ -1401,21 +1402,6 @@ constexpr int BAND_HM = 8;   // halo elements per thread held as precomputed off
 #ifndef DEOM_BAND_EARLY
 #define DEOM_BAND_EARLY 1   // undriven runs: the next stage's damping + coherent part computed before the poll (A/B: 0)
 #endif
-typedef unsigned int band_u4 __attribute__((ext_vector_type(4)));
-
-// 16-B write-through (sc1) buffer load / store of one complex element at byte offset `off`
-__device__ __forceinline__ c128 ld16_sc1(__amdgpu_buffer_rsrc_t r, int off) {
-  const band_u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
-  return cmk(__builtin_bit_cast(double, (unsigned long long)v.x | ((unsigned long long)v.y << 32)),
-             __builtin_bit_cast(double, (unsigned long long)v.z | ((unsigned long long)v.w << 32)));
-}
-__device__ __forceinline__ void st16_sc1(__amdgpu_buffer_rsrc_t r, int off, c128 x) {
-  const unsigned long long a = __builtin_bit_cast(unsigned long long, x.re);
-  const unsigned long long b = __builtin_bit_cast(unsigned long long, x.im);
-  const band_u4 v = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
-}
-
 __device__ __forceinline__ c128 ld_sc1(const c128* q) {
   return cmk(__hip_atomic_load(&q->re, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
              __hip_atomic_load(&q->im, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -1592,12 +1578,6 @@ __global__ __launch_bounds__(TPB) void deom_band_kernel(BandParams p) {
     hsrc[h] = q < nhe ? (p.halo_idx[hoff + q / ns2] * ns2 + q % ns2) * 16 : -1;
   }
   const int slab_bytes = __builtin_amdgcn_readfirstlane((int)(slab * sizeof(c128)));
-  // buffer descriptors from provably wave-uniform inputs (no waterfall loops around the buffer ops)
-  auto uni = [](const void* q) -> void* {
-    const unsigned long long v = (unsigned long long)q;
-    const unsigned l = __builtin_amdgcn_readfirstlane((unsigned)v), h = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-    return (void*)(((unsigned long long)h << 32) | l);
-  };
 #ifdef QD_PHASE_TIMING
   unsigned long long tph[4] = {0, 0, 0, 0};
 #endif
@@ -1605,9 +1585,9 @@ __global__ __launch_bounds__(TPB) void deom_band_kernel(BandParams p) {
   for (int g = 0; g < G4; ++g) {
     const int step = g >> 2, stage = g & 3;
     const c128* in = g == 0 ? p.ados : p.buf + (size_t)((g - 1) & 1) * slab;
-    const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(uni(in), (short)0, slab_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rin = sc1_rsrc(in, slab_bytes);
     const __amdgpu_buffer_rsrc_t rout =
-        __builtin_amdgcn_make_buffer_rsrc(uni(p.buf + (size_t)(g & 1) * slab), (short)0, slab_bytes, 0x00020000);
+        sc1_rsrc(p.buf + (size_t)(g & 1) * slab, slab_bytes);
 #ifdef QD_PHASE_TIMING
     const unsigned long long t0 = wall_clock64();
 #endif

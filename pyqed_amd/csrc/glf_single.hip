@@ -27,6 +27,7 @@
 // Observables: each workgroup sums Tr(E rho) over its tile after every step into a partial slot, and one small
 // kernel adds the T^2 partials in fixed order after the launch.
 #include "glf_kernel.hpp"
+#include "handoff.hpp"
 
 namespace qd {
 namespace {
@@ -63,28 +64,6 @@ struct SingleParams {
 #else
 #define SG_MARK(k)
 #endif
-
-typedef unsigned int sg_u4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ c128 sg_ld(__amdgpu_buffer_rsrc_t r, int off) {   // 16-B sc1 load
-  const sg_u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
-  return cmk(__builtin_bit_cast(double, (unsigned long long)v.x | ((unsigned long long)v.y << 32)),
-             __builtin_bit_cast(double, (unsigned long long)v.z | ((unsigned long long)v.w << 32)));
-}
-__device__ __forceinline__ void sg_st(__amdgpu_buffer_rsrc_t r, int off, c128 x) {   // 16-B write-through store
-  const unsigned long long a = __builtin_bit_cast(unsigned long long, x.re);
-  const unsigned long long c = __builtin_bit_cast(unsigned long long, x.im);
-  const sg_u4 v = {(unsigned)a, (unsigned)(a >> 32), (unsigned)c, (unsigned)(c >> 32)};
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
-}
-__device__ __forceinline__ void* sg_uni(const void* q) {   // provably wave-uniform pointer for a buffer descriptor
-  const unsigned long long v = (unsigned long long)q;
-  const unsigned l = __builtin_amdgcn_readfirstlane((unsigned)v), h = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-  return (void*)(((unsigned long long)h << 32) | l);
-}
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t sg_rsrc(const void* base, int bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(sg_uni(base), (short)0, bytes, 0x00020000);
-}
 
 // one complex k-step of a 16 x 16 tile: acc += a b (a: A fragment, b: B fragment of v_mfma_f64_16x16x4_f64)
 __device__ __forceinline__ void sg_mac(d4& re, d4& im, c128 a, c128 b) {
@@ -232,25 +211,25 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
         }))
       break;
     SG_MARK(0)
-    const __amdgpu_buffer_rsrc_t rr = sg_rsrc(rin, slab);
+    const __amdgpu_buffer_rsrc_t rr = sc1_rsrc(rin, slab);
     c128 rcol[KS], rrow[KS];
 #pragma unroll
     for (int q = 0; q < KS; ++q) {
       const int k = kb + 4 * q + lk;
-      rcol[q] = sg_ld(rr, ((b * Np + k) * Np + bn * 16 + lr) * 16);
-      rrow[q] = sg_ld(rr, ((b * Np + bm * 16 + lr) * Np + k) * 16);
+      rcol[q] = ld16_sc1(rr, ((b * Np + k) * Np + bn * 16 + lr) * 16);
+      rrow[q] = ld16_sc1(rr, ((b * Np + bm * 16 + lr) * Np + k) * 16);
     }
     // ---- Y_c(bm, bn) = L_c[bm, :] r[:, bn], published for the k phase of the row
     c128* ybase = p.ybuf + (size_t)(g & 1) * NC * mats * NN;
     if constexpr (NC > 0) {
-      const __amdgpu_buffer_rsrc_t ry = sg_rsrc(ybase, NC * slab);
+      const __amdgpu_buffer_rsrc_t ry = sc1_rsrc(ybase, NC * slab);
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         SgAcc<M3> acc;
 #pragma unroll
         for (int q = 0; q < KS; ++q) acc.mac(aL[c][q], rcol[q]);
         const c128 y = reduce(acc);
-        if (owner) sg_st(ry, (((c * mats + b) * Np + orow) * Np + ocol) * 16, y);
+        if (owner) st16_sc1(ry, (((c * mats + b) * Np + orow) * Np + ocol) * 16, y);
         __syncthreads();   // red is reused by the next reduction
       }
       publish(1, (unsigned)(g + 1));
@@ -266,13 +245,13 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
     if constexpr (NC > 0) {
       if (!wait_for(T, 1, (unsigned)(g + 1), [&](int l) { return b * T * T + bm * T + l; })) break;
       SG_MARK(3)
-      const __amdgpu_buffer_rsrc_t ry = sg_rsrc(ybase, NC * slab);
+      const __amdgpu_buffer_rsrc_t ry = sc1_rsrc(ybase, NC * slab);
       c128 yrow[NC][KS];
 #pragma unroll
       for (int c = 0; c < NC; ++c)
 #pragma unroll
         for (int q = 0; q < KS; ++q)
-          yrow[c][q] = sg_ld(ry, (((c * mats + b) * Np + bm * 16 + lr) * Np + kb + 4 * q + lk) * 16);
+          yrow[c][q] = ld16_sc1(ry, (((c * mats + b) * Np + bm * 16 + lr) * Np + kb + 4 * q + lk) * 16);
 #pragma unroll
       for (int c = 0; c < NC; ++c)
 #pragma unroll
@@ -283,7 +262,7 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
     const double hc = rk4_horner_coef(p.dt, m);
     const c128 v = cadd(rh, cscale(kv, hc));
     if (m == 3) rh = v;
-    if (owner && g + 1 < G4) sg_st(sg_rsrc(p.rbuf + (size_t)((g + 1) & 1) * mats * NN, slab),
+    if (owner && g + 1 < G4) st16_sc1(sc1_rsrc(p.rbuf + (size_t)((g + 1) & 1) * mats * NN, slab),
                                    ((b * Np + orow) * Np + ocol) * 16, v);
     if (m == 3) {
       const int gs = p.step0 + s + 1;
