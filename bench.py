@@ -561,9 +561,7 @@ def bench_spo2(dev, steps, n=256, dt=0.05):
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     ev = e0.elapsed_time(e1) / 1e3
-    bytes_per_step = (4 * n * n * 2 + n * n * 4 + n * n) * 16  # psi r/w x2 passes, exp_V_half, exp_K
-    # 256 x 256 x 2 runs as one persistent launch (spo2_persist_kernel) unless QD_SPO_PERSIST=0
-    spo2_persist = n == 256 and os.environ.get("QD_SPO_Q16", "1") != "0" and os.environ.get("QD_SPO_PERSIST", "1") != "0"
+    bytes_per_step = (4 * n * n * 2 + n * n * 4 + n * n) * 16  # psi r/w x2 kernels, exp_V_half, exp_K
     norm = float((psi.abs() ** 2).sum().item() / (np.abs(psi0) ** 2).sum())
     # drop-in end to end: SPO2.run (device build of the point propagators + upload + steps + download)
     sol.build(dt)
@@ -612,27 +610,16 @@ def bench_spo2(dev, steps, n=256, dt=0.05):
         "roofline": {"bound": "hbm", "achieved": round(bytes_per_step * steps / ev / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(bytes_per_step * steps / ev / 1e9 / HBM_PEAK_GBS, 4),
                      "bytes_per_step": bytes_per_step,
-                     "traffic": spo2_traffic(n),
+                     "traffic": (measured_traffic("spo2_row_q16_kernel<2>", 1) + measured_traffic("spo2_col_q16_kernel<2>", 1))
+                     if n == 256 and os.environ.get("QD_SPO_Q16", "1") != "0" else None,
                      "traffic_unit": "HBM bytes per Strang step (row + column pass; PMC FETCH_SIZE+WRITE_SIZE, calibrated; "
                                      "profiles/pmc_traffic.json)",
-                     "kernel": "spo2_persist_kernel (the whole run as one launch)" if spo2_persist
-                               else "spo2_row_q16_kernel<2> + spo2_col_q16_kernel<2> per step",
                      "note": "working set (7 MiB) is MALL-resident; two dependent passes per step bound it (latency)"},
         "us_per_step": round(wall / steps * 1e6, 2), "norm_ratio": norm,
         "build_ms": round(build_ms, 3),
         "run_wall_s": round(run_wall, 4),
         "run_note": f"SPO2.run(nt={steps}) end to end incl. build, transfers and the 2 returned states",
     }
-
-
-def spo2_traffic(n):
-    """PMC bytes per Strang step of the single-wavefunction 256 x 256 x 2 run, for the path that ran."""
-    if n != 256 or os.environ.get("QD_SPO_Q16", "1") == "0":
-        return None
-    if os.environ.get("QD_SPO_PERSIST", "1") != "0":
-        return measured_traffic("spo2_persist_kernel", 1)
-    row, col = measured_traffic("spo2_row_q16_kernel<2>", 1), measured_traffic("spo2_col_q16_kernel<2>", 1)
-    return row + col if row is not None and col is not None else None
 
 
 def bench_spo3(dev, steps=200, n=64, dt=0.05):

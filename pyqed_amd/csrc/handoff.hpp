@@ -3,7 +3,7 @@
 // wave drains (s_waitcnt vmcnt(0)), a workgroup barrier, then one lane stores the epoch word (relaxed agent atomic);
 // the consumer polls the epochs with relaxed agent loads from one wave, joins a workgroup barrier, and loads the
 // handed-off bytes with 16-B sc1 buffer loads only (never a plain or flat load of them).  One workgroup per CU.
-// Users: glf_single.hip (one trajectory), deom.hip (banded hierarchy), spo.hip (persistent SPO2 step loop).
+// Users: glf_single.hip (one trajectory), deom.hip (banded hierarchy).
 #pragma once
 #include "qd_common.hpp"
 

@@ -19,7 +19,6 @@
 // separately (no V/2 V/2 -> V merge) so every step is the reference's
 // return_states=True arithmetic.  psi is read and written once per kernel;
 // exp_V_half (ns^2 per point) once per row pass, exp_K once per column pass.
-#include "handoff.hpp"
 #include "qd_common.hpp"
 
 #include <cstdlib>
@@ -840,143 +839,6 @@ __global__ __launch_bounds__(64) void spo2_col_q16_kernel(c128* psi, const c128*
   for (int a = 0; a < 4; ++a) psi[((size_t)(64 * a + 16 * s + g) * pitch + j) * NS + c] = x[0][a];
 }
 
-// One wavefunction on a 256 x 256 x 2 grid, the whole Strang run as ONE persistent launch (qd_spo2_run's default at
-// that shape).  The two kernels above pay a kernel boundary (end-of-grid drain, dispatch of the next grid, reload of
-// the point operators, exp_K and twiddles) twice per step; here workgroup i (256 workgroups, one per CU) owns row i in
-// the row passes and column i in the column passes, wave c = state c, and its row's point operators, its column's
-// exp_K / (nx ny) factors and the twiddles stay in registers for the whole run.  Consecutive passes are separated by
-// a grid-wide hand-off inside the launch (handoff.hpp form): every workgroup publishes its pass epoch after its sc1
-// stores drained, and before pass k every workgroup waits until all 256 epochs reached k (wave 0 polls 4 words per
-// lane).  psi is updated in place: a pass writes only the elements it read, and no workgroup starts pass k + 1
-// before every workgroup has finished pass k.  Same operations in the same order as spo2_row_q16_kernel<2, false>
-// and spo2_col_q16_kernel<2>; the results agree with the two-kernel loop to rounding (the compiler contracts a few
-// multiply-adds differently; tests/test_spo_gpu.py).  Every spin is bounded; a timeout sets *status and the host
-// restores psi and re-runs the two-kernel loop.
-constexpr int SP_WG = 256;
-constexpr int SP_FLAG_STRIDE = 16;                 // 64-B epoch slots
-constexpr unsigned SP_SPIN_LIMIT = 1u << 22;       // polls (s_sleep between): ~2 s
-constexpr int SP_LDS_BYTES = 96 * 1024;            // more than half a CU's LDS: one workgroup per CU
-
-struct Spo2PersistParams {
-  c128* psi;            // [256][256][2], in / out
-  const c128* U;        // exp_V_half [256 * 256][2][2]
-  const c128* expKT;    // exp_K^T / (nx ny) [256 (column)][256 (row)]
-  const c128* tw;       // 256 twiddles
-  c128* snap;           // [nsave][256][256][2] or null
-  unsigned* flags;      // [256][SP_FLAG_STRIDE] pass epochs
-  int* status;
-  int nsteps, nout;
-};
-
-__global__ __launch_bounds__(128) void spo2_persist_kernel(Spo2PersistParams p) {
-  extern __shared__ c128 sp_dyn[];
-  __shared__ int sAbort;
-  c128* S = sp_dyn;               // [2][272] per-wave FFT exchange
-  c128* Xs = sp_dyn + 2 * 272;    // [2][256] point-operator exchange: [state][lane * 4 + a]
-  const int i = blockIdx.x, tid = threadIdx.x, c = tid >> 6, lane = tid & 63, g = lane >> 2, s = lane & 3;
-  const size_t row = (size_t)i * 256;
-  c128 x[1][4], u[4][2], kf[4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    const size_t pt = row + 64 * a + 16 * s + g;
-#pragma unroll
-    for (int b = 0; b < 2; ++b) u[a][b] = p.U[(pt * 2 + c) * 2 + b];   // row c of the point's operator
-    kf[a] = p.expKT[row + 64 * a + 16 * s + g];                         // column i's factors
-  }
-  const Q16Tw t = q16_twiddles(p.tw, g, s);
-  c128* Sw = S + c * 272;
-  if (tid == 0) sAbort = 0;
-  const __amdgpu_buffer_rsrc_t rp = sc1_rsrc(p.psi, 256 * 256 * 2 * (int)sizeof(c128));
-  unsigned* fl = p.flags;
-
-  auto wait_all = [&](unsigned target) -> bool {
-    if (c == 0) {
-      unsigned spins = 0;
-      for (;;) {
-        bool ok = true;
-#pragma unroll
-        for (int q = 0; q < SP_WG / 64; ++q)
-          ok = ok && __hip_atomic_load(fl + (size_t)(lane + 64 * q) * SP_FLAG_STRIDE, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT) >= target;
-        if (__all(ok)) break;
-        ++spins;
-        if (spins > SP_SPIN_LIMIT ||
-            ((spins & 255) == 0 && __hip_atomic_load(p.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
-          if (lane == 0) {
-            sAbort = 1;
-            __hip_atomic_store(p.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the payload loads below the poll
-    __syncthreads();
-    return sAbort == 0;
-  };
-  auto publish = [&](unsigned epoch) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's write-through stores are complete
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(fl + (size_t)i * SP_FLAG_STRIDE, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  };
-  auto point_op = [&]() {
-#pragma unroll
-    for (int a = 0; a < 4; ++a) Xs[c * 256 + lane * 4 + a] = x[0][a];
-    __syncthreads();
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      c128 acc = cmk(0, 0);
-#pragma unroll
-      for (int b = 0; b < 2; ++b) acc = cadd(acc, cmul(u[a][b], Xs[b * 256 + lane * 4 + a]));
-      x[0][a] = acc;
-    }
-    __syncthreads();   // Xs is rewritten by the next operator
-  };
-  // row pass: [IFFT_y] -> V/2 -> [snapshot] -> [V/2] -> [FFT_y]
-  auto row_pass = [&](int flags, c128* sp) {
-#pragma unroll
-    for (int a = 0; a < 4; ++a) x[0][a] = ld16_sc1(rp, (int)(((row + 64 * a + 16 * s + g) * 2 + c) * sizeof(c128)));
-    if (flags & ROW_INV) fft256_wave<true, 1>(x, t, Sw, g, s);
-    if (flags & ROW_VH1) point_op();
-    if (flags & ROW_SNAP) {
-#pragma unroll
-      for (int a = 0; a < 4; ++a) sp[(row + 64 * a + 16 * s + g) * 2 + c] = x[0][a];
-    }
-    if (flags & ROW_VH2) point_op();
-    if (flags & ROW_FWD) fft256_wave<false, 1>(x, t, Sw, g, s);
-#pragma unroll
-    for (int a = 0; a < 4; ++a) st16_sc1(rp, (int)(((row + 64 * a + 16 * s + g) * 2 + c) * sizeof(c128)), x[0][a]);
-  };
-  // column pass: FFT_x -> * exp_K / (nx ny) -> IFFT_x
-  auto col_pass = [&]() {
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-      x[0][a] = ld16_sc1(rp, (int)((((size_t)(64 * a + 16 * s + g) * 256 + i) * 2 + c) * sizeof(c128)));
-    fft256_wave<false, 1>(x, t, Sw, g, s);
-#pragma unroll
-    for (int a = 0; a < 4; ++a) x[0][a] = cmul(x[0][a], kf[a]);
-    fft256_wave<true, 1>(x, t, Sw, g, s);
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-      st16_sc1(rp, (int)((((size_t)(64 * a + 16 * s + g) * 256 + i) * 2 + c) * sizeof(c128)), x[0][a]);
-  };
-
-  unsigned k = 0;
-  row_pass(ROW_VH1 | ROW_FWD, nullptr);
-  for (int st = 1; st <= p.nsteps; ++st) {
-    publish(++k);
-    if (!wait_all(k)) break;
-    col_pass();
-    publish(++k);
-    if (!wait_all(k)) break;
-    const bool take = p.snap && st % p.nout == 0;
-    int flags = ROW_INV | ROW_VH1 | (take ? ROW_SNAP : 0);
-    if (st < p.nsteps) flags |= ROW_VH2 | ROW_FWD;
-    row_pass(flags, take ? p.snap + (size_t)(st / p.nout - 1) * (256 * 256 * 2) : nullptr);
-  }
-}
-
 // Column pass for batches (qd_spo2_run_batch), coalesced: one 512-thread workgroup per 4 adjacent columns
 // and both states of one wavefunction (8 lines, wave w = column j0 + w / 2, state w % 2).  The 256 x 4 x 2
 // tile is read row by row as 128-B contiguous pieces into LDS, each wave runs the register FFT of its line
@@ -1392,66 +1254,6 @@ int col_fast(int L, int ns, int cols, c128* psi, const c128* expKT, const c128* 
   return QD_OK;
 }
 
-// QD_SPO_PERSIST=0: the two-kernel loop at 256 x 256 x 2 (A/B, tests); QD_SPO_PERSIST_COOP=0: a plain launch of the
-// persistent grid (profiler passes: rocprofv3 crashes at exit after cooperative launches)
-bool spo2_persist_enabled() {
-  const char* e = getenv("QD_SPO_PERSIST");
-  return !(e && e[0] == '0');
-}
-
-// The Strang run of spo2_persist_kernel.  *fallback = true when the launch was refused (nothing ran) or a hand-off
-// spin expired (psi restored from the copy taken before the launch): the caller then runs the two-kernel loop.
-int spo2_persist_run(c128* psi, const c128* U, const c128* expKT, const c128* tw, int nsteps, int nout, c128* snap,
-                     bool* fallback, hipStream_t st) {
-  *fallback = false;
-  const size_t ge = (size_t)256 * 256 * 2;
-  const size_t flag_bytes = ((size_t)SP_WG * SP_FLAG_STRIDE + 4) * sizeof(unsigned);
-  void* w = nullptr;
-  int rc = workspace(WS_MISC, ge * sizeof(c128) + flag_bytes, &w, st);
-  if (rc) return rc;
-  c128* backup = (c128*)w;
-  Spo2PersistParams p;
-  p.psi = psi;
-  p.U = U;
-  p.expKT = expKT;
-  p.tw = tw;
-  p.snap = snap;
-  p.flags = (unsigned*)(backup + ge);
-  p.status = (int*)(p.flags + (size_t)SP_WG * SP_FLAG_STRIDE);
-  p.nsteps = nsteps;
-  p.nout = nout;
-  QD_HIP(hipMemsetAsync(p.flags, 0, flag_bytes, st));
-  QD_HIP(hipMemcpyAsync(backup, psi, ge * sizeof(c128), hipMemcpyDeviceToDevice, st));
-  static const hipError_t attr =
-      hipFuncSetAttribute((const void*)spo2_persist_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, SP_LDS_BYTES);
-  QD_HIP(attr);
-  const char* ce = getenv("QD_SPO_PERSIST_COOP");
-  hipError_t e;
-  if (ce && ce[0] == '0') {
-    hipLaunchKernelGGL(spo2_persist_kernel, dim3(SP_WG), dim3(128), SP_LDS_BYTES, st, p);
-    e = hipGetLastError();
-  } else {
-    void* args[] = {(void*)&p};
-    e = hipLaunchCooperativeKernel((const void*)spo2_persist_kernel, dim3(SP_WG), dim3(128), args, SP_LDS_BYTES, st);
-  }
-  if (e == hipErrorCooperativeLaunchTooLarge) {
-    (void)hipGetLastError();
-    *fallback = true;
-    return QD_OK;
-  }
-  QD_HIP(e);
-  if (const char* fe = getenv("QD_SPO_PERSIST_FAKE_TIMEOUT"))   // tests: report a hand-off timeout after the run
-    if (fe[0] == '1') QD_HIP(hipMemsetAsync(p.status, 1, 1, st));
-  int h = 0;
-  QD_HIP(hipMemcpyAsync(&h, p.status, sizeof(int), hipMemcpyDeviceToHost, st));
-  QD_HIP(hipStreamSynchronize(st));
-  if (h) {
-    QD_HIP(hipMemcpyAsync(psi, backup, ge * sizeof(c128), hipMemcpyDeviceToDevice, st));
-    *fallback = true;
-  }
-  return QD_OK;
-}
-
 }  // namespace
 
 // spo_gen.hip: every grid the specialised power-of-two kernels below do not cover
@@ -1542,11 +1344,6 @@ extern "C" int qd_spo2_run_ex(qd_c128* psi_, const qd_c128* expVh_, const qd_c12
     return QD_OK;
   };
   const size_t grid_elems = (size_t)nx * ny * ns;
-  if (fast && nx == 256 && ny == 256 && ns == 2 && !expV && !expKy && q16_enabled() && spo2_persist_enabled()) {
-    bool fb = false;
-    if ((rc = spo2_persist_run(psi, expVh, expKT, twy, nsteps, nout, snap, &fb, st))) return rc;
-    if (!fb) return QD_OK;
-  }
   if ((rc = row(ROW_VH1 | ROW_FWD | ky, nullptr, expVh))) return rc;
   for (int s = 1; s <= nsteps; ++s) {
     if ((rc = col())) return rc;

@@ -88,42 +88,6 @@ def test_spo2_norm_conservation_long():
     assert pops.shape == (2, 2) and abs(pops[-1].sum() - n0 * dx * dx) < 1e-9
 
 
-@pytest.mark.parametrize("nt,nout", [(1, 1), (7, 3), (40, 5)])
-def test_spo2_persistent_launch_matches_two_kernel_loop(nt, nout, monkeypatch):
-    """spo2_persist_kernel (the whole Strang run at 256x256x2 as one launch, in-launch hand-offs between the row and
-    column passes) against the two-kernel loop (QD_SPO_PERSIST=0), a reported hand-off timeout
-    (QD_SPO_PERSIST_FAKE_TIMEOUT=1: psi restored and the two-kernel loop re-run) and the oracle."""
-    import sys, os
-    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
-    from oracle import spo as ospo
-    from pyqed_amd.wpd import SPO2
-    n = 256
-    x = np.linspace(-6, 6, n)
-    X, Y = np.meshgrid(x, x, indexing="ij")
-    sol = SPO2(x, x, mass=[1.0, 1.0], nstates=2)
-    sol.set_DPES([0.5 * ((X + 1) ** 2 + Y ** 2), 0.5 * ((X - 1) ** 2 + Y ** 2) + 0.1], [[[0, 1], 0.2 * X]])
-    psi0 = np.zeros((n, n, 2), complex)
-    psi0[:, :, 0] = np.exp(-((X + 1.5) ** 2 + Y ** 2) / 2 + 0.5j * X) / np.sqrt(np.pi)
-    psi0[:, :, 1] = 0.3 * np.exp(-((X - 1) ** 2 + (Y - 0.5) ** 2) / 2) / np.sqrt(np.pi)
-    runs = {}
-    for mode, env in (("persist", {}), ("two_kernel", {"QD_SPO_PERSIST": "0"}),
-                      ("timeout", {"QD_SPO_PERSIST_FAKE_TIMEOUT": "1"})):
-        for k in ("QD_SPO_PERSIST", "QD_SPO_PERSIST_FAKE_TIMEOUT"):
-            monkeypatch.delenv(k, raising=False)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        r = sol.run(psi0, dt=0.05, nt=nt, nout=nout)
-        runs[mode] = (np.array(r.psilist), np.array(r.psi))
-    # the fallback re-runs the two-kernel loop from the restored state: identical to it
-    assert np.array_equal(runs["timeout"][0], runs["two_kernel"][0])
-    assert np.array_equal(runs["timeout"][1], runs["two_kernel"][1])
-    # same operations in the same order; the compiler's FMA contraction may differ between the kernels (rounding level)
-    assert relerr(runs["persist"][0], runs["two_kernel"][0]) < 1e-14
-    assert relerr(runs["persist"][1], runs["two_kernel"][1]) < 1e-14
-    ref = ospo.spo2_run(sol.exp_V_half, sol.exp_K, psi0, nt, nout)
-    assert relerr(runs["persist"][0], np.array(ref)) < TOL
-
-
 def test_spo1d_batched_independent():
     from pyqed_amd.wpd import SPO
     from oracle import spo as ospo
