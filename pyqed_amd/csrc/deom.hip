@@ -410,6 +410,9 @@ __global__ __launch_bounds__(DEOM_TPB) __attribute__((amdgpu_waves_per_eu(5))) v
 // rows, then the neighbour rows the tables point at), once per wave generation; here a wave pays about one per group
 // after the first.  Same per-element arithmetic in the same order as deom_stage_grp_body<4, KMAX, true, false, 1>,
 // so the result is bit-identical (tests/test_deom_gpu.py); H / Q go to LDS once per workgroup.
+#ifndef DEOM_PIPE_BUF
+#define DEOM_PIPE_BUF 1   // gathers as 32-bit-offset buffer loads (A/B builds: 0 = 64-bit global addresses)
+#endif
 template <int KMAX>
 __global__ __launch_bounds__(DEOM_TPB) void deom_stage_pipe_kernel(DeomParams p) {
   constexpr int G = 4, NI = (KMAX + G - 1) / G, NC = (3 * KMAX + G - 1) / G;
@@ -455,12 +458,37 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_pipe_kernel(DeomParams p)
     unsigned hb;
     bool live;
   };
+#if DEOM_PIPE_BUF
+  // every gather is a buffer load at a 32-bit byte offset (the host keeps every table below 2^31 bytes and the
+  // factors of the __umul24 products below 2^24); a dead load takes BUF_OOB and returns zeros, the value the plain
+  // form selects (no 64-bit address arithmetic, no branch around the loads)
+  const unsigned nx = (unsigned)p.nmax;
+  const __amdgpu_buffer_rsrc_t rX = buf_rsrc(p.xin, (int)(nx * (unsigned)p.B * 64u));
+  const __amdgpu_buffer_rsrc_t rCo = buf_rsrc(p.coef, (int)(nx * (unsigned)K * 48u));
+  const __amdgpu_buffer_rsrc_t rDa = buf_rsrc(p.damp, (int)(nx * 16u));
+  const __amdgpu_buffer_rsrc_t rMi = buf_rsrc(p.minus, (int)(nx * (unsigned)K * 4u));
+  const __amdgpu_buffer_rsrc_t rPl = buf_rsrc(p.plus, (int)(nx * (unsigned)K * 4u));
+  const unsigned rsb = (unsigned)p.B * 64u;                 // ADO row stride in bytes
+#endif
   auto head = [&](unsigned uu, Head& h) {
     const unsigned lgrp = uu / G;
     h.live = uu < per;
     const unsigned hi = lgrp / Bx, lo = lgrp - hi * Bx;
     h.n = h.live ? (int)hi : 0;
     h.hb = cls * Bx + (h.live ? lo : 0);
+#if DEOM_PIPE_BUF
+    const unsigned nk = __umul24((unsigned)h.n, (unsigned)K);
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      const int k = e + G * q;
+      const bool ok = h.live && k < K;
+      const int vm = ld4_buf(rMi, ok ? (nk + (unsigned)k) * 4u : BUF_OOB);
+      const int vp = ld4_buf(rPl, ok ? (nk + (unsigned)k) * 4u : BUF_OOB);
+      h.lm[q] = ok ? vm : -1;
+      h.lp[q] = ok ? vp : -1;
+    }
+    h.own = ld16_buf(rX, h.live ? __umul24((unsigned)h.n, rsb) + h.hb * 64u + (unsigned)e * 16u : BUF_OOB);
+#else
 #pragma unroll
     for (int q = 0; q < NI; ++q) {
       const int k = e + G * q;
@@ -469,6 +497,7 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_pipe_kernel(DeomParams p)
     }
     const c128* X = p.xin + (size_t)h.hb * 4;
     h.own = h.live ? X[(size_t)h.n * rs + e] : cmk(0, 0);
+#endif
   };
   unsigned u = (blockIdx.x >> 3) * blockDim.x + threadIdx.x;
   Head cur;
@@ -476,22 +505,42 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_pipe_kernel(DeomParams p)
   while (__builtin_amdgcn_readfirstlane(u - lane) < per) {   // wave-uniform trip count (DPP needs whole quads)
     // this group's prefactors, damping and neighbour rows
     c128 lc[NC];
+#if DEOM_PIPE_BUF
+    const unsigned n3k = __umul24((unsigned)cur.n, 3u * (unsigned)K);
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      const int c = e + G * q;
+      lc[q] = ld16_buf(rCo, (cur.live && c < 3 * K) ? (n3k + (unsigned)c) * 16u : BUF_OOB);
+    }
+    const c128 dmp = ld16_buf(rDa, cur.live ? (unsigned)cur.n * 16u : BUF_OOB);
+#else
 #pragma unroll
     for (int q = 0; q < NC; ++q) {
       const int c = e + G * q;
       lc[q] = (cur.live && c < 3 * K) ? p.coef[(size_t)cur.n * K * 3 + c] : cmk(0, 0);
     }
     const c128 dmp = cur.live ? p.damp[cur.n] : cmk(0, 0);
+#endif
     const size_t idx = ((size_t)cur.n * p.B + cur.hb) * 4 + e;
     const c128 r0 = !cur.live ? cmk(0, 0) : p.stage == 0 ? cur.own : ld_once(p.rho + idx, p.ntst);
-    const c128* X = p.xin + (size_t)cur.hb * 4;
     c128 ym[KMAX], yp[KMAX];
+#if DEOM_PIPE_BUF
+    const unsigned xb = cur.hb * 64u + (unsigned)e * 16u;   // this lane's element within a row
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int im = bci(cur.lm[k / G], k % G), ip = bci(cur.lp[k / G], k % G);
+      ym[k] = ld16_buf(rX, (k < K && im >= 0) ? __umul24((unsigned)im, rsb) + xb : BUF_OOB);
+      yp[k] = ld16_buf(rX, (k < K && ip >= 0) ? __umul24((unsigned)ip, rsb) + xb : BUF_OOB);
+    }
+#else
+    const c128* X = p.xin + (size_t)cur.hb * 4;
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
       const int im = bci(cur.lm[k / G], k % G), ip = bci(cur.lp[k / G], k % G);
       ym[k] = (k < K && im >= 0) ? X[(size_t)im * rs + e] : cmk(0, 0);
       yp[k] = (k < K && ip >= 0) ? X[(size_t)ip * rs + e] : cmk(0, 0);
     }
+#endif
     // the next group's head, in flight with the rows above
     const unsigned un = u + stride;
     Head nxt;
@@ -1049,8 +1098,11 @@ int deom_launch_stage(const DeomParams& p, hipStream_t st) {
     // the software-pipelined persistent form (undriven ns = 2 ADO-major batches of >= 64 hierarchies in 8 XCD classes,
     // no hierarchy chunks); QD_DEOM_PIPE=0 keeps the stage kernels, QD_DEOM_PIPE_BPC sets the workgroups per class
     const char* pe = getenv("QD_DEOM_PIPE");
+    // (its buffer loads take 32-bit byte offsets: every table below 2^31 - 2^20 bytes, __umul24 factors below 2^24)
+    const bool small_tables = (size_t)nmax * B * 64 < ((size_t)1 << 31) - ((size_t)1 << 20) && nmax < (1 << 24) &&
+                              (size_t)B * 64 < ((size_t)1 << 24);
     if (G == 4 && q.horner && bminor && q.xsplit == 8 && q.bchunk == 0 && B >= 64 && K <= 6 && !(pe && pe[0] == '0') &&
-        tpb == DEOM_TPB) {
+        tpb == DEOM_TPB && small_tables) {
       auto go = [&](const void* fn, auto kern) {
         // workgroups per class: what one XCD's CUs hold at once (every wave persistent, no tail generation)
         static thread_local const void* last_fn = nullptr;   // one lookup per kernel / LDS size / device

@@ -3,7 +3,7 @@
 // wave drains (s_waitcnt vmcnt(0)), a workgroup barrier, then one lane stores the epoch word (relaxed agent atomic);
 // the consumer polls the epochs with relaxed agent loads from one wave, joins a workgroup barrier, and loads the
 // handed-off bytes with 16-B sc1 buffer loads only (never a plain or flat load of them).  One workgroup per CU.
-// Users: glf_single.hip (one trajectory), deom.hip (banded hierarchy).
+// Users: glf_single.hip (one trajectory), deom.hip (banded hierarchy; the pipelined stage kernel's plain buffer loads).
 #pragma once
 #include "qd_common.hpp"
 
@@ -30,9 +30,22 @@ __device__ __forceinline__ void* wave_uniform_ptr(const void* q) {
   const unsigned l = __builtin_amdgcn_readfirstlane((unsigned)v), h = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
   return (void*)(((unsigned long long)h << 32) | l);
 }
-// raw buffer descriptor over `bytes` bytes at `base`
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t sc1_rsrc(const void* base, int bytes) {
+// raw buffer descriptor over `bytes` bytes at `base` (the cache policy is the load / store's, not the descriptor's)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(wave_uniform_ptr(base), (short)0, bytes, 0x00020000);
 }
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sc1_rsrc(const void* base, int bytes) { return buf_rsrc(base, bytes); }
+
+// plain (default cache policy) buffer loads with 32-bit byte offsets: an offset at or past the descriptor's size
+// returns zeros (raw buffer range check), so a dead load needs no branch and no select
+__device__ __forceinline__ c128 ld16_buf(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  const ho_u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+  return cmk(__builtin_bit_cast(double, (unsigned long long)v.x | ((unsigned long long)v.y << 32)),
+             __builtin_bit_cast(double, (unsigned long long)v.z | ((unsigned long long)v.w << 32)));
+}
+__device__ __forceinline__ int ld4_buf(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return (int)__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
+}
+constexpr unsigned BUF_OOB = 0x7FFFFFF0u;   // an offset past every descriptor this library builds (sizes < 2^31 - 2^20)
 
 }  // namespace qd
