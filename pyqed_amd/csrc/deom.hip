@@ -409,10 +409,11 @@ __global__ __launch_bounds__(DEOM_TPB) __attribute__((amdgpu_waves_per_eu(5))) v
 // stage state are loaded.  The stage kernels above spend two dependent memory round trips per wave (tables + own
 // rows, then the neighbour rows the tables point at), once per wave generation; here a wave pays about one per group
 // after the first.  Same per-element arithmetic in the same order as deom_stage_grp_body<4, KMAX, true, false, 1>,
-// so the result is bit-identical (tests/test_deom_gpu.py); H / Q go to LDS once per workgroup.
-#ifndef DEOM_PIPE_BUF
-#define DEOM_PIPE_BUF 1   // gathers as 32-bit-offset buffer loads (A/B builds: 0 = 64-bit global addresses)
-#endif
+// so the result is bit-identical (tests/test_deom_gpu.py); H / Q go to LDS once per workgroup.  Every gather and the
+// state accesses are buffer loads / stores at 32-bit byte offsets, a dead lane's at BUF_OOB (zeros / dropped), and the
+// lane-group coordinates advance by a carry step: against 64-bit global addresses with a branch around each
+// conditional load and a division per group, 64 hierarchies 28.9 -> 26.0 us per stage
+// (profiles/r04/deom/deom_buf_ab.txt, deom_buf2_ab.txt).
 template <int KMAX>
 __global__ __launch_bounds__(DEOM_TPB) void deom_stage_pipe_kernel(DeomParams p) {
   constexpr int G = 4, NI = (KMAX + G - 1) / G, NC = (3 * KMAX + G - 1) / G;
@@ -430,7 +431,6 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_pipe_kernel(DeomParams p)
   const unsigned lane = threadIdx.x & 63;
   const int e = (int)(threadIdx.x & 3);
   const int base = (int)lane & ~(G - 1);
-  const size_t rs = (size_t)p.B * 4;                        // ADO row stride
   const int i = e >> 1, j = e & 1;
   auto bc = [&](c128 v, int src) -> c128 {
     switch (src) {
@@ -455,10 +455,9 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_pipe_kernel(DeomParams p)
     int lm[NI], lp[NI];
     c128 own;
     int n;
-    unsigned hb;
+    unsigned hb, off;   // off: byte offset of this lane's element of the ADO row (BUF_OOB for a dead lane)
     bool live;
   };
-#if DEOM_PIPE_BUF
   // every gather is a buffer load at a 32-bit byte offset (the host keeps every table below 2^31 bytes and the
   // factors of the __umul24 products below 2^24); a dead load takes BUF_OOB and returns zeros, the value the plain
   // form selects (no 64-bit address arithmetic, no branch around the loads)
@@ -469,14 +468,15 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_pipe_kernel(DeomParams p)
   const __amdgpu_buffer_rsrc_t rMi = buf_rsrc(p.minus, (int)(nx * (unsigned)K * 4u));
   const __amdgpu_buffer_rsrc_t rPl = buf_rsrc(p.plus, (int)(nx * (unsigned)K * 4u));
   const unsigned rsb = (unsigned)p.B * 64u;                 // ADO row stride in bytes
-#endif
-  auto head = [&](unsigned uu, Head& h) {
-    const unsigned lgrp = uu / G;
+  const int xbytes = (int)(nx * (unsigned)p.B * 64u);
+  const __amdgpu_buffer_rsrc_t rR = buf_rsrc(p.rho, xbytes), rXo = buf_rsrc(p.xout, xbytes);
+  const __amdgpu_buffer_rsrc_t rRo = buf_rsrc(p.rho_out, xbytes);
+  // lane group lgrp = u / G of the class is (ADO hi, hierarchy lo) with lgrp = hi Bx + lo; a wave's next group is
+  // stride / G further on, so (hi, lo) advance by a constant carry step instead of a division per group
+  auto head = [&](unsigned uu, unsigned hi, unsigned lo, Head& h) {
     h.live = uu < per;
-    const unsigned hi = lgrp / Bx, lo = lgrp - hi * Bx;
     h.n = h.live ? (int)hi : 0;
     h.hb = cls * Bx + (h.live ? lo : 0);
-#if DEOM_PIPE_BUF
     const unsigned nk = __umul24((unsigned)h.n, (unsigned)K);
 #pragma unroll
     for (int q = 0; q < NI; ++q) {
@@ -487,25 +487,22 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_pipe_kernel(DeomParams p)
       h.lm[q] = ok ? vm : -1;
       h.lp[q] = ok ? vp : -1;
     }
-    h.own = ld16_buf(rX, h.live ? __umul24((unsigned)h.n, rsb) + h.hb * 64u + (unsigned)e * 16u : BUF_OOB);
-#else
-#pragma unroll
-    for (int q = 0; q < NI; ++q) {
-      const int k = e + G * q;
-      h.lm[q] = (h.live && k < K) ? p.minus[(size_t)h.n * K + k] : -1;
-      h.lp[q] = (h.live && k < K) ? p.plus[(size_t)h.n * K + k] : -1;
-    }
-    const c128* X = p.xin + (size_t)h.hb * 4;
-    h.own = h.live ? X[(size_t)h.n * rs + e] : cmk(0, 0);
-#endif
+    h.off = h.live ? __umul24((unsigned)h.n, rsb) + h.hb * 64u + (unsigned)e * 16u : BUF_OOB;
+    h.own = ld16_buf(rX, h.off);
   };
   unsigned u = (blockIdx.x >> 3) * blockDim.x + threadIdx.x;
+  const unsigned sg = stride / G, sg_hi = sg / Bx, sg_lo = sg - sg_hi * Bx;
+  unsigned ghi = (u / G) / Bx, glo = (u / G) - ghi * Bx;
   Head cur;
-  head(u, cur);
+  head(u, ghi, glo, cur);
+  // the modes of the K directions, once (scalar loads): the per-group mode tests are then uniform branches that wait
+  // on no memory
+  int modek[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) modek[k] = k < K ? ld_uniform(p.mode + k) : 0;
   while (__builtin_amdgcn_readfirstlane(u - lane) < per) {   // wave-uniform trip count (DPP needs whole quads)
     // this group's prefactors, damping and neighbour rows
     c128 lc[NC];
-#if DEOM_PIPE_BUF
     const unsigned n3k = __umul24((unsigned)cur.n, 3u * (unsigned)K);
 #pragma unroll
     for (int q = 0; q < NC; ++q) {
@@ -513,18 +510,9 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_pipe_kernel(DeomParams p)
       lc[q] = ld16_buf(rCo, (cur.live && c < 3 * K) ? (n3k + (unsigned)c) * 16u : BUF_OOB);
     }
     const c128 dmp = ld16_buf(rDa, cur.live ? (unsigned)cur.n * 16u : BUF_OOB);
-#else
-#pragma unroll
-    for (int q = 0; q < NC; ++q) {
-      const int c = e + G * q;
-      lc[q] = (cur.live && c < 3 * K) ? p.coef[(size_t)cur.n * K * 3 + c] : cmk(0, 0);
-    }
-    const c128 dmp = cur.live ? p.damp[cur.n] : cmk(0, 0);
-#endif
-    const size_t idx = ((size_t)cur.n * p.B + cur.hb) * 4 + e;
-    const c128 r0 = !cur.live ? cmk(0, 0) : p.stage == 0 ? cur.own : ld_once(p.rho + idx, p.ntst);
+    // r0: the own element at stage 0, else rho's (zero on a dead lane: its offset is out of range)
+    const c128 r0 = p.stage == 0 ? cur.own : p.ntst ? ld16_buf_nt(rR, cur.off) : ld16_buf(rR, cur.off);
     c128 ym[KMAX], yp[KMAX];
-#if DEOM_PIPE_BUF
     const unsigned xb = cur.hb * 64u + (unsigned)e * 16u;   // this lane's element within a row
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
@@ -532,19 +520,15 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_pipe_kernel(DeomParams p)
       ym[k] = ld16_buf(rX, (k < K && im >= 0) ? __umul24((unsigned)im, rsb) + xb : BUF_OOB);
       yp[k] = ld16_buf(rX, (k < K && ip >= 0) ? __umul24((unsigned)ip, rsb) + xb : BUF_OOB);
     }
-#else
-    const c128* X = p.xin + (size_t)cur.hb * 4;
-#pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-      const int im = bci(cur.lm[k / G], k % G), ip = bci(cur.lp[k / G], k % G);
-      ym[k] = (k < K && im >= 0) ? X[(size_t)im * rs + e] : cmk(0, 0);
-      yp[k] = (k < K && ip >= 0) ? X[(size_t)ip * rs + e] : cmk(0, 0);
-    }
-#endif
     // the next group's head, in flight with the rows above
     const unsigned un = u + stride;
+    unsigned nlo = glo + sg_lo, nhi = ghi + sg_hi;
+    if (nlo >= Bx) {
+      nlo -= Bx;
+      ++nhi;
+    }
     Head nxt;
-    head(un, nxt);
+    head(un, nhi, nlo, nxt);
     // stencil: deom_stage_grp_body's ns = 2 arithmetic, operation for operation
     c128 d = cmul(dmp, cur.own);
     c128 comm = cmk(0, 0);
@@ -560,11 +544,11 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_pipe_kernel(DeomParams p)
       for (int l = 0; l < 2; ++l) t = cadd(t, cadd(cmul(Qm[i * 2 + l], colv(SL, l)), cmul(rowv(SR, l), Qm[l * 2 + j])));
       d = cadd(d, t);
     };
-    int mcur = p.mode[0];
+    int mcur = modek[0];
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
       if (k >= K) break;
-      const int m = p.mode[k];
+      const int m = modek[k];
       if (m != mcur) {
         flush(mcur);
         SL = SR = cmk(0, 0);
@@ -578,18 +562,20 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_pipe_kernel(DeomParams p)
       SR = cadd(SR, csub(cmul(cR, ym[k]), py));
     }
     flush(mcur);
-    if (cur.live) {
+    {   // a dead lane's store goes to an out-of-range offset (dropped)
       c128 a0 = cmk(0, 0);
       const c128 v = deom_rk4_next(p.stage, true, p.dt, r0, a0, d);
       if (p.stage < 3) {
-        p.xout[idx] = v;
+        st16_buf(rXo, cur.off, v);
       } else {
-        p.rho_out[idx] = v;
-        if (p.snap && cur.n == 0) p.snap[((size_t)cur.hb * (p.nsteps + 1) + p.step + 1) * 4 + e] = v;
+        st16_buf(rRo, cur.off, v);
+        if (p.snap && cur.live && cur.n == 0) p.snap[((size_t)cur.hb * (p.nsteps + 1) + p.step + 1) * 4 + e] = v;
       }
     }
     cur = nxt;
     u = un;
+    ghi = nhi;
+    glo = nlo;
   }
 }
 

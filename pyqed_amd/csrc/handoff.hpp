@@ -43,6 +43,18 @@ __device__ __forceinline__ c128 ld16_buf(__amdgpu_buffer_rsrc_t r, unsigned off)
   return cmk(__builtin_bit_cast(double, (unsigned long long)v.x | ((unsigned long long)v.y << 32)),
              __builtin_bit_cast(double, (unsigned long long)v.z | ((unsigned long long)v.w << 32)));
 }
+__device__ __forceinline__ c128 ld16_buf_nt(__amdgpu_buffer_rsrc_t r, unsigned off) {   // non-temporal
+  const ho_u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 2);
+  return cmk(__builtin_bit_cast(double, (unsigned long long)v.x | ((unsigned long long)v.y << 32)),
+             __builtin_bit_cast(double, (unsigned long long)v.z | ((unsigned long long)v.w << 32)));
+}
+// plain buffer store; an out-of-range offset drops it
+__device__ __forceinline__ void st16_buf(__amdgpu_buffer_rsrc_t r, unsigned off, c128 x) {
+  const unsigned long long a = __builtin_bit_cast(unsigned long long, x.re);
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, x.im);
+  const ho_u4 v = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, 0);
+}
 __device__ __forceinline__ int ld4_buf(__amdgpu_buffer_rsrc_t r, unsigned off) {
   return (int)__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
 }
