@@ -1037,12 +1037,22 @@ int deom_launch_stage(const DeomParams& p, hipStream_t st) {
   q.ntst = tot * sizeof(c128) >= ((size_t)64 << 20);
   if (const char* s = getenv("QD_DEOM_NT")) q.ntst = atoi(s) != 0;
   const size_t lds = (size_t)(1 + nmod) * ns2 * sizeof(c128);   // H(t), Q(t) of the group kernel
-  // hierarchy chunks of 16 in classes of more (ADO-major): 256 hierarchies = 8 classes of 32, see the kernel;
-  // QD_DEOM_BCHUNK overrides (0 = off, else a divisor of the class size)
+  // the software-pipelined persistent form (undriven ns = 2 ADO-major batches of >= 64 hierarchies in 8 XCD classes,
+  // no hierarchy chunks); QD_DEOM_PIPE=0 keeps the stage kernels.  Its buffer loads take 32-bit byte offsets: every
+  // table below 2^31 - 2^20 bytes, __umul24 factors below 2^24.
+  const char* pe = getenv("QD_DEOM_PIPE");
+  const bool small_tables = (size_t)nmax * B * 64 < ((size_t)1 << 31) - ((size_t)1 << 20) && nmax < (1 << 24) &&
+                            (size_t)B * 64 < ((size_t)1 << 24);
+  const bool pipe_ok = grp && G == 4 && q.horner && bminor && q.xsplit == 8 && B >= 64 && K <= 6 &&
+                       !(pe && pe[0] == '0') && tpb == DEOM_TPB && small_tables;
+  // hierarchy chunks of 16 in classes of more (ADO-major) for the stage kernels: 256 hierarchies = 8 classes of 32,
+  // see the kernel; not for the pipelined form (256 hierarchies: 97.0 us per stage unchunked vs 102.7-103.3 for the
+  // chunked stage kernel, profiles/r04/deom/deom_bchunk_pipe_ab.txt).  QD_DEOM_BCHUNK overrides (0 = off, else a
+  // divisor of the class size)
   q.bchunk = 0;
   if (grp && bminor && q.xsplit > 0) {
     const int Bx = B / q.xsplit;
-    int c = (Bx > 16 && Bx % 16 == 0) ? 16 : 0;
+    int c = (!pipe_ok && Bx > 16 && Bx % 16 == 0) ? 16 : 0;
     if (const char* s = getenv("QD_DEOM_BCHUNK")) c = atoi(s);
     q.bchunk = (c > 0 && c < Bx && Bx % c == 0) ? c : 0;
   }
@@ -1081,14 +1091,8 @@ int deom_launch_stage(const DeomParams& p, hipStream_t st) {
       hipLaunchKernelGGL(deom_stage_kernel, dim3(grid), dim3(tpb), 0, st, q);
       return;
     }
-    // the software-pipelined persistent form (undriven ns = 2 ADO-major batches of >= 64 hierarchies in 8 XCD classes,
-    // no hierarchy chunks); QD_DEOM_PIPE=0 keeps the stage kernels, QD_DEOM_PIPE_BPC sets the workgroups per class
-    const char* pe = getenv("QD_DEOM_PIPE");
-    // (its buffer loads take 32-bit byte offsets: every table below 2^31 - 2^20 bytes, __umul24 factors below 2^24)
-    const bool small_tables = (size_t)nmax * B * 64 < ((size_t)1 << 31) - ((size_t)1 << 20) && nmax < (1 << 24) &&
-                              (size_t)B * 64 < ((size_t)1 << 24);
-    if (G == 4 && q.horner && bminor && q.xsplit == 8 && q.bchunk == 0 && B >= 64 && K <= 6 && !(pe && pe[0] == '0') &&
-        tpb == DEOM_TPB && small_tables) {
+    // the software-pipelined persistent form (pipe_ok above); QD_DEOM_PIPE_BPC sets the workgroups per class
+    if (pipe_ok && q.bchunk == 0) {
       auto go = [&](const void* fn, auto kern) {
         // workgroups per class: what one XCD's CUs hold at once (every wave persistent, no tail generation)
         static thread_local const void* last_fn = nullptr;   // one lookup per kernel / LDS size / device
