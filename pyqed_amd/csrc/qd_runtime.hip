@@ -21,8 +21,8 @@ void set_error(const char* fmt, ...) {
 // (release threshold = max, so the pool keeps what is released reserved), live until the enclosing WsScope (one per
 // entry point) ends.  At the end of a scope its buffers are PARKED for reuse rather than released: hipFreeAsync on
 // this ROCm blocks the host until the stream has drained the work queued so far (median 1.1 ms, one 2DES grid, in the
-// HIP API trace of profiles/r04/2des/hipfree_block.txt), which left a launch-latency bubble in front of every call
-// that followed another on a busy stream (10.6 us per 0.17 ms shard grid).  A parked buffer is
+// HIP API trace of profiles/r04/2des/hipfree_block.txt), which made every library call synchronous in effect (the
+// bench's 2DES leg: 1.19 -> 0.035 ms of host time per grid, profiles/r04/2des/ws_park_ab.txt).  A parked buffer is
 //   - reused by a later workspace() request on the SAME stream (stream order puts the new user behind every kernel
 //     of the old one; the park happens after the old call queued its last kernel), the smallest parked buffer of at
 //     least the requested size and at most 4x it;
