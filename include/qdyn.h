@@ -9,11 +9,9 @@
  *   - matrices are row-major and contiguous; vec(rho) is row-major
  *     (rho.flatten(), reference pyqed/superoperator.py:125-150);
  *   - the caller owns every buffer it passes; the library's own scratch is
- *     stream-ordered memory of the device's default pool, live for one call and
- *     then parked for reuse by later calls on the same stream (hipFreeAsync would
- *     block the host until the stream drains); parked scratch is released once its
- *     work has completed, by qd_workspace_stats / qd_shutdown or past an 8 GiB cap,
- *     and the pool keeps released memory reserved until qd_shutdown trims it;
+ *     call-scoped (stream-ordered hipMallocAsync / hipFreeAsync from the device's
+ *     default memory pool, released when the entry point returns; the pool keeps
+ *     it reserved until qd_shutdown trims it);
  *   - calls are asynchronous on `stream` (a hipStream_t, NULL = default stream);
  *   - return 0 on success, a negative QD_E* code on failure; the message is
  *     available from qd_last_error() (thread-local).
@@ -55,9 +53,8 @@ int qd_device_count(int* count);      /* host pointer                         */
 int qd_shutdown(void);                /* trims the scratch memory pools       */
 int qd_synchronize(void* stream);     /* hipStreamSynchronize                 */
 /* Current device's scratch pool: bytes reserved and bytes in use (host pointers).
- * First releases the parked scratch whose work has completed, so in use returns to 0
- * once every stream that called the library has drained; reserved is bounded by the
- * peak concurrent scratch plus the park cap, not by the number of streams. */
+ * In use returns to 0 once every stream that called the library has drained;
+ * reserved is bounded by the peak concurrent scratch, not by the number of streams. */
 int qd_workspace_stats(size_t* reserved, size_t* used);
 
 /* ------------------------------------------------------------ Lindblad --- */
