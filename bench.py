@@ -470,23 +470,19 @@ def bench_2des_t2scan(dev, world, rank, M_total, n2, reps, n=256):
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     wall = float(tt.item())
-    # compute-only time of this rank's launch sequence (no collective), for the scaling breakdown;
-    # HIP events around the bucket applies (E table + the t2 GEMM + slab reduction) give the
-    # dominant kernel's rate as a lower bound (rocprof's kernel-only average is in profiles/)
+    # the roofline comes from THIS timed region: HIP events on the launch stream around the same `reps` scans
+    # (operand build + bucket applies, and the bucket reduces at world > 1), so frac follows ms_per_scan
+    # (a separately timed loop gave a different frac)
+    ev_scan = e0.elapsed_time(e1) / 1e3 / reps
+    # compute-only time of this rank's launch sequence (no collective), for the scaling breakdown
     torch.cuda.synchronize(dev)
     c0 = time.perf_counter()
-    ev_apply = 0.0
     for _ in range(reps):
         scan[0] = T2Scan(lam_t, alpha_t, B_t, C_t, beta_t, t, t)
-        a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a0.record(stream)
         for b in buckets:
             local(lo, hi, b)
-        a1.record(stream)
-        torch.cuda.synchronize(dev)
-        ev_apply += a0.elapsed_time(a1) / 1e3
+    torch.cuda.synchronize(dev)
     comp = (time.perf_counter() - c0) / reps
-    ev_apply /= reps
     nr = scan[0].nL                         # executed K per member: the pruned waiting-time index set
     Kp = ((hi - lo) * nr + 15) // 16 * 16
     gemm_flop = 8.0 * n * n * n2 * Kp
@@ -502,15 +498,17 @@ def bench_2des_t2scan(dev, world, rank, M_total, n2, reps, n=256):
         "compute_ms_per_scan": round(comp * 1e3, 4),
         "gemm_tflops": round(gemm_flop / comp / 1e12, 2),
         "index_set_sizes_p_r_q": list(scan[0].index_sizes),
-        "roofline": {"bound": "mfma", "kernel": "ens_t2_gemm_kernel", "achieved": round(gemm_flop / ev_apply / 1e12, 3),
+        "roofline": {"bound": "mfma", "kernel": "ens_t2_gemm_kernel", "achieved": round(gemm_flop / ev_scan / 1e12, 3),
                      "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(gemm_flop / ev_apply / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
+                     "frac": round(gemm_flop / ev_scan / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
+                     "ms_per_scan_events": round(ev_scan * 1e3, 4),
                      "flop_per_scan": gemm_flop,
                      "traffic": measured_traffic("ens_t2_gemm_kernel_pruned", 1) if (M_total, n, world) == (65536, 256, 1) else None,
                      "traffic_unit": "HBM bytes per ens_t2_gemm_kernel launch (4 waiting times; PMC FETCH_SIZE+WRITE_SIZE, "
                                      "calibrated; profiles/pmc_traffic.json)",
-                     "note": "8 n3 n1 n2 K flop per scan (K = members x nL) / event time of the bucket applies "
-                             "(E table + GEMM + slab reduction): a lower bound on the GEMM kernel's own rate"},
+                     "note": "8 n3 n1 n2 K flop per scan (K = members x nL) / the timed region's HIP-event time per "
+                             "scan (operand build, E tables, GEMM, slab reduction, and the reduces at world > 1): a "
+                             "lower bound on the GEMM kernel's own rate"},
     }
 
 
@@ -987,6 +985,13 @@ _T0 = time.perf_counter()
 def progress(msg):
     """One line per leg on stderr (stdout carries only the JSON line): long runs under a profiler show activity."""
     print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+    maps = os.environ.get("BENCH_MAPS")   # diagnostics: the process's library map, to resolve a crash's frames
+    if maps:
+        try:
+            with open("/proc/self/maps") as fi, open(maps, "w") as fo:
+                fo.write(fi.read())
+        except OSError:
+            pass
 
 
 def write_detail(out, path):

@@ -9,10 +9,17 @@
  *   - matrices are row-major and contiguous; vec(rho) is row-major
  *     (rho.flatten(), reference pyqed/superoperator.py:125-150);
  *   - the caller owns every buffer it passes; the library's own scratch is
- *     call-scoped (stream-ordered hipMallocAsync / hipFreeAsync from the device's
- *     default memory pool, released when the entry point returns; the pool keeps
- *     it reserved until qd_shutdown trims it);
- *   - calls are asynchronous on `stream` (a hipStream_t, NULL = default stream);
+ *     call-scoped: slabs of a library arena, held by one live call at a time
+ *     and ordered behind their previous user on the device (hipStreamWaitEvent),
+ *     never by a host wait; qd_shutdown releases the arena;
+ *   - calls are asynchronous on `stream` (a hipStream_t, NULL = default stream):
+ *     they enqueue their kernels and return without waiting for the device.
+ *     Exceptions, each stated at its entry point: qd_gather_rows with check != 0,
+ *     the single-trajectory Lindblad launch inside qd_lindblad_rk4 /
+ *     qd_lindblad_rk4_herm (B <= glf_single_max_batch: it reads its hand-off
+ *     status back), and qd_deom_rk4_banded with status == NULL;
+ *     host-array inputs (fvals of the driven entry points) are copied before
+ *     the call returns;
  *   - return 0 on success, a negative QD_E* code on failure; the message is
  *     available from qd_last_error() (thread-local).
  *
@@ -50,11 +57,12 @@ int qd_version(void);                 /* e.g. 100 = 0.1.0                      *
 const char* qd_last_error(void);      /* thread-local message of last failure */
 int qd_init(int device);              /* hipSetDevice + warm-up               */
 int qd_device_count(int* count);      /* host pointer                         */
-int qd_shutdown(void);                /* trims the scratch memory pools       */
+int qd_shutdown(void);                /* waits for and frees the scratch arena */
 int qd_synchronize(void* stream);     /* hipStreamSynchronize                 */
-/* Current device's scratch pool: bytes reserved and bytes in use (host pointers).
- * In use returns to 0 once every stream that called the library has drained;
- * reserved is bounded by the peak concurrent scratch, not by the number of streams. */
+/* Scratch arena (current process, all devices): bytes reserved and bytes in use
+ * (host pointers).  In use returns to 0 once every stream that called the library
+ * has drained; reserved is bounded by the peak concurrent scratch plus a capped
+ * idle cache, not by the number of streams. */
 int qd_workspace_stats(size_t* reserved, size_t* used);
 
 /* ------------------------------------------------------------ Lindblad --- */

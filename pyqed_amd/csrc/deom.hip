@@ -1314,7 +1314,7 @@ __global__ void gather_rows_kernel(const c128* src, int nsrc, const int32_t* idx
       dst[e] = src[(size_t)r * row + e % row];
     } else {
       dst[e] = cmk(__builtin_nan(""), __builtin_nan(""));
-      *bad = 1;   // vector store (global_store): benign race, every writer stores 1
+      if (bad) *bad = 1;   // vector store (global_store): benign race, every writer stores 1
     }
   }
 }
@@ -1329,10 +1329,12 @@ extern "C" int qd_gather_rows(const qd_c128* src, int nsrc, const int32_t* idx, 
   if (n == 0) return QD_OK;
   QD_CHECK_ARG(src && idx && dst, "qd_gather_rows: null pointer");
   WsScope wss_((hipStream_t)stream);
-  void* w = nullptr;
-  int rc = workspace(WS_MISC, sizeof(int), &w, (hipStream_t)stream);
-  if (rc) return rc;
-  QD_HIP(hipMemsetAsync(w, 0, sizeof(int), (hipStream_t)stream));
+  void* w = nullptr;   // the bad-index flag, only when the caller asks for the check
+  if (check) {
+    int rc = workspace(WS_MISC, sizeof(int), &w, (hipStream_t)stream);
+    if (rc) return rc;
+    QD_HIP(hipMemsetAsync(w, 0, sizeof(int), (hipStream_t)stream));
+  }
   const size_t tot = (size_t)n * row_elems;
   hipLaunchKernelGGL(gather_rows_kernel, dim3((int)std::min<size_t>((tot + 255) / 256, 8192)), dim3(256), 0,
                      (hipStream_t)stream, (const c128*)src, nsrc, idx, n, row_elems, (c128*)dst, (int*)w);

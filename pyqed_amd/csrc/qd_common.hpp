@@ -40,11 +40,11 @@ void set_error(const char* fmt, ...);
   } while (0)
 
 // Library-owned scratch, never handed to the caller (qd_runtime.hip).  Every entry point that needs
-// scratch opens a WsScope on its stream; workspace() then returns a fresh stream-ordered allocation
-// (hipMallocAsync on `st`, default memory pool with a max release threshold) that the scope releases
-// with hipFreeAsync on the same stream when the entry point returns.  Distinct streams / host threads
-// never share live scratch (SURVEY.md §8(b) threading contract), and the pool's reserved memory is
-// bounded by the peak concurrent use, not by the number of streams seen (qd_workspace_stats).
+// scratch opens a WsScope on its stream; workspace() returns a slab of the library's arena that no other
+// live call holds, ordered on the device behind the slab's previous user (hipStreamWaitEvent), and the
+// scope's end records the slab's event on the stream -- no host wait anywhere.  Distinct streams / host
+// threads never share live scratch (SURVEY.md §8(b) threading contract); the arena is bounded by the peak
+// concurrent use plus a capped idle cache, not by the number of streams seen (qd_workspace_stats).
 enum WsSlot { WS_LINDBLAD = 0, WS_LINDBLAD_OPS = 1, WS_SPO = 2, WS_DEOM = 3,
               WS_SUPEROP = 4, WS_2DES = 5, WS_MISC = 6, WS_2DES_OPS = 7, WS_TDSE_H = 8,
               WS_TDSE_GEMM = 9, WS_SUPEROP_OPS = 10, WS_NSLOTS = 11 };

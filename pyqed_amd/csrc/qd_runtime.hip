@@ -1,9 +1,7 @@
-// qd_runtime.hip — error reporting, device selection and the per-device
-// workspace cache of libqdyn.
+// qd_runtime.hip — error reporting, device selection and the library's scratch arena.
 #include "qd_common.hpp"
 
 #include <mutex>
-#include <set>
 #include <vector>
 
 namespace qd {
@@ -17,86 +15,155 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
-// Scratch is call-scoped: every workspace() call takes a fresh stream-ordered allocation
-// (hipMallocAsync on the call's stream) from the device's default memory pool, and the enclosing
-// WsScope (one per entry point) returns it with hipFreeAsync on the same stream once every kernel
-// that uses it has been enqueued.  The pool keeps released memory reserved (release threshold =
-// max), so steady-state calls sub-allocate without touching the driver, any stream may reuse what
-// another stream released (the pool orders the reuse), and the reserved total is bounded by the
-// peak CONCURRENT use -- not by the number of streams ever seen.  qd_shutdown trims the pools.
-struct LiveBuf {
+// Scratch arena.  Every entry point that needs scratch opens a WsScope on its stream; workspace() hands it a SLAB
+// (a plain hipMalloc buffer kept by the library) that no other live call holds, and the scope's end records the
+// slab's `done` event on the call's stream behind the last kernel that uses it.  The next call that takes the slab --
+// on any stream, from any host thread -- first queues hipStreamWaitEvent(its stream, done): the reuse is ordered on
+// the DEVICE, so no library call waits on the host for earlier work (round 4's hipFreeAsync blocked the host until
+// the stream drained, 1.1 ms per 2DES grid: profiles/r04/2des/hipfree_block.txt).  Ordering by event rather than by
+// stream identity keeps reuse correct when a stream is destroyed and its handle recycled, and
+// no stream-ordered pool is involved (round 4's parked pool buffers faulted under rocprofv3 --pmc).
+//   - a request takes the smallest idle slab of at least the request and at most 4x it, else a new one (sizes are
+//     rounded up to a power of two >= 64 KiB, so a call sequence of varying sizes settles on a few slabs);
+//   - the reservation is bounded by the peak CONCURRENT scratch (two live calls never share a slab) -- not by the
+//     number of streams seen -- plus idle slabs, which are released (hipFree) once more than kIdleCap bytes are
+//     cached and the event says their last user has completed, on allocation failure, and by qd_shutdown.
+struct Slab {
   void* ptr;
+  size_t bytes;
+  int dev;
+  hipEvent_t done;   // recorded behind the slab's last user
+  bool busy;         // held by a live WsScope
+  bool recorded;     // `done` has been recorded at least once
+};
+struct LiveRef {
+  Slab* slab;
   hipStream_t st;
 };
-static thread_local std::vector<LiveBuf> g_live;
+static std::mutex g_mu;              // guards g_slabs and every Slab's busy / recorded fields
+static std::vector<Slab*> g_slabs;
+static thread_local std::vector<LiveRef> g_live;
 static thread_local int g_depth = 0;
-static std::mutex g_pool_mu;
-static std::set<int> g_pool_ready;
+static constexpr size_t kIdleCap = (size_t)16 << 30;
 
-static int ensure_pool(int dev) {
-  std::lock_guard<std::mutex> lk(g_pool_mu);
-  if (g_pool_ready.count(dev)) return QD_OK;
-  hipMemPool_t pool;
-  QD_HIP(hipDeviceGetDefaultMemPool(&pool, dev));
-  uint64_t thr = UINT64_MAX;
-  QD_HIP(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr));
-  g_pool_ready.insert(dev);
-  return QD_OK;
+static size_t slab_size(size_t bytes) {
+  size_t s = (size_t)64 << 10;
+  while (s < bytes) s <<= 1;
+  return s;
+}
+
+static bool slab_idle_done(const Slab* s) {
+  return !s->busy && (!s->recorded || hipEventQuery(s->done) == hipSuccess);
+}
+
+// frees slab k (caller holds g_mu; the slab is idle and its last user has completed)
+static void drop_slab(size_t k) {
+  Slab* s = g_slabs[k];
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  if (cur != s->dev) (void)hipSetDevice(s->dev);
+  (void)hipFree(s->ptr);
+  (void)hipEventDestroy(s->done);
+  if (cur != s->dev) (void)hipSetDevice(cur);
+  delete s;
+  g_slabs.erase(g_slabs.begin() + (long)k);
+}
+
+// releases idle, completed slabs until at most `keep` bytes are cached (caller holds g_mu)
+static void trim_idle(size_t keep) {
+  size_t tot = 0;
+  for (const Slab* s : g_slabs) tot += s->bytes;
+  for (size_t k = g_slabs.size(); tot > keep && k-- > 0;)
+    if (slab_idle_done(g_slabs[k])) {
+      tot -= g_slabs[k]->bytes;
+      drop_slab(k);
+    }
 }
 
 WsScope::WsScope(hipStream_t s) : st(s), mark(g_live.size()) { ++g_depth; }
 
 WsScope::~WsScope() {
-  // stream-ordered release: runs after the work this call queued on `st`
-  for (size_t k = g_live.size(); k > mark; --k) (void)hipFreeAsync(g_live[k - 1].ptr, g_live[k - 1].st);
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (size_t k = g_live.size(); k > mark; --k) {
+    Slab* s = g_live[k - 1].slab;
+    // every kernel of this call that touches the slab is queued on st by now
+    if (hipEventRecord(s->done, g_live[k - 1].st) == hipSuccess) {
+      s->recorded = true;
+    } else {   // cannot order a later reuse behind this call: wait for the stream instead
+      (void)hipStreamSynchronize(g_live[k - 1].st);
+      s->recorded = false;
+    }
+    s->busy = false;
+  }
   g_live.resize(mark);
   --g_depth;
 }
 
 int workspace(WsSlot slot, size_t bytes, void** ptr, hipStream_t st) {
-  (void)slot;  // the slot names the buffer's role; every call gets its own allocation
+  (void)slot;  // the slot names the buffer's role; every call gets its own slab
   if (g_depth <= 0) {
     set_error("internal: workspace() outside a WsScope");
     return QD_EINVAL;
   }
   int dev = 0;
   QD_HIP(hipGetDevice(&dev));
-  int rc = ensure_pool(dev);
-  if (rc) return rc;
-  void* p = nullptr;
-  hipError_t e = hipMallocAsync(&p, bytes ? bytes : 16, st);
-  if (e != hipSuccess) {
-    set_error("workspace allocation of %zu bytes failed: %s", bytes, hipGetErrorString(e));
-    return QD_ENOMEM;
+  const size_t want = slab_size(bytes ? bytes : 16);
+  std::lock_guard<std::mutex> lk(g_mu);
+  Slab* best = nullptr;
+  for (Slab* s : g_slabs)
+    if (!s->busy && s->dev == dev && s->bytes >= want && s->bytes / 4 <= want && (!best || s->bytes < best->bytes))
+      best = s;
+  if (best) {
+    // device-side order behind the slab's previous user (no host wait)
+    if (best->recorded) QD_HIP(hipStreamWaitEvent(st, best->done, 0));
+  } else {
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, want);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      trim_idle(0);
+      e = hipMalloc(&p, want);
+    }
+    if (e != hipSuccess) {
+      set_error("workspace allocation of %zu bytes failed: %s", want, hipGetErrorString(e));
+      return QD_ENOMEM;
+    }
+    hipEvent_t ev = nullptr;
+    e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e != hipSuccess) {
+      (void)hipFree(p);
+      set_error("workspace event creation failed: %s", hipGetErrorString(e));
+      return QD_EHIP;
+    }
+    best = new Slab{p, want, dev, ev, false, false};
+    g_slabs.push_back(best);
+    trim_idle(kIdleCap);
   }
-  g_live.push_back({p, st});
-  *ptr = p;
+  best->busy = true;
+  g_live.push_back({best, st});
+  *ptr = best->ptr;
   return QD_OK;
 }
 
 void free_workspaces() {
-  std::lock_guard<std::mutex> lk(g_pool_mu);
-  int cur = 0;
-  (void)hipGetDevice(&cur);
-  for (int dev : g_pool_ready) {
-    hipMemPool_t pool;
-    (void)hipSetDevice(dev);
-    (void)hipDeviceSynchronize();
-    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) (void)hipMemPoolTrimTo(pool, 0);
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (size_t k = g_slabs.size(); k-- > 0;) {
+    Slab* s = g_slabs[k];
+    if (s->busy) continue;   // held by a call still running in another host thread
+    if (s->recorded) (void)hipEventSynchronize(s->done);
+    drop_slab(k);
   }
-  (void)hipSetDevice(cur);
 }
 
 int pool_stats(size_t* reserved, size_t* used) {
-  int dev = 0;
-  QD_HIP(hipGetDevice(&dev));
-  hipMemPool_t pool;
-  QD_HIP(hipDeviceGetDefaultMemPool(&pool, dev));
-  uint64_t r = 0, u = 0;
-  QD_HIP(hipMemPoolGetAttribute(pool, hipMemPoolAttrReservedMemCurrent, &r));
-  QD_HIP(hipMemPoolGetAttribute(pool, hipMemPoolAttrUsedMemCurrent, &u));
-  if (reserved) *reserved = (size_t)r;
-  if (used) *used = (size_t)u;
+  std::lock_guard<std::mutex> lk(g_mu);
+  size_t r = 0, u = 0;
+  for (const Slab* s : g_slabs) {
+    r += s->bytes;
+    if (!slab_idle_done(s)) u += s->bytes;
+  }
+  if (reserved) *reserved = r;
+  if (used) *used = u;
   return QD_OK;
 }
 

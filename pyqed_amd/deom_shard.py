@@ -207,6 +207,9 @@ class CollectiveExchange:
         for q in sorted(me.recv):
             pos = np.searchsorted(exp[q], plans[q].send[rank])
             idx.append(q * self.E + pos)
+        # the packed export rows are this band's own rows, checked once here (the device gather runs unchecked)
+        if len(exp[rank]) and (int(exp[rank].min()) < 0 or int(exp[rank].max()) >= me.n_own):
+            raise ValueError(f"band {rank}: export rows outside [0, {me.n_own})")
         self.n_halo = len(me.halo)
         self.halo_idx = torch.from_numpy(np.concatenate(idx).astype(np.int64) if idx else np.zeros(0, np.int64)).to(
             self.dev)

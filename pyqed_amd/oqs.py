@@ -35,22 +35,27 @@ HERM_NP64_MIN_BATCH = 160   # 33 <= N <= 64 (padded to 64): the general split-K 
                             # Hermitian DM-steps/s; B = 192 1.18M vs 1.40M)
 
 
-_HERM_CHECKED = {}   # id(H) -> (weakref to H, H._version, result)
+_HERM_CHECKED = {}   # id(H) -> (weakref to H, H._version, H.data_ptr(), result)
 
 
 def _is_hermitian_cached(H: torch.Tensor) -> bool:
-    """H == H^+ bit for bit.  The check is a device reduction plus a host synchronisation, so its result is kept per
-    tensor object and version (a weak reference guards against a new tensor at a recycled id; an in-place update
-    bumps _version): repeated calls on the same Hamiltonian skip it."""
+    """H == H^+ bit for bit.  The check is a device reduction plus a host synchronisation, so a True result is kept
+    per tensor object, version and storage address (a weak reference guards against a new tensor at a recycled id; an
+    in-place torch update bumps _version; a re-pointed .data changes data_ptr): repeated calls on the same
+    Hamiltonian skip it.  Writes torch cannot see -- raw device-pointer writes through ctypes / DLPack into H's
+    storage -- are not detected: a caller that mutates H that way passes hermitian= explicitly."""
     import weakref
     key = id(H)
     hit = _HERM_CHECKED.get(key)
-    if hit is not None and hit[0]() is H and hit[1] == H._version:
-        return hit[2]
+    if hit is not None and hit[0]() is H and hit[1] == H._version and hit[2] == H.data_ptr():
+        return True
     res = bool(torch.equal(H, H.transpose(-1, -2).conj()))
     if len(_HERM_CHECKED) > 64:
         _HERM_CHECKED.clear()
-    _HERM_CHECKED[key] = (weakref.ref(H), H._version, res)
+    if res:   # a False result is cheap to recompute and must not stick (the Hermitian kernel is the risky pick)
+        _HERM_CHECKED[key] = (weakref.ref(H), H._version, H.data_ptr(), res)
+    else:
+        _HERM_CHECKED.pop(key, None)
     return res
 
 

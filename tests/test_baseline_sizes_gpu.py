@@ -23,6 +23,28 @@ def test_redfield_n128_evolve_matches_reference():
     assert relerr(r.rholist[-1], g["rho_final"]) < TOL
 
 
+@pytest.mark.gpu
+def test_lindblad_n128_b256_headline_dispatch_matches_oracle():
+    """The benched headline instantiation itself: N = 128, n_c = 1, B = 256 pure states, the
+    bench's seeded inputs and dt, auto dispatch (exactly Hermitian states -> the persistent Hermitian kernel
+    lindblad_rk4_kernel<128, true, true>), 5 RK4 steps, against the oracle's RK4 of oqs.liouvillian (oqs.py:697-714,
+    1596-1696) on a spread of the 256 matrices, first and last included."""
+    import torch
+    from oracle import lindblad as olb
+    from pyqed_amd import lindblad_rk4
+    N, B, steps, dt = 128, 256, 5, 1e-3
+    H, cs = olb.synthetic_lindblad(N, nc=1)
+    rho0 = olb.random_pure_states(B, N, seed=2)
+    sel = [0, 1, 63, 64, 127, 128, 200, 255]
+    ref = olb.lindblad_batch(H, cs, rho0[sel], dt, steps)
+    dev = torch.device("cuda", 0)
+    rho = torch.from_numpy(rho0.copy()).to(dev)
+    lindblad_rk4(torch.from_numpy(H).to(dev), torch.from_numpy(np.array(cs)).to(dev), rho, dt, steps)
+    got = rho.cpu().numpy()
+    assert relerr(got[sel], ref) < 1e-12
+    assert np.array_equal(got, np.conj(np.swapaxes(got, 1, 2)))   # every stage exactly Hermitian
+
+
 def test_redfield_n128_tensor_rows_match_reference():
     """Host setup at N = 128 (no GPU): rows of the reference's csr R (oqs.py:519-570) from this package's GLF
     operands, R[(a,b),(c,d)] = P[a,c] d_bd + d_ac Q[d,b] + sum_k L_k[a,c] R_k[d,b] (row-major vec, SURVEY §8

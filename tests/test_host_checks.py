@@ -20,3 +20,12 @@ def test_hermitian_check_cache_follows_the_tensor():
         c = torch.eye(6, dtype=torch.complex128)
         assert _is_hermitian_cached(c)
         del c
+
+
+def test_hermitian_check_cache_follows_a_repointed_data():
+    """swapping the storage under the same tensor object (h.data = ...) must not reuse a cached True."""
+    a = torch.randn(6, 6, dtype=torch.complex128)
+    h = a + a.conj().T
+    assert _is_hermitian_cached(h)
+    h.data = torch.randn(6, 6, dtype=torch.complex128)
+    assert not _is_hermitian_cached(h)

@@ -447,6 +447,58 @@ def test_workspace_bounded_over_many_streams():
     assert max(reserved) <= 2 * reserved[0], reserved
 
 
+def test_scratch_reuse_is_device_ordered_across_streams():
+    """VERDICT r04 item 1 (SURVEY §8(b) threading): library calls do not wait on the host, and a scratch slab released
+    by a call still running on one stream is reused by a call on ANOTHER stream only behind it on the device
+    (qd_runtime.hip: hipStreamWaitEvent on the slab's event).  A long general-path batch (B = 8 at N = 128: split-K
+    path, scratch per matrix) is queued on raw stream A; the same call is queued at once on raw stream B (it takes A's
+    slab while A's kernels still run); then both streams are destroyed and a fresh stream C -- whose handle may be a
+    recycled one -- runs a third call.  Each result matches the oracle, and the long call returns to the host in well
+    under its device time."""
+    import ctypes
+    import time
+    import torch
+    from oracle import lindblad as olb
+    from pyqed_amd import _lib
+    hip = ctypes.CDLL("libamdhip64.so")
+    N, B, dt, steps = 128, 8, 1e-3, 300
+    H, cs = olb.synthetic_lindblad(N, nc=1)
+    dev = torch.device("cuda", 0)
+    lib = _lib.load()
+    Ht, Ct = torch.from_numpy(H).to(dev), torch.from_numpy(np.array(cs)).to(dev)
+    r0 = [olb.random_pure_states(B, N, seed=31 + k) for k in range(3)]
+    rhos = [torch.from_numpy(r.copy()).to(dev) for r in r0]
+    torch.cuda.synchronize()
+
+    def mk():
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+        return s
+
+    def call(rho, s):
+        rc = lib.qd_lindblad_rk4(Ht.data_ptr(), Ct.data_ptr(), 1, rho.data_ptr(), B, N, dt, steps, None, 0, None,
+                                 None, 0, s)
+        _lib.check(rc, "qd_lindblad_rk4")
+
+    sa, sb = mk(), mk()
+    t0 = time.perf_counter()
+    call(rhos[0], sa)
+    host_a = time.perf_counter() - t0
+    call(rhos[1], sb)
+    assert hip.hipStreamSynchronize(sa) == 0
+    dev_a = time.perf_counter() - t0
+    assert hip.hipStreamSynchronize(sb) == 0
+    assert hip.hipStreamDestroy(sa) == 0 and hip.hipStreamDestroy(sb) == 0
+    sc = mk()
+    call(rhos[2], sc)
+    assert hip.hipStreamSynchronize(sc) == 0 and hip.hipStreamDestroy(sc) == 0
+    sel = [0, 5, 7]
+    for k in range(3):
+        ref = olb.lindblad_batch(H, cs, r0[k][sel], dt, steps)
+        assert relerr(rhos[k].cpu().numpy()[sel], ref) < TOL, k
+    assert host_a < 0.3 * dev_a, (host_a, dev_a)
+
+
 @pytest.mark.parametrize("N,B", [(64, 24), (48, 100), (64, 200)])
 def test_lindblad_np64_hermitian_dispatch_matches_oracle(N, B):
     """Default dispatch (hermitian=None) for exactly Hermitian batches at N_p = 64 (the general split-K path below
