@@ -609,7 +609,7 @@ def bench_spo2(dev, steps, n=256, dt=0.05):
                      "unit": "GB/s", "frac": round(bytes_per_step * steps / ev / 1e9 / HBM_PEAK_GBS, 4),
                      "bytes_per_step": bytes_per_step,
                      "traffic": (measured_traffic("spo2_row_q16_kernel<2>", 1) + measured_traffic("spo2_col_q16_kernel<2>", 1))
-                     if n == 256 and os.environ.get("QD_SPO_Q16", "1") != "0" else None,
+                     if n == 256 else None,
                      "traffic_unit": "HBM bytes per Strang step (row + column pass; PMC FETCH_SIZE+WRITE_SIZE, calibrated; "
                                      "profiles/pmc_traffic.json)",
                      "note": "working set (7 MiB) is MALL-resident; two dependent passes per step bound it (latency)"},

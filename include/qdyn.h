@@ -65,6 +65,36 @@ int qd_synchronize(void* stream);     /* hipStreamSynchronize                 */
  * idle cache, not by the number of streams. */
 int qd_workspace_stats(size_t* reserved, size_t* used);
 
+/* Process options: the library's only run-time switches.  Each is read once from
+ * the environment variable named below when the library loads; qd_set_option
+ * changes it for the whole process (thread-safe).  Dispatch is otherwise a
+ * function of the problem's shape alone.
+ *   QD_OPT_COOP_LAUNCH  (QD_COOP_LAUNCH, default 1): 0 launches the persistent
+ *       hand-off kernels (qd_deom_rk4_banded, the single-trajectory Lindblad
+ *       launch) with a plain launch instead of hipLaunchCooperativeKernel (same
+ *       kernels and residency; rocprofv3 faults at exit after cooperative launches);
+ *   QD_OPT_FAKE_TIMEOUT (QD_TEST_FAKE_TIMEOUT, default 0): tests only; 1 makes
+ *       those two launches report a hand-off timeout after a real run, to exercise
+ *       the callers' recovery;
+ *   QD_OPT_GLF_PATH     (QD_GLF_PATH, default QD_GLF_AUTO): the Lindblad / GLF
+ *       batch path -- QD_GLF_SINGLE (single-trajectory launch, where it applies),
+ *       QD_GLF_SPLIT (a workgroup per output block and phase; pair blocks for
+ *       Hermitian batches), QD_GLF_PERSISTENT (a workgroup per matrix); for
+ *       comparing the paths on one input.
+ * qd_take_path copies the dispatch decisions of this thread's calls since the
+ * last qd_take_path (space-separated kernel-path names) into buf and clears them. */
+#define QD_OPT_COOP_LAUNCH 0
+#define QD_OPT_FAKE_TIMEOUT 1
+#define QD_OPT_GLF_PATH 2
+#define QD_OPT_COUNT 3
+#define QD_GLF_AUTO 0
+#define QD_GLF_SINGLE 1
+#define QD_GLF_SPLIT 2
+#define QD_GLF_PERSISTENT 3
+int qd_set_option(int opt, int value);
+int qd_get_option(int opt, int* value);      /* value: host pointer */
+int qd_take_path(char* buf, size_t len);     /* buf: host pointer   */
+
 /* ------------------------------------------------------------ Lindblad --- */
 /*
  * Batched RK4 propagation of the Lindblad master equation
@@ -357,7 +387,7 @@ int qd_heom_chain_euler(qd_c128* ados, int B, int nado, int ns, const qd_c128* H
  *   psi  [B][N] in/out; nsteps RK4 steps
  *   snap [B][nsteps/save_every][N]  psi after steps save_every, 2 save_every, ... or NULL
  *   E [ne][N][N], obs [B][nsteps/save_every + 1][ne] = <psi|E_m|psi> at t0 and at
- *   every snapshot (phys.obs, phys.py:1266-1283), or NULL.   N <= 2048.
+ *   every snapshot (phys.obs, phys.py:1266-1283), or NULL.   Any N.
  */
 int qd_tdse_rk4(const qd_c128* H, qd_c128* psi, int B, int N, double dt,
                 int nsteps, int save_every, qd_c128* snap, const qd_c128* E,
@@ -371,7 +401,7 @@ int qd_tdse_rk4(const qd_c128* H, qd_c128* psi, int B, int N, double dt,
  * start time).  fvals is a HOST array [nblocks][nd] (f_d(t_k), complex).
  *   psi  [B][N] in/out; snap [B][nblocks][N] psi after each block, or NULL;
  *   E [ne][N][N], obs [B][nblocks+1][ne] = <psi|E_m|psi> at t0 and after
- *   each block, or NULL.   N <= 2048, 0 <= nd <= 16, nout >= 1.
+ *   each block, or NULL.   Any N, 0 <= nd <= 16, nout >= 1.
  */
 int qd_tdse_driven_rk4(const qd_c128* H0, const qd_c128* Hd, int nd,
                        const qd_c128* fvals, qd_c128* psi, int B, int N,

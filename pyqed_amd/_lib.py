@@ -22,6 +22,12 @@ QD_ERCCL = -3
 QD_ENOMEM = -4
 QD_EBUSY = -5
 
+# process options (include/qdyn.h QD_OPT_*)
+QD_OPT_COOP_LAUNCH = 0
+QD_OPT_FAKE_TIMEOUT = 1
+QD_OPT_GLF_PATH = 2
+GLF_PATHS = {"auto": 0, "single": 1, "split": 2, "persistent": 3}
+
 c_int = ctypes.c_int
 c_double = ctypes.c_double
 c_long = ctypes.c_long
@@ -38,6 +44,9 @@ SIGNATURES = {
     "qd_shutdown": (c_int, []),
     "qd_synchronize": (c_int, [c_void_p]),
     "qd_workspace_stats": (c_int, [ctypes.POINTER(c_size_t), ctypes.POINTER(c_size_t)]),
+    "qd_set_option": (c_int, [c_int, c_int]),
+    "qd_get_option": (c_int, [c_int, ctypes.POINTER(c_int)]),
+    "qd_take_path": (c_int, [ctypes.c_char_p, c_size_t]),
     "qd_lindblad_rk4": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_double, c_int,
                                 c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "qd_lindblad_rk4_herm": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_double, c_int,
@@ -171,6 +180,22 @@ def ensure_device(device: torch.device) -> None:
     with torch.cuda.device(idx):
         check(lib.qd_init(idx), "qd_init")
     _inited_devices.add(idx)
+
+
+def set_option(opt: int, value: int) -> int:
+    """Set a process option (qd_set_option); returns the previous value."""
+    lib = load()
+    prev = c_int(0)
+    check(lib.qd_get_option(opt, ctypes.byref(prev)), "qd_get_option")
+    check(lib.qd_set_option(opt, int(value)), "qd_set_option")
+    return prev.value
+
+
+def take_path() -> str:
+    """The kernel paths this thread's library calls took since the last take_path() (qd_take_path)."""
+    buf = ctypes.create_string_buffer(4096)
+    check(load().qd_take_path(buf, len(buf)), "qd_take_path")
+    return buf.value.decode()
 
 
 def stream_ptr(device: torch.device | None = None) -> int:

@@ -998,89 +998,74 @@ int deom_launch_stage(const DeomParams& p, hipStream_t st) {
   const int ns = p.ns, K = p.K, nmod = p.nmod, B = p.B, nmax = p.nmax, bminor = p.bminor;
   const size_t ns2 = (size_t)ns * ns;
   const size_t tot = (size_t)B * nmax * ns2;
-  // group kernel when ns^2 <= 64 lanes and K <= 8; MFMA tile kernel for 9 <= ns <= 16 (nmod <= 2, K <= 21);
-  // else the element kernel (QD_DEOM_MFMA=0 keeps ns > 8 on the element kernel, for A/B runs)
+  // group kernel when ns^2 <= 64 lanes and K <= 8; MFMA tile kernel for 9 <= ns <= 16 (nmod <= 2, K <= 21); the
+  // tiled kernels for what the element kernel's LDS tables (ns <= 16, nmod <= 8) do not hold; else the element kernel
   int G = 1;
   while (G < (int)ns2) G *= 2;
   const bool grp = G <= 64 && K <= 8;
-  const char* mf_env = getenv("QD_DEOM_MFMA");
-  const bool mfma = !grp && !bminor && ns >= 9 && ns <= 16 && nmod <= 2 && K <= 21 && !(mf_env && mf_env[0] == '0');
+  const bool mfma = !grp && !bminor && ns >= 9 && ns <= 16 && nmod <= 2 && K <= 21;
   QD_CHECK_ARG(!bminor || grp, "qd_deom_rk4_ado_major: needs ns^2 <= 64 and K <= 8 (group kernel)");
   QD_CHECK_ARG(!grp || (size_t)B * nmax * G < (1u << 31), "qd_deom_rk4: B nmax = %zu ADO rows exceed the 32-bit lane range", (size_t)B * nmax);
   const size_t nthreads = grp ? (size_t)B * nmax * G : tot;
   // A small hierarchy (one at L = 12, K = 5: 24.8k lanes) as 256-thread blocks would occupy ~100 of the
-  // 256 CUs, each CU then issuing the loads of 4 waves; 64-thread blocks spread the same lanes over every
-  // CU.  QD_DEOM_TPB overrides (64 or 256) for A/B runs.
+  // 256 CUs, each CU then issuing the loads of 4 waves; 64-thread blocks spread the same lanes over every CU.
   int tpb = (nthreads + DEOM_TPB - 1) / DEOM_TPB < 1024 ? 64 : DEOM_TPB;
-  if (const char* s = getenv("QD_DEOM_TPB")) tpb = atoi(s) == 64 ? 64 : DEOM_TPB;
   if (!grp) tpb = DEOM_TPB;
   int grid = (int)((nthreads + tpb - 1) / tpb);
   // XCD classes for the group kernel (p.xsplit, see the kernel): batches of 8k hierarchies are dealt over the
-  // 8 block classes by default; QD_DEOM_XCD = 0 (flat), 1, 2, 4 or 8 overrides where B allows it.
+  // 8 block classes
   DeomParams q = p;
   q.xsplit = 0;
-  if (grp) {
-    int X = (B >= 8 && B % 8 == 0) ? 8 : 0;
-    if (const char* s = getenv("QD_DEOM_XCD")) {
-      const int v = atoi(s);
-      X = (v == 1 || v == 2 || v == 4 || v == 8) && B % v == 0 ? v : 0;
-    }
-    if (X > 0) {
-      q.xsplit = X;
-      const size_t per = (size_t)(B / X) * nmax * G;   // lanes per class
-      grid = 8 * (int)((per + tpb - 1) / tpb);
-    }
+  if (grp && B >= 8 && B % 8 == 0) {
+    q.xsplit = 8;
+    const size_t per = (size_t)(B / 8) * nmax * G;   // lanes per class
+    grid = 8 * (int)((per + tpb - 1) / tpb);
   }
   // non-temporal rho / acc from 64 MB of state per buffer (four buffers of 25 MB at 64 hierarchies of the bench
   // hierarchy stay in the 256 MB Infinity Cache: 32.7 vs 34.2 us per stage plain / non-temporal; at 256, 101 MB
-  // each: 127 vs 116 us, profiles/r02/deom/nontemporal_state_ab.txt); QD_DEOM_NT = 0 / 1 forces either
+  // each: 127 vs 116 us, profiles/r02/deom/nontemporal_state_ab.txt)
   q.ntst = tot * sizeof(c128) >= ((size_t)64 << 20);
-  if (const char* s = getenv("QD_DEOM_NT")) q.ntst = atoi(s) != 0;
   const size_t lds = (size_t)(1 + nmod) * ns2 * sizeof(c128);   // H(t), Q(t) of the group kernel
   // the software-pipelined persistent form (undriven ns = 2 ADO-major batches of >= 64 hierarchies in 8 XCD classes,
-  // no hierarchy chunks); QD_DEOM_PIPE=0 keeps the stage kernels.  Its buffer loads take 32-bit byte offsets: every
-  // table below 2^31 - 2^20 bytes, __umul24 factors below 2^24.
-  const char* pe = getenv("QD_DEOM_PIPE");
+  // no hierarchy chunks).  Its buffer loads take 32-bit byte offsets: every table below 2^31 - 2^20 bytes, __umul24
+  // factors below 2^24.
   const bool small_tables = (size_t)nmax * B * 64 < ((size_t)1 << 31) - ((size_t)1 << 20) && nmax < (1 << 24) &&
                             (size_t)B * 64 < ((size_t)1 << 24);
   const bool pipe_ok = grp && G == 4 && q.horner && bminor && q.xsplit == 8 && B >= 64 && K <= 6 &&
-                       !(pe && pe[0] == '0') && tpb == DEOM_TPB && small_tables;
+                       tpb == DEOM_TPB && small_tables;
   // hierarchy chunks of 16 in classes of more (ADO-major) for the stage kernels: 256 hierarchies = 8 classes of 32,
   // see the kernel; not for the pipelined form (256 hierarchies: 97.0 us per stage unchunked vs 102.7-103.3 for the
-  // chunked stage kernel, profiles/r04/deom/deom_bchunk_pipe_ab.txt).  QD_DEOM_BCHUNK overrides (0 = off, else a
-  // divisor of the class size)
+  // chunked stage kernel, profiles/r04/deom/deom_bchunk_pipe_ab.txt)
   q.bchunk = 0;
   if (grp && bminor && q.xsplit > 0) {
     const int Bx = B / q.xsplit;
-    int c = (!pipe_ok && Bx > 16 && Bx % 16 == 0) ? 16 : 0;
-    if (const char* s = getenv("QD_DEOM_BCHUNK")) c = atoi(s);
-    q.bchunk = (c > 0 && c < Bx && Bx % c == 0) ? c : 0;
+    q.bchunk = (!pipe_ok && Bx > 16 && Bx % 16 == 0) ? 16 : 0;
   }
   // wave-uniform ADO (scalar tables): ADO-major, classes (chunks) of a multiple of 64 / G hierarchies, 64-multiple
   // blocks
-  const char* ue = getenv("QD_DEOM_UNI");
   const int wb = q.bchunk > 0 ? q.bchunk : (q.xsplit > 0 ? B / q.xsplit : 0);
-  const bool uni = grp && G == 4 && bminor && q.xsplit > 0 && wb % (64 / G) == 0 && tpb % 64 == 0 &&
-                   !(ue && ue[0] == '0');
-  // the tiled kernel: everything the element kernel's LDS tables (ns <= 16, nmod <= 8) do not hold
-  // (QD_DEOM_TILED=1 forces it wherever the layout allows, for tests / A/B)
-  const char* te = getenv("QD_DEOM_TILED");
-  const bool tiled = !bminor && ((!grp && !mfma && (ns > DEOM_MAX_NS || nmod > DEOM_MAX_NMOD)) || (te && te[0] == '1'));
+  const bool uni = grp && G == 4 && bminor && q.xsplit > 0 && wb % (64 / G) == 0 && tpb % 64 == 0;
+  const bool tiled = !bminor && !grp && !mfma && (ns > DEOM_MAX_NS || nmod > DEOM_MAX_NMOD);
+  const bool first = p.step == 0 && p.stage == 0;   // dispatch notes once per run (qd_take_path)
+  auto note = [&](const char* name) {
+    if (first) note_path(name);
+  };
   auto launch_stage = [&]() {
     if (tiled) {
       q.xsplit = 0;
-      // ns >= 17: MFMA tiles (QD_DEOM_TMFMA=0 keeps the VALU tile kernel, for A/B runs and tests)
-      const char* tm = getenv("QD_DEOM_TMFMA");
-      if (ns >= 17 && !(tm && tm[0] == '0')) {
+      if (ns >= 17) {   // MFMA tiles
+        note("deom_tmfma");
         const int nt = (ns + 15) / 16, nbk = (nt + 1) / 2;
         hipLaunchKernelGGL(deom_stage_tmfma_kernel, dim3((unsigned)((long)B * nmax * nbk * nbk)), dim3(256), 0, st, q);
         return;
       }
+      note("deom_tile");
       const int nt = (ns + DEOM_TT - 1) / DEOM_TT;
       hipLaunchKernelGGL(deom_stage_tile_kernel, dim3((unsigned)((long)B * nmax * nt * nt)), dim3(256), 0, st, q);
       return;
     }
     if (mfma) {
+      note("deom_mfma16");
       const int wg = (int)(((long)B * nmax + 3) / 4);
       const size_t lds_m = (size_t)(256 * (1 + nmod) + 4 * 16 * 17) * sizeof(c128);
       if (nmod == 1) hipLaunchKernelGGL(deom_stage_mfma16_kernel<1>, dim3(wg), dim3(256), lds_m, st, q);
@@ -1088,10 +1073,11 @@ int deom_launch_stage(const DeomParams& p, hipStream_t st) {
       return;
     }
     if (!grp) {
+      note("deom_element");
       hipLaunchKernelGGL(deom_stage_kernel, dim3(grid), dim3(tpb), 0, st, q);
       return;
     }
-    // the software-pipelined persistent form (pipe_ok above); QD_DEOM_PIPE_BPC sets the workgroups per class
+    // the software-pipelined persistent form (pipe_ok above)
     if (pipe_ok && q.bchunk == 0) {
       auto go = [&](const void* fn, auto kern) {
         // workgroups per class: what one XCD's CUs hold at once (every wave persistent, no tail generation)
@@ -1109,18 +1095,23 @@ int deom_launch_stage(const DeomParams& p, hipStream_t st) {
           last_dev = dev;
           last_bpc = std::max(1, per_cu) * std::max(1, cus / 8);
         }
-        int bpc = last_bpc;
-        if (const char* s = getenv("QD_DEOM_PIPE_BPC")) bpc = std::max(1, atoi(s));
-        hipLaunchKernelGGL(kern, dim3((unsigned)(8 * bpc)), dim3(DEOM_TPB), lds, st, q);
+        hipLaunchKernelGGL(kern, dim3((unsigned)(8 * last_bpc)), dim3(DEOM_TPB), lds, st, q);
       };
-      if (K == 5) go((const void*)deom_stage_pipe_kernel<5>, deom_stage_pipe_kernel<5>);
-      else if (K <= 4) go((const void*)deom_stage_pipe_kernel<4>, deom_stage_pipe_kernel<4>);
-      else go((const void*)deom_stage_pipe_kernel<6>, deom_stage_pipe_kernel<6>);
+      if (K == 5) {
+        note("deom_pipe_k5");
+        go((const void*)deom_stage_pipe_kernel<5>, deom_stage_pipe_kernel<5>);
+      } else if (K <= 4) {
+        note("deom_pipe_k4");
+        go((const void*)deom_stage_pipe_kernel<4>, deom_stage_pipe_kernel<4>);
+      } else {
+        note("deom_pipe_k6");
+        go((const void*)deom_stage_pipe_kernel<6>, deom_stage_pipe_kernel<6>);
+      }
       return;
     }
-    const char* w5e = getenv("QD_DEOM_W5");   // 0: keep the unconstrained kernel for >= 64 hierarchies (A/B)
     auto launch_g4 = [&](auto hmc) {
       constexpr int HM = decltype(hmc)::value;
+      note(uni ? "deom_grp4_uniform" : (K == 5 && HM && B >= 64) ? "deom_grp4_w5" : "deom_grp4");
       if (uni) {
         if (K <= 4) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 4, true, true, HM>), dim3(grid), dim3(tpb), lds, st, q);
         else if (K == 5) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 5, true, true, HM>), dim3(grid), dim3(tpb), lds, st, q);
@@ -1128,13 +1119,14 @@ int deom_launch_stage(const DeomParams& p, hipStream_t st) {
         else hipLaunchKernelGGL((deom_stage_grp_kernel<4, 8, true, true, HM>), dim3(grid), dim3(tpb), lds, st, q);
       } else {
         if (K <= 4) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 4, true, false, HM>), dim3(grid), dim3(tpb), lds, st, q);
-        else if (K == 5 && HM && B >= 64 && !(w5e && w5e[0] == '0'))
+        else if (K == 5 && HM && B >= 64)
           hipLaunchKernelGGL((deom_stage_grp_w5_kernel<4, 5, true, false, 1>), dim3(grid), dim3(tpb), lds, st, q);
         else if (K == 5) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 5, true, false, HM>), dim3(grid), dim3(tpb), lds, st, q);
         else if (K <= 6) hipLaunchKernelGGL((deom_stage_grp_kernel<4, 6, true, false, HM>), dim3(grid), dim3(tpb), lds, st, q);
         else hipLaunchKernelGGL((deom_stage_grp_kernel<4, 8, true, false, HM>), dim3(grid), dim3(tpb), lds, st, q);
       }
     };
+    if (G != 4) note("deom_grp");
     switch (G) {
       case 1: hipLaunchKernelGGL((deom_stage_grp_kernel<1, 8, false>), dim3(grid), dim3(tpb), lds, st, q); break;
       case 4:  // ns = 2; registers sized to K (ym/yp/indices scale with KMAX); K = 5 (the bench bath, Pade npsd = 4):
@@ -1206,9 +1198,8 @@ int deom_run(qd_c128* ados, int B, int nmax, int K, int ns, const int32_t* minus
   p.nsteps = nsteps;
   p.dt = dt;
   p.bminor = bminor;
-  // Horner-form RK4 unless the run is driven (QD_DEOM_HORNER=0 keeps the classic form, for A/B runs)
-  const char* he = getenv("QD_DEOM_HORNER");
-  p.horner = !Hdip && !Qdip && !(he && he[0] == '0');
+  // Horner-form RK4 unless the run is driven
+  p.horner = !Hdip && !Qdip;
   static const int stage_time[4] = {0, 1, 1, 2};
   for (int s = 0; s < nsteps; ++s) {
     p.step = s;
@@ -1776,11 +1767,10 @@ __global__ __launch_bounds__(TPB) void deom_band_kernel(BandParams p) {
 // (hipLaunchCooperativeKernel checks the grid against the occupancy of the kernel and refuses an oversize one with
 // hipErrorCooperativeLaunchTooLarge instead of stranding bands; +15-19 us once per run, MI355X_MICROARCH.md row
 // coop-launch).  Work queued on other streams can still delay a band's start; the bounded spin then sets *status and
-// the caller re-runs on the stage launches (DEOMSolver.run).  QD_DEOM_BAND_COOP=0: plain launch (A/B).
+// the caller re-runs on the stage launches (DEOMSolver.run).  QD_OPT_COOP_LAUNCH = 0: plain launch (profiling).
 template <typename Kern>
 hipError_t band_launch_one(Kern kern, BandParams p, int nbands, int tpb, size_t lds, hipStream_t st) {
-  const char* ce = getenv("QD_DEOM_BAND_COOP");
-  if (ce && ce[0] == '0') {
+  if (!option(QD_OPT_COOP_LAUNCH)) {
     hipLaunchKernelGGL(kern, dim3(nbands), dim3(tpb), lds, st, p);
     return hipGetLastError();
   }
@@ -1898,13 +1888,14 @@ extern "C" int qd_deom_rk4_banded(qd_c128* ados, int nmax, int K, int ns, const 
     p.dt = dt;
     hipError_t le;
     if (G == 4) {
-      const char* fe = getenv("QD_DEOM_BAND_FAST");
-      const bool fast = nmod == 1 && !(fe && fe[0] == '0');
+      const bool fast = nmod == 1;
+      note_path(fast && (K == 5 || K == 6) ? "deom_banded_fast" : "deom_banded");
       if (fast && K == 5) le = launch_band<4, 5, true, true>(p, nbands, tpb, lds, st);        // the bench bath
       else if (fast && K == 6) le = launch_band<4, 6, true, true>(p, nbands, tpb, lds, st);   // its stretch (npsd 5)
       else if (K <= 5) le = launch_band<4, 5, true>(p, nbands, tpb, lds, st);
       else le = launch_band<4, 8, true>(p, nbands, tpb, lds, st);
     } else {
+      note_path("deom_banded_g16");
       le = launch_band<16, 8, false>(p, nbands, tpb, lds, st);
     }
     if (le == hipErrorCooperativeLaunchTooLarge) {
@@ -1914,8 +1905,8 @@ extern "C" int qd_deom_rk4_banded(qd_c128* ados, int nmax, int K, int ns, const 
       return QD_EBUSY;
     }
     QD_HIP(le);
-    if (const char* fe = getenv("QD_DEOM_BAND_FAKE_TIMEOUT"))   // tests: report a hand-off timeout after the run
-      if (fe[0] == '1') QD_HIP(hipMemsetAsync(stat, 1, 1, st));
+    if (option(QD_OPT_FAKE_TIMEOUT))   // tests: report a hand-off timeout after the run
+      QD_HIP(hipMemsetAsync(stat, 1, 1, st));
 #ifdef QD_PHASE_TIMING
     {   // per-phase wall-clock (100 MHz ticks) summed over the stages: mean and max over bands, per stage, in us
       std::vector<unsigned long long> h((size_t)nbands * 4);

@@ -149,7 +149,8 @@ extern "C" int qd_fft_axis(qd_c128* data, int outer, int n, int inner, int inver
                (long)outer * n * inner);
   hipStream_t st = (hipStream_t)stream;
   const int batch = outer * inner;
-  const bool pow2 = n >= 16 && n <= 1024 && (n & (n - 1)) == 0 && !std::getenv("QD_FFT_GENERIC");
+  const bool pow2 = n >= 16 && n <= 1024 && (n & (n - 1)) == 0;
+  note_path(pow2 ? "fft_pow2" : "fft_any");
   if (pow2) {
     void* w = nullptr;
     int rc = workspace(WS_MISC, n * sizeof(c128), &w, st);

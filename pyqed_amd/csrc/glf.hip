@@ -366,67 +366,12 @@ __device__ __forceinline__ void split_herm_rk4(const LindbladParams& p, c128* rh
   if (gi != gj) out[mid] = cconj(v);
 }
 
-template <int BT>
-__global__ __launch_bounds__(CG_WG) void glf_split_hk_kernel(LindbladParams p) {
-  __shared__ CgLds<BT> L;
-  __shared__ CgSeg segs[1 + MAX_NC];
-  const int nb = p.Np / BT;
-  int pi = blockIdx.x, bm = 0;   // pair index -> (bm, bn), row-major over the upper block triangle
-  while (pi >= nb - bm) {
-    pi -= nb - bm;
-    ++bm;
-  }
-  const int bn = bm + pi, b = blockIdx.y;
-  const int Np = p.Np, nc = p.nc;
-  const size_t NN = (size_t)Np * Np;
-  const c128* r = split_buf(p, b, p.rin);
-  c128* rn = p.rout ? split_buf(p, b, p.rout) : nullptr;
-  c128* rho = p.rho + (size_t)b * NN;
-  const c128* Y = p.ws + (size_t)b * (2 + nc) * NN + 2 * NN;
-  const int tps = Np / CG_KT;
-  if (threadIdx.x == 0) {
-    segs[0].A = p.mK + (size_t)bm * BT * Np;
-    segs[0].B = r + bn * BT;
-    for (int c = 0; c < nc; ++c) {
-      segs[1 + c].A = Y + (size_t)c * NN + (size_t)bm * BT * Np;
-      segs[1 + c].B = p.Cd + (size_t)c * NN + bn * BT;
-    }
-  }
-  __syncthreads();
-  CgAcc<BT> XU, XL;
-  {
-    CgSegAScaled<BT> pa{segs, tps, Np, bm < bn ? 2.0 : 1.0};
-    CgSegB<BT> pb{segs, tps, Np};
-    split_gemm<BT>((1 + nc) * tps, pa, pb, L, XU);
-  }
-  if (bm < bn) {
-    if (threadIdx.x == 0) {
-      segs[0].A = p.mK + (size_t)bn * BT * Np;
-      segs[0].B = r + bm * BT;
-    }
-    __syncthreads();
-    CgSegA<BT> pa{segs, tps, Np};
-    CgSegB<BT> pb{segs, tps, Np};
-    split_gemm<BT>(tps, pa, pb, L, XL);
-  }
-  constexpr int LD = BT + 1;
-  static_assert(BT * LD * sizeof(c128) <= sizeof(CgLds<BT>), "LDS transpose buffer");
-  c128* T = reinterpret_cast<c128*>(&L);
-  auto put = [&](int row, int col, c128 v) { T[row * LD + col] = v; };
-  if (bm < bn) cg_epilogue<BT>(XL, put);
-  else cg_epilogue<BT>(XU, put);
-  __syncthreads();
-  cg_epilogue<BT>(XU, [&](int row, int col, c128 v) {
-    if (bm == bn && row > col) return;
-    split_herm_rk4(p, rho, rn, bm * BT + row, bn * BT + col, cadd(v, cconj(T[col * LD + row])));
-  });
-}
-
-// The same stage with each off-diagonal pair's two GEMMs on two workgroups (glf_split_hk2_kernel, grid x = pairs +
-// off-diagonal pairs): the pair's workgroup computes XU (16 K-tiles at N_p = 128, n_c = 1), an extra workgroup XL
-// (8 K-tiles), so the longest workgroup no longer runs all 24.  Both publish their block to a slab (write-through)
-// and take the pair's arrival ticket (split_arrive, the split-K hand-off); the last arriver forms k from its own
-// accumulator and the other's slab and runs the update.  The same GEMMs and sums as glf_split_hk_kernel: bit-identical.
+// Each off-diagonal pair's two GEMMs run on two workgroups (grid x = pairs + off-diagonal pairs): the pair's
+// workgroup computes XU (16 K-tiles at N_p = 128, n_c = 1), an extra workgroup XL (8 K-tiles), so the longest
+// workgroup does not run all 24 (round 3's one-workgroup-per-pair form, removed in round 5).  Both publish their
+// block to a slab (write-through) and take the pair's arrival ticket (split_arrive, the split-K hand-off); the last
+// arriver forms k from its own accumulator and the other's slab and runs the update.  A diagonal block takes the
+// half-weighted X and its own transpose.
 template <int BT>
 __global__ __launch_bounds__(CG_WG) void glf_split_hk2_kernel(LindbladParams p) {
   __shared__ CgLds<BT> L;
@@ -596,11 +541,18 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   // state workspace: per-matrix scratch (+ padded rho when N != Np)
   const bool pad = (Np != N);
   if (Np > 128) herm = 0;  // the Hermitian path is single-block
-  // Split path (glf_split_*): each output block of a phase is a workgroup, for batches too small to
-  // occupy the chip with one persistent workgroup per matrix.  QD_GLF_SPLIT=0 / 1 forces it off / on.
-  // Measured (tools/glf_split_bench.py, N = 128 / 256, B = 1 .. 256): the split path wins for every batch
-  // below ~192 matrices at Np <= 128 (6.6x at one trajectory) and at every batch size above Np = 128;
-  // the block is the largest BT < Np that still gives >= 512 workgroups, else 32.
+  // Paths (QD_OPT_GLF_PATH forces one where it applies; otherwise the batch shape decides):
+  //  - single-trajectory launch (glf_single.hip) for few undriven non-Hermitian matrices, below;
+  //  - split path (glf_split_*): each output block of a phase is a workgroup, for batches too small to occupy the chip
+  //    with one persistent workgroup per matrix.  Measured (tools/glf_split_bench.py, N = 128 / 256, B = 1 .. 256):
+  //    it wins below ~192 matrices at Np <= 128 (6.6x at one trajectory) and at every batch size above Np = 128; the
+  //    block is the largest BT < Np that still gives >= 512 workgroups, else 32.  nc > MAX_NC: the persistent
+  //    kernels' chunked segment lists (the split kernels hold one LDS table);
+  //  - Hermitian Lindblad batches at Np = 128 below 208 matrices: the pair-block split path (glf_split_hk2_kernel,
+  //    32-blocks; tools/glf_hsplit_sweep.sh: 198k / 233k / 258k / 264k DM-steps/s at 64 / 128 / 192 / 224 matrices
+  //    against 82k / 164k / 242k / 278k for the persistent kernel);
+  //  - else the persistent kernel (a workgroup per matrix).
+  const int force = option(QD_OPT_GLF_PATH);
   int split_bt = 0;
   bool hsplit = false;
   {
@@ -611,50 +563,27 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
         break;
       }
     }
-    if (const char* e = std::getenv("QD_GLF_SPLIT_BT")) {  // A/B override: 32, 64 or 128 (dividing Np)
-      const int v = std::atoi(e);
-      if ((v == 32 || v == 64 || v == 128) && Np % v == 0) bt = v;
-    }
-    // nc > MAX_NC: the persistent kernels' chunked segment lists (the split kernels hold one LDS table)
-    bool use = !herm && Np >= 64 && (Np > 128 || B < 192) && nc <= MAX_NC;
-    if (const char* e = std::getenv("QD_GLF_SPLIT")) use = std::atoi(e) != 0 && !herm && Np >= 64 && nc <= MAX_NC;
-    if (use) split_bt = bt;
-    // Hermitian Lindblad batches below the persistent kernel's range: the pair-block split path
-    // (glf_split_hk_kernel; QD_GLF_HSPLIT=0 keeps the persistent Hermitian kernel)
-    const char* hse = std::getenv("QD_GLF_HSPLIT");
-    // N = 128 (tools/glf_hsplit_sweep.sh): 32-blocks 198k / 233k / 258k / 264k DM-steps/s at 64 / 128 / 192 / 224
-    // matrices against 82k / 164k / 242k / 278k for the persistent kernel, so the split path runs below 208;
-    // 64-blocks are no better overall (172k / 231k / 232k / 247k).  QD_GLF_HSPLIT_MAX / _BT override (A/B).
-    const char* hme = std::getenv("QD_GLF_HSPLIT_MAX");
-    const int hmax = hme ? std::atoi(hme) : 208;
-    // Np = 64 only on request (QD_GLF_HSPLIT_NP64=1) until its crossover is measured
-    const char* h64 = std::getenv("QD_GLF_HSPLIT_NP64");
-    const bool np_ok = Np == 128 || (Np == 64 && h64 && h64[0] == '1');
-    if (herm && src == GLF_FROM_LINDBLAD && np_ok && B < hmax && nc <= MAX_NC && !(hse && hse[0] == '0')) {
+    const bool split_ok = !herm && Np >= 64 && nc <= MAX_NC;
+    const bool hsplit_ok = herm && src == GLF_FROM_LINDBLAD && Np == 128 && nc <= MAX_NC;
+    const bool want_split = force == QD_GLF_SPLIT || (force == QD_GLF_AUTO && (Np > 128 || B < (herm ? 208 : 192)));
+    if (want_split && split_ok) split_bt = bt;
+    if (want_split && hsplit_ok) {
       hsplit = true;
       split_bt = 32;
-      if (const char* e = std::getenv("QD_GLF_HSPLIT_BT")) split_bt = std::atoi(e) == 64 && Np % 64 == 0 ? 64 : 32;
     }
   }
-  // Split-K of the split path when its blocks leave the chip under-filled: up to 256 workgroups per phase,
-  // >= 3 K-tiles each, at most 4 (k phase) / 8 (Y phase) partial slabs per block.  Measured (N = 128 / 256,
-  // one trajectory, tools/ks_sweep.sh): 4 k-splits 12.0k / 6.9k steps/s, 8: 11.8k / 6.6k, 16: 9.8k / 5.8k,
-  // none: 8.4k / 4.2k.  QD_GLF_SPLITK=0 turns it off; QD_GLF_KS / QD_GLF_YS force the counts (A/B).
+  // Split-K of the (general) split path when its blocks leave the chip under-filled: up to 256 workgroups per phase,
+  // >= 3 K-tiles each, at most 4 (k phase) / 8 (Y phase) partial slabs per block.  Measured (N = 128 / 256, one
+  // trajectory, tools/ks_sweep.sh): 4 k-splits 12.0k / 6.9k steps/s, 8: 11.8k / 6.6k, 16: 9.8k / 5.8k, none: 8.4k / 4.2k.
   int ks = 1, ys = 1;
   if (split_bt) {
     const long blocks = (long)B * (Np / split_bt) * (Np / split_bt);
     const int Tk = (2 + nc) * (Np / CG_KT), Ty = Np / CG_KT;
     ks = hsplit ? 1 : (int)std::max(1L, std::min<long>({4L, 256L / blocks, (long)Tk / 3}));
     ys = nc ? (int)std::max(1L, std::min<long>({8L, 256L / (blocks * nc), (long)Ty / 3})) : 1;
-    if (const char* e = std::getenv("QD_GLF_SPLITK"))
-      if (std::atoi(e) == 0) ks = ys = 1;
-    if (const char* e = std::getenv("QD_GLF_KS")) ks = std::max(1, std::min(Tk, std::atoi(e)));  // A/B overrides
-    if (const char* e = std::getenv("QD_GLF_YS")) ys = nc ? std::max(1, std::min(Ty, std::atoi(e))) : 1;
   }
-  // two-workgroup Hermitian pairs (glf_split_hk2_kernel; QD_GLF_HK2=0 keeps one workgroup per pair): one N_p^2
-  // slab slot per matrix holds the off-diagonal pairs' XU / XL blocks
-  const char* hk2e = std::getenv("QD_GLF_HK2");
-  const bool hk2 = hsplit && !(hk2e && hk2e[0] == '0');
+  // Hermitian pairs on two workgroups each: one N_p^2 slab slot per matrix holds the off-diagonal pairs' XU / XL blocks
+  const bool hk2 = hsplit;
   const int kslots = (ks > 1 ? ks : 0) + (hk2 ? 1 : 0);
   const size_t per = (size_t)(split_bt ? 2 + nc + kslots + (ys > 1 ? nc * ys : 0)
                                        : glf_slots(Np, nc, herm)) * NN;
@@ -695,13 +624,10 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
 
   // Few undriven matrices: one persistent launch with a workgroup per 16 x 16 output tile (glf_single.hip; the split
   // path takes eight dependent launches per step).  A refused cooperative launch or a hand-off timeout re-runs the
-  // batch below from a saved copy.  QD_GLF_SINGLE=0 / 1 turns it off / keeps it on wherever it applies.
+  // batch below from a saved copy (on the path the shape selects: split, or persistent when the single path was forced).
   {
-    const char* sge = std::getenv("QD_GLF_SINGLE");
-    const bool forced_split = std::getenv("QD_GLF_SPLIT") != nullptr;   // A/B runs and tests of the split path
-    const bool single = !herm && !nd && B <= glf_single_max_batch(Np, nc) && !(sge && sge[0] == '0') &&
-                        !(forced_split && !(sge && sge[0] == '1'));
-    if (single) {
+    const bool fits = !herm && !nd && B <= glf_single_max_batch(Np, nc);
+    if (fits && (force == QD_GLF_AUTO || force == QD_GLF_SINGLE)) {
       void* wsave = nullptr;
       if ((rc = workspace(WS_MISC, (size_t)B * NN * sizeof(c128), &wsave, st))) return rc;
       QD_HIP(hipMemcpyAsync(wsave, rho_p, (size_t)B * NN * sizeof(c128), hipMemcpyDeviceToDevice, st));
@@ -709,6 +635,7 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
       rc = glf_single_run(mK, iKd, Cop, Cd, nc, eT, ne, rho_p, B, N, Np, dt, nsteps, obs,
                           save_every > 0 ? snap : nullptr, save_every, &timed_out, st);
       if (rc == QD_OK && !timed_out) {
+        note_path("glf_single");
         if (pad) {
           const size_t tot = (size_t)B * N * N;
           hipLaunchKernelGGL(unpad_kernel, dim3((int)std::min<size_t>((tot + threads - 1) / threads, 65535)),
@@ -747,7 +674,6 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   p.herm = herm;
   p.hseg = herm && src == GLF_FROM_LINDBLAD;
   p.tbuf = nullptr;
-  p.stagger = 0;
   p.stage = p.rin = p.rout = 0;
   p.ks = ks;
   p.ys = ys;
@@ -756,7 +682,6 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   p.yslab = split_bt ? p.kslab + (size_t)B * kslots * NN : nullptr;
   p.ticket = split_bt ? (unsigned*)(scratch + (size_t)B * per + (pad ? (size_t)B * NN : 0)) : nullptr;
   if (split_bt && (ks > 1 || ys > 1 || hk2)) QD_HIP(hipMemsetAsync(p.ticket, 0, nticket * sizeof(unsigned), st));
-  if (const char* e = std::getenv("QD_STAGGER_US")) p.stagger = (unsigned long long)(std::atof(e) * 100.0);  // 100 MHz
 #ifdef QD_PHASE_TIMING
   const bool timing = true;  // diagnostics build: per-phase clocks to stderr
 #else
@@ -791,17 +716,9 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
           QD_SPLIT(glf_split_y_kernel, dim3(nb * nb, nc, B * ys));
           QD_HIP(hipGetLastError());
         }
-        if (hk2) {   // split_bt is 32 or 64 here
+        if (hk2) {   // split_bt is 32 here
           const unsigned np2 = nb * (nb + 1) / 2 + nb * (nb - 1) / 2;
-          if (split_bt == 64)
-            hipLaunchKernelGGL(glf_split_hk2_kernel<64>, dim3(np2, B), dim3(CG_WG), 0, st, p);
-          else
-            hipLaunchKernelGGL(glf_split_hk2_kernel<32>, dim3(np2, B), dim3(CG_WG), 0, st, p);
-        } else if (hsplit) {
-          if (split_bt == 64)
-            hipLaunchKernelGGL(glf_split_hk_kernel<64>, dim3(nb * (nb + 1) / 2, B), dim3(CG_WG), 0, st, p);
-          else
-            hipLaunchKernelGGL(glf_split_hk_kernel<32>, dim3(nb * (nb + 1) / 2, B), dim3(CG_WG), 0, st, p);
+          hipLaunchKernelGGL(glf_split_hk2_kernel<32>, dim3(np2, B), dim3(CG_WG), 0, st, p);
         } else {
           QD_SPLIT(glf_split_k_kernel, dim3(nb * nb, B * ks));
         }
@@ -813,6 +730,8 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
     }
     return QD_OK;
   };
+  note_path(split_bt ? (hsplit ? "glf_split_pairs" : "glf_split") : nc > MAX_NC ? "glf_persistent_chunk"
+                                                                                : "glf_persistent");
   auto launch = [&]() -> int {
     if (split_bt) return launch_split();
     if (nc > MAX_NC) return glf_launch_chunk(p, B, st);   // glf_chunk.hip

@@ -29,7 +29,6 @@ struct LindbladParams {
                            // sum A r Lam^+), so its redundant tiles below the diagonal may be skipped (cg_herm_x_gemm)
   double dt;
   unsigned long long* tbuf;  // [B][8] per-phase wall-clock ticks (QD_PHASE_TIMING diagnostics) or null
-  unsigned long long stagger;  // start offset (wall-clock ticks) of the odd workgroup group of each XCD
   int stage, rin, rout;        // split path: RK4 stage; stage input / output buffer (0 = rho, 1/2 = scratch 0/1)
   int ks, ys;                  // split path: K-splits of the k / Y phases (1 = none)
   c128* kslab;                 // [B][nb^2][ks][BT^2] partial k blocks
@@ -212,13 +211,6 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
   const int nb = Np / BT;
   const double dt = p.dt;
   CgAcc<BT> A;
-  // Phase offset: the workgroups run identical schedules, so without an offset every CU reaches its
-  // memory-bound RK4 epilogue at the same moment.  Delaying every other workgroup of each XCD
-  // (blocks b, b + 8 share an XCD) interleaves one group's epilogue with the other's MFMA phase.
-  if (p.stagger && ((b >> 3) & 1)) {
-    const unsigned long long t0s = wall_clock64();
-    while (wall_clock64() - t0s < p.stagger) __builtin_amdgcn_s_sleep(32);
-  }
   QD_TIMING_DECL
 
   for (int step = 0; step < p.nsteps; ++step) {

@@ -305,11 +305,11 @@ hipError_t sg_launch3(SingleParams p, int grid, bool coop, hipStream_t st) {
 }
 // The 3-product complex MACs on a half-filled chip (<= 128 workgroups), the 4-product ones above: N = 128, one matrix
 // 29.7k -> 34.9k steps/s and two 61.7k -> 69.4k with 3 products, four (256 workgroups) 117k -> 103k; N = 32, 64
-// matrices 2.91M -> 2.61M (profiles/r04/lindblad/glf_single_bench.txt).  QD_GLF_SINGLE_3M=0 / 1 forces either (A/B).
+// matrices 2.91M -> 2.61M (profiles/r04/lindblad/glf_single_bench.txt).
 template <int KS, int NC>
 hipError_t sg_launch(SingleParams p, int grid, bool coop, hipStream_t st) {
-  const char* me = getenv("QD_GLF_SINGLE_3M");
-  const bool m3 = me ? me[0] == '1' : (grid <= 128 && NC < 2);   // (NC = 2 with 3 products spills)
+  const bool m3 = grid <= 128 && NC < 2;   // (NC = 2 with 3 products spills)
+  note_path(m3 ? "glf_single_3m" : "glf_single_4m");
   if (m3) return sg_launch3<KS, NC, true>(p, grid, coop, st);
   return sg_launch3<KS, NC, false>(p, grid, coop, st);
 }
@@ -367,8 +367,7 @@ int glf_single_run(const c128* P, const c128* Q, const c128* Lop, const c128* Ro
   QD_HIP(hipMemsetAsync(tw, 0, (size_t)B * T2 * 8 * sizeof(unsigned long long), st));
   p.tim = (unsigned long long*)tw;
 #endif
-  const char* ce = getenv("QD_GLF_SINGLE_COOP");
-  const bool coop = !(ce && ce[0] == '0');
+  const bool coop = option(QD_OPT_COOP_LAUNCH) != 0;
   const int grid = B * T2;
   hipError_t e = hipErrorInvalidValue;
 #define SG_CASE(KS_)                                                    \
@@ -389,8 +388,8 @@ int glf_single_run(const c128* P, const c128* Q, const c128* Lop, const c128* Ro
     return QD_EBUSY;
   }
   QD_HIP(e);
-  if (const char* fe = getenv("QD_GLF_SINGLE_FAKE_TIMEOUT"))   // tests: report a hand-off timeout after the run
-    if (fe[0] == '1') QD_HIP(hipMemsetAsync(p.status, 1, 1, st));
+  if (option(QD_OPT_FAKE_TIMEOUT))   // tests: report a hand-off timeout after the run
+    QD_HIP(hipMemsetAsync(p.status, 1, 1, st));
   int h = 0;
   QD_HIP(hipMemcpyAsync(&h, p.status, sizeof(int), hipMemcpyDeviceToHost, st));
   QD_HIP(hipStreamSynchronize(st));

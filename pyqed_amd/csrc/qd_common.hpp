@@ -60,6 +60,13 @@ int workspace(WsSlot slot, size_t bytes, void** ptr, hipStream_t st);
 int pool_stats(size_t* reserved, size_t* used);
 void free_workspaces();
 
+// Process options (qd_runtime.hip): the library's only run-time switches, read once from the environment when the
+// library loads and changeable with qd_set_option (include/qdyn.h QD_OPT_*).  Dispatch is otherwise a function of
+// the problem's shape alone.
+int option(int opt);
+// Records a dispatch decision of the current call for qd_take_path (tests assert which kernel a shape reaches).
+void note_path(const char* name);
+
 // ---------------------------------------------------------------- complex
 struct alignas(16) c128 {
   double re, im;

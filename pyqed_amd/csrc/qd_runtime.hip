@@ -1,7 +1,9 @@
 // qd_runtime.hip — error reporting, device selection and the library's scratch arena.
 #include "qd_common.hpp"
 
+#include <atomic>
 #include <mutex>
+#include <string>
 #include <vector>
 
 namespace qd {
@@ -167,9 +169,58 @@ int pool_stats(size_t* reserved, size_t* used) {
   return QD_OK;
 }
 
+// ---------------------------------------------------------------- options and dispatch notes
+static std::atomic<int> g_opt[QD_OPT_COUNT];
+static const bool g_opt_init = [] {
+  struct {
+    int opt;
+    const char* env;
+    int dflt;
+  } tab[] = {{QD_OPT_COOP_LAUNCH, "QD_COOP_LAUNCH", 1}, {QD_OPT_FAKE_TIMEOUT, "QD_TEST_FAKE_TIMEOUT", 0},
+             {QD_OPT_GLF_PATH, "QD_GLF_PATH", QD_GLF_AUTO}};
+  for (auto& t : tab) {
+    const char* e = std::getenv(t.env);
+    g_opt[t.opt].store(e && *e ? std::atoi(e) : t.dflt);
+  }
+  return true;
+}();
+
+int option(int opt) { return (opt >= 0 && opt < QD_OPT_COUNT) ? g_opt[opt].load(std::memory_order_relaxed) : 0; }
+
+static thread_local std::string g_path;
+
+void note_path(const char* name) {
+  if (g_path.size() < 4096) {
+    if (!g_path.empty()) g_path += ' ';
+    g_path += name;
+  }
+}
+
 }  // namespace qd
 
 extern "C" {
+
+int qd_set_option(int opt, int value) {
+  QD_CHECK_ARG(opt >= 0 && opt < QD_OPT_COUNT, "qd_set_option: unknown option %d", opt);
+  QD_CHECK_ARG(opt != QD_OPT_GLF_PATH || (value >= QD_GLF_AUTO && value <= QD_GLF_PERSISTENT),
+               "qd_set_option: QD_OPT_GLF_PATH value %d", value);
+  (void)qd::g_opt_init;
+  qd::g_opt[opt].store(value);
+  return QD_OK;
+}
+
+int qd_get_option(int opt, int* value) {
+  QD_CHECK_ARG(opt >= 0 && opt < QD_OPT_COUNT && value, "qd_get_option: bad arguments");
+  *value = qd::option(opt);
+  return QD_OK;
+}
+
+int qd_take_path(char* buf, size_t len) {
+  QD_CHECK_ARG(buf && len > 0, "qd_take_path: bad arguments");
+  std::snprintf(buf, len, "%s", qd::g_path.c_str());
+  qd::g_path.clear();
+  return QD_OK;
+}
 
 int qd_version(void) { return 100; }
 

@@ -216,7 +216,7 @@ __global__ __launch_bounds__(256) void ens_z_uniform_kernel(const c128* Mt, cons
                                                             int nL, int nz, int G, double t0, double dt, int n1,
                                                             int n1p, c128* Z, const c128* alpha, const c128* lamx,
                                                             int K, int Kp, double t3_0, double dt3, int n3, int n3p,
-                                                            int xbx, c128* X, int recur) {
+                                                            int xbx, c128* X) {
   extern __shared__ c128 zs[];
   const int nMB = (M + G - 1) / G;
   if ((int)blockIdx.y >= nMB) {
@@ -240,41 +240,25 @@ __global__ __launch_bounds__(256) void ens_z_uniform_kernel(const c128* Mt, cons
   }
   __syncthreads();
   // round 2: the exponential tables from LDS operands (no global latency inside the loop)
-  const int tab = nz * (16 + nC);
-  if (recur) {
-    // one thread per (member, q): fine[j] = e^{lam j dt} as powers of e^{lam dt}, coarse[l] = beta e^{lam t0} times
-    // powers of e^{16 lam dt} (3 exponentials instead of 16 + nC; relative error ~1e-14)
-    for (int e = threadIdx.x; e < g * nz; e += 256) {
-      const int gi = e / nz, q = e - gi * nz;
-      const c128 l = sLam[gi * nz + q];
-      c128* fine = zs + gi * per + nL * nz + q * 16;
-      c128* coarse = zs + gi * per + nL * nz + nz * 16 + q * nC;
-      const c128 e1 = cexp_t(l, dt);
-      c128 f = cmk(1.0, 0.0);
-      fine[0] = f;
-      for (int j = 1; j < 16; ++j) {
-        f = cmul(f, e1);
-        fine[j] = f;
-      }
-      const c128 e16 = cexp_t(l, 16.0 * dt);
-      c128 c = cmul(sBeta[gi * nz + q], cexp_t(l, t0));
-      for (int u = 0; u < nC; ++u) {
-        coarse[u] = c;
-        c = cmul(c, e16);
-      }
+  // one thread per (member, q): fine[j] = e^{lam j dt} as powers of e^{lam dt}, coarse[l] = beta e^{lam t0} times
+  // powers of e^{16 lam dt} (3 exponentials instead of 16 + nC; relative error ~1e-14)
+  for (int e = threadIdx.x; e < g * nz; e += 256) {
+    const int gi = e / nz, q = e - gi * nz;
+    const c128 l = sLam[gi * nz + q];
+    c128* fine = zs + gi * per + nL * nz + q * 16;
+    c128* coarse = zs + gi * per + nL * nz + nz * 16 + q * nC;
+    const c128 e1 = cexp_t(l, dt);
+    c128 f = cmk(1.0, 0.0);
+    fine[0] = f;
+    for (int j = 1; j < 16; ++j) {
+      f = cmul(f, e1);
+      fine[j] = f;
     }
-  } else {
-    for (int e = threadIdx.x; e < g * tab; e += 256) {
-      const int gi = e / tab, r = e % tab;
-      c128 v;
-      if (r < nz * 16) {
-        v = cexp_t(sLam[gi * nz + r / 16], (double)(r % 16) * dt);
-      } else {
-        const int u = r - nz * 16;
-        const int q = u / nC;
-        v = cmul(sBeta[gi * nz + q], cexp_t(sLam[gi * nz + q], t0 + 16.0 * (double)(u % nC) * dt));
-      }
-      zs[gi * per + nL * nz + r] = v;
+    const c128 e16 = cexp_t(l, 16.0 * dt);
+    c128 c = cmul(sBeta[gi * nz + q], cexp_t(l, t0));
+    for (int u = 0; u < nC; ++u) {
+      coarse[u] = c;
+      c = cmul(c, e16);
     }
   }
   __syncthreads();
@@ -298,26 +282,13 @@ __global__ __launch_bounds__(256) void ens_z_uniform_kernel(const c128* Mt, cons
   }
 }
 
-// Z tables by recurrence (default) or one exponential per entry (QD_Z_RECUR=0, A/B)
-int z_recur() {
-  static const int r = [] {
-    const char* e = std::getenv("QD_Z_RECUR");
-    return e ? std::atoi(e) : 1;
-  }();
-  return r;
-}
-
 // members per block of ens_z_uniform_kernel: tables of <= 32 KB LDS, at most 32 members
 // and at least 1024 member blocks when M allows (M = 4096: 0.128 -> 0.116 ms per 256 x 256 grid; no change at
-// M = 32k, where the LDS cap binds); QD_Z_MINBLOCKS overrides the 1024 (A/B, tools/zblocks_ab.sh)
+// M = 32k, where the LDS cap binds; tools/zblocks_ab.sh)
 int z_group(int nL, int nz, int n1p, int M) {
   const int per = nL * nz + nz * (16 + n1p / 16) + 2 * nz;
   const int G = std::max(1, std::min(32, 2048 / per));
-  static const int mb = [] {
-    const char* e = std::getenv("QD_Z_MINBLOCKS");
-    return e ? std::atoi(e) : 1024;
-  }();
-  return mb > 0 ? std::max(1, std::min(G, M / mb)) : G;
+  return std::max(1, std::min(G, M / 1024));
 }
 // its dynamic LDS bytes
 size_t z_lds(int G, int nL, int nz, int n1p) {
@@ -472,40 +443,28 @@ struct SplitPlan {
   int bt, S;
 };
 SplitPlan split_plan(int Mp, int Np, int tiles) {
-  static const int force = [] {
-    const char* e = std::getenv("QD_ENS_BT");
-    return e ? std::atoi(e) : 0;
-  }();
   auto splits = [&](int bt) {
     const int blocks = (Mp / bt) * (Np / bt);
     return std::max(1, std::min(ceil_div(256, blocks), std::max(1, tiles / 4)));
   };
-  static const int force_s = [] {   // QD_ENS_S: split count override (A/B sweeps)
-    const char* e = std::getenv("QD_ENS_S");
-    return e ? std::atoi(e) : 0;
-  }();
   const int S128 = splits(128);
   const bool small = (Mp / 128) * (Np / 128) * S128 < 256 || tiles / S128 < 32;
-  const int bt = force == 64 || force == 128 ? force : (small ? 64 : 128);
-  const int S = force_s > 0 ? std::max(1, std::min(force_s, tiles)) : splits(bt);
-  return {bt, S};
+  const int bt = small ? 64 : 128;
+  return {bt, splits(bt)};
 }
 
 // fine != nullptr: X is the coarse table of ens_xtab_kernel (generated A operand)
 void launch_ens_gemm(const SplitPlan& pl, const c128* X, int Kp, const c128* Z, int Mp, int Np, int tiles,
                      c128* slabs, hipStream_t st, const c128* fine = nullptr) {
   const dim3 g(Np / pl.bt, Mp / pl.bt, pl.S);
-  // QD_ENS_DEPTH=1/2: K-tiles of global loads in flight on the 64-block path (read per call: tests switch it)
-  // 4,096-member shard: 0.111 ms per grid at 2 vs 0.113 at 1 (tools/ens_depth_ab.sh)
-  const char* de = std::getenv("QD_ENS_DEPTH");
-  const int depth = de ? std::atoi(de) : 2;
+  // the 64-block path keeps two K-tiles of global loads in flight (4,096-member shard: 0.111 ms per grid at 2 vs
+  // 0.113 at 1, tools/ens_depth_ab.sh)
+  note_path(pl.bt == 64 ? (fine ? "ens_gemm64_xtab" : "ens_gemm64") : (fine ? "ens_gemm128_xtab" : "ens_gemm128"));
   if (pl.bt == 64) {
     if (fine)
       hipLaunchKernelGGL((ens_gemm_kernel<64, true>), g, dim3(CG_WG), 0, st, X, Kp, Z, Np, tiles, pl.S, slabs, Mp, fine);
-    else if (depth == 2)
-      hipLaunchKernelGGL((ens_gemm_kernel<64, false, 2>), g, dim3(CG_WG), 0, st, X, Kp, Z, Np, tiles, pl.S, slabs, Mp, fine);
     else
-      hipLaunchKernelGGL((ens_gemm_kernel<64, false>), g, dim3(CG_WG), 0, st, X, Kp, Z, Np, tiles, pl.S, slabs, Mp, fine);
+      hipLaunchKernelGGL((ens_gemm_kernel<64, false, 2>), g, dim3(CG_WG), 0, st, X, Kp, Z, Np, tiles, pl.S, slabs, Mp, fine);
   } else {
     if (fine)
       hipLaunchKernelGGL((ens_gemm_kernel<128, true>), g, dim3(CG_WG), 0, st, X, Kp, Z, Np, tiles, pl.S, slabs, Mp, fine);
@@ -802,12 +761,8 @@ int ens_run(const char* fn, const qd_c128* alpha, const qd_c128* Mt, const qd_c1
   const bool zfast = nL <= ZMAX && nz <= ZMAX && M <= 65535 - 4096;
   const int xbx = ceil_div(Kp, 256), xblocks = xbx * (n3p / XU_ROWS);
   // uniform t3: the A operand is generated in the GEMM staging from (n3p/16 + 16) x Kp tables held in
-  // the X buffer (QD_ENS_XTAB=0: materialise X as before, for A/B runs)
-  static const bool xtab_on = [] {
-    const char* e = std::getenv("QD_ENS_XTAB");
-    return !(e && e[0] == '0');
-  }();
-  const bool xtab = !t3 && xtab_on && plan.bt == 128;  // 64-blocks are already load-bound in the staging
+  // the X buffer (round 3)
+  const bool xtab = !t3 && plan.bt == 128;  // 64-blocks are already load-bound in the staging
   c128* coarse = X;
   c128* fine = X + (size_t)(n3p / 16) * Kp;
   if (xtab) {
@@ -823,8 +778,7 @@ int ens_run(const char* fn, const qd_c128* alpha, const qd_c128* Mt, const qd_c1
     const bool xin = !t3 && !xtab;
     hipLaunchKernelGGL(ens_z_uniform_kernel, dim3(zbx, nMB + (xin ? xblocks : 0)), dim3(256),
                        z_lds(G, nL, nz, n1p), st, (const c128*)Mt, (const c128*)beta, lamz, M, nL, nz, G, t1_0,
-                       dt1, n1, n1p, Z, (const c128*)alpha, (const c128*)lam, K, Kp, t3_0, dt3, n3, n3p, xbx, X,
-                       z_recur());
+                       dt1, n1, n1p, Z, (const c128*)alpha, (const c128*)lam, K, Kp, t3_0, dt3, n3, n3p, xbx, X);
     QD_HIP(hipGetLastError());
     if (Kp > K) {
       hipLaunchKernelGGL(ens_z_pad_kernel, dim3(64), dim3(256), 0, st, K, Kp, n1p, Z);
@@ -961,7 +915,7 @@ extern "C" int qd_response2d_t2_operands_rect(const qd_c128* alpha, const qd_c12
   hipLaunchKernelGGL(ens_z_uniform_kernel, dim3(ceil_div(d.n1p, 256), ceil_div(M, G)), dim3(256),
                      z_lds(G, nr, nq, d.n1p), st, (const c128*)Cm,
                      (const c128*)beta, (const c128*)lamq, M, nr, nq, G, t1_0, dt1, n1, d.n1p, Q, (const c128*)nullptr,
-                     (const c128*)nullptr, d.K, d.Kp, 0.0, 0.0, n3, d.n3p, 1, (c128*)nullptr, z_recur());
+                     (const c128*)nullptr, d.K, d.Kp, 0.0, 0.0, n3, d.n3p, 1, (c128*)nullptr);
   QD_HIP(hipGetLastError());
   if (d.Kp > d.K) {
     hipLaunchKernelGGL(ens_z_pad_kernel, dim3(64), dim3(256), 0, st, d.K, d.Kp, d.n1p, Q);

@@ -670,67 +670,6 @@ __global__ __launch_bounds__(64 * NS) void spo2_row_q16_kernel(c128* psi, const 
   for (int a = 0; a < 4; ++a) psi[(row + 64 * a + 16 * s + g) * NS + c] = x[0][a];
 }
 
-// Row pass for batches (qd_spo2_run_batch, ns = 2): one workgroup per (row i, MB members), wave w = (member
-// w >> 1, state w & 1).  The point operators of row i are shared by every member: the workgroup stages them in
-// LDS once (16 KB, two loads per thread) instead of every wave loading its 8 values per lane from L2 (two thirds of
-// the single-row kernel's loads).  The FFT exchange buffers double as the point-operator exchange (they are never
-// live at the same time).  Same arithmetic and order as spo2_row_q16_kernel<2, false>.
-template <int MB>
-__global__ __launch_bounds__(128 * MB) void spo2_row_q16_batch_kernel(c128* psi, const c128* U, const c128* twy,
-                                                                      int flags, c128* snap, int B, size_t wstride,
-                                                                      size_t sstride) {
-  __shared__ c128 Us[256 * 4];          // [point][row c][col b]
-  __shared__ c128 S[2 * MB * 272];      // per-wave FFT exchange; per member [2][256] point-operator exchange
-  const int i = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 2, s = lane & 3;
-  const int m = w >> 1, c = w & 1;
-  const int member = blockIdx.y * MB + m;
-  const bool live = member < B;          // uniform per wave; dead waves still join the barriers
-  c128* ps = psi + (size_t)(live ? member : 0) * wstride;
-  const size_t row = (size_t)i * 256;
-  c128 x[1][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a) x[0][a] = ps[(row + 64 * a + 16 * s + g) * 2 + c];
-  const bool vh = flags & (ROW_VH1 | ROW_VH2);
-  if (vh) {
-#pragma unroll
-    for (int q = 0; q < 1024 / (128 * MB); ++q) {
-      const int e = threadIdx.x + 128 * MB * q;
-      Us[e] = U[row * 4 + e];
-    }
-  }
-  const Q16Tw t = q16_twiddles(twy, g, s);
-  c128* Sw = S + w * 272;
-  c128* Xs = S + m * 2 * 272;            // member m's exchange: [state][lane * 4 + a] (2 x 256 <= 2 x 272)
-  if (vh) __syncthreads();
-  auto point_op = [&]() {
-#pragma unroll
-    for (int a = 0; a < 4; ++a) Xs[c * 256 + lane * 4 + a] = x[0][a];
-    __syncthreads();
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      const int pt = 64 * a + 16 * s + g;
-      c128 acc = cmk(0, 0);
-#pragma unroll
-      for (int b = 0; b < 2; ++b) acc = cadd(acc, cmul(Us[pt * 4 + c * 2 + b], Xs[b * 256 + lane * 4 + a]));
-      x[0][a] = acc;
-    }
-    __syncthreads();   // Xs aliases the FFT buffers and is rewritten by the next operator
-  };
-  if (flags & ROW_INV) fft256_wave<true, 1>(x, t, Sw, g, s);
-  if (flags & (ROW_VH1 | ROW_VH2)) __syncthreads();   // every wave is done with its FFT buffer before Xs reuses it
-  if (flags & ROW_VH1) point_op();
-  if ((flags & ROW_SNAP) && live) {
-    c128* sn = snap + (size_t)member * sstride;
-#pragma unroll
-    for (int a = 0; a < 4; ++a) sn[(row + 64 * a + 16 * s + g) * 2 + c] = x[0][a];
-  }
-  if (flags & ROW_VH2) point_op();
-  if (flags & ROW_FWD) fft256_wave<false, 1>(x, t, Sw, g, s);
-  if (!live) return;
-#pragma unroll
-  for (int a = 0; a < 4; ++a) ps[(row + 64 * a + 16 * s + g) * 2 + c] = x[0][a];
-}
-
 // Row pass for batches, one wave per (row i, member): the wave holds both states of its points (x[c][a] =
 // psi[64 a + 16 s + g][c]), so the point operators are lane-local (no state exchange through LDS, no workgroup
 // barrier but the one after the operator staging) and every lane loads 32 contiguous bytes per point.  The MB
@@ -839,58 +778,11 @@ __global__ __launch_bounds__(64) void spo2_col_q16_kernel(c128* psi, const c128*
   for (int a = 0; a < 4; ++a) psi[((size_t)(64 * a + 16 * s + g) * pitch + j) * NS + c] = x[0][a];
 }
 
-// Column pass for batches (qd_spo2_run_batch), coalesced: one 512-thread workgroup per 4 adjacent columns
-// and both states of one wavefunction (8 lines, wave w = column j0 + w / 2, state w % 2).  The 256 x 4 x 2
-// tile is read row by row as 128-B contiguous pieces into LDS, each wave runs the register FFT of its line
-// (FFT_x -> * exp_K / (nx ny) -> IFFT_x), the lines go back through LDS and out as 128-B rows.  (The
-// single-wavefunction pass reads each column directly with an 8 KB stride: fine from L2 for one grid,
-// L2-request-bound for a batch.)  NS = 2, nx = ny = 256.
-__global__ __launch_bounds__(512) void spo2_col_tile_kernel(c128* psi, const c128* expKT, const c128* twx,
-                                                            size_t wstride) {
-  __shared__ c128 T[256 * 9];        // [row][8 lines + 1 pad]
-  __shared__ c128 S[8 * 272];        // per-wave FFT exchange
-  psi += blockIdx.y * wstride;
-  const int j0 = blockIdx.x * 4;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 2, s = lane & 3;
-  c128 v[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {      // element e = row * 8 + (column - j0) * 2 + state: 128 B per row
-    const int e = tid + 512 * q, r = e >> 3, cs = e & 7;
-    v[q] = psi[((size_t)r * 256 + j0) * 2 + cs];
-  }
-  const int j = j0 + (w >> 1), c = w & 1;
-  c128 x[1][4], kf[4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a) kf[a] = expKT[(size_t)j * 256 + 64 * a + 16 * s + g];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int e = tid + 512 * q;
-    T[(e >> 3) * 9 + (e & 7)] = v[q];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int a = 0; a < 4; ++a) x[0][a] = T[(64 * a + 16 * s + g) * 9 + w];
-  const Q16Tw t = q16_twiddles(twx, g, s);
-  fft256_wave<false, 1>(x, t, S + w * 272, g, s);
-#pragma unroll
-  for (int a = 0; a < 4; ++a) x[0][a] = cmul(x[0][a], kf[a]);
-  fft256_wave<true, 1>(x, t, S + w * 272, g, s);
-  __syncthreads();                   // every wave has read its line of T
-#pragma unroll
-  for (int a = 0; a < 4; ++a) T[(64 * a + 16 * s + g) * 9 + w] = x[0][a];
-  __syncthreads();
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int e = tid + 512 * q, r = e >> 3, cs = e & 7;
-    psi[((size_t)r * 256 + j0) * 2 + cs] = T[r * 9 + cs];
-  }
-}
-
 // Column pass for batches with NC adjacent columns per 64 NC-thread workgroup and one wave per column holding
 // both states (x[c][a], c = state): the 256 x NC x 2 tile is read and written as NC x 32-B contiguous row pieces
 // (256 B at NC = 8), and the waves' FFT exchange buffers live inside the tile (it is dead between the line reads
 // and the write-back), so the workgroup's LDS is the tile alone (NC = 8: 68 KB, two workgroups per CU as the
-// 4-column kernel).  Same arithmetic per line as spo2_col_tile_kernel.  NS = 2, nx = ny = 256.
+// round-3 4-column kernel).  Same arithmetic per line as spo2_col_q16_kernel.  NS = 2, nx = ny = 256.
 template <int NC>
 __global__ __launch_bounds__(64 * NC) void spo2_col_tile8_kernel(c128* psi, const c128* expKT, const c128* twx,
                                                                  size_t wstride) {
@@ -1162,21 +1054,7 @@ __global__ __launch_bounds__(256) void spo_row64_kernel(c128* psi, const c128* U
     for (int c = 0; c < NS; ++c) pr[(lane16 + 16 * k) * NS + c] = x[c][k];
 }
 
-bool q16_enabled() {
-  static const int on = [] {
-    const char* e = getenv("QD_SPO_Q16");
-    return e ? atoi(e) : 1;
-  }();
-  return on != 0;
-}
-
 bool pow2_in_range(int n) { return n >= 16 && n <= 1024 && (n & (n - 1)) == 0; }
-
-// QD_SPO_GENERIC=1 routes every grid through spo_gen.hip (A/B and tests of the any-size engine)
-bool force_generic() {
-  const char* e = getenv("QD_SPO_GENERIC");
-  return e && e[0] == '1';
-}
 
 // L dispatch helpers
 #define QD_FFT_DISPATCH(L, CALL) \
@@ -1200,7 +1078,7 @@ int twiddles(int L, hipStream_t st, c128* tw) {
 // Launch the latency-shaped row pass (ns <= 2): `rows` rows of length L.
 int row_fast(int L, int ns, int rows, int flags, c128* psi, const c128* U, const c128* tw, c128* snap,
              const c128* expKy, hipStream_t st) {
-  if (L == 256 && q16_enabled()) {
+  if (L == 256) {
     const bool ky = (flags & ROW_KY) && expKy;
 #define RQ16(NS, KYV) hipLaunchKernelGGL((spo2_row_q16_kernel<NS, KYV>), dim3(rows), dim3(64 * NS), 0, st, psi, U, tw, flags, snap, expKy)
     if (ns == 1) { if (ky) RQ16(1, true); else RQ16(1, false); }
@@ -1209,9 +1087,8 @@ int row_fast(int L, int ns, int rows, int flags, c128* psi, const c128* U, const
     QD_HIP(hipGetLastError());
     return QD_OK;
   }
-  // L = 64: register transform, 16 lanes per row (QD_SPO_ROW64=0: the LDS Stockham kernel; A/B, tests)
-  const char* r64e = getenv("QD_SPO_ROW64");
-  if (L == 64 && rows % 16 == 0 && !(flags & ROW_KY) && !(r64e && r64e[0] == '0')) {
+  // L = 64: register transform, 16 lanes per row
+  if (L == 64 && rows % 16 == 0 && !(flags & ROW_KY)) {
     if (ns == 1) hipLaunchKernelGGL(spo_row64_kernel<1>, dim3(rows / 16), dim3(256), 0, st, psi, U, tw, flags, snap);
     else hipLaunchKernelGGL(spo_row64_kernel<2>, dim3(rows / 16), dim3(256), 0, st, psi, U, tw, flags, snap);
     QD_HIP(hipGetLastError());
@@ -1234,7 +1111,7 @@ int row_fast(int L, int ns, int rows, int flags, c128* psi, const c128* U, const
 // `pitch` = points per row of psi.
 int col_fast(int L, int ns, int cols, c128* psi, const c128* expKT, const c128* tw, hipStream_t st, int pitch = -1) {
   if (pitch < 0) pitch = cols;
-  if (L == 256 && q16_enabled()) {
+  if (L == 256) {
     if (ns == 1) hipLaunchKernelGGL(spo2_col_q16_kernel<1>, dim3(cols, 1), dim3(64), 0, st, psi, expKT, tw, cols, pitch);
     else hipLaunchKernelGGL(spo2_col_q16_kernel<2>, dim3(cols, 2), dim3(64), 0, st, psi, expKT, tw, cols, pitch);
     QD_HIP(hipGetLastError());
@@ -1281,7 +1158,8 @@ extern "C" int qd_spo2_run_ex(qd_c128* psi_, const qd_c128* expVh_, const qd_c12
     // workgroup; every other grid runs the any-size engine (spo_gen.hip)
     const size_t row_lds = (size_t)(ny + 2 * ns * ny) * sizeof(c128), col_lds = (size_t)(nx + 4 * ns * nx) * sizeof(c128);
     const bool special = pow2_in_range(nx) && pow2_in_range(ny) && ns <= SPO_MAX_NS && ns * (ny / 4) <= 256 &&
-                         ns * (nx / 4) <= 256 && row_lds <= 160 * 1024 && col_lds <= 160 * 1024 && !force_generic();
+                         ns * (nx / 4) <= 256 && row_lds <= 160 * 1024 && col_lds <= 160 * 1024;
+    note_path(special ? "spo2_pow2" : "spo_any");
     if (!special) {
       const int dims[2] = {nx, ny};
       return spo_generic_run((c128*)psi_, (const c128*)expVh_, (const c128*)expV_, (const c128*)expK_,
@@ -1377,7 +1255,7 @@ extern "C" int qd_spo2_run_batch(qd_c128* psi_, int B, const qd_c128* expVh_, co
   QD_CHECK_ARG(nsteps >= 0 && nout >= 1, "qd_spo2_run_batch: nsteps=%d nout=%d", nsteps, nout);
   const size_t grid_elems = (size_t)nx * ny * ns;
   const int nsave = nsteps / nout;
-  if (!(nx == 256 && ny == 256 && ns <= 2 && q16_enabled())) {
+  if (!(nx == 256 && ny == 256 && ns <= 2)) {
     // other shapes: one member at a time on the single-wavefunction path
     for (int w = 0; w < B; ++w) {
       const int rc = qd_spo2_run_ex(psi_ + w * grid_elems, expVh_, nullptr, expK_, nullptr, nx, ny, ns, nsteps, nout,
@@ -1404,55 +1282,25 @@ extern "C" int qd_spo2_run_batch(qd_c128* psi_, int B, const qd_c128* expVh_, co
                      (const c128*)expK_, nx, ny, 1.0 / ((double)nx * ny), expKT);
   QD_HIP(hipGetLastError());
   const size_t sstride = (size_t)nsave * grid_elems;
-  // ns = 2: MB members per workgroup sharing the staged point operators (QD_SPO_ROWMB = 1 / 2 / 4, default 2; 1 = the
-  // single-row kernel with a batch grid axis)
-  const char* mbe = getenv("QD_SPO_ROWMB");
-  const int rowmb = mbe ? atoi(mbe) : 2;   // 64 wavepackets: MB = 1 405k, 2 438k, 4 418k wavepacket-steps/s
-  // QD_SPO_ROWWAVE: members per workgroup of the wave-per-member row kernel (2 / 4 / 8; 0 = the group kernels above,
-  // which an explicit QD_SPO_ROWMB also selects); 64 wavepackets: group MB = 2 428k, wave MB = 4 476k
-  const char* rwe = getenv("QD_SPO_ROWWAVE");
-  const int rowwave = rwe ? atoi(rwe) : (mbe ? 0 : 4);
+  // ns = 2: a wave per member, 4 members per workgroup sharing the staged point operators (64 wavepackets: 476k
+  // wavepacket-steps/s against 428k for 2-member groups of the single-row kernel); the column pass in tiles of 8
+  // columns (503k against 477k for 4)
+  note_path("spo2_batch256");
   auto row = [&](int flags, c128* sp) {
     if (ns == 1)
       hipLaunchKernelGGL((spo2_row_q16_kernel<1, false>), dim3(nx, B), dim3(64), 0, st, psi, U, twy, flags, sp,
                          (const c128*)nullptr, grid_elems, sstride);
-    else if (rowwave == 4)
+    else
       hipLaunchKernelGGL(spo2_row_wave_kernel<4>, dim3(nx, (B + 3) / 4), dim3(256), 0, st, psi, U, twy, flags, sp, B,
                          grid_elems, sstride);
-    else if (rowwave == 8)
-      hipLaunchKernelGGL(spo2_row_wave_kernel<8>, dim3(nx, (B + 7) / 8), dim3(512), 0, st, psi, U, twy, flags, sp, B,
-                         grid_elems, sstride);
-    else if (rowwave == 2)
-      hipLaunchKernelGGL(spo2_row_wave_kernel<2>, dim3(nx, (B + 1) / 2), dim3(128), 0, st, psi, U, twy, flags, sp, B,
-                         grid_elems, sstride);
-    else if (rowmb == 4)
-      hipLaunchKernelGGL(spo2_row_q16_batch_kernel<4>, dim3(nx, (B + 3) / 4), dim3(512), 0, st, psi, U, twy, flags,
-                         sp, B, grid_elems, sstride);
-    else if (rowmb == 2)
-      hipLaunchKernelGGL(spo2_row_q16_batch_kernel<2>, dim3(nx, (B + 1) / 2), dim3(256), 0, st, psi, U, twy, flags,
-                         sp, B, grid_elems, sstride);
-    else
-      hipLaunchKernelGGL((spo2_row_q16_kernel<2, false>), dim3(nx, B), dim3(128), 0, st, psi, U, twy, flags, sp,
-                         (const c128*)nullptr, grid_elems, sstride);
   };
-  const char* cte = getenv("QD_SPO_COLTILE");   // 0: the per-column pass, 4 / 8 / 16: column tiles
-  const int coltile = cte ? atoi(cte) : 8;   // 64 wavepackets: 4 -> 477k, 8 -> 503k wavepacket-steps/s
   auto col = [&]() {
     if (ns == 1)
       hipLaunchKernelGGL(spo2_col_q16_kernel<1>, dim3(ny, 1, B), dim3(64), 0, st, psi, (const c128*)expKT,
                          (const c128*)twx, ny, ny, grid_elems);
-    else if (coltile == 8)
+    else
       hipLaunchKernelGGL(spo2_col_tile8_kernel<8>, dim3(ny / 8, B), dim3(512), 0, st, psi, (const c128*)expKT,
                          (const c128*)twx, grid_elems);
-    else if (coltile == 16)
-      hipLaunchKernelGGL(spo2_col_tile8_kernel<16>, dim3(ny / 16, B), dim3(1024), 0, st, psi, (const c128*)expKT,
-                         (const c128*)twx, grid_elems);
-    else if (coltile != 0)
-      hipLaunchKernelGGL(spo2_col_tile_kernel, dim3(ny / 4, B), dim3(512), 0, st, psi, (const c128*)expKT,
-                         (const c128*)twx, grid_elems);
-    else
-      hipLaunchKernelGGL(spo2_col_q16_kernel<2>, dim3(ny, 2, B), dim3(64), 0, st, psi, (const c128*)expKT,
-                         (const c128*)twx, ny, ny, grid_elems);
   };
   // the Strang step sequence of qd_spo2_run_ex (both V/2 halves, wpd.py:723-730)
   row(ROW_VH1 | ROW_FWD, nullptr);
@@ -1473,7 +1321,8 @@ extern "C" int qd_spo1d_run(qd_c128* psi_, const qd_c128* expV_, const qd_c128* 
   WsScope wss_((hipStream_t)stream);  // call-scoped scratch (qd_runtime.hip)
   QD_CHECK_ARG(psi_ && expV_ && expVh_ && expK_, "qd_spo1d_run: null pointer");
   QD_CHECK_ARG(nx >= 1 && B >= 1 && nt >= 0 && nout >= 1, "qd_spo1d_run: nx=%d B=%d nt=%d nout=%d", nx, B, nt, nout);
-  if (!pow2_in_range(nx) || force_generic())
+  note_path(pow2_in_range(nx) ? "spo1d_pow2" : "spo_any");
+  if (!pow2_in_range(nx))
     return spo1d_generic_run((c128*)psi_, (const c128*)expV_, (const c128*)expVh_, (const c128*)expK_, nx, B, nt, nout,
                              (c128*)snap_, (hipStream_t)stream);
   hipStream_t st = (hipStream_t)stream;
@@ -1503,7 +1352,8 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
     const size_t row_lds = (size_t)(nz + 2 * ns * nz) * sizeof(c128), col_lds = (size_t)(nx + 4 * ns * nx) * sizeof(c128);
     const bool special = pow2_in_range(nx) && pow2_in_range(ny) && pow2_in_range(nz) && nx <= 256 && ny <= 256 &&
                          nz <= 256 && ns <= SPO_MAX_NS && ns * (nz / 4) <= 256 && ns * (nx / 4) <= 256 &&
-                         row_lds <= 160 * 1024 && col_lds <= 160 * 1024 && !force_generic();
+                         row_lds <= 160 * 1024 && col_lds <= 160 * 1024;
+    note_path(special ? "spo3_pow2" : "spo_any");
     if (!special) {
       const int dims[3] = {nx, ny, nz};
       return spo_generic_run((c128*)psi_, (const c128*)expVh_, nullptr, (const c128*)expK_, nullptr, dims, 3, ns,
@@ -1548,19 +1398,14 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
   };
   // Mid pass: C consecutive inner indices (C * 16 B per row read) per block. C is the largest of
   // 16 / 8 / 4 that still gives >= 4 blocks per CU (on its own worth ~1% at 64^3 x 2: 512 -> 1024
-  // blocks; C = 4 costs 13% at 128^3); QD_SPO3_MID_C overrides it for sweeps.
+  // blocks; C = 4 costs 13% at 128^3; tools/spo3_midc_sweep.sh).
   int midC = 4;
   for (int c : {16, 8}) {
     if (c * ny <= 1024 && inner % c == 0 && (size_t)nx * (inner / c) >= 1024) { midC = c; break; }
   }
-  if (const char* e = getenv("QD_SPO3_MID_C")) {
-    const int c = atoi(e);
-    if ((c == 4 || c == 8 || c == 16) && c * ny <= 1024 && inner % c == 0) midC = c;
-  }
   while (midC > 1 && inner % midC) midC >>= 1;  // inner = nz * ns >= 16 keeps midC >= 4
   // x pass: the latency-shaped two-column kernel (colC = 0), or the LDS-staged kernel over colC
-  // columns x ns states per block (colC * ns * 16 B contiguous per row); QD_SPO3_COL_C overrides
-  // (0 = two-column kernel) for sweeps (tools/spo3_midc_sweep.sh).
+  // columns x ns states per block (colC * ns * 16 B contiguous per row).
   // Default: at <= 64^3 x 2 points and midC >= 8 the LDS-staged kernel with the mid pass's row width
   // (colC * ns == midC, 128 B rows at 64^3 x 2: 41.1 -> 33.4 us per step); above that the
   // two-column kernel (128^3 x 2: 142 us either way, 146 us with colC * ns == midC).
@@ -1569,18 +1414,8 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
     const int c = midC / ns;
     if ((c == 2 || c == 4 || c == 8) && nyz % c == 0 && c * ns * (nx / 4) <= 256) colC = c;
   }
-  if (const char* e = getenv("QD_SPO3_COL_C")) {
-    const int c = atoi(e);
-    if (c == 0 || ((c == 2 || c == 4 || c == 8) && nyz % c == 0 && c * ns * (nx / 4) <= 256)) colC = c;
-  }
-  // QD_SPO3_FAST=0: the generic LDS-staged mid / x kernels instead of the latency-shaped ones (A/B runs)
-  const char* f3e = getenv("QD_SPO3_FAST");
-  const bool fast3 = !(f3e && f3e[0] == '0');
-  // QD_SPO_ROW64=0: the LDS Stockham kernels at L = 64 instead of the 64-point register transforms (A/B, tests)
-  const char* r64e = getenv("QD_SPO_ROW64");
-  const bool r64 = !(r64e && r64e[0] == '0');
   auto col = [&]() -> int {
-    if (colC && fast && fast3 && r64 && nx == 64) {
+    if (colC && fast && nx == 64) {
 #define COL64(CC)                                                                                                    \
   if (ns == 1) hipLaunchKernelGGL((spo_col64_kernel<CC, 1>), dim3(nyz / CC), dim3(16 * CC), 0, st, psi, expKT, twx, nyz); \
   else hipLaunchKernelGGL((spo_col64_kernel<CC, 2>), dim3(nyz / CC), dim3(32 * CC), 0, st, psi, expKT, twx, nyz)
@@ -1589,7 +1424,7 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
       QD_HIP(hipGetLastError());
       return QD_OK;
     }
-    if (colC && fast && fast3) {
+    if (colC && fast) {
       const int threads = std::max(64, colC * ns * (nx / 4));
       const size_t lds = (size_t)(nx + 2 * colC * ns * nx) * sizeof(c128);
 #define COLFASTC(L)                                                                                                       if (colC == 2) { if (ns == 1) hipLaunchKernelGGL((spo2_col_fast_kernel<L, 2, 1>), dim3(nyz / 2), dim3(threads), lds, st, psi, expKT, twx, nyz);                    else hipLaunchKernelGGL((spo2_col_fast_kernel<L, 2, 2>), dim3(nyz / 2), dim3(threads), lds, st, psi, expKT, twx, nyz); }   else if (colC == 4) { if (ns == 1) hipLaunchKernelGGL((spo2_col_fast_kernel<L, 4, 1>), dim3(nyz / 4), dim3(threads), lds, st, psi, expKT, twx, nyz);                    else hipLaunchKernelGGL((spo2_col_fast_kernel<L, 4, 2>), dim3(nyz / 4), dim3(threads), lds, st, psi, expKT, twx, nyz); }   else { if (ns == 1) hipLaunchKernelGGL((spo2_col_fast_kernel<L, 8, 1>), dim3(nyz / 8), dim3(threads), lds, st, psi, expKT, twx, nyz);          else hipLaunchKernelGGL((spo2_col_fast_kernel<L, 8, 2>), dim3(nyz / 8), dim3(threads), lds, st, psi, expKT, twx, nyz); }
@@ -1626,7 +1461,7 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
   auto mid = [&](bool inv) -> int {
     const int grid = nx * (inner / midC);
     const int threads = std::max(64, midC * (ny / 4));
-    if (fast3 && r64 && ny == 64) {
+    if (ny == 64) {
 #define MID64(C)                                                                                                  \
   if (inv) hipLaunchKernelGGL((spo_mid64_kernel<C, true>), dim3(grid), dim3(16 * C), 0, st, psi, twy, inner); \
   else hipLaunchKernelGGL((spo_mid64_kernel<C, false>), dim3(grid), dim3(16 * C), 0, st, psi, twy, inner)
@@ -1635,7 +1470,7 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
       QD_HIP(hipGetLastError());
       return QD_OK;
     }
-    if (fast3 && midC * ny / 4 <= 256 && ny <= 64) {
+    if (midC * ny / 4 <= 256 && ny <= 64) {
 #define MIDF_C(L, C)                                                                                               \
   if (inv) hipLaunchKernelGGL((spo_mid_fast_kernel<L, C, true>), dim3(grid), dim3(threads), 0, st, psi, twy, inner); \
   else hipLaunchKernelGGL((spo_mid_fast_kernel<L, C, false>), dim3(grid), dim3(threads), 0, st, psi, twy, inner)

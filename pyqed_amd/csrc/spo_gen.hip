@@ -98,9 +98,6 @@ struct AxisArgs {
   int O, L, I, C, G, flags, ns;
   FDiv dLC, dC, dLns, dns;   // L C, C, L ns, ns
   int twl;             // 1: twiddles staged in LDS (M more c128 of dynamic LDS)
-  int aux;             // operators staged in LDS with the tile (one load round trip per pass): 1 = U1 (and U2 when it
-                       // differs) rows [G][L][ns][ns]; 2 = the tile's exp_K / N factors [L][C]; 0 = read from HBM/L2
-  int u2same;          // U2 == U1 (the Strang row pass applies exp(-i V dt/2) twice)
   const c128* U1;      // [points][ns][ns] (F_PT1)
   const c128* U2;      // (F_PT2)
   c128* snap;          // (F_SNAP) same layout as psi
@@ -298,22 +295,8 @@ __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
   const int o0 = blockIdx.x * G, i0 = blockIdx.y * C;
   const int gv = min(G, a.O - o0), cv = min(C, I - i0);
   const int tot = G * L * C;
-  // operators of this tile, staged in LDS by the same load phase as the tile (no dependent HBM round trip later)
-  c128* aux = (a.twl ? oth + (size_t)nl * M + M : oth + (size_t)nl * M);
-  const int ns = a.ns, nsq = ns * ns;
-  const int nU = a.aux == 1 ? gv * L * nsq : 0;            // U1 rows of the tile's valid rows (contiguous)
-  const c128* U1 = a.aux == 1 ? aux : a.U1;
-  const c128* U2 = a.aux == 1 ? (a.u2same ? aux : aux + (size_t)G * L * nsq) : a.U2;
+  const int ns = a.ns;
   const int pts = I / ns;
-  for (int q = threadIdx.x; q < nU; q += blockDim.x) {
-    aux[q] = a.U1[(size_t)o0 * L * nsq + q];
-    if (!a.u2same && (a.flags & F_PT2)) aux[(size_t)G * L * nsq + q] = a.U2[(size_t)o0 * L * nsq + q];
-  }
-  if (a.aux == 2)
-    for (int q = threadIdx.x; q < L * C; q += blockDim.x) {
-      const int e = (int)fdiv((unsigned)q, a.dC), c = q - e * C;
-      aux[q] = c < cv ? a.K[(size_t)e * pts + (int)fdiv((unsigned)(i0 + c), a.dns)] : cmk(0.0, 0.0);
-    }
   for (int f = threadIdx.x; f < tot; f += blockDim.x) {
     const int g = (int)fdiv((unsigned)f, a.dLC), r = f - g * (L * C), e = (int)fdiv((unsigned)r, a.dC), c = r - e * C;
     cur[(g * C + c) * M + e] =
@@ -325,7 +308,7 @@ __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
   SPO_MARK(1)
   auto point_op = [&](const c128* U) {   // C == I == ns: line g * ns + s holds state s of row g
     const int n = G * L * ns;
-    const int row0 = a.aux == 1 ? 0 : o0;   // staged rows start at the tile's first row
+    const int row0 = o0;
     for (int f = threadIdx.x; f < n; f += blockDim.x) {
       const int g = (int)fdiv((unsigned)f, a.dLns), r = f - g * (L * ns), e = (int)fdiv((unsigned)r, a.dns),
                 s = r - e * ns;
@@ -340,14 +323,14 @@ __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
     cur = oth;
     oth = t;
   };
-  if (a.flags & F_PT1) point_op(U1);
+  if (a.flags & F_PT1) point_op(a.U1);
   if (a.flags & F_SNAP) {
     for (int f = threadIdx.x; f < tot; f += blockDim.x) {
       const int g = (int)fdiv((unsigned)f, a.dLC), r = f - g * (L * C), e = (int)fdiv((unsigned)r, a.dC), c = r - e * C;
       if (g < gv && c < cv) a.snap[((size_t)(o0 + g) * L + e) * I + i0 + c] = cur[(g * C + c) * M + e];
     }
   }
-  if (a.flags & F_PT2) point_op(U2);
+  if (a.flags & F_PT2) point_op(a.U2);
   SPO_MARK(2)
   if (a.flags & F_FWD) lds_fft<false>(p, tw, cur, oth, nl);
   if (a.flags & F_KY) {
@@ -365,8 +348,7 @@ __global__ __launch_bounds__(256) void spo_axis_kernel(Fft p, AxisArgs a) {
         const int g = (int)fdiv((unsigned)f, a.dLC);
         if (g < gv) cur[(g * C + c) * M + e] = cmul(cur[(g * C + c) * M + e], a.K[(size_t)(o0 + g) * L + e]);
       } else if (c < cv) {
-        cur[c * M + e] = cmul(cur[c * M + e], a.aux == 2 ? aux[e * C + c]
-                                                          : a.K[(size_t)e * pts + (int)fdiv((unsigned)(i0 + c), a.dns)]);
+        cur[c * M + e] = cmul(cur[c * M + e], a.K[(size_t)e * pts + (int)fdiv((unsigned)(i0 + c), a.dns)]);
       }
     }
     __syncthreads();
@@ -455,14 +437,6 @@ __global__ void kmul_kernel(c128* psi, const c128* __restrict__ K, long n, int n
 }
 
 // dst[z][y][x] = s src[x][y][z] (src [n0][n1][n2]): the kinetic table of the 3D rotated passes
-__global__ void scale_permute3_kernel(const c128* __restrict__ src, c128* __restrict__ dst, int n0, int n1, int n2,
-                                      double s) {
-  const long n = (long)n0 * n1 * n2;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
-    const int z = (int)(e % n2), y = (int)((e / n2) % n1), x = (int)(e / ((long)n1 * n2));
-    dst[((size_t)z * n1 + y) * n0 + x] = cscale(src[e], s);
-  }
-}
 // dst[j][i] = s src[i][j] (src [r][c]): the kinetic table of the xpose passes
 __global__ void scale_transpose_kernel(const c128* __restrict__ src, c128* __restrict__ dst, int r, int c, double s) {
   const long n = (long)r * c;
@@ -754,12 +728,8 @@ void factor_stages(int M, Fft& f) {
     n /= r;
   };
   // radix 8 first (one LDS stage and barrier instead of a radix-4 and a radix-2 one: 200 = 8 5 5 in three stages
-  // instead of four); QD_SPO_RADIX8=0 keeps radix 4 / 2 (A/B)
-  static const bool r8 = [] {
-    const char* e = getenv("QD_SPO_RADIX8");
-    return !(e && e[0] == '0');
-  }();
-  if (r8) {
+  // instead of four)
+  {
     // 8s as long as no single 2 would be left over unpaired with a 4 (16 = 8 2 would take as many stages as 4 4)
     int twos = 0;
     for (int m = n; m % 2 == 0; m /= 2) ++twos;
@@ -781,15 +751,7 @@ void factor_stages(int M, Fft& f) {
 
 // Kind and table sizes of an axis of length L (count of c128 table slots in *tab).
 void plan_kind(int L, int* kind, int* M, size_t* tab) {
-  const char* e = getenv("QD_SPO_FORCE_KIND");   // tests: 1 = Bluestein, 2 = direct wherever legal
-  const int force = e ? atoi(e) : 0;
-  if (force == 2) {
-    *kind = DIRECT;
-    *M = L;
-    *tab = L;
-    return;
-  }
-  if (force != 1 && L <= MAX_LDS_M && all_factors_small(L, GEN_MAXP)) {
+  if (L <= MAX_LDS_M && all_factors_small(L, GEN_MAXP)) {
     *kind = MIXED;
     *M = L;
     *tab = L;
@@ -858,7 +820,7 @@ struct Exec {
   c128* psi = nullptr;
   c128* tmp = nullptr;     // grid-sized scratch (unfused passes)
   const c128* Ks = nullptr;   // exp_K / N
-  const c128* KsT = nullptr;  // exp_K / N in the kinetic pass's input layout (xpose): [n1][n0] / [n2][n1][n0]
+  const c128* KsT = nullptr;  // exp_K / N in the kinetic pass's input layout (xpose): [n1][n0]
   const c128* Ky = nullptr;   // Jacobi k_y phase [n0][n1] (D == 2)
   bool xpose = false;         // 2D: alternating layouts (file header); psi [n0][n1][ns] <-> tmp [n1][n0][ns]
   int kin_g = 1;              // xpose: rows per tile of the kinetic pass
@@ -902,24 +864,8 @@ struct Exec {
     size_t lds = (size_t)2 * G * C * p.M * sizeof(c128);
     a.twl = lds + (size_t)p.M * sizeof(c128) <= LDS_MAX;
     if (a.twl) lds += (size_t)p.M * sizeof(c128);
-    // QD_SPO_AUX=1: stage the pass's operators with the tile (one load round trip per pass).  Off by default: same-box
-    // A/B (profiles/r04/spo/spo_any_aux_*.txt) 200^2 x 2 25.3 vs 24.8 us per step, 500^2 x 2 50.3 vs 43.8 (the larger
-    // tile lowers the workgroups per CU), so the operator loads are not what bounds these passes.
-    a.u2same = U1 == U2;
-    a.aux = 0;
-    const char* xe = getenv("QD_SPO_AUX");   // 1: both kinds of pass, 2: kinetic passes only
-    if (xe && !(flags & F_KROW) && (xe[0] == '1' || (xe[0] == '2' && (flags & F_KMUL)))) {
-      const size_t ub = (size_t)G * L * ns * ns * sizeof(c128) * ((flags & F_PT2) && !a.u2same ? 2 : 1);
-      const size_t kb = (size_t)L * C * sizeof(c128);
-      if ((flags & (F_PT1 | F_PT2)) && lds + ub <= LDS_MAX) {
-        a.aux = 1;
-        lds += ub;
-      } else if ((flags & F_KMUL) && lds + kb <= LDS_MAX) {
-        a.aux = 2;
-        lds += kb;
-      }
-    }
-    if ((flags & F_PT2) && !(flags & F_PT1) && a.aux == 1) a.aux = 0;   // (the staging loop keys on U1)
+    // (round 4 tried staging the pass's operators in LDS with the tile: 500^2 x 2 50.3 vs 43.8 us per step, the larger
+    // tile lowering the workgroups per CU; profiles/r04/spo/spo_any_aux_*.txt)
     (void)hipFuncSetAttribute((const void*)spo_axis_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
     hipLaunchKernelGGL(spo_axis_kernel, dim3((a.O + G - 1) / G, (a.I + C - 1) / C), dim3(256), lds, st, p, a);
     QD_HIP(hipGetLastError());
@@ -945,32 +891,6 @@ struct Exec {
     return launch_tile(f[0], n[1], ns, F_KMUL | F_KROW | F_XOUT, ns, kin_g, nullptr, nullptr, nullptr, tmp, psi, KsT,
                        Store{n[1], 0, ns, (long)n[1] * ns});
   }
-  // D == 3 rotation (n0, n1, n2 = x, y, z; canonical C = [x][y][z] in psi):
-  //   z pass   reads C (psi), FWD: stores [x][z][y] into tmp (else in place)
-  //   y FWD    reads [x][z][y] (tmp), stores [z][y][x] into psi
-  //   x KMUL   reads [z][y][x] (psi, exp_K / N permuted to match), stores [x][z][y] into tmp
-  //   y INV    reads [x][z][y] (tmp), stores C into psi
-  int z3_pass(int flags, const c128* U1, const c128* U2, c128* snap) {
-    const bool xo = flags & F_FWD;
-    const long O = (long)n[0] * n[1];
-    const int G = stack_rows(O, n[2], ns, f[2].M);
-    return launch_tile(f[2], O, ns, flags | (xo ? F_XOUT : 0), ns, G, U1, U2, snap, psi, xo ? tmp : psi, Ks,
-                       Store{n[1], (long)n[2] * n[1] * ns, ns, (long)n[1] * ns});
-  }
-  int y3_pass(bool inv) {
-    const long O = (long)n[0] * n[2];
-    const int G = stack_rows(O, n[1], ns, f[1].M);
-    if (!inv)
-      return launch_tile(f[1], O, ns, F_FWD | F_XOUT, ns, G, nullptr, nullptr, nullptr, tmp, psi, Ks,
-                         Store{n[2], ns, (long)n[1] * n[0] * ns, (long)n[0] * ns});
-    return launch_tile(f[1], O, ns, F_INV | F_XOUT, ns, G, nullptr, nullptr, nullptr, tmp, psi, Ks,
-                       Store{n[2], (long)n[1] * n[2] * ns, ns, (long)n[2] * ns});
-  }
-  int x3_pass() {
-    const long O = (long)n[2] * n[1];
-    return launch_tile(f[0], O, ns, F_KMUL | F_KROW | F_XOUT, ns, kin_g, nullptr, nullptr, nullptr, psi, tmp, KsT,
-                       Store{n[1], (long)n[1] * ns, ns, (long)n[2] * n[1] * ns});
-  }
 
   // lines-per-tile choice for an LDS pass over axis d; C == I (whole rows) required for point ops
   bool tile(int d, bool rows, int* C, int* G) const {
@@ -981,9 +901,7 @@ struct Exec {
       c = (int)I;
     } else {   // 8 consecutive columns (128-B rows) when that still leaves >= 256 tiles, else fewer
       c = (int)std::min<long>(I, 8);
-      int minc = 1;   // QD_SPO_GEN_MINC: never fewer columns per tile than this (A/B of coalescing vs tile count)
-      if (const char* e = getenv("QD_SPO_GEN_MINC")) minc = std::max(1, std::min(8, atoi(e)));
-      while (c > minc && ((size_t)c * line > LDS_SOFT || ((I + c - 1) / c) * O < 256)) c >>= 1;
+      while (c > 1 && ((size_t)c * line > LDS_SOFT || ((I + c - 1) / c) * O < 256)) c >>= 1;
     }
     if ((size_t)c * line > LDS_MAX) return false;
     int g = 1;
@@ -1055,27 +973,6 @@ int run_nd(Exec& x, const c128* Uh, const c128* Ufull, int nsteps, int nout, c12
   const int kyf = ky ? F_KY : 0;
   const size_t grid_elems = (size_t)x.npts * x.ns;
   int rc;
-  if (x.xpose && D == 3) {   // the same pass sequence over the rotated layouts (Exec::z3_pass)
-    if ((rc = x.z3_pass(F_PT1 | F_FWD, Uh, nullptr, nullptr))) return rc;
-    if ((rc = x.y3_pass(false))) return rc;
-    for (int s = 1; s <= nsteps; ++s) {
-      if ((rc = x.x3_pass())) return rc;
-      if ((rc = x.y3_pass(true))) return rc;
-      const bool take = snap && (s % nout == 0);
-      c128* sp = take ? snap + (size_t)(s / nout - 1) * grid_elems : nullptr;
-      int flags = F_INV | F_PT1 | (take ? F_SNAP : 0);
-      if (Ufull) flags |= F_FWD;
-      else if (s < nsteps) flags |= F_PT2 | F_FWD;
-      if ((rc = x.z3_pass(flags, Ufull ? Ufull : Uh, Uh, sp))) return rc;
-      if ((flags & F_FWD) && (rc = x.y3_pass(false))) return rc;
-    }
-    if (Ufull) {
-      if ((rc = x.x3_pass())) return rc;
-      if ((rc = x.y3_pass(true))) return rc;
-      if ((rc = x.z3_pass(F_INV | F_PT1, Uh, nullptr, nullptr))) return rc;
-    }
-    return QD_OK;
-  }
   if (x.xpose) {   // D == 2, nsteps >= 1: the same pass sequence with the row pass storing into the other layout
     if ((rc = x.row_pass(F_PT1 | F_FWD | kyf, Uh, nullptr, nullptr, true))) return rc;
     for (int s = 1; s <= nsteps; ++s) {
@@ -1132,9 +1029,8 @@ int fft_lines(c128* x, long O, int L, long I, bool inv, hipStream_t st, int* l2)
   int kind, M;
   size_t nslots;
   plan_kind(L, &kind, &M, &nslots);
-  const char* fk = getenv("QD_SPO_FORCE_KIND");
   int L1 = 0;
-  if (kind == DIRECT && !(fk && fk[0] == '2')) {
+  if (kind == DIRECT) {
     for (int a = 2; (long)a * a <= L; ++a) {
       if (L % a) continue;
       int k1, k2, m1, m2;
@@ -1217,27 +1113,22 @@ int spo_generic_run(c128* psi, const c128* expVh, const c128* expV, const c128* 
   QD_HIP(hipGetLastError());
   x.Ks = ks;
   x.Ky = expKy;
-  // alternating layouts (2D, every axis an LDS plan whose whole-row tile fits; QD_SPO_XPOSE=0: in-place passes)
+  // alternating layouts (2D, every axis an LDS plan whose whole-row tile fits).  (Round 4 measured the same rotation
+  // for 3D grids: 60^3 x 2 55.4 -> 54.4 us per step, but 96^3 126.5 -> 143.4 and 100^3 140.7 -> 161.7, the scattered
+  // 32-B stores at large strides costing more than the strided loads removed; profiles/r04/spo/spo_xpose_ab.txt.)
   {
-    const char* xev = getenv("QD_SPO_XPOSE");   // read per run (tests switch it)
-    const bool xe = !(xev && xev[0] == '0');
-    // 3D rotation: opt-in (QD_SPO_XPOSE3=1).  Same-box A/B (profiles/r04/spo/spo_xpose_ab.txt): 60^3 x 2 55.4 -> 54.4 us
-    // per step, but 96^3 126.5 -> 143.4 and 100^3 140.7 -> 161.7: three of the four 3D passes then store scattered
-    // 32-B pieces at large strides, which costs more than the strided loads they remove
-    const char* x3v = getenv("QD_SPO_XPOSE3");
-    const bool x3 = x3v && x3v[0] == '1';
-    bool fit = nsteps >= 1 && (D == 2 || (D == 3 && x3));
+    bool fit = nsteps >= 1 && D == 2;
     for (int d = 0; d < D && fit; ++d)   // every axis a whole-row LDS pass (C == ns)
       fit = x.f[d].kind != DIRECT && (size_t)2 * ns * x.f[d].M * sizeof(c128) <= LDS_MAX;
-    x.xpose = xe && fit;
+    x.xpose = fit;
+    for (int d = 0; d < D; ++d)
+      note_path(x.f[d].kind == DIRECT ? "spo_axis_direct" : x.f[d].kind == BLUESTEIN ? "spo_axis_bluestein"
+                                                                                      : "spo_axis_mixed");
+    note_path(x.xpose ? "spo_layout_alternating" : "spo_layout_in_place");
     if (x.xpose) {
       c128* kt = tab;   // behind the plan tables
-      if (D == 2)
-        hipLaunchKernelGGL(scale_transpose_kernel, dim3(grid_for(x.npts)), dim3(256), 0, st, expK, kt, dims[0], dims[1],
-                           1.0 / (double)x.npts);
-      else
-        hipLaunchKernelGGL(scale_permute3_kernel, dim3(grid_for(x.npts)), dim3(256), 0, st, expK, kt, dims[0], dims[1],
-                           dims[2], 1.0 / (double)x.npts);
+      hipLaunchKernelGGL(scale_transpose_kernel, dim3(grid_for(x.npts)), dim3(256), 0, st, expK, kt, dims[0], dims[1],
+                         1.0 / (double)x.npts);
       QD_HIP(hipGetLastError());
       x.KsT = kt;
       x.kin_g = x.stack_rows(x.npts / dims[0], dims[0], ns, x.f[0].M);
@@ -1298,6 +1189,7 @@ int spo1d_generic_run(c128* psi, const c128* expV, const c128* expVh, const c128
   c128* ks = tmp + 2 * n;
   Fft f;
   if ((rc = plan_axis(nx, tab, f, st))) return rc;
+  note_path(f.kind == DIRECT ? "spo1d_long" : f.kind == BLUESTEIN ? "spo1d_bluestein" : "spo1d_mixed");
   if (f.kind != DIRECT) {
     const int twl = (size_t)3 * f.M * sizeof(c128) <= LDS_MAX;
     const size_t lds = (size_t)(2 + twl) * f.M * sizeof(c128);
@@ -1310,9 +1202,8 @@ int spo1d_generic_run(c128* psi, const c128* expV, const c128* expVh, const c128
   // the line viewed as [L1][L2] (n = L2 n1 + n2), FFT_L1 over n1 (stride L2), twiddle w_L^(n2 k1), FFT_L2 over n2
   // (contiguous) leaves X[k1 + L1 k2] at L2 k1 + k2; the kinetic factor is applied in that order (exp_K permuted once)
   // and the inverse runs the same passes backwards, so no transpose is ever made.  Other lengths: direct DFT.
-  const char* fk = getenv("QD_SPO_FORCE_KIND");
   int L1 = 0;
-  if (!(fk && fk[0] == '2')) {
+  {
     int best = 0;
     for (int a = 2; (long)a * a <= nx; ++a) {
       if (nx % a) continue;
@@ -1321,6 +1212,7 @@ int spo1d_generic_run(c128* psi, const c128* expV, const c128* expVh, const c128
         best = a;   // the largest divisor <= sqrt(L): the most balanced split
     }
     L1 = best;
+    note_path(L1 ? "spo1d_fourstep" : "spo1d_direct");
   }
   const long total = n;
   auto vmul = [&](const c128* V) -> int {   // psi[b][k] *= V[k]

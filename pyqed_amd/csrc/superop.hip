@@ -246,9 +246,9 @@ extern "C" int qd_superop_rk4(const qd_c128* L_, qd_c128* v_, int B, int N2, dou
   };
   int rc;
   if (ne && (rc = record(0))) return rc;
-  int gemm_min = 48;
-  if (const char* e = std::getenv("QD_SUPEROP_GEMM_MIN")) gemm_min = std::max(1, std::atoi(e));
-  if (B >= gemm_min && N2 >= 64) {
+  // from 48 vectors the stages are MFMA GEMMs (one pass over L for the batch), below that GEMVs
+  note_path(B >= 48 && N2 >= 64 ? "superop_gemm" : "superop_gemv");
+  if (B >= 48 && N2 >= 64) {
     const int N2p = ceil_div(N2, 128) * 128;
     const int Bp = B <= 64 ? 64 : ceil_div(B, 128) * 128;
     constexpr int MAXS = 8;

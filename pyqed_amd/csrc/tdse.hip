@@ -6,9 +6,9 @@
 // <psi|E_m|psi> (phys.obs, phys.py:1266-1283) at t0 and after every
 // `save_every` steps.
 //
-// One workgroup per wavefunction, persistent over all steps: psi, the stage
-// state and the RK4 accumulator live in LDS; (-iH)^T is streamed from L2/HBM
-// each stage with lanes over rows (coalesced), so a stage is one GEMV.
+// Every stage is one launch: a wave per row of H (the row path), or, for batches at larger N, a split-K MFMA GEMM of
+// the whole batch (the GEMM path).  Round 1's persistent one-workgroup-per-wavefunction kernel lost to the row path at
+// every measured size (tools/tdse_bench.py) and was removed in round 5.
 #include "qd_common.hpp"
 
 #include <cstdlib>
@@ -16,19 +16,6 @@
 
 namespace qd {
 namespace {
-
-constexpr int TD_TPB = 256;
-constexpr int TD_MAXN = 2048;
-
-// mHT[j][r] = -i H[r][j] ; ET[m][j][r] = E_m[r][j]
-__global__ void tdse_prep_kernel(const c128* H, const c128* E, int ne, int N, c128* mHT, c128* ET) {
-  const size_t NN = (size_t)N * N;
-  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < NN; e += (size_t)gridDim.x * blockDim.x) {
-    const int r = (int)(e / N), j = (int)(e % N);
-    mHT[(size_t)j * N + r] = cmulmi(H[e]);
-    for (int m = 0; m < ne; ++m) ET[m * NN + (size_t)j * N + r] = E[m * NN + e];
-  }
-}
 
 // Ht = H0 - sum_d f_d Hd_d, row-major (driven step block of the row-parallel path; f on the device)
 __global__ void tdse_driven_h_kernel(const c128* H0, const c128* Hd, int nd, const c128* f, int N, c128* Ht) {
@@ -40,111 +27,9 @@ __global__ void tdse_driven_h_kernel(const c128* H0, const c128* Hd, int nd, con
   }
 }
 
-// mHT[j][r] = -i (H0 - sum_d f_d Hd_d)[r][j]   (driven step block; f on the device)
-__global__ void tdse_driven_prep_kernel(const c128* H0, const c128* Hd, int nd, const c128* f, int N, c128* mHT) {
-  const size_t NN = (size_t)N * N;
-  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < NN; e += (size_t)gridDim.x * blockDim.x) {
-    const int r = (int)(e / N), j = (int)(e % N);
-    c128 h = H0[e];
-    for (int d = 0; d < nd; ++d) h = csub(h, cmul(f[d], Hd[d * NN + e]));
-    mHT[(size_t)j * N + r] = cmulmi(h);
-  }
-}
-
-__global__ void tdse_et_kernel(const c128* E, int ne, int N, c128* ET) {
-  const size_t NN = (size_t)N * N;
-  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < NN; e += (size_t)gridDim.x * blockDim.x) {
-    const int r = (int)(e / N), j = (int)(e % N);
-    for (int m = 0; m < ne; ++m) ET[m * NN + (size_t)j * N + r] = E[m * NN + e];
-  }
-}
-
-__device__ void td_expect(const c128* psi, const c128* ET, int ne, int N, c128* out, c128* red) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int m = 0; m < ne; ++m) {
-    const c128* Em = ET + (size_t)m * N * N;
-    double sr = 0, si = 0;
-    for (int r = tid; r < N; r += TD_TPB) {
-      c128 y = cmk(0, 0);
-      for (int j = 0; j < N; ++j) y = cadd(y, cmul(Em[(size_t)j * N + r], psi[j]));
-      const c128 v = cmul(cconj(psi[r]), y);
-      sr += v.re;
-      si += v.im;
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-      sr += __shfl_xor(sr, off, 64);
-      si += __shfl_xor(si, off, 64);
-    }
-    if (lane == 0) red[wave] = cmk(sr, si);
-    __syncthreads();
-    if (tid == 0) {
-      c128 s = red[0];
-      for (int w = 1; w < TD_TPB / 64; ++w) s = cadd(s, red[w]);
-      out[m] = s;
-    }
-    __syncthreads();
-  }
-}
-
-// save0: index of this launch's first save in snap/obs (driven runs launch once per block of
-// save_every steps); obs row 0 (t0) is written only when save0 == 0.
-__global__ __launch_bounds__(TD_TPB) void tdse_rk4_kernel(const c128* mHT, c128* psi_g, int N, double dt, int nsteps,
-                                                          int save_every, int nsave, int save0, c128* snap,
-                                                          const c128* ET, int ne, c128* obs) {
-  extern __shared__ c128 sm[];
-  c128* psi = sm;          // N
-  c128* xs = psi + N;      // N  stage input
-  c128* acc = xs + N;      // N
-  __shared__ c128 red[TD_TPB / 64];
-  const int b = blockIdx.x;
-  c128* pg = psi_g + (size_t)b * N;
-  for (int r = threadIdx.x; r < N; r += TD_TPB) {
-    psi[r] = pg[r];
-    xs[r] = psi[r];
-  }
-  __syncthreads();
-  c128* ob = obs ? obs + (size_t)b * (nsave + 1) * ne : nullptr;
-  if (ob && save0 == 0) td_expect(psi, ET, ne, N, ob, red);
-  for (int s = 0; s < nsteps; ++s) {
-    for (int stage = 0; stage < 4; ++stage) {
-      // k = (-iH) xs ; each thread owns rows r
-      constexpr int QMAX = TD_MAXN / TD_TPB;  // rows per thread; fully unrolled -> registers, not scratch
-      c128 kreg[QMAX];
-#pragma unroll
-      for (int q = 0; q < QMAX; ++q) {
-        const int r = threadIdx.x + q * TD_TPB;
-        c128 k = cmk(0, 0);
-        if (r < N)
-          for (int j = 0; j < N; ++j) k = cadd(k, cmul(mHT[(size_t)j * N + r], xs[j]));
-        kreg[q] = k;
-      }
-      __syncthreads();  // all reads of xs done
-#pragma unroll
-      for (int q = 0; q < QMAX; ++q) {
-        const int r = threadIdx.x + q * TD_TPB;
-        if (r >= N) break;
-        // Horner-form RK4 (rk4_horner_coef): H is constant over the step
-        const c128 v = cadd(psi[r], cscale(kreg[q], rk4_horner_coef(dt, stage)));
-        if (stage == 3) psi[r] = v;
-        xs[r] = v;
-      }
-      __syncthreads();
-    }
-    if (save_every > 0 && (s + 1) % save_every == 0) {
-      const int idx = save0 + (s + 1) / save_every;  // 1..nsave
-      if (snap)
-        for (int r = threadIdx.x; r < N; r += TD_TPB) snap[((size_t)b * nsave + idx - 1) * N + r] = psi[r];
-      if (ob) td_expect(psi, ET, ne, N, ob + (size_t)idx * ne, red);
-    }
-  }
-  for (int r = threadIdx.x; r < N; r += TD_TPB) pg[r] = psi[r];
-}
-
-// ---- row-parallel path (small batches, any N): the persistent kernel runs one wavefunction on one CU,
-// which leaves the chip idle and re-streams H through that CU every stage (N = 2048: ~1 ms per stage).
-// Here every stage is one launch: a wave per row r computes k_r = -i sum_j H[r][j] x_j (lanes over j,
-// coalesced 1 KB row pieces, fixed-order wave reduction) and lane 0 runs the RK4 update of element r
-// (same arithmetic order as the persistent kernel).  Buffers per wavefunction: psi (in place), two stage
+// ---- row path (any N): every stage is one launch: a wave per row r computes k_r = -i sum_j H[r][j] x_j (lanes over
+// j, coalesced 1 KB row pieces, fixed-order wave reduction) and lane 0 runs the RK4 update of element r.  (A
+// persistent workgroup per wavefunction leaves the chip idle and re-streams H through one CU every stage.)  Buffers per wavefunction: psi (in place), two stage
 // inputs and the accumulator.  Observables: a wave per (row, E_m) forms conj(psi_r) (E_m psi)_r, then one
 // block per (b, m) sums the rows in fixed order.
 __device__ __forceinline__ c128 wave_row_dot(const c128* row, const c128* x, int N) {
@@ -331,10 +216,12 @@ int tdse_rows_run(const c128* H, c128* psi, int B, int N, double dt, int nsteps,
   };
   // batches: MFMA GEMM stages where they win (tools/tdse_bench.py, wavefunction-steps/s, rows -> GEMM:
   // N = 1024, B = 64: 230k -> 523k; N = 2048, B = 256: 31k -> 427k; N = 256, B = 64: 1.77M -> 1.08M, B = 256:
-  // 2.42M -> 4.06M); QD_TDSE_GEMM=0 keeps the row kernel
-  const char* ge = std::getenv("QD_TDSE_GEMM");
-  if (((B >= 64 && N >= 512) || (B >= 128 && N >= 256)) && !(ge && ge[0] == '0'))
+  // 2.42M -> 4.06M)
+  if ((B >= 64 && N >= 512) || (B >= 128 && N >= 256)) {
+    note_path("tdse_gemm");
     return tdse_gemm_steps(H, psi, B, N, dt, nsteps, st, save_every, save);
+  }
+  note_path("tdse_rows");
   for (int s = 0; s < nsteps; ++s) {
     for (int stage = 0; stage < 4; ++stage) {
       hipLaunchKernelGGL(tdse_row_stage_kernel<1>, rows, dim3(256), 0, st, H, psi, ws, N, B, dt, stage);
@@ -405,30 +292,8 @@ extern "C" int qd_tdse_rk4(const qd_c128* H, qd_c128* psi, int B, int N, double 
   QD_CHECK_ARG(ne >= 0 && (ne == 0 || (E && obs)), "qd_tdse_rk4: E/obs null but ne=%d", ne);
   QD_CHECK_ARG(!obs || save_every > 0 || nsteps == 0, "qd_tdse_rk4: observables need save_every > 0");
   hipStream_t st = (hipStream_t)stream;
-  // row-parallel path (a wave per row per stage) unless QD_TDSE_ROWS=0 asks for the persistent kernel
-  // (one workgroup per wavefunction, N <= 2048; kept for A/B runs):
-  // measured (tools/tdse_bench.py, wavefunction-steps/s, persistent -> rows): N = 64, B = 1: 33k -> 97k;
-  // B = 256: 8.5M -> 9.3M; N = 1024, B = 1: 239 -> 33.6k; B = 64: 16k -> 230k; N = 2048, B = 1: 55 -> 17.6k;
-  // N = 4096 (rows only): 6.1k.  The rows path wins at every measured size, so it is the default.
-  bool rows = true;
-  if (const char* e = std::getenv("QD_TDSE_ROWS")) rows = N > TD_MAXN || std::atoi(e) != 0;
-  if (rows)
-    return tdse_rows_run((const c128*)H, (c128*)psi, B, N, dt, nsteps, save_every, (c128*)snap, (const c128*)E, ne,
-                         ne ? (c128*)obs : nullptr, st);
-  const size_t NN = (size_t)N * N;
-  void* w = nullptr;
-  int rc = workspace(WS_MISC, (1 + ne) * NN * sizeof(c128), &w, st);
-  if (rc) return rc;
-  c128* mHT = (c128*)w;
-  c128* ET = mHT + NN;
-  hipLaunchKernelGGL(tdse_prep_kernel, dim3((int)std::min<size_t>((NN + 255) / 256, 4096)), dim3(256), 0, st,
-                     (const c128*)H, (const c128*)E, ne, N, mHT, ET);
-  QD_HIP(hipGetLastError());
-  const int nsave = save_every > 0 ? nsteps / save_every : 0;
-  hipLaunchKernelGGL(tdse_rk4_kernel, dim3(B), dim3(TD_TPB), 3 * N * sizeof(c128), st, mHT, (c128*)psi, N, dt, nsteps,
-                     save_every, nsave, 0, (c128*)snap, ET, ne, ne ? (c128*)obs : nullptr);
-  QD_HIP(hipGetLastError());
-  return QD_OK;
+  return tdse_rows_run((const c128*)H, (c128*)psi, B, N, dt, nsteps, save_every, (c128*)snap, (const c128*)E, ne,
+                       ne ? (c128*)obs : nullptr, st);
 }
 
 extern "C" int qd_tdse_driven_rk4(const qd_c128* H0, const qd_c128* Hd, int nd, const qd_c128* fvals, qd_c128* psi,
@@ -440,63 +305,26 @@ extern "C" int qd_tdse_driven_rk4(const qd_c128* H0, const qd_c128* Hd, int nd, 
                "qd_tdse_driven_rk4: bad sizes N=%d B=%d nblocks=%d nout=%d nd=%d", N, B, nblocks, nout, nd);
   QD_CHECK_ARG(ne >= 0 && (ne == 0 || (E && obs)), "qd_tdse_driven_rk4: E/obs null but ne=%d", ne);
   hipStream_t st = (hipStream_t)stream;
-  bool rows = true;  // row-parallel path as qd_tdse_rk4 (QD_TDSE_ROWS=0: persistent kernel, N <= 2048)
-  if (const char* e = std::getenv("QD_TDSE_ROWS")) rows = N > TD_MAXN || std::atoi(e) != 0;
-  if (rows) {
-    const size_t NN = (size_t)N * N, fl = (size_t)nblocks * nd;
-    void* w = nullptr;
-    int rc = workspace(WS_TDSE_H, (NN + fl) * sizeof(c128), &w, st);  // H(t) + drive values (WS_MISC: the row path)
-    if (rc) return rc;
-    c128* Ht = (c128*)w;
-    c128* fdev = Ht + NN;
-    if (fl) QD_HIP(hipMemcpyAsync(fdev, fvals, fl * sizeof(c128), hipMemcpyHostToDevice, st));
-    const int blocks = (int)std::min<size_t>((NN + 255) / 256, 4096);
-    if (nblocks == 0) {  // observables at t0 only
-      return tdse_rows_run((const c128*)H0, (c128*)psi, B, N, dt, 0, nout, nullptr, (const c128*)E, ne,
-                           ne ? (c128*)obs : nullptr, st, 0, 0);
-    }
-    // H constant within a block of nout steps (mol.py:1944-1951 evaluates calcH(t) once per block)
-    for (int k = 0; k < nblocks; ++k) {
-      hipLaunchKernelGGL(tdse_driven_h_kernel, dim3(blocks), dim3(256), 0, st, (const c128*)H0, (const c128*)Hd, nd,
-                         (const c128*)fdev + (size_t)k * nd, N, Ht);
-      QD_HIP(hipGetLastError());
-      if ((rc = tdse_rows_run(Ht, (c128*)psi, B, N, dt, nout, nout, (c128*)snap, (const c128*)E, ne,
-                              ne ? (c128*)obs : nullptr, st, k, nblocks)))
-        return rc;
-    }
-    return QD_OK;
-  }
-  QD_CHECK_ARG(N <= TD_MAXN, "qd_tdse_driven_rk4: N=%d > %d on the persistent kernel", N, TD_MAXN);
-  const size_t NN = (size_t)N * N;
-  const size_t fl = (size_t)nblocks * nd;
+  const size_t NN = (size_t)N * N, fl = (size_t)nblocks * nd;
   void* w = nullptr;
-  int rc = workspace(WS_MISC, ((1 + ne) * NN + fl) * sizeof(c128), &w, st);
+  int rc = workspace(WS_TDSE_H, (NN + fl) * sizeof(c128), &w, st);  // H(t) + drive values (WS_MISC: the row path)
   if (rc) return rc;
-  c128* mHT = (c128*)w;
-  c128* ET = mHT + NN;
-  c128* fdev = ET + ne * NN;
-  const int blocks = (int)std::min<size_t>((NN + 255) / 256, 4096);
-  if (ne) {
-    hipLaunchKernelGGL(tdse_et_kernel, dim3(blocks), dim3(256), 0, st, (const c128*)E, ne, N, ET);
-    QD_HIP(hipGetLastError());
-  }
+  c128* Ht = (c128*)w;
+  c128* fdev = Ht + NN;
   if (fl) QD_HIP(hipMemcpyAsync(fdev, fvals, fl * sizeof(c128), hipMemcpyHostToDevice, st));
-  if (nblocks == 0 && ne) {  // observables at t0 only
-    hipLaunchKernelGGL(tdse_driven_prep_kernel, dim3(blocks), dim3(256), 0, st, (const c128*)H0, (const c128*)Hd, 0,
-                       (const c128*)fdev, N, mHT);
-    hipLaunchKernelGGL(tdse_rk4_kernel, dim3(B), dim3(TD_TPB), 3 * N * sizeof(c128), st, mHT, (c128*)psi, N, dt, 0,
-                       nout, 0, 0, (c128*)nullptr, ET, ne, (c128*)obs);
-    QD_HIP(hipGetLastError());
+  const int blocks = (int)std::min<size_t>((NN + 255) / 256, 4096);
+  if (nblocks == 0) {  // observables at t0 only
+    return tdse_rows_run((const c128*)H0, (c128*)psi, B, N, dt, 0, nout, nullptr, (const c128*)E, ne,
+                         ne ? (c128*)obs : nullptr, st, 0, 0);
   }
-  // one launch per block of nout steps: H is constant within a block (mol.py:1944-1951 evaluates
-  // calcH(t) with t advanced only after the block)
+  // H constant within a block of nout steps (mol.py:1944-1951 evaluates calcH(t) once per block)
   for (int k = 0; k < nblocks; ++k) {
-    hipLaunchKernelGGL(tdse_driven_prep_kernel, dim3(blocks), dim3(256), 0, st, (const c128*)H0, (const c128*)Hd, nd,
-                       (const c128*)fdev + (size_t)k * nd, N, mHT);
+    hipLaunchKernelGGL(tdse_driven_h_kernel, dim3(blocks), dim3(256), 0, st, (const c128*)H0, (const c128*)Hd, nd,
+                       (const c128*)fdev + (size_t)k * nd, N, Ht);
     QD_HIP(hipGetLastError());
-    hipLaunchKernelGGL(tdse_rk4_kernel, dim3(B), dim3(TD_TPB), 3 * N * sizeof(c128), st, mHT, (c128*)psi, N, dt, nout,
-                       nout, nblocks, k, (c128*)snap, ET, ne, ne ? (c128*)obs : nullptr);
-    QD_HIP(hipGetLastError());
+    if ((rc = tdse_rows_run(Ht, (c128*)psi, B, N, dt, nout, nout, (c128*)snap, (const c128*)E, ne,
+                            ne ? (c128*)obs : nullptr, st, k, nblocks)))
+      return rc;
   }
   return QD_OK;
 }

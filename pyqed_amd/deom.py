@@ -352,6 +352,12 @@ class DEOMSolver:
         self.V = None
         self.V_inv = None
         self.propgator = None
+        # extensions (not in the reference): run_batch's ADO layout ("ado_major" / "element_major"; None = by batch
+        # size), the one-hierarchy banded launch (False = the stage launches; None = where it applies) and its band
+        # count (None = by hierarchy size, band_tables)
+        self.layout = None
+        self.banded = None
+        self.bands = None
 
     def set_hierarchy(self, lmax):
         self.lmax = lmax
@@ -427,9 +433,11 @@ class DEOMSolver:
         b = self.bath
         c128 = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=complex))).to(dev)
         # batches of >= 16 hierarchies run ADO-major ([nmax][B]: coalesced neighbour reads across
-        # hierarchies, wave-uniform index / prefactor loads); QD_DEOM_ADO_MAJOR=0/1 forces the layout
-        am_env = os.environ.get("QD_DEOM_ADO_MAJOR")
-        ado_major = (B >= 16 if am_env is None else am_env != "0") and ns * ns <= 64 and K <= 8
+        # hierarchies, wave-uniform index / prefactor loads); self.layout picks the layout explicitly
+        if self.layout not in (None, "ado_major", "element_major"):
+            raise ValueError(f"DEOMSolver.layout must be None, 'ado_major' or 'element_major', got {self.layout!r}")
+        want_am = B >= 16 if self.layout is None else self.layout == "ado_major"
+        ado_major = want_am and ns * ns <= 64 and K <= 8
         if ado_major:
             ados = torch.zeros((nmax, B, ns, ns), dtype=torch.complex128, device=dev)
             ados[0] = c128(rho0)
@@ -513,13 +521,13 @@ class DEOMSolver:
     def band_tables(self, dev, nbands=None):
         """Band tables of qd_deom_rk4_banded (one hierarchy as one persistent launch over tier bands), or None
         when the hierarchy does not qualify (ns outside [2, 4], K > 8, rows beyond one workgroup's lanes / LDS)
-        or QD_DEOM_BANDED=0.  Default band count: ~24 ADOs per band (ns = 2; 8 for ns = 3, 4), at most one band
+        or self.banded is False.  Default band count: ~24 ADOs per band (ns = 2; 8 for ns = 3, 4), at most one band
         per CU (the bands must be co-resident); hierarchies that would then need more than 80 (20) rows per band
         stay on the stage launches.  Measured at 6188 ADOs: 256 bands 94.7k steps/s against 51.7k for the stage
         launches; 18,564 ADOs on 256 bands 68k against 42.1k (tools/deom_band_sweep.py,
-        profiles/r03/deom/band_sweep.txt).  QD_DEOM_BANDS overrides.  Cached per (device, count)."""
-        if os.environ.get("QD_DEOM_BANDED") == "0" or os.environ.get("QD_DEOM_HORNER") == "0":
-            return None   # QD_DEOM_HORNER=0 (classic-RK4 A/B runs) is a stage-launch switch: the bands run Horner
+        profiles/r03/deom/band_sweep.txt).  self.bands sets the count.  Cached per (device, count)."""
+        if self.banded is False:
+            return None
         ns, K, nmax = self.nsys, self.nind, self.nmax
         if not (2 <= ns <= 4) or K > 8:
             return None
@@ -527,9 +535,8 @@ class DEOMSolver:
         per, fat = (24, 80) if G == 4 else (8, 20)
         cap = min(BANDS_MAX, torch.cuda.get_device_properties(dev).multi_processor_count)
         if nbands is None:
-            env = os.environ.get("QD_DEOM_BANDS")
-            if env:
-                nbands = int(env)
+            if self.bands:
+                nbands = int(self.bands)
             else:
                 nbands = min(cap, max(1, -(-nmax // per)))
                 if -(-nmax // nbands) > fat:   # fat bands lose to the stage launches (146 rows: 0.78x)

@@ -104,8 +104,7 @@ def lindblad_rk4(H: torch.Tensor, c_ops: torch.Tensor | None, rho: torch.Tensor,
     # rho H, not rho H^+), so the Hermitian kernel is gated on both, bit for bit.
     h_herm = _is_hermitian_cached(H)
     if hermitian is None:
-        np64 = 32 < N <= 64 and os.environ.get("QD_GLF_HSPLIT_NP64") != "1"   # =1: the pair-block path (tests)
-        min_b = HERM_NP64_MIN_BATCH if np64 else HERM_SPLIT_MIN_BATCH
+        min_b = HERM_NP64_MIN_BATCH if 32 < N <= 64 else HERM_SPLIT_MIN_BATCH
         hermitian = (N <= 128 and B >= min_b and h_herm
                      and bool(torch.equal(rho, rho.transpose(-1, -2).conj())))
     elif hermitian and not h_herm:

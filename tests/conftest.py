@@ -37,3 +37,30 @@ SPECTRA = {
     "flat005": lambda w: 0.05,
     "tanh": lambda w: 0.02 * (1.0 + np.tanh(2.0 * w)),
 }
+
+
+import contextlib  # noqa: E402
+
+
+@contextlib.contextmanager
+def qd_option(name, value):
+    """Set a libqdyn process option (include/qdyn.h QD_OPT_*: "coop", "fake_timeout", "glf_path") for the block and
+    restore it after."""
+    from pyqed_amd import _lib
+    opt = {"coop": _lib.QD_OPT_COOP_LAUNCH, "fake_timeout": _lib.QD_OPT_FAKE_TIMEOUT,
+           "glf_path": _lib.QD_OPT_GLF_PATH}[name]
+    if isinstance(value, str):
+        value = _lib.GLF_PATHS[value]
+    prev = _lib.set_option(opt, value)
+    try:
+        yield
+    finally:
+        _lib.set_option(opt, prev)
+
+
+def took(path_name):
+    """True when the library calls since the last check took a kernel path whose name starts with path_name
+    (qd_take_path; clears the record)."""
+    from pyqed_amd import _lib
+    got = _lib.take_path().split()
+    return any(p.startswith(path_name) for p in got), got

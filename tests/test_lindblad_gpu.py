@@ -197,52 +197,42 @@ def test_lindblad_hermitian_kernel_matches_general(N, nc, B):
         assert relerr(a, b) < TOL
 
 
-@pytest.mark.parametrize("N,nc,B,bt", [(128, 1, 16, None), (128, 1, 64, None), (128, 2, 20, None),
-                                       (128, 1, 40, "64"), (64, 1, 24, None), (100, 1, 17, None),
-                                       (128, 0, 16, None), (64, 3, 18, "64")])
-def test_lindblad_hermitian_split_path(N, nc, B, bt, monkeypatch):
-    """Hermitian batches below the persistent kernel's range run the pair-block split path (glf_split_hk2_kernel, or
-    glf_split_hk_kernel with QD_GLF_HK2=0: one workgroup per upper block pair, the Hermitian part C r C^+ only on the upper block; 32-blocks, 64-blocks
-    forced by QD_GLF_HSPLIT_BT; N = 100 is zero-padded to 128; no collapse operators, three): vs the oracle, the persistent Hermitian kernel
-    (QD_GLF_HSPLIT=0) and the general kernel, exactly Hermitian, with observables and snapshots."""
-    if bt is not None:
-        monkeypatch.setenv("QD_GLF_HSPLIT_BT", bt)
-    if N <= 64:   # N_p = 64 runs the pair-block path only on request (the general split-K path is faster there)
-        monkeypatch.setenv("QD_GLF_HSPLIT_NP64", "1")
+@pytest.mark.parametrize("N,nc,B", [(128, 1, 16), (128, 1, 64), (128, 2, 20), (128, 1, 40), (100, 1, 17),
+                                    (128, 0, 16), (100, 3, 18), (128, 1, 207)])
+def test_lindblad_hermitian_split_path(N, nc, B):
+    """Hermitian batches at N_p = 128 below the persistent kernel's range run the pair-block split path
+    (glf_split_hk2_kernel: two workgroups per off-diagonal 32-block pair, the Hermitian part C r C^+ only on the upper
+    block; N = 100 is zero-padded to 128; no collapse operators, three; B = 207, the last batch size before the
+    persistent kernel): vs the oracle, the persistent Hermitian kernel (QD_OPT_GLF_PATH persistent) and the general
+    kernel, exactly Hermitian, with observables and snapshots."""
     import torch
     from oracle import lindblad as olb
     from pyqed_amd import lindblad_rk4
+    from conftest import qd_option, took
     H, cs = olb.synthetic_lindblad(N, nc=max(nc, 1))
     cs = cs[:nc]
     rho0 = olb.random_pure_states(B, N, seed=N + B)
     steps, dt = 6, 1e-2
-    ref = olb.lindblad_batch(H, cs, rho0, dt, steps)
+    sel = sorted({0, B // 2, B - 1})
+    ref = olb.lindblad_batch(H, cs, rho0[sel], dt, steps)
     dev = torch.device("cuda", 0)
     Ht = torch.from_numpy(H).to(dev)
     Ct = torch.from_numpy(np.array(cs)).to(dev) if nc else None
     E = torch.eye(N, dtype=torch.complex128, device=dev).unsqueeze(0)
     out = {}
-    for tag, herm, env, hk2 in (("split", None, None, None), ("split1", None, None, "0"), ("persistent", True, "0", None),
-                                ("general", False, None, None)):
-        if env is None:
-            monkeypatch.delenv("QD_GLF_HSPLIT", raising=False)
-        else:
-            monkeypatch.setenv("QD_GLF_HSPLIT", env)
-        if hk2 is None:
-            monkeypatch.delenv("QD_GLF_HK2", raising=False)
-        else:
-            monkeypatch.setenv("QD_GLF_HK2", hk2)
+    for tag, herm, path, want in (("split", None, "auto", "glf_split_pairs"), ("persistent", True, "persistent",
+                                                                              "glf_persistent"),
+                                  ("general", False, "auto", "glf_split" if B < 192 else "glf_persistent")):
         rho = torch.from_numpy(rho0.copy()).to(dev)
-        obs, snap = lindblad_rk4(Ht, Ct, rho, dt, steps, e_ops=E, save_every=3, hermitian=herm)
+        took("")
+        with qd_option("glf_path", path):
+            obs, snap = lindblad_rk4(Ht, Ct, rho, dt, steps, e_ops=E, save_every=3, hermitian=herm)
         torch.cuda.synchronize()
+        assert want in took("")[1], tag
         out[tag] = (rho.cpu().numpy(), obs.cpu().numpy(), snap.cpu().numpy())
     r = out["split"][0]
-    assert relerr(r, ref) < TOL
+    assert relerr(r[sel], ref) < TOL
     assert np.array_equal(r, np.conj(np.swapaxes(r, 1, 2)))
-    # two workgroups per off-diagonal pair (glf_split_hk2_kernel, default) vs one (QD_GLF_HK2=0): the same GEMMs and
-    # sums, so bit-identical
-    for a, b in zip(out["split"], out["split1"]):
-        assert np.array_equal(a, b)
     for other in ("persistent", "general"):
         for a, b in zip(out["split"], out[other]):
             assert relerr(a, b) < TOL
@@ -288,15 +278,16 @@ def test_correlation_3p_1t_matches_reference(tmp_path, monkeypatch):
         correlation_3p_1t(g["H"], g["rho0"], ops, [], g["tlist"], lambda r, H, c: r)
 
 
-@pytest.mark.parametrize("N,nc,B", [(128, 1, 1), (96, 2, 3), (64, 1, 2), (256, 1, 1)])
-def test_lindblad_split_path_matches_persistent_and_oracle(N, nc, B, monkeypatch):
-    """Small batches: every output block of a stage phase is its own workgroup (glf_split_*, forced with
-    QD_GLF_SPLIT=1), with the phases' K-tiles split over workgroups and summed by the last arriver (default)
-    or not (QD_GLF_SPLITK=0) -- observables, snapshots and the final state against the persistent kernel and
-    the oracle."""
+@pytest.mark.parametrize("N,nc,B", [(128, 1, 1), (96, 2, 3), (64, 1, 2), (256, 1, 1), (128, 1, 24), (256, 2, 8)])
+def test_lindblad_split_path_matches_persistent_and_oracle(N, nc, B):
+    """Small batches: every output block of a stage phase is its own workgroup (glf_split_*, QD_OPT_GLF_PATH split),
+    with the phases' K-tiles split over workgroups and summed by the last arriver where the blocks leave the chip
+    under-filled (one matrix at N = 128: 4-way split-K; 24 matrices: none) -- observables, snapshots and the final
+    state against the persistent kernel and the oracle."""
     import torch
     from oracle import lindblad as olb
     from pyqed_amd import lindblad_rk4
+    from conftest import qd_option, took
     H, cs = olb.synthetic_lindblad(N, nc=nc)
     rho0 = olb.random_pure_states(B, N)
     E = np.array([np.diag(np.arange(N, dtype=float)).astype(complex), cs[0] + cs[0].conj().T])
@@ -304,18 +295,20 @@ def test_lindblad_split_path_matches_persistent_and_oracle(N, nc, B, monkeypatch
     dev = torch.device("cuda", 0)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     out = {}
-    for mode in ("1", "1nk", "0"):
-        monkeypatch.setenv("QD_GLF_SPLIT", mode[0])
-        monkeypatch.setenv("QD_GLF_SPLITK", "0" if mode == "1nk" else "1")
+    for mode in ("split", "persistent"):
         rho = t(rho0.copy())
-        obs, snap = lindblad_rk4(t(H), t(np.array(cs)), rho, dt, steps, t(E), save_every=2, hermitian=False)
+        took("")
+        with qd_option("glf_path", mode):
+            obs, snap = lindblad_rk4(t(H), t(np.array(cs)), rho, dt, steps, t(E), save_every=2, hermitian=False)
         torch.cuda.synchronize()
+        assert ("glf_" + mode) in took("")[1]
         out[mode] = (rho.cpu().numpy(), obs.cpu().numpy(), snap.cpu().numpy())
-    ref = olb.lindblad_batch(H, cs, rho0, dt, steps)
-    assert relerr(out["1"][0], ref) < TOL
-    for a, b, c in zip(out["1"], out["0"], out["1nk"]):
-        assert relerr(a, b) < 1e-12 and relerr(c, b) < 1e-12
-    tr = np.einsum("bsii->bs", out["1"][2])
+    sel = sorted({0, B - 1})
+    ref = olb.lindblad_batch(H, cs, rho0[sel], dt, steps)
+    assert relerr(out["split"][0][sel], ref) < TOL
+    for a, b in zip(out["split"], out["persistent"]):
+        assert relerr(a, b) < 1e-12
+    tr = np.einsum("bsii->bs", out["split"][2])
     assert np.max(np.abs(tr - 1)) < 1e-12
 
 
@@ -516,20 +509,19 @@ def test_lindblad_np64_hermitian_dispatch_matches_oracle(N, B):
     assert relerr(rho.cpu().numpy()[:3], ref) < TOL
 
 
-@pytest.mark.parametrize("N,nc,B,m3", [(128, 1, 1, None), (128, 1, 1, "0"), (128, 2, 1, None), (100, 1, 4, None),
-                                       (100, 1, 4, "1"), (64, 1, 3, None), (40, 2, 2, None), (20, 0, 5, None),
-                                       (32, 1, 64, None)])
-def test_lindblad_single_launch_matches_split_path_and_oracle(N, nc, B, m3, monkeypatch):
+@pytest.mark.parametrize("N,nc,B,prod", [(128, 1, 1, "3m"), (128, 2, 1, "4m"), (128, 1, 2, "3m"), (100, 1, 4, "4m"),
+                                         (64, 1, 3, "3m"), (40, 2, 2, "4m"), (20, 0, 5, "3m"), (32, 1, 64, "4m"),
+                                         (32, 1, 8, "3m")])
+def test_lindblad_single_launch_matches_split_path_and_oracle(N, nc, B, prod):
     """Few density matrices as ONE persistent launch (glf_single.hip: a workgroup per 16 x 16 output tile, operator
     fragments in registers, Y_c and stage outputs handed over inside the launch): final state, observables after every
-    step and snapshots against the split path (QD_GLF_SINGLE=0) and the oracle's RK4 (oqs.py:697-714, 1596-1696);
-    Np = 128 / 64 / 32, nc = 0 / 1 / 2, up to the 256-workgroup cap (B = 4 at Np = 128, 64 at Np = 32); the 3- and
-    4-product complex MACs (QD_GLF_SINGLE_3M; default: 3 products up to 128 workgroups)."""
+    step and snapshots against the split path (N_p >= 64) or the persistent kernel (N_p = 32) and the oracle's RK4
+    (oqs.py:697-714, 1596-1696); Np = 128 / 64 / 32, nc = 0 / 1 / 2, up to the 256-workgroup cap (B = 4 at Np = 128,
+    64 at Np = 32); the 3-product complex MACs up to 128 workgroups (nc < 2), 4 products above (qd_take_path)."""
     import torch
-    if m3 is not None:
-        monkeypatch.setenv("QD_GLF_SINGLE_3M", m3)
     from oracle import lindblad as olb
     from pyqed_amd import lindblad_rk4
+    from conftest import qd_option, took
     H, cs = olb.synthetic_lindblad(N, nc=max(nc, 1))
     cs = cs[:nc]
     rho0 = olb.random_pure_states(B, N, seed=9)
@@ -539,39 +531,45 @@ def test_lindblad_single_launch_matches_split_path_and_oracle(N, nc, B, m3, monk
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     Ct = t(np.array(cs)) if nc else None
     out = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("QD_GLF_SINGLE", mode)
+    other = "split" if N > 32 else "persistent"
+    for mode in ("single", other):
         rho = t(rho0.copy())
-        obs, snap = lindblad_rk4(t(H), Ct, rho, dt, steps, t(E), save_every=1, hermitian=False)
+        took("")
+        with qd_option("glf_path", mode):
+            obs, snap = lindblad_rk4(t(H), Ct, rho, dt, steps, t(E), save_every=1, hermitian=False)
         torch.cuda.synchronize()
+        got = took("")[1]
+        assert ("glf_" + mode) in got, (mode, got)
+        if mode == "single":
+            assert ("glf_single_" + prod) in got, got
         out[mode] = (rho.cpu().numpy(), obs.cpu().numpy(), snap.cpu().numpy())
     ref = olb.lindblad_batch(H, cs, rho0, dt, steps)
-    assert relerr(out["1"][0], ref) < TOL
-    for a, b in zip(out["1"], out["0"]):
+    assert relerr(out["single"][0], ref) < TOL
+    for a, b in zip(out["single"], out[other]):
         assert relerr(a, b) < 1e-12
-    assert relerr(out["1"][2][:, -1], out["1"][0]) == 0.0
+    assert relerr(out["single"][2][:, -1], out["single"][0]) == 0.0
     obs_ref = np.einsum("bij,mji->bm", rho0, E)
-    assert relerr(out["1"][1][:, 0], obs_ref) < 1e-13
+    assert relerr(out["single"][1][:, 0], obs_ref) < 1e-13
 
 
-def test_lindblad_single_launch_timeout_falls_back(monkeypatch, capfd):
-    """A hand-off timeout of the single-trajectory launch (forced after a real run by QD_GLF_SINGLE_FAKE_TIMEOUT) makes
-    libqdyn restore the initial state and re-run on the split path: same result as the split path."""
+def test_lindblad_single_launch_timeout_falls_back(capfd):
+    """A hand-off timeout of the single-trajectory launch (forced after a real run by the QD_OPT_FAKE_TIMEOUT test
+    option) makes libqdyn restore the initial state and re-run on the split path: same result as the split path."""
     import torch
     from oracle import lindblad as olb
     from pyqed_amd import lindblad_rk4
+    from conftest import qd_option
     N, steps, dt = 128, 4, 1e-2
     H, cs = olb.synthetic_lindblad(N, nc=1)
     rho0 = olb.random_pure_states(1, N, seed=4)
     dev = torch.device("cuda", 0)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-    monkeypatch.setenv("QD_GLF_SINGLE", "0")
     r_split = t(rho0.copy())
-    lindblad_rk4(t(H), t(np.array(cs)), r_split, dt, steps, hermitian=False)
-    monkeypatch.setenv("QD_GLF_SINGLE", "1")
-    monkeypatch.setenv("QD_GLF_SINGLE_FAKE_TIMEOUT", "1")
+    with qd_option("glf_path", "split"):
+        lindblad_rk4(t(H), t(np.array(cs)), r_split, dt, steps, hermitian=False)
     r = t(rho0.copy())
-    lindblad_rk4(t(H), t(np.array(cs)), r, dt, steps, hermitian=False)
+    with qd_option("fake_timeout", 1):
+        lindblad_rk4(t(H), t(np.array(cs)), r, dt, steps, hermitian=False)
     torch.cuda.synchronize()
     assert "timed out" in capfd.readouterr().err
     assert torch.equal(r, r_split)

@@ -141,24 +141,23 @@ def test_ensemble_large_linearity_and_shards():
 
 
 @pytest.mark.parametrize("M", [1000, 2048])
-def test_ensemble_gemm_load_depth_bit_identical(M, monkeypatch):
-    """The 64-block ensemble GEMM with operand loads two K-tiles ahead (QD_ENS_DEPTH=2, default) equals the
-    one-tile-ahead engine bit for bit (same MFMA order; M = 1000 gives workgroups with odd and even K-tile
-    counts), and both match the closed form."""
+def test_ensemble_gemm64_matches_closed_form(M):
+    """The 64-block ensemble GEMM (operand loads two K-tiles ahead; M = 1000 gives workgroups with odd and even K-tile
+    counts) against the closed form summed over every member."""
     from pyqed_amd.response import response2d_ensemble
+    from conftest import took
     rng = np.random.default_rng(M)
     E = np.array([0.0, 1.0, 1.5]) + np.array([0.0, 0.05, 0.08]) * rng.standard_normal((M, 3))
     t = 0.5 * np.arange(256)
     lam, (alpha, Mt, beta) = _ensemble_inputs(E, 0.0)
-    res = {}
-    for d in ("1", "2"):
-        monkeypatch.setenv("QD_ENS_DEPTH", d)
-        res[d] = response2d_ensemble(lam, alpha, Mt, beta, t, t).cpu().numpy()
-    assert np.array_equal(res["1"], res["2"])
-    ref = sum((-1j) ** 3 * (alpha[m][None, :] * np.exp(np.outer(t, lam[m]))) @ Mt[m]
-              @ (beta[m][None, :] * np.exp(np.outer(t, lam[m]))).T for m in range(0, M, 97))
-    sub = response2d_ensemble(lam[::97], alpha[::97], Mt[::97], beta[::97], t, t).cpu().numpy()
-    assert relerr(sub, ref) < TOL
+    took("")
+    got = response2d_ensemble(lam, alpha, Mt, beta, t, t).cpu().numpy()
+    hit, paths = took("ens_gemm64")
+    assert hit, paths
+    X = alpha[:, None, :] * np.exp(t[None, :, None] * lam[:, None, :])      # [M][n3][K]
+    Y = beta[:, None, :] * np.exp(t[None, :, None] * lam[:, None, :])       # [M][n1][K]
+    ref = (-1j) ** 3 * np.einsum("mik,mkl,mjl->ij", X, Mt, Y, optimize=True)
+    assert relerr(got, ref) < TOL
 
 
 @pytest.mark.parametrize("name", ["redfield_n4", "redfield_n6_k2"])

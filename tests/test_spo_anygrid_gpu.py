@@ -3,8 +3,6 @@ lengths (Bluestein axes), lines longer than the LDS plan (direct DFT axes), ns >
 round 2 refused, all through the any-size engine (pyqed_amd/csrc/spo_gen.hip) against reference fixtures
 (tests/golden/make_golden.py: spo2_20x20, spo2_96x80, spo2_67x45_ns3, spo2_12x10_ns9, spo2_1024, spo3_24x20x18,
 spo1d_any).  fp64 with a different FFT factorisation than pocketfft: 1e-10 relative (L2)."""
-import os
-
 import numpy as np
 import pytest
 
@@ -15,23 +13,14 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-10
 
 
-def _spo2(name, env=None):
+def _spo2(name):
     from pyqed_amd import SPO2
     g = load_golden(name)
     nx, ny, ns = int(g["nx"]), int(g["ny"]), int(g["ns"])
     x, y, surfaces, couplings, psi0 = spo2_model_rect(nx, ny, ns)
     sol = SPO2(x, y, mass=[1.0, 1.3], nstates=ns)
     sol.set_DPES(surfaces, couplings)
-    old = {k: os.environ.get(k) for k in (env or {})}
-    os.environ.update(env or {})
-    try:
-        r = sol.run(psi0, dt=float(g["dt"]), nt=int(g["nt"]), nout=int(g["nout"]))
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+    r = sol.run(psi0, dt=float(g["dt"]), nt=int(g["nt"]), nout=int(g["nout"]))
     return g, r, x, y
 
 
@@ -43,11 +32,27 @@ def test_spo2_any_grid_matches_reference(name):
     assert relerr(np.array(r.psilist), g["psilist"]) < TOL
 
 
-@pytest.mark.parametrize("kind", ["1", "2"])
-def test_spo2_forced_bluestein_and_direct_axes(kind):
-    """Every axis forced onto the chirp-z plan (1) or the direct HBM DFT (2, unfused passes)."""
-    g, r, x, y = _spo2("spo2_96x80", env={"QD_SPO_FORCE_KIND": kind})
-    assert relerr(np.array(r.psilist), g["psilist"]) < TOL
+@pytest.mark.parametrize("nx,ny,axes,layout", [(2579, 12, ("spo_axis_direct", "spo_axis_mixed"), "spo_layout_in_place"),
+                                               (67, 45, ("spo_axis_bluestein", "spo_axis_mixed"), "spo_layout_alternating"),
+                                               (96, 80, ("spo_axis_mixed",), "spo_layout_alternating")])
+def test_spo2_axis_plans_and_layouts_match_oracle(nx, ny, axes, layout):
+    """Each axis plan of the any-size engine, reached by its length: a prime line beyond the chirp-z plan (2579: the
+    direct HBM DFT, in-place passes), a prime within it (67: Bluestein) and smooth lengths (mixed radix); the 2D
+    alternating layouts wherever every axis is an LDS plan.  Strang runs against the oracle restatement (pinned to the
+    reference at 32 x 32 and by the spo2_* fixtures)."""
+    from oracle import spo as osp
+    from pyqed_amd import SPO2
+    from conftest import took
+    x, y, surfaces, couplings, psi0 = spo2_model_rect(nx, ny, 2)
+    sol = SPO2(x, y, mass=[1.0, 1.3], nstates=2)
+    sol.set_DPES(surfaces, couplings)
+    took("")
+    r = sol.run(psi0, dt=0.05, nt=4, nout=2)
+    got = took("")[1]
+    for a in axes + (layout,):
+        assert a in got, (a, got)
+    pl, _ = osp.spo2_strang_run(sol.exp_V_half, osp.keo_linear(sol.exp_K), psi0, 4, 2)
+    assert relerr(np.array(r.psilist), np.array(pl)) < TOL
 
 
 def test_spo2_1024_matches_reference():
@@ -59,21 +64,6 @@ def test_spo2_1024_matches_reference():
     dx, dy = x[1] - x[0], y[1] - y[0]
     pops = np.array([[np.vdot(p[:, :, k], p[:, :, k]).real * dx * dy for k in range(2)] for p in r.psilist])
     assert relerr(pops, g["populations"]) < TOL
-
-
-def test_spo2_pow2_through_generic_engine_matches_reference():
-    """QD_SPO_GENERIC=1 sends a power-of-two grid (spo2_32) through the any-size engine too."""
-    import os
-    from pyqed_amd import SPO2
-    g = load_golden("spo2_32")
-    sol = SPO2(g["x"], g["y"], mass=list(g["masses"]), nstates=2)
-    sol.set_DPES([g["v0"], g["v1"]], [[[0, 1], g["coupling"]]])
-    os.environ["QD_SPO_GENERIC"] = "1"
-    try:
-        r = sol.run(g["psi0"], dt=float(g["dt"]), nt=int(g["nt"]), nout=int(g["nout"]))
-    finally:
-        os.environ.pop("QD_SPO_GENERIC", None)
-    assert relerr(np.array(r.psilist), g["psilist"]) < TOL
 
 
 def test_spo2_merged_and_jacobi_any_grid_match_oracle():
@@ -121,57 +111,24 @@ def test_spo1d_any_grid_matches_reference():
             assert relerr(np.array(r.psilist), g[f"n{n}_psilist"]) < TOL, n
 
 
-def test_spo1d_long_line_direct_dft_matches_reference(monkeypatch):
-    """The 6000-point line runs the four-step FFT by default (6000 = 75 x 80); QD_SPO_FORCE_KIND=2 sends it through the
-    direct O(L^2) DFT instead — both against the reference fixture."""
+@pytest.mark.parametrize("n,path", [(6000, "spo1d_fourstep"), (2579, "spo1d_direct"), (97, "spo1d_bluestein"),
+                                    (200, "spo1d_mixed")])
+def test_spo1d_line_plans_match_oracle(n, path):
+    """1D lines by plan: 6000 = 75 x 80 beyond the LDS plans (four-step FFT), the prime 2579 beyond the chirp-z plan
+    (direct DFT), the prime 97 (Bluestein) and 200 (mixed radix), against the oracle's SPO.run restatement (wpd.py:
+    225-273; the 6000-point line also against the reference fixture in test_spo1d_any_grid_matches_reference)."""
+    from oracle import spo as osp
     from pyqed_amd import SPO
-    g = load_golden("spo1d_any")
-    n = 6000
+    from conftest import took
     x, psi0 = spo1d_model(n)
-    monkeypatch.setenv("QD_SPO_FORCE_KIND", "2")
     sol = SPO(x, mass=1.0)
     sol.set_potential(lambda q: q ** 2 / 2)
-    r = sol.run(psi0, dt=0.01, nt=int(g[f"n{n}_nt"]), nout=int(g[f"n{n}_nout"]))
-    assert relerr(r.psi, g[f"n{n}_psi"]) < TOL
+    took("")
+    r = sol.run(psi0, dt=0.01, nt=6, nout=2)
+    hit, got = took(path)
+    assert hit, got
+    pl, fin = osp.spo1d_run(x, x ** 2 / 2, psi0, 0.01, 6, 2)
+    assert relerr(r.psi, fin) < TOL
+    assert relerr(np.array(r.psilist), np.array(pl)) < TOL
 
 
-@pytest.mark.parametrize("name", ["spo2_96x80", "spo2_67x45_ns3"])
-def test_spo2_alternating_layouts_bit_identical_to_in_place_passes(name, monkeypatch):
-    """The 2D generic passes alternate [x][y][s] / [y][x][s] layouts (spo_gen.hip Exec::xpose): same FFT plans, same
-    operations on the same line values, so the result equals the in-place passes (QD_SPO_XPOSE=0) bit for bit —
-    Strang, merged-V and Jacobi step sequences — and the reference fixture."""
-    from pyqed_amd import SPO2
-    g, r1, x, y = _spo2(name)
-    _, r0, _, _ = _spo2(name, env={"QD_SPO_XPOSE": "0"})
-    assert np.array_equal(np.array(r1.psilist), np.array(r0.psilist))
-    assert relerr(np.array(r1.psilist), g["psilist"]) < TOL
-    xs, ys, surfaces, couplings, psi0 = spo2_model_rect(30, 22, 2)
-    for kw, coords in (({"return_states": False}, "linear"), ({}, "jacobi")):
-        mass = [1.0, 1.3] if coords == "linear" else [1.0, lambda q: 1.5 + 0.2 * q ** 2]
-        out = []
-        for xp in ("1", "0"):
-            monkeypatch.setenv("QD_SPO_XPOSE", xp)
-            sol = SPO2(xs, ys, mass=mass, nstates=2, coords=coords)
-            sol.set_DPES(surfaces, couplings)
-            out.append(sol.run(psi0, dt=0.05, nt=5, nout=2, **kw).psi)
-        assert np.array_equal(out[0], out[1]), coords
-
-
-def test_spo3_rotated_layouts_bit_identical_to_in_place_passes(monkeypatch):
-    """3D grids can rotate their layouts (QD_SPO_XPOSE3=1, opt-in): [x][y][z] -> [x][z][y] -> [z][y][x] -> [x][z][y]
-    -> [x][y][z] over a step's four passes (spo_gen.hip Exec::z3_pass), equal bit for bit to the in-place passes
-    (QD_SPO_XPOSE3=0), Strang and merged V."""
-    from pyqed_amd import SPO3
-    g = load_golden("spo3_24x20x18")
-    (x, y, z), masses, surfaces, couplings, psi0 = spo3_model()
-    out = {}
-    for xp in ("1", "0"):
-        monkeypatch.setenv("QD_SPO_XPOSE3", xp)
-        sol = SPO3(x, y, z, masses=masses, nstates=2)
-        sol.set_DPES(surfaces, couplings)
-        r = sol.run(psi0=psi0, dt=float(g["dt"]), nt=int(g["nt"]), nout=int(g["nout"]))
-        rm = sol.run(psi0=psi0, dt=float(g["dt"]), nt=3, nout=1, return_states=False)
-        out[xp] = (np.array(r.psilist), r.psi, rm.psi)
-    for a, b in zip(out["1"], out["0"]):
-        assert np.array_equal(a, b)
-    assert relerr(out["1"][0], g["psilist"]) < TOL

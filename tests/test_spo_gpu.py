@@ -124,31 +124,28 @@ def test_spo3_matches_reference():
     assert relerr(r.psi, g["psi"]) < TOL
 
 
-@pytest.mark.parametrize("mid_c,col_c,fast,r64", [(None, None, None, None), ("4", "2", None, None),
-                                                   ("8", "4", None, None), ("16", "8", None, None),
-                                                   ("8", None, None, None), (None, "0", None, None),
-                                                   (None, None, "0", None), ("16", "8", "0", None),
-                                                   (None, None, None, "0"), ("16", "8", "0", "0")])
-def test_spo3_example_size_vs_oracle(mid_c, col_c, fast, r64, monkeypatch):
-    """examples/spo.py size: 64^3 x 2, vs the NumPy fftn restatement, and norm conservation; every
-    mid-axis and x-axis block width (QD_SPO3_MID_C / QD_SPO3_COL_C; None = the default launch), on the
-    latency-shaped mid / x kernels (default) and the generic LDS-staged ones (QD_SPO3_FAST=0), with the z pass on
-    the 64-point register transform (default) or the LDS Stockham kernel (QD_SPO_ROW64=0)."""
-    if r64 is not None:
-        monkeypatch.setenv("QD_SPO_ROW64", r64)
-    if fast is not None:
-        monkeypatch.setenv("QD_SPO3_FAST", fast)
-    if mid_c is not None:
-        monkeypatch.setenv("QD_SPO3_MID_C", mid_c)
-    if col_c is not None:
-        monkeypatch.setenv("QD_SPO3_COL_C", col_c)
+@pytest.mark.parametrize("dims,ns", [((64, 64, 64), 2), ((32, 32, 32), 2), ((128, 64, 64), 1), ((64, 128, 32), 2),
+                                     ((16, 32, 64), 2), ((32, 16, 16), 4), ((128, 128, 128), 2)])
+def test_spo3_pow2_grids_vs_oracle(dims, ns):
+    """Power-of-two SPO3 grids through the specialised kernels, each shape selecting its own mid-axis / x-axis
+    launches (64^3 x 2 is examples/spo.py's size: 64-point register transforms, LDS-staged x pass over the mid pass's
+    row width; 32^3: narrower blocks; 128 x 64^2 x 1: one state; ny = 128: the generic mid kernel; ns = 4: the LDS
+    kernels of ns > 2; 128^3: the two-column x pass) vs the NumPy fftn restatement (wpd.py:1349-1411) and norm
+    conservation."""
     from oracle import spo as ospo
     from pyqed_amd.wpd import SPO3
-    x, X, Y, Z, psi0 = _spo3_model(64)
-    sol = SPO3(x, x, x, masses=[1.0, 1.0, 1.0], nstates=2)
-    sol.set_DPES([0.5 * ((X + 1) ** 2 + Y ** 2 + Z ** 2), 0.5 * ((X - 1) ** 2 + Y ** 2 + Z ** 2)],
-                 [[[0, 1], 0.2 * X]])
+    from conftest import took
+    ax = [np.linspace(-6, 6, n) for n in dims]
+    X, Y, Z = np.meshgrid(*ax, indexing="ij")
+    psi0 = np.zeros(dims + (ns,), dtype=complex)
+    psi0[..., ns - 1] = np.exp(-((X + 1) ** 2 + Y ** 2 + Z ** 2) / 2 + 0.3j * Y) / np.pi ** 0.75
+    sol = SPO3(*ax, masses=[1.0, 1.0, 1.0], nstates=ns)
+    sol.set_DPES([0.5 * ((X + (-1) ** a) ** 2 + Y ** 2 + Z ** 2) + 0.1 * a for a in range(ns)],
+                 [[[a, a + 1], 0.2 * X] for a in range(ns - 1)])
+    took("")
     r = sol.run(psi0=psi0, dt=0.25, nt=4, nout=2)
+    hit, got = took("spo3_pow2")
+    assert hit, got
     ref, psi = ospo.spo3_run(sol.exp_V_half, sol.exp_K, psi0, 4, 2)
     assert relerr(np.array(r.psilist), np.array(ref)) < TOL
     assert abs(np.vdot(r.psi, r.psi).real / np.vdot(psi0, psi0).real - 1) < 1e-12
@@ -157,8 +154,7 @@ def test_spo3_example_size_vs_oracle(mid_c, col_c, fast, r64, monkeypatch):
 @pytest.mark.parametrize("nx,nout", [(64, 1), (32, 3)])
 def test_spo3_row64_single_state_and_shapes(nx, nout):
     """The 64-point register z pass with one electronic state and nx != 64: vs the NumPy fftn restatement,
-    snapshots every nout steps, and equal to the LDS Stockham z pass (QD_SPO_ROW64=0)."""
-    import os
+    snapshots every nout steps."""
     from oracle import spo as ospo
     from pyqed_amd.wpd import SPO3
     x = np.linspace(-6, 6, nx)
@@ -171,12 +167,6 @@ def test_spo3_row64_single_state_and_shapes(nx, nout):
     r = sol.run(psi0=psi0, dt=0.1, nt=6, nout=nout)
     ref, _ = ospo.spo3_run(sol.exp_V_half, sol.exp_K, psi0, 6, nout)
     assert relerr(np.array(r.psilist), np.array(ref)) < TOL
-    os.environ["QD_SPO_ROW64"] = "0"
-    try:
-        r0 = sol.run(psi0=psi0, dt=0.1, nt=6, nout=nout)
-    finally:
-        del os.environ["QD_SPO_ROW64"]
-    assert relerr(np.array(r.psilist), np.array(r0.psilist)) < 1e-13
 
 
 @pytest.mark.parametrize("return_states", [True, False])
@@ -275,23 +265,13 @@ def test_device_point_propagators_match_eigh(ns, cplx):
     assert (sol.apes is None) if cplx else np.array_equal(sol.apes, w2)
 
 
-@pytest.mark.parametrize("n,ns,B,rowmb", [(256, 2, 5, None), (256, 2, 6, "4"), (256, 2, 3, "1"), (256, 1, 3, None),
-                                          (64, 2, 2, None), (256, 2, 6, "wave4"), (256, 2, 5, "wave8"),
-                                          (256, 2, 3, "wave2"), (256, 2, 3, "col8"), (256, 2, 2, "col4"),
-                                          (256, 2, 3, "col16")])
-def test_spo2_run_batch_vs_single_and_oracle(n, ns, B, rowmb, monkeypatch):
+@pytest.mark.parametrize("n,ns,B", [(256, 2, 5), (256, 2, 6), (256, 2, 3), (256, 1, 3), (64, 2, 2), (256, 2, 8)])
+def test_spo2_run_batch_vs_single_and_oracle(n, ns, B):
     """SPO2.run_batch (qd_spo2_run_batch: one launch per pass for B wavepackets; 256x256 register-FFT kernels
     with a batch grid axis, member by member for other shapes): every member equals run() of that member
-    and the oracle's Strang steps, snapshots included.  ns = 2 row passes run MB members per workgroup sharing the
-    staged point operators (QD_SPO_ROWMB: default 2, 4, or 1 = one member per workgroup; QD_SPO_ROWWAVE: one wave
-    per member holding both states, 2 / 4 / 8 members per workgroup, default 4); column pass over 4- or 8-column
-    tiles (QD_SPO_COLTILE 4 / 8 / 16, default 8); ragged last groups."""
-    if rowmb is not None and rowmb.startswith("col"):
-        monkeypatch.setenv("QD_SPO_COLTILE", rowmb[3:])
-    elif rowmb is not None and rowmb.startswith("wave"):
-        monkeypatch.setenv("QD_SPO_ROWWAVE", rowmb[4:])
-    elif rowmb is not None:
-        monkeypatch.setenv("QD_SPO_ROWMB", rowmb)
+    and the oracle's Strang steps, snapshots included.  ns = 2 row passes run one wave per member holding both states,
+    4 members per workgroup sharing the staged point operators; the column pass runs 8-column tiles; ragged last
+    groups (B = 5, 6, 3)."""
     from oracle import spo as ospo
     from pyqed_amd.wpd import SPO2
     x = np.linspace(-6, 6, n)

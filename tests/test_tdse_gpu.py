@@ -129,22 +129,18 @@ def test_driven_batch_vs_oracle(N, B):
         assert relerr(snap[b].cpu().numpy(), psit[:, 1:].T) < TOL
 
 
-@pytest.mark.parametrize("gemm", ["auto", "0"])
-@pytest.mark.parametrize("N,B,save_every", [(300, 1, 2), (2500, 2, 3), (1024, 64, 5), (600, 130, 2)])
-def test_tdse_row_path_vs_persistent_and_oracle(N, B, save_every, gemm, monkeypatch):
-    """Row-parallel TDSE path (a wave per row and stage launch; the only path past N = 2048) and, where
-    tdse.hip's dispatch takes it ((B >= 64 and N >= 512) or (B >= 128 and N >= 256)), the MFMA GEMM stages
-    (padded [Bp][Np] state, split-K slabs): snapshots and observables (E_m = H, diag) against the persistent
-    kernel (N <= 2048) and the oracle's RK4 (oracle.tdse restates mol.py:1603-1691); B = 64 / 130 and N = 600
-    exercise the GEMM's padding to multiples of 128.  gemm="0" (QD_TDSE_GEMM=0) keeps the row kernel at the
-    batch sizes the GEMM would otherwise take."""
-    if gemm == "0":
-        if B < 64:
-            pytest.skip("the GEMM path is not taken at this batch size either way")
-        monkeypatch.setenv("QD_TDSE_GEMM", "0")
+@pytest.mark.parametrize("N,B,save_every,path", [(300, 1, 2, "tdse_rows"), (2500, 2, 3, "tdse_rows"),
+                                                  (1024, 64, 5, "tdse_gemm"), (600, 130, 2, "tdse_gemm"),
+                                                  (1024, 8, 2, "tdse_rows")])
+def test_tdse_row_and_gemm_paths_vs_oracle(N, B, save_every, path):
+    """The row path (a wave per row and stage launch) and, where tdse.hip's dispatch takes it ((B >= 64 and N >= 512)
+    or (B >= 128 and N >= 256)), the MFMA GEMM stages (padded [Bp][Np] state, split-K slabs): snapshots and
+    observables (E_m = H, diag) against the oracle's RK4 (oracle.tdse restates mol.py:1603-1691); B = 64 / 130 and
+    N = 600 exercise the GEMM's padding to multiples of 128."""
     import torch
     from oracle import tdse as otd
     from pyqed_amd.mol import tdse_rk4
+    from conftest import took
     rng = np.random.default_rng(N + B)
     A = rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N))
     H = (A + A.conj().T) / 2 / np.sqrt(N)
@@ -154,15 +150,12 @@ def test_tdse_row_path_vs_persistent_and_oracle(N, B, save_every, gemm, monkeypa
     dev = torch.device("cuda", 0)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     steps, dt = 6, 0.02
-    out = {}
-    for mode in (("1", "0") if N <= 2048 else ("1",)):
-        monkeypatch.setenv("QD_TDSE_ROWS", mode)
-        psi = t(psi0.copy())
-        snap, obs = tdse_rk4(t(H), psi, dt, steps, save_every=save_every, e_ops=t(np.array([H, Ed])))
-        out[mode] = (psi.cpu().numpy(), snap.cpu().numpy(), obs.cpu().numpy())
-    if "0" in out:
-        for a, b in zip(out["1"], out["0"]):
-            assert relerr(a, b) < 1e-13
+    took("")
+    psi = t(psi0.copy())
+    snap, obs = tdse_rk4(t(H), psi, dt, steps, save_every=save_every, e_ops=t(np.array([H, Ed])))
+    hit, got = took(path)
+    assert hit, got
+    out = {"1": (psi.cpu().numpy(), snap.cpu().numpy(), obs.cpu().numpy())}
     psi, snap, obs = out["1"]
     ref = psi0[0].copy()
     for s in range(steps):

@@ -33,7 +33,7 @@ def main():
         r = _deom_event_rate(dev, sol, bath, sz + sx, sx[None], 1, steps, dt=dt, banded=False)
         print(f"nmax {sol.nmax}: stage launches {r:.0f} steps/s ({1e6 / r:.2f} us/step)", flush=True)
         for nb in counts:
-            os.environ["QD_DEOM_BANDS"] = str(nb)
+            sol.bands = nb
             bt = sol.band_tables(dev)
             if bt is None:
                 print(f"  {nb} bands: not eligible", flush=True)
@@ -41,7 +41,7 @@ def main():
             r = _deom_event_rate(dev, sol, bath, sz + sx, sx[None], 1, steps, dt=dt)
             print(f"  {bt.nbands} bands (own <= {bt.max_own}, rows <= {bt.max_loc}): {r:.0f} steps/s "
                   f"({1e6 / r:.2f} us/step)", flush=True)
-        os.environ.pop("QD_DEOM_BANDS", None)
+        sol.bands = None
 
 
 if __name__ == "__main__":

@@ -1,6 +1,6 @@
 """DEOM stage kernels timed by HIP events on device-resident state (no host transfers in the timed region): the
 bench hierarchy (spin-boson, Drude, Pade npsd=4 -> K=5, L=12 -> 6188 ADOs, dt=0.002) at B hierarchies.
-usage: python tools/deom_bench.py [B ...]   (env QD_DEOM_XCD / QD_DEOM_ADO_MAJOR select the variants)
+usage: python tools/deom_bench.py [B ...]   (env DEOM_LAYOUT = ado_major / element_major forces the layout)
 One JSON line per B: RK4 steps/s, ADO-steps/s, and algorithmic HBM GB/s at 768 B per ADO-step."""
 import json
 import os
@@ -30,10 +30,10 @@ i32 = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=np.int
 tabs = (i32(sol._minus), i32(sol._plus), c128(coef), c128(damp), i32(bath.mode))
 H, Q = c128(sz + sx), c128(sx[None])
 lib = _lib.load()
-am_env = os.environ.get("QD_DEOM_ADO_MAJOR")
+am_env = os.environ.get("DEOM_LAYOUT")
 steps = int(os.environ.get("DEOM_STEPS", "100"))
 for B in [int(a) for a in sys.argv[1:]] or [1, 64, 256]:
-    ado_major = B >= 16 if am_env is None else am_env != "0"
+    ado_major = B >= 16 if am_env is None else am_env == "ado_major"
     fn = lib.qd_deom_rk4_ado_major if ado_major else lib.qd_deom_rk4
     shape = (nmax, B, ns, ns) if ado_major else (B, nmax, ns, ns)
     ados = torch.zeros(shape, dtype=torch.complex128, device=dev)
@@ -54,7 +54,7 @@ for B in [int(a) for a in sys.argv[1:]] or [1, 64, 256]:
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1)
     sps = steps / ms * 1e3
-    print(json.dumps({"B": B, "ado_major": ado_major, "xcd": os.environ.get("QD_DEOM_XCD", "default"),
+    print(json.dumps({"B": B, "ado_major": ado_major, "path": _lib.take_path(),
                       "steps_per_s": round(sps, 1), "ado_steps_per_s": round(sps * nmax * B, 1),
                       "us_per_stage": round(ms * 1e3 / steps / 4, 2),
                       "algo_gbs": round(sps * nmax * B * 768 / 1e9, 1),

@@ -11,7 +11,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from oracle import lindblad as olb  # noqa: E402  (input synthesis only)
-from pyqed_amd import lindblad_rk4  # noqa: E402
+from pyqed_amd import _lib, lindblad_rk4  # noqa: E402
 
 dev = torch.device("cuda", 0)
 Bs = [int(x) for x in (sys.argv[1].split(",") if len(sys.argv) > 1 else "1,4,16,32,64,128,256".split(","))]
@@ -20,14 +20,10 @@ for N in (128, 256):
     Ht, Ct = torch.from_numpy(H).to(dev), torch.from_numpy(np.array(cs)).to(dev)
     for B in Bs:
         rho0 = torch.from_numpy(olb.random_pure_states(B, N)).to(dev)
-        modes = [("herm-persistent", True, "0", "")] if N <= 128 else []
-        modes += [("persistent", False, "0", ""), ("split32", False, "1", "32"), ("split64", False, "1", "64"),
-                  ("split128", False, "1", "128")]
-        for mode, herm, split, bt in modes:
-            if N == 128 and bt == "128":
-                continue
-            os.environ["QD_GLF_SPLIT"] = split
-            os.environ["QD_GLF_SPLIT_BT"] = bt
+        modes = [("herm-persistent", True, "persistent")] if N <= 128 else []
+        modes += [("persistent", False, "persistent"), ("split", False, "split")]
+        for mode, herm, path in modes:
+            _lib.set_option(_lib.QD_OPT_GLF_PATH, _lib.GLF_PATHS[path])
             rho = rho0.clone()
             lindblad_rk4(Ht, Ct, rho, 1e-3, 2, hermitian=herm)
             torch.cuda.synchronize()

@@ -15,7 +15,7 @@ cd /tmp && export TMPDIR=/tmp
 # a cooperative launch makes rocprofv3 segfault at process exit, with --pmc and (seen in r04) with --kernel-trace
 # too, after the output is written (profiles/r04/pmc_crash/SUMMARY.md): every profiled run takes the plain launch
 # of the banded DEOM and single-trajectory Lindblad kernels (same kernels, same residency)
-export QD_DEOM_BAND_COOP=0 QD_GLF_SINGLE_COOP=0
+export QD_COOP_LAUNCH=0
 if [ "$PART" = stats ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- python3 $R/bench.py --steps 50 --warmup 5 --no-cpu > $OUT/stats.log 2>&1
   timeout -k 10 60 $R/tools/mfma_f64_peak > $OUT/mfma_f64_peak.log 2>&1

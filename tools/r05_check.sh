@@ -12,6 +12,6 @@ tail -2 $OUT/gputest.log
 timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --detail $OUT/bench_detail.json > $OUT/bench.json 2> $OUT/bench.err
 cat $OUT/bench.json | head -c 1500; echo
 cd /tmp && export TMPDIR=/tmp
-export QD_DEOM_BAND_COOP=0 QD_GLF_SINGLE_COOP=0 BENCH_MAPS=$OUT/maps.txt
+export QD_COOP_LAUNCH=0 BENCH_MAPS=$OUT/maps.txt
 timeout -k 10 250 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu --detail $OUT/fetch_detail.json > $OUT/fetch.log 2>&1
 echo "pmc pass ok"

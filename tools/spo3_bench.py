@@ -35,6 +35,6 @@ for n in [int(v) for v in os.environ.get("SPO3_SIZES", "64,128").split(",")]:
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     byts = (6 * n ** 3 * 2 + n ** 3 * 4 + n ** 3) * 16   # psi r+w in 3 passes, exp_V_half, exp_K
-    print(json.dumps({"n": n, "mid_c": os.environ.get("QD_SPO3_MID_C", "auto"),
-                      "col_c": os.environ.get("QD_SPO3_COL_C", "fast"), "steps_per_s": round(steps / el, 1), "us_per_step": round(el / steps * 1e6, 2),
+    print(json.dumps({"n": n, 
+                      "steps_per_s": round(steps / el, 1), "us_per_step": round(el / steps * 1e6, 2),
                       "alg_GBs": round(byts * steps / el / 1e9, 1)}), flush=True)
