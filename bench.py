@@ -886,8 +886,9 @@ def time_reduce_one_rank(dev, reps=50):
 
 def _deom_banded_cases():
     """(name, solver, rho0, dt) of the tier-banded leg: BASELINE.json configs[3] (spin-boson, ns = 2, L = 12, K = 5,
-    6188 ADOs) and a capacity-style hierarchy whose per-ADO work is ns^3-heavy (ns = 96 GUE H, Q = diag, Drude
-    npsd = 3 -> K = 4, L = 4: 70 ADOs of 147 KB, 10.3 MB of state; the tiled stage kernel)."""
+    6188 ADOs) and compute-heavy hierarchies whose per-ADO work is ns^3 (GUE H, Q = diag, Drude npsd = 3 -> K = 4):
+    ns = 64, L = 6 (210 ADOs of 64 KB), ns = 128 and 192, L = 4 (70 ADOs of 256 / 576 KB) -- the tiled MFMA stage
+    kernel."""
     import sympy as sp
     from pyqed_amd.deom import Bath, DEOMSolver
     w = sp.symbols(r"\omega", real=True)
@@ -898,25 +899,74 @@ def _deom_banded_cases():
     bath = Bath([2 * 0.5 * 1.0 * w / (1.0 + w ** 2)], w, [1.0], [4], [0] * 5)
     cases = [("spin_boson_L12_K5 (configs[3])", DEOMSolver(sz + sx, None, bath, np.array([sx]), None, None, None, 12),
               r0, 0.002)]
-    ns = 96
-    rng = np.random.default_rng(96)
-    a = rng.standard_normal((ns, ns)) + 1j * rng.standard_normal((ns, ns))
-    H = (a + a.conj().T) / 2 / np.sqrt(ns)
-    Q = np.diag(np.linspace(-1, 1, ns)).astype(complex)
     bath3 = Bath([2 * 0.3 * w / (1.0 + w ** 2)], w, [1.0], [3], [0] * 4)
-    rb = np.zeros((ns, ns), complex)
-    rb[0, 0] = 1
-    cases.append((f"ns{ns}_L4_K4", DEOMSolver(H, None, bath3, np.array([Q]), None, None, None, 4), rb, 0.002))
+    for ns, L in ((64, 6), (128, 4), (192, 4)):
+        rng = np.random.default_rng(ns)
+        a = rng.standard_normal((ns, ns)) + 1j * rng.standard_normal((ns, ns))
+        H = (a + a.conj().T) / 2 / np.sqrt(ns)
+        Q = np.diag(np.linspace(-1, 1, ns)).astype(complex)
+        rb = np.zeros((ns, ns), complex)
+        rb[0, 0] = 1
+        cases.append((f"ns{ns}_L{L}_K4", DEOMSolver(H, None, bath3, np.array([Q]), None, None, None, L), rb, 0.002))
     return cases
+
+
+XGMI_LINK_GBS = 153.0     # one xGMI link per direction (MI355X: 7 links per GPU), the band model's transfer rate
+RCCL_LATENCY_US = 10.0    # assumed per-exchange latency floor of a small RCCL send / recv or all-gather over xGMI
+
+
+def deom_band_model(dev, sh, single_ms, reps=24):
+    """Per-band model of one hierarchy tier-banded over len(sh.plans) GPUs, from quantities one
+    GPU can measure: each band's RK4 stage timed ALONE (qd_deom_stage on its own rows, HIP events, `reps` stages),
+    and the bytes each band receives per stage.  Per stage the bands run concurrently, then exchange halos:
+        T_stage = max_b t_stage(b) + max_b max_q bytes(q -> b) / XGMI_LINK_GBS + latency
+    (point-to-point: every peer arrives over its own link, so the largest single transfer bounds the exchange; the
+    all-gather variant moves (n - 1) export sets over one ring link), four exchanges per RK4 step.  The projected
+    speed-up is the unbanded one-GPU step time over 4 T_stage; latency = 0 and RCCL_LATENCY_US bracket it."""
+    import torch
+    ns = sh.solver.nsys
+    row = ns * ns * 16
+    stream = torch.cuda.current_stream(dev)
+    t_band = []
+    for b in sh.bands:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for k in range(4):
+            b.stage(k, 0, 1e-6, 0j, 0j)
+        e0.record(stream)
+        for k in range(reps):
+            b.stage(k % 4, 0, 1e-6, 0j, 0j)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        t_band.append(e0.elapsed_time(e1) / reps * 1e-3)
+    recv_peer = [max([c for (_, c) in p.recv.values()] or [0]) * row for p in sh.plans]
+    recv_tot = [len(p.halo) * row for p in sh.plans]
+    export = max(len(np.unique(np.concatenate(list(p.send.values())))) if p.send else 0 for p in sh.plans) * row
+    n = len(sh.plans)
+    link = XGMI_LINK_GBS * 1e9
+    comp = max(t_band)
+    p2p = max(recv_peer) / link
+    ring = (n - 1) * export / link
+    out = {"bands": n, "band_stage_us": [round(t * 1e6, 2) for t in t_band],
+           "max_band_stage_us": round(comp * 1e6, 2),
+           "halo_bytes_per_stage_max": max(recv_tot), "largest_peer_transfer_bytes": max(recv_peer),
+           "allgather_export_bytes": export, "xgmi_link_GBs": XGMI_LINK_GBS, "latency_us_assumed": RCCL_LATENCY_US,
+           "one_gpu_unbanded_ms_per_step": round(single_ms, 4)}
+    for tag, xfer in (("p2p", p2p), ("allgather", ring)):
+        for lat in (0.0, RCCL_LATENCY_US * 1e-6):
+            step = 4 * (comp + xfer + lat)
+            key = f"{tag}_{'lat' if lat else 'nolat'}"
+            out[key] = {"ms_per_step": round(step * 1e3, 4), "speedup": round(single_ms / (step * 1e3), 3)}
+    return out
 
 
 def bench_deom_banded(dev, world, rank, steps=40):
     """ONE hierarchy tier-banded over the ranks (BASELINE.json configs[3]: "ADOs sharded over
     8xMI355X via xGMI"): one band per rank, one RCCL all-gather of the bands' export rows per RK4 stage
-    (deom_shard.CollectiveExchange), HIP stage kernels per band.  World 1: the same 8-band partition in one process
-    (LoopbackExchange, device-side copies) so the halo cost is known without a second GPU.  Timed: `steps` RK4 steps
-    of device-resident bands between barriers + device syncs, max over ranks; beside it the unbanded qd_deom_rk4 rate
-    of the same hierarchy on one GPU (rank 0)."""
+    (deom_shard.CollectiveExchange), HIP stage kernels per band.  World > 1: timed `steps` RK4 steps of
+    device-resident bands between barriers + device syncs, max over ranks.  World 1: the 8-band per-band model
+    (deom_band_model: each band's stage timed alone, halo bytes over one xGMI link, four exchanges per step) against the
+    unbanded qd_deom_rk4 rate of the same hierarchy, plus the loopback run of all 8 bands on this GPU (serialised
+    bands and device-copy exchanges: the correctness harness's cost, not a multi-GPU time)."""
     import torch
     import torch.distributed as dist
     from pyqed_amd.deom_shard import ShardedDEOM, run_bands
@@ -947,16 +997,18 @@ def bench_deom_banded(dev, world, rank, steps=40):
         halo = [len(p.halo) for p in sh.plans]
         own = [p.n_own for p in sh.plans]
         ent = {"nmax": sol.nmax, "ns": ns, "K": sol.nind, "L": sol.lmax, "bands": nb,
-               "exchange": "loopback (device copies, one GPU)" if world == 1 else "RCCL all-gather per stage",
-               "ms_per_step": round(el / steps * 1e3, 4), "steps": steps,
-               "ado_steps_per_s": round(sol.nmax * steps / el, 1),
                "max_halo_over_owned": round(max(h / o for h, o in zip(halo, own)), 3),
                "state_bytes": sol.nmax * ns * ns * 16}
         if world > 1:
-            ent["allgather_bytes_per_stage"] = sh.exchange.bytes_per_exchange
-        if single is not None:
-            ent["one_gpu_unbanded_ms_per_step"] = round(single, 4)
-            ent["speedup_vs_one_gpu"] = round(single / (el / steps * 1e3), 3)
+            ent.update({"exchange": "RCCL all-gather per stage", "ms_per_step": round(el / steps * 1e3, 4),
+                        "steps": steps, "ado_steps_per_s": round(sol.nmax * steps / el, 1),
+                        "allgather_bytes_per_stage": sh.exchange.bytes_per_exchange})
+            if single is not None:
+                ent["one_gpu_unbanded_ms_per_step"] = round(single, 4)
+        else:
+            ent["loopback_ms_per_step"] = round(el / steps * 1e3, 4)
+            ent["loopback_note"] = "8 bands serialised on one GPU with device-copy exchanges (correctness harness)"
+            ent["model_8gpu"] = deom_band_model(dev, sh, single)
         out[name] = ent
     return out
 
@@ -1059,7 +1111,13 @@ def compact_line(out, detail):
             s2[name] = leg if isinstance(leg, dict) else None
             continue
         if name == "deom_banded":
-            s2[name] = {k: _pick(v, "nmax", "bands", "ms_per_step", "speedup_vs_one_gpu") for k, v in leg.items()}
+            s2[name] = {}
+            for k, v in leg.items():
+                e = _pick(v, "nmax", "bands", "ms_per_step")
+                m = v.get("model_8gpu")
+                if isinstance(m, dict):
+                    e["model_8gpu_speedup"] = {"p2p": m["p2p_lat"]["speedup"], "p2p_nolat": m["p2p_nolat"]["speedup"]}
+                s2[name][k] = e
             continue
         e = _pick(leg, "value", "unit")
         if "roofline" in leg:

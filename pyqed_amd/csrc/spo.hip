@@ -1410,7 +1410,8 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
   // (colC * ns == midC, 128 B rows at 64^3 x 2: 41.1 -> 33.4 us per step); above that the
   // two-column kernel (128^3 x 2: 142 us either way, 146 us with colC * ns == midC).
   int colC = 0;
-  if (nk * ns <= (size_t)1 << 19 && midC >= 8 && midC % ns == 0) {  // 32^3 x 2 (midC = 4): 15.4 vs 16.6 us
+  // (nx <= 64: the LDS-staged x kernels are instantiated for 16 / 32 / 64-point columns)
+  if (nk * ns <= (size_t)1 << 19 && midC >= 8 && midC % ns == 0 && nx <= 64) {  // 32^3 x 2 (midC = 4): 15.4 vs 16.6 us
     const int c = midC / ns;
     if ((c == 2 || c == 4 || c == 8) && nyz % c == 0 && c * ns * (nx / 4) <= 256) colC = c;
   }
@@ -1432,7 +1433,9 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
         case 16: COLFASTC(16); break;
         case 32: COLFASTC(32); break;
         case 64: COLFASTC(64); break;
-        default: return QD_EINVAL;   // colC is set only at <= 64^3 x 2 points
+        default:   // colC is set only for nx <= 64
+          set_error("qd_spo3_run: internal: column tile for nx = %d", nx);
+          return QD_EINVAL;
       }
 #undef COLFASTC
       QD_HIP(hipGetLastError());
