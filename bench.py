@@ -884,11 +884,26 @@ def time_reduce_one_rank(dev, reps=50):
         _lib.check(lib.qd_comm_destroy(), "qd_comm_destroy")
 
 
+def _band_case(ns, L, npsd=3):
+    """A compute-heavy hierarchy for the tier-band model: GUE H / sqrt(ns), Q = diag(linspace(-1, 1)), one Drude bath
+    (npsd Pade terms), rho0 = |0><0|."""
+    import sympy as sp
+    from pyqed_amd.deom import Bath, DEOMSolver
+    w = sp.symbols(r"\omega", real=True)
+    bath3 = Bath([2 * 0.3 * w / (1.0 + w ** 2)], w, [1.0], [npsd], [0] * (npsd + 1))
+    rng = np.random.default_rng(ns)
+    a = rng.standard_normal((ns, ns)) + 1j * rng.standard_normal((ns, ns))
+    H = (a + a.conj().T) / 2 / np.sqrt(ns)
+    Q = np.diag(np.linspace(-1, 1, ns)).astype(complex)
+    rb = np.zeros((ns, ns), complex)
+    rb[0, 0] = 1
+    return (f"ns{ns}_L{L}_K{npsd + 1}", DEOMSolver(H, None, bath3, np.array([Q]), None, None, None, L), rb, 0.002)
+
+
 def _deom_banded_cases():
     """(name, solver, rho0, dt) of the tier-banded leg: BASELINE.json configs[3] (spin-boson, ns = 2, L = 12, K = 5,
-    6188 ADOs) and compute-heavy hierarchies whose per-ADO work is ns^3 (GUE H, Q = diag, Drude npsd = 3 -> K = 4):
-    ns = 64, L = 6 (210 ADOs of 64 KB), ns = 128 and 192, L = 4 (70 ADOs of 256 / 576 KB) -- the tiled MFMA stage
-    kernel."""
+    6188 ADOs) and two compute-heavy hierarchies whose per-ADO work is ns^3 (_band_case: ns = 96 and 128, L = 8, K = 4:
+    495 ADOs, 70 / 124 MB) -- the tiled MFMA stage kernel.  tools/deom_band_model.py runs the model on others."""
     import sympy as sp
     from pyqed_amd.deom import Bath, DEOMSolver
     w = sp.symbols(r"\omega", real=True)
@@ -899,15 +914,8 @@ def _deom_banded_cases():
     bath = Bath([2 * 0.5 * 1.0 * w / (1.0 + w ** 2)], w, [1.0], [4], [0] * 5)
     cases = [("spin_boson_L12_K5 (configs[3])", DEOMSolver(sz + sx, None, bath, np.array([sx]), None, None, None, 12),
               r0, 0.002)]
-    bath3 = Bath([2 * 0.3 * w / (1.0 + w ** 2)], w, [1.0], [3], [0] * 4)
-    for ns, L in ((64, 6), (128, 4), (192, 4)):
-        rng = np.random.default_rng(ns)
-        a = rng.standard_normal((ns, ns)) + 1j * rng.standard_normal((ns, ns))
-        H = (a + a.conj().T) / 2 / np.sqrt(ns)
-        Q = np.diag(np.linspace(-1, 1, ns)).astype(complex)
-        rb = np.zeros((ns, ns), complex)
-        rb[0, 0] = 1
-        cases.append((f"ns{ns}_L{L}_K4", DEOMSolver(H, None, bath3, np.array([Q]), None, None, None, L), rb, 0.002))
+    for ns, L in ((96, 8), (128, 8)):
+        cases.append(_band_case(ns, L))
     return cases
 
 
@@ -959,7 +967,7 @@ def deom_band_model(dev, sh, single_ms, reps=24):
     return out
 
 
-def bench_deom_banded(dev, world, rank, steps=40):
+def bench_deom_banded(dev, world, rank, steps=40, cases=None):
     """ONE hierarchy tier-banded over the ranks (BASELINE.json configs[3]: "ADOs sharded over
     8xMI355X via xGMI"): one band per rank, one RCCL all-gather of the bands' export rows per RK4 stage
     (deom_shard.CollectiveExchange), HIP stage kernels per band.  World > 1: timed `steps` RK4 steps of
@@ -971,7 +979,7 @@ def bench_deom_banded(dev, world, rank, steps=40):
     import torch.distributed as dist
     from pyqed_amd.deom_shard import ShardedDEOM, run_bands
     out = {}
-    for name, sol, rho0, dt in _deom_banded_cases():
+    for name, sol, rho0, dt in (cases if cases is not None else _deom_banded_cases()):
         sol.check_()
         sol.init_()
         single = None
@@ -979,7 +987,10 @@ def bench_deom_banded(dev, world, rank, steps=40):
             Qm = np.asarray(sol.coupling, dtype=complex).reshape(-1, sol.nsys, sol.nsys)
             single = 1e3 / _deom_event_rate(dev, sol, sol.bath, np.asarray(sol.system, complex), Qm, 1, steps, dt)
         nb = world if world > 1 else 8
-        sh = ShardedDEOM(sol, nbands=nb, loopback=world == 1, device=dev, exchange="allgather")
+        # compute-heavy hierarchies exchange point to point (each peer's rows over its own link: the model's p2p
+        # form); the small-state bench hierarchy with one all-gather per stage
+        exch = "p2p" if sol.nsys >= 32 else "allgather"
+        sh = ShardedDEOM(sol, nbands=nb, loopback=world == 1, device=dev, exchange=exch)
         fs, fc = sh.setup(dt, steps)
         run_bands(sh.bands, sh.exchange, rho0, dt, 2, fs, fc)          # warm-up
         torch.cuda.synchronize(dev)
@@ -1000,9 +1011,12 @@ def bench_deom_banded(dev, world, rank, steps=40):
                "max_halo_over_owned": round(max(h / o for h, o in zip(halo, own)), 3),
                "state_bytes": sol.nmax * ns * ns * 16}
         if world > 1:
-            ent.update({"exchange": "RCCL all-gather per stage", "ms_per_step": round(el / steps * 1e3, 4),
-                        "steps": steps, "ado_steps_per_s": round(sol.nmax * steps / el, 1),
-                        "allgather_bytes_per_stage": sh.exchange.bytes_per_exchange})
+            ent.update({"exchange": ("RCCL all-gather per stage" if exch == "allgather" else
+                                     "RCCL point-to-point halo exchange per stage"),
+                        "ms_per_step": round(el / steps * 1e3, 4),
+                        "steps": steps, "ado_steps_per_s": round(sol.nmax * steps / el, 1)})
+            if exch == "allgather":
+                ent["allgather_bytes_per_stage"] = sh.exchange.bytes_per_exchange
             if single is not None:
                 ent["one_gpu_unbanded_ms_per_step"] = round(single, 4)
         else:
