@@ -443,9 +443,11 @@ struct SplitPlan {
   int bt, S;
 };
 SplitPlan split_plan(int Mp, int Np, int tiles) {
+  // 64-blocks: two workgroups per CU (69.6 KB of LDS each), 512 in all (8,192-member shard: 0.169-0.170 vs 0.172-0.173
+  // ms per grid at 256; 384 and 768 slower, profiles/r05/2des/wg64_splits_ab.txt); 128-blocks hold one per CU
   auto splits = [&](int bt) {
     const int blocks = (Mp / bt) * (Np / bt);
-    return std::max(1, std::min(ceil_div(256, blocks), std::max(1, tiles / 4)));
+    return std::max(1, std::min(ceil_div(bt == 64 ? 512 : 256, blocks), std::max(1, tiles / 4)));
   };
   const int S128 = splits(128);
   const bool small = (Mp / 128) * (Np / 128) * S128 < 256 || tiles / S128 < 32;

@@ -122,6 +122,29 @@ def test_2des_256_ensemble_path_matches_reference(j):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("j", [0, 37])
+def test_2des_bench_size_gemm128_path_matches_reference(j):
+    """the benched instantiation itself (the 128-block split-K GEMM with the generated A operand,
+    ens_gemm_kernel<128, xtab>, which only ensembles of >= 32k eigen-index columns reach) pinned to the reference: the
+    fixture's three members, each repeated 21,846 times (65,538 members, the bench's size), summed by the GPU and
+    divided by the repeat count, equal the sum of the reference's slices."""
+    from pyqed_amd.response import ensemble_factors, response2d_ensemble
+    from conftest import took
+    g = load_golden("corr4_2des_256")
+    tau = g["tau"]
+    lam, U1, U2, ops, rho0 = _two_des_members(g)
+    alpha, Mt, beta = ensemble_factors(lam, U1, U2, ops, rho0.flatten(), tau[j])
+    R = 21846
+    rep = lambda a: np.tile(a, (R,) + (1,) * (a.ndim - 1))
+    took("")
+    S = response2d_ensemble(rep(lam), rep(alpha), rep(Mt), rep(beta), tau, tau).cpu().numpy()
+    hit, paths = took("ens_gemm128_xtab")
+    assert hit, paths
+    tot = sum(g[f"m{m}_j{j}"] for m in range(len(g["E"])))
+    assert relerr(S / R, tot) < TOL
+
+
+@pytest.mark.gpu
 def test_spo2_256_matches_reference():
     """Config d2 (256 x 256 x 2, the bench potential, dt = 0.05): 20 Strang steps of SPO2.run (wpd.py:692-758)
     against the reference's final state and per-output populations."""
