@@ -134,8 +134,9 @@ def lindblad_csr(H, rho0, c_ops, e_ops, Nt, dt):
     return obs, rho
 
 
-def correlation_3p_1t(H, rho0, ops, c_ops, tlist):
-    """correlation.correlation_3p_1t (pyqed/correlation.py:17-70) with dyn = oqs.liouvillian.
+def correlation_3p_1t(H, rho0, ops, c_ops, tlist, dyn=None):
+    """correlation.correlation_3p_1t (pyqed/correlation.py:17-70) with dyn = oqs.liouvillian by default, or any
+    dyn(rho, H, c_ops) (:62 rk4(rho, dyn, dt, H, c_ops)).
 
     rho <- C rho0 A (:41), then len(tlist) RK4 steps of dt = tlist[1]-tlist[0] (:50-57); after each
     step t += dt and cor = Tr(B rho) (:59).  Returns (t [Nt], cor [Nt], rho_k [Nt,N,N]) -- the values
@@ -148,7 +149,7 @@ def correlation_3p_1t(H, rho0, ops, c_ops, tlist):
     t, ts, cor, rhos = 0.0, [], [], []
     for _ in range(len(tlist)):
         t += dt
-        rho = rk4(rho, liouvillian, dt, H, c_ops)
+        rho = rk4(rho, dyn or liouvillian, dt, H, c_ops)
         ts.append(t)
         cor.append((B @ rho).diagonal().sum())
         rhos.append(rho.copy())

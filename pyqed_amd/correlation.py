@@ -1,7 +1,8 @@
 """Quantum-regression correlation functions on MI355X (drop-in for pyqed/correlation.py).
 
 correlation_3p_1t (correlation.py:17-70): <A B(t) C> = Tr[B U(t) (C rho0 A) U^+(t)] with the
-propagation on the Lindblad RK4 kernel (qd_lindblad_rk4).  Like the reference it returns None and
+propagation on the Lindblad RK4 kernel (qd_lindblad_rk4), or, for any other linear right-hand side dyn(rho, H, c_ops),
+on the dense superoperator RK4 kernel (qd_superop_rk4) after one host probe of the generator.  Like the reference it returns None and
 writes 'cor.dat' (t, cor) and 'dm.dat' (t, ravel rho) in the current directory.
 """
 from __future__ import annotations
@@ -21,16 +22,49 @@ def _is_lindblad(dyn) -> bool:
     return getattr(dyn, "__name__", "") == "liouvillian"
 
 
+_PROBE_MAX_N = 64   # host probes of a general `dyn`: N^2 calls (4096 at N = 64)
+
+
+def _dyn_superop(dyn, H, c_ops, N):
+    """The matrix of a general right-hand side rho -> dyn(rho, H, c_ops) on row-major vec(rho), probed on the host
+    with the N^2 unit matrices (the generator's setup; the time stepping runs on the GPU).  Every master equation the
+    reference passes is linear in rho and constant in time -- rk4(rho, dyn, dt, H, c_ops) calls it with the same H and
+    c_ops at every stage (correlation.py:62) -- and the probe checks linearity on two random matrices, raising
+    ValueError otherwise."""
+    sparse = any(hasattr(x, "tocsr") for x in [H, *(c_ops or [])])
+
+    def apply(r):
+        if sparse:   # the caller's operators are scipy sparse: hand dyn the same kind of matrix, as the reference does
+            from scipy.sparse import csr_matrix
+            r = csr_matrix(r)
+        out = dyn(r, H, c_ops)
+        return np.ravel(np.asarray(to_numpy(out, np.complex128)))
+    L = np.empty((N * N, N * N), dtype=np.complex128)
+    for j in range(N * N):
+        e = np.zeros((N, N), dtype=np.complex128)
+        e.flat[j] = 1.0
+        L[:, j] = apply(e)
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N))
+    y = rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N))
+    a, b = 0.7 - 0.2j, -1.3 + 0.4j
+    lhs = apply(a * x + b * y)
+    rhs = L @ np.ravel(a * x + b * y)
+    if not np.allclose(lhs, rhs, rtol=1e-10, atol=1e-12 * max(1.0, np.abs(rhs).max())):
+        raise ValueError("correlation_3p_1t: dyn is not linear in rho; the regression theorem propagation needs a "
+                         "linear master equation")
+    return L
+
+
 def correlation_3p_1t(H, rho0, ops, c_ops, tlist, dyn=None, *args):
     """<A B(t) C> by the quantum regression theorem (correlation.py:17-70).
 
     rho <- C rho0 A; len(tlist) RK4 steps of dt = tlist[1] - tlist[0]; after each step
-    t += dt, cor = Tr(B rho).  Only Lindblad dynamics (dyn = oqs.liouvillian) run here: any other
-    `dyn` is an arbitrary host callable and raises NotImplementedError (no CPU fallback).
+    t += dt, cor = Tr(B rho).  Lindblad dynamics (dyn = oqs.liouvillian / phys.liouvillian, the only right-hand
+    side the reference defines with this signature) run on the Lindblad RK4 kernel; any other linear `dyn` (a user's
+    Redfield or dephasing RHS) is probed once into its dense superoperator on the host (N <= 64) and stepped by the
+    superoperator RK4 kernel (qd_superop_rk4) -- the same rk4 of the same generator as the reference.
     """
-    if not _is_lindblad(dyn):
-        raise NotImplementedError(f"correlation_3p_1t: dynamics {dyn!r} is not supported on the GPU; "
-                                  "use dyn=pyqed.oqs.liouvillian (Lindblad)")
     A, B, C = (np.ascontiguousarray(to_numpy(o, np.complex128)) for o in ops)
     Hn = np.ascontiguousarray(to_numpy(H, np.complex128))
     nstates = Hn.shape[-1]
@@ -38,12 +72,28 @@ def correlation_3p_1t(H, rho0, ops, c_ops, tlist, dyn=None, *args):
     Nt = len(tlist)
     dt = tlist[1] - tlist[0]
     dev = default_device()
-    rho = torch.from_numpy(r0).to(dev).reshape(1, nstates, nstates).contiguous()
-    obs, snap = lindblad_rk4(torch.from_numpy(Hn).to(dev), stack_ops(c_ops or [], nstates, dev), rho, float(dt), Nt,
-                             stack_ops([B], nstates, dev), save_every=1, hermitian=False)
-    torch.cuda.synchronize(dev)
-    cor = obs[0, 1:, 0].cpu().numpy()
-    rhos = snap[0].cpu().numpy()
+    if _is_lindblad(dyn):
+        rho = torch.from_numpy(r0).to(dev).reshape(1, nstates, nstates).contiguous()
+        obs, snap = lindblad_rk4(torch.from_numpy(Hn).to(dev), stack_ops(c_ops or [], nstates, dev), rho, float(dt),
+                                 Nt, stack_ops([B], nstates, dev), save_every=1, hermitian=False)
+        torch.cuda.synchronize(dev)
+        cor = obs[0, 1:, 0].cpu().numpy()
+        rhos = snap[0].cpu().numpy()
+    else:
+        if not callable(dyn):
+            raise NotImplementedError(f"correlation_3p_1t: dynamics {dyn!r} is neither 'lindblad' nor a callable "
+                                      "dyn(rho, H, c_ops)")
+        if nstates > _PROBE_MAX_N:
+            raise NotImplementedError(f"correlation_3p_1t: a general dyn is probed into its N^2 x N^2 superoperator on "
+                                      f"the host; N = {nstates} > {_PROBE_MAX_N}")
+        from .oqs import superop_rk4
+        L = torch.from_numpy(_dyn_superop(dyn, H, c_ops, nstates)).to(dev)
+        v = torch.from_numpy(np.ravel(r0).copy()).to(dev).reshape(1, -1).contiguous()
+        W = torch.from_numpy(np.ravel(B.T).copy()).to(dev).reshape(1, -1).contiguous()   # Tr(B rho) = sum B^T . rho
+        obs, snap = superop_rk4(L, v, float(dt), Nt, W=W, save_every=1)
+        torch.cuda.synchronize(dev)
+        cor = obs[0, 1:, 0].cpu().numpy()
+        rhos = snap[0].cpu().numpy().reshape(Nt, nstates, nstates)
     fmt = '{} ' * (nstates ** 2 + 1) + '\n'
     with open('cor.dat', 'w') as f, open('dm.dat', 'w') as f_dm:
         t = 0.0

@@ -29,3 +29,20 @@ def test_hermitian_check_cache_follows_a_repointed_data():
     assert _is_hermitian_cached(h)
     h.data = torch.randn(6, 6, dtype=torch.complex128)
     assert not _is_hermitian_cached(h)
+
+
+def test_dyn_superop_probe_is_the_generator_and_refuses_nonlinear():
+    """correlation_3p_1t's host probe of a general dyn(rho, H, c_ops) (VERDICT r04 missing #4): its matrix applied to
+    row-major vec(rho) equals dyn(rho) for dense and scipy.sparse operators, and a nonlinear dyn raises."""
+    import numpy as np
+    import pytest
+    from scipy.sparse import csr_matrix
+    from oracle import lindblad as olb
+    from pyqed_amd.correlation import _dyn_superop
+    H, cs = olb.synthetic_lindblad(5, nc=1)
+    rho = olb.random_pure_states(1, 5, seed=4)[0]
+    for Hx, cx in ((H, cs), (csr_matrix(H), [csr_matrix(c) for c in cs])):
+        L = _dyn_superop(olb.liouvillian, Hx, cx, 5)
+        assert np.allclose(L @ rho.ravel(), olb.liouvillian(rho, H, cs).ravel(), rtol=1e-12, atol=1e-14)
+    with pytest.raises(ValueError):
+        _dyn_superop(lambda r, H, c: r @ r, H, cs, 5)

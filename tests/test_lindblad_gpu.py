@@ -274,8 +274,35 @@ def test_correlation_3p_1t_matches_reference(tmp_path, monkeypatch):
     td, dm = _parse_dat(open(tmp_path / "dm.dat").read())
     _, dmr = _parse_dat(g["dmdat"])
     assert np.array_equal(td, tr) and relerr(dm, dmr) < TOL
-    with pytest.raises(NotImplementedError):
-        correlation_3p_1t(g["H"], g["rho0"], ops, [], g["tlist"], lambda r, H, c: r)
+    with pytest.raises(ValueError):   # a nonlinear right-hand side is refused
+        correlation_3p_1t(g["H"], g["rho0"], ops, [], g["tlist"], lambda r, H, c: r @ r)
+
+
+def test_correlation_3p_1t_general_dyn_matches_oracle(tmp_path, monkeypatch):
+    """VERDICT r04 missing #4: a right-hand side other than the Lindblad one -- here a user's pure-dephasing master
+    equation -i[H, rho] - g (rho - diag rho) written in scipy.sparse like the reference's -- is probed once into its
+    superoperator and stepped on the superoperator RK4 kernel: cor.dat / dm.dat equal the oracle's rk4 of the same dyn
+    (correlation.py:50-66)."""
+    from scipy.sparse import csr_matrix, diags
+    from oracle import lindblad as olb
+    from pyqed_amd.correlation import correlation_3p_1t
+    from test_oracle_golden import _parse_dat
+    g = load_golden("corr3p_1t")
+    monkeypatch.chdir(tmp_path)
+    gam = 0.3
+
+    def dephasing(rho, H, c_ops):
+        d = diags(rho.diagonal()) if hasattr(rho, "tocsr") else np.diag(np.diag(rho))
+        return -1j * (H @ rho - rho @ H) - gam * (rho - d)
+
+    ops = [csr_matrix(g[k]) for k in ("A", "B", "Cop")]
+    correlation_3p_1t(csr_matrix(g["H"]), csr_matrix(g["rho0"]), ops, [], g["tlist"], dephasing)
+    ts, cor, rhos = olb.correlation_3p_1t(g["H"], g["rho0"], [g[k] for k in ("A", "B", "Cop")], [], g["tlist"],
+                                          dyn=dephasing)
+    t, c = _parse_dat(open(tmp_path / "cor.dat").read())
+    assert np.allclose(t, ts) and relerr(c, cor) < TOL
+    td, dm = _parse_dat(open(tmp_path / "dm.dat").read())
+    assert relerr(dm, rhos.reshape(len(ts), -1)) < TOL
 
 
 @pytest.mark.parametrize("N,nc,B", [(128, 1, 1), (96, 2, 3), (64, 1, 2), (256, 1, 1), (128, 1, 24), (256, 2, 8)])
