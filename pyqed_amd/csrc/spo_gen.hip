@@ -576,15 +576,16 @@ __global__ __launch_bounds__(256) void spo1d_gen_kernel(Fft p, c128* psi, const 
 // directly, by scaling and squaring a degree-18 Taylor polynomial (||X|| <= 1/2 after scaling: truncation
 // < 1e-22), so no eigenvectors are needed on the device.  exp(-i V dt) = exp(-i V dt/2)^2 (one more product).
 // herm: the Hermitian matrix LAPACK's eigh sees (lower triangle, real diagonal); otherwise the full matrix.
-// One workgroup per grid point (grid-stride), lane e = i ns + j owns element (i, j); products through LDS.
-template <bool CPLX>
+// One workgroup per grid point (grid-stride), lane e = i ns + j owns element (i, j).  GLB = false: the four ns x ns
+// matrices live in LDS (ns <= 50: 160 KB at ns = 50); GLB = true (50 < ns <= 256): in a per-workgroup slice of a
+// global scratch buffer (64 ns^2 bytes, L2-resident up to ns ~ 90), with the same code -- the workgroup barrier
+// orders its global stores and loads as it does LDS ones.
+template <bool CPLX, bool GLB>
 __global__ __launch_bounds__(1024) void spo_expm_kernel(const void* v_, int herm, long npts, int ns, double dt,
-                                                        c128* expV, c128* expVh) {
-  // ns <= 50: four ns x ns matrices in LDS (160 KB at ns = 50); thread t owns elements t, t + blockDim, ... (one each up
-  // to ns = 32, where blockDim = ns^2 rounded up to 64)
+                                                        c128* expV, c128* expVh, c128* work) {
   extern __shared__ c128 sm[];
   const int ns2 = ns * ns;
-  c128* X = sm;
+  c128* X = GLB ? work + (size_t)blockIdx.x * 4 * ns2 : sm;
   c128* T = X + ns2;
   c128* S = T + ns2;
   c128* W = S + ns2;
@@ -594,24 +595,13 @@ __global__ __launch_bounds__(1024) void spo_expm_kernel(const void* v_, int herm
     const size_t o = (size_t)p * ns2 + (size_t)r * ns + c;
     return CPLX ? ((const c128*)v_)[o] : cmk(((const double*)v_)[o], 0.0);
   };
-  auto matmul = [&](const c128* A, const c128* B, c128* C, double scale) {   // C = scale A B
+  auto matmul = [&](const c128* A, const c128* B, c128* C, double scale) {   // C = scale A B (C distinct from A, B)
     __syncthreads();
-    constexpr int PER = 3;   // elements per thread: ceil(2500 / 1024)
-    c128 acc[PER];
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      const int e = t0 + q * nt;
-      acc[q] = cmk(0.0, 0.0);
-      if (e < ns2) {
-        const int i = e / ns, j = e - i * ns;
-        for (int l = 0; l < ns; ++l) acc[q] = cadd(acc[q], cmul(A[i * ns + l], B[l * ns + j]));
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      const int e = t0 + q * nt;
-      if (e < ns2) C[e] = cscale(acc[q], scale);
+    for (int e = t0; e < ns2; e += nt) {
+      const int i = e / ns, j = e - i * ns;
+      c128 acc = cmk(0.0, 0.0);
+      for (int l = 0; l < ns; ++l) acc = cadd(acc, cmul(A[i * ns + l], B[l * ns + j]));
+      C[e] = cscale(acc, scale);
     }
     __syncthreads();
   };
@@ -1155,21 +1145,42 @@ int spo_generic_run(c128* psi, const c128* expVh, const c128* expV, const c128* 
 #endif
 }
 
-// exp(-i V dt/2), exp(-i V dt) per point for any ns <= 50 (spo_expm_kernel).
+// exp(-i V dt/2), exp(-i V dt) per point for any ns <= SPO_EXPM_MAX_NS (spo_expm_kernel): LDS-resident matrices up to
+// ns = 50, a global scratch slice per workgroup above (grid bounded by a 512 MB slab).
 int spo_expm_run(const void* v, int v_complex, int herm, long npts, int ns, double dt, c128* expV, c128* expVh,
                  hipStream_t st) {
   using namespace spog;
+  if (npts == 0) return QD_OK;
   const int threads = std::min(1024, std::max(64, ((ns * ns + 63) / 64) * 64));
-  const size_t lds = (size_t)4 * ns * ns * sizeof(c128);
-  (void)hipFuncSetAttribute((const void*)spo_expm_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(LDS_MAX - 64));
-  (void)hipFuncSetAttribute((const void*)spo_expm_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(LDS_MAX - 64));
-  const int grid = (int)std::min<long>(npts, 16384);
-  if (v_complex)
-    hipLaunchKernelGGL(spo_expm_kernel<true>, dim3(grid), dim3(threads), lds, st, v, herm, npts, ns, dt, expV, expVh);
-  else
-    hipLaunchKernelGGL(spo_expm_kernel<false>, dim3(grid), dim3(threads), lds, st, v, herm, npts, ns, dt, expV, expVh);
+  if (ns <= 50) {
+    const size_t lds = (size_t)4 * ns * ns * sizeof(c128);
+    (void)hipFuncSetAttribute((const void*)spo_expm_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(LDS_MAX - 64));
+    (void)hipFuncSetAttribute((const void*)spo_expm_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(LDS_MAX - 64));
+    const int grid = (int)std::min<long>(npts, 16384);
+    if (v_complex)
+      hipLaunchKernelGGL((spo_expm_kernel<true, false>), dim3(grid), dim3(threads), lds, st, v, herm, npts, ns, dt,
+                         expV, expVh, nullptr);
+    else
+      hipLaunchKernelGGL((spo_expm_kernel<false, false>), dim3(grid), dim3(threads), lds, st, v, herm, npts, ns, dt,
+                         expV, expVh, nullptr);
+    note_path("spo_expm_lds");
+  } else {
+    const size_t per = (size_t)4 * ns * ns * sizeof(c128);
+    const int grid = (int)std::max<long>(1, std::min<long>({npts, 1024, (long)((512ull << 20) / per)}));
+    WsScope wss_(st);
+    void* work = nullptr;
+    const int rc = workspace(WS_SPO, per * grid, &work, st);
+    if (rc) return rc;
+    if (v_complex)
+      hipLaunchKernelGGL((spo_expm_kernel<true, true>), dim3(grid), dim3(threads), 0, st, v, herm, npts, ns, dt, expV,
+                         expVh, (c128*)work);
+    else
+      hipLaunchKernelGGL((spo_expm_kernel<false, true>), dim3(grid), dim3(threads), 0, st, v, herm, npts, ns, dt,
+                         expV, expVh, (c128*)work);
+    note_path("spo_expm_global");
+  }
   QD_HIP(hipGetLastError());
   return QD_OK;
 }

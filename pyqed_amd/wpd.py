@@ -1,7 +1,8 @@
 """Split-operator wavepacket dynamics on MI355X (drop-in for pyqed/wpd.py SPO, SPO2).
 
 Setup: grids and exp_K on the host like the reference's build (wpd.py:217-223, 496-625);
-the per-point propagators exp(-i V dt), exp(-i V dt/2) on the device (qd_spo_expv, ns <= 2).
+the per-point propagators exp(-i V dt), exp(-i V dt/2) on the device (qd_spo_expv: closed form for
+ns <= 2, a matrix exponential up to ns = 256).
 Every propagation step runs in libqdyn (qd_spo1d_run / qd_spo2_run_ex / qd_spo3_run).
 """
 from __future__ import annotations
@@ -13,6 +14,8 @@ from scipy.fftpack import fftfreq
 from . import _lib
 from ._util import default_device
 from .mol import Result
+
+DEVICE_EXPM_MAX_NS = 256   # qd_spo_expv / qd_spo_expm: work matrices in LDS to ns = 50, in device scratch above
 
 pi = np.pi
 
@@ -135,9 +138,9 @@ class _PointPropagators:
     The reference's build (wpd.py:585-623, SPO3 :1290-1330) loops over grid points calling eigh and
     forming U e^{-i w tau} U^+.  qd_spo_expv evaluates the same point propagators on the GPU (LAPACK
     conventions: lower triangle, real diagonal): in closed form for ns <= 2, as a scaling-and-squaring
-    matrix exponential for 2 < ns <= 50; they stay on the device for the run and are copied to the
+    matrix exponential for 2 < ns <= 256; they stay on the device for the run and are copied to the
     host only when exp_V / exp_V_half are read.  The eigen data (d2a = U, apes = w) are host eigh
-    results computed on first access.  ns > 50 builds on the host with a vectorised eigh.
+    results computed on first access.  ns > 256 builds on the host with a vectorised eigh.
     """
     _eV_dev = _eVh_dev = None
     _exp_V_host = _exp_V_half_host = None
@@ -196,7 +199,7 @@ class _PointPropagators:
         v = self._pot()
         ns = v.shape[-1]
         _check_finite(v)
-        if ns > 50:   # beyond the device exponential's LDS (four ns x ns matrices, 160 KB): host eigh, as the reference
+        if ns > DEVICE_EXPM_MAX_NS:   # beyond the device exponential's cap (qd_spo_expv): host eigh, as the reference
             w, u = self._host_eig()
             ud = np.conj(np.swapaxes(u, -1, -2))
             self.exp_V = (u * np.exp(-1j * w * dt)[..., None, :]) @ ud
@@ -406,7 +409,7 @@ class SPO2NH(SPO2):
 
     def build(self, dt):
         """wpd.py:960-985.  exp_V = U_R e^{-i w dt} U_R^-1 is the matrix exponential exp(-i V dt); it is evaluated on
-        the GPU (qd_spo_expm, scaling and squaring, no eigenvectors) for ns <= 50.  The right eigenvectors and their
+        the GPU (qd_spo_expm, scaling and squaring, no eigenvectors) for ns <= 256.  The right eigenvectors and their
         overlap (right_eigenstates, ovlp_rr; nonherm.eig order, eigenvalues by argsort) are host eig results made
         on first access (position() reads ovlp_rr)."""
         nx, ny = self.nx, self.ny
@@ -417,7 +420,7 @@ class SPO2NH(SPO2):
         self._ur = self._ovlp = None
         ns = v.shape[-1]
         _check_finite(v)
-        if ns > 50:
+        if ns > DEVICE_EXPM_MAX_NS:
             ur = self.right_eigenstates
             w = self._w
             ul = np.linalg.inv(ur)
