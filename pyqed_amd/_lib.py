@@ -75,6 +75,8 @@ SIGNATURES = {
                                    c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_double, c_int,
                                    c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "qd_deom_apply": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                               c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_double, c_int, c_void_p]),
     "qd_deom_stage": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                               c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_double,
                               c_double, c_double, c_double, c_int, c_double, c_void_p, c_int, c_int, c_void_p]),

@@ -1293,6 +1293,57 @@ extern "C" int qd_deom_stage(qd_c128* rho, const qd_c128* xin, qd_c128* xout, qd
   return deom_launch_stage(p, (hipStream_t)stream);
 }
 
+// y = alpha P x for B ADO vectors (the generator of generate_dot_element, heom/deom.py:641-664, as an operator; the
+// Krylov form of DEOMSolver.correlation_4op_3t applies it and its transpose, pyqed_amd/deom_krylov.py).  One stage
+// launch of the stage kernels: Horner stage 2 (s_3 = rho + dt / 2 L s_2) with rho = 0 and dt = 2 alpha, so the
+// coefficient is alpha exactly and the kernel reads its input only from xin.
+extern "C" int qd_deom_apply(const qd_c128* x, qd_c128* y, int B, int nmax, int K, int ns, const int32_t* minus,
+                             const int32_t* plus, const qd_c128* coef, const qd_c128* damp, const int32_t* mode,
+                             int nmod, const qd_c128* H, const qd_c128* Q, double alpha, int ado_major, void* stream) {
+  QD_CHECK_ARG(x && y && minus && plus && coef && damp && mode && H && Q, "qd_deom_apply: null pointer");
+  QD_CHECK_ARG(x != y, "qd_deom_apply: x and y must not alias");
+  QD_CHECK_ARG(B >= 1 && nmax >= 1 && K >= 1 && ns >= 1 && nmod >= 1, "qd_deom_apply: bad sizes B=%d nmax=%d K=%d ns=%d",
+               B, nmax, K, ns);
+  hipStream_t st = (hipStream_t)stream;
+  WsScope wss_(st);
+  const size_t tot = (size_t)B * nmax * ns * ns;
+  void* z = nullptr;
+  int rc = workspace(WS_DEOM, tot * sizeof(c128), &z, st);
+  if (rc) return rc;
+  QD_HIP(hipMemsetAsync(z, 0, tot * sizeof(c128), st));
+  DeomParams p{};
+  p.rho = (const c128*)z;
+  p.rho_out = (c128*)z;
+  p.xin = (const c128*)x;
+  p.xout = (c128*)y;
+  p.acc = nullptr;
+  p.minus = minus;
+  p.plus = plus;
+  p.coef = (const c128*)coef;
+  p.damp = (const c128*)damp;
+  p.mode = mode;
+  p.H = (const c128*)H;
+  p.Hdip = nullptr;
+  p.Q = (const c128*)Q;
+  p.Qdip = nullptr;
+  p.fs = cmk(0.0, 0.0);
+  p.fc = cmk(0.0, 0.0);
+  p.snap = nullptr;
+  p.B = B;
+  p.nmax = nmax;
+  p.K = K;
+  p.ns = ns;
+  p.nmod = nmod;
+  p.stage = 2;
+  p.step = 1;   // not a run's first stage: no dispatch notes from the launcher
+  p.nsteps = 2;
+  p.dt = 2.0 * alpha;
+  p.bminor = ado_major ? 1 : 0;
+  p.horner = 1;
+  note_path("deom_apply");
+  return deom_launch_stage(p, st);
+}
+
 namespace {
 // Bounds-checked (the round-3 kernel trusted idx): a row index outside [0, nsrc) reads
 // nothing, writes NaN and raises *bad, which the host entry point reports.

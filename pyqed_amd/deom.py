@@ -302,6 +302,9 @@ def _action_block(A, lcr):
 
 # --------------------------------------------------------------------------- solver
 BANDS_MAX = 256   # one workgroup per CU at most (the bands must be co-resident)
+# correlation_4op_3t(if_full=True) runs the Krylov form (deom_krylov.py) from this ADO-space dimension nmax ns^2 on:
+# the host eig of P is O(n^3) (n = 1024: seconds; the bench hierarchy's 24,752: beyond the reference itself)
+KRYLOV_MIN_DIM = 1024
 
 
 class _BandTables:
@@ -358,6 +361,10 @@ class DEOMSolver:
         self.layout = None
         self.banded = None
         self.bands = None
+        # correlation_4op_3t's method: None = the eigen form (as the reference) below KRYLOV_MIN_DIM, the Krylov form
+        # above; "eig" / "krylov" force one (last_corr4 records what ran)
+        self.corr4_method = None
+        self.last_corr4 = None
 
     def set_hierarchy(self, lmax):
         self.lmax = lmax
@@ -575,12 +582,29 @@ class DEOMSolver:
         """heom/deom.py:1127-1209: c_w[i, j] = Tr_sys[A1 V r(w_x_i) (V^-1 A2 V) e^{Delta T} (V^-1 A3 V)
         r(w_y_j) V^-1 A4 rho], r(w) = diag(1 / (-Delta - i w)).
 
-        Host (as the reference): P, eig + pinv, the O(n^3) basis changes.  GPU: the (w_x, w_y) grid,
-        which the reference evaluates with a matrix-vector trace per grid point, runs as two split-K
-        MFMA GEMMs (qd_resolvent_grid2d).  if_full=False keeps the eigenvalues with
-        min(Re) * cut_off_min < Re < max(Re) * cut_off_max; if_load / if_save use correlation_4op_3t.npz."""
+        Eigen form (as the reference; ADO dimension n = nmax ns^2 below KRYLOV_MIN_DIM, if_full=False, if_load,
+        if_save): host P, eig + pinv, the O(n^3) basis changes; the (w_x, w_y) grid, which the reference evaluates
+        with a matrix-vector trace per grid point, as two split-K MFMA GEMMs (qd_resolvent_grid2d).
+        if_full=False keeps the eigenvalues with min(Re) * cut_off_min < Re < max(Re) * cut_off_max; if_load /
+        if_save use correlation_4op_3t.npz.
+        Krylov form (if_full=True from n = KRYLOV_MIN_DIM, e.g. the bench hierarchy's 24,752 whose dense P the
+        reference cannot diagonalise): the same quantity u^T R(w_x) A2 e^{PT} A3 R(w_y) v with R(w) = (-P - i w)^-1
+        from multi-shift Krylov solves of P and P^T on the GPU stencil kernel (pyqed_amd/deom_krylov.py); agrees with
+        the eigen form to ~1e-12 (tests/test_deom_krylov_*.py).  self.corr4_method forces either."""
         import os
         import scipy.linalg as la
+        self.check_()
+        self.init_()
+        n = self.nmax * self.nsys ** 2
+        if self.corr4_method not in (None, "eig", "krylov"):
+            raise ValueError(f"DEOMSolver.corr4_method must be None, 'eig' or 'krylov', got {self.corr4_method!r}")
+        krylov_ok = if_full and not if_load and not if_save
+        if self.corr4_method == "krylov" and not krylov_ok:
+            raise ValueError("correlation_4op_3t: the Krylov form serves if_full=True without if_load / if_save "
+                             "(the eigen cut and the eigendecomposition cache need P's eigenvectors)")
+        if krylov_ok and (self.corr4_method == "krylov" or (self.corr4_method is None and n >= KRYLOV_MIN_DIM)):
+            return self._corr4_krylov(operator_a, operator_b, operator_c, operator_d, rho0, T, w_x, w_y, lcr)
+        self.last_corr4 = {"method": "eig", "n": n}
         if self.propgator is None:
             self.gen_generate_propgator()
         if if_load and os.path.exists('correlation_4op_3t.npz'):
@@ -623,3 +647,27 @@ class DEOMSolver:
                                                  wyt.data_ptr(), len(wy), out.data_ptr(), _lib.stream_ptr(dev))
         _lib.check(rc, "qd_resolvent_grid2d")
         return out.cpu().numpy()
+
+    def _corr4_krylov(self, operator_a, operator_b, operator_c, operator_d, rho0, T, w_x, w_y, lcr):
+        """correlation_4op_3t(if_full=True) as u^T R(w_x) A2 e^{PT} A3 R(w_y) v: multi-shift Krylov solves of P and
+        P^T and a Taylor-substep exponential, every generator application the DEOM stencil kernel (qd_deom_apply;
+        pyqed_amd/deom_krylov.py).  P is never formed: the bench hierarchy's would be 9.8 GB."""
+        from .deom_krylov import DeomOperator, corr4_krylov, transposed_tables
+        dev = default_device()
+        _lib.ensure_device(dev)
+        b = self.bath
+        ns = self.nsys
+        coef, damp = ado_coefficients(self.keys, np.asarray(b.etal), np.asarray(b.etar), np.asarray(b.etaa),
+                                      np.asarray(b.expn), self.lmax)
+        H = _thresh(np.asarray(self.system, dtype=complex))   # the P of generate_propgator (ado_liouvillian)
+        Q = np.asarray(self.coupling, dtype=complex).reshape(-1, ns, ns)
+        mode = np.asarray(b.mode)
+        op = DeomOperator(dev, self._minus, self._plus, coef, damp, mode, H, Q, ns)
+        mT, pT, cT = transposed_tables(self._minus, self._plus, coef)
+        opT = DeomOperator(dev, mT, pT, cT, damp, mode, H.T, np.swapaxes(Q, 1, 2), ns)
+        A1, A2, A3, A4 = (_action_block(o, c) for o, c in
+                          zip((operator_d, operator_c, operator_b, operator_a), (lcr[3], lcr[2], lcr[1], lcr[0])))
+        c, info = corr4_krylov(op, opT, A1, A2, A3, A4, rho0, float(T), w_x, w_y, self.nmax, ns)
+        info["n"] = self.nmax * ns * ns
+        self.last_corr4 = info
+        return c

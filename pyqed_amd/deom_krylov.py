@@ -1,0 +1,227 @@
+"""DEOMSolver.correlation_4op_3t without the eigendecomposition (heom/deom.py:1127-1209, if_full=True).
+
+The reference diagonalises the dense ADO Liouvillian P (n = nmax ns^2; 24,752 at the bench hierarchy, a 9.8 GB
+matrix whose eig the reference cannot run) and evaluates, for every (w_x, w_y),
+
+    c(w_x, w_y) = Tr_sys[ A1 V D(w_x) (V^-1 A2 V) e^{Delta T} (V^-1 A3 V) D(w_y) V^-1 A4 rho ],
+    D(w) = diag(1 / (-Delta - i w)),
+
+which is, for a diagonalisable P, exactly
+
+    c(w_x, w_y) = u^T R(w_x) A2 e^{P T} A3 R(w_y) v,    R(w) = (-P - i w)^-1,
+
+with u^T x = Tr_sys(A1 x_0) (the ADO-0 rows) and v = A4 rho in the ADO-0 rows.  Here:
+
+  * r(w_y) = R(w_y) v for every w_y from ONE Arnoldi basis of P started at v (Krylov spaces are shift
+    invariant: (-P - s) V_k = V_{k+1} (-H_k - s)), the small shifted Hessenberg systems solved per shift;
+  * l(w_x) = R(w_x)^T u likewise from one Arnoldi basis of P^T started at u;
+  * e^{P T} on the n_w vectors of the shorter side (or e^{P^T T} on the left ones) by Taylor substeps with
+    ||P tau|| <= 1 (degree 20, remainder < 1e-19 per substep);
+  * c = l(w_x)^T A2 e^{PT} A3 r(w_y): one complex GEMM.
+
+Every application of P or P^T is the DEOM stencil kernel (qd_deom_apply); P^T is the same operator form on
+transposed tables (transposed_tables).  Orthogonalisation (classical Gram-Schmidt twice) and the final products
+are device BLAS calls on device-resident bases; the host only solves the k x k shifted systems.  The Krylov
+residual of every shift is driven below `tol` relative to its solution norm.  Accuracy against the eigen form:
+tests/test_deom_krylov_gpu.py (1e-9 at the fixture hierarchies; the eigen form itself carries cond(V) eps).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+
+TAYLOR_DEGREE = 20   # terms per substep of e^{P tau}, ||P tau||_inf <= 1: remainder <= e / 21! < 2e-19
+
+
+def transposed_tables(minus, plus, coef):
+    """(minus', plus', coef') with ado_liouvillian(keys, minus', plus', coef', damp, H^T, Q^T) = P^T.
+
+    P's block from ADO n to its minus neighbour m = minus[n, k] is coef0 (Q (x) I) + coef1 (I (x) Q^T); transposed
+    it is coef0 (Q^T (x) I) + coef1 (I (x) Q), ADO m's link to its PLUS neighbour n: the same operator form with
+    Q -> Q^T, the roles of the two tables exchanged and the prefactors read at the other end of the link (the
+    commutator-form plus links likewise become minus links).  Checked against P.T in tests/test_deom_krylov_cpu.py."""
+    minus = np.asarray(minus)
+    plus = np.asarray(plus)
+    coef = np.asarray(coef)
+    cT = np.zeros_like(coef)
+    for k in range(minus.shape[1]):
+        h = plus[:, k] >= 0
+        cT[h, k, 0] = coef[plus[h, k], k, 0]
+        cT[h, k, 1] = coef[plus[h, k], k, 1]
+        h = minus[:, k] >= 0
+        cT[h, k, 2] = coef[minus[h, k], k, 2]
+    return plus.copy(), minus.copy(), cT
+
+
+def inf_norm_bound(minus, plus, coef, damp, H, Q, mode):
+    """An upper bound of ||P||_inf (max row sum of the dense generator), from the tables."""
+    H = np.asarray(H)
+    Q = np.asarray(Q).reshape(-1, H.shape[0], H.shape[0])
+    nH = np.abs(H).sum(1).max() + np.abs(H).sum(0).max()
+    qi = np.abs(Q).sum(2).max(1)   # ||Q_m||_inf
+    q1 = np.abs(Q).sum(1).max(1)   # ||Q_m||_1
+    mode = np.asarray(mode)
+    has_m = np.asarray(minus) >= 0
+    has_p = np.asarray(plus) >= 0
+    c = np.abs(np.asarray(coef))
+    rows = np.abs(np.asarray(damp)) + nH
+    rows = rows + (has_m * (c[..., 0] * qi[mode][None] + c[..., 1] * q1[mode][None])).sum(1)
+    rows = rows + (has_p * c[..., 2] * (qi + q1)[mode][None]).sum(1)
+    return float(rows.max())
+
+
+class DeomOperator:
+    """y = alpha P x (or P^T) on device vectors [B][nmax][ns][ns] through qd_deom_apply."""
+
+    def __init__(self, dev, minus, plus, coef, damp, mode, H, Q, ns):
+        i32 = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=np.int32))).to(dev)
+        c128 = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=complex))).to(dev)
+        self.dev, self.ns = dev, ns
+        self.nmax, self.K = np.asarray(minus).shape
+        self.tabs = (i32(minus), i32(plus), c128(coef), c128(damp), i32(mode))
+        self.H = c128(H)
+        self.Q = c128(np.asarray(Q).reshape(-1, ns, ns))
+        self.nmod = self.Q.shape[0]
+        self.n = self.nmax * ns * ns
+        self.norm = inf_norm_bound(minus, plus, coef, damp, H, Q, mode)
+
+    def apply(self, x, y, alpha=1.0):
+        """y <- alpha P x; x, y contiguous [B, n] (or [n]) complex128 on the device, not aliased."""
+        B = x.numel() // self.n
+        mi, pl, coef, damp, mode = self.tabs
+        with torch.cuda.device(self.dev):
+            rc = _lib.load().qd_deom_apply(x.data_ptr(), y.data_ptr(), B, self.nmax, self.K, self.ns, mi.data_ptr(),
+                                           pl.data_ptr(), coef.data_ptr(), damp.data_ptr(), mode.data_ptr(),
+                                           self.nmod, self.H.data_ptr(), self.Q.data_ptr(), float(alpha), 0,
+                                           _lib.stream_ptr(self.dev))
+        _lib.check(rc, "qd_deom_apply")
+        return y
+
+
+def _shift_solutions(Hk, beta, shifts):
+    """y(s) with (-H_k - s I) y = beta e_1 for every shift s (k x k upper Hessenberg H_k), on the host: one complex
+    Schur form H_k = Z T Z^H (unitary Z), then per shift the triangular system (-T - s) z = beta Z^H e_1 by back
+    substitution vectorised over the shifts (O(S k^2)), y = Z z."""
+    from scipy.linalg import schur
+    Tm, Z = schur(Hk, output="complex")
+    k = Tm.shape[0]
+    shifts = np.asarray(shifts, dtype=complex)
+    c = beta * np.conj(Z[0, :])
+    z = np.zeros((len(shifts), k), dtype=complex)
+    for i in range(k - 1, -1, -1):
+        acc = c[i] + z[:, i + 1:] @ Tm[i, i + 1:]
+        z[:, i] = acc / (-Tm[i, i] - shifts)
+    return z @ Z.T
+
+
+def shifted_krylov_solve(op, b, shifts, tol=1e-12, m_max=None, first_check=20, growth=1.3):
+    """x(s) = (-P - s)^-1 b for every s in `shifts` (complex array) from one Arnoldi basis of P.
+
+    Classical Gram-Schmidt with one re-orthogonalisation on device-resident basis vectors; at checkpoints k (20,
+    then x1.3) the shifted k x k systems are solved on the host and the Krylov residual |h_{k+1,k} y_k(s)| of every
+    shift compared with tol ||y(s)||.  Returns (X [S, n] on the device, k)."""
+    n = op.n
+    if m_max is None:   # basis memory capped at ~8 GB
+        m_max = int(max(50, min(4000, (8 << 30) // (16 * n) - 2)))
+    dev = op.dev
+    V = torch.empty((m_max + 1, n), dtype=torch.complex128, device=dev)
+    Hd = torch.zeros((m_max + 1, m_max), dtype=torch.complex128, device=dev)
+    W = torch.empty(n, dtype=torch.complex128, device=dev)
+    beta = float(torch.linalg.vector_norm(b))
+    if beta == 0.0:
+        return torch.zeros((len(shifts), n), dtype=torch.complex128, device=dev), 0
+    V[0] = b / beta
+    shifts = np.asarray(shifts, dtype=complex)
+    check = first_check
+    k_done = None
+    for j in range(m_max):
+        op.apply(V[j], W)
+        Vj = V[:j + 1]
+        h = torch.mv(Vj, W.conj()).conj()
+        W -= torch.mv(Vj.transpose(0, 1), h)
+        h2 = torch.mv(Vj, W.conj()).conj()
+        W -= torch.mv(Vj.transpose(0, 1), h2)
+        h += h2
+        nrm = torch.linalg.vector_norm(W)
+        Hd[:j + 1, j] = h
+        Hd[j + 1, j] = nrm
+        V[j + 1] = W / nrm
+        k = j + 1
+        if k == check or k == m_max:
+            Hh = Hd[:k + 1, :k].cpu().numpy()
+            sub = np.abs(np.diag(Hh, -1))
+            scale = max(np.abs(Hh).max(), 1e-300)
+            brk = np.nonzero(sub < 1e-14 * scale)[0]
+            if len(brk):   # invariant subspace: the Krylov solution is exact
+                k_done = int(brk[0]) + 1
+                break
+            Y = _shift_solutions(Hh[:k, :k], beta, shifts)
+            res = np.abs(Hh[k, k - 1] * Y[:, -1]) / np.maximum(np.linalg.norm(Y, axis=1), 1e-300)
+            if np.all(res < tol):
+                k_done = k
+                break
+            check = max(k + 1, int(k * growth))
+    if k_done is None:
+        raise RuntimeError(f"shifted Krylov solve: no convergence to {tol:g} within {m_max} Arnoldi steps")
+    Hh = Hd[:k_done, :k_done].cpu().numpy()
+    Y = _shift_solutions(Hh, beta, shifts)
+    Yt = torch.from_numpy(np.ascontiguousarray(Y)).to(dev)
+    return Yt @ V[:k_done], k_done
+
+
+def expv_taylor(op, X, T):
+    """e^{P T} X for X [B, n] on the device: Taylor substeps tau = T / s with ||P tau||_inf <= 1, TAYLOR_DEGREE
+    terms each (every term one batched stencil launch)."""
+    if T == 0:
+        return X.clone(), 0
+    s = max(1, int(np.ceil(abs(T) * op.norm)))
+    tau = T / s
+    out = X.clone()
+    t1 = torch.empty_like(X)
+    t2 = torch.empty_like(X)
+    for _ in range(s):
+        term = out.clone()
+        acc = out
+        for j in range(1, TAYLOR_DEGREE + 1):
+            dst = t1 if j % 2 else t2
+            op.apply(term, dst, tau / j)
+            acc += dst
+            term = dst
+        out = acc
+    return out, s
+
+
+def act_block(blk, X, nmax, n2):
+    """(I_nmax (x) blk) on the rows of X [S, nmax n2] (generate_actions' per-ADO action)."""
+    b = torch.from_numpy(np.ascontiguousarray(blk)).to(X.device)
+    S = X.shape[0]
+    return torch.einsum('xy,say->sax', b, X.reshape(S, nmax, n2)).reshape(S, nmax * n2).contiguous()
+
+
+def corr4_krylov(op, opT, A1, A2, A3, A4, rho0, T, w_x, w_y, nmax, ns, tol=1e-12):
+    """c[i, j] of correlation_4op_3t(if_full=True) from the operators P (op) and P^T (opT): A1..A4 the per-ADO action
+    blocks (ns^2 x ns^2) of operator_d, _c, _b, _a in the reference's order.  Returns (c [len(w_x), len(w_y)] numpy,
+    info dict)."""
+    n2 = ns * ns
+    n = nmax * n2
+    dev = op.dev
+    wx = np.asarray(w_x, dtype=float)
+    wy = np.asarray(w_y, dtype=float)
+    v = torch.zeros(n, dtype=torch.complex128, device=dev)
+    v[:n2] = torch.from_numpy(np.ascontiguousarray(A4 @ np.asarray(rho0, dtype=complex).reshape(-1))).to(dev)
+    diag = np.arange(ns) * (ns + 1)
+    u = torch.zeros(n, dtype=torch.complex128, device=dev)
+    u[:n2] = torch.from_numpy(np.ascontiguousarray(A1[diag].sum(axis=0))).to(dev)   # u^T x = Tr_sys(A1 x_0)
+    R, kr = shifted_krylov_solve(op, v, 1j * wy, tol)    # r(w_y) = (-P - i w_y)^-1 v      [n_wy, n]
+    L, kl = shifted_krylov_solve(opT, u, 1j * wx, tol)   # l(w_x) = (-P^T - i w_x)^-1 u    [n_wx, n]
+    if len(wy) <= len(wx):   # e^{PT} on the right-hand vectors
+        Rm, s = expv_taylor(op, act_block(A3, R, nmax, n2), T)
+        C = L @ act_block(A2, Rm, nmax, n2).transpose(0, 1)
+    else:                    # e^{P^T T} on the left-hand ones: c = (e^{P^T T} A2^T l)^T (A3 r)
+        Lm, s = expv_taylor(opT, act_block(A2.T, L, nmax, n2), T)
+        C = Lm @ act_block(A3, R, nmax, n2).transpose(0, 1)
+    info = {"method": "krylov", "krylov_dim_right": kr, "krylov_dim_left": kl, "taylor_substeps": s,
+            "norm_bound": op.norm}
+    return C.cpu().numpy(), info

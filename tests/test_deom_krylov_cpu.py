@@ -1,0 +1,81 @@
+"""Krylov form of DEOMSolver.correlation_4op_3t (pyqed_amd/deom_krylov.py), host parts: the transposed-generator
+tables against P.T of the assembled ADO Liouvillian (heom/deom.py:769-893 via ado_liouvillian), the row-sum bound, and
+the whole Krylov algebra on a dense CPU operator against the eigen form of heom/deom.py:1127-1209 (the GPU runs the
+same code with the stencil kernel: tests/test_deom_krylov_gpu.py)."""
+import numpy as np
+import pytest
+import sympy as sp
+import torch
+
+from conftest import relerr
+
+
+class _DenseOp:
+    """A CPU stand-in for deom_krylov.DeomOperator (dense P); test infrastructure only."""
+
+    def __init__(self, P, norm):
+        self.P = torch.from_numpy(np.ascontiguousarray(P))
+        self.n = P.shape[0]
+        self.dev = torch.device("cpu")
+        self.norm = norm
+
+    def apply(self, x, y, alpha=1.0):
+        y.copy_((alpha * (self.P @ x.reshape(-1, self.n).T).T).reshape(y.shape))
+        return y
+
+
+def _hierarchy(ns, npsd, L, nmod=1, seed=0):
+    from pyqed_amd.deom import Bath, DEOMSolver, ado_coefficients
+    w = sp.symbols(r"\omega", real=True)
+    spes = [2 * 0.5 * (1 + 0.3 * m) * w / (1.0 + w ** 2) for m in range(nmod)]
+    mode = [m for m in range(nmod) for _ in range(npsd + 1)]
+    bath = Bath(spes, w, [1.0] * nmod, [npsd] * nmod, mode)
+    rng = np.random.default_rng(seed)
+    A = rng.standard_normal((ns, ns)) + 1j * rng.standard_normal((ns, ns))
+    H = (A + A.conj().T) / 2
+    Q = np.array([np.diag(np.arange(ns, dtype=float) + m) + 0.3 * (np.eye(ns, k=1) + np.eye(ns, k=-1))
+                  + 0.1j * m * (np.eye(ns, k=1) - np.eye(ns, k=-1)) for m in range(nmod)], dtype=complex)
+    sol = DEOMSolver(H, None, bath, Q, None, None, None, L)
+    sol.check_()
+    sol.init_()
+    b = sol.bath
+    coef, damp = ado_coefficients(sol.keys, np.asarray(b.etal), np.asarray(b.etar), np.asarray(b.etaa),
+                                  np.asarray(b.expn), sol.lmax)
+    return sol, H, Q, coef, damp, np.asarray(b.mode)
+
+
+@pytest.mark.parametrize("ns,npsd,L,nmod", [(2, 3, 3, 1), (3, 2, 3, 1), (2, 1, 4, 2)])
+def test_transposed_tables_give_the_transposed_generator(ns, npsd, L, nmod):
+    from pyqed_amd.deom import ado_liouvillian
+    from pyqed_amd.deom_krylov import inf_norm_bound, transposed_tables
+    sol, H, Q, coef, damp, mode = _hierarchy(ns, npsd, L, nmod)
+    P = ado_liouvillian(sol.keys, sol._minus, sol._plus, coef, damp, H, Q, mode)
+    mT, pT, cT = transposed_tables(sol._minus, sol._plus, coef)
+    PT = ado_liouvillian(sol.keys, mT, pT, cT, damp, H.T, np.swapaxes(Q, 1, 2), mode)
+    assert np.array_equal(PT, P.T)
+    nb = inf_norm_bound(sol._minus, sol._plus, coef, damp, H, Q, mode)
+    assert np.abs(P).sum(1).max() <= nb * (1 + 1e-12)
+    assert np.abs(PT).sum(1).max() <= inf_norm_bound(mT, pT, cT, damp, H.T, np.swapaxes(Q, 1, 2), mode) * (1 + 1e-12)
+
+
+@pytest.mark.parametrize("lcr,nwx,nwy", [("llll", 9, 7), ("lccc", 6, 8), ("lrlr", 5, 5)])
+def test_krylov_corr4_matches_eigen_form(lcr, nwx, nwy):
+    """Both orientations of the exponential (right vectors when n_wy <= n_wx, else the left ones)."""
+    from oracle import deom as od
+    from pyqed_amd.deom import _action_block, ado_liouvillian
+    from pyqed_amd.deom_krylov import corr4_krylov, inf_norm_bound, transposed_tables
+    sol, H, Q, coef, damp, mode = _hierarchy(2, 2, 3)
+    P = ado_liouvillian(sol.keys, sol._minus, sol._plus, coef, damp, H, Q, mode)
+    mT, pT, cT = transposed_tables(sol._minus, sol._plus, coef)
+    nb = inf_norm_bound(sol._minus, sol._plus, coef, damp, H, Q, mode)
+    sx = np.array([[0, 1], [1, 0]], complex)
+    sz = np.diag([1.0, -1.0]).astype(complex)
+    ops = [sz, sx, sx, sz]   # operator_a .. operator_d
+    rho0 = np.array([[0.7, 0.2 - 0.1j], [0.2 + 0.1j, 0.3]])
+    T = 0.3
+    wx = np.linspace(-4, 3, nwx)
+    wy = np.linspace(-2.3, 5.1, nwy)   # w = 0 is the steady state pole (the eigen form divides by 0 there too)
+    A1, A2, A3, A4 = (_action_block(o, c) for o, c in zip(ops[::-1], lcr[::-1]))
+    c, info = corr4_krylov(_DenseOp(P, nb), _DenseOp(P.T.copy(), nb), A1, A2, A3, A4, rho0, T, wx, wy, sol.nmax, 2)
+    ref = od.correlation_4op_3t(P, sol.nmax, 2, ops, rho0, T, wx, wy, if_full=True, lcr=lcr)
+    assert relerr(c, ref) < 1e-10, (lcr, info)

@@ -1,0 +1,102 @@
+"""Krylov form of DEOMSolver.correlation_4op_3t on the GPU (pyqed_amd/deom_krylov.py, qd_deom_apply): the stencil
+operator P and its transposed-table form P^T against the assembled ADO Liouvillian (heom/deom.py:769-893), the
+correlation against the reference fixture and the eigen form, and the bench hierarchy (L = 12, K = 5, n = 24,752,
+whose dense P the reference cannot diagonalise) through the two orientations of the algorithm."""
+import numpy as np
+import pytest
+import sympy as sp
+import torch
+
+from conftest import load_golden, relerr
+from test_deom_krylov_cpu import _hierarchy
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("ns,npsd,L,nmod,B", [(2, 3, 4, 1, 1), (2, 3, 4, 1, 5), (3, 2, 3, 1, 2), (5, 1, 3, 1, 1),
+                                              (2, 1, 4, 2, 3), (2, 8, 2, 1, 1)])
+def test_deom_apply_is_the_generator_and_its_transpose(ns, npsd, L, nmod, B):
+    from pyqed_amd import _lib
+    from pyqed_amd.deom import ado_liouvillian
+    from pyqed_amd.deom_krylov import DeomOperator, transposed_tables
+    dev = torch.device("cuda", 0)
+    sol, H, Q, coef, damp, mode = _hierarchy(ns, npsd, L, nmod)
+    P = ado_liouvillian(sol.keys, sol._minus, sol._plus, coef, damp, H, Q, mode)
+    mT, pT, cT = transposed_tables(sol._minus, sol._plus, coef)
+    op = DeomOperator(dev, sol._minus, sol._plus, coef, damp, mode, H, Q, ns)
+    opT = DeomOperator(dev, mT, pT, cT, damp, mode, H.T, np.swapaxes(Q, 1, 2), ns)
+    rng = np.random.default_rng(7)
+    x = rng.standard_normal((B, P.shape[0])) + 1j * rng.standard_normal((B, P.shape[0]))
+    xd = torch.from_numpy(x).to(dev)
+    y = torch.empty_like(xd)
+    _lib.take_path()
+    op.apply(xd, y, 0.75)
+    torch.cuda.synchronize()
+    assert "deom_apply" in _lib.take_path()
+    assert relerr(y.cpu().numpy(), 0.75 * (x @ P.T)) < 1e-13
+    opT.apply(xd, y, -2.0)
+    assert relerr(y.cpu().numpy(), -2.0 * (x @ P)) < 1e-13
+
+
+def _fixture_solver(g):
+    from pyqed_amd.deom import Bath, DEOMSolver
+    bath = Bath.__new__(Bath)
+    bath.etal, bath.etar, bath.etaa, bath.expn = g["etal"], g["etar"], g["etaa"], g["expn"]
+    bath.mode = np.zeros(len(g["expn"]), dtype=np.int64)
+    return DEOMSolver(g["H"], np.zeros((2, 2), complex), bath, g["Q"], np.zeros((1, 2, 2), complex),
+                      lambda t: 0, lambda t: 0, int(g["lmax"]))
+
+
+def test_krylov_corr4_matches_reference_fixture():
+    """The reference's own outputs (tests/golden/deom_corr4.npz, eig of its 140 x 140 P) from the Krylov form."""
+    g = load_golden("deom_corr4")
+    sx = g["Q"][0]
+    sol = _fixture_solver(g)
+    sol.corr4_method = "krylov"
+    for lcr in ["llll", "lrlr", "lccc"]:
+        cw = sol.correlation_4op_3t(sx, sx, sx, sx, g["rho0"], float(g["T"]), g["wx"], g["wy"], lcr=lcr)
+        assert sol.last_corr4["method"] == "krylov"
+        assert relerr(cw, g["cw_" + lcr]) < 1e-9, lcr
+    with pytest.raises(ValueError):
+        sol.correlation_4op_3t(sx, sx, sx, sx, g["rho0"], 0.5, g["wx"], g["wy"], if_full=False)
+
+
+def test_krylov_corr4_auto_above_threshold_matches_eigen_form():
+    """n = nmax ns^2 = 1320 >= KRYLOV_MIN_DIM takes the Krylov form by default; the eigen form (host eig of the
+    1320 x 1320 P, the reference's algorithm) agrees."""
+    from pyqed_amd.deom import KRYLOV_MIN_DIM, Bath, DEOMSolver
+    w = sp.symbols(r"\omega", real=True)
+    bath = Bath([2 * 0.5 * w / (1.0 + w ** 2)], w, [1.0], [3], [0] * 4)
+    sx = np.array([[0, 1], [1, 0]], complex)
+    sz = np.diag([1.0, -1.0]).astype(complex)
+    sol = DEOMSolver(sz + sx, None, bath, np.array([sx]), None, None, None, 7)
+    rho0 = np.array([[1, 0], [0, 0]], complex)
+    wx = np.linspace(-4.1, 4.3, 12)
+    wy = np.linspace(-3.7, 4.9, 10)
+    c = sol.correlation_4op_3t(sz, sx, sx, sz, rho0, 0.4, wx, wy, lcr="lccc")
+    assert sol.last_corr4["method"] == "krylov" and sol.last_corr4["n"] == 1320 >= KRYLOV_MIN_DIM
+    sol.corr4_method = "eig"
+    ref = sol.correlation_4op_3t(sz, sx, sx, sz, rho0, 0.4, wx, wy, lcr="lccc")
+    assert sol.last_corr4["method"] == "eig"
+    assert relerr(c, ref) < 1e-9
+
+
+def test_krylov_corr4_bench_hierarchy_orientations_agree():
+    """L = 12, K = 5 (6188 ADOs, n = 24,752): the reference would diagonalise a 9.8 GB P.  The Krylov form's two
+    orientations (e^{PT} on the right-hand vectors when n_wy <= n_wx, e^{P^T T} on the left-hand ones otherwise)
+    share only the resolvent solves' definition, not their arithmetic order: they agree to 1e-9."""
+    from pyqed_amd.deom import Bath, DEOMSolver
+    w = sp.symbols(r"\omega", real=True)
+    bath = Bath([2 * 0.5 * w / (1.0 + w ** 2)], w, [1.0], [4], [0] * 5)
+    sx = np.array([[0, 1], [1, 0]], complex)
+    sz = np.diag([1.0, -1.0]).astype(complex)
+    sol = DEOMSolver(sz + sx, None, bath, np.array([sx]), None, None, None, 12)
+    rho0 = np.array([[1, 0], [0, 0]], complex)
+    wx = np.linspace(-4.1, 4.3, 8)
+    wy = np.linspace(-3.7, 4.9, 6)
+    c1 = sol.correlation_4op_3t(sz, sx, sx, sz, rho0, 0.2, wx, wy)
+    info1 = dict(sol.last_corr4)
+    assert info1["method"] == "krylov" and info1["n"] == 24752
+    c2 = sol.correlation_4op_3t(sz, sx, sx, sz, rho0, 0.2, wx, np.concatenate([wy, [5.3, 6.1, 7.7]]))
+    assert np.all(np.isfinite(c1))
+    assert relerr(c2[:, :len(wy)], c1) < 1e-9, (info1, sol.last_corr4)
