@@ -1027,6 +1027,36 @@ def bench_deom_banded(dev, world, rank, steps=40, cases=None):
     return out
 
 
+def bench_deom_corr4(dev, nw=32, T=0.5):
+    """DEOMSolver.correlation_4op_3t at the bench hierarchy (L = 12, K = 5, n = nmax ns^2 = 24,752; SURVEY §8(f)
+    rank 2) on an nw x nw (w_x, w_y) grid, signature 'lccc': the Krylov form (pyqed_amd/deom_krylov.py: multi-shift
+    Krylov solves of P and P^T on the stencil kernel, Taylor-substep e^{PT}), wall clock of the whole call after a
+    warm-up call.  The reference's eigen form would diagonalise the 9.8 GB dense P (O(n^3) ~ 6e13 flop on the host):
+    not run, so there is no CPU baseline for this leg."""
+    import torch
+    import sympy as sp
+    from pyqed_amd.deom import Bath, DEOMSolver
+    w = sp.symbols(r"\omega", real=True)
+    bath = Bath([2 * 0.5 * w / (1.0 + w ** 2)], w, [1.0], [4], [0] * 5)
+    sx = np.array([[0, 1], [1, 0]], complex)
+    sz = np.diag([1.0, -1.0]).astype(complex)
+    sol = DEOMSolver(sz + sx, None, bath, np.array([sx]), None, None, None, 12)
+    rho0 = np.array([[1, 0], [0, 0]], complex)
+    wx = np.linspace(-4.1, 4.3, nw)   # grids clear of w = 0 (the steady-state pole)
+    wy = np.linspace(-3.7, 4.9, nw)
+    sol.correlation_4op_3t(sz, sx, sx, sz, rho0, T, wx[:4], wy[:4], lcr="lccc")   # warm-up (tables, kernels)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    c = sol.correlation_4op_3t(sz, sx, sx, sz, rho0, T, wx, wy, lcr="lccc")
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    assert np.all(np.isfinite(c))
+    info = {k: v for k, v in sol.last_corr4.items() if k != "method"}
+    return {"value": round(nw * nw / el, 2), "unit": "(w_x, w_y) points/s (one correlation_4op_3t call, L=12 K=5)",
+            "seconds": round(el, 3), "grid": [nw, nw], "T": T, "method": sol.last_corr4["method"], **info,
+            "note": "eigen form of the reference (eig of the 24,752^2 P) not run: no CPU baseline"}
+
+
 def cpu_baseline_deom(budget_s=8.0):
     import sympy as sp
     from oracle import deom as od
@@ -1178,6 +1208,7 @@ def main():
     ap.add_argument("--deom-batch", type=int, default=64)
     ap.add_argument("--no-deom", action="store_true")
     ap.add_argument("--no-deom-banded", action="store_true", help="skip the tier-banded DEOM leg")
+    ap.add_argument("--no-deom-corr4", action="store_true", help="skip the bench-hierarchy correlation_4op_3t leg")
     ap.add_argument("--deom-banded-ranks", action="store_true",
                     help="world > 1: also run ONE hierarchy tier-banded over the ranks (RCCL all-gather per stage)")
     ap.add_argument("--no-redfield", action="store_true")
@@ -1346,6 +1377,10 @@ def main():
     # exception would leave the others waiting in the all-gather), and the halo is 2.5x the owned rows at 8 bands, so
     # it is a capacity tool, not a speed-up, for the bench hierarchy.  World 1 runs the 8-band loopback.
     progress("deom leg done")
+    deom_corr4 = None
+    if world == 1 and not args.no_deom and not args.no_deom_corr4:
+        deom_corr4 = guarded(bench_deom_corr4, dev)
+        progress("deom corr4 leg done")
     deom_banded = None
     if not args.no_deom and not args.no_deom_banded:
         if world > 1:
@@ -1434,6 +1469,8 @@ def main():
             if world == 1 and not args.no_cpu and "error" not in deom:
                 deom["cpu_baseline"] = cpu_baseline_deom()
             out.setdefault("secondary", {})["deom"] = deom
+        if deom_corr4 is not None:
+            out.setdefault("secondary", {})["deom_corr4"] = deom_corr4
         if deom_banded is not None:
             out.setdefault("secondary", {})["deom_banded"] = deom_banded
         detail = write_detail(out, args.detail)

@@ -24,8 +24,8 @@ if [ "$PART" = stats ]; then
 else
   # without the banded-DEOM leg: the profiler's dispatch callback can read past a 1 MiB kernel-argument pool chunk
   # and segfault, likeliest on that leg's thousands of small launches (profiles/r05/runtime/pmc_crash/SUMMARY.md)
-  timeout -k 10 250 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu --no-deom-banded > $OUT/fetch.log 2>&1
-  timeout -k 10 250 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu --no-deom-banded > $OUT/write.log 2>&1
+  timeout -k 10 250 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu --no-deom-banded --no-deom-corr4 > $OUT/fetch.log 2>&1
+  timeout -k 10 250 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu --no-deom-banded --no-deom-corr4 > $OUT/write.log 2>&1
   timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/gfetch -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu --general --no-2des --no-spo --no-deom --no-redfield > $OUT/gfetch.log 2>&1
   timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/gwrite -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu --general --no-2des --no-spo --no-deom --no-redfield > $OUT/gwrite.log 2>&1
 fi
