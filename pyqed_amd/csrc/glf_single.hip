@@ -10,6 +10,9 @@
 //   - its tile of rho stays in registers (threads 0..255, one element each);
 //   - the 8 waves split K = Np into 8 chunks (KS k-steps of 4 each) and the partial tiles are summed in LDS in the
 //     fixed wave order (deterministic);
+//   - split roles (round 5, while 2 B T^2 <= 256): a second workgroup per tile computes and publishes the Y_c tile,
+//     so the tile's k workgroup runs P r + r Q while the row's Y_c tiles are made (N = 128, one matrix: 35.5k ->
+//     39.6k steps/s, profiles/r05/lindblad/glf_single_split_roles.txt); otherwise one workgroup does both in turn;
 //   - per RK4 stage two hand-offs inside the launch: Y_c(bm, bn) = L_c[bm, :] r[:, bn] is published, then
 //     k(bm, bn) = P[bm, :] r[:, bn] + r[bm, :] Q[:, bn] + sum_c Y_c[bm, :] R_c[:, bn] needs the Y_c row block bm;
 //     the Horner update s' = rho + dt / (4 - m) k (glf.hip header) is published as the next stage input, whose row
@@ -51,6 +54,7 @@ struct SingleParams {
   int* status;
   unsigned long long* tim;   // QD_PHASE_TIMING builds: [grid][8] wall-clock ticks per phase (thread 0's view)
   int N, ne, nsteps, step0, total_steps, save_every, nsave;
+  int split;           // 1: a second workgroup per tile computes the Y_c tiles (grid = 2 B T^2)
   double dt;
 };
 
@@ -105,7 +109,12 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
   constexpr int T = 2 * KS, Np = 32 * KS, NN = Np * Np;
   __shared__ c128 red[8][256];
   __shared__ int sAbort;
-  const int w = blockIdx.x, b = w / (T * T), tile = w - b * (T * T), bm = tile / T, bn = tile - bm * T;
+  // split: workgroups [0, B T^2) are the tiles' k workgroups, [B T^2, 2 B T^2) their Y workgroups; a tile's two
+  // epoch words (0: stage output, 1: Y_c) are written by its k and its Y workgroup respectively
+  const int nk = p.split ? (int)gridDim.x / 2 : (int)gridDim.x;
+  const bool yrole = p.split && (int)blockIdx.x >= nk;
+  const int w = yrole ? (int)blockIdx.x - nk : (int)blockIdx.x;
+  const int b = w / (T * T), tile = w - b * (T * T), bm = tile / T, bn = tile - bm * T;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lk = lane >> 4;
   const int kb = wave * 4 * KS;
   // constant operator fragments, loaded once: A rows bm (P, L_c), B columns bn (Q, R_c)
@@ -121,12 +130,12 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
       bR[c][q] = p.Rop[(size_t)c * NN + k * Np + bn * 16 + lr];
     }
   }
-  const bool owner = tid < 256;
+  const bool owner = tid < 256 && !yrole;
   const int orow = bm * 16 + ((tid >> 4) & 15), ocol = bn * 16 + (tid & 15);
   c128* rhob = p.rho + (size_t)b * NN;
   c128 rh = owner ? rhob[orow * Np + ocol] : cmk(0, 0);
   if (tid == 0) sAbort = 0;
-  const int mats = gridDim.x / (T * T);
+  const int mats = nk / (T * T);
   const int slab = mats * NN * (int)sizeof(c128);   // bytes of one [B][Np][Np] buffer
   unsigned* fl = p.flags;
   auto flag_at = [&](int wg, int kind) { return fl + ((size_t)wg * 2 + kind) * SG_FLAG_STRIDE; };
@@ -151,7 +160,7 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
       }
     }
   };
-  if (p.ne > 0 && p.step0 == 0) observe(0);
+  if (p.ne > 0 && p.step0 == 0 && !yrole) observe(0);
 
   // fixed-order sum of the 8 waves' partial tiles; returns element tid (tid < 256) of the tile
   auto reduce = [&](const SgAcc<M3>& acc) -> c128 {
@@ -161,7 +170,7 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
     for (int r = 0; r < 4; ++r) red[wave][(lk + 4 * r) * 16 + lr] = cmk(re[r], im[r]);
     __syncthreads();
     c128 v = cmk(0, 0);
-    if (owner) {
+    if (tid < 256) {
       v = red[0][tid];
 #pragma unroll
       for (int q = 1; q < 8; ++q) v = cadd(v, red[q][tid]);
@@ -206,7 +215,11 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
     const int s = g >> 2, m = g & 3;
     // ---- stage input r_g: the caller's rho at g = 0, else the previous stage's output in rbuf[g & 1]
     const c128* rin = g == 0 ? p.rho : p.rbuf + (size_t)(g & 1) * mats * NN;
-    if (g > 0 && !wait_for(2 * T, 0, (unsigned)g, [&](int l) {   // column bn and row bm of r_g
+    // column bn and row bm of r_g (a Y workgroup reads the column only).  Buffer reuse with split roles: the k
+    // workgroup of (l, bn) finishing stage g - 1 implies the Y workgroup of (l, bn) published stage g - 1's Y_c (it
+    // waited for it), i.e. finished reading r_{g-1}; and a Y workgroup entering stage g has seen its own tile's k
+    // workgroup finish stage g - 1, which had seen its row finish stage g - 2 (the readers of Y_{g-2}).
+    if (g > 0 && !wait_for(yrole ? T : 2 * T, 0, (unsigned)g, [&](int l) {
           return b * T * T + (l < T ? l * T + bn : bm * T + (l - T));
         }))
       break;
@@ -221,7 +234,7 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
     }
     // ---- Y_c(bm, bn) = L_c[bm, :] r[:, bn], published for the k phase of the row
     c128* ybase = p.ybuf + (size_t)(g & 1) * NC * mats * NN;
-    if constexpr (NC > 0) {
+    if (NC > 0 && (yrole || !p.split)) {
       const __amdgpu_buffer_rsrc_t ry = sc1_rsrc(ybase, NC * slab);
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
@@ -229,10 +242,14 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
 #pragma unroll
         for (int q = 0; q < KS; ++q) acc.mac(aL[c][q], rcol[q]);
         const c128 y = reduce(acc);
-        if (owner) st16_sc1(ry, (((c * mats + b) * Np + orow) * Np + ocol) * 16, y);
+        if (tid < 256) st16_sc1(ry, (((c * mats + b) * Np + orow) * Np + ocol) * 16, y);
         __syncthreads();   // red is reused by the next reduction
       }
       publish(1, (unsigned)(g + 1));
+    }
+    if (yrole) {
+      SG_MARK(1)
+      continue;
     }
     SG_MARK(1)
     // ---- k(bm, bn) = P r + r Q + sum_c Y_c R_c; the P r + r Q part runs while the row's Y_c are handed over
@@ -280,7 +297,7 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
   if (owner) rhob[orow * Np + ocol] = rh;
 #ifdef QD_PHASE_TIMING
   if (tid == 0 && p.tim)
-    for (int k = 0; k < 6; ++k) p.tim[(size_t)w * 8 + k] = tacc[k];
+    for (int k = 0; k < 6; ++k) p.tim[(size_t)blockIdx.x * 8 + k] = tacc[k];
 #endif
 }
 
@@ -363,12 +380,16 @@ int glf_single_run(const c128* P, const c128* Q, const c128* Lop, const c128* Ro
   p.tim = nullptr;
 #ifdef QD_PHASE_TIMING
   void* tw = nullptr;
-  if ((rc = workspace(WS_MISC, (size_t)B * T2 * 8 * sizeof(unsigned long long), &tw, st))) return rc;
-  QD_HIP(hipMemsetAsync(tw, 0, (size_t)B * T2 * 8 * sizeof(unsigned long long), st));
+  if ((rc = workspace(WS_MISC, (size_t)2 * B * T2 * 8 * sizeof(unsigned long long), &tw, st))) return rc;
+  QD_HIP(hipMemsetAsync(tw, 0, (size_t)2 * B * T2 * 8 * sizeof(unsigned long long), st));
   p.tim = (unsigned long long*)tw;
 #endif
   const bool coop = option(QD_OPT_COOP_LAUNCH) != 0;
-  const int grid = B * T2;
+  // a second workgroup per tile for the Y_c tiles when the chip has room: the k workgroup's P r + r Q then runs
+  // while the Y_c tiles are computed and handed over, instead of after its own Y_c tile
+  p.split = nc > 0 && 2 * B * T2 <= 256;
+  note_path(p.split ? "glf_single_split" : "glf_single_joint");
+  const int grid = (p.split ? 2 : 1) * B * T2;
   hipError_t e = hipErrorInvalidValue;
 #define SG_CASE(KS_)                                                    \
   switch (nc) {                                                         \
@@ -399,16 +420,19 @@ int glf_single_run(const c128* P, const c128* Q, const c128* Lop, const c128* Ro
   }
 #ifdef QD_PHASE_TIMING
   {   // per-phase wall clock (100 MHz ticks, workgroup thread 0), mean over workgroups, per stage, in us
-    std::vector<unsigned long long> hv((size_t)B * T2 * 8);
+    std::vector<unsigned long long> hv((size_t)grid * 8);
     QD_HIP(hipMemcpy(hv.data(), p.tim, hv.size() * 8, hipMemcpyDeviceToHost));
     const char* nm[6] = {"wait_r", "y_publish", "pr_rq_mfma", "wait_y", "y_mfma_reduce", "update_publish"};
-    fprintf(stderr, "[glf single phase timing] N=%d B=%d nsteps=%d, us per stage:", N, B, nsteps);
-    for (int k = 0; k < 6; ++k) {
-      double sm = 0;
-      for (int q = 0; q < B * T2; ++q) sm += (double)hv[(size_t)q * 8 + k];
-      fprintf(stderr, " %s %.3f", nm[k], sm / (B * T2) / 100.0 / (4.0 * nsteps));
+    for (int role = 0; role < (p.split ? 2 : 1); ++role) {
+      fprintf(stderr, "[glf single phase timing] N=%d B=%d nsteps=%d %s workgroups, us per stage:", N, B, nsteps,
+              role ? "Y" : (p.split ? "k" : "joint"));
+      for (int k = 0; k < 6; ++k) {
+        double sm = 0;
+        for (int q = 0; q < B * T2; ++q) sm += (double)hv[((size_t)role * B * T2 + q) * 8 + k];
+        fprintf(stderr, " %s %.3f", nm[k], sm / (B * T2) / 100.0 / (4.0 * nsteps));
+      }
+      fprintf(stderr, "\n");
     }
-    fprintf(stderr, "\n");
   }
 #endif
   if (ne) {

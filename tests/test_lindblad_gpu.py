@@ -536,15 +536,18 @@ def test_lindblad_np64_hermitian_dispatch_matches_oracle(N, B):
     assert relerr(rho.cpu().numpy()[:3], ref) < TOL
 
 
-@pytest.mark.parametrize("N,nc,B,prod", [(128, 1, 1, "3m"), (128, 2, 1, "4m"), (128, 1, 2, "3m"), (100, 1, 4, "4m"),
-                                         (64, 1, 3, "3m"), (40, 2, 2, "4m"), (20, 0, 5, "3m"), (32, 1, 64, "4m"),
-                                         (32, 1, 8, "3m")])
-def test_lindblad_single_launch_matches_split_path_and_oracle(N, nc, B, prod):
+@pytest.mark.parametrize("N,nc,B,prod,role", [(128, 1, 1, "3m", "split"), (128, 2, 1, "4m", "split"),
+                                              (128, 1, 2, "4m", "split"), (100, 1, 4, "4m", "joint"),
+                                              (64, 1, 3, "3m", "split"), (40, 2, 2, "4m", "split"),
+                                              (20, 0, 5, "3m", "joint"), (32, 1, 64, "4m", "joint"),
+                                              (32, 1, 8, "3m", "split"), (64, 1, 16, "4m", "joint")])
+def test_lindblad_single_launch_matches_split_path_and_oracle(N, nc, B, prod, role):
     """Few density matrices as ONE persistent launch (glf_single.hip: a workgroup per 16 x 16 output tile, operator
     fragments in registers, Y_c and stage outputs handed over inside the launch): final state, observables after every
     step and snapshots against the split path (N_p >= 64) or the persistent kernel (N_p = 32) and the oracle's RK4
     (oqs.py:697-714, 1596-1696); Np = 128 / 64 / 32, nc = 0 / 1 / 2, up to the 256-workgroup cap (B = 4 at Np = 128,
-    64 at Np = 32); the 3-product complex MACs up to 128 workgroups (nc < 2), 4 products above (qd_take_path)."""
+    64 at Np = 32); the 3-product complex MACs up to 128 workgroups (nc < 2), 4 products above; a second workgroup
+    per tile for the Y_c tiles ("split" roles) while 2 B T^2 <= 256 (qd_take_path)."""
     import torch
     from oracle import lindblad as olb
     from pyqed_amd import lindblad_rk4
@@ -568,7 +571,7 @@ def test_lindblad_single_launch_matches_split_path_and_oracle(N, nc, B, prod):
         got = took("")[1]
         assert ("glf_" + mode) in got, (mode, got)
         if mode == "single":
-            assert ("glf_single_" + prod) in got, got
+            assert ("glf_single_" + prod) in got and ("glf_single_" + role) in got, got
         out[mode] = (rho.cpu().numpy(), obs.cpu().numpy(), snap.cpu().numpy())
     ref = olb.lindblad_batch(H, cs, rho0, dt, steps)
     assert relerr(out["single"][0], ref) < TOL
