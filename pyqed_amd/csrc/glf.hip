@@ -377,10 +377,13 @@ __global__ __launch_bounds__(CG_WG) void glf_split_hk2_kernel(LindbladParams p) 
   __shared__ CgLds<BT> L;
   __shared__ CgSeg segs[1 + MAX_NC];
   const int nb = p.Np / BT, npairs = nb * (nb + 1) / 2, noff = nb * (nb - 1) / 2;
-  const bool xl_role = (int)blockIdx.x >= npairs;
+  // grid (B, pairs + off-diagonal pairs): the linear dispatch order runs every matrix's 16-K-tile workgroups (XU and
+  // diagonal blocks) before the 8-K-tile XL ones, so the short workgroups fill the launch's tail
+  const int role = blockIdx.y;
+  const bool xl_role = role >= npairs;
   int bm = 0, bn, oj = -1;   // (bm, bn) block pair; oj = its index among the off-diagonal pairs (row-major)
   if (!xl_role) {
-    int pi = blockIdx.x;
+    int pi = role;
     while (pi >= nb - bm) {
       pi -= nb - bm;
       ++bm;
@@ -388,7 +391,7 @@ __global__ __launch_bounds__(CG_WG) void glf_split_hk2_kernel(LindbladParams p) 
     bn = bm + pi;
     if (bm < bn) oj = bm * (nb - 1) - bm * (bm - 1) / 2 + (bn - bm - 1);
   } else {
-    oj = blockIdx.x - npairs;
+    oj = role - npairs;
     int j = oj;
     while (j >= nb - 1 - bm) {
       j -= nb - 1 - bm;
@@ -396,7 +399,7 @@ __global__ __launch_bounds__(CG_WG) void glf_split_hk2_kernel(LindbladParams p) 
     }
     bn = bm + 1 + j;
   }
-  const int b = blockIdx.y;
+  const int b = blockIdx.x;
   const int Np = p.Np, nc = p.nc;
   const size_t NN = (size_t)Np * Np;
   const c128* r = split_buf(p, b, p.rin);
@@ -718,7 +721,7 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
         }
         if (hk2) {   // split_bt is 32 here
           const unsigned np2 = nb * (nb + 1) / 2 + nb * (nb - 1) / 2;
-          hipLaunchKernelGGL(glf_split_hk2_kernel<32>, dim3(np2, B), dim3(CG_WG), 0, st, p);
+          hipLaunchKernelGGL(glf_split_hk2_kernel<32>, dim3(B, np2), dim3(CG_WG), 0, st, p);
         } else {
           QD_SPLIT(glf_split_k_kernel, dim3(nb * nb, B * ks));
         }
