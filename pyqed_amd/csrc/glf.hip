@@ -555,6 +555,9 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   //    32-blocks; tools/glf_hsplit_sweep.sh: 198k / 233k / 258k / 264k DM-steps/s at 64 / 128 / 192 / 224 matrices
   //    against 82k / 164k / 242k / 278k for the persistent kernel);
   //  - else the persistent kernel (a workgroup per matrix).
+#ifndef GLF_HSPLIT_Y64
+#define GLF_HSPLIT_Y64 1
+#endif
   const int force = option(QD_OPT_GLF_PATH);
   int split_bt = 0;
   bool hsplit = false;
@@ -579,18 +582,22 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   // >= 3 K-tiles each, at most 4 (k phase) / 8 (Y phase) partial slabs per block.  Measured (N = 128 / 256, one
   // trajectory, tools/ks_sweep.sh): 4 k-splits 12.0k / 6.9k steps/s, 8: 11.8k / 6.6k, 16: 9.8k / 5.8k, none: 8.4k / 4.2k.
   int ks = 1, ys = 1;
+  // the Hermitian pair path's Y launch takes 64-blocks (all eight waves of a workgroup issuing MFMAs) from two per CU:
+  // 128 matrices 288k -> 293k DM-steps/s, 64 matrices (one per CU) 255k -> 254k (profiles/r05/lindblad/y64_ab.txt)
+  const int y_bt = (hsplit && GLF_HSPLIT_Y64 && (long)B * (Np / 64) * (Np / 64) >= 512) ? 64 : split_bt;
   if (split_bt) {
     const long blocks = (long)B * (Np / split_bt) * (Np / split_bt);
+    const long yblocks = (long)B * (Np / y_bt) * (Np / y_bt);
     const int Tk = (2 + nc) * (Np / CG_KT), Ty = Np / CG_KT;
     ks = hsplit ? 1 : (int)std::max(1L, std::min<long>({4L, 256L / blocks, (long)Tk / 3}));
-    ys = nc ? (int)std::max(1L, std::min<long>({8L, 256L / (blocks * nc), (long)Ty / 3})) : 1;
+    ys = nc ? (int)std::max(1L, std::min<long>({8L, 256L / (yblocks * nc), (long)Ty / 3})) : 1;
   }
   // Hermitian pairs on two workgroups each: one N_p^2 slab slot per matrix holds the off-diagonal pairs' XU / XL blocks
   const bool hk2 = hsplit;
   const int kslots = (ks > 1 ? ks : 0) + (hk2 ? 1 : 0);
   const size_t per = (size_t)(split_bt ? 2 + nc + kslots + (ys > 1 ? nc * ys : 0)
                                        : glf_slots(Np, nc, herm)) * NN;
-  const size_t nticket = split_bt ? (size_t)B * (1 + nc) * (Np / split_bt) * (Np / split_bt) : 0;
+  const size_t nticket = split_bt ? (size_t)B * (1 + nc) * (Np / std::min(split_bt, y_bt)) * (Np / std::min(split_bt, y_bt)) : 0;
   const size_t st_elems = (size_t)B * per + (pad ? (size_t)B * NN : 0) + (nticket + 3) / 4;
   void* wst = nullptr;
   rc = workspace(WS_LINDBLAD, st_elems * sizeof(c128), &wst, st);
@@ -716,7 +723,9 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
     default: hipLaunchKernelGGL(KERN<128>, GRID, dim3(CG_WG), 0, st, p); break;                  \
   }
         if (nc > 0) {
-          QD_SPLIT(glf_split_y_kernel, dim3(nb * nb, nc, B * ys));
+          const int ynb = Np / y_bt;
+          if (y_bt == 64) hipLaunchKernelGGL(glf_split_y_kernel<64>, dim3(ynb * ynb, nc, B * ys), dim3(CG_WG), 0, st, p);
+          else QD_SPLIT(glf_split_y_kernel, dim3(nb * nb, nc, B * ys));
           QD_HIP(hipGetLastError());
         }
         if (hk2) {   // split_bt is 32 here
