@@ -20,6 +20,11 @@
  *     status back), and qd_deom_rk4_banded with status == NULL;
  *     host-array inputs (fvals of the driven entry points) are copied before
  *     the call returns;
+ *   - the asynchronous calls may be captured into a HIP graph (stream capture on
+ *     `stream`): their scratch then comes from stream-ordered allocations that
+ *     become the graph's own alloc / free nodes, so replays never share arena
+ *     slabs with uncaptured calls (the synchronising exceptions above cannot be
+ *     captured);
  *   - return 0 on success, a negative QD_E* code on failure; the message is
  *     available from qd_last_error() (thread-local).
  *

@@ -39,8 +39,9 @@ struct Slab {
   bool recorded;     // `done` has been recorded at least once
 };
 struct LiveRef {
-  Slab* slab;
+  Slab* slab;        // null: a stream-ordered allocation made while `st` was being captured into a graph
   hipStream_t st;
+  void* cap;         // that allocation (freed stream-ordered at the scope's end)
 };
 static std::mutex g_mu;              // guards g_slabs and every Slab's busy / recorded fields
 static std::vector<Slab*> g_slabs;
@@ -88,6 +89,10 @@ WsScope::~WsScope() {
   std::lock_guard<std::mutex> lk(g_mu);
   for (size_t k = g_live.size(); k > mark; --k) {
     Slab* s = g_live[k - 1].slab;
+    if (!s) {   // graph capture: the free becomes the graph's free node, ordered after the call's kernels
+      (void)hipFreeAsync(g_live[k - 1].cap, g_live[k - 1].st);
+      continue;
+    }
     // every kernel of this call that touches the slab is queued on st by now
     if (hipEventRecord(s->done, g_live[k - 1].st) == hipSuccess) {
       s->recorded = true;
@@ -110,6 +115,22 @@ int workspace(WsSlot slot, size_t bytes, void** ptr, hipStream_t st) {
   int dev = 0;
   QD_HIP(hipGetDevice(&dev));
   const size_t want = slab_size(bytes ? bytes : 16);
+  // A stream being captured into a HIP graph cannot wait on an event recorded outside the capture, and a slab handed
+  // to a graph would be reused behind the graph's back at every replay: captured calls take stream-ordered
+  // allocations instead, which become the graph's own alloc / free nodes.
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cap) == hipSuccess && cap == hipStreamCaptureStatusActive) {
+    void* p = nullptr;
+    hipError_t e = hipMallocAsync(&p, want, st);
+    if (e != hipSuccess) {
+      set_error("workspace allocation of %zu bytes inside a graph capture failed: %s", want, hipGetErrorString(e));
+      return QD_ENOMEM;
+    }
+    g_live.push_back({nullptr, st, p});
+    *ptr = p;
+    return QD_OK;
+  }
+  (void)hipGetLastError();
   std::lock_guard<std::mutex> lk(g_mu);
   Slab* best = nullptr;
   for (Slab* s : g_slabs)
@@ -142,7 +163,7 @@ int workspace(WsSlot slot, size_t bytes, void** ptr, hipStream_t st) {
     trim_idle(kIdleCap);
   }
   best->busy = true;
-  g_live.push_back({best, st});
+  g_live.push_back({best, st, nullptr});
   *ptr = best->ptr;
   return QD_OK;
 }
