@@ -562,9 +562,12 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   int split_bt = 0;
   bool hsplit = false;
   {
+#ifndef GLF_SPLIT_MINWG
+#define GLF_SPLIT_MINWG 512
+#endif
     int bt = 32;
     for (int v : {128, 64}) {
-      if (v < Np && Np % v == 0 && (long)B * (Np / v) * (Np / v) >= 512) {
+      if (v < Np && Np % v == 0 && (long)B * (Np / v) * (Np / v) >= GLF_SPLIT_MINWG) {
         bt = v;
         break;
       }
