@@ -450,7 +450,10 @@ SplitPlan split_plan(int Mp, int Np, int tiles) {
     return std::max(1, std::min(ceil_div(bt == 64 ? 512 : 256, blocks), std::max(1, tiles / 4)));
   };
   const int S128 = splits(128);
-  const bool small = (Mp / 128) * (Np / 128) * S128 < 256 || tiles / S128 < 32;
+#ifndef ENS_MIN_TILES128
+#define ENS_MIN_TILES128 32
+#endif
+  const bool small = (Mp / 128) * (Np / 128) * S128 < 256 || tiles / S128 < ENS_MIN_TILES128;
   const int bt = small ? 64 : 128;
   return {bt, splits(bt)};
 }
