@@ -13,20 +13,27 @@
 //   - split roles (round 5, while 2 B T^2 <= 256): a second workgroup per tile computes and publishes the Y_c tile,
 //     so the tile's k workgroup runs P r + r Q while the row's Y_c tiles are made (N = 128, one matrix: 35.5k ->
 //     39.6k steps/s, profiles/r05/lindblad/glf_single_split_roles.txt); otherwise one workgroup does both in turn;
+//   - at N_p = 128 the Y workgroup also makes the tile's P r (see PRY below);
 //   - per RK4 stage two hand-offs inside the launch: Y_c(bm, bn) = L_c[bm, :] r[:, bn] is published, then
 //     k(bm, bn) = P[bm, :] r[:, bn] + r[bm, :] Q[:, bn] + sum_c Y_c[bm, :] R_c[:, bn] needs the Y_c row block bm;
 //     the Horner update s' = rho + dt / (4 - m) k (glf.hip header) is published as the next stage input, whose row
 //     block bm and column block bn the next stage reads.
-// Hand-off form (MI355X_MICROARCH.md "Valid forms", table row 1, as deom.hip's banded kernel): 16-B write-through
-// (sc1) buffer stores of the payload, every wave drains (s_waitcnt vmcnt(0)), workgroup barrier, one lane stores the
-// epoch (relaxed agent atomic); consumers poll the producers' epochs with relaxed agent loads from one wave and load
-// the payload with 16-B sc1 buffer loads only (never a plain or flat load of handed-off bytes).
+// Hand-off form (cdna_hip_programming.md Guideline 16, R2: the data is the flag): every handed-off double carries the
+// parity of its epoch in its lowest mantissa bit, stored with 16-B write-through (sc1) buffer stores (no drain, no
+// barrier, no flag word); each consuming wave re-loads with 16-B sc1 buffer loads until every granule of its chunk
+// holds the expected parity (granules observed untorn on gfx950, MI355X_MICROARCH.md "Valid forms").  Stage outputs
+// and Y_c alternate between two buffers, so a buffer's previous contents (two stages back) carry the other parity,
+// and the host presets each buffer to the parity its first epoch does not have.  The tag perturbs a handed-off value
+// by at most one unit in its last place; it enters the result only through dt k(r), never the state rho the
+// workgroup keeps in registers.  Against the epoch-flag form (drain, barrier, flag, poll, barrier, load): N = 128, one
+// matrix 39.9k -> 43.5k steps/s, N = 64 50k -> 70k, N = 32 61k -> 92k (profiles/r05/lindblad/glf_single_r2.txt).
 // Buffer reuse: stage outputs and Y_c alternate between two buffers.  A workgroup overwrites r_{g-1} (buffer
-// (g+1) & 1) at the end of stage g only after it has seen stage g's Y_c of every workgroup of its row and stage g's
+// (g+1) & 1) at the end of stage g only after it has loaded stage g's Y_c of every workgroup of its row and stage g's
 // input from every workgroup of its row and column, i.e. after every reader of its r_{g-1} tile (the workgroups of
-// its row and column) finished stage g - 1; likewise Y_{g-2} (buffer g & 1) is overwritten in stage g after every
-// reader of it (its row) published stage g - 1's output, seen at the start of stage g.  Every spin is bounded; a
-// timeout sets *status (the host re-runs the batch on the split path).
+// its row and column) finished loading in stage g - 1 (their stage-g values depend on what they loaded); likewise
+// Y_{g-2} and the P r tile (buffer g & 1) are overwritten in stage g after every reader of them (the row; the tile's k
+// workgroup) produced stage g - 1's output, loaded at the start of stage g.  Every spin is bounded; a timeout sets
+// *status (the host re-runs the batch on the split path).
 // Observables: each workgroup sums Tr(E rho) over its tile after every step into a partial slot, and one small
 // kernel adds the T^2 partials in fixed order after the launch.
 #include "glf_kernel.hpp"
@@ -36,8 +43,7 @@ namespace qd {
 namespace {
 
 constexpr int SG_WG = 512;
-constexpr int SG_FLAG_STRIDE = 16;              // 64-B epoch slots
-constexpr unsigned SG_SPIN_LIMIT = 1u << 22;    // polls (one round trip each, s_sleep between): ~2 s
+constexpr unsigned SG_SPIN_LIMIT = 1u << 22;    // sweeps (one round trip each, s_sleep between): ~2 s
 
 struct SingleParams {
   const c128* P;       // [Np][Np] padded GLF operators (glf_run's operator workspace)
@@ -47,8 +53,7 @@ struct SingleParams {
   const c128* eT;      // [ne][Np][Np] E_m^T
   c128* rho;           // [B][Np][Np] state (in / out)
   c128* rbuf;          // [2][B][Np][Np] stage outputs
-  c128* ybuf;          // [2][nc][B][Np][Np]
-  unsigned* flags;     // [B T^2][2][SG_FLAG_STRIDE]: 0 = stage output epoch, 1 = Y epoch
+  c128* ybuf;          // [2][nc][B][Np][Np] Y_c, then [2][B][Np][Np] P r tiles (split roles)
   c128* obs_part;      // [B][total_steps + 1][ne][T^2]
   c128* snap;          // [B][nsave][N][N] or null
   int* status;
@@ -68,6 +73,52 @@ struct SingleParams {
 #else
 #define SG_MARK(k)
 #endif
+
+// the epoch parity t in the lowest mantissa bit of both halves (at most one unit in the last place)
+__device__ __forceinline__ c128 sg_tag(c128 v, unsigned t) {
+  const unsigned long long a = __builtin_bit_cast(unsigned long long, v.re);
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v.im);
+  return cmk(__builtin_bit_cast(double, (a & ~1ull) | t), __builtin_bit_cast(double, (b & ~1ull) | t));
+}
+__device__ __forceinline__ bool sg_has(c128 v, unsigned t) {
+  const unsigned a = (unsigned)__builtin_bit_cast(unsigned long long, v.re);
+  const unsigned b = (unsigned)__builtin_bit_cast(unsigned long long, v.im);
+  return (((a ^ t) | (b ^ t)) & 1u) == 0;
+}
+// One wave loads its NL handed-off granules (byte offsets off(q)) with sc1 loads and re-loads the ones without parity
+// t until all have it.  False after SG_SPIN_LIMIT sweeps or when another workgroup reported a timeout (*status).
+#ifndef SG_SLEEP_K
+#define SG_SLEEP_K 1
+#endif
+#ifndef SG_SLEEP_Y
+#define SG_SLEEP_Y 1
+#endif
+template <int SL, int NL, typename Off>
+__device__ __forceinline__ bool sg_sweep(c128 (&v)[NL], __amdgpu_buffer_rsrc_t rs, Off off, unsigned t, int* status,
+                                         int lane) {
+#pragma unroll
+  for (int q = 0; q < NL; ++q) v[q] = ld16_sc1(rs, off(q));
+  for (unsigned spins = 0;;) {
+    bool okq[NL], ok = true;
+#pragma unroll
+    for (int q = 0; q < NL; ++q) {
+      okq[q] = sg_has(v[q], t);
+      ok &= okq[q];
+    }
+    if (__all(ok)) return true;
+    ++spins;
+    if (spins > SG_SPIN_LIMIT ||
+        ((spins & 255) == 0 && __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
+      if (lane == 0) __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(SL);
+    asm volatile("" ::: "memory");   // the granules change under us: re-load, never reuse the value
+#pragma unroll
+    for (int q = 0; q < NL; ++q)
+      if (!okq[q]) v[q] = ld16_sc1(rs, off(q));
+  }
+}
 
 // one complex k-step of a 16 x 16 tile: acc += a b (a: A fragment, b: B fragment of v_mfma_f64_16x16x4_f64)
 __device__ __forceinline__ void sg_mac(d4& re, d4& im, c128 a, c128 b) {
@@ -103,42 +154,56 @@ struct SgAcc {
   }
 };
 
-// KS: k-steps of 4 per wave (Np = 32 KS), NC collapse operators / GLF pairs, M3: SgAcc form
-template <int KS, int NC, bool M3>
+// KS: k-steps of 4 per wave (Np = 32 KS), NC collapse operators / GLF pairs, M3: SgAcc form, SPLIT: p.split (a
+// workgroup holds only its role's operator fragments)
+template <int KS, int NC, bool M3, bool SPLIT>
 __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
   constexpr int T = 2 * KS, Np = 32 * KS, NN = Np * Np;
-  __shared__ c128 red[8][256];
-  __shared__ int sAbort;
-  // split: workgroups [0, B T^2) are the tiles' k workgroups, [B T^2, 2 B T^2) their Y workgroups; a tile's two
-  // epoch words (0: stage output, 1: Y_c) are written by its k and its Y workgroup respectively
-  const int nk = p.split ? (int)gridDim.x / 2 : (int)gridDim.x;
-  const bool yrole = p.split && (int)blockIdx.x >= nk;
+  // partial tiles of the reductions, by stage parity: a wave writes stage g + 2's partials only after the barrier of
+  // stage g + 1, which every wave reaches after reading stage g's (there is no other barrier between stages)
+  __shared__ c128 red[2][8][256];
+  __shared__ int sAbort[2];   // a wave's timed-out sweep in stage g sets sAbort[g & 1]; read after the next barrier
+  // split: workgroups [0, B T^2) are the tiles' k workgroups, [B T^2, 2 B T^2) their Y workgroups
+  const int nk = SPLIT ? (int)gridDim.x / 2 : (int)gridDim.x;
+  const bool yrole = SPLIT && (int)blockIdx.x >= nk;
   const int w = yrole ? (int)blockIdx.x - nk : (int)blockIdx.x;
   const int b = w / (T * T), tile = w - b * (T * T), bm = tile / T, bn = tile - bm * T;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lk = lane >> 4;
   const int kb = wave * 4 * KS;
-  // constant operator fragments, loaded once: A rows bm (P, L_c), B columns bn (Q, R_c)
-  c128 aP[KS], bQ[KS], aL[NC > 0 ? NC : 1][KS], bR[NC > 0 ? NC : 1][KS];
+  // split roles at N_p = 128: the Y workgroup also makes the tile's P r (from the column it reads anyway), so the k
+  // workgroup ingests the row of r and the row of Y_c only -- per-CU load bandwidth, not the MFMAs, bounds the stage
+  // there (N = 128, one matrix: 42.2k -> 43.5k steps/s; at N_p = 32 / 64 the extra hand-off costs more than it saves,
+  // profiles/r05/lindblad/glf_single_r2.txt)
+  constexpr bool PRY = SPLIT && KS == 4;
+  // constant operator fragments, loaded once: A rows bm (L_c at [c], P at [NC]), B columns bn (R_c, Q); with split
+  // roles a Y workgroup holds the A fragments and a k workgroup the B fragments, in the same registers (a k workgroup
+  // that makes P r itself holds P in aPk)
+  c128 fA[NC + 1][KS], fBj[NC + 1][KS], aPk[SPLIT && !PRY ? KS : 1];
+  c128(&fB)[NC + 1][KS] = SPLIT ? fA : fBj;
 #pragma unroll
   for (int q = 0; q < KS; ++q) {
     const int k = kb + 4 * q + lk;
-    aP[q] = p.P[(bm * 16 + lr) * Np + k];
-    bQ[q] = p.Q[k * Np + bn * 16 + lr];
+    if constexpr (SPLIT && !PRY)
+      if (!yrole) aPk[q] = p.P[(bm * 16 + lr) * Np + k];
+    if (!SPLIT || yrole) {
+      fA[NC][q] = p.P[(bm * 16 + lr) * Np + k];
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      aL[c][q] = p.Lop[(size_t)c * NN + (bm * 16 + lr) * Np + k];
-      bR[c][q] = p.Rop[(size_t)c * NN + k * Np + bn * 16 + lr];
+      for (int c = 0; c < NC; ++c) fA[c][q] = p.Lop[(size_t)c * NN + (bm * 16 + lr) * Np + k];
+    }
+    if (!SPLIT || !yrole) {
+      fB[NC][q] = p.Q[k * Np + bn * 16 + lr];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) fB[c][q] = p.Rop[(size_t)c * NN + k * Np + bn * 16 + lr];
     }
   }
   const bool owner = tid < 256 && !yrole;
   const int orow = bm * 16 + ((tid >> 4) & 15), ocol = bn * 16 + (tid & 15);
   c128* rhob = p.rho + (size_t)b * NN;
   c128 rh = owner ? rhob[orow * Np + ocol] : cmk(0, 0);
-  if (tid == 0) sAbort = 0;
+  if (tid < 2) sAbort[tid] = 0;
+  __syncthreads();
   const int mats = nk / (T * T);
   const int slab = mats * NN * (int)sizeof(c128);   // bytes of one [B][Np][Np] buffer
-  unsigned* fl = p.flags;
-  auto flag_at = [&](int wg, int kind) { return fl + ((size_t)wg * 2 + kind) * SG_FLAG_STRIDE; };
 
   // Tr(E_m rho) partial over this tile -> obs_part (fixed-order sums: lanes of a wave, then the 4 owner waves)
   auto observe = [&](int gs) {
@@ -151,60 +216,31 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
         v.im += __shfl_xor(v.im, off, 64);
       }
       __syncthreads();
-      if (lane == 0) red[0][wave] = v;
+      if (lane == 0) red[0][0][wave] = v;
       __syncthreads();
       if (tid == 0) {
-        c128 s = red[0][0];
-        for (int q = 1; q < 4; ++q) s = cadd(s, red[0][q]);
+        c128 s = red[0][0][0];
+        for (int q = 1; q < 4; ++q) s = cadd(s, red[0][0][q]);
         p.obs_part[(((size_t)b * (p.total_steps + 1) + gs) * p.ne + m) * (T * T) + tile] = s;
       }
     }
   };
   if (p.ne > 0 && p.step0 == 0 && !yrole) observe(0);
 
-  // fixed-order sum of the 8 waves' partial tiles; returns element tid (tid < 256) of the tile
-  auto reduce = [&](const SgAcc<M3>& acc) -> c128 {
+  // fixed-order sum of the 8 waves' partial tiles (slot par); returns element tid (tid < 256) of the tile
+  auto reduce = [&](const SgAcc<M3>& acc, int par) -> c128 {
     d4 re, im;
     acc.result(re, im);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[wave][(lk + 4 * r) * 16 + lr] = cmk(re[r], im[r]);
+    for (int r = 0; r < 4; ++r) red[par][wave][(lk + 4 * r) * 16 + lr] = cmk(re[r], im[r]);
     __syncthreads();
     c128 v = cmk(0, 0);
     if (tid < 256) {
-      v = red[0][tid];
+      v = red[par][0][tid];
 #pragma unroll
-      for (int q = 1; q < 8; ++q) v = cadd(v, red[q][tid]);
+      for (int q = 1; q < 8; ++q) v = cadd(v, red[par][q][tid]);
     }
     return v;
-  };
-  // wave 0 waits until every listed workgroup's epoch word `kind` reaches `target`; the other waves wait at the barrier
-  auto wait_for = [&](int nsrc, int kind, unsigned target, auto&& src_of) {
-    if (wave == 0) {
-      const unsigned* f = lane < nsrc ? flag_at(src_of(lane), kind) : nullptr;
-      unsigned spins = 0;
-      for (;;) {
-        const bool ok = !f || __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target;
-        if (__all(ok)) break;
-        ++spins;
-        if (spins > SG_SPIN_LIMIT ||
-            ((spins & 255) == 0 && __hip_atomic_load(p.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
-          if (lane == 0) {
-            sAbort = 1;
-            __hip_atomic_store(p.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the payload loads below the poll
-    __syncthreads();
-    return sAbort == 0;
-  };
-  auto publish = [&](int kind, unsigned epoch) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's write-through stores are complete
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(flag_at(w, kind), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
 
 #ifdef QD_PHASE_TIMING
@@ -212,75 +248,115 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
 #endif
   const int G4 = 4 * p.nsteps;
   for (int g = 0; g < G4; ++g) {
-    const int s = g >> 2, m = g & 3;
-    // ---- stage input r_g: the caller's rho at g = 0, else the previous stage's output in rbuf[g & 1]
+    const int s = g >> 2, m = g & 3, par = g & 1;
+    // r_j (j >= 1) lives in rbuf[j & 1] with parity (j >> 1) & 1, Y_g in ybuf[g & 1] with parity (g >> 1) & 1
+    const unsigned tr = (unsigned)(g >> 1) & 1u, ty = tr;
+    bool good = true;
+    // ---- stage input r_g: the caller's rho at g = 0, else the previous stage's output in rbuf[g & 1]; column bn
+    // and row bm (a Y workgroup reads the column only)
     const c128* rin = g == 0 ? p.rho : p.rbuf + (size_t)(g & 1) * mats * NN;
-    // column bn and row bm of r_g (a Y workgroup reads the column only).  Buffer reuse with split roles: the k
-    // workgroup of (l, bn) finishing stage g - 1 implies the Y workgroup of (l, bn) published stage g - 1's Y_c (it
-    // waited for it), i.e. finished reading r_{g-1}; and a Y workgroup entering stage g has seen its own tile's k
-    // workgroup finish stage g - 1, which had seen its row finish stage g - 2 (the readers of Y_{g-2}).
-    if (g > 0 && !wait_for(yrole ? T : 2 * T, 0, (unsigned)g, [&](int l) {
-          return b * T * T + (l < T ? l * T + bn : bm * T + (l - T));
-        }))
-      break;
-    SG_MARK(0)
     const __amdgpu_buffer_rsrc_t rr = sc1_rsrc(rin, slab);
     c128 rcol[KS], rrow[KS];
+    auto col_off = [&](int q) { return ((b * Np + kb + 4 * q + lk) * Np + bn * 16 + lr) * 16; };
+    auto row_off = [&](int q) { return ((b * Np + bm * 16 + lr) * Np + kb + 4 * q + lk) * 16; };
+    if (g == 0) {
 #pragma unroll
-    for (int q = 0; q < KS; ++q) {
-      const int k = kb + 4 * q + lk;
-      rcol[q] = ld16_sc1(rr, ((b * Np + k) * Np + bn * 16 + lr) * 16);
-      rrow[q] = ld16_sc1(rr, ((b * Np + bm * 16 + lr) * Np + k) * 16);
+      for (int q = 0; q < KS; ++q) {
+        if (yrole || !PRY) rcol[q] = ld16_sc1(rr, col_off(q));
+        if (!yrole) rrow[q] = ld16_sc1(rr, row_off(q));
+      }
+    } else if (yrole) {
+      good = sg_sweep<SG_SLEEP_Y>(rcol, rr, col_off, tr, p.status, lane);
+    } else if (PRY) {   // the k workgroup reads the row only (its Y workgroup makes P r)
+      good = sg_sweep<SG_SLEEP_K>(rrow, rr, row_off, tr, p.status, lane);
+    } else if (NC > 1 && KS == 4) {   // (one sweep of both would spill here)
+      good = sg_sweep<SG_SLEEP_K>(rcol, rr, col_off, tr, p.status, lane);
+      if (good) good = sg_sweep<SG_SLEEP_K>(rrow, rr, row_off, tr, p.status, lane);
+    } else {   // column and row in one sweep: one round trip per pass for both
+      c128 rcr[2 * KS];
+      good = sg_sweep<SG_SLEEP_K>(rcr, rr, [&](int q) { return q < KS ? col_off(q) : row_off(q - KS); }, tr,
+                                  p.status, lane);
+#pragma unroll
+      for (int q = 0; q < KS; ++q) {
+        rcol[q] = rcr[q];
+        rrow[q] = rcr[KS + q];
+      }
     }
-    // ---- Y_c(bm, bn) = L_c[bm, :] r[:, bn], published for the k phase of the row
-    c128* ybase = p.ybuf + (size_t)(g & 1) * NC * mats * NN;
-    if (NC > 0 && (yrole || !p.split)) {
-      const __amdgpu_buffer_rsrc_t ry = sc1_rsrc(ybase, NC * slab);
+    if (!good && lane == 0) sAbort[par] = 1;
+    SG_MARK(0)
+    // ---- Y_c(bm, bn) = L_c[bm, :] r[:, bn], handed to the k phase of the row
+    // ybuf: [2][NC][B][Np][Np] Y_c, then (split roles) [2][B][Np][Np] P r tiles, one descriptor over both
+    const int yo = (g & 1) * NC * mats * NN, vo = (2 * NC + (g & 1)) * mats * NN;
+    const __amdgpu_buffer_rsrc_t ry = sc1_rsrc(p.ybuf, 2 * (NC + 1) * slab);
+    if (NC > 0 && (yrole || !SPLIT)) {
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         SgAcc<M3> acc;
 #pragma unroll
-        for (int q = 0; q < KS; ++q) acc.mac(aL[c][q], rcol[q]);
-        const c128 y = reduce(acc);
-        if (tid < 256) st16_sc1(ry, (((c * mats + b) * Np + orow) * Np + ocol) * 16, y);
-        __syncthreads();   // red is reused by the next reduction
+        for (int q = 0; q < KS; ++q) acc.mac(fA[c][q], rcol[q]);
+        const c128 y = reduce(acc, par);
+        if (c + 1 < NC) __syncthreads();   // the slot is reused by the next reduction
+        if (tid < 256) st16_sc1(ry, (yo + ((c * mats + b) * Np + orow) * Np + ocol) * 16, sg_tag(y, ty));
       }
-      publish(1, (unsigned)(g + 1));
-    }
-    if (yrole) {
-      SG_MARK(1)
-      continue;
+      if (yrole) {
+        if constexpr (PRY) {   // P r (bm, bn) for the tile's k workgroup
+          SgAcc<M3> av;
+#pragma unroll
+          for (int q = 0; q < KS; ++q) av.mac(fA[NC][q], rcol[q]);
+          __syncthreads();   // the Y reduction's slot
+          const c128 pv = reduce(av, par);
+          if (tid < 256) st16_sc1(ry, (vo + (b * Np + orow) * Np + ocol) * 16, sg_tag(pv, ty));
+        }
+        if (sAbort[par]) break;   // read after the reductions' barriers, which a timed-out wave reached
+        SG_MARK(1)
+        continue;
+      }
     }
     SG_MARK(1)
     // ---- k(bm, bn) = P r + r Q + sum_c Y_c R_c; the P r + r Q part runs while the row's Y_c are handed over
     SgAcc<M3> acc;
+    if constexpr (!SPLIT) {
 #pragma unroll
-    for (int q = 0; q < KS; ++q) acc.mac(aP[q], rcol[q]);
+      for (int q = 0; q < KS; ++q) acc.mac(fA[NC][q], rcol[q]);
+    } else if constexpr (!PRY) {
 #pragma unroll
-    for (int q = 0; q < KS; ++q) acc.mac(rrow[q], bQ[q]);
-    SG_MARK(2)
-    if constexpr (NC > 0) {
-      if (!wait_for(T, 1, (unsigned)(g + 1), [&](int l) { return b * T * T + bm * T + l; })) break;
-      SG_MARK(3)
-      const __amdgpu_buffer_rsrc_t ry = sc1_rsrc(ybase, NC * slab);
-      c128 yrow[NC][KS];
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-#pragma unroll
-        for (int q = 0; q < KS; ++q)
-          yrow[c][q] = ld16_sc1(ry, (((c * mats + b) * Np + bm * 16 + lr) * Np + kb + 4 * q + lk) * 16);
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-#pragma unroll
-        for (int q = 0; q < KS; ++q) acc.mac(yrow[c][q], bR[c][q]);
+      for (int q = 0; q < KS; ++q) acc.mac(aPk[q], rcol[q]);
     }
-    const c128 kv = reduce(acc);
+#pragma unroll
+    for (int q = 0; q < KS; ++q) acc.mac(rrow[q], fB[NC][q]);
+    SG_MARK(2)
+    c128 pv = cmk(0, 0);   // PRY: the P r tile of the Y workgroup (element tid & 255)
+    if constexpr (NC > 0) {
+      if (!SPLIT) __syncthreads();   // this stage's Y reductions read the slot the k reduction writes
+      c128 yrow[NC][KS];
+      auto y_off = [&](int c, int q) {
+        return (yo + ((c * mats + b) * Np + bm * 16 + lr) * Np + kb + 4 * q + lk) * 16;
+      };
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (good) good = sg_sweep<SG_SLEEP_K>(yrow[c], ry, [&](int q) { return y_off(c, q); }, ty, p.status, lane);
+      SG_MARK(3)
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int q = 0; q < KS; ++q) acc.mac(yrow[c][q], fB[c][q]);
+      if (PRY && good) {   // the P r element (tid & 255), published after the tile's Y_c, sought under the MFMAs
+        c128 pe[1];
+        const int v_off = (vo + (b * Np + bm * 16 + ((tid >> 4) & 15)) * Np + bn * 16 + (tid & 15)) * 16;
+        good = sg_sweep<SG_SLEEP_K>(pe, ry, [&](int) { return v_off; }, ty, p.status, lane);
+        pv = pe[0];
+      }
+      if (!good && lane == 0) sAbort[par] = 1;
+    }
+    const c128 kv = cadd(reduce(acc, par), pv);
+    if (sAbort[par]) break;
     SG_MARK(4)
     const double hc = rk4_horner_coef(p.dt, m);
     const c128 v = cadd(rh, cscale(kv, hc));
     if (m == 3) rh = v;
-    if (owner && g + 1 < G4) st16_sc1(sc1_rsrc(p.rbuf + (size_t)((g + 1) & 1) * mats * NN, slab),
-                                   ((b * Np + orow) * Np + ocol) * 16, v);
+    if (owner && g + 1 < G4)
+      st16_sc1(sc1_rsrc(p.rbuf + (size_t)((g + 1) & 1) * mats * NN, slab), ((b * Np + orow) * Np + ocol) * 16,
+               sg_tag(v, (unsigned)((g + 1) >> 1) & 1u));
     if (m == 3) {
       const int gs = p.step0 + s + 1;
       if (p.snap && p.save_every > 0 && gs % p.save_every == 0) {
@@ -290,8 +366,6 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
       }
       if (p.ne > 0) observe(gs);
     }
-    if (g + 1 < G4) publish(0, (unsigned)(g + 1));
-    else __syncthreads();
     SG_MARK(5)
   }
   if (owner) rhob[orow * Np + ocol] = rh;
@@ -311,14 +385,21 @@ __global__ void glf_single_obs_kernel(const c128* part, int T2, long n, c128* ob
   }
 }
 
-template <int KS, int NC, bool M3>
-hipError_t sg_launch3(SingleParams p, int grid, bool coop, hipStream_t st) {
+template <int KS, int NC, bool M3, bool SPLIT>
+hipError_t sg_launch4(SingleParams p, int grid, bool coop, hipStream_t st) {
   if (!coop) {
-    hipLaunchKernelGGL((glf_single_kernel<KS, NC, M3>), dim3(grid), dim3(SG_WG), 0, st, p);
+    hipLaunchKernelGGL((glf_single_kernel<KS, NC, M3, SPLIT>), dim3(grid), dim3(SG_WG), 0, st, p);
     return hipGetLastError();
   }
   void* args[] = {(void*)&p};
-  return hipLaunchCooperativeKernel((const void*)glf_single_kernel<KS, NC, M3>, dim3(grid), dim3(SG_WG), args, 0, st);
+  return hipLaunchCooperativeKernel((const void*)glf_single_kernel<KS, NC, M3, SPLIT>, dim3(grid), dim3(SG_WG), args,
+                                    0, st);
+}
+template <int KS, int NC, bool M3>
+hipError_t sg_launch3(SingleParams p, int grid, bool coop, hipStream_t st) {
+  if constexpr (NC > 0)
+    if (p.split) return sg_launch4<KS, NC, M3, true>(p, grid, coop, st);
+  return sg_launch4<KS, NC, M3, false>(p, grid, coop, st);
 }
 // The 3-product complex MACs on a half-filled chip (<= 128 workgroups), the 4-product ones above: N = 128, one matrix
 // 29.7k -> 34.9k steps/s and two 61.7k -> 69.4k with 3 products, four (256 workgroups) 117k -> 103k; N = 32, 64
@@ -349,9 +430,9 @@ int glf_single_run(const c128* P, const c128* Q, const c128* Lop, const c128* Ro
   if (nsteps <= 0 && ne == 0) return QD_OK;
   const int T = Np / 16, T2 = T * T;
   const size_t NN = (size_t)Np * Np;
-  const size_t flag_bytes = ((size_t)B * T2 * 2 * SG_FLAG_STRIDE + 4) * sizeof(unsigned);
+  const size_t flag_bytes = 16;   // *status, padded
   const size_t obs_elems = ne ? (size_t)B * (nsteps + 1) * ne * T2 : 0;
-  const size_t elems = 2 * (size_t)B * NN + 2 * (size_t)(nc > 0 ? nc : 0) * B * NN + obs_elems;
+  const size_t elems = 2 * (size_t)B * NN + 2 * (size_t)(nc > 0 ? nc + 1 : 0) * B * NN + obs_elems;
   void* w = nullptr;
   int rc = workspace(WS_LINDBLAD, elems * sizeof(c128) + flag_bytes, &w, st);
   if (rc) return rc;
@@ -364,9 +445,8 @@ int glf_single_run(const c128* P, const c128* Q, const c128* Lop, const c128* Ro
   p.rho = rho;
   p.rbuf = (c128*)w;
   p.ybuf = p.rbuf + 2 * (size_t)B * NN;
-  p.obs_part = ne ? p.ybuf + 2 * (size_t)nc * B * NN : nullptr;
-  p.flags = (unsigned*)((c128*)w + elems);
-  p.status = (int*)(p.flags + (size_t)B * T2 * 2 * SG_FLAG_STRIDE);
+  p.obs_part = ne ? p.ybuf + 2 * (size_t)(nc > 0 ? nc + 1 : 0) * B * NN : nullptr;
+  p.status = (int*)((c128*)w + elems);
   p.N = N;
   p.ne = ne;
   p.nsteps = nsteps;
@@ -376,7 +456,12 @@ int glf_single_run(const c128* P, const c128* Q, const c128* Lop, const c128* Ro
   p.nsave = save_every > 0 ? nsteps / save_every : 0;
   p.snap = p.nsave > 0 ? snap : nullptr;
   p.dt = dt;
-  QD_HIP(hipMemsetAsync(p.flags, 0, flag_bytes, st));
+  // every handed-off buffer preset to the parity its first epoch does not have: r_1 (buffer 1) and r_2 (buffer 0)
+  // carry parities 0 and 1, Y_0 and Y_1 (buffers 0 and 1) both 0; bytes of 0x01 make every double's lowest bit 1
+  QD_HIP(hipMemsetAsync(p.status, 0, flag_bytes, st));
+  QD_HIP(hipMemsetAsync(p.rbuf, 0, (size_t)B * NN * sizeof(c128), st));
+  QD_HIP(hipMemsetAsync(p.rbuf + (size_t)B * NN, 1, (size_t)B * NN * sizeof(c128), st));
+  if (nc > 0) QD_HIP(hipMemsetAsync(p.ybuf, 1, 2 * (size_t)(nc + 1) * B * NN * sizeof(c128), st));
   p.tim = nullptr;
 #ifdef QD_PHASE_TIMING
   void* tw = nullptr;

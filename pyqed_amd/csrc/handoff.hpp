@@ -3,7 +3,8 @@
 // wave drains (s_waitcnt vmcnt(0)), a workgroup barrier, then one lane stores the epoch word (relaxed agent atomic);
 // the consumer polls the epochs with relaxed agent loads from one wave, joins a workgroup barrier, and loads the
 // handed-off bytes with 16-B sc1 buffer loads only (never a plain or flat load of them).  One workgroup per CU.
-// Users: glf_single.hip (one trajectory), deom.hip (banded hierarchy; the pipelined stage kernel's plain buffer loads).
+// Users: deom.hip (banded hierarchy; the pipelined stage kernel's plain buffer loads); glf_single.hip uses its
+// loaders with the R2 form instead (the data is the flag, glf_single.hip header).
 #pragma once
 #include "qd_common.hpp"
 
