@@ -309,14 +309,17 @@ int qd_deom_rk4_ado_major(qd_c128* ados, int B, int nmax, int K, int ns,
  * tier bands (DEOMSolver.run, pyqed/heom/deom.py:1072-1114, with rk4 /
  * rem_cal :641-766).  Workgroup w owns ADO rows [band_lo[w], band_lo[w+1]) and
  * keeps their stage input plus its halo rows in LDS; the bands hand each RK4
- * stage's rows to each other inside the launch (write-through stores, one
- * epoch word per band).  Band tables (device int32, deom_shard.make_plans):
+ * stage's rows to each other inside the launch (write-through stores whose
+ * doubles carry the stage's parity in their lowest mantissa bit: the data is
+ * the flag).  Band tables (device int32, deom_shard.make_plans):
  * halo_off[nbands+1] / halo_idx (global halo rows per band), src_off[nbands+1]
  * / src (bands owning them), lminus / lplus [nmax][K] local rows (owned rows
  * first, then the band's halo rows; -1 absent); max_own / max_loc the largest
  * owned / owned + halo row counts.  ns in [2, 4], K <= 8,
  * max_own * (ns == 2 ? 4 : 16) <= 1024, (2 + nmod + max_loc) ns^2 16 B <= 160 KB.
- * Other arguments and results as qd_deom_rk4 with B = 1 (bit-identical).
+ * Other arguments and results as qd_deom_rk4 with B = 1 (bit-identical with
+ * one band; with several a halo value differs by at most one unit in its last
+ * place, which reaches the result through dt x stencil: within 1e-13).
  * status: device int32 set to 1 if a hand-off timed out (bands not
  * co-resident; results invalid, ados overwritten), or null: the call then
  * synchronises the stream and returns QD_EHIP in that case.  The launch is

@@ -1441,26 +1441,29 @@ namespace {
 // ordered, so a band's outside neighbours sit in tiers l -/+ 1 of it).  Its LDS holds the stage input of its owned
 // rows followed by its halo rows (local rows: lminus / lplus), its registers hold rho and the RK4 accumulator of
 // its owned elements for the whole run.  Per stage a workgroup
-//   1. waits until every band owning one of its halo rows (src) has published the previous stage (ONE wave polls
-//      the sources' epoch words, relaxed agent-scope loads, s_sleep between polls, bounded spin);
-//   2. loads its halo rows of that stage's output with sc1 (L1-bypassing) loads into LDS;
-//   3. evaluates the stencil of the group kernel (same arithmetic, same operand order: bit-identical results) from
-//      LDS and runs the RK4 epilogue in registers;
-//   4. writes the next stage input to its LDS rows and, write-through (sc1 stores), to buf[g & 1]; every wave
-//      drains its stores (s_waitcnt vmcnt(0)), the workgroup meets at a barrier and one lane stores the new epoch.
-// That is the MI355X_MICROARCH.md hand-off form "sc1 payload + drained flag, sc1 loads" (no release / acquire
-// fences).  Reuse of buf[g & 1] is safe: a band overwrites it at stage g only after every source has published
-// stage g - 1, i.e. finished reading it, and the neighbour relation is symmetric (sources == consumers).
+//   1. loads its halo rows of the previous stage's output with sc1 (L1-bypassing) 16-B loads into LDS, re-loading
+//      every element whose doubles do not yet carry that stage's parity in their lowest mantissa bit (the data is
+//      the flag, cdna_hip_programming.md Guideline 16 R2; s_sleep between sweeps, bounded spin);
+//   2. evaluates the stencil of the group kernel (same arithmetic, same operand order) from LDS and runs the RK4
+//      epilogue in registers;
+//   3. writes the next stage input to its LDS rows (exact) and, write-through (sc1 stores) with its parity in every
+//      double's lowest bit, to buf[g & 1]; no drain, no barrier, no epoch word.
+// A halo value is thus off by at most one unit in its last place; it reaches the result only through dt x stencil
+// (never a band's own state, which stays exact in registers and LDS; the last stage stores untagged): within 1e-13 of
+// the stage launches, bit-identical with one band.  Against the epoch-word form (drain, barrier, flag; one wave
+// polls, barrier, loads) 100-104k -> 115k steps/s at 6188 ADOs, 73.6k -> 85.2k at 18,564
+// (profiles/r05/deom/band_r2_handoff_ab.txt).  Reuse of buf[g & 1] is safe: a band overwrites its rows at stage g
+// after it loaded stage g - 1's rows of every source, which each stored only after loading its halo of stage g - 2
+// (its halo loads complete before its stencil's barrier), and the neighbour relation is symmetric (sources ==
+// consumers).  Both buffers are preset to parity 1 (stages 0 and 1, their first writers, carry 0).
 // Stage 0 of step 0 reads the caller's ados (written before the launch); the final rho is buf[1] (the output of
 // the last stage 3), copied to ados behind the launch.  A spin that exceeds its bound (bands not co-resident)
 // sets *status = 1 and every band leaves its loop (results then invalid; the host reports it).
-constexpr int BAND_FLAG_STRIDE = 16;          // 64-B epoch slots
-constexpr unsigned BAND_SPIN_LIMIT = 1u << 21;  // polls (one round trip each): ~1 s
+constexpr unsigned BAND_SPIN_LIMIT = 1u << 21;  // sweeps (one round trip each): ~1 s
 
 struct BandParams {
   const c128* ados;      // [nmax][ns2] rho at t = 0 (read at stage 0 of step 0 only)
   c128* buf;             // [2][nmax][ns2] stage outputs (hand-off buffers)
-  unsigned* flags;       // [nbands][BAND_FLAG_STRIDE] last published epoch (stage g output = g + 1)
   int* status;           // [1] 0 = ok, 1 = a hand-off timed out
   const int* band_lo;    // [nbands + 1]
   const int* halo_off;   // [nbands + 1]
@@ -1497,12 +1500,30 @@ __device__ __forceinline__ void st_sc1(c128* q, c128 v) {
   __hip_atomic_store(&q->im, v.im, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// R2 hand-off granules (cdna_hip_programming.md Guideline 16: the data is the flag): the parity of the producing
+// stage in the lowest mantissa bit of both halves of a handed-off element (at most one unit in the last place; it
+// reaches the result only through dt times the stencil of a neighbour, never a band's own state)
+__device__ __forceinline__ c128 band_tag(c128 v, unsigned t) {
+  const unsigned long long x = __builtin_bit_cast(unsigned long long, v.re);
+  const unsigned long long y = __builtin_bit_cast(unsigned long long, v.im);
+  return cmk(__builtin_bit_cast(double, (x & ~1ull) | t), __builtin_bit_cast(double, (y & ~1ull) | t));
+}
+__device__ __forceinline__ bool band_has(c128 v, unsigned t) {
+  const unsigned x = (unsigned)__builtin_bit_cast(unsigned long long, v.re);
+  const unsigned y = (unsigned)__builtin_bit_cast(unsigned long long, v.im);
+  return (((x ^ t) | (y ^ t)) & 1u) == 0;
+}
+// every 256 sweeps: has another band reported a timeout?
+__device__ __forceinline__ bool band_abort_seen(const int* status, unsigned spins) {
+  return (spins & 255) == 0 && __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
+
 // FAST (ns = 2, K == KMAX, one bath mode): the mode loop, the K bound and H / Q fold to constants and registers.
 template <int G, int KMAX, bool NS2, int TPB, bool FAST>
 __global__ __launch_bounds__(TPB) void deom_band_kernel(BandParams p) {
   static_assert(!FAST || NS2, "FAST is the ns = 2 specialisation");
   extern __shared__ c128 deom_lds[];
-  __shared__ int sAbort;
+  __shared__ int sAbort[2];   // a band's timed-out sweep in stage g sets sAbort[g & 1]
   const int ns = NS2 ? 2 : p.ns, ns2 = ns * ns, K = FAST ? KMAX : p.K;
   c128* sH = deom_lds;
   c128* sQ = deom_lds + ns2;
@@ -1586,7 +1607,7 @@ __global__ __launch_bounds__(TPB) void deom_band_kernel(BandParams p) {
   c128 r0 = valid ? p.ados[(size_t)n * ns2 + e] : cmk(0, 0);
   c128 acc = cmk(0, 0);
   if (valid) sX[(size_t)a * ns2 + e] = r0;
-  if (tid == 0) sAbort = 0;
+  if (tid < 2) sAbort[tid] = 0;
   // LDS element index of the own and neighbour elements this lane reads every stage; absent neighbours read the
   // zero row after the band's rows (the host sizes LDS for max_loc + 1 rows; halo writes never reach it)
   const int zrow = p.max_loc;
@@ -1677,33 +1698,8 @@ __global__ __launch_bounds__(TPB) void deom_band_kernel(BandParams p) {
 #ifdef QD_PHASE_TIMING
     const unsigned long long t0 = wall_clock64();
 #endif
-    // 1. wait for every source band's stage g - 1 output (one wave polls; the others wait at the barrier)
-    if (g > 0 && tid < 64) {
-      // lane j < nsrc watches source j's epoch word (one poll in flight: several in flight, checked oldest first,
-      // measured slower: 80.0k vs 89.1k steps/s at 128 bands, the extra polls' traffic and the drain of the polls
-      // still in flight)
-      const int f = tid < nsrc ? p.src[soff + tid] : -1;
-      unsigned spins = 0;
-      int fail = 0;
-      for (;;) {
-        const bool ok = f < 0 || __hip_atomic_load(p.flags + (size_t)f * BAND_FLAG_STRIDE, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)g;
-        if (__all(ok)) break;
-        ++spins;
-        if (spins > BAND_SPIN_LIMIT ||
-            ((spins & 255) == 0 && __hip_atomic_load(p.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
-          fail = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (fail && tid == 0) {
-        sAbort = 1;
-        __hip_atomic_store(p.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the loads below the poll (no instruction)
-    // H(t), Q(t) of this stage (driven runs)
+    // H(t), Q(t) of this stage (driven runs; every read of the previous stage's values is behind the barrier that
+    // closed its stencil)
     if (pulsed) {
       const int ti = step * 3 + stage_time[stage];
       const c128 fs = p.fsv ? p.fsv[ti] : cmk(0, 0), fc = p.fcv ? p.fcv[ti] : cmk(0, 0);
@@ -1711,25 +1707,61 @@ __global__ __launch_bounds__(TPB) void deom_band_kernel(BandParams p) {
       for (int q = tid; q < p.nmod * ns2; q += blockDim.x)
         sQ[q] = p.Qdip ? cadd(p.Q[q], cmul(p.Qdip[q], fc)) : p.Q[q];
     }
-    __syncthreads();
-    if (sAbort) break;   // uniform: every wave read it behind the barrier
 #ifdef QD_PHASE_TIMING
     const unsigned long long t1 = wall_clock64();
 #endif
-    // 2. halo rows of the stage input -> LDS (sc1 loads: another workgroup wrote them in this launch)
+    // 1-2. halo rows of the stage input -> LDS: sc1 loads re-issued for the granules whose lowest bits do not yet
+    // hold stage g - 1's parity (the data is the flag; stage 0 of step 0 reads the caller's ados)
     {
+      const unsigned tg = (unsigned)((g - 1) >> 1) & 1u;
+      bool good = true;
       c128 hv[BAND_HM];
 #pragma unroll
       for (int h = 0; h < BAND_HM; ++h) hv[h] = ld16_sc1(rin, hsrc[h] < 0 ? 0 : hsrc[h]);
+      if (g > 0) {
+        for (unsigned spins = 0;;) {
+          bool okh[BAND_HM], ok = true;
+#pragma unroll
+          for (int h = 0; h < BAND_HM; ++h) {
+            okh[h] = hsrc[h] < 0 || band_has(hv[h], tg);
+            ok &= okh[h];
+          }
+          if (__all(ok)) break;
+          if (++spins > BAND_SPIN_LIMIT || band_abort_seen(p.status, spins)) {
+            good = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          asm volatile("" ::: "memory");   // the granules change under us: re-load, never reuse the value
+#pragma unroll
+          for (int h = 0; h < BAND_HM; ++h)
+            if (!okh[h]) hv[h] = ld16_sc1(rin, hsrc[h]);
+        }
+      }
 #pragma unroll
       for (int h = 0; h < BAND_HM; ++h)
         if (hsrc[h] >= 0) sX[(size_t)no * ns2 + tid + h * blockDim.x] = hv[h];
-      for (int q = tid + BAND_HM * (int)blockDim.x; q < nhe; q += blockDim.x) {
-        const int r = q / ns2, c = q - r * ns2;
-        sX[(size_t)(no + r) * ns2 + c] = ld16_sc1(rin, (p.halo_idx[hoff + r] * ns2 + c) * 16);
+      for (int q = tid + BAND_HM * (int)blockDim.x; q < nhe && good; q += blockDim.x) {
+        const int r = q / ns2, c = q - r * ns2, off = (p.halo_idx[hoff + r] * ns2 + c) * 16;
+        c128 v = ld16_sc1(rin, off);
+        for (unsigned spins = 0; g > 0 && !band_has(v, tg);) {
+          if (++spins > BAND_SPIN_LIMIT || band_abort_seen(p.status, spins)) {
+            good = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          asm volatile("" ::: "memory");
+          v = ld16_sc1(rin, off);
+        }
+        sX[(size_t)(no + r) * ns2 + c] = v;
+      }
+      if (!good) {
+        sAbort[g & 1] = 1;
+        __hip_atomic_store(p.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     __syncthreads();
+    if (sAbort[g & 1]) break;   // uniform: written before this barrier, rewritten (slot g & 1) only after the next
 #ifdef QD_PHASE_TIMING
     const unsigned long long t2 = wall_clock64();
 #endif
@@ -1788,17 +1820,13 @@ __global__ __launch_bounds__(TPB) void deom_band_kernel(BandParams p) {
 #ifdef QD_PHASE_TIMING
     const unsigned long long t3 = wall_clock64();
 #endif
-    // 4. publish: LDS row, write-through global row, drain, barrier, epoch
+    // 4. publish: LDS row, and the global row write-through with stage g's parity in every double's lowest bit (the
+    // last stage's rows, read by no band, carry the exact final state the host copies out)
     if (valid) {
       sX[(size_t)a * ns2 + e] = xo;
-      st16_sc1(rout, (n * ns2 + e) * 16, xo);
+      st16_sc1(rout, (n * ns2 + e) * 16, g + 1 < G4 ? band_tag(xo, (unsigned)(g >> 1) & 1u) : xo);
       if (stage == 3 && p.snap && n == 0) p.snap[(size_t)(step + 1) * ns2 + e] = r0;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0)
-      __hip_atomic_store(p.flags + (size_t)w * BAND_FLAG_STRIDE, (unsigned)(g + 1), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
     if (early) dpre = dlocal(xo);   // next stage's own element is xo (a padding lane's is never read)
 #ifdef QD_PHASE_TIMING
     const unsigned long long t4 = wall_clock64();
@@ -1883,7 +1911,7 @@ extern "C" int qd_deom_rk4_banded(qd_c128* ados, int nmax, int K, int ns, const 
   const bool need_snap = rho_sys || trace;
   const size_t snap_elems = need_snap && !rho_sys ? (size_t)(nsteps + 1) * ns2 : 0;
   const size_t nf = fsys ? (size_t)nsteps * 3 : 0, nc = fcoup ? (size_t)nsteps * 3 : 0;
-  const size_t flag_bytes = ((size_t)nbands * BAND_FLAG_STRIDE + 4) * sizeof(unsigned);   // + status, 16-B padded
+  const size_t flag_bytes = 16;   // the status word, 16-B padded
   void* w = nullptr;
   int rc = workspace(WS_DEOM, (2 * tot + snap_elems + nf + nc) * sizeof(c128) + flag_bytes, &w, st);
   if (rc) return rc;
@@ -1891,11 +1919,13 @@ extern "C" int qd_deom_rk4_banded(qd_c128* ados, int nmax, int K, int ns, const 
   c128* snap = rho_sys ? (c128*)rho_sys : (need_snap ? buf + 2 * tot : nullptr);
   c128* fsv = nf ? buf + 2 * tot + snap_elems : nullptr;
   c128* fcv = nc ? buf + 2 * tot + snap_elems + nf : nullptr;
-  unsigned* flags = (unsigned*)(buf + 2 * tot + snap_elems + nf + nc);
-  int* stat = status ? (int*)status : (int*)(flags + (size_t)nbands * BAND_FLAG_STRIDE);
+  int* stat_ws = (int*)(buf + 2 * tot + snap_elems + nf + nc);
+  int* stat = status ? (int*)status : stat_ws;
   if (fsv) QD_HIP(hipMemcpyAsync(fsv, fsys, nf * sizeof(c128), hipMemcpyHostToDevice, st));
   if (fcv) QD_HIP(hipMemcpyAsync(fcv, fcoup, nc * sizeof(c128), hipMemcpyHostToDevice, st));
-  QD_HIP(hipMemsetAsync(flags, 0, flag_bytes, st));
+  QD_HIP(hipMemsetAsync(stat_ws, 0, flag_bytes, st));
+  // both hand-off buffers preset to parity 1 in every double: stages 0 and 1, their first writers, carry parity 0
+  QD_HIP(hipMemsetAsync(buf, 1, 2 * tot * sizeof(c128), st));
   if (status) QD_HIP(hipMemsetAsync(status, 0, sizeof(int32_t), st));
   if (snap) {
     hipLaunchKernelGGL(deom_snap0_kernel, dim3(1), dim3(64), 0, st, (const c128*)ados, snap, 1, nmax, ns, nsteps, 0);
@@ -1905,7 +1935,6 @@ extern "C" int qd_deom_rk4_banded(qd_c128* ados, int nmax, int K, int ns, const 
     BandParams p;
     p.ados = (const c128*)ados;
     p.buf = buf;
-    p.flags = flags;
     p.status = stat;
     p.band_lo = band_lo;
     p.halo_off = halo_off;

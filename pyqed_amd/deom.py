@@ -470,7 +470,8 @@ class DEOMSolver:
             # The bands wait on each other inside one launch: if the device cannot hold them all at once
             # (QD_EBUSY from the cooperative launch, nothing ran) or a hand-off timed out (status, e.g. work on
             # another stream delayed a band; ados was overwritten), the run is repeated on the stage launches,
-            # which need no co-residency and give bit-identical results.
+            # which need no co-residency and give the same results (bit-identical with one band, within 1e-13
+            # with several: the halo hand-off tags, qdyn.h).
             ados0 = ados.clone()
             status = torch.zeros(1, dtype=torch.int32, device=dev)
             with torch.cuda.device(dev):

@@ -1,5 +1,7 @@
 """qd_deom_rk4_banded (one hierarchy as one persistent launch over tier bands) against the per-stage launch
-sequence (qd_deom_rk4: same arithmetic; bit-identical at ns = 2) and the NumPy restatement (oracle/deom.py)."""
+sequence (qd_deom_rk4: same arithmetic; bit-identical with one band, within 1e-13 with several -- the handed-off halo
+rows carry their stage's parity in the lowest mantissa bit, deom.hip band_tag) and the NumPy restatement
+(oracle/deom.py)."""
 import numpy as np
 import pytest
 import sympy as sp
@@ -84,16 +86,23 @@ def _spin_boson(L, npsd=4, pulses=False):
     return DEOMSolver(sz + sx, None, _bath(npsd), np.array([sx]), None, None, None, L)
 
 
+HALO_TAG_TOL = 1e-13   # a halo value is off by at most one unit in its last place; it enters through dt x stencil
+
+
 @pytest.mark.parametrize("L,nbands", [(5, 1), (5, 2), (5, 7), (12, 65), (12, 128), (12, 194), (12, 256)])
-def test_banded_bit_identical_to_stage_launches(L, nbands):
+def test_banded_matches_stage_launches(L, nbands):
     """K = 5 at L = 5 (252 ADOs: one, two and seven bands) and the bench hierarchy (L = 12: 6188 ADOs, 65 to 256
-    bands), 12 RK4 steps."""
+    bands), 12 RK4 steps: bit-identical with one band (no halo), within HALO_TAG_TOL with several."""
     sol = _spin_boson(L)
     rho0 = np.array([[1, 0], [0, 0]], complex)
     ref, ref_ados = _run(sol, rho0, 0.002, 12, None)
     got, got_ados = _run(sol, rho0, 0.002, 12, nbands)
-    assert np.array_equal(got, ref)
-    assert np.array_equal(got_ados, ref_ados)
+    if nbands == 1:
+        assert np.array_equal(got, ref)
+        assert np.array_equal(got_ados, ref_ados)
+    else:
+        assert relerr(got, ref) < HALO_TAG_TOL
+        assert relerr(got_ados, ref_ados) < HALO_TAG_TOL
 
 
 def test_banded_pulsed_trace_matches_oracle():
@@ -110,7 +119,7 @@ def test_banded_pulsed_trace_matches_oracle():
     ref = np.einsum("ij,tji->t", p1, ref_rho)
     assert relerr(got, ref) < TOL
     ref2, _ = _run(sol, rho0, 0.01, 30, None, p1=p1)
-    assert np.array_equal(got, ref2)
+    assert relerr(got, ref2) < HALO_TAG_TOL
 
 
 @pytest.mark.parametrize("ns,nmod", [(3, 1), (4, 2)])
@@ -155,7 +164,7 @@ def test_solver_run_takes_banded_path_and_attribute_disables_it():
     sol.banded = False
     assert sol.band_tables(default_device()) is None
     t2, b = sol.run(rho0.copy(), 0.005, 20)
-    assert np.array_equal(np.array(a), np.array(b))
+    assert relerr(np.array(a), np.array(b)) < HALO_TAG_TOL
     torch.cuda.synchronize()
 
 
@@ -166,8 +175,8 @@ def test_banded_stretch_hierarchy_256_bands_matches_stage_launches():
     rho0 = np.array([[1, 0], [0, 0]], complex)
     ref, ref_ados = _run(sol, rho0, 0.001, 6, None)
     got, got_ados = _run(sol, rho0, 0.001, 6, 256)
-    assert np.array_equal(got, ref)
-    assert np.array_equal(got_ados, ref_ados)
+    assert relerr(got, ref) < HALO_TAG_TOL
+    assert relerr(got_ados, ref_ados) < HALO_TAG_TOL
 
 
 def test_solver_run_falls_back_to_stage_launches_after_band_timeout():
@@ -191,11 +200,12 @@ def test_solver_run_falls_back_to_stage_launches_after_band_timeout():
     assert np.array_equal(sol.ddos, ref_ddos)
     _, again = sol.run(rho0.copy(), 0.005, 20)
     assert sol.last_run_banded is True
-    assert np.array_equal(np.array(again), np.array(ref))
+    assert relerr(np.array(again), np.array(ref)) < HALO_TAG_TOL
 
 
 def test_banded_cooperative_and_plain_launch_agree():
-    """The cooperative launch (default) and the plain launch (QD_OPT_COOP_LAUNCH = 0) give identical results."""
+    """The cooperative launch (default) and the plain launch (QD_OPT_COOP_LAUNCH = 0) give identical results (a band
+    only ever consumes the tagged values, whatever the timing)."""
     from conftest import qd_option
     sol = _spin_boson(12)
     rho0 = np.array([[1, 0], [0, 0]], complex)
