@@ -1275,7 +1275,7 @@ def main():
                      else "glf split-K (general kernel)"),
             "roofline": {"bound": "mfma", "achieved": round(tf, 3), "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(tf / FP64_MFMA_PEAK_TFLOPS, 4), "flop_per_dm_step": fl,
-                         "traffic": (measured_traffic("glf_single_kernel<4,1,true>_b1", ss)
+                         "traffic": (measured_traffic("glf_single_kernel<4,1,true,true>_b1", ss)
                                      if (Bs, N, nc) == (1, 128, 1) else None)}}
     single_rate = batch_sweep["1"]["dm_steps_per_s"]
 
