@@ -1716,6 +1716,9 @@ __global__ __launch_bounds__(TPB) void deom_band_kernel(BandParams p) {
       const unsigned tg = (unsigned)((g - 1) >> 1) & 1u;
       bool good = true;
       c128 hv[BAND_HM];
+      // the first pass ~256 clocks after the publish (sooner only adds traffic; 116k -> 119k steps/s at 6188 ADOs,
+      // 8 or 16 units were no better, 32 slower: profiles/r05/deom/band_first_sweep.txt)
+      if (g > 0) __builtin_amdgcn_s_sleep(4);
 #pragma unroll
       for (int h = 0; h < BAND_HM; ++h) hv[h] = ld16_sc1(rin, hsrc[h] < 0 ? 0 : hsrc[h]);
       if (g > 0) {

@@ -86,16 +86,14 @@ __device__ __forceinline__ bool sg_has(c128 v, unsigned t) {
   return (((a ^ t) | (b ^ t)) & 1u) == 0;
 }
 // One wave loads its NL handed-off granules (byte offsets off(q)) with sc1 loads and re-loads the ones without parity
-// t until all have it.  False after SG_SPIN_LIMIT sweeps or when another workgroup reported a timeout (*status).
-#ifndef SG_SLEEP_K
-#define SG_SLEEP_K 1
-#endif
-#ifndef SG_SLEEP_Y
-#define SG_SLEEP_Y 1
-#endif
-template <int SL, int NL, typename Off>
+// t until all have it, s_sleep(1) between passes.  FS: s_sleep units (64 clocks) before the first pass -- a pass
+// issued before the producers' stores can have landed only adds traffic (profiles/r05/lindblad/glf_single_r2.txt).
+// False after SG_SPIN_LIMIT sweeps or when another workgroup reported a timeout (*status).
+template <int FS, int NL, typename Off>
 __device__ __forceinline__ bool sg_sweep(c128 (&v)[NL], __amdgpu_buffer_rsrc_t rs, Off off, unsigned t, int* status,
                                          int lane) {
+  if constexpr (FS > 0) __builtin_amdgcn_s_sleep(FS > 8 ? 8 : FS);   // the first pass after the data can land
+  if constexpr (FS > 8) __builtin_amdgcn_s_sleep(FS - 8);
 #pragma unroll
   for (int q = 0; q < NL; ++q) v[q] = ld16_sc1(rs, off(q));
   for (unsigned spins = 0;;) {
@@ -112,7 +110,7 @@ __device__ __forceinline__ bool sg_sweep(c128 (&v)[NL], __amdgpu_buffer_rsrc_t r
       if (lane == 0) __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;
     }
-    __builtin_amdgcn_s_sleep(SL);
+    __builtin_amdgcn_s_sleep(1);
     asm volatile("" ::: "memory");   // the granules change under us: re-load, never reuse the value
 #pragma unroll
     for (int q = 0; q < NL; ++q)
@@ -175,6 +173,10 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
   // there (N = 128, one matrix: 42.2k -> 43.5k steps/s; at N_p = 32 / 64 the extra hand-off costs more than it saves,
   // profiles/r05/lindblad/glf_single_r2.txt)
   constexpr bool PRY = SPLIT && KS == 4;
+  // delay before a sweep's first pass (s_sleep units), per shape class: none where one matrix's tiles hand off at
+  // N_p = 128 or many N_p = 32 matrices run joint, else 8 or 16 (N = 128 four matrices 112k -> 121k, N = 64 sixteen
+  // 746k -> 794k, N = 32 thirty-two 2.42M -> 2.60M; profiles/r05/lindblad/glf_single_first_sweep.txt)
+  constexpr int FS = (KS == 4 && SPLIT) || (KS == 1 && !SPLIT) ? 0 : (KS == 2 && SPLIT) ? 8 : 16;
   // constant operator fragments, loaded once: A rows bm (L_c at [c], P at [NC]), B columns bn (R_c, Q); with split
   // roles a Y workgroup holds the A fragments and a k workgroup the B fragments, in the same registers (a k workgroup
   // that makes P r itself holds P in aPk)
@@ -266,15 +268,15 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
         if (!yrole) rrow[q] = ld16_sc1(rr, row_off(q));
       }
     } else if (yrole) {
-      good = sg_sweep<SG_SLEEP_Y>(rcol, rr, col_off, tr, p.status, lane);
+      good = sg_sweep<FS>(rcol, rr, col_off, tr, p.status, lane);
     } else if (PRY) {   // the k workgroup reads the row only (its Y workgroup makes P r)
-      good = sg_sweep<SG_SLEEP_K>(rrow, rr, row_off, tr, p.status, lane);
+      good = sg_sweep<FS>(rrow, rr, row_off, tr, p.status, lane);
     } else if (NC > 1 && KS == 4) {   // (one sweep of both would spill here)
-      good = sg_sweep<SG_SLEEP_K>(rcol, rr, col_off, tr, p.status, lane);
-      if (good) good = sg_sweep<SG_SLEEP_K>(rrow, rr, row_off, tr, p.status, lane);
+      good = sg_sweep<FS>(rcol, rr, col_off, tr, p.status, lane);
+      if (good) good = sg_sweep<0>(rrow, rr, row_off, tr, p.status, lane);
     } else {   // column and row in one sweep: one round trip per pass for both
       c128 rcr[2 * KS];
-      good = sg_sweep<SG_SLEEP_K>(rcr, rr, [&](int q) { return q < KS ? col_off(q) : row_off(q - KS); }, tr,
+      good = sg_sweep<FS>(rcr, rr, [&](int q) { return q < KS ? col_off(q) : row_off(q - KS); }, tr,
                                   p.status, lane);
 #pragma unroll
       for (int q = 0; q < KS; ++q) {
@@ -334,7 +336,7 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
       };
 #pragma unroll
       for (int c = 0; c < NC; ++c)
-        if (good) good = sg_sweep<SG_SLEEP_K>(yrow[c], ry, [&](int q) { return y_off(c, q); }, ty, p.status, lane);
+        if (good) good = sg_sweep<FS>(yrow[c], ry, [&](int q) { return y_off(c, q); }, ty, p.status, lane);
       SG_MARK(3)
 #pragma unroll
       for (int c = 0; c < NC; ++c)
@@ -343,7 +345,7 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
       if (PRY && good) {   // the P r element (tid & 255), published after the tile's Y_c, sought under the MFMAs
         c128 pe[1];
         const int v_off = (vo + (b * Np + bm * 16 + ((tid >> 4) & 15)) * Np + bn * 16 + (tid & 15)) * 16;
-        good = sg_sweep<SG_SLEEP_K>(pe, ry, [&](int) { return v_off; }, ty, p.status, lane);
+        good = sg_sweep<FS>(pe, ry, [&](int) { return v_off; }, ty, p.status, lane);
         pv = pe[0];
       }
       if (!good && lane == 0) sAbort[par] = 1;
