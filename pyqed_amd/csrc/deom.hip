@@ -1819,15 +1819,16 @@ __global__ __launch_bounds__(TPB) void deom_band_kernel(BandParams p) {
     // RK4 epilogue (deom_rk4_next, as the stage kernels: Horner form unless driven)
     const c128 xo = deom_rk4_next(stage, !pulsed, dt, r0, acc, d);
     if (stage == 3) r0 = xo;
+    // 4. publish: the global row write-through with stage g's parity in every double's lowest bit (the last stage's
+    // rows, read by no band, carry the exact final state the host copies out) -- ahead of the barrier, which only
+    // guards the band's LDS rows -- then the LDS row
+    if (valid) st16_sc1(rout, (n * ns2 + e) * 16, g + 1 < G4 ? band_tag(xo, (unsigned)(g >> 1) & 1u) : xo);
     __syncthreads();   // every read of sX done
 #ifdef QD_PHASE_TIMING
     const unsigned long long t3 = wall_clock64();
 #endif
-    // 4. publish: LDS row, and the global row write-through with stage g's parity in every double's lowest bit (the
-    // last stage's rows, read by no band, carry the exact final state the host copies out)
     if (valid) {
       sX[(size_t)a * ns2 + e] = xo;
-      st16_sc1(rout, (n * ns2 + e) * 16, g + 1 < G4 ? band_tag(xo, (unsigned)(g >> 1) & 1u) : xo);
       if (stage == 3 && p.snap && n == 0) p.snap[(size_t)(step + 1) * ns2 + e] = r0;
     }
     if (early) dpre = dlocal(xo);   // next stage's own element is xo (a padding lane's is never read)
