@@ -118,6 +118,20 @@ __device__ __forceinline__ bool sg_sweep(c128 (&v)[NL], __amdgpu_buffer_rsrc_t r
   }
 }
 
+// Split roles at N_p = 128: before sweeping for its stage input a wave sleeps num/8 of its previous stage's wait (Y
+// workgroups 6/8, k workgroups 4/8; capped at 20 us), so the passes that could only find stale data -- traffic in
+// the way of the k workgroups' loads -- are skipped; self-tuning, it settles below the data's arrival (a factor
+// f overshoots for good once f RT / (1 - f) exceeds the wait: 7/8 was slower).  N = 128 one matrix 43.3k -> 46.5k,
+// two 73k -> 78.5k (profiles/r05/lindblad/glf_single_adaptive_delay.txt)
+constexpr int SG_ADAPT_Y = 6, SG_ADAPT_K = 4;
+__device__ __forceinline__ unsigned long long sg_delay_ticks(unsigned long long prev, int num) {
+  const unsigned long long d = prev * (unsigned)num / 8u;
+  return d < 2000u ? d : 2000u;
+}
+__device__ __forceinline__ void sg_delay_until(unsigned long long t) {
+  while (wall_clock64() < t) __builtin_amdgcn_s_sleep(2);
+}
+
 // one complex k-step of a 16 x 16 tile: acc += a b (a: A fragment, b: B fragment of v_mfma_f64_16x16x4_f64)
 __device__ __forceinline__ void sg_mac(d4& re, d4& im, c128 a, c128 b) {
   re = __builtin_amdgcn_mfma_f64_16x16x4f64(a.re, b.re, re, 0, 0, 0);
@@ -249,6 +263,7 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
   unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = wall_clock64();
 #endif
   const int G4 = 4 * p.nsteps;
+  unsigned long long wy = 0, wk = 0;   // this wave's last stage-input wait (10 ns ticks), Y and k roles
   for (int g = 0; g < G4; ++g) {
     const int s = g >> 2, m = g & 3, par = g & 1;
     // r_j (j >= 1) lives in rbuf[j & 1] with parity (j >> 1) & 1, Y_g in ybuf[g & 1] with parity (g >> 1) & 1
@@ -268,9 +283,15 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
         if (!yrole) rrow[q] = ld16_sc1(rr, row_off(q));
       }
     } else if (yrole) {
+      const unsigned long long t0 = wall_clock64();
+      if constexpr (PRY) sg_delay_until(t0 + sg_delay_ticks(wy, SG_ADAPT_Y));
       good = sg_sweep<FS>(rcol, rr, col_off, tr, p.status, lane);
+      wy = wall_clock64() - t0;
     } else if (PRY) {   // the k workgroup reads the row only (its Y workgroup makes P r)
+      const unsigned long long t0 = wall_clock64();
+      sg_delay_until(t0 + sg_delay_ticks(wk, SG_ADAPT_K));
       good = sg_sweep<FS>(rrow, rr, row_off, tr, p.status, lane);
+      wk = wall_clock64() - t0;
     } else if (NC > 1 && KS == 4) {   // (one sweep of both would spill here)
       good = sg_sweep<FS>(rcol, rr, col_off, tr, p.status, lane);
       if (good) good = sg_sweep<0>(rrow, rr, row_off, tr, p.status, lane);
