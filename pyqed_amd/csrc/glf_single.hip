@@ -118,12 +118,12 @@ __device__ __forceinline__ bool sg_sweep(c128 (&v)[NL], __amdgpu_buffer_rsrc_t r
   }
 }
 
-// Split roles at N_p = 128: before sweeping for its stage input a wave sleeps num/8 of its previous stage's wait (Y
-// workgroups 6/8, k workgroups 4/8; capped at 20 us), so the passes that could only find stale data -- traffic in
-// the way of the k workgroups' loads -- are skipped; self-tuning, it settles below the data's arrival (a factor
-// f overshoots for good once f RT / (1 - f) exceeds the wait: 7/8 was slower).  N = 128 one matrix 43.3k -> 46.5k,
-// two 73k -> 78.5k (profiles/r05/lindblad/glf_single_adaptive_delay.txt)
-constexpr int SG_ADAPT_Y = 6, SG_ADAPT_K = 4;
+// Split roles at N_p = 128: before a sweep a wave sleeps num/8 of its previous stage's wait for the same data (Y
+// workgroups' stage input 6/8, k workgroups' stage input 4/8 and Y_c rows 4/8; capped at 20 us), so the passes that
+// could only find stale data -- traffic in the way of the k workgroups' loads -- are skipped; self-tuning, it settles
+// below the data's arrival (a factor f overshoots for good once f RT / (1 - f) exceeds the wait: 7/8 was slower).
+// N = 128 one matrix 43.3k -> 47.3k, two 73k -> 80k (profiles/r05/lindblad/glf_single_adaptive_delay.txt)
+constexpr int SG_ADAPT_Y = 6, SG_ADAPT_K = 4, SG_ADAPT_KY = 4;
 __device__ __forceinline__ unsigned long long sg_delay_ticks(unsigned long long prev, int num) {
   const unsigned long long d = prev * (unsigned)num / 8u;
   return d < 2000u ? d : 2000u;
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
   unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = wall_clock64();
 #endif
   const int G4 = 4 * p.nsteps;
-  unsigned long long wy = 0, wk = 0;   // this wave's last stage-input wait (10 ns ticks), Y and k roles
+  unsigned long long wy = 0, wk = 0, wky = 0;   // this wave's last waits (10 ns ticks): Y / k stage input, Y_c rows
   for (int g = 0; g < G4; ++g) {
     const int s = g >> 2, m = g & 3, par = g & 1;
     // r_j (j >= 1) lives in rbuf[j & 1] with parity (j >> 1) & 1, Y_g in ybuf[g & 1] with parity (g >> 1) & 1
@@ -283,10 +283,10 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
         if (!yrole) rrow[q] = ld16_sc1(rr, row_off(q));
       }
     } else if (yrole) {
-      const unsigned long long t0 = wall_clock64();
+      const unsigned long long t0 = PRY ? wall_clock64() : 0;
       if constexpr (PRY) sg_delay_until(t0 + sg_delay_ticks(wy, SG_ADAPT_Y));
       good = sg_sweep<FS>(rcol, rr, col_off, tr, p.status, lane);
-      wy = wall_clock64() - t0;
+      if constexpr (PRY) wy = wall_clock64() - t0;
     } else if (PRY) {   // the k workgroup reads the row only (its Y workgroup makes P r)
       const unsigned long long t0 = wall_clock64();
       sg_delay_until(t0 + sg_delay_ticks(wk, SG_ADAPT_K));
@@ -355,9 +355,12 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
       auto y_off = [&](int c, int q) {
         return (yo + ((c * mats + b) * Np + bm * 16 + lr) * Np + kb + 4 * q + lk) * 16;
       };
+      const unsigned long long ty0 = PRY ? wall_clock64() : 0;
+      if constexpr (PRY) sg_delay_until(ty0 + sg_delay_ticks(wky, SG_ADAPT_KY));
 #pragma unroll
       for (int c = 0; c < NC; ++c)
         if (good) good = sg_sweep<FS>(yrow[c], ry, [&](int q) { return y_off(c, q); }, ty, p.status, lane);
+      if constexpr (PRY) wky = wall_clock64() - ty0;
       SG_MARK(3)
 #pragma unroll
       for (int c = 0; c < NC; ++c)
