@@ -187,6 +187,9 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
   // there (N = 128, one matrix: 42.2k -> 43.5k steps/s; at N_p = 32 / 64 the extra hand-off costs more than it saves,
   // profiles/r05/lindblad/glf_single_r2.txt)
   constexpr bool PRY = SPLIT && KS == 4;
+  // adaptive sweep delays (SG_ADAPT_*) at N_p = 128 with split roles; at N_p = 32 / 64 they measured 0-2 % slower
+  // than the static first-pass delays FS (glf_single_adaptive_delay.txt)
+  constexpr bool ADAPT = PRY;
   // delay before a sweep's first pass (s_sleep units), per shape class: none where one matrix's tiles hand off at
   // N_p = 128 or many N_p = 32 matrices run joint, else 8 or 16 (N = 128 four matrices 112k -> 121k, N = 64 sixteen
   // 746k -> 794k, N = 32 thirty-two 2.42M -> 2.60M; profiles/r05/lindblad/glf_single_first_sweep.txt)
@@ -283,10 +286,10 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
         if (!yrole) rrow[q] = ld16_sc1(rr, row_off(q));
       }
     } else if (yrole) {
-      const unsigned long long t0 = PRY ? wall_clock64() : 0;
-      if constexpr (PRY) sg_delay_until(t0 + sg_delay_ticks(wy, SG_ADAPT_Y));
-      good = sg_sweep<FS>(rcol, rr, col_off, tr, p.status, lane);
-      if constexpr (PRY) wy = wall_clock64() - t0;
+      const unsigned long long t0 = ADAPT ? wall_clock64() : 0;
+      if constexpr (ADAPT) sg_delay_until(t0 + sg_delay_ticks(wy, SG_ADAPT_Y));
+      good = sg_sweep<ADAPT ? 0 : FS>(rcol, rr, col_off, tr, p.status, lane);
+      if constexpr (ADAPT) wy = wall_clock64() - t0;
     } else if (PRY) {   // the k workgroup reads the row only (its Y workgroup makes P r)
       const unsigned long long t0 = wall_clock64();
       sg_delay_until(t0 + sg_delay_ticks(wk, SG_ADAPT_K));
@@ -297,8 +300,11 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
       if (good) good = sg_sweep<0>(rrow, rr, row_off, tr, p.status, lane);
     } else {   // column and row in one sweep: one round trip per pass for both
       c128 rcr[2 * KS];
-      good = sg_sweep<FS>(rcr, rr, [&](int q) { return q < KS ? col_off(q) : row_off(q - KS); }, tr,
-                                  p.status, lane);
+      const unsigned long long t0 = ADAPT ? wall_clock64() : 0;
+      if constexpr (ADAPT) sg_delay_until(t0 + sg_delay_ticks(wk, SG_ADAPT_K));
+      good = sg_sweep<ADAPT ? 0 : FS>(rcr, rr, [&](int q) { return q < KS ? col_off(q) : row_off(q - KS); }, tr,
+                                      p.status, lane);
+      if constexpr (ADAPT) wk = wall_clock64() - t0;
 #pragma unroll
       for (int q = 0; q < KS; ++q) {
         rcol[q] = rcr[q];
@@ -355,12 +361,12 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
       auto y_off = [&](int c, int q) {
         return (yo + ((c * mats + b) * Np + bm * 16 + lr) * Np + kb + 4 * q + lk) * 16;
       };
-      const unsigned long long ty0 = PRY ? wall_clock64() : 0;
-      if constexpr (PRY) sg_delay_until(ty0 + sg_delay_ticks(wky, SG_ADAPT_KY));
+      const unsigned long long ty0 = ADAPT ? wall_clock64() : 0;
+      if constexpr (ADAPT) sg_delay_until(ty0 + sg_delay_ticks(wky, SG_ADAPT_KY));
 #pragma unroll
       for (int c = 0; c < NC; ++c)
-        if (good) good = sg_sweep<FS>(yrow[c], ry, [&](int q) { return y_off(c, q); }, ty, p.status, lane);
-      if constexpr (PRY) wky = wall_clock64() - ty0;
+        if (good) good = sg_sweep<ADAPT ? 0 : FS>(yrow[c], ry, [&](int q) { return y_off(c, q); }, ty, p.status, lane);
+      if constexpr (ADAPT) wky = wall_clock64() - ty0;
       SG_MARK(3)
 #pragma unroll
       for (int c = 0; c < NC; ++c)
