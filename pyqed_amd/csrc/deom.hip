@@ -724,6 +724,19 @@ __global__ void deom_snap0_kernel(const c128* rho, c128* snap, int B, int nmax, 
   }
 }
 
+// Per-call setup of the banded launch in one kernel (instead of three memsets and a copy): both hand-off buffers to
+// parity 1 in every double (bytes 0x01), the status words to 0, row 0 of the snapshots from the initial ADO 0.
+__global__ void deom_band_prep_kernel(unsigned long long* buf, long nwords, int* stat, int* stat2, const c128* ados,
+                                      c128* snap, int ns2) {
+  const long i0 = blockIdx.x * (long)blockDim.x + threadIdx.x, st = (long)gridDim.x * blockDim.x;
+  for (long i = i0; i < nwords; i += st) buf[i] = 0x0101010101010101ull;
+  if (i0 == 0) {
+    *stat = 0;
+    if (stat2) *stat2 = 0;
+  }
+  if (snap && i0 < ns2) snap[i0] = ados[i0];
+}
+
 // obs[b][s][m] = Tr(E_m rho_0(s)) = sum_ij E_m[j][i] rho[i][j]   (deom.py:1100,1113)
 __global__ void deom_trace_kernel(const c128* snap, const c128* E, int ne, int B, int ns, int nsnap, c128* obs) {
   const int ns2 = ns * ns;
@@ -1456,8 +1469,8 @@ namespace {
 // after it loaded stage g - 1's rows of every source, which each stored only after loading its halo of stage g - 2
 // (its halo loads complete before its stencil's barrier), and the neighbour relation is symmetric (sources ==
 // consumers).  Both buffers are preset to parity 1 (stages 0 and 1, their first writers, carry 0).
-// Stage 0 of step 0 reads the caller's ados (written before the launch); the final rho is buf[1] (the output of
-// the last stage 3), copied to ados behind the launch.  A spin that exceeds its bound (bands not co-resident)
+// Stage 0 of step 0 reads the caller's ados (written before the launch); the last stage 3 writes the final rho
+// straight into ados.  A spin that exceeds its bound (bands not co-resident)
 // sets *status = 1 and every band leaves its loop (results then invalid; the host reports it).
 constexpr unsigned BAND_SPIN_LIMIT = 1u << 21;  // sweeps (one round trip each): ~1 s
 
@@ -1693,8 +1706,10 @@ __global__ __launch_bounds__(TPB) void deom_band_kernel(BandParams p) {
     const int step = g >> 2, stage = g & 3;
     const c128* in = g == 0 ? p.ados : p.buf + (size_t)((g - 1) & 1) * slab;
     const __amdgpu_buffer_rsrc_t rin = sc1_rsrc(in, slab_bytes);
+    // the last stage's rows go straight to the caller's ados (every read of ados, stage 0's, is long done: a band
+    // at stage >= 2 has loaded its sources' stage-1 rows, made after their stage-0 reads)
     const __amdgpu_buffer_rsrc_t rout =
-        sc1_rsrc(p.buf + (size_t)(g & 1) * slab, slab_bytes);
+        sc1_rsrc(g + 1 < G4 ? p.buf + (size_t)(g & 1) * slab : (c128*)p.ados, slab_bytes);
 #ifdef QD_PHASE_TIMING
     const unsigned long long t0 = wall_clock64();
 #endif
@@ -1927,12 +1942,13 @@ extern "C" int qd_deom_rk4_banded(qd_c128* ados, int nmax, int K, int ns, const 
   int* stat = status ? (int*)status : stat_ws;
   if (fsv) QD_HIP(hipMemcpyAsync(fsv, fsys, nf * sizeof(c128), hipMemcpyHostToDevice, st));
   if (fcv) QD_HIP(hipMemcpyAsync(fcv, fcoup, nc * sizeof(c128), hipMemcpyHostToDevice, st));
-  QD_HIP(hipMemsetAsync(stat_ws, 0, flag_bytes, st));
-  // both hand-off buffers preset to parity 1 in every double: stages 0 and 1, their first writers, carry parity 0
-  QD_HIP(hipMemsetAsync(buf, 1, 2 * tot * sizeof(c128), st));
-  if (status) QD_HIP(hipMemsetAsync(status, 0, sizeof(int32_t), st));
-  if (snap) {
-    hipLaunchKernelGGL(deom_snap0_kernel, dim3(1), dim3(64), 0, st, (const c128*)ados, snap, 1, nmax, ns, nsteps, 0);
+  // both hand-off buffers preset to parity 1 in every double (stages 0 and 1, their first writers, carry parity 0),
+  // the status words zeroed, snapshot row 0 written: one kernel
+  {
+    const long nwords = (long)(2 * tot * sizeof(c128) / 8);
+    hipLaunchKernelGGL(deom_band_prep_kernel, dim3((int)std::min<long>((nwords + 255) / 256, 1024)), dim3(256), 0, st,
+                       (unsigned long long*)buf, nwords, stat_ws, status ? (int*)status : nullptr,
+                       (const c128*)ados, snap, (int)ns2);
     QD_HIP(hipGetLastError());
   }
   if (nsteps > 0) {
@@ -2008,8 +2024,7 @@ extern "C" int qd_deom_rk4_banded(qd_c128* ados, int nmax, int K, int ns, const 
       }
     }
 #endif
-    // the last stage 3 wrote the final rho to buf[1]
-    QD_HIP(hipMemcpyAsync(ados, buf + tot, tot * sizeof(c128), hipMemcpyDeviceToDevice, st));
+    // the last stage 3 wrote the final rho straight into ados (deom_band_kernel)
   }
   if (trace) {
     const int n = (nsteps + 1) * ne;
