@@ -85,13 +85,17 @@ int qd_workspace_stats(size_t* reserved, size_t* used);
  *       batch path -- QD_GLF_SINGLE (single-trajectory launch, where it applies),
  *       QD_GLF_SPLIT (a workgroup per output block and phase; pair blocks for
  *       Hermitian batches), QD_GLF_PERSISTENT (a workgroup per matrix); for
- *       comparing the paths on one input.
+ *       comparing the paths on one input;
+ *   QD_OPT_IDLE_CAP_MIB (no environment variable, default -1 = 16384): the
+ *       scratch arena's idle cache in MiB -- idle slabs beyond it are released once
+ *       their last user has completed (tests lower it to exercise the release).
  * qd_take_path copies the dispatch decisions of this thread's calls since the
  * last qd_take_path (space-separated kernel-path names) into buf and clears them. */
 #define QD_OPT_COOP_LAUNCH 0
 #define QD_OPT_FAKE_TIMEOUT 1
 #define QD_OPT_GLF_PATH 2
-#define QD_OPT_COUNT 3
+#define QD_OPT_IDLE_CAP_MIB 3
+#define QD_OPT_COUNT 4
 #define QD_GLF_AUTO 0
 #define QD_GLF_SINGLE 1
 #define QD_GLF_SPLIT 2

@@ -26,6 +26,7 @@ QD_EBUSY = -5
 QD_OPT_COOP_LAUNCH = 0
 QD_OPT_FAKE_TIMEOUT = 1
 QD_OPT_GLF_PATH = 2
+QD_OPT_IDLE_CAP_MIB = 3
 GLF_PATHS = {"auto": 0, "single": 1, "split": 2, "persistent": 3}
 
 c_int = ctypes.c_int

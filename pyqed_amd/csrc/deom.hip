@@ -134,7 +134,7 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_kernel(DeomParams p) {
   }
 
   // RK4 bookkeeping (deom_rk4_next)
-  const c128 r0 = p.rho[e];
+  const c128 r0 = p.rho ? p.rho[e] : cmk(0, 0);   // rho == nullptr: qd_deom_apply
   c128 a = (p.stage > 0 && !p.horner) ? p.acc[e] : cmk(0, 0);
   const c128 v = deom_rk4_next(p.stage, p.horner, p.dt, r0, a, d);
   if (p.stage < 3) {
@@ -288,7 +288,7 @@ __device__ __forceinline__ void deom_stage_grp_body(const DeomParams& p) {
   const c128 dmp = UNI ? ld_uniform(p.damp + nu) : (live ? p.damp[n] : cmk(0, 0));
   const size_t idx = grp * ns2 + e;
   // stage 0 of the Horner form: the stage input is rho itself (own == rho[idx] for a valid lane)
-  const c128 r0 = !valid ? cmk(0, 0) : (horner && p.stage == 0) ? own : ld_once(p.rho + idx, p.ntst);
+  const c128 r0 = !valid ? cmk(0, 0) : (horner && p.stage == 0) ? own : p.rho ? ld_once(p.rho + idx, p.ntst) : cmk(0, 0);
   c128 a0 = (valid && p.stage > 0 && !horner) ? ld_once(p.acc + idx, p.ntst) : cmk(0, 0);
   for (int q = threadIdx.x; q < ns2; q += blockDim.x)
     sH[q] = p.Hdip ? cadd(p.H[q], cmul(p.Hdip[q], p.fs)) : p.H[q];
@@ -469,7 +469,7 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_pipe_kernel(DeomParams p)
   const __amdgpu_buffer_rsrc_t rPl = buf_rsrc(p.plus, (int)(nx * (unsigned)K * 4u));
   const unsigned rsb = (unsigned)p.B * 64u;                 // ADO row stride in bytes
   const int xbytes = (int)(nx * (unsigned)p.B * 64u);
-  const __amdgpu_buffer_rsrc_t rR = buf_rsrc(p.rho, xbytes), rXo = buf_rsrc(p.xout, xbytes);
+  const __amdgpu_buffer_rsrc_t rR = buf_rsrc(p.rho, p.rho ? xbytes : 0), rXo = buf_rsrc(p.xout, xbytes);
   const __amdgpu_buffer_rsrc_t rRo = buf_rsrc(p.rho_out, xbytes);
   // lane group lgrp = u / G of the class is (ADO hi, hierarchy lo) with lgrp = hi Bx + lo; a wave's next group is
   // stride / G further on, so (hi, lo) advance by a constant carry step instead of a division per group
@@ -628,7 +628,7 @@ __global__ __launch_bounds__(256) void deom_stage_mfma16_kernel(DeomParams p) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     x[r] = ld(X + (size_t)n * ns2, r);
-    r0[r] = ld(p.rho + own, r);
+    r0[r] = p.rho ? ld(p.rho + own, r) : cmk(0, 0);
     a0[r] = (p.stage > 0 && !p.horner) ? ld(p.acc + own, r) : cmk(0, 0);
   }
   const c128 dmp = p.damp[n];
@@ -887,7 +887,7 @@ __global__ __launch_bounds__(256) void deom_stage_tile_kernel(DeomParams p) {
     if (i >= ns || j >= ns) continue;
     const size_t e = bbase + (size_t)n * ns2 + (size_t)i * ns + j;
     const c128 d = cadd(sacc[f], cmul(p.damp[n], xn[i * ns + j]));
-    const c128 r0 = p.rho[e];
+    const c128 r0 = p.rho ? p.rho[e] : cmk(0, 0);   // rho == nullptr: qd_deom_apply
     c128 a = (p.stage > 0 && !p.horner) ? p.acc[e] : cmk(0, 0);
     const c128 v = deom_rk4_next(p.stage, p.horner, dt, r0, a, d);
     if (p.stage < 3) {
@@ -984,7 +984,7 @@ __global__ __launch_bounds__(256) void deom_stage_tmfma_kernel(DeomParams p) {
     if (i >= ns || j >= ns) continue;
     const size_t e = bbase + (size_t)n * ns2 + (size_t)i * ns + j;
     const c128 d = cadd(cmk(Dre[r], Dim[r]), cmul(dmp, xn[i * ns + j]));
-    const c128 r0 = p.rho[e];
+    const c128 r0 = p.rho ? p.rho[e] : cmk(0, 0);   // rho == nullptr: qd_deom_apply
     c128 a = (p.stage > 0 && !p.horner) ? p.acc[e] : cmk(0, 0);
     const c128 v = deom_rk4_next(p.stage, p.horner, dt, r0, a, d);
     if (p.stage < 3) {
@@ -1308,8 +1308,8 @@ extern "C" int qd_deom_stage(qd_c128* rho, const qd_c128* xin, qd_c128* xout, qd
 
 // y = alpha P x for B ADO vectors (the generator of generate_dot_element, heom/deom.py:641-664, as an operator; the
 // Krylov form of DEOMSolver.correlation_4op_3t applies it and its transpose, pyqed_amd/deom_krylov.py).  One stage
-// launch of the stage kernels: Horner stage 2 (s_3 = rho + dt / 2 L s_2) with rho = 0 and dt = 2 alpha, so the
-// coefficient is alpha exactly and the kernel reads its input only from xin.
+// launch of the stage kernels: Horner stage 2 (s_3 = rho + dt / 2 L s_2) with rho = 0 (a null rho: nothing is read
+// for it) and dt = 2 alpha, so the coefficient is alpha exactly and the kernel reads its input only from xin.
 extern "C" int qd_deom_apply(const qd_c128* x, qd_c128* y, int B, int nmax, int K, int ns, const int32_t* minus,
                              const int32_t* plus, const qd_c128* coef, const qd_c128* damp, const int32_t* mode,
                              int nmod, const qd_c128* H, const qd_c128* Q, double alpha, int ado_major, void* stream) {
@@ -1318,15 +1318,11 @@ extern "C" int qd_deom_apply(const qd_c128* x, qd_c128* y, int B, int nmax, int 
   QD_CHECK_ARG(B >= 1 && nmax >= 1 && K >= 1 && ns >= 1 && nmod >= 1, "qd_deom_apply: bad sizes B=%d nmax=%d K=%d ns=%d",
                B, nmax, K, ns);
   hipStream_t st = (hipStream_t)stream;
-  WsScope wss_(st);
-  const size_t tot = (size_t)B * nmax * ns * ns;
-  void* z = nullptr;
-  int rc = workspace(WS_DEOM, tot * sizeof(c128), &z, st);
-  if (rc) return rc;
-  QD_HIP(hipMemsetAsync(z, 0, tot * sizeof(c128), st));
+  // rho == nullptr: the stage kernels take rho = 0 without a zeroed buffer to read (a full-size memset
+  // and read per application); stage 2 never writes rho_out
   DeomParams p{};
-  p.rho = (const c128*)z;
-  p.rho_out = (c128*)z;
+  p.rho = nullptr;
+  p.rho_out = nullptr;
   p.xin = (const c128*)x;
   p.xout = (c128*)y;
   p.acc = nullptr;

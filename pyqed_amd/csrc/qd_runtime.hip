@@ -47,7 +47,11 @@ static std::mutex g_mu;              // guards g_slabs and every Slab's busy / r
 static std::vector<Slab*> g_slabs;
 static thread_local std::vector<LiveRef> g_live;
 static thread_local int g_depth = 0;
-static constexpr size_t kIdleCap = (size_t)16 << 30;
+static constexpr size_t kIdleCapMiB = (size_t)16 << 10;   // QD_OPT_IDLE_CAP_MIB default: 16 GiB of idle slabs
+static size_t idle_cap() {
+  const int v = option(QD_OPT_IDLE_CAP_MIB);
+  return v < 0 ? kIdleCapMiB << 20 : (size_t)v << 20;
+}
 
 static size_t slab_size(size_t bytes) {
   size_t s = (size_t)64 << 10;
@@ -158,9 +162,11 @@ int workspace(WsSlot slot, size_t bytes, void** ptr, hipStream_t st) {
       set_error("workspace event creation failed: %s", hipGetErrorString(e));
       return QD_EHIP;
     }
-    best = new Slab{p, want, dev, ev, false, false};
+    // the new slab is marked busy BEFORE the trim, which only releases idle slabs (a new slab pushed
+    // idle was the first one trim_idle freed once the cache exceeded the cap)
+    best = new Slab{p, want, dev, ev, true, false};
     g_slabs.push_back(best);
-    trim_idle(kIdleCap);
+    trim_idle(idle_cap());
   }
   best->busy = true;
   g_live.push_back({best, st, nullptr});
@@ -198,9 +204,9 @@ static const bool g_opt_init = [] {
     const char* env;
     int dflt;
   } tab[] = {{QD_OPT_COOP_LAUNCH, "QD_COOP_LAUNCH", 1}, {QD_OPT_FAKE_TIMEOUT, "QD_TEST_FAKE_TIMEOUT", 0},
-             {QD_OPT_GLF_PATH, "QD_GLF_PATH", QD_GLF_AUTO}};
+             {QD_OPT_GLF_PATH, "QD_GLF_PATH", QD_GLF_AUTO}, {QD_OPT_IDLE_CAP_MIB, nullptr, -1}};
   for (auto& t : tab) {
-    const char* e = std::getenv(t.env);
+    const char* e = t.env ? std::getenv(t.env) : nullptr;
     g_opt[t.opt].store(e && *e ? std::atoi(e) : t.dflt);
   }
   return true;
@@ -225,6 +231,7 @@ int qd_set_option(int opt, int value) {
   QD_CHECK_ARG(opt >= 0 && opt < QD_OPT_COUNT, "qd_set_option: unknown option %d", opt);
   QD_CHECK_ARG(opt != QD_OPT_GLF_PATH || (value >= QD_GLF_AUTO && value <= QD_GLF_PERSISTENT),
                "qd_set_option: QD_OPT_GLF_PATH value %d", value);
+  QD_CHECK_ARG(opt != QD_OPT_IDLE_CAP_MIB || value >= -1, "qd_set_option: QD_OPT_IDLE_CAP_MIB value %d", value);
   (void)qd::g_opt_init;
   qd::g_opt[opt].store(value);
   return QD_OK;

@@ -200,7 +200,10 @@ def shifted_krylov_solve(op, b, shifts, tol=1e-12, m_max=None, first_check=20):
         nrm = torch.linalg.vector_norm(W)
         Hd[:j + 1, j] = h
         Hd[j + 1, j] = nrm
-        V[j + 1] = W / nrm
+        # an exact breakdown (nrm == 0: b lies in a small invariant subspace) must not turn the basis into NaN
+        # before the next checkpoint, where the zero sub-diagonal entry ends the solve; the guard
+        # stays on the device (no host read per step)
+        V[j + 1] = W / torch.clamp(nrm, min=1e-300)
         k = j + 1
         if k != check and k != m_max:
             continue

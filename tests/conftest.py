@@ -44,11 +44,12 @@ import contextlib  # noqa: E402
 
 @contextlib.contextmanager
 def qd_option(name, value):
-    """Set a libqdyn process option (include/qdyn.h QD_OPT_*: "coop", "fake_timeout", "glf_path") for the block and
+    """Set a libqdyn process option (include/qdyn.h QD_OPT_*: "coop", "fake_timeout", "glf_path", "idle_cap") for the
+    block and
     restore it after."""
     from pyqed_amd import _lib
     opt = {"coop": _lib.QD_OPT_COOP_LAUNCH, "fake_timeout": _lib.QD_OPT_FAKE_TIMEOUT,
-           "glf_path": _lib.QD_OPT_GLF_PATH}[name]
+           "glf_path": _lib.QD_OPT_GLF_PATH, "idle_cap": _lib.QD_OPT_IDLE_CAP_MIB}[name]
     if isinstance(value, str):
         value = _lib.GLF_PATHS[value]
     prev = _lib.set_option(opt, value)

@@ -79,3 +79,23 @@ def test_krylov_corr4_matches_eigen_form(lcr, nwx, nwy):
     c, info = corr4_krylov(_DenseOp(P, nb), _DenseOp(P.T.copy(), nb), A1, A2, A3, A4, rho0, T, wx, wy, sol.nmax, 2)
     ref = od.correlation_4op_3t(P, sol.nmax, 2, ops, rho0, T, wx, wy, if_full=True, lcr=lcr)
     assert relerr(c, ref) < 1e-10, (lcr, info)
+
+
+def test_shifted_krylov_exact_breakdown_is_detected():
+    """an Arnoldi breakdown with ||w|| exactly 0 (here P = 0, so K_1 is invariant) ends the solve with
+    the exact answer x(s) = -b / s instead of NaN vectors and a 'no convergence' error; a one-step invariant
+    subspace of a nonzero P (P b = c b, b a basis vector) too."""
+    from pyqed_amd.deom_krylov import shifted_krylov_solve
+    n = 12
+    shifts = np.array([0.3 + 1j, -0.7 + 0.5j, 2.0 + 0.1j])
+    b = torch.from_numpy(np.random.default_rng(1).standard_normal(n) + 0j)
+    X, k = shifted_krylov_solve(_DenseOp(np.zeros((n, n), complex), 1.0), b, shifts)
+    assert k == 1
+    assert np.all(np.isfinite(X.numpy()))
+    assert relerr(X.numpy(), -b.numpy()[None, :] / shifts[:, None]) < 1e-14
+    P = np.diag(np.arange(n, dtype=complex) - 2.5)
+    e = torch.zeros(n, dtype=torch.complex128)
+    e[3] = 2.0
+    X, k = shifted_krylov_solve(_DenseOp(P, 10.0), e, shifts)
+    assert k == 1
+    assert relerr(X.numpy(), e.numpy()[None, :] / (-P[3, 3] - shifts)[:, None]) < 1e-14

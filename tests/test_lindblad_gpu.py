@@ -467,6 +467,44 @@ def test_workspace_bounded_over_many_streams():
     assert max(reserved) <= 2 * reserved[0], reserved
 
 
+def test_new_scratch_slab_survives_idle_trim():
+    """workspace() trims the idle cache right after it allocates a slab; the new slab must not be
+    the one released.  With the idle cap lowered to 0 MiB (QD_OPT_IDLE_CAP_MIB) every allocation releases every
+    other idle slab, so calls whose scratch sizes differ by more than 4x (a new slab each) alternate; each call's
+    result matches the oracle and the arena keeps only the slabs the last call used."""
+    import ctypes
+    import torch
+    from conftest import qd_option
+    from oracle import lindblad as olb
+    from pyqed_amd import lindblad_rk4, _lib
+    dev = torch.device("cuda", 0)
+    lib = _lib.load()
+    lib.qd_shutdown()
+    cases = []
+    for N, B in ((64, 2), (128, 8)):
+        H, cs = olb.synthetic_lindblad(N, nc=1)
+        r0 = olb.random_pure_states(B, N, seed=N + B)
+        cases.append((torch.from_numpy(H).to(dev), torch.from_numpy(np.array(cs)).to(dev), r0,
+                      olb.lindblad_batch(H, cs, r0, 1e-2, 2)))
+    sizes = []
+    with qd_option("idle_cap", 0):
+        for k in range(6):
+            Ht, Ct, r0, ref = cases[k % 2]
+            rho = torch.from_numpy(r0.copy()).to(dev)
+            lindblad_rk4(Ht, Ct, rho, 1e-2, 2)
+            torch.cuda.synchronize()
+            assert relerr(rho.cpu().numpy(), ref) < TOL, k
+            res, used = ctypes.c_size_t(0), ctypes.c_size_t(0)
+            _lib.check(lib.qd_workspace_stats(ctypes.byref(res), ctypes.byref(used)), "qd_workspace_stats")
+            assert used.value == 0, (k, used.value)
+            sizes.append(res.value)
+    lib.qd_shutdown()
+    assert all(s > 0 for s in sizes), sizes
+    # a call may hold several slabs and reuse one within 4x of a request, so the arena settles after the first round
+    # and then stays at what the alternating calls hold
+    assert sizes[0] != sizes[1] and sizes[4:] == sizes[2:4], sizes
+
+
 def test_scratch_reuse_is_device_ordered_across_streams():
     """VERDICT r04 item 1 (SURVEY §8(b) threading): library calls do not wait on the host, and a scratch slab released
     by a call still running on one stream is reused by a call on ANOTHER stream only behind it on the device
@@ -580,6 +618,35 @@ def test_lindblad_single_launch_matches_split_path_and_oracle(N, nc, B, prod, ro
     assert relerr(out["single"][2][:, -1], out["single"][0]) == 0.0
     obs_ref = np.einsum("bij,mji->bm", rho0, E)
     assert relerr(out["single"][1][:, 0], obs_ref) < 1e-13
+
+
+def test_lindblad_single_launch_long_run_matches_split_path():
+    """the single-trajectory launch's data-as-flag hand-offs change a handed-off value by at most one ulp
+    per stage; over a production-length run (2000 RK4 steps at N = 128, one matrix, the LindbladSolver.run case) the
+    result stays within 1e-11 of the split path, and both within 1e-10 of the oracle's RK4 at 2000 steps."""
+    import torch
+    from oracle import lindblad as olb
+    from pyqed_amd import lindblad_rk4
+    from conftest import qd_option, took
+    N, steps, dt = 128, 2000, 1e-3
+    H, cs = olb.synthetic_lindblad(N, nc=1)
+    rho0 = olb.random_pure_states(1, N, seed=4)
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    out = {}
+    for mode in ("single", "split"):
+        rho = t(rho0.copy())
+        took("")
+        with qd_option("glf_path", mode):
+            lindblad_rk4(t(H), t(np.array(cs)), rho, dt, steps, hermitian=False)
+        torch.cuda.synchronize()
+        assert ("glf_" + mode) in took("")[1]
+        out[mode] = rho.cpu().numpy()
+    err = relerr(out["single"], out["split"])
+    print(f"single vs split, 2000 steps: {err:.3e}")
+    assert err < 1e-11
+    ref = olb.lindblad_batch(H, cs, rho0, dt, steps)
+    assert relerr(out["single"], ref) < TOL
 
 
 def test_lindblad_single_launch_timeout_falls_back(capfd):
