@@ -14,12 +14,20 @@
  *     never by a host wait; qd_shutdown releases the arena;
  *   - calls are asynchronous on `stream` (a hipStream_t, NULL = default stream):
  *     they enqueue their kernels and return without waiting for the device.
- *     Exceptions, each stated at its entry point: qd_gather_rows with check != 0,
- *     the single-trajectory Lindblad launch inside qd_lindblad_rk4 /
- *     qd_lindblad_rk4_herm (B <= glf_single_max_batch: it reads its hand-off
- *     status back), and qd_deom_rk4_banded with status == NULL;
+ *     The one exception: qd_gather_rows with check != 0 (stated there).  The two
+ *     persistent hand-off launches (the single-trajectory Lindblad launch inside
+ *     qd_lindblad_rk4, qd_deom_rk4_banded without a status word) report a
+ *     hand-off timeout in a device status word and queue a stream-ordered
+ *     fallback behind themselves that re-runs the call only in that case;
  *     host-array inputs (fvals of the driven entry points) are copied before
  *     the call returns;
+ *   - the hand-off launches pass data between workgroups with the flag carried
+ *     in the data: every handed-off double carries its epoch's parity in the
+ *     LOWEST bit of its low dword, and a consumer takes a 16-B granule whose
+ *     doubles carry the expected parity.  This assumes a 16-B granule written by
+ *     one store is never observed torn at dword level (new low dwords with stale
+ *     high dwords) -- observed on MI355X, not an architectural guarantee
+ *     (MI355X_MICROARCH.md); a torn granule would pass the parity test silently;
  *   - the asynchronous calls may be captured into a HIP graph (stream capture on
  *     `stream`): their scratch then comes from stream-ordered allocations that
  *     become the graph's own alloc / free nodes, so replays never share arena
@@ -123,6 +131,13 @@ int qd_take_path(char* buf, size_t len);     /* buf: host pointer   */
  *                         (NULL or save_every <= 0: no snapshots)
  * Constraints: 1 <= N <= 16384, 0 <= nc <= 256, ne >= 0, B >= 1.  RK4 is evaluated
  * in Horner form (phys.rk4 in exact arithmetic; no accumulator buffer).
+ * Few undriven matrices (B <= 256 / (N_p/16)^2, N_p in {32, 64, 128}, nc <= 2) run
+ * as ONE cooperative persistent launch with a workgroup per 16 x 16 output tile
+ * and in-launch hand-offs (data-as-flag, above); behind it the call queues a
+ * guarded restore of the initial state and a guarded run of the persistent
+ * kernel (a workgroup per matrix), both no-ops unless the launch reported a
+ * hand-off timeout: the call never waits on the host.  A refused cooperative
+ * launch (known at once) runs the split path instead.
  */
 int qd_lindblad_rk4(const qd_c128* H, const qd_c128* C, int nc, qd_c128* rho,
                     int B, int N, double dt, int nsteps, const qd_c128* E,
@@ -325,8 +340,11 @@ int qd_deom_rk4_ado_major(qd_c128* ados, int B, int nmax, int K, int ns,
  * one band; with several a halo value differs by at most one unit in its last
  * place, which reaches the result through dt x stencil: within 1e-13).
  * status: device int32 set to 1 if a hand-off timed out (bands not
- * co-resident; results invalid, ados overwritten), or null: the call then
- * synchronises the stream and returns QD_EHIP in that case.  The launch is
+ * co-resident; results invalid, ados overwritten: the caller re-runs), or null:
+ * the call then saves the initial ADOs and queues a stream-ordered fallback that,
+ * only after a timeout, restores them and re-runs the propagation on one
+ * workgroup (the stage launches' element stencil; slow but correct) -- either
+ * way the call returns without waiting for the device.  The launch is
  * cooperative: a band count the device cannot hold at once returns QD_EBUSY
  * before anything runs.  Undriven runs always use the Horner form of RK4 (the
  * QD_DEOM_HORNER=0 A/B switch of qd_deom_rk4 does not apply here; DEOMSolver

@@ -81,19 +81,10 @@ __device__ __forceinline__ c128 deom_rk4_next(int stage, bool horner, double dt,
 }
 
 
-__global__ __launch_bounds__(DEOM_TPB) void deom_stage_kernel(DeomParams p) {
-  __shared__ c128 sH[DEOM_MAX_NS * DEOM_MAX_NS];
-  __shared__ c128 sQ[DEOM_MAX_NMOD * DEOM_MAX_NS * DEOM_MAX_NS];
+// One element e of a stage (any B, ns <= DEOM_MAX_NS, nmod <= DEOM_MAX_NMOD, driven or not) with H(t), Q(t) of the
+// stage in sH / sQ: the generic stage kernel and the banded launch's stream-ordered fallback run this.
+__device__ __forceinline__ void deom_stage_element(const DeomParams& p, size_t e, const c128* sH, const c128* sQ) {
   const int ns = p.ns, ns2 = ns * ns;
-  for (int e = threadIdx.x; e < ns2; e += blockDim.x)
-    sH[e] = p.Hdip ? cadd(p.H[e], cmul(p.Hdip[e], p.fs)) : p.H[e];
-  for (int e = threadIdx.x; e < p.nmod * ns2; e += blockDim.x)
-    sQ[e] = p.Qdip ? cadd(p.Q[e], cmul(p.Qdip[e], p.fc)) : p.Q[e];
-  __syncthreads();
-
-  const size_t tot = (size_t)p.B * p.nmax * ns2;
-  const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (e >= tot) return;
   const int j = (int)(e % ns), i = (int)((e / ns) % ns);
   const size_t bn = e / ns2;                  // b * nmax + n
   const int n = (int)(bn % p.nmax);
@@ -145,6 +136,80 @@ __global__ __launch_bounds__(DEOM_TPB) void deom_stage_kernel(DeomParams p) {
     if (p.snap && n == 0) {
       const size_t b = bn / p.nmax;
       p.snap[(b * (p.nsteps + 1) + p.step + 1) * ns2 + i * ns + j] = v;
+    }
+  }
+}
+
+__device__ __forceinline__ void deom_stage_ops(const DeomParams& p, c128* sH, c128* sQ) {
+  const int ns2 = p.ns * p.ns;
+  for (int e = threadIdx.x; e < ns2; e += blockDim.x)
+    sH[e] = p.Hdip ? cadd(p.H[e], cmul(p.Hdip[e], p.fs)) : p.H[e];
+  for (int e = threadIdx.x; e < p.nmod * ns2; e += blockDim.x)
+    sQ[e] = p.Qdip ? cadd(p.Q[e], cmul(p.Qdip[e], p.fc)) : p.Q[e];
+}
+
+__global__ __launch_bounds__(DEOM_TPB) void deom_stage_kernel(DeomParams p) {
+  __shared__ c128 sH[DEOM_MAX_NS * DEOM_MAX_NS];
+  __shared__ c128 sQ[DEOM_MAX_NMOD * DEOM_MAX_NS * DEOM_MAX_NS];
+  deom_stage_ops(p, sH, sQ);
+  __syncthreads();
+  const size_t tot = (size_t)p.B * p.nmax * p.ns * p.ns;
+  const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (e < tot) deom_stage_element(p, e, sH, sQ);
+}
+
+// Stream-ordered fallback of qd_deom_rk4_banded called without a status word: queued behind the banded launch, it
+// returns at once unless that launch reported a hand-off timeout in *stat; then ONE workgroup restores the saved
+// initial ADOs and runs the whole propagation on deom_stage_element (the stage launches' arithmetic), stage by stage
+// with a device-scope fence and a workgroup barrier between stages (slow -- one CU -- but no host wait: the banded
+// entry point stays asynchronous).  x0 / x1: stage buffers, acc: the classic-form accumulator (driven runs).
+// The band tables' local neighbour rows (lminus / lplus: a band's own rows first, then its halo rows) are mapped back
+// to global ADO rows into gminus / gplus first.
+__global__ __launch_bounds__(1024) void deom_banded_fallback_kernel(DeomParams p, const int* stat, const c128* saved,
+                                                                     c128* ados, c128* x0, c128* x1,
+                                                                     const c128* fsv, const c128* fcv,
+                                                                     const int* lminus, const int* lplus,
+                                                                     const int* band_lo, const int* halo_off,
+                                                                     const int* halo_idx, int nbands, int* gminus,
+                                                                     int* gplus) {
+  if (__hip_atomic_load(stat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  __shared__ c128 sH[DEOM_MAX_NS * DEOM_MAX_NS];
+  __shared__ c128 sQ[DEOM_MAX_NMOD * DEOM_MAX_NS * DEOM_MAX_NS];
+  const size_t tot = (size_t)p.nmax * p.ns * p.ns;
+  for (size_t e = threadIdx.x; e < tot; e += blockDim.x) ados[e] = saved[e];
+  for (int e = threadIdx.x; e < p.nmax * p.K; e += blockDim.x) {
+    const int n = e / p.K;
+    int lo = 0, hi = nbands;   // band b with band_lo[b] <= n < band_lo[b + 1]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) / 2;
+      if (band_lo[mid] <= n) lo = mid;
+      else hi = mid;
+    }
+    const int own = band_lo[lo + 1] - band_lo[lo];
+    auto glob = [&](int r) { return r < 0 ? -1 : r < own ? band_lo[lo] + r : halo_idx[halo_off[lo] + r - own]; };
+    gminus[e] = glob(lminus[e]);
+    gplus[e] = glob(lplus[e]);
+  }
+  __threadfence();
+  __syncthreads();
+  p.minus = gminus;
+  p.plus = gplus;
+  p.rho = ados;
+  p.rho_out = ados;
+  for (int s = 0; s < p.nsteps; ++s) {
+    p.step = s;
+    for (int stage = 0; stage < 4; ++stage) {
+      p.stage = stage;
+      p.xin = stage == 0 ? (const c128*)ados : ((stage - 1) & 1 ? x1 : x0);
+      p.xout = stage & 1 ? x1 : x0;
+      const int ti = s * 3 + (stage + 1) / 2;   // pulse values at t, t + dt/2, t + dt
+      p.fs = fsv ? fsv[ti] : cmk(0, 0);
+      p.fc = fcv ? fcv[ti] : cmk(0, 0);
+      deom_stage_ops(p, sH, sQ);
+      __syncthreads();
+      for (size_t e = threadIdx.x; e < tot; e += blockDim.x) deom_stage_element(p, e, sH, sQ);
+      __threadfence();   // agent-scope release / acquire: the next stage's loads see these stores, not stale L1 lines
+      __syncthreads();
     }
   }
 }
@@ -727,9 +792,11 @@ __global__ void deom_snap0_kernel(const c128* rho, c128* snap, int B, int nmax, 
 // Per-call setup of the banded launch in one kernel (instead of three memsets and a copy): both hand-off buffers to
 // parity 1 in every double (bytes 0x01), the status words to 0, row 0 of the snapshots from the initial ADO 0.
 __global__ void deom_band_prep_kernel(unsigned long long* buf, long nwords, int* stat, int* stat2, const c128* ados,
-                                      c128* snap, int ns2) {
+                                      c128* snap, int ns2, c128* saved, long tot) {
   const long i0 = blockIdx.x * (long)blockDim.x + threadIdx.x, st = (long)gridDim.x * blockDim.x;
   for (long i = i0; i < nwords; i += st) buf[i] = 0x0101010101010101ull;
+  if (saved)   // the initial ADOs for the stream-ordered fallback
+    for (long i = i0; i < tot; i += st) saved[i] = ados[i];
   if (i0 == 0) {
     *stat = 0;
     if (stat2) *stat2 = 0;
@@ -1885,8 +1952,9 @@ hipError_t launch_band(const BandParams& p, int nbands, int tpb, size_t lds, hip
 // tables come from deom_shard.make_plans: band_lo [nbands + 1], halo_off / halo_idx (global halo rows per band),
 // src_off / src (bands owning them), lminus / lplus [nmax][K] local rows; max_own / max_loc the largest band's
 // owned / owned + halo row counts.  ns^2 <= 16 (ns <= 4), K <= 8, max_own ns'^2 <= 1024 lanes (ns' = 2 or 4),
-// every band's rows in LDS.  status (device int, or null): 1 after the run if a hand-off timed out; with null the
-// call synchronises the stream and returns QD_EHIP in that case.
+// every band's rows in LDS.  status (device int, or null): 1 after the run if a hand-off timed out (the caller
+// re-runs); with null the call stays asynchronous and queues a stream-ordered fallback that re-runs the propagation
+// on one workgroup when (and only when) a hand-off timed out (deom_banded_fallback_kernel).
 extern "C" int qd_deom_rk4_banded(qd_c128* ados, int nmax, int K, int ns, const int32_t* lminus, const int32_t* lplus,
                                   const int32_t* band_lo, const int32_t* halo_off, const int32_t* halo_idx,
                                   const int32_t* src_off, const int32_t* src, int nbands, int max_own, int max_loc,
@@ -1927,14 +1995,22 @@ extern "C" int qd_deom_rk4_banded(qd_c128* ados, int nmax, int K, int ns, const 
   const size_t snap_elems = need_snap && !rho_sys ? (size_t)(nsteps + 1) * ns2 : 0;
   const size_t nf = fsys ? (size_t)nsteps * 3 : 0, nc = fcoup ? (size_t)nsteps * 3 : 0;
   const size_t flag_bytes = 16;   // the status word, 16-B padded
+  // without a caller status word the call stays asynchronous: the initial ADOs are saved (and, for driven runs, an
+  // accumulator kept) for a stream-ordered fallback launch that re-runs the propagation only if a hand-off timed out
+  const bool guard = !status && nsteps > 0;
+  const size_t gtab_elems = ((size_t)2 * nmax * K * sizeof(int32_t) + sizeof(c128) - 1) / sizeof(c128);
+  const size_t fb_elems = guard ? (Hdip || Qdip ? 2 : 1) * tot + gtab_elems : 0;
   void* w = nullptr;
-  int rc = workspace(WS_DEOM, (2 * tot + snap_elems + nf + nc) * sizeof(c128) + flag_bytes, &w, st);
+  int rc = workspace(WS_DEOM, (2 * tot + snap_elems + nf + nc + fb_elems) * sizeof(c128) + flag_bytes, &w, st);
   if (rc) return rc;
   c128* buf = (c128*)w;
   c128* snap = rho_sys ? (c128*)rho_sys : (need_snap ? buf + 2 * tot : nullptr);
   c128* fsv = nf ? buf + 2 * tot + snap_elems : nullptr;
   c128* fcv = nc ? buf + 2 * tot + snap_elems + nf : nullptr;
-  int* stat_ws = (int*)(buf + 2 * tot + snap_elems + nf + nc);
+  c128* saved = guard ? buf + 2 * tot + snap_elems + nf + nc : nullptr;
+  c128* fb_acc = guard && (Hdip || Qdip) ? saved + tot : nullptr;
+  int* gtab = guard ? (int*)(saved + (Hdip || Qdip ? 2 : 1) * tot) : nullptr;
+  int* stat_ws = (int*)(buf + 2 * tot + snap_elems + nf + nc + fb_elems);
   int* stat = status ? (int*)status : stat_ws;
   if (fsv) QD_HIP(hipMemcpyAsync(fsv, fsys, nf * sizeof(c128), hipMemcpyHostToDevice, st));
   if (fcv) QD_HIP(hipMemcpyAsync(fcv, fcoup, nc * sizeof(c128), hipMemcpyHostToDevice, st));
@@ -1944,7 +2020,7 @@ extern "C" int qd_deom_rk4_banded(qd_c128* ados, int nmax, int K, int ns, const 
     const long nwords = (long)(2 * tot * sizeof(c128) / 8);
     hipLaunchKernelGGL(deom_band_prep_kernel, dim3((int)std::min<long>((nwords + 255) / 256, 1024)), dim3(256), 0, st,
                        (unsigned long long*)buf, nwords, stat_ws, status ? (int*)status : nullptr,
-                       (const c128*)ados, snap, (int)ns2);
+                       (const c128*)ados, snap, (int)ns2, saved, (long)tot);
     QD_HIP(hipGetLastError());
   }
   if (nsteps > 0) {
@@ -2021,21 +2097,37 @@ extern "C" int qd_deom_rk4_banded(qd_c128* ados, int nmax, int K, int ns, const 
     }
 #endif
     // the last stage 3 wrote the final rho straight into ados (deom_band_kernel)
+    if (guard) {   // stream-ordered fallback: a no-op unless the banded launch reported a hand-off timeout
+      DeomParams f{};
+      f.acc = fb_acc;
+      f.coef = (const c128*)coef;
+      f.damp = (const c128*)damp;
+      f.mode = mode;
+      f.H = (const c128*)H;
+      f.Hdip = (const c128*)Hdip;
+      f.Q = (const c128*)Q;
+      f.Qdip = (const c128*)Qdip;
+      f.snap = snap;
+      f.B = 1;
+      f.nmax = nmax;
+      f.K = K;
+      f.ns = ns;
+      f.nmod = nmod;
+      f.nsteps = nsteps;
+      f.dt = dt;
+      f.horner = !Hdip && !Qdip;
+      note_path("deom_banded_guarded");
+      hipLaunchKernelGGL(deom_banded_fallback_kernel, dim3(1), dim3(1024), 0, st, f, (const int*)stat,
+                         (const c128*)saved, (c128*)ados, buf, buf + tot, (const c128*)fsv, (const c128*)fcv,
+                         lminus, lplus, band_lo, halo_off, halo_idx, nbands, gtab, gtab + (size_t)nmax * K);
+      QD_HIP(hipGetLastError());
+    }
   }
   if (trace) {
     const int n = (nsteps + 1) * ne;
     hipLaunchKernelGGL(deom_trace_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0, st,
                        (const c128*)snap, (const c128*)E, ne, 1, ns, nsteps + 1, (c128*)trace);
     QD_HIP(hipGetLastError());
-  }
-  if (!status && nsteps > 0) {
-    int h = 0;
-    QD_HIP(hipMemcpyAsync(&h, stat, sizeof(int), hipMemcpyDeviceToHost, st));
-    QD_HIP(hipStreamSynchronize(st));
-    if (h) {
-      set_error("qd_deom_rk4_banded: a band hand-off timed out (bands not co-resident); results invalid");
-      return QD_EHIP;
-    }
   }
   return QD_OK;
 }

@@ -102,6 +102,13 @@ __global__ void pad_kernel(const c128* src, c128* dst, int B, int N, int Np) {
   }
 }
 
+// dst = src when *guard != 0 (restores the saved state behind a single-trajectory launch that timed out)
+__global__ void guarded_copy_kernel(const c128* src, c128* dst, size_t n, const int* guard) {
+  if (__hip_atomic_load(guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x)
+    dst[e] = src[e];
+}
+
 __global__ void unpad_kernel(const c128* src, c128* dst, int B, int N, int Np) {
   const size_t tot = (size_t)B * N * N;
   for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
@@ -636,35 +643,37 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   }
 
   // Few undriven matrices: one persistent launch with a workgroup per 16 x 16 output tile (glf_single.hip; the split
-  // path takes eight dependent launches per step).  A refused cooperative launch or a hand-off timeout re-runs the
-  // batch below from a saved copy (on the path the shape selects: split, or persistent when the single path was forced).
+  // path takes eight dependent launches per step).  A refused cooperative launch re-runs on the path the shape selects
+  // (split, or persistent when the single path was forced).  A hand-off timeout is only known on the device: behind the
+  // single launch the call queues a guarded restore of the saved initial state and a guarded run of the persistent
+  // kernel (a workgroup per matrix), both no-ops unless the launch's status word reports the timeout -- no host wait.
+  const int* single_guard = nullptr;
+  void* wsave = nullptr;
   {
     const bool fits = !herm && !nd && B <= glf_single_max_batch(Np, nc);
     if (fits && (force == QD_GLF_AUTO || force == QD_GLF_SINGLE)) {
-      void* wsave = nullptr;
       if ((rc = workspace(WS_MISC, (size_t)B * NN * sizeof(c128), &wsave, st))) return rc;
       QD_HIP(hipMemcpyAsync(wsave, rho_p, (size_t)B * NN * sizeof(c128), hipMemcpyDeviceToDevice, st));
-      int timed_out = 0;
       rc = glf_single_run(mK, iKd, Cop, Cd, nc, eT, ne, rho_p, B, N, Np, dt, nsteps, obs,
-                          save_every > 0 ? snap : nullptr, save_every, &timed_out, st);
-      if (rc == QD_OK && !timed_out) {
+                          save_every > 0 ? snap : nullptr, save_every, &single_guard, st);
+      if (rc == QD_OK && !single_guard) {   // nothing to run
         note_path("glf_single");
-        if (pad) {
-          const size_t tot = (size_t)B * N * N;
-          hipLaunchKernelGGL(unpad_kernel, dim3((int)std::min<size_t>((tot + threads - 1) / threads, 65535)),
-                             dim3(threads), 0, st, rho_p, rho, B, N, Np);
-          QD_HIP(hipGetLastError());
-        }
         return QD_OK;
       }
-      if (rc != QD_OK && rc != QD_EBUSY) return rc;
-      std::fprintf(stderr, "[libqdyn] glf single-trajectory launch %s; re-running on the split path\n",
-                   timed_out ? "timed out" : "refused");
-      QD_HIP(hipMemcpyAsync(rho_p, wsave, (size_t)B * NN * sizeof(c128), hipMemcpyDeviceToDevice, st));
+      if (rc == QD_OK) {
+        note_path("glf_single");
+        hipLaunchKernelGGL(guarded_copy_kernel, dim3(std::min<size_t>((B * NN + 255) / 256, 1024)), dim3(256), 0, st,
+                           (const c128*)wsave, rho_p, (size_t)B * NN, single_guard);
+        QD_HIP(hipGetLastError());
+        split_bt = 0;   // the guarded re-run takes the persistent kernel
+      } else {
+        if (rc != QD_EBUSY) return rc;
+        std::fprintf(stderr, "[libqdyn] glf single-trajectory launch refused; re-running on the split path\n");
+      }
     }
   }
 
-  LindbladParams p;
+  LindbladParams p{};
   p.Cop = Cop;
   p.mK = mK;
   p.iKd = iKd;
@@ -694,6 +703,7 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   p.kslab = split_bt ? scratch + (size_t)B * (2 + nc) * NN : nullptr;
   p.yslab = split_bt ? p.kslab + (size_t)B * kslots * NN : nullptr;
   p.ticket = split_bt ? (unsigned*)(scratch + (size_t)B * per + (pad ? (size_t)B * NN : 0)) : nullptr;
+  p.guard = single_guard;
   if (split_bt && (ks > 1 || ys > 1 || hk2)) QD_HIP(hipMemsetAsync(p.ticket, 0, nticket * sizeof(unsigned), st));
 #ifdef QD_PHASE_TIMING
   const bool timing = true;  // diagnostics build: per-phase clocks to stderr
@@ -745,8 +755,8 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
     }
     return QD_OK;
   };
-  note_path(split_bt ? (hsplit ? "glf_split_pairs" : "glf_split") : nc > MAX_NC ? "glf_persistent_chunk"
-                                                                                : "glf_persistent");
+  note_path(single_guard ? "glf_single_guarded" : split_bt ? (hsplit ? "glf_split_pairs" : "glf_split")
+                                                 : nc > MAX_NC ? "glf_persistent_chunk" : "glf_persistent");
   auto launch = [&]() -> int {
     if (split_bt) return launch_split();
     if (nc > MAX_NC) return glf_launch_chunk(p, B, st);   // glf_chunk.hip

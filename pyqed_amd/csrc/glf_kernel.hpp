@@ -34,6 +34,7 @@ struct LindbladParams {
   c128* kslab;                 // [B][nb^2][ks][BT^2] partial k blocks
   c128* yslab;                 // [B][nc][nb^2][ys][BT^2] partial Y blocks
   unsigned* ticket;            // [B][1 + nc][nb^2] arrival counters (zero between launches)
+  const int* guard;            // persistent kernel: run only if *guard != 0 (the single launch's fallback), or null
 };
 
 namespace {
@@ -189,6 +190,7 @@ __device__ __forceinline__ void herm_k_pass(const CgAcc<128>& A, c128* T01, c128
 // GEMMs run in chunks of MAX_NC collapse-operator segments through the LDS table, accumulating in registers.
 template <int BT, bool HERM, bool HSEG = false, bool CHUNK = false>
 __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
+  if (p.guard && __hip_atomic_load(p.guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
   __shared__ CgLds<BT> L;
   __shared__ c128 sred[CG_WG / 64];
   __shared__ CgSeg segs[2 + MAX_NC];   // segment table in LDS (no scratch)
@@ -488,5 +490,5 @@ int glf_launch_chunk(const LindbladParams& p, int B, hipStream_t st);
 int glf_single_max_batch(int Np, int nc);
 int glf_single_run(const c128* P, const c128* Q, const c128* Lop, const c128* Rop, int nc, const c128* eT, int ne,
                    c128* rho, int B, int N, int Np, double dt, int nsteps, c128* obs, c128* snap, int save_every,
-                   int* timed_out, hipStream_t st);
+                   const int** status_out, hipStream_t st);
 }  // namespace qd

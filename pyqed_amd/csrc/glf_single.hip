@@ -408,7 +408,9 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
 }
 
 // obs[b][gs][m] = sum over the T^2 tiles of obs_part, fixed order
-__global__ void glf_single_obs_kernel(const c128* part, int T2, long n, c128* obs) {
+// (skipped when the launch reported a hand-off timeout: the guarded persistent re-run writes obs itself)
+__global__ void glf_single_obs_kernel(const c128* part, int T2, long n, c128* obs, const int* stat) {
+  if (__hip_atomic_load(stat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
     const c128* s = part + e * T2;
     c128 v = s[0];
@@ -452,13 +454,14 @@ int glf_single_max_batch(int Np, int nc) {
   return 256 / (T * T);
 }
 
-// One persistent launch for B matrices (B <= glf_single_max_batch), undriven GLF operators already padded.  Returns
-// QD_OK with *timed_out = 1 if a hand-off spin expired (the state is then invalid: the caller re-runs it), QD_EBUSY
-// when the cooperative launch is refused (nothing ran).
+// One persistent launch for B matrices (B <= glf_single_max_batch), undriven GLF operators already padded.  Nothing
+// waits on the host: *status_out is the device status word (1 after the launch if a hand-off spin expired -- the state
+// is then invalid and the caller queues a guarded re-run behind it), or null when nothing was launched.  QD_EBUSY when
+// the cooperative launch is refused (nothing ran).
 int glf_single_run(const c128* P, const c128* Q, const c128* Lop, const c128* Rop, int nc, const c128* eT, int ne,
                    c128* rho, int B, int N, int Np, double dt, int nsteps, c128* obs, c128* snap, int save_every,
-                   int* timed_out, hipStream_t st) {
-  *timed_out = 0;
+                   const int** status_out, hipStream_t st) {
+  *status_out = nullptr;
   if (nsteps <= 0 && ne == 0) return QD_OK;
   const int T = Np / 16, T2 = T * T;
   const size_t NN = (size_t)Np * Np;
@@ -528,13 +531,7 @@ int glf_single_run(const c128* P, const c128* Q, const c128* Lop, const c128* Ro
   QD_HIP(e);
   if (option(QD_OPT_FAKE_TIMEOUT))   // tests: report a hand-off timeout after the run
     QD_HIP(hipMemsetAsync(p.status, 1, 1, st));
-  int h = 0;
-  QD_HIP(hipMemcpyAsync(&h, p.status, sizeof(int), hipMemcpyDeviceToHost, st));
-  QD_HIP(hipStreamSynchronize(st));
-  if (h) {
-    *timed_out = 1;
-    return QD_OK;
-  }
+  *status_out = p.status;
 #ifdef QD_PHASE_TIMING
   {   // per-phase wall clock (100 MHz ticks, workgroup thread 0), mean over workgroups, per stage, in us
     std::vector<unsigned long long> hv((size_t)grid * 8);
@@ -555,7 +552,7 @@ int glf_single_run(const c128* P, const c128* Q, const c128* Lop, const c128* Ro
   if (ne) {
     const long n = (long)B * (nsteps + 1) * ne;
     hipLaunchKernelGGL(glf_single_obs_kernel, dim3((int)std::min<long>((n + 255) / 256, 1024)), dim3(256), 0, st,
-                       (const c128*)p.obs_part, T2, n, obs);
+                       (const c128*)p.obs_part, T2, n, obs, (const int*)p.status);
     QD_HIP(hipGetLastError());
   }
   return QD_OK;

@@ -145,6 +145,29 @@ def test_2des_bench_size_gemm128_path_matches_reference(j):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("j", [0, 37])
+def test_2des_shard_size_gemm64_matches_reference(j):
+    """The one-rank 1/8 shard of the bench ensemble (8,192+ members) takes the 64-block split-K GEMM (ens_gemm64, the
+    path the bench's shard_1of8 line times): the fixture's three members repeated 2,731 times (8,193 members,
+    K = 16,386 -- not a multiple of the 16-wide K-tile), summed by the GPU and divided by the repeat count, equal the
+    sum of the reference's slices."""
+    from pyqed_amd.response import ensemble_factors, response2d_ensemble
+    from conftest import took
+    g = load_golden("corr4_2des_256")
+    tau = g["tau"]
+    lam, U1, U2, ops, rho0 = _two_des_members(g)
+    alpha, Mt, beta = ensemble_factors(lam, U1, U2, ops, rho0.flatten(), tau[j])
+    R = 2731
+    rep = lambda a: np.tile(a, (R,) + (1,) * (a.ndim - 1))
+    took("")
+    S = response2d_ensemble(rep(lam), rep(alpha), rep(Mt), rep(beta), tau, tau).cpu().numpy()
+    hit, paths = took("ens_gemm64")
+    assert hit, paths
+    tot = sum(g[f"m{m}_j{j}"] for m in range(len(g["E"])))
+    assert relerr(S / R, tot) < TOL
+
+
+@pytest.mark.gpu
 def test_spo2_256_matches_reference():
     """Config d2 (256 x 256 x 2, the bench potential, dt = 0.05): 20 Strang steps of SPO2.run (wpd.py:692-758)
     against the reference's final state and per-output populations."""

@@ -19,8 +19,9 @@ def _bath(npsd, nmod=1):
                 [m for m in range(nmod) for _ in range(npsd + 1)])
 
 
-def _run(sol, rho0, dt, nt, nbands, p1=None):
-    """(rho_sys or trace, final ADOs) of one hierarchy: banded with `nbands` bands, or (None) the stage launches."""
+def _run(sol, rho0, dt, nt, nbands, p1=None, status=True):
+    """(rho_sys or trace, final ADOs) of one hierarchy: banded with `nbands` bands, or (None) the stage launches.
+    status=False passes no status word (the asynchronous form with the stream-ordered fallback)."""
     import torch
     from pyqed_amd import _lib
     from pyqed_amd.deom import ado_coefficients
@@ -63,14 +64,15 @@ def _run(sol, rho0, dt, nt, nbands, p1=None):
     else:
         bt = sol.band_tables(dev, nbands)
         assert bt is not None and bt.nbands == min(nbands, nmax)
-        status = torch.zeros(1, dtype=torch.int32, device=dev)
+        stat = torch.zeros(1, dtype=torch.int32, device=dev) if status else None
         rc = lib.qd_deom_rk4_banded(ados.data_ptr(), nmax, K, ns, *bt.args(), coef_t.data_ptr(), damp_t.data_ptr(),
                                     mode_t.data_ptr(), nmod, H.data_ptr(), _lib.ptr(Hd), Q.data_ptr(), _lib.ptr(Qd),
                                     fsp, fcp, dt, nt, rho_sys.data_ptr(), _lib.ptr(p1_t), 1 if p1 is not None else 0,
-                                    _lib.ptr(trace), status.data_ptr(), st)
+                                    _lib.ptr(trace), _lib.ptr(stat), st)
         _lib.check(rc, "qd_deom_rk4_banded")
         torch.cuda.synchronize(dev)
-        assert int(status.item()) == 0
+        if status:
+            assert int(stat.item()) == 0
     torch.cuda.synchronize(dev)
     out = trace[:, 0] if p1 is not None else rho_sys
     return out.cpu().numpy(), ados.cpu().numpy()
@@ -218,6 +220,72 @@ def test_solver_run_falls_back_to_stage_launches_after_band_timeout():
     _, again = sol.run(rho0.copy(), 0.005, 20)
     assert sol.last_run_banded is True
     assert relerr(np.array(again), np.array(ref)) < HALO_TAG_TOL
+
+
+@pytest.mark.parametrize("pulsed", [False, True])
+def test_banded_without_status_word_falls_back_on_device(pulsed):
+    """qd_deom_rk4_banded without a status word stays asynchronous -- a hand-off timeout (forced by
+    QD_OPT_FAKE_TIMEOUT after a real banded run) is repaired by the stream-ordered fallback queued behind the launch
+    (one workgroup restores the saved ADOs and re-runs every stage on the element stencil, band tables mapped back to
+    global rows): rho_sys at every step, the trace and the final ADOs equal the stage launches' within 1e-13, for the
+    Horner form and for a driven (classic RK4) run; without the timeout the guard changes nothing."""
+    from conftest import qd_option, took
+    sol = _spin_boson(5, npsd=3, pulses=pulsed)
+    rho0 = np.array([[1, 0], [0, 0]], complex)
+    ref, ref_ados = _run(sol, rho0, 0.01, 12, None)
+    took("")
+    with qd_option("fake_timeout", 1):
+        got, got_ados = _run(sol, rho0, 0.01, 12, 9, status=False)
+    assert "deom_banded_guarded" in took("")[1]
+    assert relerr(got, ref) < 1e-13 and relerr(got_ados, ref_ados) < 1e-13
+    plain, plain_ados = _run(sol, rho0, 0.01, 12, 9, status=False)
+    banded, banded_ados = _run(sol, rho0, 0.01, 12, 9)
+    assert np.array_equal(plain, banded) and np.array_equal(plain_ados, banded_ados)
+
+
+def test_banded_call_without_status_returns_before_its_kernels_finish():
+    """VERDICT r05 item 6 (SURVEY §8(b) threading): with no status word the banded call queues its launch and the
+    guarded fallback and returns; a 2000-step call at the bench hierarchy (~17 ms of device time) returns to the host in
+    a small fraction of it."""
+    import time
+    import torch
+    from pyqed_amd import _lib
+    from pyqed_amd.deom import ado_coefficients
+    sol = _spin_boson(12)
+    sol.check_()
+    sol.init_()
+    dev = torch.device("cuda", 0)
+    ns, K, nmax = sol.nsys, sol.nind, sol.nmax
+    b = sol.bath
+    coef, damp = ado_coefficients(sol.keys, np.asarray(b.etal), np.asarray(b.etar), np.asarray(b.etaa),
+                                  np.asarray(b.expn), sol.lmax)
+    c128 = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=complex))).to(dev)
+    i32 = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=np.int32))).to(dev)
+    ados = torch.zeros((nmax, ns, ns), dtype=torch.complex128, device=dev)
+    ados[0, 0, 0] = 1
+    H, Q = c128(sol.system), c128(np.asarray(sol.coupling, dtype=complex).reshape(-1, ns, ns))
+    coef_t, damp_t, mode_t = c128(coef), c128(damp), i32(b.mode)
+    bt = sol.band_tables(dev, 256)
+    lib = _lib.load()
+    st = _lib.stream_ptr(dev)
+
+    def call(nt):
+        rc = lib.qd_deom_rk4_banded(ados.data_ptr(), nmax, K, ns, *bt.args(), coef_t.data_ptr(), damp_t.data_ptr(),
+                                    mode_t.data_ptr(), Q.shape[0], H.data_ptr(), None, Q.data_ptr(), None, None, None,
+                                    0.002, nt, None, None, 0, None, None, st)
+        _lib.check(rc, "qd_deom_rk4_banded")
+
+    call(5)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    call(2000)
+    host = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    total = time.perf_counter() - t0
+    print(f"host return {host * 1e3:.2f} ms of {total * 1e3:.2f} ms")
+    assert host < 0.25 * total, (host, total)
+    tr = torch.diagonal(ados[0]).sum().item()
+    assert abs(tr - 1) < 1e-10
 
 
 def test_banded_cooperative_and_plain_launch_agree():

@@ -140,10 +140,11 @@ def test_ensemble_large_linearity_and_shards():
     assert relerr(one.cpu().numpy(), ref) < TOL
 
 
-@pytest.mark.parametrize("M", [1000, 2048])
-def test_ensemble_gemm64_matches_closed_form(M):
-    """The 64-block ensemble GEMM (operand loads two K-tiles ahead; M = 1000 gives workgroups with odd and even K-tile
-    counts) against the closed form summed over every member."""
+@pytest.mark.parametrize("M,grid", [(1000, "uniform"), (1001, "uniform"), (2048, "uniform"), (1000, "array")])
+def test_ensemble_gemm64_matches_closed_form(M, grid):
+    """The 64-block ensemble GEMM (operand loads two K-tiles ahead) against the closed form summed over every member:
+    M = 1000 gives workgroups with odd and even K-tile counts, M = 1001 a K that is not a multiple of the K-tile; uniform
+    grids build X and Z from exponential tables, an array grid from the time arrays."""
     from pyqed_amd.response import response2d_ensemble
     from conftest import took
     rng = np.random.default_rng(M)
@@ -151,10 +152,13 @@ def test_ensemble_gemm64_matches_closed_form(M):
     t = 0.5 * np.arange(256)
     lam, (alpha, Mt, beta) = _ensemble_inputs(E, 0.0)
     took("")
-    got = response2d_ensemble(lam, alpha, Mt, beta, t, t).cpu().numpy()
+    import torch
+    tg = t if grid == "uniform" else torch.from_numpy(t + 1e-3 * np.sin(np.arange(256))).cuda()
+    got = response2d_ensemble(lam, alpha, Mt, beta, tg, t).cpu().numpy()
     hit, paths = took("ens_gemm64")
     assert hit, paths
-    X = alpha[:, None, :] * np.exp(t[None, :, None] * lam[:, None, :])      # [M][n3][K]
+    t3 = t if grid == "uniform" else tg.cpu().numpy()
+    X = alpha[:, None, :] * np.exp(t3[None, :, None] * lam[:, None, :])     # [M][n3][K]
     Y = beta[:, None, :] * np.exp(t[None, :, None] * lam[:, None, :])       # [M][n1][K]
     ref = (-1j) ** 3 * np.einsum("mik,mkl,mjl->ij", X, Mt, Y, optimize=True)
     assert relerr(got, ref) < TOL
