@@ -1302,30 +1302,39 @@ def main():
     # (profiles/r04/lindblad/launch_overhead.txt).  The auto dispatch runs B = 64 (Hermitian states, 16 <= B < 192) on
     # the Hermitian pair-block split path and B = 1 as one single-trajectory launch; each entry's flops are its own
     # path's (Hermitian GLF form / general GLF form)
+    from pyqed_amd import _lib
     from pyqed_amd.oqs import HERM_SPLIT_MIN_BATCH
     batch_sweep = {}
     for Bs in (1, 64):
         rs = rho[:Bs].clone()
-        hs = Bs >= HERM_SPLIT_MIN_BATCH and not args.general and N <= 128
-        lindblad_rk4(Ht, Ct, rs, args.dt, 2)
+        _lib.take_path()
+        lindblad_rk4(Ht, Ct, rs, args.dt, 2, hermitian=False if args.general else None)
         torch.cuda.synchronize(dev)
+        taken = _lib.take_path()
+        # B = 1 of Hermitian states runs the Hermitian single launch (glf_single_herm_kernel), B = 64 the Hermitian
+        # pair-block split path: both execute the Hermitian form's flops
+        hsingle = "glf_single_herm" in taken
+        hs = hsingle or (Bs >= HERM_SPLIT_MIN_BATCH and not args.general and N <= 128)
         ss = 300   # ~90 ms of B = 64 work: a measured leg that also carries the GPU out of idle clocks
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
-        lindblad_rk4(Ht, Ct, rs, args.dt, ss)
+        lindblad_rk4(Ht, Ct, rs, args.dt, ss, hermitian=False if args.general else None)
         e1.record(stream)
         torch.cuda.synchronize(dev)
         sec = e0.elapsed_time(e1) / 1e3
-        fl = lindblad_flops_per_step(N, nc, hs)
+        fl = lindblad_executed_flops_per_step(N, nc, True) if hsingle else lindblad_flops_per_step(N, nc, hs)
         tf = fl * Bs * ss / sec / 1e12
         batch_sweep[str(Bs)] = {
             "dm_steps_per_s": round(Bs * ss / sec, 1), "us_per_step": round(sec / ss * 1e6, 2),
-            "path": ("Hermitian pair-block split (glf_split_hk)" if hs else
+            "path": ("Hermitian single-trajectory launch (glf_single_herm_kernel, executed Hermitian-form flops)"
+                     if hsingle else "Hermitian pair-block split (glf_split_hk)" if hs else
                      "single-trajectory tile launch (glf_single_kernel)" if Bs == 1 and N in (32, 64, 128) and nc <= 2
                      else "glf split-K (general kernel)"),
+            "paths_taken": taken,
             "roofline": {"bound": "mfma", "achieved": round(tf, 3), "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(tf / FP64_MFMA_PEAK_TFLOPS, 4), "flop_per_dm_step": fl,
-                         "traffic": (measured_traffic("glf_single_kernel<4,1,true,true>_b1", ss)
+                         "traffic": (measured_traffic("glf_single_herm_kernel<1,true>_b1" if hsingle else
+                                                      "glf_single_kernel<4,1,true,true>_b1", ss)
                                      if (Bs, N, nc) == (1, 128, 1) else None)}}
     single_rate = batch_sweep["1"]["dm_steps_per_s"]
 

@@ -650,12 +650,14 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   const int* single_guard = nullptr;
   void* wsave = nullptr;
   {
-    const bool fits = !herm && !nd && B <= glf_single_max_batch(Np, nc);
+    // Hermitian Lindblad states at N_p = 128 (B <= 2, nc in {1, 2}) take the Hermitian single launch
+    const bool hsingle = herm && src == GLF_FROM_LINDBLAD && B <= glf_single_max_batch(Np, nc, 1);
+    const bool fits = !nd && (herm ? hsingle : B <= glf_single_max_batch(Np, nc));
     if (fits && (force == QD_GLF_AUTO || force == QD_GLF_SINGLE)) {
       if ((rc = workspace(WS_MISC, (size_t)B * NN * sizeof(c128), &wsave, st))) return rc;
       QD_HIP(hipMemcpyAsync(wsave, rho_p, (size_t)B * NN * sizeof(c128), hipMemcpyDeviceToDevice, st));
       rc = glf_single_run(mK, iKd, Cop, Cd, nc, eT, ne, rho_p, B, N, Np, dt, nsteps, obs,
-                          save_every > 0 ? snap : nullptr, save_every, &single_guard, st);
+                          save_every > 0 ? snap : nullptr, save_every, &single_guard, st, hsingle ? 1 : 0);
       if (rc == QD_OK && !single_guard) {   // nothing to run
         note_path("glf_single");
         return QD_OK;

@@ -487,8 +487,8 @@ namespace qd {
 // The CHUNK instantiations of lindblad_rk4_kernel (nc > MAX_NC), one workgroup per matrix (glf_chunk.hip).
 int glf_launch_chunk(const LindbladParams& p, int B, hipStream_t st);
 // Few matrices as one persistent launch, a workgroup per 16 x 16 output tile (glf_single.hip).
-int glf_single_max_batch(int Np, int nc);
+int glf_single_max_batch(int Np, int nc, int herm = 0);
 int glf_single_run(const c128* P, const c128* Q, const c128* Lop, const c128* Rop, int nc, const c128* eT, int ne,
                    c128* rho, int B, int N, int Np, double dt, int nsteps, c128* obs, c128* snap, int save_every,
-                   const int** status_out, hipStream_t st);
+                   const int** status_out, hipStream_t st, int herm = 0);
 }  // namespace qd

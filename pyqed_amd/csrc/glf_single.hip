@@ -60,6 +60,7 @@ struct SingleParams {
   unsigned long long* tim;   // QD_PHASE_TIMING builds: [grid][8] wall-clock ticks per phase (thread 0's view)
   int N, ne, nsteps, step0, total_steps, save_every, nsave;
   int split;           // 1: a second workgroup per tile computes the Y_c tiles (grid = 2 B T^2)
+  int B;               // matrices (the Hermitian launch)
   double dt;
 };
 
@@ -407,6 +408,262 @@ __global__ __launch_bounds__(SG_WG) void glf_single_kernel(SingleParams p) {
 #endif
 }
 
+// ---------------------------------------------------------------- Hermitian single launch (N_p = 128)
+// For exactly Hermitian H and rho (the usual LindbladSolver.run case) the right-hand side is
+//   k = P r + (P r)^+ + sum_c (C_c r) C_c^+,   P = -iK,
+// Hermitian itself, so only the T (T + 1) / 2 tiles with bm <= bn are made.  Roles:
+//   - Y workgroups (every tile (bm, bn), as the general launch's split roles): sweep the column bn of the stage input,
+//     publish Y_c(bm, bn) = C_c[bm, :] r[:, bn] and the tile (P r)(bm, bn);
+//   - k workgroups (the upper tiles): never read the stage input -- they sweep the Y_c row bm and the two tiles
+//     (P r)(bm, bn), (P r)(bn, bm), form t = sum_c Y_c[bm, :] (C_c^+ / 2)[:, bn] on the MFMAs and
+//       bm < bn:  k = (P r)(bm, bn) + conj((P r)(bn, bm))^T + 2 t      (the halved operator doubled: exact)
+//       bm = bn:  k = (P r)(bm, bm) + conj((P r)(bm, bm))^T + (t + conj(t)^T)
+//     (every element's mirror is formed from the same operands in the commuted order, so each diagonal tile -- and with
+//     the mirrors written as conjugates, every stage -- is Hermitian bit for bit), update s = rho + dt / (4 - m) k and
+//     publish the tile and, off the diagonal, its conjugate transpose at (bn, bm).
+// So a k workgroup ingests one 32 KB strip (Y_c row, per c) and two tiles instead of two strips, and a stage runs
+// 64 (1 + nc) + 36 nc tile products instead of 64 (2 + 2 nc).  Hand-offs, buffers and parities as the general launch;
+// the buffer-reuse order holds through the Y workgroups' P r tiles (a tile's owner consumed, in stage g - 1, the P r or
+// Y_c tile of every Y workgroup that reads its tile).
+template <int NC, bool M3>
+__global__ __launch_bounds__(SG_WG) void glf_single_herm_kernel(SingleParams p) {
+  constexpr int KS = 4, T = 8, Np = 128, NN = Np * Np, TU = T * (T + 1) / 2;
+  __shared__ c128 red[2][8][256];
+  __shared__ c128 tT[256];    // the diagonal tiles' t, for its transpose
+  __shared__ int sAbort[2];
+  const int mats = p.B;
+  const int nk = mats * TU;
+  const bool yrole = (int)blockIdx.x >= nk;
+  int b, bm, bn;
+  if (yrole) {
+    const int w = (int)blockIdx.x - nk;
+    b = w / (T * T);
+    bm = (w - b * T * T) / T;
+    bn = w - b * T * T - bm * T;
+  } else {
+    b = (int)blockIdx.x / TU;
+    int u = (int)blockIdx.x - b * TU;
+    bm = 0;
+    while (u >= T - bm) {   // upper pair u -> (bm, bn), row-major over bm <= bn
+      u -= T - bm;
+      ++bm;
+    }
+    bn = bm + u;
+  }
+  const bool diag = bm == bn;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lk = lane >> 4;
+  const int kb = wave * 4 * KS;
+  // Y workgroups: A fragments (rows bm of C_c and of P); k workgroups: B fragments (columns bn of C_c^+ / 2)
+  c128 fA[NC + 1][KS];
+#pragma unroll
+  for (int q = 0; q < KS; ++q) {
+    const int k = kb + 4 * q + lk;
+    if (yrole) {
+      fA[NC][q] = p.P[(bm * 16 + lr) * Np + k];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) fA[c][q] = p.Lop[(size_t)c * NN + (bm * 16 + lr) * Np + k];
+    } else {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) fA[c][q] = p.Rop[(size_t)c * NN + k * Np + bn * 16 + lr];
+    }
+  }
+  const bool owner = tid < 256 && !yrole;
+  const int ti = (tid >> 4) & 15, tj = tid & 15;
+  const int orow = bm * 16 + ti, ocol = bn * 16 + tj;
+  c128* rhob = p.rho + (size_t)b * NN;
+  c128 rh = owner ? rhob[orow * Np + ocol] : cmk(0, 0);
+  if (tid < 2) sAbort[tid] = 0;
+  __syncthreads();
+  const int slab = mats * NN * (int)sizeof(c128);
+
+  // Tr(E_m rho) over the tile and (off the diagonal) its mirror -> slot (bm, bn); slot (bn, bm) gets zero
+  auto observe = [&](int gs) {
+    for (int m = 0; m < p.ne; ++m) {
+      c128 v = cmk(0, 0);
+      if (owner) {
+        const c128* E = p.eT + (size_t)m * NN;
+        v = cmul(rh, E[orow * Np + ocol]);
+        if (!diag) v = cadd(v, cmul(cconj(rh), E[ocol * Np + orow]));
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        v.re += __shfl_xor(v.re, off, 64);
+        v.im += __shfl_xor(v.im, off, 64);
+      }
+      __syncthreads();
+      if (lane == 0) red[0][0][wave] = v;
+      __syncthreads();
+      if (tid == 0) {
+        c128 s = red[0][0][0];
+        for (int q = 1; q < 4; ++q) s = cadd(s, red[0][0][q]);
+        c128* part = p.obs_part + (((size_t)b * (p.total_steps + 1) + gs) * p.ne + m) * (T * T);
+        part[bm * T + bn] = s;
+        if (!diag) part[bn * T + bm] = cmk(0, 0);
+      }
+    }
+  };
+  if (p.ne > 0 && p.step0 == 0 && !yrole) observe(0);
+
+  auto reduce = [&](const SgAcc<M3>& acc, int par) -> c128 {
+    d4 re, im;
+    acc.result(re, im);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[par][wave][(lk + 4 * r) * 16 + lr] = cmk(re[r], im[r]);
+    __syncthreads();
+    c128 v = cmk(0, 0);
+    if (tid < 256) {
+      v = red[par][0][tid];
+#pragma unroll
+      for (int q = 1; q < 8; ++q) v = cadd(v, red[par][q][tid]);
+    }
+    return v;
+  };
+
+#ifdef QD_PHASE_TIMING
+  unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = wall_clock64();
+#endif
+  const int G4 = 4 * p.nsteps;
+  unsigned long long wy = 0, wky = 0;
+  for (int g = 0; g < G4; ++g) {
+    const int s = g >> 2, m = g & 3, par = g & 1;
+    const unsigned tr = (unsigned)(g >> 1) & 1u, ty = tr;
+    bool good = true;
+    const int yo = (g & 1) * NC * mats * NN, vo = (2 * NC + (g & 1)) * mats * NN;
+    const __amdgpu_buffer_rsrc_t ry = sc1_rsrc(p.ybuf, 2 * (NC + 1) * slab);
+    if (yrole) {
+      // ---- stage input column bn -> Y_c(bm, bn), (P r)(bm, bn)
+      const c128* rin = g == 0 ? p.rho : p.rbuf + (size_t)(g & 1) * mats * NN;
+      const __amdgpu_buffer_rsrc_t rr = sc1_rsrc(rin, slab);
+      c128 rcol[KS];
+      auto col_off = [&](int q) { return ((b * Np + kb + 4 * q + lk) * Np + bn * 16 + lr) * 16; };
+      if (g == 0) {
+#pragma unroll
+        for (int q = 0; q < KS; ++q) rcol[q] = ld16_sc1(rr, col_off(q));
+      } else {
+        const unsigned long long t0 = wall_clock64();
+        sg_delay_until(t0 + sg_delay_ticks(wy, SG_ADAPT_Y));
+        good = sg_sweep<0>(rcol, rr, col_off, tr, p.status, lane);
+        wy = wall_clock64() - t0;
+      }
+      if (!good && lane == 0) sAbort[par] = 1;
+      SG_MARK(0)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        SgAcc<M3> acc;
+#pragma unroll
+        for (int q = 0; q < KS; ++q) acc.mac(fA[c][q], rcol[q]);
+        const c128 y = reduce(acc, par);
+        __syncthreads();   // the slot is reused by the next reduction
+        if (tid < 256) st16_sc1(ry, (yo + ((c * mats + b) * Np + orow) * Np + ocol) * 16, sg_tag(y, ty));
+      }
+      SgAcc<M3> av;
+#pragma unroll
+      for (int q = 0; q < KS; ++q) av.mac(fA[NC][q], rcol[q]);
+      const c128 pv = reduce(av, par);
+      if (tid < 256) st16_sc1(ry, (vo + (b * Np + orow) * Np + ocol) * 16, sg_tag(pv, ty));
+      if (sAbort[par]) break;   // read after the reductions' barriers, which a timed-out wave reached
+      SG_MARK(1)
+      continue;
+    }
+    // ---- k workgroup: t = sum_c Y_c[bm, :] (C_c^+ / 2)[:, bn]
+    c128 t = cmk(0, 0);
+    c128 pe[2];
+    auto sweep_pr = [&]() {
+      const int o1 = (vo + (b * Np + bm * 16 + ti) * Np + bn * 16 + tj) * 16;
+      const int o2 = (vo + (b * Np + bn * 16 + tj) * Np + bm * 16 + ti) * 16;
+      return sg_sweep<0>(pe, ry, [&](int q) { return q ? o2 : o1; }, ty, p.status, lane);
+    };
+    if constexpr (NC > 0) {
+      c128 yrow[NC][KS];
+      auto y_off = [&](int c, int q) {
+        return (yo + ((c * mats + b) * Np + bm * 16 + lr) * Np + kb + 4 * q + lk) * 16;
+      };
+      const unsigned long long t0 = wall_clock64();
+      sg_delay_until(t0 + sg_delay_ticks(wky, SG_ADAPT_KY));
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (good) good = sg_sweep<0>(yrow[c], ry, [&](int q) { return y_off(c, q); }, ty, p.status, lane);
+      wky = wall_clock64() - t0;
+      SG_MARK(3)
+      SgAcc<M3> acc;
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int q = 0; q < KS; ++q) acc.mac(yrow[c][q], fA[c][q]);
+      // the two P r tiles (element (ti, tj) of (bm, bn) and element (tj, ti) of (bn, bm)), sought under the MFMAs
+      if (good) good = sweep_pr();
+      if (!good && lane == 0) sAbort[par] = 1;
+      t = reduce(acc, par);
+    } else {
+      if (good) good = sweep_pr();
+      if (!good && lane == 0) sAbort[par] = 1;
+      __syncthreads();
+    }
+    if (diag) {
+      if (tid < 256) tT[tid] = t;
+    }
+    __syncthreads();
+    if (sAbort[par]) break;
+    SG_MARK(4)
+    c128 kv;
+    if (diag) {
+      const c128 tt = tT[tj * 16 + ti];
+      kv = cadd(cadd(pe[0], cconj(pe[1])), cadd(t, cconj(tt)));
+    } else {
+      kv = cadd(cadd(pe[0], cconj(pe[1])), cmk(t.re + t.re, t.im + t.im));
+    }
+    const double hc = rk4_horner_coef(p.dt, m);
+    const c128 v = cadd(rh, cscale(kv, hc));
+    if (m == 3) rh = v;
+    if (owner && g + 1 < G4) {
+      const __amdgpu_buffer_rsrc_t ro = sc1_rsrc(p.rbuf + (size_t)((g + 1) & 1) * mats * NN, slab);
+      const unsigned tn = (unsigned)((g + 1) >> 1) & 1u;
+      st16_sc1(ro, ((b * Np + orow) * Np + ocol) * 16, sg_tag(v, tn));
+      if (!diag) st16_sc1(ro, ((b * Np + ocol) * Np + orow) * 16, sg_tag(cconj(v), tn));
+    }
+    if (m == 3) {
+      const int gs = p.step0 + s + 1;
+      if (p.snap && p.save_every > 0 && gs % p.save_every == 0) {
+        const int si = gs / p.save_every - 1;
+        if (owner && si < p.nsave) {
+          c128* sn = p.snap + ((size_t)b * p.nsave + si) * p.N * p.N;
+          if (orow < p.N && ocol < p.N) {
+            sn[(size_t)orow * p.N + ocol] = v;
+            if (!diag) sn[(size_t)ocol * p.N + orow] = cconj(v);
+          }
+        }
+      }
+      if (p.ne > 0) observe(gs);
+    }
+    SG_MARK(5)
+  }
+  if (owner) {
+    rhob[orow * Np + ocol] = rh;
+    if (!diag) rhob[ocol * Np + orow] = cconj(rh);
+  }
+#ifdef QD_PHASE_TIMING
+  if (tid == 0 && p.tim)
+    for (int k = 0; k < 6; ++k) p.tim[(size_t)blockIdx.x * 8 + k] = tacc[k];
+#endif
+}
+
+template <int NC, bool M3>
+hipError_t sgh_launch2(SingleParams p, int grid, bool coop, hipStream_t st) {
+  if (!coop) {
+    hipLaunchKernelGGL((glf_single_herm_kernel<NC, M3>), dim3(grid), dim3(SG_WG), 0, st, p);
+    return hipGetLastError();
+  }
+  void* args[] = {(void*)&p};
+  return hipLaunchCooperativeKernel((const void*)glf_single_herm_kernel<NC, M3>, dim3(grid), dim3(SG_WG), args, 0, st);
+}
+template <int NC>
+hipError_t sgh_launch(SingleParams p, int B, bool coop, hipStream_t st, int& grid) {
+  grid = B * (36 + 64);
+  const bool m3 = grid <= 128 && NC < 2;
+  note_path(m3 ? "glf_single_herm_3m" : "glf_single_herm_4m");
+  return m3 ? sgh_launch2<NC, true>(p, grid, coop, st) : sgh_launch2<NC, false>(p, grid, coop, st);
+}
+
 // obs[b][gs][m] = sum over the T^2 tiles of obs_part, fixed order
 // (skipped when the launch reported a hand-off timeout: the guarded persistent re-run writes obs itself)
 __global__ void glf_single_obs_kernel(const c128* part, int T2, long n, c128* obs, const int* stat) {
@@ -448,7 +705,8 @@ hipError_t sg_launch(SingleParams p, int grid, bool coop, hipStream_t st) {
 
 }  // namespace
 
-int glf_single_max_batch(int Np, int nc) {
+int glf_single_max_batch(int Np, int nc, int herm) {
+  if (herm) return (Np == 128 && nc >= 1 && nc <= 2) ? 256 / (64 + 36) : 0;
   if (nc > 2 || (Np != 32 && Np != 64 && Np != 128)) return 0;
   const int T = Np / 16;
   return 256 / (T * T);
@@ -460,7 +718,7 @@ int glf_single_max_batch(int Np, int nc) {
 // the cooperative launch is refused (nothing ran).
 int glf_single_run(const c128* P, const c128* Q, const c128* Lop, const c128* Rop, int nc, const c128* eT, int ne,
                    c128* rho, int B, int N, int Np, double dt, int nsteps, c128* obs, c128* snap, int save_every,
-                   const int** status_out, hipStream_t st) {
+                   const int** status_out, hipStream_t st, int herm) {
   *status_out = nullptr;
   if (nsteps <= 0 && ne == 0) return QD_OK;
   const int T = Np / 16, T2 = T * T;
@@ -491,6 +749,7 @@ int glf_single_run(const c128* P, const c128* Q, const c128* Lop, const c128* Ro
   p.nsave = save_every > 0 ? nsteps / save_every : 0;
   p.snap = p.nsave > 0 ? snap : nullptr;
   p.dt = dt;
+  p.B = B;
   // every handed-off buffer preset to the parity its first epoch does not have: r_1 (buffer 1) and r_2 (buffer 0)
   // carry parities 0 and 1, Y_0 and Y_1 (buffers 0 and 1) both 0; bytes of 0x01 make every double's lowest bit 1
   QD_HIP(hipMemsetAsync(p.status, 0, flag_bytes, st));
@@ -505,6 +764,46 @@ int glf_single_run(const c128* P, const c128* Q, const c128* Lop, const c128* Ro
   p.tim = (unsigned long long*)tw;
 #endif
   const bool coop = option(QD_OPT_COOP_LAUNCH) != 0;
+  if (herm) {   // Hermitian H and rho, N_p = 128, nc in {1, 2}: upper k tiles + Y workgroups (glf_single_herm_kernel)
+    p.split = 1;
+    int grid = 0;
+    note_path("glf_single_herm");
+    hipError_t e = nc == 1 ? sgh_launch<1>(p, B, coop, st, grid) : sgh_launch<2>(p, B, coop, st, grid);
+    if (e == hipErrorCooperativeLaunchTooLarge) {
+      (void)hipGetLastError();
+      set_error("glf Hermitian single-trajectory launch: %d workgroups cannot be co-resident", grid);
+      return QD_EBUSY;
+    }
+    QD_HIP(e);
+    if (option(QD_OPT_FAKE_TIMEOUT)) QD_HIP(hipMemsetAsync(p.status, 1, 1, st));
+    *status_out = p.status;
+#ifdef QD_PHASE_TIMING
+    {   // per-phase wall clock (100 MHz ticks, thread 0), mean over each role's workgroups, per stage, in us
+      std::vector<unsigned long long> hv((size_t)grid * 8);
+      QD_HIP(hipMemcpy(hv.data(), p.tim, hv.size() * 8, hipMemcpyDeviceToHost));
+      const char* nm[6] = {"wait_r", "y_publish", "-", "wait_y", "yr_reduce_pr", "update_publish"};
+      const int nkw = B * T * (T + 1) / 2;
+      for (int role = 0; role < 2; ++role) {
+        const int q0 = role ? nkw : 0, q1 = role ? std::min(grid, nkw + B * T2) : nkw;
+        fprintf(stderr, "[glf herm single phase timing] N=%d B=%d nsteps=%d %s workgroups, us per stage:", N, B, nsteps,
+                role ? "Y" : "k");
+        for (int k = 0; k < 6; ++k) {
+          double sm = 0;
+          for (int q = q0; q < q1; ++q) sm += (double)hv[(size_t)q * 8 + k];
+          fprintf(stderr, " %s %.3f", nm[k], sm / (q1 - q0) / 100.0 / (4.0 * nsteps));
+        }
+        fprintf(stderr, "\n");
+      }
+    }
+#endif
+    if (ne) {
+      const long n = (long)B * (nsteps + 1) * ne;
+      hipLaunchKernelGGL(glf_single_obs_kernel, dim3((int)std::min<long>((n + 255) / 256, 1024)), dim3(256), 0, st,
+                         (const c128*)p.obs_part, T2, n, obs, (const int*)p.status);
+      QD_HIP(hipGetLastError());
+    }
+    return QD_OK;
+  }
   // a second workgroup per tile for the Y_c tiles when the chip has room: the k workgroup's P r + r Q then runs
   // while the Y_c tiles are computed and handed over, instead of after its own Y_c tile
   p.split = nc > 0 && 2 * B * T2 <= 256;

@@ -71,7 +71,8 @@ def lindblad_rk4(H: torch.Tensor, c_ops: torch.Tensor | None, rho: torch.Tensor,
     hermitian: use the Hermitian-state kernel (qd_lindblad_rk4_herm: L[rho] = X + X^+,
     1 + 2nc complex GEMMs per RHS instead of 2 + 2nc, one persistent workgroup per matrix).
     None = auto: on when H and every rho in the batch equal their conjugate transposes bit for bit,
-    N <= 128 and B >= HERM_SPLIT_MIN_BATCH.  From 208 matrices the library runs the persistent
+    N <= 128 and B >= HERM_SPLIT_MIN_BATCH, or one or two matrices at 64 < N <= 128 with 1 or 2 collapse operators (the
+    Hermitian single-trajectory launch, glf_single_herm_kernel).  From 208 matrices the library runs the persistent
     Hermitian kernel (one workgroup per matrix); below that its pair-block split path
     (one workgroup per upper block pair, 2/3 of the general split path's GEMM work); smaller batches run
     the general kernel's split path, which spreads each matrix over many workgroups (qd_lindblad_rk4:
@@ -105,7 +106,9 @@ def lindblad_rk4(H: torch.Tensor, c_ops: torch.Tensor | None, rho: torch.Tensor,
     h_herm = _is_hermitian_cached(H)
     if hermitian is None:
         min_b = HERM_NP64_MIN_BATCH if 32 < N <= 64 else HERM_SPLIT_MIN_BATCH
-        hermitian = (N <= 128 and B >= min_b and h_herm
+        # one or two trajectories at N_p = 128 with 1 or 2 collapse operators: the Hermitian single launch
+        single_h = 64 < N <= 128 and B <= 2 and 1 <= nc <= 2
+        hermitian = (N <= 128 and (B >= min_b or single_h) and h_herm
                      and bool(torch.equal(rho, rho.transpose(-1, -2).conj())))
     elif hermitian and not h_herm:
         raise ValueError("hermitian=True needs a Hermitian H (the X + X^+ form drops the anti-Hermitian part of H)")

@@ -649,6 +649,69 @@ def test_lindblad_single_launch_long_run_matches_split_path():
     assert relerr(out["single"], ref) < TOL
 
 
+@pytest.mark.parametrize("N,nc,B", [(128, 1, 1), (128, 2, 1), (128, 1, 2), (100, 1, 1)])
+def test_lindblad_hermitian_single_launch(N, nc, B):
+    """exactly Hermitian H and rho at N_p = 128 run the Hermitian single launch
+    (glf_single_herm_kernel: Y workgroups for every tile, k workgroups for the 36 upper tiles only, no stage-input row
+    ingest): final state, observables after every step and snapshots against the oracle's RK4 (oqs.py:697-714,
+    1596-1696) and the general single launch; every snapshot and the final state exactly Hermitian; the auto dispatch
+    picks it (qd_take_path)."""
+    import torch
+    from oracle import lindblad as olb
+    from pyqed_amd import lindblad_rk4
+    from conftest import took
+    H, cs = olb.synthetic_lindblad(N, nc=nc)
+    rho0 = olb.random_pure_states(B, N, seed=3)
+    E = np.array([np.diag(np.arange(N, dtype=float)).astype(complex), H])
+    steps, dt = 9, 1e-2
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    out = {}
+    for herm in (None, False):
+        rho = t(rho0.copy())
+        took("")
+        obs, snap = lindblad_rk4(t(H), t(np.array(cs)), rho, dt, steps, t(E), save_every=3, hermitian=herm)
+        torch.cuda.synchronize()
+        got = took("")[1]
+        out[herm] = (rho.cpu().numpy(), obs.cpu().numpy(), snap.cpu().numpy(), got)
+    assert "glf_single_herm" in out[None][3], out[None][3]
+    assert "glf_single_herm" not in out[False][3], out[False][3]
+    r, obs, snap, _ = out[None]
+    ref = olb.lindblad_batch(H, cs, rho0, dt, steps)
+    assert relerr(r, ref) < TOL
+    assert np.array_equal(r, np.conj(np.swapaxes(r, -1, -2)))
+    assert np.array_equal(snap, np.conj(np.swapaxes(snap, -1, -2)))
+    assert relerr(snap[:, -1], r) == 0.0
+    for a, b in zip(out[None][:3], out[False][:3]):
+        assert relerr(a, b) < 1e-12
+    obs_ref = np.einsum("bij,mji->bm", rho0, E)
+    assert relerr(obs[:, 0], obs_ref) < 1e-13
+
+
+def test_lindblad_hermitian_single_launch_timeout_falls_back():
+    """A hand-off timeout of the Hermitian single launch (QD_OPT_FAKE_TIMEOUT) is repaired on the device by the guarded
+    restore and the guarded persistent Hermitian kernel: the result equals that kernel's own run bit for bit."""
+    import torch
+    from oracle import lindblad as olb
+    from pyqed_amd import lindblad_rk4
+    from conftest import qd_option, took
+    N, steps, dt = 128, 4, 1e-2
+    H, cs = olb.synthetic_lindblad(N, nc=1)
+    rho0 = olb.random_pure_states(1, N, seed=8)
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    runs = {}
+    for name, opt in (("persistent", ("glf_path", "persistent")), ("timeout", ("fake_timeout", 1))):
+        r = t(rho0.copy())
+        took("")
+        with qd_option(*opt):
+            lindblad_rk4(t(H), t(np.array(cs)), r, dt, steps, hermitian=True)
+        torch.cuda.synchronize()
+        runs[name] = (r.cpu().numpy(), took("")[1])
+    assert "glf_single_guarded" in runs["timeout"][1] and "glf_single_herm" in runs["timeout"][1], runs["timeout"][1]
+    assert np.array_equal(runs["timeout"][0], runs["persistent"][0])
+
+
 def test_lindblad_single_launch_timeout_falls_back():
     """A hand-off timeout of the single-trajectory launch (forced after a real run by the QD_OPT_FAKE_TIMEOUT test
     option) is handled on the device: the guarded restore of the saved initial state and the
