@@ -86,6 +86,8 @@ class DeomOperator:
         self.nmod = self.Q.shape[0]
         self.n = self.nmax * ns * ns
         self.norm = inf_norm_bound(minus, plus, coef, damp, H, Q, mode)
+        self.launches = 0        # qd_deom_apply calls and the vectors they applied P to (roofline bookkeeping)
+        self.vec_applies = 0
 
     def apply(self, x, y, alpha=1.0):
         """y <- alpha P x; x, y contiguous [B, n] (or [n]) complex128 on the device, not aliased."""
@@ -97,6 +99,8 @@ class DeomOperator:
                                            self.nmod, self.H.data_ptr(), self.Q.data_ptr(), float(alpha), 0,
                                            _lib.stream_ptr(self.dev))
         _lib.check(rc, "qd_deom_apply")
+        self.launches += 1
+        self.vec_applies += B
         return y
 
 
@@ -285,5 +289,6 @@ def corr4_krylov(op, opT, A1, A2, A3, A4, rho0, T, w_x, w_y, nmax, ns, tol=1e-12
         Lm, s = expv_taylor(opT, act_block(A2.T, L, nmax, n2), T)
         C = Lm @ act_block(A3, R, nmax, n2).transpose(0, 1)
     info = {"method": "krylov", "krylov_dim_right": kr, "krylov_dim_left": kl, "taylor_substeps": s,
-            "norm_bound": op.norm}
+            "norm_bound": op.norm, "stencil_launches": op.launches + opT.launches,
+            "stencil_vector_applications": op.vec_applies + opT.vec_applies}
     return C.cpu().numpy(), info
