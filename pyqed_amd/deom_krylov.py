@@ -289,6 +289,8 @@ def corr4_krylov(op, opT, A1, A2, A3, A4, rho0, T, w_x, w_y, nmax, ns, tol=1e-12
         Lm, s = expv_taylor(opT, act_block(A2.T, L, nmax, n2), T)
         C = Lm @ act_block(A3, R, nmax, n2).transpose(0, 1)
     info = {"method": "krylov", "krylov_dim_right": kr, "krylov_dim_left": kl, "taylor_substeps": s,
-            "norm_bound": op.norm, "stencil_launches": op.launches + opT.launches,
-            "stencil_vector_applications": op.vec_applies + opT.vec_applies}
+            "norm_bound": op.norm}
+    if hasattr(op, "launches"):   # DeomOperator's bookkeeping (the bench's roofline)
+        info["stencil_launches"] = op.launches + opT.launches
+        info["stencil_vector_applications"] = op.vec_applies + opT.vec_applies
     return C.cpu().numpy(), info
