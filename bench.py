@@ -1204,7 +1204,8 @@ def compact_line(out, detail):
             sh = tw["shard_1of8"]
             t["shard_1of8"] = {"members": sh["members"], "ms_per_grid": sh["ms_per_grid"],
                                "frac": sh["roofline"]["frac"],
-                               "projected_8gpu_speedup_compute_only": sh["projected_8gpu_speedup_compute_only"]}
+                               "projected_8gpu_speedup_compute_only": sh["projected_8gpu_speedup_compute_only"],
+                               "projected_8gpu_speedup_reduce_serial": sh.get("projected_8gpu_speedup_reduce_serial")}
         if isinstance(tw.get("t2scan"), dict):
             ts = tw["t2scan"]
             t["t2scan"] = {"value": ts["value"], "n_t2": ts["config"]["n_t2"], "ms_per_scan": ts["ms_per_scan"],
@@ -1403,10 +1404,18 @@ def main():
             # the 8-GPU expectation from one GPU: an 8-way member shard timed alone (its reduce is pipelined
             # behind the next grid's compute at N > 1, so the shard's compute bounds the per-grid time)
             shard, _, _ = bench_2des(dev, 1, 0, args.ens // 8, args.ens_reps)
+            # reduce model: the 1 MiB grid over ONE 153 GB/s xGMI link; pipelined behind the next
+            # grid's compute it is hidden (the compute-only figure), serialised it adds to every grid
+            red_ms = 256 * 256 * 16 / XGMI_LINK_GBS / 1e6
             twodes["shard_1of8"] = {
                 "members": args.ens // 8, "ms_per_grid": shard["ms_per_grid"],
                 "event_ms_per_grid": shard["event_ms_per_grid"], "roofline": shard["roofline"],
-                "projected_8gpu_speedup_compute_only": round(twodes["ms_per_grid"] / shard["ms_per_grid"], 3)}
+                "projected_8gpu_speedup_compute_only": round(twodes["ms_per_grid"] / shard["ms_per_grid"], 3),
+                "projected_8gpu_speedup_reduce_serial": round(twodes["ms_per_grid"] / (shard["ms_per_grid"] + red_ms),
+                                                              3),
+                "reduce_model_ms": round(red_ms, 4),
+                "reduce_model": "1 MiB reduce(sum) to rank 0 over one 153 GB/s xGMI link per grid: hidden when "
+                                "pipelined behind the next grid (compute_only), added when serialised (reduce_serial)"}
             # (round 3 also printed a "serial reduce" projection from a 1 MiB reduce on a ONE-rank communicator: that
             # moves no bytes over xGMI, so it priced nothing and is gone; the driver's 8-GPU run measures the reduce)
             if not args.no_reduce:
