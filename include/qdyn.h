@@ -250,14 +250,14 @@ int qd_spo2_run_ex(qd_c128* psi, const qd_c128* expVh, const qd_c128* expV,
  * SPO2.build / SPO3.build, pyqed/wpd.py:585-623 and :1290-1330): for every grid point
  *   expV  = U e^{-i w dt} U^+,  expVh = U e^{-i w dt/2} U^+,  (w, U) = eigh(V_point)
  * with LAPACK's conventions (lower triangle, real diagonal).  v is [npts][ns][ns] float64
- * (v_complex = 0) or complex128 (v_complex = 1); ns in [1, 256] (ns <= 2 closed form,
+ * (v_complex = 0) or complex128 (v_complex = 1); ns in [1, 1024] (ns <= 2 closed form,
  * ns > 2 the scaling-and-squaring exponential of qd_spo_expm); expV may be null.
  */
 int qd_spo_expv(const void* v, int v_complex, long npts, int ns, double dt,
                 qd_c128* expV, qd_c128* expVh, void* stream);
 
 /*
- * exp(-i V dt/2) and exp(-i V dt) per grid point for any ns in [1, 256], V complex
+ * exp(-i V dt/2) and exp(-i V dt) per grid point for any ns in [1, 1024], V complex
  * [npts][ns][ns]: hermitian = 1 reads the Hermitian matrix eigh sees (SPO2 / SPO3
  * build, wpd.py:585-623, 1290-1330), hermitian = 0 the full matrix (SPO2NH.build,
  * wpd.py:960-985, eig -> U_R e^{-iw dt} U_R^-1).  Scaling and squaring of a degree-18

@@ -1529,7 +1529,7 @@ extern "C" int qd_spo3_run(qd_c128* psi_, const qd_c128* expVh_, const qd_c128* 
 extern "C" int qd_spo_expv(const void* v, int v_complex, long npts, int ns, double dt, qd_c128* expV_,
                            qd_c128* expVh_, void* stream) {
   QD_CHECK_ARG(v && expVh_, "qd_spo_expv: null pointer");
-  QD_CHECK_ARG(ns >= 1 && ns <= 256, "qd_spo_expv: ns=%d outside [1, 256]", ns);
+  QD_CHECK_ARG(ns >= 1 && ns <= 1024, "qd_spo_expv: ns=%d outside [1, 1024]", ns);
   QD_CHECK_ARG(npts >= 0, "qd_spo_expv: npts=%ld", npts);
   if (npts == 0) return QD_OK;
   if (ns > 2)   // scaling-and-squaring Taylor exponential of the Hermitian matrix eigh reads (spo_gen.hip)
@@ -1548,7 +1548,7 @@ extern "C" int qd_spo_expv(const void* v, int v_complex, long npts, int ns, doub
 extern "C" int qd_spo_expm(const qd_c128* v, int hermitian, long npts, int ns, double dt, qd_c128* expV_,
                            qd_c128* expVh_, void* stream) {
   QD_CHECK_ARG(v && expVh_, "qd_spo_expm: null pointer");
-  QD_CHECK_ARG(ns >= 1 && ns <= 256, "qd_spo_expm: ns=%d outside [1, 256]", ns);
+  QD_CHECK_ARG(ns >= 1 && ns <= 1024, "qd_spo_expm: ns=%d outside [1, 1024]", ns);
   QD_CHECK_ARG(npts >= 0, "qd_spo_expm: npts=%ld", npts);
   if (npts == 0) return QD_OK;
   return spo_expm_run(v, 1, hermitian ? 1 : 0, npts, ns, dt, (c128*)expV_, (c128*)expVh_, (hipStream_t)stream);

@@ -577,7 +577,7 @@ __global__ __launch_bounds__(256) void spo1d_gen_kernel(Fft p, c128* psi, const 
 // < 1e-22), so no eigenvectors are needed on the device.  exp(-i V dt) = exp(-i V dt/2)^2 (one more product).
 // herm: the Hermitian matrix LAPACK's eigh sees (lower triangle, real diagonal); otherwise the full matrix.
 // One workgroup per grid point (grid-stride), lane e = i ns + j owns element (i, j).  GLB = false: the four ns x ns
-// matrices live in LDS (ns <= 50: 160 KB at ns = 50); GLB = true (50 < ns <= 256): in a per-workgroup slice of a
+// matrices live in LDS (ns <= 50: 160 KB at ns = 50); GLB = true (50 < ns <= 1024): in a per-workgroup slice of a
 // global scratch buffer (64 ns^2 bytes, L2-resident up to ns ~ 90), with the same code -- the workgroup barrier
 // orders its global stores and loads as it does LDS ones.
 template <bool CPLX, bool GLB>

@@ -15,7 +15,7 @@ from . import _lib
 from ._util import default_device
 from .mol import Result
 
-DEVICE_EXPM_MAX_NS = 256   # qd_spo_expv / qd_spo_expm: work matrices in LDS to ns = 50, in device scratch above
+DEVICE_EXPM_MAX_NS = 1024   # qd_spo_expv / qd_spo_expm: work matrices in LDS to ns = 50, in device scratch above
 
 pi = np.pi
 
@@ -138,9 +138,9 @@ class _PointPropagators:
     The reference's build (wpd.py:585-623, SPO3 :1290-1330) loops over grid points calling eigh and
     forming U e^{-i w tau} U^+.  qd_spo_expv evaluates the same point propagators on the GPU (LAPACK
     conventions: lower triangle, real diagonal): in closed form for ns <= 2, as a scaling-and-squaring
-    matrix exponential for 2 < ns <= 256; they stay on the device for the run and are copied to the
+    matrix exponential for 2 < ns <= 1024; they stay on the device for the run and are copied to the
     host only when exp_V / exp_V_half are read.  The eigen data (d2a = U, apes = w) are host eigh
-    results computed on first access.  ns > 256 builds on the host with a vectorised eigh.
+    results computed on first access.  ns > 1024 builds on the host with a vectorised eigh.
     """
     _eV_dev = _eVh_dev = None
     _exp_V_host = _exp_V_half_host = None
@@ -409,7 +409,7 @@ class SPO2NH(SPO2):
 
     def build(self, dt):
         """wpd.py:960-985.  exp_V = U_R e^{-i w dt} U_R^-1 is the matrix exponential exp(-i V dt); it is evaluated on
-        the GPU (qd_spo_expm, scaling and squaring, no eigenvectors) for ns <= 256.  The right eigenvectors and their
+        the GPU (qd_spo_expm, scaling and squaring, no eigenvectors) for ns <= 1024.  The right eigenvectors and their
         overlap (right_eigenstates, ovlp_rr; nonherm.eig order, eigenvalues by argsort) are host eig results made
         on first access (position() reads ovlp_rr)."""
         nx, ny = self.nx, self.ny
