@@ -1451,7 +1451,7 @@ extern "C" int qd_gather_rows(const qd_c128* src, int nsrc, const int32_t* idx, 
   if (check) {
     int rc = workspace(WS_MISC, sizeof(int), &w, (hipStream_t)stream);
     if (rc) return rc;
-    QD_HIP(hipMemsetAsync(w, 0, sizeof(int), (hipStream_t)stream));
+    QD_TRY(fill_bytes(w, 0, sizeof(int), (hipStream_t)stream));
   }
   const size_t tot = (size_t)n * row_elems;
   hipLaunchKernelGGL(gather_rows_kernel, dim3((int)std::min<size_t>((tot + 255) / 256, 8192)), dim3(256), 0,
@@ -2012,8 +2012,8 @@ extern "C" int qd_deom_rk4_banded(qd_c128* ados, int nmax, int K, int ns, const 
   int* gtab = guard ? (int*)(saved + (Hdip || Qdip ? 2 : 1) * tot) : nullptr;
   int* stat_ws = (int*)(buf + 2 * tot + snap_elems + nf + nc + fb_elems);
   int* stat = status ? (int*)status : stat_ws;
-  if (fsv) QD_HIP(hipMemcpyAsync(fsv, fsys, nf * sizeof(c128), hipMemcpyHostToDevice, st));
-  if (fcv) QD_HIP(hipMemcpyAsync(fcv, fcoup, nc * sizeof(c128), hipMemcpyHostToDevice, st));
+  if (fsv) QD_TRY(upload(fsv, fsys, nf * sizeof(c128), st));
+  if (fcv) QD_TRY(upload(fcv, fcoup, nc * sizeof(c128), st));
   // both hand-off buffers preset to parity 1 in every double (stages 0 and 1, their first writers, carry parity 0),
   // the status words zeroed, snapshot row 0 written: one kernel
   {
@@ -2078,7 +2078,7 @@ extern "C" int qd_deom_rk4_banded(qd_c128* ados, int nmax, int K, int ns, const 
     }
     QD_HIP(le);
     if (option(QD_OPT_FAKE_TIMEOUT))   // tests: report a hand-off timeout after the run
-      QD_HIP(hipMemsetAsync(stat, 1, 1, st));
+      QD_TRY(fill_bytes(stat, 1, 1, st));
 #ifdef QD_PHASE_TIMING
     {   // per-phase wall-clock (100 MHz ticks) summed over the stages: mean and max over bands, per stage, in us
       std::vector<unsigned long long> h((size_t)nbands * 4);

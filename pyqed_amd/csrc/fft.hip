@@ -180,7 +180,7 @@ extern "C" int qd_fft_axis(qd_c128* data, int outer, int n, int inner, int inver
   int rc = workspace(WS_MISC, (size_t)tot * sizeof(c128), &w, st);
   if (rc) return rc;
   c128* X = (c128*)w;
-  QD_HIP(hipMemcpyAsync(X, data, (size_t)tot * sizeof(c128), hipMemcpyDeviceToDevice, st));
+  QD_TRY(copy_device(X, data, (size_t)tot * sizeof(c128), st));
   int l2 = 0;
   if ((rc = fft_lines(X, outer, n, inner, inverse != 0, st, &l2))) return rc;
   const int grid = (int)std::max<long>(1, std::min<long>((tot + 255) / 256, 16384));

@@ -633,7 +633,7 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
                        P0, Q0);
     QD_HIP(hipGetLastError());
     if (nsteps > 0)
-      QD_HIP(hipMemcpyAsync(fdev, fvals, (size_t)nd * nsteps * sizeof(c128), hipMemcpyHostToDevice, st));
+      if ((rc = upload(fdev, fvals, (size_t)nd * nsteps * sizeof(c128), st))) return rc;
   }
   if (pad) {
     const size_t tot = (size_t)B * NN;
@@ -655,7 +655,7 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
     const bool fits = !nd && (herm ? hsingle : B <= glf_single_max_batch(Np, nc));
     if (fits && (force == QD_GLF_AUTO || force == QD_GLF_SINGLE)) {
       if ((rc = workspace(WS_MISC, (size_t)B * NN * sizeof(c128), &wsave, st))) return rc;
-      QD_HIP(hipMemcpyAsync(wsave, rho_p, (size_t)B * NN * sizeof(c128), hipMemcpyDeviceToDevice, st));
+      if ((rc = copy_device(wsave, rho_p, (size_t)B * NN * sizeof(c128), st))) return rc;
       rc = glf_single_run(mK, iKd, Cop, Cd, nc, eT, ne, rho_p, B, N, Np, dt, nsteps, obs,
                           save_every > 0 ? snap : nullptr, save_every, &single_guard, st, hsingle ? 1 : 0);
       if (rc == QD_OK && !single_guard) {   // nothing to run
@@ -706,7 +706,7 @@ int glf_run(GlfSource src, const c128* H, const c128* C, const c128* P, const c1
   p.yslab = split_bt ? p.kslab + (size_t)B * kslots * NN : nullptr;
   p.ticket = split_bt ? (unsigned*)(scratch + (size_t)B * per + (pad ? (size_t)B * NN : 0)) : nullptr;
   p.guard = single_guard;
-  if (split_bt && (ks > 1 || ys > 1 || hk2)) QD_HIP(hipMemsetAsync(p.ticket, 0, nticket * sizeof(unsigned), st));
+  if (split_bt && (ks > 1 || ys > 1 || hk2) && (rc = fill_bytes(p.ticket, 0, nticket * sizeof(unsigned), st))) return rc;
 #ifdef QD_PHASE_TIMING
   const bool timing = true;  // diagnostics build: per-phase clocks to stderr
 #else

@@ -659,9 +659,11 @@ hipError_t sgh_launch2(SingleParams p, int grid, bool coop, hipStream_t st) {
 template <int NC>
 hipError_t sgh_launch(SingleParams p, int B, bool coop, hipStream_t st, int& grid) {
   grid = B * (36 + 64);
-  const bool m3 = grid <= 128 && NC < 2;
+  const bool m3 = grid <= 128 && NC < 2;   // (NC = 2 with 3 products spills)
   note_path(m3 ? "glf_single_herm_3m" : "glf_single_herm_4m");
-  return m3 ? sgh_launch2<NC, true>(p, grid, coop, st) : sgh_launch2<NC, false>(p, grid, coop, st);
+  if constexpr (NC < 2)
+    if (m3) return sgh_launch2<NC, true>(p, grid, coop, st);
+  return sgh_launch2<NC, false>(p, grid, coop, st);
 }
 
 // obs[b][gs][m] = sum over the T^2 tiles of obs_part, fixed order
@@ -752,15 +754,15 @@ int glf_single_run(const c128* P, const c128* Q, const c128* Lop, const c128* Ro
   p.B = B;
   // every handed-off buffer preset to the parity its first epoch does not have: r_1 (buffer 1) and r_2 (buffer 0)
   // carry parities 0 and 1, Y_0 and Y_1 (buffers 0 and 1) both 0; bytes of 0x01 make every double's lowest bit 1
-  QD_HIP(hipMemsetAsync(p.status, 0, flag_bytes, st));
-  QD_HIP(hipMemsetAsync(p.rbuf, 0, (size_t)B * NN * sizeof(c128), st));
-  QD_HIP(hipMemsetAsync(p.rbuf + (size_t)B * NN, 1, (size_t)B * NN * sizeof(c128), st));
-  if (nc > 0) QD_HIP(hipMemsetAsync(p.ybuf, 1, 2 * (size_t)(nc + 1) * B * NN * sizeof(c128), st));
+  QD_TRY(fill_bytes(p.status, 0, flag_bytes, st));
+  QD_TRY(fill_bytes(p.rbuf, 0, (size_t)B * NN * sizeof(c128), st));
+  QD_TRY(fill_bytes(p.rbuf + (size_t)B * NN, 1, (size_t)B * NN * sizeof(c128), st));
+  if (nc > 0) QD_TRY(fill_bytes(p.ybuf, 1, 2 * (size_t)(nc + 1) * B * NN * sizeof(c128), st));
   p.tim = nullptr;
 #ifdef QD_PHASE_TIMING
   void* tw = nullptr;
   if ((rc = workspace(WS_MISC, (size_t)2 * B * T2 * 8 * sizeof(unsigned long long), &tw, st))) return rc;
-  QD_HIP(hipMemsetAsync(tw, 0, (size_t)2 * B * T2 * 8 * sizeof(unsigned long long), st));
+  QD_TRY(fill_bytes(tw, 0, (size_t)2 * B * T2 * 8 * sizeof(unsigned long long), st));
   p.tim = (unsigned long long*)tw;
 #endif
   const bool coop = option(QD_OPT_COOP_LAUNCH) != 0;
@@ -775,7 +777,7 @@ int glf_single_run(const c128* P, const c128* Q, const c128* Lop, const c128* Ro
       return QD_EBUSY;
     }
     QD_HIP(e);
-    if (option(QD_OPT_FAKE_TIMEOUT)) QD_HIP(hipMemsetAsync(p.status, 1, 1, st));
+    if (option(QD_OPT_FAKE_TIMEOUT)) QD_TRY(fill_bytes(p.status, 1, 1, st));
     *status_out = p.status;
 #ifdef QD_PHASE_TIMING
     {   // per-phase wall clock (100 MHz ticks, thread 0), mean over each role's workgroups, per stage, in us
@@ -829,7 +831,7 @@ int glf_single_run(const c128* P, const c128* Q, const c128* Lop, const c128* Ro
   }
   QD_HIP(e);
   if (option(QD_OPT_FAKE_TIMEOUT))   // tests: report a hand-off timeout after the run
-    QD_HIP(hipMemsetAsync(p.status, 1, 1, st));
+    QD_TRY(fill_bytes(p.status, 1, 1, st));
   *status_out = p.status;
 #ifdef QD_PHASE_TIMING
   {   // per-phase wall clock (100 MHz ticks, workgroup thread 0), mean over workgroups, per stage, in us

@@ -29,6 +29,11 @@ void set_error(const char* fmt, ...);
     }                                                   \
   } while (0)
 
+#define QD_TRY(call)        \
+  do {                      \
+    const int rc_ = (call); \
+    if (rc_) return rc_;    \
+  } while (0)
 #define QD_HIP(call)                                                        \
   do {                                                                      \
     hipError_t _e = (call);                                                 \
@@ -66,6 +71,16 @@ void free_workspaces();
 int option(int opt);
 // Records a dispatch decision of the current call for qd_take_path (tests assert which kernel a shape reaches).
 void note_path(const char* name);
+// true while `st` is being captured into a HIP graph
+bool stream_capturing(hipStream_t st);
+// Stream-ordered fills and copies of device memory done by kernels, not by hipMemsetAsync / hipMemcpyAsync: inside a
+// graph capture those become memset / memcpy nodes, whose replays did not order reliably against the kernels around
+// them on this ROCm (profiles/r06/graph/replay_diag.txt).  fill_bytes sets n bytes to `v`.
+int fill_bytes(void* dst, unsigned char v, size_t n, hipStream_t st);
+int copy_device(void* dst, const void* src, size_t n, hipStream_t st);
+// Host array -> device scratch, stream-ordered.  Outside a capture a hipMemcpyAsync; inside one the bytes are copied
+// at capture time (the replays reuse the values the host array held then, and never read the host pointer again).
+int upload(void* dst, const void* src, size_t n, hipStream_t st);
 
 // ---------------------------------------------------------------- complex
 struct alignas(16) c128 {

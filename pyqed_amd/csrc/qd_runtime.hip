@@ -39,11 +39,74 @@ struct Slab {
   bool recorded;     // `done` has been recorded at least once
 };
 struct LiveRef {
-  Slab* slab;        // null: a stream-ordered allocation made while `st` was being captured into a graph
+  Slab* slab;
   hipStream_t st;
-  void* cap;         // that allocation (freed stream-ordered at the scope's end)
 };
 static std::mutex g_mu;              // guards g_slabs and every Slab's busy / recorded fields
+// Scratch of calls captured into a HIP graph: a plain hipMalloc buffer owned by the GRAPH (a user object retained by
+// the graph being captured), since every replay reuses it; the graph's destruction queues it here and the next
+// uncaptured workspace() call (or qd_shutdown) frees it.  Stream-ordered graph allocations (hipMallocAsync alloc /
+// free nodes) gave non-reproducible replays on this ROCm (profiles/r06/graph/replay_diag.txt).
+static std::mutex g_cap_mu;
+static std::vector<std::pair<void*, int>> g_cap_dead;
+static void cap_release(void* ud) {
+  auto* b = static_cast<std::pair<void*, int>*>(ud);
+  std::lock_guard<std::mutex> lk(g_cap_mu);
+  g_cap_dead.push_back(*b);
+  delete b;
+}
+static void free_dead_capture_buffers() {
+  std::vector<std::pair<void*, int>> dead;
+  {
+    std::lock_guard<std::mutex> lk(g_cap_mu);
+    dead.swap(g_cap_dead);
+  }
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  for (auto& d : dead) {
+    if (d.second != cur) (void)hipSetDevice(d.second);
+    (void)hipFree(d.first);
+    if (d.second != cur) (void)hipSetDevice(cur);
+  }
+}
+// hipMalloc while `st` is captured (relaxed capture mode for this thread around the call), owned by the captured graph
+static int capture_alloc(size_t bytes, void** ptr, hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  hipGraph_t graph = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t ndeps = 0;
+  hipError_t e = hipStreamGetCaptureInfo_v2(st, &cs, &id, &graph, &deps, &ndeps);
+  if (e != hipSuccess || cs != hipStreamCaptureStatusActive || !graph) {
+    set_error("workspace inside a graph capture: cannot query the graph being captured (%s)", hipGetErrorString(e));
+    return QD_EHIP;
+  }
+  int dev = 0;
+  QD_HIP(hipGetDevice(&dev));
+  void* p = nullptr;
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  e = hipMalloc(&p, bytes);
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  if (e != hipSuccess) {
+    set_error("workspace allocation of %zu bytes inside a graph capture failed: %s", bytes, hipGetErrorString(e));
+    return QD_ENOMEM;
+  }
+  auto* ud = new std::pair<void*, int>(p, dev);
+  hipUserObject_t obj = nullptr;
+  e = hipUserObjectCreate(&obj, ud, cap_release, 1, hipUserObjectNoDestructorSync);
+  if (e == hipSuccess) e = hipGraphRetainUserObject(graph, obj, 1, hipGraphUserObjectMove);
+  if (e != hipSuccess) {
+    if (!obj) {
+      delete ud;
+      (void)hipFree(p);
+    }
+    set_error("workspace inside a graph capture: cannot attach the buffer to the graph (%s)", hipGetErrorString(e));
+    return QD_EHIP;
+  }
+  *ptr = p;
+  return QD_OK;
+}
 static std::vector<Slab*> g_slabs;
 static thread_local std::vector<LiveRef> g_live;
 static thread_local int g_depth = 0;
@@ -93,10 +156,6 @@ WsScope::~WsScope() {
   std::lock_guard<std::mutex> lk(g_mu);
   for (size_t k = g_live.size(); k > mark; --k) {
     Slab* s = g_live[k - 1].slab;
-    if (!s) {   // graph capture: the free becomes the graph's free node, ordered after the call's kernels
-      (void)hipFreeAsync(g_live[k - 1].cap, g_live[k - 1].st);
-      continue;
-    }
     // every kernel of this call that touches the slab is queued on st by now
     if (hipEventRecord(s->done, g_live[k - 1].st) == hipSuccess) {
       s->recorded = true;
@@ -120,20 +179,9 @@ int workspace(WsSlot slot, size_t bytes, void** ptr, hipStream_t st) {
   QD_HIP(hipGetDevice(&dev));
   const size_t want = slab_size(bytes ? bytes : 16);
   // A stream being captured into a HIP graph cannot wait on an event recorded outside the capture, and a slab handed
-  // to a graph would be reused behind the graph's back at every replay: captured calls take stream-ordered
-  // allocations instead, which become the graph's own alloc / free nodes.
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cap) == hipSuccess && cap == hipStreamCaptureStatusActive) {
-    void* p = nullptr;
-    hipError_t e = hipMallocAsync(&p, want, st);
-    if (e != hipSuccess) {
-      set_error("workspace allocation of %zu bytes inside a graph capture failed: %s", want, hipGetErrorString(e));
-      return QD_ENOMEM;
-    }
-    g_live.push_back({nullptr, st, p});
-    *ptr = p;
-    return QD_OK;
-  }
+  // to a graph would be reused behind the graph's back at every replay: captured calls take a buffer the graph owns.
+  if (stream_capturing(st)) return capture_alloc(want, ptr, st);
+  free_dead_capture_buffers();
   (void)hipGetLastError();
   std::lock_guard<std::mutex> lk(g_mu);
   Slab* best = nullptr;
@@ -169,12 +217,13 @@ int workspace(WsSlot slot, size_t bytes, void** ptr, hipStream_t st) {
     trim_idle(idle_cap());
   }
   best->busy = true;
-  g_live.push_back({best, st, nullptr});
+  g_live.push_back({best, st});
   *ptr = best->ptr;
   return QD_OK;
 }
 
 void free_workspaces() {
+  free_dead_capture_buffers();
   std::lock_guard<std::mutex> lk(g_mu);
   for (size_t k = g_slabs.size(); k-- > 0;) {
     Slab* s = g_slabs[k];
@@ -213,6 +262,77 @@ static const bool g_opt_init = [] {
 }();
 
 int option(int opt) { return (opt >= 0 && opt < QD_OPT_COUNT) ? g_opt[opt].load(std::memory_order_relaxed) : 0; }
+
+bool stream_capturing(hipStream_t st) {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(st, &cap) == hipSuccess && cap == hipStreamCaptureStatusActive;
+}
+
+// ---------------------------------------------------------------- fills, copies, uploads (qd_common.hpp)
+__global__ void fill_bytes_kernel(unsigned char* __restrict__ d, unsigned char v, size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t head = std::min<size_t>(n, (16 - ((uintptr_t)d & 15)) & 15);
+  for (size_t i = i0; i < head; i += stride) d[i] = v;
+  const unsigned w = 0x01010101u * v;
+  uint4 q;
+  q.x = q.y = q.z = q.w = w;
+  uint4* d16 = (uint4*)(d + head);
+  const size_t n16 = (n - head) / 16;
+  for (size_t i = i0; i < n16; i += stride) d16[i] = q;
+  for (size_t i = head + n16 * 16 + i0; i < n; i += stride) d[i] = v;
+}
+
+__global__ void copy_bytes_kernel(unsigned char* __restrict__ d, const unsigned char* __restrict__ s, size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((((uintptr_t)d | (uintptr_t)s) & 15) == 0) {
+    const size_t n16 = n / 16;
+    for (size_t i = i0; i < n16; i += stride) ((uint4*)d)[i] = ((const uint4*)s)[i];
+    for (size_t i = n16 * 16 + i0; i < n; i += stride) d[i] = s[i];
+  } else {
+    for (size_t i = i0; i < n; i += stride) d[i] = s[i];
+  }
+}
+
+static int byte_grid(size_t n) { return (int)std::max<size_t>(1, std::min<size_t>((n / 16 + 255) / 256, 2048)); }
+
+int fill_bytes(void* dst, unsigned char v, size_t n, hipStream_t st) {
+  if (!n) return QD_OK;
+  hipLaunchKernelGGL(fill_bytes_kernel, dim3(byte_grid(n)), dim3(256), 0, st, (unsigned char*)dst, v, n);
+  QD_HIP(hipGetLastError());
+  return QD_OK;
+}
+
+int copy_device(void* dst, const void* src, size_t n, hipStream_t st) {
+  if (!n) return QD_OK;
+  hipLaunchKernelGGL(copy_bytes_kernel, dim3(byte_grid(n)), dim3(256), 0, st, (unsigned char*)dst,
+                     (const unsigned char*)src, n);
+  QD_HIP(hipGetLastError());
+  return QD_OK;
+}
+
+int upload(void* dst, const void* src, size_t n, hipStream_t st) {
+  if (!n) return QD_OK;
+  if (!stream_capturing(st)) {
+    QD_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st));
+    return QD_OK;
+  }
+  // dst is capture-owned scratch no kernel has touched yet: a blocking copy now, outside the capture
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  hipStream_t side = nullptr;
+  hipError_t e = hipStreamCreateWithFlags(&side, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, side);
+  if (e == hipSuccess) e = hipStreamSynchronize(side);
+  if (side) (void)hipStreamDestroy(side);
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  if (e != hipSuccess) {
+    set_error("host upload of %zu bytes inside a graph capture failed: %s", n, hipGetErrorString(e));
+    return QD_EHIP;
+  }
+  return QD_OK;
+}
 
 static thread_local std::string g_path;
 

@@ -916,14 +916,14 @@ struct Exec {
     else
       hipLaunchKernelGGL(dft_axis_kernel<false>, grid, dim3(256), 0, st, (const c128*)psi, tmp, O, L, I, f[d].tw);
     QD_HIP(hipGetLastError());
-    QD_HIP(hipMemcpyAsync(psi, tmp, (size_t)npts * ns * sizeof(c128), hipMemcpyDeviceToDevice, st));
+    QD_TRY(copy_device(psi, tmp, (size_t)npts * ns * sizeof(c128), st));
     return QD_OK;
   }
 
   int pointop(const c128* U) {
     hipLaunchKernelGGL(pointop_kernel, dim3(grid_for(npts * ns)), dim3(256), 0, st, (const c128*)psi, tmp, U, npts, ns);
     QD_HIP(hipGetLastError());
-    QD_HIP(hipMemcpyAsync(psi, tmp, (size_t)npts * ns * sizeof(c128), hipMemcpyDeviceToDevice, st));
+    QD_TRY(copy_device(psi, tmp, (size_t)npts * ns * sizeof(c128), st));
     return QD_OK;
   }
 
@@ -944,7 +944,7 @@ struct Exec {
     if ((flags & F_INV) && (rc = transform(d, true))) return rc;
     if ((flags & F_PT1) && (rc = pointop(U1))) return rc;
     if (flags & F_SNAP)
-      QD_HIP(hipMemcpyAsync(snap, psi, (size_t)npts * ns * sizeof(c128), hipMemcpyDeviceToDevice, st));
+      QD_TRY(copy_device(snap, psi, (size_t)npts * ns * sizeof(c128), st));
     if ((flags & F_PT2) && (rc = pointop(U2))) return rc;
     if ((flags & F_FWD) && (rc = transform(d, false))) return rc;
     if ((flags & F_KY) && (rc = kmul(Ky))) return rc;
@@ -1286,8 +1286,7 @@ int spo1d_generic_run(c128* psi, const c128* expV, const c128* expVh, const c128
     }
     if (snap)
       for (int b = 0; b < B; ++b)
-        QD_HIP(hipMemcpyAsync(snap + ((size_t)b * nsnap + (blk - 1)) * nx, psi + (size_t)b * nx, nx * sizeof(c128),
-                              hipMemcpyDeviceToDevice, st));
+        QD_TRY(copy_device(snap + ((size_t)b * nsnap + (blk - 1)) * nx, psi + (size_t)b * nx, nx * sizeof(c128), st));
   }
   if ((rc = kstep())) return rc;
   return vmul(expVh);

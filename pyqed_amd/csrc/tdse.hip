@@ -311,7 +311,7 @@ extern "C" int qd_tdse_driven_rk4(const qd_c128* H0, const qd_c128* Hd, int nd, 
   if (rc) return rc;
   c128* Ht = (c128*)w;
   c128* fdev = Ht + NN;
-  if (fl) QD_HIP(hipMemcpyAsync(fdev, fvals, fl * sizeof(c128), hipMemcpyHostToDevice, st));
+  if (fl) QD_TRY(upload(fdev, fvals, fl * sizeof(c128), st));
   const int blocks = (int)std::min<size_t>((NN + 255) / 256, 4096);
   if (nblocks == 0) {  // observables at t0 only
     return tdse_rows_run((const c128*)H0, (c128*)psi, B, N, dt, 0, nout, nullptr, (const c128*)E, ne,

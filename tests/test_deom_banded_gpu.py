@@ -19,9 +19,11 @@ def _bath(npsd, nmod=1):
                 [m for m in range(nmod) for _ in range(npsd + 1)])
 
 
-def _run(sol, rho0, dt, nt, nbands, p1=None, status=True):
+def _run(sol, rho0, dt, nt, nbands, p1=None, status=True, calls=1, graph=False):
     """(rho_sys or trace, final ADOs) of one hierarchy: banded with `nbands` bands, or (None) the stage launches.
-    status=False passes no status word (the asynchronous form with the stream-ordered fallback)."""
+    status=False passes no status word (the asynchronous form with the stream-ordered fallback).  calls > 1 chains
+    that many banded calls on the same ADOs; graph=True captures one banded call (no status word) into a HIP graph on
+    a side stream and replays it `calls` times."""
     import torch
     from pyqed_amd import _lib
     from pyqed_amd.deom import ado_coefficients
@@ -64,14 +66,28 @@ def _run(sol, rho0, dt, nt, nbands, p1=None, status=True):
     else:
         bt = sol.band_tables(dev, nbands)
         assert bt is not None and bt.nbands == min(nbands, nmax)
-        stat = torch.zeros(1, dtype=torch.int32, device=dev) if status else None
-        rc = lib.qd_deom_rk4_banded(ados.data_ptr(), nmax, K, ns, *bt.args(), coef_t.data_ptr(), damp_t.data_ptr(),
-                                    mode_t.data_ptr(), nmod, H.data_ptr(), _lib.ptr(Hd), Q.data_ptr(), _lib.ptr(Qd),
-                                    fsp, fcp, dt, nt, rho_sys.data_ptr(), _lib.ptr(p1_t), 1 if p1 is not None else 0,
-                                    _lib.ptr(trace), _lib.ptr(stat), st)
-        _lib.check(rc, "qd_deom_rk4_banded")
+        stat = torch.zeros(1, dtype=torch.int32, device=dev) if status and not graph else None
+
+        def call(stream):
+            rc = lib.qd_deom_rk4_banded(ados.data_ptr(), nmax, K, ns, *bt.args(), coef_t.data_ptr(),
+                                        damp_t.data_ptr(), mode_t.data_ptr(), nmod, H.data_ptr(), _lib.ptr(Hd),
+                                        Q.data_ptr(), _lib.ptr(Qd), fsp, fcp, dt, nt, rho_sys.data_ptr(),
+                                        _lib.ptr(p1_t), 1 if p1 is not None else 0, _lib.ptr(trace), _lib.ptr(stat),
+                                        stream)
+            _lib.check(rc, "qd_deom_rk4_banded")
+        if graph:
+            side = torch.cuda.Stream(dev)
+            torch.cuda.synchronize(dev)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=side):
+                call(side.cuda_stream)
+            for _ in range(calls):
+                g.replay()
+        else:
+            for _ in range(calls):
+                call(st)
         torch.cuda.synchronize(dev)
-        if status:
+        if stat is not None:
             assert int(stat.item()) == 0
     torch.cuda.synchronize(dev)
     out = trace[:, 0] if p1 is not None else rho_sys
@@ -311,3 +327,16 @@ def test_band_table_cache_keyed_on_ns_and_modes():
     t1 = sol.band_tables(dev, 4)
     assert sol._band_cache[0][-2:] == (2, 1)
     assert sol.band_tables(dev, 4) is t1
+
+
+@pytest.mark.parametrize("pulsed", [False, True])
+def test_banded_call_replays_from_a_graph(pulsed):
+    """One banded call (16 bands, spin-boson L = 5) captured into a HIP graph and replayed three times equals three
+    chained direct calls bit for bit: the call's
+    scratch belongs to the graph (qd_runtime.hip capture_alloc), its fills are kernels, and the driven run's pulse
+    values are uploaded at capture time."""
+    sol = _spin_boson(5, npsd=3, pulses=pulsed)
+    rho0 = np.array([[1, 0], [0, 0]], complex)
+    ref, ref_ados = _run(sol, rho0, 0.01, 12, 16, calls=3)
+    out, ados = _run(sol, rho0, 0.01, 12, 16, calls=3, graph=True)
+    assert np.array_equal(out, ref) and np.array_equal(ados, ref_ados)

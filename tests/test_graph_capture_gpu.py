@@ -1,6 +1,7 @@
-"""Library calls captured into a HIP graph (torch.cuda.graph): scratch comes from stream-ordered allocations that
-become the graph's own alloc / free nodes (qd_runtime.hip workspace), so a captured call neither waits on events
-recorded outside the capture nor shares an arena slab with later uncaptured calls.  Replays equal direct calls."""
+"""Library calls captured into a HIP graph (torch.cuda.graph): a captured call's scratch is a buffer the graph owns
+(qd_runtime.hip capture_alloc: released when the graph is destroyed), so it neither waits on events recorded outside
+the capture nor shares an arena slab with uncaptured calls, and its fills are kernels, not memset nodes.  Replays
+equal direct calls bit for bit, sequence after sequence."""
 import numpy as np
 import pytest
 import torch
@@ -80,3 +81,89 @@ def test_lindblad_batch_replays_from_a_graph():
     lindblad_rk4(Ht, Ct, y, 1e-2, 6, hermitian=True)
     torch.cuda.synchronize()
     assert relerr(y.cpu().numpy(), ref.cpu().numpy()) < 1e-12
+
+
+def _replays(g, x, x0, side, sequences=3, replays=2):
+    """States after `replays` replays of g from x0, once per sequence: alternately on the current (null) stream and
+    on the side stream, with no host sync between the copy and the replays."""
+    outs = []
+    for k in range(sequences):
+        if k % 2:
+            with torch.cuda.stream(side):
+                x.copy_(x0)
+                for _ in range(replays):
+                    g.replay()
+        else:
+            x.copy_(x0)
+            for _ in range(replays):
+                g.replay()
+        torch.cuda.synchronize()
+        outs.append(x.clone())
+    return outs
+
+
+@pytest.mark.parametrize("path,herm", [("single", True), ("single", False), ("split", True), ("split", False),
+                                       ("persistent", True), ("persistent", False)])
+def test_lindblad_call_replays_repeat_bit_for_bit(path, herm):
+    """One N = 128 trajectory captured on each Lindblad path (the single-trajectory hand-off launch, the split path's
+    dependent launches with their arrival tickets, the persistent kernel): every sequence of two replays equals two
+    direct calls bit for bit, sequence after sequence.  Round 6 found later sequences wrong on this ROCm while
+    captured scratch came from stream-ordered graph allocations and the tickets / flags were set by memset nodes;
+    captured scratch is now a buffer the graph owns and every fill is a kernel (qd_runtime.hip)."""
+    from conftest import qd_option
+    from oracle import lindblad as olb
+    from pyqed_amd import _lib, lindblad_rk4
+    dev = torch.device("cuda", 0)
+    N = 128
+    H, cs = olb.synthetic_lindblad(N, nc=1)
+    Ht, Ct = torch.from_numpy(H).to(dev), torch.from_numpy(np.array(cs)).to(dev)
+    r0 = torch.from_numpy(olb.random_pure_states(1, N, seed=12)).to(dev)
+    s = torch.cuda.Stream(dev)
+    with qd_option("glf_path", path):
+        ref = r0.clone()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                lindblad_rk4(Ht, Ct, ref, 1e-3, 6, hermitian=herm, stream=s.cuda_stream)
+        torch.cuda.synchronize()
+        x = r0.clone()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        _lib.take_path()
+        with torch.cuda.graph(g, stream=s):
+            lindblad_rk4(Ht, Ct, x, 1e-3, 6, hermitian=herm, stream=s.cuda_stream)
+        taken = _lib.take_path()
+    assert ("glf_single" in taken) == (path == "single"), taken
+    for k, out in enumerate(_replays(g, x, r0, s)):
+        assert torch.equal(out, ref), (k, float((out - ref).abs().max()))
+
+
+def test_graph_scratch_is_released_with_the_graph():
+    """A captured call's scratch is owned by the graph: destroying the graph hands it back, and the next uncaptured
+    call frees it (device memory returns to its level before the capture)."""
+    import gc
+    from oracle import lindblad as olb
+    from pyqed_amd import lindblad_rk4
+    dev = torch.device("cuda", 0)
+    N, B = 128, 64
+    H, cs = olb.synthetic_lindblad(N, nc=1)
+    Ht, Ct = torch.from_numpy(H).to(dev), torch.from_numpy(np.array(cs)).to(dev)
+    x = torch.from_numpy(olb.random_pure_states(B, N, seed=3)).to(dev)
+    s = torch.cuda.Stream(dev)
+    y = x.clone()
+    lindblad_rk4(Ht, Ct, y, 1e-3, 2, hermitian=False)   # the arena's slab for this shape exists before the baseline
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info(dev)[0]
+    for _ in range(3):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            lindblad_rk4(Ht, Ct, x, 1e-3, 2, hermitian=False, stream=s.cuda_stream)
+        g.replay()
+        torch.cuda.synchronize()
+        held = free0 - torch.cuda.mem_get_info(dev)[0]
+        assert held >= B * N * N * 16   # the graph holds at least one state-sized buffer
+        del g
+        gc.collect()
+        lindblad_rk4(Ht, Ct, y, 1e-3, 2, hermitian=False)   # an uncaptured call frees what destroyed graphs released
+        torch.cuda.synchronize()
+        assert free0 - torch.cuda.mem_get_info(dev)[0] < 64 << 20
