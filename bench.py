@@ -719,7 +719,46 @@ def bench_spo3(dev, steps=200, n=64, dt=0.05):
                      "note": "four passes over an 8 MiB state that stays in the Infinity Cache: dependent-pass "
                              "latency, not bytes, bounds one wavepacket"},
         "norm_ratio": norm, "run_100_steps_wall_s": round(run_wall, 4),
+        "any_grid_60": _spo3_axes_leg(dev, steps, 60, dt, ev / steps),
     }
+
+
+def _spo3_axes_leg(dev, steps, n, dt, us64_s):
+    """SPO3 on a grid that is not a power of two (n^3 x 2, same model): the path SPO3.run takes there, the kinetic
+    step as three per-axis mode products on the MFMAs (qd_spo3_run_axes), HIP events over `steps` Strang steps; the
+    cost per point against the 64^3 power-of-two line."""
+    import torch
+    from pyqed_amd import _lib
+    from pyqed_amd.wpd import SPO3, axis_propagator
+    x = np.linspace(-6, 6, n)
+    X, Y, Z = np.meshgrid(x, x, x, indexing="ij")
+    sol = SPO3(x, x, x, masses=[1.0, 1.0, 1.0], nstates=2)
+    sol.set_DPES([0.5 * ((X + 1) ** 2 + Y ** 2 + Z ** 2), 0.5 * ((X - 1) ** 2 + Y ** 2 + Z ** 2)], [[[0, 1], 0.2 * X]])
+    sol.build(dt)
+    assert sol._use_axes()
+    psi0 = np.zeros((n, n, n, 2), complex)
+    psi0[..., 1] = np.exp(-((X + 1) ** 2 + Y ** 2 + Z ** 2) / 2) / np.pi ** 0.75
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    psi, eVh = t(psi0), t(sol.exp_V_half)
+    m = [t(axis_propagator(k, ma, dt)) for k, ma in zip((sol.kx, sol.ky, sol.kz), sol.masses)]
+    lib = _lib.load()
+    st = _lib.stream_ptr(dev)
+
+    def run(k):
+        _lib.check(lib.qd_spo3_run_axes(psi.data_ptr(), eVh.data_ptr(), *(v.data_ptr() for v in m), n, n, n, 2, k, k,
+                                        None, st), "qd_spo3_run_axes")
+
+    ramp_warmup(lambda: run(5), dev)
+    stream = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    run(steps)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    sec = e0.elapsed_time(e1) / 1e3 / steps
+    return {"grid": [n, n, n], "nstates": 2, "path": "spo3_axes", "us_per_step": round(sec * 1e6, 2),
+            "per_point_vs_64cubed": round(sec / n ** 3 / (us64_s / 64 ** 3), 3),
+            "norm_ratio": float((psi.abs() ** 2).sum().item() / (np.abs(psi0) ** 2).sum())}
 
 
 def cpu_baseline_spo3(n=64, dt=0.05, budget_s=5.0):

@@ -465,6 +465,19 @@ int qd_spo3_run(qd_c128* psi, const qd_c128* expVh, const qd_c128* expK, int nx,
                 void* stream);
 
 /*
+ * qd_spo3_run with a separable kinetic propagator (linear coordinates, wpd.py:1255-1262:
+ * exp_K = e_x (x) e_y (x) e_z): the kinetic step fftn, * exp_K, ifftn of _KEO_linear
+ * (wpd.py:1418-1432) is applied as three per-axis mode products with the circulant axis
+ * propagators M_a = F^-1 diag(e_a) F, given by their first columns m_a = ifft(e_a) [n_a]
+ * (M_a[i][k] = m_a[(i - k) mod n_a]; out[i] = sum_k M_a[i][k] in[k] along axis a), on the
+ * f64 MFMAs.  Same step structure, snapshots and result as qd_spo3_run (to rounding).
+ * n_a in [1, 64], ns in {1, 2}.
+ */
+int qd_spo3_run_axes(qd_c128* psi, const qd_c128* expVh, const qd_c128* mx,
+                     const qd_c128* my, const qd_c128* mz, int nx, int ny, int nz, int ns,
+                     int nsteps, int nout, qd_c128* snap, void* stream);
+
+/*
  * RK4 with a dense Liouville-space generator, d v/dt = L v (B vectors).
  * Replaces the csr GEMV loop of pyqed/oqs.py:436-463 (_redfield + rhs) for any
  * dense superoperator.  L [N2][N2], v [B][N2] in/out (row-major vec(rho)),

@@ -126,6 +126,8 @@ SIGNATURES = {
                         c_void_p, c_void_p]),
     "qd_spo3_run": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
                             c_void_p]),
+    "qd_spo3_run_axes": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                                 c_int, c_void_p, c_void_p]),
     "qd_superop_from_glf": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "qd_superop_lindblad": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "qd_superop_rk4": (c_int, [c_void_p, c_void_p, c_int, c_int, c_double, c_int, c_void_p, c_int, c_void_p,

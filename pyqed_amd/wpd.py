@@ -484,8 +484,36 @@ class SPO2NH(SPO2):
         return r
 
 
+def axis_propagator(k, m, dt):
+    """First column m_a = ifft(e_a) of the circulant kinetic propagator of one axis, M_a = F^-1 diag(e_a) F with
+    e_a = exp(-i k^2/(2m) dt) (M_a[i][j] = m_a[(i - j) mod n]; M_a @ v = ifft(e_a * fft(v))): exp_K of linear
+    coordinates (wpd.py:1255-1262) is the outer product of the axis factors, so fftn, * exp_K, ifftn (wpd.py:1418-1432)
+    is M_x (x) M_y (x) M_z.  Host setup, like exp_K itself."""
+    k = np.asarray(k, dtype=float)
+    return np.ascontiguousarray(np.fft.ifft(np.exp(-1j * k * k / 2. / m * dt)))
+
+
 class SPO3(_PointPropagators):
-    """Drop-in for pyqed.wpd.SPO3 (wpd.py:1105-1432), linear coordinates."""
+    """Drop-in for pyqed.wpd.SPO3 (wpd.py:1105-1432), linear coordinates.
+
+    kinetic_path: "auto" takes the kinetic step as three per-axis mode products on the MFMAs (qd_spo3_run_axes; any
+    length, no FFT plan) when every axis has at most AXES_MAX_N points, one or two states and some axis is not a power
+    of two (64^3 x 2: 26 us per step on the power-of-two FFT passes against 32 on the axis products; 60^3 x 2: 52
+    against 31, profiles/r06/spo/spo3_axes_ab.txt); "axes" / "fft" force one (tests)."""
+
+    AXES_MAX_N = 64
+    kinetic_path = "auto"
+
+    def _use_axes(self):
+        dims = (self.nx, self.ny, self.nz)
+        fits = max(dims) <= self.AXES_MAX_N and self.nstates <= 2
+        if self.kinetic_path == "axes":
+            if not fits:
+                raise ValueError(f"kinetic_path='axes' needs every axis <= {self.AXES_MAX_N} points and nstates <= 2")
+            return True
+        if self.kinetic_path == "fft":
+            return False
+        return fits and not all(n & (n - 1) == 0 for n in dims)
 
     def __init__(self, x, y, z, masses, nstates=2, coords='linear', G=None, abc=False):
         self.x, self.y, self.z = x, y, z
@@ -558,11 +586,20 @@ class SPO3(_PointPropagators):
         shape = (self.nx, self.ny, self.nz, self.nstates)
         snap = torch.empty((nsnap,) + shape, dtype=torch.complex128, device=dev) if nsnap else None
         _, eVh = self._point_ops_dev(dev)
-        eK = _dev_c128(self.exp_K, dev)
-        with torch.cuda.device(dev):
-            rc = _lib.load().qd_spo3_run(psi.data_ptr(), eVh.data_ptr(), eK.data_ptr(), self.nx, self.ny, self.nz,
-                                         self.nstates, int(nsteps), int(nout), _lib.ptr(snap), _lib.stream_ptr(dev))
-        _lib.check(rc, "qd_spo3_run")
+        if self._use_axes():
+            M = [_dev_c128(axis_propagator(k, m, dt), dev) for k, m in zip((self.kx, self.ky, self.kz), self.masses)]
+            with torch.cuda.device(dev):
+                rc = _lib.load().qd_spo3_run_axes(psi.data_ptr(), eVh.data_ptr(), *(m.data_ptr() for m in M),
+                                                  self.nx, self.ny, self.nz, self.nstates, int(nsteps), int(nout),
+                                                  _lib.ptr(snap), _lib.stream_ptr(dev))
+            _lib.check(rc, "qd_spo3_run_axes")
+        else:
+            eK = _dev_c128(self.exp_K, dev)
+            with torch.cuda.device(dev):
+                rc = _lib.load().qd_spo3_run(psi.data_ptr(), eVh.data_ptr(), eK.data_ptr(), self.nx, self.ny,
+                                             self.nz, self.nstates, int(nsteps), int(nout), _lib.ptr(snap),
+                                             _lib.stream_ptr(dev))
+            _lib.check(rc, "qd_spo3_run")
         r = Result(dt=dt, psi0=psi0, Nt=nt, t0=t0, nout=nout)
         if snap is not None:
             host = snap.cpu().numpy()

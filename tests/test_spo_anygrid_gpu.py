@@ -85,13 +85,18 @@ def test_spo2_merged_and_jacobi_any_grid_match_oracle():
     assert relerr(np.array(rj.psilist), np.array(pl)) < TOL
 
 
-def test_spo3_any_grid_matches_reference():
+def test_spo3_any_grid_matches_reference(monkeypatch):
+    """The mixed-radix FFT passes (spo_any); tests/test_spo3_axes_gpu.py runs the same fixture on the axis path."""
     from pyqed_amd import SPO3
+    from conftest import took
     g = load_golden("spo3_24x20x18")
     (x, y, z), masses, surfaces, couplings, psi0 = spo3_model()
     sol = SPO3(x, y, z, masses=masses, nstates=2)
     sol.set_DPES(surfaces, couplings)
+    monkeypatch.setattr(SPO3, "kinetic_path", "fft")
+    took("")
     r = sol.run(psi0=psi0, dt=float(g["dt"]), nt=int(g["nt"]), nout=int(g["nout"]))
+    assert took("spo_any")[0]
     assert relerr(np.array(r.psilist), g["psilist"]) < TOL
     assert relerr(r.psi, g["psi"]) < TOL
 

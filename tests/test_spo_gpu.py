@@ -126,7 +126,7 @@ def test_spo3_matches_reference():
 
 @pytest.mark.parametrize("dims,ns", [((64, 64, 64), 2), ((32, 32, 32), 2), ((128, 64, 64), 1), ((64, 128, 32), 2),
                                      ((16, 32, 64), 2), ((32, 16, 16), 4), ((128, 128, 128), 2)])
-def test_spo3_pow2_grids_vs_oracle(dims, ns):
+def test_spo3_pow2_grids_vs_oracle(dims, ns, monkeypatch):
     """Power-of-two SPO3 grids through the specialised kernels, each shape selecting its own mid-axis / x-axis
     launches (64^3 x 2 is examples/spo.py's size: 64-point register transforms, LDS-staged x pass over the mid pass's
     row width; 32^3: narrower blocks; 128 x 64^2 x 1: one state; ny = 128: the generic mid kernel; ns = 4: the LDS
@@ -142,6 +142,7 @@ def test_spo3_pow2_grids_vs_oracle(dims, ns):
     sol = SPO3(*ax, masses=[1.0, 1.0, 1.0], nstates=ns)
     sol.set_DPES([0.5 * ((X + (-1) ** a) ** 2 + Y ** 2 + Z ** 2) + 0.1 * a for a in range(ns)],
                  [[[a, a + 1], 0.2 * X] for a in range(ns - 1)])
+    monkeypatch.setattr(SPO3, "kinetic_path", "fft")   # the FFT passes (qd_spo3_run)
     took("")
     r = sol.run(psi0=psi0, dt=0.25, nt=4, nout=2)
     hit, got = took("spo3_pow2")
@@ -152,7 +153,7 @@ def test_spo3_pow2_grids_vs_oracle(dims, ns):
 
 
 @pytest.mark.parametrize("nx,nout", [(64, 1), (32, 3)])
-def test_spo3_row64_single_state_and_shapes(nx, nout):
+def test_spo3_row64_single_state_and_shapes(nx, nout, monkeypatch):
     """The 64-point register z pass with one electronic state and nx != 64: vs the NumPy fftn restatement,
     snapshots every nout steps."""
     from oracle import spo as ospo
@@ -164,6 +165,7 @@ def test_spo3_row64_single_state_and_shapes(nx, nout):
     psi0 = (np.exp(-((X + 1) ** 2 + Y ** 2 + Z ** 2) / 2 + 1j * rng.uniform(-1, 1) * Z) / np.pi ** 0.75)[..., None]
     sol = SPO3(x, yz, yz, masses=[1.0, 1.0, 1.0], nstates=1)
     sol.set_DPES([0.5 * (X ** 2 + Y ** 2 + Z ** 2) + 0.05 * X * Y * Z], [])
+    monkeypatch.setattr(SPO3, "kinetic_path", "fft")
     r = sol.run(psi0=psi0, dt=0.1, nt=6, nout=nout)
     ref, _ = ospo.spo3_run(sol.exp_V_half, sol.exp_K, psi0, 6, nout)
     assert relerr(np.array(r.psilist), np.array(ref)) < TOL
