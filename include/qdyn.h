@@ -389,15 +389,28 @@ int qd_deom_stage(qd_c128* rho, const qd_c128* xin, qd_c128* xout, qd_c128* acc,
                   void* stream);
 
 /*
- * y = alpha P x for B ADO vectors, P the DEOM generator that DEOMSolver.run steps and
+ * The shifted Hessenberg solves of the multi-shift Krylov form of
+ * DEOMSolver.correlation_4op_3t (pyqed_amd/deom_krylov.py; the reference diagonalises P
+ * instead, pyqed/heom/deom.py:1127-1209): for each of the S shifts s, (-H_k - s I) y = beta e_1
+ * with H_k the leading k x k block of the upper Hessenberg Arnoldi matrix H (row-major, leading
+ * dimension ldh, k + 1 rows: row k holds h_{k+1,k}).  Y [S][k] (or NULL) receives the
+ * solutions, res [S] (or NULL) the FOM residuals |h_{k+1,k} y_{k-1}| / beta.  Gaussian
+ * elimination with adjacent-row pivoting, one workgroup per shift; k <= 4096.
+ */
+int qd_shifted_hessenberg_solve(const qd_c128* H, int ldh, int k, const qd_c128* shifts, int S,
+                                double beta, qd_c128* Y, double* res, void* stream);
+
+/*
+ * y = x0 + alpha P x (x0 NULL: y = alpha P x) for B ADO vectors, P the DEOM generator that DEOMSolver.run steps and
  * DEOMSolver.correlation_4op_3t diagonalises (generate_dot_element, pyqed/heom/deom.py:641-664;
  * generate_propgator :769-893 as a dense matrix).  x, y: [B][nmax][ns][ns] (element-major) or
- * [nmax][B][ns][ns] (ado_major = 1, needs ns^2 <= 64 and K <= 8); x and y must not alias.
+ * [nmax][B][ns][ns] (ado_major = 1, needs ns^2 <= 64 and K <= 8), x0 in the same layout; y
+ * aliases neither x nor x0.
  * Tables as qd_deom_rk4.  The transposed generator P^T is the same operator on transposed
  * tables (H^T, Q^T, minus <-> plus, prefactors moved to the other end of each link;
  * pyqed_amd/deom_krylov.py), which the Krylov form of correlation_4op_3t applies.
  */
-int qd_deom_apply(const qd_c128* x, qd_c128* y, int B, int nmax, int K, int ns,
+int qd_deom_apply(const qd_c128* x, qd_c128* y, const qd_c128* x0, int B, int nmax, int K, int ns,
                   const int32_t* minus, const int32_t* plus, const qd_c128* coef,
                   const qd_c128* damp, const int32_t* mode, int nmod, const qd_c128* H,
                   const qd_c128* Q, double alpha, int ado_major, void* stream);

@@ -76,7 +76,9 @@ SIGNATURES = {
                                    c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_double, c_int,
                                    c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
-    "qd_deom_apply": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+    "qd_shifted_hessenberg_solve": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_double, c_void_p, c_void_p,
+                                            c_void_p]),
+    "qd_deom_apply": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_double, c_int, c_void_p]),
     "qd_deom_stage": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                               c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_double,

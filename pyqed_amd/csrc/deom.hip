@@ -1377,18 +1377,19 @@ extern "C" int qd_deom_stage(qd_c128* rho, const qd_c128* xin, qd_c128* xout, qd
 // Krylov form of DEOMSolver.correlation_4op_3t applies it and its transpose, pyqed_amd/deom_krylov.py).  One stage
 // launch of the stage kernels: Horner stage 2 (s_3 = rho + dt / 2 L s_2) with rho = 0 (a null rho: nothing is read
 // for it) and dt = 2 alpha, so the coefficient is alpha exactly and the kernel reads its input only from xin.
-extern "C" int qd_deom_apply(const qd_c128* x, qd_c128* y, int B, int nmax, int K, int ns, const int32_t* minus,
+extern "C" int qd_deom_apply(const qd_c128* x, qd_c128* y, const qd_c128* x0, int B, int nmax, int K, int ns,
+                             const int32_t* minus,
                              const int32_t* plus, const qd_c128* coef, const qd_c128* damp, const int32_t* mode,
                              int nmod, const qd_c128* H, const qd_c128* Q, double alpha, int ado_major, void* stream) {
   QD_CHECK_ARG(x && y && minus && plus && coef && damp && mode && H && Q, "qd_deom_apply: null pointer");
-  QD_CHECK_ARG(x != y, "qd_deom_apply: x and y must not alias");
+  QD_CHECK_ARG(x != y && x0 != y, "qd_deom_apply: y must alias neither x nor x0");
   QD_CHECK_ARG(B >= 1 && nmax >= 1 && K >= 1 && ns >= 1 && nmod >= 1, "qd_deom_apply: bad sizes B=%d nmax=%d K=%d ns=%d",
                B, nmax, K, ns);
   hipStream_t st = (hipStream_t)stream;
-  // rho == nullptr: the stage kernels take rho = 0 without a zeroed buffer to read (a full-size memset
-  // and read per application); stage 2 never writes rho_out
+  // the Horner stage-2 form y = rho + (dt / 2) L x with rho = x0 and dt = 2 alpha; rho == nullptr (x0 NULL): the stage
+  // kernels take rho = 0 without a zeroed buffer to read; stage 2 never writes rho_out
   DeomParams p{};
-  p.rho = nullptr;
+  p.rho = (const c128*)x0;
   p.rho_out = nullptr;
   p.xin = (const c128*)x;
   p.xout = (c128*)y;

@@ -89,19 +89,43 @@ class DeomOperator:
         self.launches = 0        # qd_deom_apply calls and the vectors they applied P to (roofline bookkeeping)
         self.vec_applies = 0
 
-    def apply(self, x, y, alpha=1.0):
-        """y <- alpha P x; x, y contiguous [B, n] (or [n]) complex128 on the device, not aliased."""
+    def apply(self, x, y, alpha=1.0, ado_major=False, x0=None):
+        """y <- x0 + alpha P x (x0 None: alpha P x); x, y, x0 contiguous [B, n] (or [n]) complex128 on the device, y
+        aliasing neither; ado_major: all three are [nmax][B][ns][ns] (the batched ADO-major kernels, ns^2 <= 64 and
+        K <= 8)."""
         B = x.numel() // self.n
         mi, pl, coef, damp, mode = self.tabs
         with torch.cuda.device(self.dev):
-            rc = _lib.load().qd_deom_apply(x.data_ptr(), y.data_ptr(), B, self.nmax, self.K, self.ns, mi.data_ptr(),
+            rc = _lib.load().qd_deom_apply(x.data_ptr(), y.data_ptr(), _lib.ptr(x0), B, self.nmax, self.K, self.ns, mi.data_ptr(),
                                            pl.data_ptr(), coef.data_ptr(), damp.data_ptr(), mode.data_ptr(),
-                                           self.nmod, self.H.data_ptr(), self.Q.data_ptr(), float(alpha), 0,
+                                           self.nmod, self.H.data_ptr(), self.Q.data_ptr(), float(alpha),
+                                           1 if ado_major else 0,
                                            _lib.stream_ptr(self.dev))
         _lib.check(rc, "qd_deom_apply")
         self.launches += 1
         self.vec_applies += B
         return y
+
+
+def _hess_solve_dev(Hd, k, beta, shifts, want_y):
+    """qd_shifted_hessenberg_solve on the device Arnoldi matrix Hd [(m + 1), m] (leading k x k block, row k the
+    sub-diagonal entry h_{k+1,k}): (Y [S, k] or None, residuals [S] on the device).  Shifts are chunked so that the
+    pivot-row scratch (S k^2 complex) stays <= 1 GB."""
+    dev = Hd.device
+    sh_all = torch.from_numpy(np.asarray(shifts, dtype=complex)).to(dev)
+    S = len(sh_all)
+    Y = torch.empty((S, k), dtype=torch.complex128, device=dev) if want_y else None
+    res = torch.empty(S, dtype=torch.float64, device=dev)
+    chunk = max(1, (1 << 30) // (16 * k * k)) if want_y else S
+    lib = _lib.load()
+    with torch.cuda.device(dev):
+        for c0 in range(0, S, chunk):
+            c1 = min(S, c0 + chunk)
+            rc = lib.qd_shifted_hessenberg_solve(Hd.data_ptr(), Hd.shape[1], k, sh_all[c0:].data_ptr(), c1 - c0,
+                                                 float(beta), Y[c0:].data_ptr() if want_y else None,
+                                                 res[c0:].data_ptr(), _lib.stream_ptr(dev))
+            _lib.check(rc, "qd_shifted_hessenberg_solve")
+    return Y, res
 
 
 def _shift_solutions_dev(Hk, beta, shifts):
@@ -211,18 +235,32 @@ def shifted_krylov_solve(op, b, shifts, tol=1e-12, m_max=None, first_check=20):
         k = j + 1
         if k != check and k != m_max:
             continue
-        Hh = Hd[:k + 1, :k].cpu().numpy()
-        sub = np.abs(np.diag(Hh, -1))
-        brk = np.nonzero(sub < 1e-14 * max(np.abs(Hh).max(), 1e-300))[0]
+        if dev.type == "cuda":   # device solves (qd_shifted_hessenberg_solve); only scalars come back
+            Hk1 = Hd[:k + 1, :k]
+            sub_d = torch.diagonal(Hk1, -1).abs()
+            small = torch.cat([sub_d, Hk1.abs().max()[None]]).cpu().numpy()
+            sub, hmax = small[:k], small[k]
+        else:
+            Hh = Hd[:k + 1, :k].cpu().numpy()
+            sub, hmax = np.abs(np.diag(Hh, -1)), np.abs(Hh).max()
+        brk = np.nonzero(sub < 1e-14 * max(hmax, 1e-300))[0]
         if len(brk):   # invariant subspace: the Krylov solution is exact
             k_done = int(brk[0]) + 1
             break
-        res = float(_shift_residuals(Hh, k, beta, shifts).max())
+        if dev.type == "cuda":
+            res = float(_hess_solve_dev(Hd, k, beta, shifts, False)[1].max())
+        else:
+            res = float(_shift_residuals(Hh, k, beta, shifts).max())
         hist.append((k, res))
         if res < target:
-            Yd = _shift_solutions_dev(Hd[:k, :k], beta, shifts)
-            Y = Yd.cpu().numpy()
-            if np.all(np.abs(Hh[k, k - 1] * Y[:, -1]) < tol * np.maximum(np.linalg.norm(Y, axis=1), 1e-300)):
+            if dev.type == "cuda":
+                Yd, rd = _hess_solve_dev(Hd, k, beta, shifts, True)
+                ok = bool(torch.all(rd * beta < tol * torch.clamp(torch.linalg.vector_norm(Yd, dim=1), min=1e-300)))
+            else:
+                Yd = _shift_solutions_dev(Hd[:k, :k], beta, shifts)
+                Y = Yd.cpu().numpy()
+                ok = np.all(np.abs(Hh[k, k - 1] * Y[:, -1]) < tol * np.maximum(np.linalg.norm(Y, axis=1), 1e-300))
+            if ok:
                 k_done = k
                 return Yd @ V[:k], k
         step = max(10, k // 4)
@@ -234,29 +272,61 @@ def shifted_krylov_solve(op, b, shifts, tol=1e-12, m_max=None, first_check=20):
         check = min(m_max, k + step)
     if k_done is None:
         raise RuntimeError(f"shifted Krylov solve: no convergence to {tol:g} within {m_max} Arnoldi steps")
+    if dev.type == "cuda":
+        return _hess_solve_dev(Hd, k_done, beta, shifts, True)[0] @ V[:k_done], k_done
     return _shift_solutions_dev(Hd[:k_done, :k_done], beta, shifts) @ V[:k_done], k_done
 
 
-def expv_taylor(op, X, T):
-    """e^{P T} X for X [B, n] on the device: Taylor substeps tau = T / s with ||P tau||_inf <= 1, TAYLOR_DEGREE
-    terms each (every term one batched stencil launch)."""
+def expv_taylor(op, X, T, graph=True):
+    """e^{P T} X for X [B, n] on the device: Taylor substeps tau = T / s with ||P tau||_inf <= 1, each the degree-
+    TAYLOR_DEGREE polynomial in Horner form, y <- x + (tau / j) P y for j = TAYLOR_DEGREE .. 1 (every step one stencil
+    launch with the axpy fused: qd_deom_apply's x0).  B > 1 vectors run ADO-major ([nmax][B][ns][ns], the batched
+    stencil kernels).  graph=True captures one substep (its stencil launches and the closing copy, fixed buffers) into
+    a HIP graph and replays it s times (replays are bit for bit, tests/test_graph_capture_gpu.py)."""
     if T == 0:
         return X.clone(), 0
     s = max(1, int(np.ceil(abs(T) * op.norm)))
     tau = T / s
-    out = X.clone()
-    t1 = torch.empty_like(X)
-    t2 = torch.empty_like(X)
+    B = X.numel() // op.n
+    am = X.is_cuda and B > 1 and op.ns * op.ns <= 64 and getattr(op, "K", 99) <= 8
+    out = X.reshape(B, op.nmax, -1).transpose(0, 1).contiguous() if am else X.clone()
+    t1 = torch.empty_like(out)
+    t2 = torch.empty_like(out)
+    fused = hasattr(op, "K")   # DeomOperator (the CPU stand-ins of the host tests have no x0)
+
+    def substep():
+        src = out
+        for j in range(TAYLOR_DEGREE, 0, -1):
+            dst = t1 if j % 2 == 0 else t2
+            if fused:
+                op.apply(src, dst, tau / j, ado_major=am, x0=out)
+            else:
+                op.apply(src, dst, tau / j)
+                dst.add_(out)
+            src = dst
+        out.copy_(src)
+
+    def result():
+        return out.transpose(0, 1).reshape(X.shape).contiguous() if am else out
+
+    if not graph or s < 2 or not X.is_cuda:   # (CPU stand-in operators in the host tests)
+        for _ in range(s):
+            substep()
+        return result(), s
+    side = torch.cuda.Stream(op.dev)
+    side.wait_stream(torch.cuda.current_stream(op.dev))
+    g = torch.cuda.CUDAGraph()
+    launches, vecs = getattr(op, "launches", 0), getattr(op, "vec_applies", 0)
+    with torch.cuda.graph(g, stream=side):
+        substep()
+    if hasattr(op, "launches"):   # the capture enqueued nothing; count the replays' stencil launches instead
+        op.launches, op.vec_applies = launches, vecs
     for _ in range(s):
-        term = out.clone()
-        acc = out
-        for j in range(1, TAYLOR_DEGREE + 1):
-            dst = t1 if j % 2 else t2
-            op.apply(term, dst, tau / j)
-            acc += dst
-            term = dst
-        out = acc
-    return out, s
+        g.replay()
+        if hasattr(op, "launches"):
+            op.launches += TAYLOR_DEGREE
+            op.vec_applies += TAYLOR_DEGREE * B
+    return result(), s
 
 
 def act_block(blk, X, nmax, n2):

@@ -38,6 +38,51 @@ def test_deom_apply_is_the_generator_and_its_transpose(ns, npsd, L, nmod, B):
     assert relerr(y.cpu().numpy(), -2.0 * (x @ P)) < 1e-13
 
 
+def test_taylor_graph_replay_equals_direct_substeps():
+    """expv_taylor's graph form (one captured substep of 20 stencil launches and adds, replayed s times) equals the
+    direct loop bit for bit and counts the same stencil launches; e^{PT} x against expm of the assembled P."""
+    import scipy.linalg
+    from pyqed_amd.deom import ado_liouvillian
+    from pyqed_amd.deom_krylov import DeomOperator, expv_taylor
+    dev = torch.device("cuda", 0)
+    sol, H, Q, coef, damp, mode = _hierarchy(2, 3, 4, 1)
+    P = ado_liouvillian(sol.keys, sol._minus, sol._plus, coef, damp, H, Q, mode)
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal((3, P.shape[0])) + 1j * rng.standard_normal((3, P.shape[0]))
+    xd = torch.from_numpy(x).to(dev)
+    ops = [DeomOperator(dev, sol._minus, sol._plus, coef, damp, mode, H, Q, 2) for _ in range(2)]
+    T = 3.0 / ops[0].norm * 2.5   # several substeps
+    yd, s1 = expv_taylor(ops[0], xd, T, graph=False)
+    yg, s2 = expv_taylor(ops[1], xd, T, graph=True)
+    torch.cuda.synchronize()
+    assert s1 == s2 >= 2
+    assert torch.equal(yd, yg)
+    assert (ops[0].launches, ops[0].vec_applies) == (ops[1].launches, ops[1].vec_applies)
+    assert relerr(yg.cpu().numpy(), x @ scipy.linalg.expm(P * T).T) < 1e-11
+
+
+@pytest.mark.parametrize("k,S", [(1, 3), (7, 5), (300, 33)])
+def test_shifted_hessenberg_solve_matches_dense_solves(k, S):
+    """qd_shifted_hessenberg_solve (one workgroup per shift, adjacent-row pivoting) against numpy.linalg.solve of every
+    (-H_k - s I) y = beta e_1 and the host residual form (_shift_residuals), on a random Hessenberg matrix with a
+    leading dimension wider than k."""
+    from pyqed_amd.deom_krylov import _hess_solve_dev, _shift_residuals
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(k)
+    m = k + 4
+    H = np.triu(rng.standard_normal((m + 1, m)) + 1j * rng.standard_normal((m + 1, m)), -1)
+    shifts = 1j * rng.uniform(-3, 3, S) + 0.2
+    beta = 1.7
+    Y, res = _hess_solve_dev(torch.from_numpy(H).to(dev), k, beta, shifts, True)
+    Y = Y.cpu().numpy()
+    for i, sft in enumerate(shifts):
+        ref = np.linalg.solve(-H[:k, :k] - sft * np.eye(k), beta * np.eye(k)[:, 0])
+        assert relerr(Y[i], ref) < 1e-10
+    assert relerr(res.cpu().numpy(), _shift_residuals(H, k, beta, shifts)) < 1e-10
+    _, res2 = _hess_solve_dev(torch.from_numpy(H).to(dev), k, beta, shifts, False)
+    assert torch.equal(res, res2)
+
+
 def _fixture_solver(g):
     from pyqed_amd.deom import Bath, DEOMSolver
     bath = Bath.__new__(Bath)
