@@ -389,6 +389,16 @@ int qd_deom_stage(qd_c128* rho, const qd_c128* xin, qd_c128* xout, qd_c128* acc,
                   void* stream);
 
 /*
+ * Arnoldi steps of the same Krylov form (classical Gram-Schmidt, applied twice):
+ * qd_cgs_project: h[r] = sum_i conj(V[r][i]) w[i] for the m basis rows of V (row-major,
+ * leading dimension ldv), fixed-order reductions; hsum (or NULL) accumulates h with stride ldh
+ * (a Hessenberg column).  qd_cgs_normalize: *hsub = ||w||, v = w / max(||w||, 1e-300).
+ */
+int qd_cgs_project(const qd_c128* V, long ldv, int m, int n, const qd_c128* w, qd_c128* h,
+                   qd_c128* hsum, long ldh, void* stream);
+int qd_cgs_normalize(const qd_c128* w, int n, qd_c128* v, qd_c128* hsub, void* stream);
+
+/*
  * The shifted Hessenberg solves of the multi-shift Krylov form of
  * DEOMSolver.correlation_4op_3t (pyqed_amd/deom_krylov.py; the reference diagonalises P
  * instead, pyqed/heom/deom.py:1127-1209): for each of the S shifts s, (-H_k - s I) y = beta e_1

@@ -76,6 +76,9 @@ SIGNATURES = {
                                    c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_double, c_int,
                                    c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "qd_cgs_project": (c_int, [c_void_p, ctypes.c_long, c_int, c_int, c_void_p, c_void_p, c_void_p, ctypes.c_long,
+                               c_void_p]),
+    "qd_cgs_normalize": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "qd_shifted_hessenberg_solve": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_double, c_void_p, c_void_p,
                                             c_void_p]),
     "qd_deom_apply": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,

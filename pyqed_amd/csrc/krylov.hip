@@ -1,5 +1,5 @@
-// krylov.hip — the shifted Hessenberg solves of the multi-shift Krylov form of DEOMSolver.correlation_4op_3t
-// (pyqed_amd/deom_krylov.py; reference heom/deom.py:1127-1209 diagonalises P instead).
+// krylov.hip — the Arnoldi projections and the shifted Hessenberg solves of the multi-shift Krylov form of
+// DEOMSolver.correlation_4op_3t (pyqed_amd/deom_krylov.py; reference heom/deom.py:1127-1209 diagonalises P instead).
 //
 // For every shift s: (-H_k - s I) y = beta e_1 with H_k the k x k upper Hessenberg Arnoldi matrix (leading dimension
 // ldh, row k holding h_{k+1,k}).  One workgroup per shift runs Gaussian elimination with adjacent-row pivoting (the
@@ -87,10 +87,112 @@ __global__ __launch_bounds__(256) void hess_shift_kernel(const c128* __restrict_
   }
 }
 
+// h[r] = sum_i conj(V[r][i]) w[i] for r < m, one workgroup per basis row (contiguous, coalesced), fixed-order
+// reduction (deterministic); hsum (strided by ldh, or null) accumulates the same value (the Hessenberg column).
+__global__ __launch_bounds__(256) void cgs_project_kernel(const c128* __restrict__ V, long ldv, int n,
+                                                          const c128* __restrict__ w, c128* h, c128* hsum, long ldh) {
+  __shared__ double red[2][256];
+  const int r = blockIdx.x, tid = threadIdx.x;
+  const c128* vr = V + (size_t)r * ldv;
+  double sr = 0.0, si = 0.0;
+  constexpr int U = 8;   // loads in flight per thread (the row is one dependent-latency chain otherwise)
+  int i = tid;
+  for (; i + 256 * (U - 1) < n; i += 256 * U) {
+    c128 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      a[u] = vr[i + 256 * u];
+      b[u] = w[i + 256 * u];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      sr += a[u].re * b[u].re + a[u].im * b[u].im;   // conj(a) b
+      si += a[u].re * b[u].im - a[u].im * b[u].re;
+    }
+  }
+  for (; i < n; i += 256) {
+    const c128 a = vr[i], b = w[i];
+    sr += a.re * b.re + a.im * b.im;
+    si += a.re * b.im - a.im * b.re;
+  }
+  red[0][tid] = sr;
+  red[1][tid] = si;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+      red[0][tid] += red[0][tid + o];
+      red[1][tid] += red[1][tid + o];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const c128 v = cmk(red[0][0], red[1][0]);
+    h[r] = v;
+    if (hsum) hsum[(size_t)r * ldh] = cadd(hsum[(size_t)r * ldh], v);
+  }
+}
+
+// ||w||^2 in two fixed-order stages: per-workgroup partial sums, then one workgroup sums them, writes *hsub = nrm and
+// (with the other workgroups of the scale launch) v = w / max(nrm, 1e-300)
+constexpr int NRM_WG = 64;
+__global__ __launch_bounds__(256) void cgs_norm_partial_kernel(const c128* __restrict__ w, int n, double* part) {
+  __shared__ double red[256];
+  const int tid = threadIdx.x;
+  double s = 0.0;
+  for (int i = blockIdx.x * 256 + tid; i < n; i += NRM_WG * 256) {
+    const c128 a = w[i];
+    s += a.re * a.re + a.im * a.im;
+  }
+  red[tid] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) red[tid] += red[tid + o];
+    __syncthreads();
+  }
+  if (tid == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ __launch_bounds__(256) void cgs_norm_scale_kernel(const c128* __restrict__ w, int n, const double* part,
+                                                             c128* v, c128* hsub) {
+  double s = 0.0;
+  for (int q = 0; q < NRM_WG; ++q) s += part[q];   // same order in every workgroup
+  const double nrm = sqrt(s);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *hsub = cmk(nrm, 0.0);
+  const double inv = 1.0 / fmax(nrm, 1e-300);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const c128 a = w[i];
+    v[i] = cmk(a.re * inv, a.im * inv);
+  }
+}
+
 }  // namespace
 }  // namespace qd
 
 using namespace qd;
+
+extern "C" int qd_cgs_project(const qd_c128* V, long ldv, int m, int n, const qd_c128* w, qd_c128* h, qd_c128* hsum,
+                              long ldh, void* stream) {
+  QD_CHECK_ARG(V && w && h, "qd_cgs_project: null pointer");
+  QD_CHECK_ARG(m >= 1 && n >= 1 && ldv >= n, "qd_cgs_project: m=%d n=%d ldv=%ld", m, n, ldv);
+  hipLaunchKernelGGL(cgs_project_kernel, dim3(m), dim3(256), 0, (hipStream_t)stream, (const c128*)V, ldv, n,
+                     (const c128*)w, (c128*)h, (c128*)hsum, ldh);
+  QD_HIP(hipGetLastError());
+  return QD_OK;
+}
+
+extern "C" int qd_cgs_normalize(const qd_c128* w, int n, qd_c128* v, qd_c128* hsub, void* stream) {
+  WsScope wss_((hipStream_t)stream);
+  QD_CHECK_ARG(w && v && hsub && n >= 1, "qd_cgs_normalize: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  void* part = nullptr;
+  if (int rc = workspace(WS_MISC, NRM_WG * sizeof(double), &part, st)) return rc;
+  hipLaunchKernelGGL(cgs_norm_partial_kernel, dim3(NRM_WG), dim3(256), 0, st, (const c128*)w, n, (double*)part);
+  QD_HIP(hipGetLastError());
+  hipLaunchKernelGGL(cgs_norm_scale_kernel, dim3(std::min(256, (n + 255) / 256)), dim3(256), 0, st, (const c128*)w, n,
+                     (const double*)part, (c128*)v, (c128*)hsub);
+  QD_HIP(hipGetLastError());
+  return QD_OK;
+}
 
 extern "C" int qd_shifted_hessenberg_solve(const qd_c128* H, int ldh, int k, const qd_c128* shifts, int S,
                                            double beta, qd_c128* Y, double* res, void* stream) {

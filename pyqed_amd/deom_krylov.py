@@ -217,21 +217,36 @@ def shifted_krylov_solve(op, b, shifts, tol=1e-12, m_max=None, first_check=20):
     k_done = None
     hist = []
     target = tol ** 1.1
+    gpu = dev.type == "cuda"
+    if gpu:   # CGS2 on the device: qd_cgs_project (h = V^H w into the Hessenberg column) + in-place GEMV updates
+        lib = _lib.load()
+        hbuf = torch.empty(m_max + 1, dtype=torch.complex128, device=dev)
+        ldh = Hd.stride(0)
+        col = lambda r, c: Hd.data_ptr() + (r * ldh + c) * 16
     for j in range(m_max):
         op.apply(V[j], W)
         Vj = V[:j + 1]
-        h = torch.mv(Vj, W.conj()).conj()
-        W -= torch.mv(Vj.transpose(0, 1), h)
-        h2 = torch.mv(Vj, W.conj()).conj()
-        W -= torch.mv(Vj.transpose(0, 1), h2)
-        h += h2
-        nrm = torch.linalg.vector_norm(W)
-        Hd[:j + 1, j] = h
-        Hd[j + 1, j] = nrm
-        # an exact breakdown (nrm == 0: b lies in a small invariant subspace) must not turn the basis into NaN
-        # before the next checkpoint, where the zero sub-diagonal entry ends the solve; the guard
-        # stays on the device (no host read per step)
-        V[j + 1] = W / torch.clamp(nrm, min=1e-300)
+        if gpu:
+            st = _lib.stream_ptr(dev)
+            for _ in range(2):   # classical Gram-Schmidt, applied twice; Hd[:j+1, j] accumulates h1 + h2
+                _lib.check(lib.qd_cgs_project(V.data_ptr(), n, j + 1, n, W.data_ptr(), hbuf.data_ptr(), col(0, j),
+                                              ldh, st), "qd_cgs_project")
+                W.addmv_(Vj.transpose(0, 1), hbuf[:j + 1], alpha=-1)
+            # Hd[j+1, j] = ||W||, V[j+1] = W / max(||W||, 1e-300): an exact breakdown (||W|| = 0) must not turn the
+            # basis into NaN before the next checkpoint, where the zero sub-diagonal entry ends the solve (ADVICE
+            # r05); no host read per step
+            _lib.check(lib.qd_cgs_normalize(W.data_ptr(), n, V[j + 1].data_ptr(), col(j + 1, j), st),
+                       "qd_cgs_normalize")
+        else:
+            h = torch.mv(Vj, W.conj()).conj()
+            W -= torch.mv(Vj.transpose(0, 1), h)
+            h2 = torch.mv(Vj, W.conj()).conj()
+            W -= torch.mv(Vj.transpose(0, 1), h2)
+            h += h2
+            nrm = torch.linalg.vector_norm(W)
+            Hd[:j + 1, j] = h
+            Hd[j + 1, j] = nrm
+            V[j + 1] = W / torch.clamp(nrm, min=1e-300)
         k = j + 1
         if k != check and k != m_max:
             continue
