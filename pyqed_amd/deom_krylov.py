@@ -16,7 +16,7 @@ with u^T x = Tr_sys(A1 x_0) (the ADO-0 rows) and v = A4 rho in the ADO-0 rows.  
     invariant: (-P - s) V_k = V_{k+1} (-H_k - s)), the small shifted Hessenberg systems solved per shift;
   * l(w_x) = R(w_x)^T u likewise from one Arnoldi basis of P^T started at u;
   * e^{P T} on the n_w vectors of the shorter side (or e^{P^T T} on the left ones) by Taylor substeps with
-    ||P tau|| <= 1 (degree 20, remainder < 1e-19 per substep);
+    ||P tau|| <= 3 (degree 36, remainder < 1e-24 per substep);
   * c = l(w_x)^T A2 e^{PT} A3 r(w_y): one complex GEMM.
 
 Every application of P or P^T is the DEOM stencil kernel (qd_deom_apply); P^T is the same operator form on
@@ -32,7 +32,9 @@ import torch
 
 from . import _lib
 
-TAYLOR_DEGREE = 20   # terms per substep of e^{P tau}, ||P tau||_inf <= 1: remainder <= e / 21! < 2e-19
+TAYLOR_RADIUS = 3.0   # substeps tau with ||P tau||_inf <= TAYLOR_RADIUS
+TAYLOR_DEGREE = 36    # terms per substep: remainder <= e^3 3^37 / 37! < 1e-24; largest term 3^3 / 3! = 4.5 (no cancellation
+                      # beyond one digit); 118 substeps x 36 terms at the bench hierarchy against 352 x 20 at radius 1
 
 
 def transposed_tables(minus, plus, coef):
@@ -293,14 +295,14 @@ def shifted_krylov_solve(op, b, shifts, tol=1e-12, m_max=None, first_check=20):
 
 
 def expv_taylor(op, X, T, graph=True):
-    """e^{P T} X for X [B, n] on the device: Taylor substeps tau = T / s with ||P tau||_inf <= 1, each the degree-
-    TAYLOR_DEGREE polynomial in Horner form, y <- x + (tau / j) P y for j = TAYLOR_DEGREE .. 1 (every step one stencil
+    """e^{P T} X for X [B, n] on the device: Taylor substeps tau = T / s with ||P tau||_inf <= TAYLOR_RADIUS, each
+    the degree-TAYLOR_DEGREE polynomial in Horner form, y <- x + (tau / j) P y for j = TAYLOR_DEGREE .. 1 (every step one stencil
     launch with the axpy fused: qd_deom_apply's x0).  B > 1 vectors run ADO-major ([nmax][B][ns][ns], the batched
     stencil kernels).  graph=True captures one substep (its stencil launches and the closing copy, fixed buffers) into
     a HIP graph and replays it s times (replays are bit for bit, tests/test_graph_capture_gpu.py)."""
     if T == 0:
         return X.clone(), 0
-    s = max(1, int(np.ceil(abs(T) * op.norm)))
+    s = max(1, int(np.ceil(abs(T) * op.norm / TAYLOR_RADIUS)))
     tau = T / s
     B = X.numel() // op.n
     am = X.is_cuda and B > 1 and op.ns * op.ns <= 64 and getattr(op, "K", 99) <= 8
