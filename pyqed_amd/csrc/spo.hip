@@ -110,7 +110,7 @@ __device__ __forceinline__ void apply_point_op(const c128* in, c128* out, int st
   }
 }
 
-enum RowFlags { ROW_INV = 1, ROW_VH1 = 2, ROW_SNAP = 4, ROW_VH2 = 8, ROW_FWD = 16, ROW_KY = 32 };
+enum RowFlags { ROW_INV = 1, ROW_VH1 = 2, ROW_SNAP = 4, ROW_VH2 = 8, ROW_FWD = 16, ROW_KY = 32, ROW_KZ = 64 };
 
 // One row i of psi [nx][ny][ns]; FFTs along y (length L = ny) for each state.
 // ROW_KY (Jacobi KEO, wpd.py:850-887): after FFT_y multiply by expKy[i][ky] (row i's k_y factor).
@@ -891,8 +891,11 @@ __device__ __forceinline__ void fft64_group(c128* line, int stride, const Q16Tw&
 // Middle-axis pass at L = 64 with the register transform (same tiles and loads as spo_mid_fast_kernel<64, C>):
 // the C columns (C x 16 B per row) are staged in LDS, each 16-lane group transforms one column line in place
 // (fft64_group, wave barriers only), and the tile is stored back.
-template <int C, bool INV>
-__global__ __launch_bounds__(16 * C) void spo_mid64_kernel(c128* psi, const c128* tw_g, int inner) {
+// KD: the whole separable axis propagator F^-1 diag(d) F on each line (forward transform, * d[k], inverse; d holds
+// e_y / ny), natural order in and out (qd_spo3_run_axes on power-of-two 64-point axes)
+template <int C, bool INV, bool KD = false>
+__global__ __launch_bounds__(16 * C) void spo_mid64_kernel(c128* psi, const c128* tw_g, int inner,
+                                                           const c128* dk = nullptr) {
   constexpr int BD = 16 * C, LS = 65;  // line stride (padded)
   __shared__ c128 A[C * LS];
   __shared__ c128 tw[64];
@@ -916,6 +919,14 @@ __global__ __launch_bounds__(16 * C) void spo_mid64_kernel(c128* psi, const c128
   const Q16Tw t = q64_twiddles(tw, qq, s);
   c128* line = A + g * LS;
   fft64_group<INV>(line, 1, t, qq, s, v);
+  if constexpr (KD) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) line[lane16 + 16 * k] = cmul(v[k], dk[lane16 + 16 * k]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    fft64_group<true>(line, 1, t, qq, s, v);
+  }
 #pragma unroll
   for (int k = 0; k < 4; ++k) line[lane16 + 16 * k] = v[k];
   __syncthreads();
@@ -931,7 +942,7 @@ __global__ __launch_bounds__(16 * C) void spo_mid64_kernel(c128* psi, const c128
 // (nx ny nz) -> IFFT_x on one line in registers (natural order between the transforms).
 template <int C, int NS>
 __global__ __launch_bounds__(16 * C * NS) void spo_col64_kernel(c128* psi, const c128* expKT, const c128* tw_g,
-                                                                int ny) {
+                                                                int ny, int kstride = 64) {
   constexpr int W = C * NS, BD = 16 * W, LS = 65;
   __shared__ c128 A[W * LS];
   __shared__ c128 tw[64];
@@ -944,7 +955,7 @@ __global__ __launch_bounds__(16 * C * NS) void spo_col64_kernel(c128* psi, const
     v[n] = psi[((size_t)(e / W) * ny + j0) * NS + e % W];
   }
 #pragma unroll
-  for (int k = 0; k < 4; ++k) kf[k] = expKT[(size_t)(j0 + g / NS) * 64 + lane16 + 16 * k];
+  for (int k = 0; k < 4; ++k) kf[k] = expKT[(size_t)(j0 + g / NS) * kstride + lane16 + 16 * k];   // 0: one factor
   if (tid < 64) tw[tid] = tw_g[tid];
 #pragma unroll
   for (int n = 0; n < 4; ++n) {
@@ -979,7 +990,7 @@ __global__ __launch_bounds__(16 * C * NS) void spo_col64_kernel(c128* psi, const
 // [IFFT] -> V/2 -> [snapshot] -> [V/2] -> [FFT].
 template <int NS>
 __global__ __launch_bounds__(256) void spo_row64_kernel(c128* psi, const c128* U, const c128* tw_g, int flags,
-                                                        c128* snap) {
+                                                        c128* snap, const c128* dz = nullptr) {
   __shared__ c128 E[16 * NS * 64];      // per row: [state][64]
   __shared__ c128 tw[64];
   const int tid = threadIdx.x, grp = tid >> 4, lane16 = tid & 15, qq = lane16 >> 2, s = lane16 & 3;
@@ -1047,6 +1058,18 @@ __global__ __launch_bounds__(256) void spo_row64_kernel(c128* psi, const c128* U
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (int c = 0; c < NS; ++c) fft64_group<false>(ex + c * 64, 1, t, qq, s, x[c]);
+    if (flags & ROW_KZ) {   // * e_z / nz, inverse transform: the separable z propagator, natural order out
+#pragma unroll
+      for (int c = 0; c < NS; ++c) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ex[c * 64 + lane16 + 16 * k] = cmul(x[c][k], dz[lane16 + 16 * k]);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int c = 0; c < NS; ++c) fft64_group<true>(ex + c * 64, 1, t, qq, s, x[c]);
+    }
   }
 #pragma unroll
   for (int k = 0; k < 4; ++k)
@@ -1132,6 +1155,68 @@ int col_fast(int L, int ns, int cols, c128* psi, const c128* expKT, const c128* 
 }
 
 }  // namespace
+
+// d[a][k] = fft(m_a)[k] / n (the axis factor e_a / n of a circulant axis propagator given by its first column)
+__global__ void axis_factor_kernel(const c128* m0, const c128* m1, const c128* m2, int n, c128* d) {
+  const c128* m = blockIdx.x == 0 ? m0 : blockIdx.x == 1 ? m1 : m2;
+  const int k = threadIdx.x;
+  if (k >= n) return;
+  c128 acc = cmk(0.0, 0.0);
+  for (int j = 0; j < n; ++j) {
+    double sn, cs;
+    sincospi(-2.0 * (double)((j * k) % n) / n, &sn, &cs);
+    acc = cadd(acc, cmul(m[j], cmk(cs, sn)));
+  }
+  d[blockIdx.x * n + k] = cmk(acc.re / n, acc.im / n);
+}
+
+// SPO3 on a 64 x 64 x 64 grid with a separable kinetic propagator (qd_spo3_run_axes): three passes per step, each the
+// whole axis propagator F^-1 diag(e_a / n) F on its lines with the 64-point register transforms -- z (contiguous,
+// with the point operators: the previous step's closing half, the snapshot, this step's opening half), y (mid axis),
+// x (columns) -- where the non-separable path needs four (the x pass multiplies the 3-D exp_K between the y and z
+// transforms, so both are undone in passes of their own).
+int spo3_sep64_run(c128* psi, const c128* Vh, const c128* const m[3], int ns, int nsteps, int nout, c128* snap,
+                   hipStream_t st) {
+  void* w = nullptr;
+  int rc = workspace(WS_SPO, (size_t)4 * 64 * sizeof(c128), &w, st);
+  if (rc) return rc;
+  c128* tw = (c128*)w;
+  c128* d = tw + 64;
+  if ((rc = twiddles(64, st, tw))) return rc;
+  hipLaunchKernelGGL(axis_factor_kernel, dim3(3), dim3(64), 0, st, m[0], m[1], m[2], 64, d);
+  QD_HIP(hipGetLastError());
+  const int rows = 64 * 64, nyz = 64 * 64, inner = 64 * ns;
+  const size_t grid_elems = (size_t)64 * 64 * 64 * ns;
+  auto zpass = [&](int flags, c128* sp) -> int {
+    if (ns == 1) hipLaunchKernelGGL(spo_row64_kernel<1>, dim3(rows / 16), dim3(256), 0, st, psi, Vh, tw, flags, sp, d + 128);
+    else hipLaunchKernelGGL(spo_row64_kernel<2>, dim3(rows / 16), dim3(256), 0, st, psi, Vh, tw, flags, sp, d + 128);
+    QD_HIP(hipGetLastError());
+    return QD_OK;
+  };
+  auto ypass = [&]() -> int {
+    if (ns == 1) hipLaunchKernelGGL((spo_mid64_kernel<4, false, true>), dim3(64 * (inner / 4)), dim3(64), 0, st, psi, tw, inner, d + 64);
+    else hipLaunchKernelGGL((spo_mid64_kernel<8, false, true>), dim3(64 * (inner / 8)), dim3(128), 0, st, psi, tw, inner, d + 64);
+    QD_HIP(hipGetLastError());
+    return QD_OK;
+  };
+  auto xpass = [&]() -> int {
+    if (ns == 1) hipLaunchKernelGGL((spo_col64_kernel<4, 1>), dim3(nyz / 4), dim3(64), 0, st, psi, (const c128*)d, tw, nyz, 0);
+    else hipLaunchKernelGGL((spo_col64_kernel<4, 2>), dim3(nyz / 4), dim3(128), 0, st, psi, (const c128*)d, tw, nyz, 0);
+    QD_HIP(hipGetLastError());
+    return QD_OK;
+  };
+  for (int s = 0; s <= nsteps; ++s) {
+    // step s's z pass closes step s - 1 (its snapshot) and opens step s; the pass after the last step only closes
+    const bool take = snap && s > 0 && s % nout == 0;
+    int flags = (s > 0 ? ROW_VH1 : 0) | (take ? ROW_SNAP : 0);
+    if (s < nsteps) flags |= ROW_VH2 | ROW_FWD | ROW_KZ;
+    if ((rc = zpass(flags, take ? snap + (size_t)(s / nout - 1) * grid_elems : nullptr))) return rc;
+    if (s == nsteps) break;
+    if ((rc = ypass())) return rc;
+    if ((rc = xpass())) return rc;
+  }
+  return QD_OK;
+}
 
 // spo_gen.hip: every grid the specialised power-of-two kernels below do not cover
 int spo_generic_run(c128* psi, const c128* expVh, const c128* expV, const c128* expK, const c128* expKy,

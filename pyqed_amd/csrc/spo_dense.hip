@@ -164,6 +164,10 @@ int run_axes(c128* psi, const c128* Vh, const c128* const m[3], const int d[3], 
 }
 
 }  // namespace
+
+// spo.hip: 64^3 grids on the register transforms (three separable passes per step)
+int spo3_sep64_run(c128* psi, const c128* Vh, const c128* const m[3], int ns, int nsteps, int nout, c128* snap,
+                   hipStream_t st);
 }  // namespace qd
 
 using namespace qd;
@@ -177,10 +181,15 @@ extern "C" int qd_spo3_run_axes(qd_c128* psi, const qd_c128* expVh, const qd_c12
   QD_CHECK_ARG(ns == 1 || ns == 2, "qd_spo3_run_axes: ns=%d (1 or 2)", ns);
   QD_CHECK_ARG(nsteps >= 0 && nout >= 1, "qd_spo3_run_axes: nsteps=%d nout=%d", nsteps, nout);
   if (nsteps == 0) return QD_OK;
-  note_path("spo3_axes");
   const c128* m[3] = {(const c128*)mx, (const c128*)my, (const c128*)mz};
   const int d[3] = {nx, ny, nz};
   hipStream_t st = (hipStream_t)stream;
+  if (nx == 64 && ny == 64 && nz == 64) {
+    WsScope wss_(st);
+    note_path("spo3_sep64");
+    return spo3_sep64_run((c128*)psi, (const c128*)expVh, m, ns, nsteps, nout, (c128*)snap, st);
+  }
+  note_path("spo3_axes");
   return ns == 1 ? run_axes<1>((c128*)psi, (const c128*)expVh, m, d, nsteps, nout, (c128*)snap, st)
                  : run_axes<2>((c128*)psi, (const c128*)expVh, m, d, nsteps, nout, (c128*)snap, st);
 }

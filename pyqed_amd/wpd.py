@@ -496,10 +496,12 @@ def axis_propagator(k, m, dt):
 class SPO3(_PointPropagators):
     """Drop-in for pyqed.wpd.SPO3 (wpd.py:1105-1432), linear coordinates.
 
-    kinetic_path: "auto" takes the kinetic step as three per-axis mode products on the MFMAs (qd_spo3_run_axes; any
-    length, no FFT plan) when every axis has at most AXES_MAX_N points, one or two states and some axis is not a power
-    of two (64^3 x 2: 26 us per step on the power-of-two FFT passes against 32 on the axis products; 60^3 x 2: 52
-    against 31, profiles/r06/spo/spo3_axes_ab.txt); "axes" / "fft" force one (tests)."""
+    kinetic_path: "auto" takes the separable kinetic step (qd_spo3_run_axes) when every axis has at most AXES_MAX_N
+    points and there are one or two states: 64^3 as three register-FFT passes of F^-1 diag(e_a / n) F (22 us per
+    64^3 x 2 step against 26 on the four passes of the 3-D exp_K), every other such grid as three per-axis mode
+    products on the MFMAs (60^3 x 2: 31 us against 52 on the mixed-radix FFT passes; profiles/r06/spo/);
+    larger grids or more states the FFT passes (qd_spo3_run).  "axes" / "fft" force one (tests).
+    """
 
     AXES_MAX_N = 64
     kinetic_path = "auto"
@@ -513,7 +515,7 @@ class SPO3(_PointPropagators):
             return True
         if self.kinetic_path == "fft":
             return False
-        return fits and not all(n & (n - 1) == 0 for n in dims)
+        return fits
 
     def __init__(self, x, y, z, masses, nstates=2, coords='linear', G=None, abc=False):
         self.x, self.y, self.z = x, y, z

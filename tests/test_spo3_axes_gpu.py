@@ -23,19 +23,21 @@ def _model(dims, ns, seed=0):
     return sol, psi0
 
 
-@pytest.mark.parametrize("dims,ns,nt,nout", [((64, 64, 64), 2, 4, 2), ((60, 60, 60), 2, 3, 1), ((64, 48, 32), 1, 4, 4),
+@pytest.mark.parametrize("dims,ns,nt,nout", [((64, 64, 64), 2, 4, 2), ((64, 64, 64), 1, 5, 2), ((60, 60, 60), 2, 3, 1),
+                                             ((64, 48, 32), 1, 4, 4),
                                              ((17, 9, 33), 2, 5, 2), ((5, 7, 3), 2, 3, 1), ((2, 16, 40), 1, 2, 1),
                                              ((50, 3, 2), 2, 4, 3)])
 def test_spo3_axes_matches_fftn_restatement(dims, ns, nt, nout, monkeypatch):
     """Every length in [1, 64] alike (the z pass's tile of whole points, column tiles crossing outer boundaries,
-    padded K and rows, ragged last tiles): snapshots and the final state against the fftn restatement, norm kept."""
+    padded K and rows, ragged last tiles), and 64^3 on the three separable register-FFT passes: snapshots and the
+    final state against the fftn restatement, norm kept."""
     from oracle import spo as ospo
     from conftest import took
     sol, psi0 = _model(dims, ns)
     monkeypatch.setattr(type(sol), "kinetic_path", "axes")
     took("")
     r = sol.run(psi0=psi0, dt=0.1, nt=nt, nout=nout)
-    hit, got = took("spo3_axes")
+    hit, got = took("spo3_sep64" if tuple(dims) == (64, 64, 64) else "spo3_axes")
     assert hit, got
     ref, psi = ospo.spo3_run(sol.exp_V_half, sol.exp_K, psi0, nt, nout)
     assert len(r.psilist) == len(ref)
@@ -62,7 +64,8 @@ def test_spo3_axes_reference_fixture():
 
 
 def test_spo3_axes_long_run_matches_fft_passes():
-    """400 Strang steps at 64^3 x 2: the axis path against the FFT passes (qd_spo3_run) on the same state."""
+    """400 Strang steps at 64^3 x 2: the separable entry point (three register-FFT passes at 64^3) against the four
+    FFT passes of the 3-D exp_K (qd_spo3_run) on the same state."""
     import torch
     from pyqed_amd import _lib
     from pyqed_amd.wpd import axis_propagator
@@ -83,10 +86,10 @@ def test_spo3_axes_long_run_matches_fft_passes():
 
 
 def test_spo3_path_choice():
-    """auto: power-of-two grids keep the FFT passes, any other grid <= 64 per axis with one or two states takes the
-    axis products; larger or many-state grids the FFT passes."""
+    """auto: every grid <= 64 per axis with one or two states takes the separable entry point (qd_spo3_run_axes);
+    larger or many-state grids the FFT passes."""
     from pyqed_amd.wpd import SPO3
     pick = lambda dims, ns=2: SPO3(*[np.linspace(-1, 1, n) for n in dims], masses=[1, 1, 1], nstates=ns)._use_axes()
-    assert not pick((64, 64, 64)) and not pick((32, 16, 64))
+    assert pick((64, 64, 64)) and pick((32, 16, 64))
     assert pick((60, 60, 60)) and pick((64, 48, 32)) and pick((24, 20, 18), 1)
     assert not pick((96, 60, 60)) and not pick((60, 60, 60), 3)
