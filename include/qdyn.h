@@ -492,8 +492,10 @@ int qd_spo3_run(qd_c128* psi, const qd_c128* expVh, const qd_c128* expK, int nx,
  * exp_K = e_x (x) e_y (x) e_z): the kinetic step fftn, * exp_K, ifftn of _KEO_linear
  * (wpd.py:1418-1432) is applied as three per-axis mode products with the circulant axis
  * propagators M_a = F^-1 diag(e_a) F, given by their first columns m_a = ifft(e_a) [n_a]
- * (M_a[i][k] = m_a[(i - k) mod n_a]; out[i] = sum_k M_a[i][k] in[k] along axis a), on the
- * f64 MFMAs.  Same step structure, snapshots and result as qd_spo3_run (to rounding).
+ * (M_a[i][k] = m_a[(i - k) mod n_a]; out[i] = sum_k M_a[i][k] in[k] along axis a): 64^3 as
+ * three passes on the 64-point register transforms (e_a = fft(m_a) formed on the device),
+ * every other shape as mode products on the f64 MFMAs.  Same step structure, snapshots and
+ * result as qd_spo3_run (to rounding).
  * n_a in [1, 64], ns in {1, 2}.
  */
 int qd_spo3_run_axes(qd_c128* psi, const qd_c128* expVh, const qd_c128* mx,
