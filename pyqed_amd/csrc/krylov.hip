@@ -205,7 +205,15 @@ extern "C" int qd_shifted_hessenberg_solve(const qd_c128* H, int ldh, int k, con
     const int rc = workspace(WS_MISC, (size_t)S * k * k * sizeof(c128), &w, st);
     if (rc) return rc;
   }
-  const size_t lds = (size_t)2 * k * sizeof(c128);
+  const size_t lds = (size_t)2 * k * sizeof(c128);   // <= 128 KB at k = 4096
+  if (lds > 64 * 1024) {
+    static const bool lds_attr = [] {
+      // the 160 KiB of a CU less the kernel's static LDS (the attribute is refused above that)
+      return hipFuncSetAttribute((const void*)hess_shift_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 160 * 1024 - 1024) == hipSuccess;
+    }();
+    (void)lds_attr;
+  }
   hipLaunchKernelGGL(hess_shift_kernel, dim3(S), dim3(256), lds, st, (const c128*)H, ldh, k, (const c128*)shifts, beta,
                      (c128*)Y, res, (c128*)w);
   QD_HIP(hipGetLastError());

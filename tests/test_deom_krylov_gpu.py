@@ -61,7 +61,7 @@ def test_taylor_graph_replay_equals_direct_substeps():
     assert relerr(yg.cpu().numpy(), x @ scipy.linalg.expm(P * T).T) < 1e-11
 
 
-@pytest.mark.parametrize("k,S", [(1, 3), (7, 5), (300, 33)])
+@pytest.mark.parametrize("k,S", [(1, 3), (7, 5), (300, 33), (2500, 2)])
 def test_shifted_hessenberg_solve_matches_dense_solves(k, S):
     """qd_shifted_hessenberg_solve (one workgroup per shift, adjacent-row pivoting) against numpy.linalg.solve of every
     (-H_k - s I) y = beta e_1 and the host residual form (_shift_residuals), on a random Hessenberg matrix with a
