@@ -32,6 +32,10 @@
 // in a per-workgroup scratch slab in HBM (L2/MALL resident in practice).
 // Matrices are zero-padded to Np = 32, 64 or a multiple of 128 so every GEMM
 // tile is full; the padding stays exactly zero through the propagation.
+// The complex GEMM engine's next-tile LDS stores issue before k-step 2 of 4 in this file's kernels (cgemm_block.hpp
+// default 3): with the Hermitian epilogue's round-0 loads issued before its LDS passes (GLF_EPI_PRE 4) and 8-element
+// Horner chunks, 351.5k -> 357.6k DM-steps/s on the headline batch (profiles/r06/lindblad/epilogue_knobs.txt)
+#define CG_STAGE_AT 2
 #include "glf_kernel.hpp"
 
 namespace qd {

@@ -110,7 +110,7 @@ __device__ void wg_observables(const c128* rho, const c128* eT, int ne, size_t N
 #define GLF_HERM_X 1   // Hermitian kernel at BT = 128: X GEMM on the CgHermLayout tiles (Lindblad: no Hermitian part below the diagonal; A/B: 0)
 #endif
 #ifndef GLF_EPI_PRE
-#define GLF_EPI_PRE 0   // Hermitian epilogue: this many rho loads of round 0's first chunk issued before the LDS passes (A/B)
+#define GLF_EPI_PRE 4   // Hermitian epilogue: this many rho loads of round 0's first chunk issued before the LDS passes
 #endif
 #ifndef GLF_SPLIT_DEPTH
 #define GLF_SPLIT_DEPTH 2   // split-path GEMMs: K-tiles of global loads in flight ahead of the MFMAs (1 or 2)
@@ -289,8 +289,8 @@ __global__ __launch_bounds__(CG_WG) void lindblad_rk4_kernel(LindbladParams p) {
         {
           constexpr int TS = BT / 2, LD = TS + 1, TRI = TS * (TS + 1) / 2;
           static_assert((TS * LD + 2 * TRI) * sizeof(c128) <= sizeof(CgLds<BT>), "LDS k buffers");
-          #ifndef QD_EPI_CH
-#define QD_EPI_CH 4
+#ifndef QD_EPI_CH
+#define QD_EPI_CH 8   // rho loads per thread in flight per chunk of the Horner update
 #endif
           c128* T01 = reinterpret_cast<c128*>(&L);
           c128* Tt = T01 + TS * LD;
