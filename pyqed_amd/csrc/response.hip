@@ -420,8 +420,9 @@ __global__ __launch_bounds__(CG_WG) void ens_gemm_kernel(const c128* X, int Kp, 
       cg_block_gemm_gen<BT, ENS_PIPE>(t1 - t0, pa, pb, L, A);
     } else {
       EnsXA pa{X, Kp, bm * BT, t0 * CG_KT};
-      if constexpr (DEPTH == 2)
-        cg_block_gemm_gen2<BT, ENS_PIPE>(t1 - t0, pa, pb, L, A);
+      if constexpr (DEPTH == 2)   // fragment double-buffering for the 64-blocks (shard: 0.1630 vs 0.1653 ms per grid;
+                                  // the 128-blocks slow down with it, 1.53 vs 1.19 ms: profiles/r06/2des/knobs_ab.txt)
+        cg_block_gemm_gen2<BT, ENS_PIPE || BT == 64>(t1 - t0, pa, pb, L, A);
       else
         cg_block_gemm_gen<BT, ENS_PIPE>(t1 - t0, pa, pb, L, A);
     }
