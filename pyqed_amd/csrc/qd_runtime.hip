@@ -97,7 +97,9 @@ static int capture_alloc(size_t bytes, void** ptr, hipStream_t st) {
   e = hipUserObjectCreate(&obj, ud, cap_release, 1, hipUserObjectNoDestructorSync);
   if (e == hipSuccess) e = hipGraphRetainUserObject(graph, obj, 1, hipGraphUserObjectMove);
   if (e != hipSuccess) {
-    if (!obj) {
+    if (obj) {
+      (void)hipUserObjectRelease(obj, 1);   // its destructor queues the buffer for the next uncaptured call's free
+    } else {
       delete ud;
       (void)hipFree(p);
     }
