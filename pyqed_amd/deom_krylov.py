@@ -16,7 +16,7 @@ with u^T x = Tr_sys(A1 x_0) (the ADO-0 rows) and v = A4 rho in the ADO-0 rows.  
     invariant: (-P - s) V_k = V_{k+1} (-H_k - s)), the small shifted Hessenberg systems solved per shift;
   * l(w_x) = R(w_x)^T u likewise from one Arnoldi basis of P^T started at u;
   * e^{P T} on the n_w vectors of the shorter side (or e^{P^T T} on the left ones) by Taylor substeps with
-    ||P tau|| <= 3 (degree 36, remainder < 1e-24 per substep);
+    ||P tau|| <= 5 (degree 48, remainder < 1e-26 per substep);
   * c = l(w_x)^T A2 e^{PT} A3 r(w_y): one complex GEMM.
 
 Every application of P or P^T is the DEOM stencil kernel (qd_deom_apply); P^T is the same operator form on
@@ -32,9 +32,10 @@ import torch
 
 from . import _lib
 
-TAYLOR_RADIUS = 3.0   # substeps tau with ||P tau||_inf <= TAYLOR_RADIUS
-TAYLOR_DEGREE = 36    # terms per substep: remainder <= e^3 3^37 / 37! < 1e-24; largest term 3^3 / 3! = 4.5 (no cancellation
-                      # beyond one digit); 118 substeps x 36 terms at the bench hierarchy against 352 x 20 at radius 1
+TAYLOR_RADIUS = 5.0   # substeps tau with ||P tau||_inf <= TAYLOR_RADIUS
+TAYLOR_DEGREE = 48    # terms per substep: remainder <= e^5 5^49 / 49! < 1e-26; largest term 5^5 / 5! = 26 (the sum of the
+                      # terms' magnitudes <= e^5: ~2 digits of cancellation at most); 71 substeps x 48 terms at the bench
+                      # hierarchy against 118 x 36 at radius 3 and 352 x 20 at radius 1
 
 
 def transposed_tables(minus, plus, coef):
