@@ -167,3 +167,40 @@ def test_graph_scratch_is_released_with_the_graph():
         lindblad_rk4(Ht, Ct, y, 1e-3, 2, hermitian=False)   # an uncaptured call frees what destroyed graphs released
         torch.cuda.synchronize()
         assert free0 - torch.cuda.mem_get_info(dev)[0] < 64 << 20
+
+
+@pytest.mark.parametrize("n", [64, 60])
+def test_spo3_separable_call_replays_from_a_graph(n):
+    """qd_spo3_run_axes captured once (64^3: the separable register-FFT passes with their device-side axis factors;
+    60^3: the MFMA axis products) and replayed twice equals two direct calls bit for bit."""
+    from pyqed_amd import _lib
+    from pyqed_amd.wpd import SPO3, axis_propagator
+    dev = torch.device("cuda", 0)
+    x = np.linspace(-6, 6, n)
+    X, Y, Z = np.meshgrid(x, x, x, indexing="ij")
+    sol = SPO3(x, x, x, masses=[1.0, 1.2, 0.9], nstates=2)
+    sol.set_DPES([0.5 * ((X + 1) ** 2 + Y ** 2 + Z ** 2), 0.5 * ((X - 1) ** 2 + Y ** 2 + Z ** 2)], [[[0, 1], 0.2 * X]])
+    sol.build(0.05)
+    psi0 = np.zeros((n, n, n, 2), complex)
+    psi0[..., 1] = np.exp(-((X + 1) ** 2 + Y ** 2 + Z ** 2) / 2 + 0.3j * Y)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    eVh = t(sol.exp_V_half)
+    m = [t(axis_propagator(k, ma, 0.05)) for k, ma in zip((sol.kx, sol.ky, sol.kz), sol.masses)]
+    lib = _lib.load()
+    s = torch.cuda.Stream(dev)
+
+    def run(psi):
+        _lib.check(lib.qd_spo3_run_axes(psi.data_ptr(), eVh.data_ptr(), *(v.data_ptr() for v in m), n, n, n, 2, 3, 3,
+                                        None, s.cuda_stream), "qd_spo3_run_axes")
+    ref = t(psi0)
+    with torch.cuda.stream(s):
+        run(ref)
+        run(ref)
+    torch.cuda.synchronize()
+    xg = t(psi0)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        run(xg)
+    for out in _replays(g, xg, t(psi0), s):
+        assert torch.equal(out, ref)
