@@ -399,6 +399,18 @@ int qd_cgs_project(const qd_c128* V, long ldv, int m, int n, const qd_c128* w, q
 int qd_cgs_normalize(const qd_c128* w, int n, qd_c128* v, qd_c128* hsub, void* stream);
 
 /*
+ * One step of the delayed CGS2 Arnoldi process (two passes over the basis instead of four).
+ * Entering step j: V[0..j-1] final, V[j] = u_j (the candidate after one projection), z = P u_j,
+ * H (row-major, leading dimension ldh >= j + 1, at least j + 2 rows) with columns 0..j-2 final and
+ * column j-1 holding u_j's projection coefficients.  On return V[j] = v_j, column j-1 final
+ * (re-orthogonalisation added, h_{j,j-1} = |u_j - V_j s|), column j the projection coefficients
+ * of P v_j and V[j+1] = u_{j+1}.  Start with V[0] = b at j = 0.  An exact breakdown writes
+ * h_{j,j-1} = 0 and zero vectors from there on.  st: 2(j+1) and cs: j+2 complex scratch.
+ */
+int qd_arnoldi_dcgs2_step(qd_c128* V, long ldv, int j, int n, const qd_c128* z, qd_c128* H,
+                          long ldh, qd_c128* st, qd_c128* cs, void* stream);
+
+/*
  * The shifted Hessenberg solves of the multi-shift Krylov form of
  * DEOMSolver.correlation_4op_3t (pyqed_amd/deom_krylov.py; the reference diagonalises P
  * instead, pyqed/heom/deom.py:1127-1209): for each of the S shifts s, (-H_k - s I) y = beta e_1

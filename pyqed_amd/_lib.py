@@ -79,6 +79,8 @@ SIGNATURES = {
     "qd_cgs_project": (c_int, [c_void_p, ctypes.c_long, c_int, c_int, c_void_p, c_void_p, c_void_p, ctypes.c_long,
                                c_void_p]),
     "qd_cgs_normalize": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "qd_arnoldi_dcgs2_step": (c_int, [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p, c_long, c_void_p, c_void_p,
+                                      c_void_p]),
     "qd_shifted_hessenberg_solve": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_double, c_void_p, c_void_p,
                                             c_void_p]),
     "qd_deom_apply": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,

@@ -165,10 +165,219 @@ __global__ __launch_bounds__(256) void cgs_norm_scale_kernel(const c128* __restr
   }
 }
 
+// ---- delayed CGS2 Arnoldi step (two passes over the basis per step instead of CGS2's four) --------------------------
+// State entering step j: V[0..j-1] final orthonormal, V[j] = u_j the candidate after ONE projection (unnormalised),
+// z = P u_j, Hessenberg columns 0..j-2 final, column j-1 holding the first-pass coefficients.  One projection pass
+// gives s = V_j^H u_j (the reorthogonalisation of u_j), t = V_j^H z, alpha = |u_j|^2, gamma = u_j^H z; then
+//   rho = sqrt(alpha - |s|^2), v_j = (u_j - V_j s) / rho, column j-1 += s, h_{j,j-1} = rho,
+//   P v_j = (z - V_j H_j s - v_j rho s_{j-1}) / rho   (Arnoldi relation P V_j = V_{j+1} Hbar_j),
+//   first-pass coefficients of column j: a_r = (t_r - (H_j s)_r) / rho (r < j), a_j = ((gamma - s^H t)/rho - rho s_{j-1})/rho,
+//   u_{j+1} = z / rho - V_j c - v_j d with c = H_j s / rho + a_{<j}, d = s_{j-1} + a_j
+// and one update pass writes v_j and u_{j+1}.  Step 0 starts from V[0] = b (j = 0: no basis, rho = |b|).
+
+// st[2r] = conj(V[r]) . V[j], st[2r+1] = conj(V[r]) . z for r <= j (row j: alpha, gamma)
+__global__ __launch_bounds__(256) void dcgs_project_kernel(const c128* __restrict__ V, long ldv, int j, int n,
+                                                           const c128* __restrict__ z, c128* st) {
+  __shared__ double red[4][256];
+  const int r = blockIdx.x, tid = threadIdx.x;
+  const c128* vr = V + (size_t)r * ldv;
+  const c128* u = V + (size_t)j * ldv;
+  double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+  constexpr int U = 6;
+  int i = tid;
+  for (; i + 256 * (U - 1) < n; i += 256 * U) {
+    c128 a[U], x[U], y[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      a[q] = vr[i + 256 * q];
+      x[q] = u[i + 256 * q];
+      y[q] = z[i + 256 * q];
+    }
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      a0 += a[q].re * x[q].re + a[q].im * x[q].im;
+      a1 += a[q].re * x[q].im - a[q].im * x[q].re;
+      b0 += a[q].re * y[q].re + a[q].im * y[q].im;
+      b1 += a[q].re * y[q].im - a[q].im * y[q].re;
+    }
+  }
+  for (; i < n; i += 256) {
+    const c128 a = vr[i], x = u[i], y = z[i];
+    a0 += a.re * x.re + a.im * x.im;
+    a1 += a.re * x.im - a.im * x.re;
+    b0 += a.re * y.re + a.im * y.im;
+    b1 += a.re * y.im - a.im * y.re;
+  }
+  red[0][tid] = a0;
+  red[1][tid] = a1;
+  red[2][tid] = b0;
+  red[3][tid] = b1;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) red[c][tid] += red[c][tid + o];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    st[2 * r] = cmk(red[0][0], red[1][0]);
+    st[2 * r + 1] = cmk(red[2][0], red[3][0]);
+  }
+}
+
+// one wave per Hessenberg row r < j (4 per workgroup); every workgroup recomputes |s|^2 and s^H t in the same order.
+// cs[r] = c_r (r < j), cs[j] = d, cs[j+1] = (1/rho, 0); rho = 0 (exact breakdown) zeroes v_j, u_{j+1} and column j.
+__global__ __launch_bounds__(256) void dcgs_coef_kernel(c128* H, long ldh, int j, const c128* __restrict__ st,
+                                                        c128* cs) {
+  __shared__ double red[3][256];
+  const int tid = threadIdx.x;
+  double ss = 0.0, p0 = 0.0, p1 = 0.0;
+  for (int r = tid; r < j; r += 256) {
+    const c128 s = st[2 * r], t = st[2 * r + 1];
+    ss += s.re * s.re + s.im * s.im;
+    p0 += s.re * t.re + s.im * t.im;   // conj(s) t
+    p1 += s.re * t.im - s.im * t.re;
+  }
+  red[0][tid] = ss;
+  red[1][tid] = p0;
+  red[2][tid] = p1;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+      red[0][tid] += red[0][tid + o];
+      red[1][tid] += red[1][tid + o];
+      red[2][tid] += red[2][tid + o];
+    }
+    __syncthreads();
+  }
+  const double rho2 = st[2 * j].re - red[0][0];
+  const double rho = rho2 > 0.0 ? sqrt(rho2) : 0.0;
+  const bool zero = !(rho > 1e-300);
+  const double inv = zero ? 0.0 : 1.0 / rho;
+  const c128 sl = j > 0 ? st[2 * (j - 1)] : cmk(0.0, 0.0);
+  const int lane = tid & 63;
+  const int r = blockIdx.x * 4 + (tid >> 6);
+  if (r < j) {
+    // (H_j s)_r over the final columns: column j-1 is its first-pass value plus s_r
+    double h0 = 0.0, h1 = 0.0;
+    c128* hr = H + (size_t)r * ldh;
+    for (int c = (r > 0 ? r - 1 : 0) + lane; c < j; c += 64) {
+      c128 h = hr[c];
+      if (c == j - 1) h = cadd(h, st[2 * r]);
+      const c128 s = st[2 * c];
+      h0 += h.re * s.re - h.im * s.im;
+      h1 += h.re * s.im + h.im * s.re;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      h0 += __shfl_xor(h0, o);
+      h1 += __shfl_xor(h1, o);
+    }
+    if (lane == 0) {
+      const c128 hs = cmk(h0, h1);
+      const c128 a = zero ? cmk(0.0, 0.0) : cscale(csub(st[2 * r + 1], hs), inv);
+      hr[j - 1] = cadd(hr[j - 1], st[2 * r]);
+      hr[j] = a;
+      cs[r] = zero ? cmk(0.0, 0.0) : cadd(cscale(hs, inv), a);
+    }
+  }
+  if (blockIdx.x == 0 && tid == 0) {
+    const c128 gam = st[2 * j + 1];
+    const c128 sht = cmk(red[1][0], red[2][0]);
+    const c128 aj = zero ? cmk(0.0, 0.0) : cscale(csub(cscale(csub(gam, sht), inv), cscale(sl, rho)), inv);
+    if (j > 0) H[(size_t)j * ldh + (j - 1)] = cmk(rho, 0.0);
+    H[(size_t)j * ldh + j] = aj;
+    cs[j] = zero ? cmk(0.0, 0.0) : cadd(sl, aj);
+    cs[j + 1] = cmk(inv, 0.0);
+  }
+}
+
+// partial sums over a slice of the basis rows: part[g][i] = (sum_r V[r][i] s_r, sum_r V[r][i] c_r)
+__global__ __launch_bounds__(256) void dcgs_update_partial_kernel(const c128* __restrict__ V, long ldv, int j, int n,
+                                                                  const c128* __restrict__ st,
+                                                                  const c128* __restrict__ cs, c128* part) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int g = blockIdx.y, G = gridDim.y;
+  const int r0 = (int)((long)j * g / G), r1 = (int)((long)j * (g + 1) / G);
+  if (i >= n) return;
+  double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+  constexpr int U = 8;
+  int r = r0;
+  for (; r + U <= r1; r += U) {
+    c128 v[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) v[q] = V[(size_t)(r + q) * ldv + i];
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const c128 s = st[2 * (r + q)], c = cs[r + q];
+      a0 += v[q].re * s.re - v[q].im * s.im;
+      a1 += v[q].re * s.im + v[q].im * s.re;
+      b0 += v[q].re * c.re - v[q].im * c.im;
+      b1 += v[q].re * c.im + v[q].im * c.re;
+    }
+  }
+  for (; r < r1; ++r) {
+    const c128 v = V[(size_t)r * ldv + i], s = st[2 * r], c = cs[r];
+    a0 += v.re * s.re - v.im * s.im;
+    a1 += v.re * s.im + v.im * s.re;
+    b0 += v.re * c.re - v.im * c.im;
+    b1 += v.re * c.im + v.im * c.re;
+  }
+  part[((size_t)g * n + i) * 2] = cmk(a0, a1);
+  part[((size_t)g * n + i) * 2 + 1] = cmk(b0, b1);
+}
+
+// v_j = (u_j - V s) / rho into V[j], u_{j+1} = z / rho - V c - v_j d into V[j+1]
+__global__ __launch_bounds__(256) void dcgs_update_final_kernel(c128* V, long ldv, int j, int n,
+                                                                const c128* __restrict__ z,
+                                                                const c128* __restrict__ cs,
+                                                                const c128* __restrict__ part, int G) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  c128 p = cmk(0.0, 0.0), q = cmk(0.0, 0.0);
+  for (int g = 0; g < G; ++g) {
+    p = cadd(p, part[((size_t)g * n + i) * 2]);
+    q = cadd(q, part[((size_t)g * n + i) * 2 + 1]);
+  }
+  const double inv = cs[j + 1].re;
+  const c128 d = cs[j];
+  const c128 v = cscale(csub(V[(size_t)j * ldv + i], p), inv);
+  V[(size_t)j * ldv + i] = v;
+  V[(size_t)(j + 1) * ldv + i] = csub(csub(cscale(z[i], inv), q), cmul(v, d));
+}
+
 }  // namespace
 }  // namespace qd
 
 using namespace qd;
+
+extern "C" int qd_arnoldi_dcgs2_step(qd_c128* V, long ldv, int j, int n, const qd_c128* z, qd_c128* H, long ldh,
+                                     qd_c128* st, qd_c128* cs, void* stream) {
+  WsScope wss_((hipStream_t)stream);
+  QD_CHECK_ARG(V && z && H && st && cs, "qd_arnoldi_dcgs2_step: null pointer");
+  QD_CHECK_ARG(j >= 0 && n >= 1 && ldv >= n && ldh >= j + 1, "qd_arnoldi_dcgs2_step: j=%d n=%d ldv=%ld ldh=%ld", j,
+               n, ldv, ldh);
+  hipStream_t st_ = (hipStream_t)stream;
+  hipLaunchKernelGGL(dcgs_project_kernel, dim3(j + 1), dim3(256), 0, st_, (const c128*)V, ldv, j, n, (const c128*)z,
+                     (c128*)st);
+  QD_HIP(hipGetLastError());
+  hipLaunchKernelGGL(dcgs_coef_kernel, dim3(std::max(1, (j + 3) / 4)), dim3(256), 0, st_, (c128*)H, ldh, j,
+                     (const c128*)st, (c128*)cs);
+  QD_HIP(hipGetLastError());
+  // row slices: enough workgroups to keep HBM busy (n / 256 columns of workgroups is ~100 at the bench hierarchy)
+  const int G = std::max(1, std::min(16, j / 32));
+  void* part = nullptr;
+  if (int rc = workspace(WS_MISC, (size_t)G * n * 2 * sizeof(c128), &part, st_)) return rc;
+  const int nb = (n + 255) / 256;
+  hipLaunchKernelGGL(dcgs_update_partial_kernel, dim3(nb, G), dim3(256), 0, st_, (const c128*)V, ldv, j, n,
+                     (const c128*)st, (const c128*)cs, (c128*)part);
+  QD_HIP(hipGetLastError());
+  hipLaunchKernelGGL(dcgs_update_final_kernel, dim3(nb), dim3(256), 0, st_, (c128*)V, ldv, j, n, (const c128*)z,
+                     (const c128*)cs, (const c128*)part, G);
+  QD_HIP(hipGetLastError());
+  return QD_OK;
+}
 
 extern "C" int qd_cgs_project(const qd_c128* V, long ldv, int m, int n, const qd_c128* w, qd_c128* h, qd_c128* hsum,
                               long ldh, void* stream) {

@@ -36,6 +36,7 @@ TAYLOR_RADIUS = 5.0   # substeps tau with ||P tau||_inf <= TAYLOR_RADIUS
 TAYLOR_DEGREE = 48    # terms per substep: remainder <= e^5 5^49 / 49! < 1e-26; largest term 5^5 / 5! = 26 (the sum of the
                       # terms' magnitudes <= e^5: ~2 digits of cancellation at most); 71 substeps x 48 terms at the bench
                       # hierarchy against 118 x 36 at radius 3 and 352 x 20 at radius 1
+ARNOLDI_DCGS2 = True  # device Arnoldi by delayed CGS2 (qd_arnoldi_dcgs2_step: 2 basis passes per step); False: CGS2 (4)
 
 
 def transposed_tables(minus, plus, coef):
@@ -199,7 +200,9 @@ def _shift_residuals(Hh, k, beta, shifts):
 def shifted_krylov_solve(op, b, shifts, tol=1e-12, m_max=None, first_check=20):
     """x(s) = (-P - s)^-1 b for every s in `shifts` (complex array) from one Arnoldi basis of P.
 
-    Classical Gram-Schmidt with one re-orthogonalisation on device-resident basis vectors.  At checkpoints the FOM
+    Classical Gram-Schmidt with one re-orthogonalisation on device-resident basis vectors; on the device by default
+    in its delayed form (ARNOLDI_DCGS2: the re-orthogonalisation of v_j is folded into the projection pass of the
+    next step through the Arnoldi relation, krylov.hip).  At checkpoints the FOM
     residual |h_{k+1,k} y_k(s)| of every shift is evaluated on the host without solving for y (_shift_residuals); the
     next checkpoint is placed where the log-linear trend of the worst residual reaches the target (at least 10 and
     at most 50 % more steps).  Converged when the worst residual is below tol^1.1 (relative to ||b||) and the
@@ -208,49 +211,66 @@ def shifted_krylov_solve(op, b, shifts, tol=1e-12, m_max=None, first_check=20):
     if m_max is None:   # basis memory capped at ~8 GB
         m_max = int(max(50, min(4000, (8 << 30) // (16 * n) - 2)))
     dev = op.dev
-    V = torch.empty((m_max + 1, n), dtype=torch.complex128, device=dev)
-    Hd = torch.zeros((m_max + 1, m_max), dtype=torch.complex128, device=dev)
+    gpu = dev.type == "cuda"
+    lowsync = gpu and ARNOLDI_DCGS2
+    V = torch.empty((m_max + 2, n), dtype=torch.complex128, device=dev)
+    Hd = torch.zeros((m_max + 2, m_max + 1), dtype=torch.complex128, device=dev)
     W = torch.empty(n, dtype=torch.complex128, device=dev)
     beta = float(torch.linalg.vector_norm(b))
     if beta == 0.0:
         return torch.zeros((len(shifts), n), dtype=torch.complex128, device=dev), 0
-    V[0] = b / beta
+    if lowsync:   # the delayed step normalises V[0] itself (its j = 0 case)
+        V[0] = b
+    else:
+        V[0] = b / beta
     shifts = np.asarray(shifts, dtype=complex)
     check = first_check
     k_done = None
     hist = []
     target = tol ** 1.1
-    gpu = dev.type == "cuda"
     if gpu:   # CGS2 on the device: qd_cgs_project (h = V^H w into the Hessenberg column) + in-place GEMV updates
         lib = _lib.load()
-        hbuf = torch.empty(m_max + 1, dtype=torch.complex128, device=dev)
+        hbuf = torch.empty(m_max + 2, dtype=torch.complex128, device=dev)
         ldh = Hd.stride(0)
         col = lambda r, c: Hd.data_ptr() + (r * ldh + c) * 16
-    for j in range(m_max):
+        if lowsync:
+            stv = torch.empty(2 * (m_max + 2), dtype=torch.complex128, device=dev)
+            csv = torch.empty(m_max + 3, dtype=torch.complex128, device=dev)
+    for j in range(m_max + 1 if lowsync else m_max):
         op.apply(V[j], W)
-        Vj = V[:j + 1]
-        if gpu:
-            st = _lib.stream_ptr(dev)
-            for _ in range(2):   # classical Gram-Schmidt, applied twice; Hd[:j+1, j] accumulates h1 + h2
-                _lib.check(lib.qd_cgs_project(V.data_ptr(), n, j + 1, n, W.data_ptr(), hbuf.data_ptr(), col(0, j),
-                                              ldh, st), "qd_cgs_project")
-                W.addmv_(Vj.transpose(0, 1), hbuf[:j + 1], alpha=-1)
-            # Hd[j+1, j] = ||W||, V[j+1] = W / max(||W||, 1e-300): an exact breakdown (||W|| = 0) must not turn the
-            # basis into NaN before the next checkpoint, where the zero sub-diagonal entry ends the solve (ADVICE
-            # r05); no host read per step
-            _lib.check(lib.qd_cgs_normalize(W.data_ptr(), n, V[j + 1].data_ptr(), col(j + 1, j), st),
-                       "qd_cgs_normalize")
+        if lowsync:
+            # delayed CGS2 (krylov.hip): finishes v_{j} (its reorthogonalisation, norm and the Hessenberg column j-1)
+            # and forms the first-pass candidate u_{j+1} from W = P u_j: two passes over the basis per step
+            _lib.check(lib.qd_arnoldi_dcgs2_step(V.data_ptr(), n, j, n, W.data_ptr(), Hd.data_ptr(), ldh,
+                                                 stv.data_ptr(), csv.data_ptr(), _lib.stream_ptr(dev)),
+                       "qd_arnoldi_dcgs2_step")
+            if j == 0:
+                continue
+            k = j
         else:
-            h = torch.mv(Vj, W.conj()).conj()
-            W -= torch.mv(Vj.transpose(0, 1), h)
-            h2 = torch.mv(Vj, W.conj()).conj()
-            W -= torch.mv(Vj.transpose(0, 1), h2)
-            h += h2
-            nrm = torch.linalg.vector_norm(W)
-            Hd[:j + 1, j] = h
-            Hd[j + 1, j] = nrm
-            V[j + 1] = W / torch.clamp(nrm, min=1e-300)
-        k = j + 1
+            Vj = V[:j + 1]
+            if gpu:
+                st = _lib.stream_ptr(dev)
+                for _ in range(2):   # classical Gram-Schmidt, applied twice; Hd[:j+1, j] accumulates h1 + h2
+                    _lib.check(lib.qd_cgs_project(V.data_ptr(), n, j + 1, n, W.data_ptr(), hbuf.data_ptr(),
+                                                  col(0, j), ldh, st), "qd_cgs_project")
+                    W.addmv_(Vj.transpose(0, 1), hbuf[:j + 1], alpha=-1)
+                # Hd[j+1, j] = ||W||, V[j+1] = W / max(||W||, 1e-300): an exact breakdown (||W|| = 0) must not turn
+                # the basis into NaN before the next checkpoint, where the zero sub-diagonal entry ends the solve
+                # (ADVICE r05); no host read per step
+                _lib.check(lib.qd_cgs_normalize(W.data_ptr(), n, V[j + 1].data_ptr(), col(j + 1, j), st),
+                           "qd_cgs_normalize")
+            else:
+                h = torch.mv(Vj, W.conj()).conj()
+                W -= torch.mv(Vj.transpose(0, 1), h)
+                h2 = torch.mv(Vj, W.conj()).conj()
+                W -= torch.mv(Vj.transpose(0, 1), h2)
+                h += h2
+                nrm = torch.linalg.vector_norm(W)
+                Hd[:j + 1, j] = h
+                Hd[j + 1, j] = nrm
+                V[j + 1] = W / torch.clamp(nrm, min=1e-300)
+            k = j + 1
         if k != check and k != m_max:
             continue
         if dev.type == "cuda":   # device solves (qd_shifted_hessenberg_solve); only scalars come back

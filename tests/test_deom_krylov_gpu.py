@@ -145,3 +145,57 @@ def test_krylov_corr4_bench_hierarchy_orientations_agree():
     c2 = sol.correlation_4op_3t(sz, sx, sx, sz, rho0, 0.2, wx, np.concatenate([wy, [5.3, 6.1, 7.7]]))
     assert np.all(np.isfinite(c1))
     assert relerr(c2[:, :len(wy)], c1) < 1e-9, (info1, sol.last_corr4)
+
+
+class _DenseOpDev:
+    """A dense P on the device standing in for DeomOperator (test infrastructure only)."""
+
+    def __init__(self, P, norm):
+        self.P = torch.from_numpy(np.ascontiguousarray(P)).to("cuda:0")
+        self.n = P.shape[0]
+        self.dev = torch.device("cuda", 0)
+        self.norm = norm
+
+    def apply(self, x, y, alpha=1.0):
+        y.copy_((alpha * (self.P @ x.reshape(-1, self.n).T).T).reshape(y.shape))
+        return y
+
+
+def test_delayed_cgs2_arnoldi_matches_cgs2():
+    """qd_arnoldi_dcgs2_step (two basis passes per step, the re-orthogonalisation folded into the next projection)
+    against the four-pass CGS2 loop: the same solutions of the shifted systems, on a random dense P and on the DEOM
+    stencil operator; exact breakdowns (P = 0; b an eigenvector) end the solve with the exact answer."""
+    from pyqed_amd import deom_krylov as dk
+    from pyqed_amd.deom_krylov import DeomOperator, shifted_krylov_solve
+    rng = np.random.default_rng(5)
+    n = 300
+    P = (rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))) / 20 - 2.0 * np.eye(n)
+    b = torch.from_numpy(rng.standard_normal(n) + 1j * rng.standard_normal(n)).to("cuda:0")
+    shifts = 1j * np.linspace(-3, 3, 7) + 0.1
+    ref = np.linalg.solve(-P[None] - shifts[:, None, None] * np.eye(n)[None], b.cpu().numpy()[None, :, None])[..., 0]
+    sol, H, Q, coef, damp, mode = _hierarchy(2, 3, 4, 1)
+    op = DeomOperator(torch.device("cuda", 0), sol._minus, sol._plus, coef, damp, mode, H, Q, 2)
+    bd = torch.from_numpy(rng.standard_normal(op.n) + 0j).to("cuda:0")
+    out = {}
+    try:
+        for flag in (False, True):
+            dk.ARNOLDI_DCGS2 = flag
+            X, k = shifted_krylov_solve(_DenseOpDev(P, 1.0), b, shifts)
+            Xd, kd = shifted_krylov_solve(op, bd, shifts)
+            out[flag] = (X.cpu().numpy(), k, Xd.cpu().numpy(), kd)
+            assert relerr(out[flag][0], ref) < 1e-10, (flag, k)
+        assert relerr(out[True][2], out[False][2]) < 1e-11
+        assert abs(out[True][1] - out[False][1]) <= 10 and abs(out[True][3] - out[False][3]) <= 10
+        m = 12
+        bz = torch.from_numpy(rng.standard_normal(m) + 0j).to("cuda:0")
+        X, k = shifted_krylov_solve(_DenseOpDev(np.zeros((m, m), complex), 1.0), bz, shifts)
+        assert k == 1 and np.all(np.isfinite(X.cpu().numpy()))
+        assert relerr(X.cpu().numpy(), -bz.cpu().numpy()[None, :] / shifts[:, None]) < 1e-14
+        Pd = np.diag(np.arange(m, dtype=complex) - 2.5)
+        e = torch.zeros(m, dtype=torch.complex128, device="cuda:0")
+        e[3] = 2.0
+        X, k = shifted_krylov_solve(_DenseOpDev(Pd, 10.0), e, shifts)
+        assert k == 1
+        assert relerr(X.cpu().numpy(), e.cpu().numpy()[None, :] / (-Pd[3, 3] - shifts)[:, None]) < 1e-14
+    finally:
+        dk.ARNOLDI_DCGS2 = True
