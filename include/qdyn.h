@@ -405,7 +405,8 @@ int qd_cgs_normalize(const qd_c128* w, int n, qd_c128* v, qd_c128* hsub, void* s
  * column j-1 holding u_j's projection coefficients.  On return V[j] = v_j, column j-1 final
  * (re-orthogonalisation added, h_{j,j-1} = |u_j - V_j s|), column j the projection coefficients
  * of P v_j and V[j+1] = u_{j+1}.  Start with V[0] = b at j = 0.  An exact breakdown writes
- * h_{j,j-1} = 0 and zero vectors from there on.  st: 2(j+1) and cs: j+2 complex scratch.
+ * h_{j,j-1} = 0 and zero vectors from there on.  st: 16(j+1) and cs: 2(j+2) complex scratch;
+ * j <= 8192.
  */
 int qd_arnoldi_dcgs2_step(qd_c128* V, long ldv, int j, int n, const qd_c128* z, qd_c128* H,
                           long ldh, qd_c128* st, qd_c128* cs, void* stream);

@@ -165,6 +165,8 @@ __global__ __launch_bounds__(256) void cgs_norm_scale_kernel(const c128* __restr
   }
 }
 
+constexpr int DCGS_MAX_SLICES = 8;   // column slices of the projection pass (st holds 2 (j + 1) DCGS_MAX_SLICES)
+
 // ---- delayed CGS2 Arnoldi step (two passes over the basis per step instead of CGS2's four) --------------------------
 // State entering step j: V[0..j-1] final orthonormal, V[j] = u_j the candidate after ONE projection (unnormalised),
 // z = P u_j, Hessenberg columns 0..j-2 final, column j-1 holding the first-pass coefficients.  One projection pass
@@ -175,13 +177,17 @@ __global__ __launch_bounds__(256) void cgs_norm_scale_kernel(const c128* __restr
 //   u_{j+1} = z / rho - V_j c - v_j d with c = H_j s / rho + a_{<j}, d = s_{j-1} + a_j
 // and one update pass writes v_j and u_{j+1}.  Step 0 starts from V[0] = b (j = 0: no basis, rho = |b|).
 
-// st[2r] = conj(V[r]) . V[j], st[2r+1] = conj(V[r]) . z for r <= j (row j: alpha, gamma)
+// partial dot products over column slice g of S: st[(2r) S + g] = conj(V[r]) . V[j], st[(2r+1) S + g] = conj(V[r]) . z
+// for r <= j (row j: alpha, gamma); S slices per row keep ~4 workgroups per CU busy at small j
 __global__ __launch_bounds__(256) void dcgs_project_kernel(const c128* __restrict__ V, long ldv, int j, int n,
                                                            const c128* __restrict__ z, c128* st) {
   __shared__ double red[4][256];
-  const int r = blockIdx.x, tid = threadIdx.x;
-  const c128* vr = V + (size_t)r * ldv;
-  const c128* u = V + (size_t)j * ldv;
+  const int r = blockIdx.x, tid = threadIdx.x, g = blockIdx.y, S = gridDim.y;
+  const int c0 = (int)((long)n * g / S), c1 = (int)((long)n * (g + 1) / S);
+  const c128* vr = V + (size_t)r * ldv + c0;
+  const c128* u = V + (size_t)j * ldv + c0;
+  z += c0;
+  n = c1 - c0;
   double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
   constexpr int U = 6;
   int i = tid;
@@ -221,20 +227,30 @@ __global__ __launch_bounds__(256) void dcgs_project_kernel(const c128* __restric
     __syncthreads();
   }
   if (tid == 0) {
-    st[2 * r] = cmk(red[0][0], red[1][0]);
-    st[2 * r + 1] = cmk(red[2][0], red[3][0]);
+    st[(size_t)(2 * r) * S + g] = cmk(red[0][0], red[1][0]);
+    st[(size_t)(2 * r + 1) * S + g] = cmk(red[2][0], red[3][0]);
   }
 }
 
+// the S partial sums of entry e, in slice order (every reader gets the same value)
+__device__ __forceinline__ c128 st_sum(const c128* st, int S, int e) {
+  c128 a = st[(size_t)e * S];
+  for (int g = 1; g < S; ++g) a = cadd(a, st[(size_t)e * S + g]);
+  return a;
+}
+
 // one wave per Hessenberg row r < j (4 per workgroup); every workgroup recomputes |s|^2 and s^H t in the same order.
-// cs[r] = c_r (r < j), cs[j] = d, cs[j+1] = (1/rho, 0); rho = 0 (exact breakdown) zeroes v_j, u_{j+1} and column j.
-__global__ __launch_bounds__(256) void dcgs_coef_kernel(c128* H, long ldh, int j, const c128* __restrict__ st,
+// cs[r] = c_r (r < j), cs[j] = d, cs[j+1] = (1/rho, 0), cs[j+2+r] = s_r; rho = 0 (exact breakdown) zeroes v_j,
+// u_{j+1} and column j.
+__global__ __launch_bounds__(256) void dcgs_coef_kernel(c128* H, long ldh, int j, const c128* __restrict__ st, int S,
                                                         c128* cs) {
   __shared__ double red[3][256];
+  extern __shared__ c128 s_sh[];   // s summed over the slices, j entries (dynamic)
   const int tid = threadIdx.x;
   double ss = 0.0, p0 = 0.0, p1 = 0.0;
   for (int r = tid; r < j; r += 256) {
-    const c128 s = st[2 * r], t = st[2 * r + 1];
+    const c128 s = st_sum(st, S, 2 * r), t = st_sum(st, S, 2 * r + 1);
+    s_sh[r] = s;
     ss += s.re * s.re + s.im * s.im;
     p0 += s.re * t.re + s.im * t.im;   // conj(s) t
     p1 += s.re * t.im - s.im * t.re;
@@ -251,21 +267,22 @@ __global__ __launch_bounds__(256) void dcgs_coef_kernel(c128* H, long ldh, int j
     }
     __syncthreads();
   }
-  const double rho2 = st[2 * j].re - red[0][0];
+  const double rho2 = st_sum(st, S, 2 * j).re - red[0][0];
   const double rho = rho2 > 0.0 ? sqrt(rho2) : 0.0;
   const bool zero = !(rho > 1e-300);
   const double inv = zero ? 0.0 : 1.0 / rho;
-  const c128 sl = j > 0 ? st[2 * (j - 1)] : cmk(0.0, 0.0);
+  const c128 sl = j > 0 ? s_sh[j - 1] : cmk(0.0, 0.0);
   const int lane = tid & 63;
   const int r = blockIdx.x * 4 + (tid >> 6);
   if (r < j) {
     // (H_j s)_r over the final columns: column j-1 is its first-pass value plus s_r
     double h0 = 0.0, h1 = 0.0;
     c128* hr = H + (size_t)r * ldh;
+    const c128 sr = s_sh[r];
     for (int c = (r > 0 ? r - 1 : 0) + lane; c < j; c += 64) {
       c128 h = hr[c];
-      if (c == j - 1) h = cadd(h, st[2 * r]);
-      const c128 s = st[2 * c];
+      if (c == j - 1) h = cadd(h, sr);
+      const c128 s = s_sh[c];
       h0 += h.re * s.re - h.im * s.im;
       h1 += h.re * s.im + h.im * s.re;
     }
@@ -276,14 +293,15 @@ __global__ __launch_bounds__(256) void dcgs_coef_kernel(c128* H, long ldh, int j
     }
     if (lane == 0) {
       const c128 hs = cmk(h0, h1);
-      const c128 a = zero ? cmk(0.0, 0.0) : cscale(csub(st[2 * r + 1], hs), inv);
-      hr[j - 1] = cadd(hr[j - 1], st[2 * r]);
+      const c128 a = zero ? cmk(0.0, 0.0) : cscale(csub(st_sum(st, S, 2 * r + 1), hs), inv);
+      hr[j - 1] = cadd(hr[j - 1], sr);
       hr[j] = a;
       cs[r] = zero ? cmk(0.0, 0.0) : cadd(cscale(hs, inv), a);
+      cs[j + 2 + r] = sr;
     }
   }
   if (blockIdx.x == 0 && tid == 0) {
-    const c128 gam = st[2 * j + 1];
+    const c128 gam = st_sum(st, S, 2 * j + 1);
     const c128 sht = cmk(red[1][0], red[2][0]);
     const c128 aj = zero ? cmk(0.0, 0.0) : cscale(csub(cscale(csub(gam, sht), inv), cscale(sl, rho)), inv);
     if (j > 0) H[(size_t)j * ldh + (j - 1)] = cmk(rho, 0.0);
@@ -295,7 +313,6 @@ __global__ __launch_bounds__(256) void dcgs_coef_kernel(c128* H, long ldh, int j
 
 // partial sums over a slice of the basis rows: part[g][i] = (sum_r V[r][i] s_r, sum_r V[r][i] c_r)
 __global__ __launch_bounds__(256) void dcgs_update_partial_kernel(const c128* __restrict__ V, long ldv, int j, int n,
-                                                                  const c128* __restrict__ st,
                                                                   const c128* __restrict__ cs, c128* part) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int g = blockIdx.y, G = gridDim.y;
@@ -310,7 +327,7 @@ __global__ __launch_bounds__(256) void dcgs_update_partial_kernel(const c128* __
     for (int q = 0; q < U; ++q) v[q] = V[(size_t)(r + q) * ldv + i];
 #pragma unroll
     for (int q = 0; q < U; ++q) {
-      const c128 s = st[2 * (r + q)], c = cs[r + q];
+      const c128 s = cs[j + 2 + r + q], c = cs[r + q];
       a0 += v[q].re * s.re - v[q].im * s.im;
       a1 += v[q].re * s.im + v[q].im * s.re;
       b0 += v[q].re * c.re - v[q].im * c.im;
@@ -318,7 +335,7 @@ __global__ __launch_bounds__(256) void dcgs_update_partial_kernel(const c128* __
     }
   }
   for (; r < r1; ++r) {
-    const c128 v = V[(size_t)r * ldv + i], s = st[2 * r], c = cs[r];
+    const c128 v = V[(size_t)r * ldv + i], s = cs[j + 2 + r], c = cs[r];
     a0 += v.re * s.re - v.im * s.im;
     a1 += v.re * s.im + v.im * s.re;
     b0 += v.re * c.re - v.im * c.im;
@@ -356,14 +373,24 @@ extern "C" int qd_arnoldi_dcgs2_step(qd_c128* V, long ldv, int j, int n, const q
                                      qd_c128* st, qd_c128* cs, void* stream) {
   WsScope wss_((hipStream_t)stream);
   QD_CHECK_ARG(V && z && H && st && cs, "qd_arnoldi_dcgs2_step: null pointer");
-  QD_CHECK_ARG(j >= 0 && n >= 1 && ldv >= n && ldh >= j + 1, "qd_arnoldi_dcgs2_step: j=%d n=%d ldv=%ld ldh=%ld", j,
+  QD_CHECK_ARG(j >= 0 && j <= 8192 && n >= 1 && ldv >= n && ldh >= j + 1,
+               "qd_arnoldi_dcgs2_step: j=%d n=%d ldv=%ld ldh=%ld", j,
                n, ldv, ldh);
   hipStream_t st_ = (hipStream_t)stream;
-  hipLaunchKernelGGL(dcgs_project_kernel, dim3(j + 1), dim3(256), 0, st_, (const c128*)V, ldv, j, n, (const c128*)z,
-                     (c128*)st);
+  const int S = std::max(1, std::min(DCGS_MAX_SLICES, 1024 / (j + 1)));
+  hipLaunchKernelGGL(dcgs_project_kernel, dim3(j + 1, S), dim3(256), 0, st_, (const c128*)V, ldv, j, n,
+                     (const c128*)z, (c128*)st);
   QD_HIP(hipGetLastError());
-  hipLaunchKernelGGL(dcgs_coef_kernel, dim3(std::max(1, (j + 3) / 4)), dim3(256), 0, st_, (c128*)H, ldh, j,
-                     (const c128*)st, (c128*)cs);
+  const size_t lds = (size_t)std::max(1, j) * sizeof(c128);
+  if (lds > 48 * 1024) {
+    static const bool lds_attr = [] {
+      return hipFuncSetAttribute((const void*)dcgs_coef_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 160 * 1024 - 8 * 1024) == hipSuccess;
+    }();
+    (void)lds_attr;
+  }
+  hipLaunchKernelGGL(dcgs_coef_kernel, dim3(std::max(1, (j + 3) / 4)), dim3(256), lds, st_, (c128*)H, ldh, j,
+                     (const c128*)st, S, (c128*)cs);
   QD_HIP(hipGetLastError());
   // row slices: enough workgroups to keep HBM busy (n / 256 columns of workgroups is ~100 at the bench hierarchy)
   const int G = std::max(1, std::min(16, j / 32));
@@ -371,7 +398,7 @@ extern "C" int qd_arnoldi_dcgs2_step(qd_c128* V, long ldv, int j, int n, const q
   if (int rc = workspace(WS_MISC, (size_t)G * n * 2 * sizeof(c128), &part, st_)) return rc;
   const int nb = (n + 255) / 256;
   hipLaunchKernelGGL(dcgs_update_partial_kernel, dim3(nb, G), dim3(256), 0, st_, (const c128*)V, ldv, j, n,
-                     (const c128*)st, (const c128*)cs, (c128*)part);
+                     (const c128*)cs, (c128*)part);
   QD_HIP(hipGetLastError());
   hipLaunchKernelGGL(dcgs_update_final_kernel, dim3(nb), dim3(256), 0, st_, (c128*)V, ldv, j, n, (const c128*)z,
                      (const c128*)cs, (const c128*)part, G);

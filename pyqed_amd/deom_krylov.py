@@ -234,8 +234,8 @@ def shifted_krylov_solve(op, b, shifts, tol=1e-12, m_max=None, first_check=20):
         ldh = Hd.stride(0)
         col = lambda r, c: Hd.data_ptr() + (r * ldh + c) * 16
         if lowsync:
-            stv = torch.empty(2 * (m_max + 2), dtype=torch.complex128, device=dev)
-            csv = torch.empty(m_max + 3, dtype=torch.complex128, device=dev)
+            stv = torch.empty(16 * (m_max + 2), dtype=torch.complex128, device=dev)
+            csv = torch.empty(2 * (m_max + 3), dtype=torch.complex128, device=dev)
     for j in range(m_max + 1 if lowsync else m_max):
         op.apply(V[j], W)
         if lowsync:
