@@ -1165,20 +1165,22 @@ def bench_deom_corr4(dev, nw=32, T=0.5):
     if "stencil_vector_applications" in info:
         # the stencil kernel's roofline over the call -- algorithmic bytes per vector application
         # (read x, write y: 2 n 16 B) plus the tables once per launch (coef 3K, damp, minus / plus per ADO), over the
-        # call's wall time (so a lower bound: the call also runs the CGS2 GEMVs, the small solves and the host
-        # checkpoints); and the CGS2 orthogonalisation's own traffic (two passes over the basis per Arnoldi step,
-        # each reading the j + 1 basis vectors twice) for the record
+        # call's wall time (so a lower bound: the call also runs the Arnoldi basis passes, the small solves and the host
+        # checkpoints); and the Arnoldi orthogonalisation's own traffic for the record: the j + 1 basis vectors read
+        # twice per step by the delayed CGS2 (deom_krylov.ARNOLDI_DCGS2), four times by the plain CGS2 loop
+        from pyqed_amd import deom_krylov
         nmax, K, n = sol.nmax, sol.nind, sol.nmax * 4
         per_vec = 2 * n * 16
         per_launch = nmax * (3 * K * 16 + 16 + 2 * K * 4)
         stencil = info["stencil_vector_applications"] * per_vec + info["stencil_launches"] * per_launch
         kr, kl = info.get("krylov_dim_right", 0), info.get("krylov_dim_left", 0)
-        cgs2 = sum(4 * k * (k + 1) // 2 * n * 16 for k in (kr, kl))
+        passes = 2 if deom_krylov.ARNOLDI_DCGS2 else 4
+        cgs2 = sum(passes * k * (k + 1) // 2 * n * 16 for k in (kr, kl))
         res["roofline"] = {"bound": "hbm", "kernel": "qd_deom_apply (stencil)",
                            "achieved": round(stencil / el / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                            "frac": round(stencil / el / 1e9 / HBM_PEAK_GBS, 4),
                            "bytes_per_vector_application": per_vec, "table_bytes_per_launch": per_launch,
-                           "cgs2_gemv_bytes": cgs2,
+                           "arnoldi_basis_bytes": cgs2, "arnoldi_basis_passes_per_step": passes,
                            "note": "stencil algorithmic bytes / the whole call's wall time: the call is bound by its "
                                    "~9k dependent small launches (Arnoldi steps, Taylor terms), not by HBM"}
     return res
