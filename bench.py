@@ -1165,8 +1165,8 @@ def bench_deom_corr4(dev, nw=32, T=0.5):
     if "stencil_vector_applications" in info:
         # the stencil kernel's roofline over the call -- algorithmic bytes per vector application
         # (read x, write y: 2 n 16 B) plus the tables once per launch (coef 3K, damp, minus / plus per ADO), over the
-        # call's wall time (so a lower bound: the call also runs the Arnoldi basis passes, the small solves and the host
-        # checkpoints); and the Arnoldi orthogonalisation's own traffic for the record: the j + 1 basis vectors read
+        # call's wall time (so a lower bound: the call also runs the Arnoldi basis passes, the small solves and the
+        # host checkpoints); and the Arnoldi orthogonalisation's own traffic for the record: the j + 1 basis vectors read
         # twice per step by the delayed CGS2 (deom_krylov.ARNOLDI_DCGS2), four times by the plain CGS2 loop
         from pyqed_amd import deom_krylov
         nmax, K, n = sol.nmax, sol.nind, sol.nmax * 4
@@ -1182,7 +1182,7 @@ def bench_deom_corr4(dev, nw=32, T=0.5):
                            "bytes_per_vector_application": per_vec, "table_bytes_per_launch": per_launch,
                            "arnoldi_basis_bytes": cgs2, "arnoldi_basis_passes_per_step": passes,
                            "note": "stencil algorithmic bytes / the whole call's wall time: the call is bound by its "
-                                   "~9k dependent small launches (Arnoldi steps, Taylor terms), not by HBM"}
+                                   "thousands of dependent small launches (Arnoldi steps, Taylor terms), not by HBM"}
     return res
 
 
